@@ -1,0 +1,175 @@
+/*
+ * pcgpu.h — C ABI of the MI355X-native PC-fisherz causal-graph engine (libpcgpu.so).
+ *
+ * The reference (ai4sre/RCAEval) is pure Python; its hot path calls causal-learn's
+ * `pc(data, alpha, fisherz, stable=True, uc_rule=0, uc_priority=2, ...)` [U] from
+ *   RCAEval/e2e/pc_pagerank.py:19          (pc_pagerank)
+ *   RCAEval/graph_construction/pc.py:15-20 (pc_default, used by pc_randomwalk :21)
+ *   RCAEval/graph_construction/pc.py:46-56 (pc_fisherz_stable)
+ * and scikit-network's `PageRank().fit_transform(adj.T)` [U] from
+ *   RCAEval/e2e/pc_pagerank.py:31-32 and RCAEval/graph_heads/page_rank.py:85-89.
+ * Each entry point below replaces one piece of that path (cited per function). The
+ * Python host layer (rcaeval_amd/) binds them with ctypes; INTEGRATION.md shows the stub.
+ *
+ * Conventions
+ *  - Every call returns 0 (PCG_OK) or a negative PCG_ERR_* code; pcg_last_error() gives text.
+ *  - Pointers documented "device" are HIP device pointers (e.g. torch tensor.data_ptr()),
+ *    caller-owned; "host" pointers are ordinary host memory. Scratch (adjacency bitmask,
+ *    work lists, sepset unions, records) is owned by the handle and grows on demand.
+ *  - One handle per (process, device). Calls are ordered on the handle's HIP stream and are
+ *    synchronous w.r.t. the host on return unless stated otherwise. Not re-entrant per handle;
+ *    separate handles may be used from separate threads. No global mutable state.
+ *  - Matrices are row-major with an explicit leading dimension (in elements).
+ */
+#ifndef PCGPU_H
+#define PCGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PCG_OK 0
+#define PCG_ERR_INVALID -1   /* bad argument / unsupported configuration            */
+#define PCG_ERR_OOM -2       /* device allocation failed                             */
+#define PCG_ERR_HIP -3       /* HIP runtime error                                    */
+#define PCG_ERR_SINGULAR -4  /* a CI-test sub-correlation matrix is exactly singular
+                                (causal-learn FisherZ raises ValueError) [U]         */
+#define PCG_ERR_DOMAIN -5    /* math domain error in the Fisher-z expression
+                                (Python math.log/sqrt raise ValueError) [U]          */
+#define PCG_ERR_RCCL -6      /* reserved: collective failure                          */
+#define PCG_ERR_OVERFLOW -7  /* an internal list overflowed its capacity (retried)    */
+
+/* skeleton flags */
+#define PCG_FLAG_FULL_P 0x1   /* compute the Fisher-z p-value of every test (reference
+                                 arithmetic); default decides p > alpha through the
+                                 monotone |r| threshold and computes p only in the
+                                 +-1e-6 band around it (identical decisions)            */
+#define PCG_FLAG_RECORD 0x2   /* record (a, b, S, p) of every unique test (parity runs) */
+#define PCG_FLAG_EXACT_ALL 0x4 /* route every test through the LU (numpy.linalg.inv-like)
+                                 exact path                                            */
+
+#define PCG_MAX_LEVELS 32
+#define PCG_MAX_DEPTH 12      /* deepest conditioning-set size supported on device     */
+
+typedef struct pcg_handle pcg_handle;
+
+typedef struct {
+    int64_t tests[PCG_MAX_LEVELS];     /* unique CI tests evaluated per depth (the reference's
+                                          cache misses, GraphClass.py:87-97)              */
+    int64_t calls[PCG_MAX_LEVELS];     /* ci_test invocations incl. cache hits per depth    */
+    int64_t indep[PCG_MAX_LEVELS];     /* unique tests with p > alpha                       */
+    int64_t exact[PCG_MAX_LEVELS];     /* tests resolved by the exact (LU) path             */
+    int64_t near_alpha[PCG_MAX_LEVELS];/* tests with |p - alpha| < 1e-9 (enumerated)        */
+    int64_t edges_after[PCG_MAX_LEVELS];/* undirected edges left after each depth           */
+    int32_t max_degree[PCG_MAX_LEVELS];/* max degree at the start of each depth            */
+    double level_ms[PCG_MAX_LEVELS];   /* device wall time per depth (HIP events)           */
+    double kernel_ms[PCG_MAX_LEVELS];  /* time of the CI-test kernel alone per depth        */
+    int32_t levels;                    /* depths run                                        */
+    int32_t error;                     /* 0 or PCG_ERR_SINGULAR / PCG_ERR_DOMAIN            */
+} pcg_stats;
+
+typedef struct {                       /* one unique CI test (PCG_FLAG_RECORD / near-alpha) */
+    int32_t a, b;                      /* a < b                                             */
+    int32_t d;                         /* |S|                                               */
+    int32_t s[PCG_MAX_DEPTH];          /* sorted S, -1 padded                               */
+    double p;                          /* Fisher-z p-value                                  */
+} pcg_record;
+
+/* ---- lifetime --------------------------------------------------------------------- */
+int pcg_create(int device, pcg_handle **out);
+int pcg_destroy(pcg_handle *h);
+const char *pcg_last_error(pcg_handle *h);
+/* Use an external HIP stream (e.g. torch.cuda.current_stream().cuda_stream); NULL = own. */
+int pcg_set_stream(pcg_handle *h, void *hip_stream);
+/* Launch-shape knobs (0 = default). */
+int pcg_set_capacity(pcg_handle *h, int64_t record_capacity, int64_t deferred_capacity);
+
+/* ---- K1: correlation -------------------------------------------------------------
+ * Replaces FisherZ.__init__'s `np.corrcoef(data.T)` [U]: column means,
+ * centred X^T X on fp64 MFMA (v_mfma_f64_16x16x4_f64, LDS-tiled, upper-triangle tiles),
+ * *= 1/(N-1), /= s_i, /= s_j, clip to [-1, 1] (numpy's order).
+ * X: device, N x n (ldx >= n). C: device, n x n (ldc >= n).                            */
+int pcg_corr(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx,
+             double *C, int64_t ldc);
+
+/* ---- K2/K3: stable PC skeleton ---------------------------------------------------
+ * Replaces causal-learn skeleton_discovery(stable=True) with FisherZ
+ * (lib/causallearn/utils/PCUtils/SkeletonDiscovery.py:70-144, GraphClass.py:78-106).
+ * C: device n x n correlation (from pcg_corr or caller). N: sample count (FisherZ dof).
+ * removed_level: device n x n int8 out; -1 = edge survives, else the depth at which the
+ * edge was removed. max_depth < 0: unlimited (the reference's behaviour).
+ * stats: host out. Sepset unions are kept in the handle: see pcg_sepset_*.             */
+int pcg_skeleton(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N,
+                 double alpha, int max_depth, int flags, int8_t *removed_level,
+                 pcg_stats *stats);
+
+/* Degrees at the start of each depth of the last pcg_skeleton (host out, levels x n). */
+int pcg_degrees(pcg_handle *h, int32_t *deg_host, int64_t capacity);
+
+/* Sepset unions of the last pcg_skeleton: one row per ordered removed pair (x, y) whose
+ * union is non-empty: the union of every independent S seen from x's side
+ * (SkeletonDiscovery.py:129-130,135-136) as an n-bit mask (W = ceil(n/64) words).      */
+int pcg_sepset_count(pcg_handle *h, int64_t *count, int32_t *words_per_row);
+int pcg_sepset_export(pcg_handle *h, int32_t *xy_host /* 2*count */,
+                      uint64_t *bits_host /* count*W */, int64_t count);
+
+/* Records of the last pcg_skeleton (PCG_FLAG_RECORD) and the near-alpha list.         */
+int pcg_record_count(pcg_handle *h, int64_t *count, int64_t *near_alpha_count);
+int pcg_record_export(pcg_handle *h, pcg_record *rec_host, int64_t count,
+                      pcg_record *near_host, int64_t near_count);
+
+/* ---- multi-GPU level step (edge-sharded skeleton) ----------------------------------
+ * The host drives the level loop: pcg_level_begin prepares depth d from the current
+ * adjacency and returns the work size; pcg_level_run evaluates the chunk range
+ * [chunk_lo, chunk_hi) (an owner-disjoint slice of the level's work list), writing the
+ * removal flags (device n*n uint8, `rm_dev`, zeroed by begin) and sepset unions;
+ * the caller merges rm_dev across ranks (RCCL all-reduce MAX over xGMI) and calls
+ * pcg_level_end, which applies the removals identically on every rank.               */
+int pcg_skeleton_init(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N,
+                      double alpha, int flags, int8_t *removed_level);
+int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, int32_t *max_degree,
+                    uint8_t **rm_dev);
+int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi);
+int pcg_level_end(pcg_handle *h, pcg_stats *stats);
+/* Work weight of each chunk prefix (host out, total_chunks+1 int64) for load balance.  */
+int pcg_level_chunk_work(pcg_handle *h, int64_t *prefix_host, int64_t capacity);
+
+/* ---- K4: PageRank head -------------------------------------------------------------
+ * Replaces scikit-network 0.31.0 PageRank(damping_factor, solver='piteration', n_iter,
+ * tol).fit_transform(A) [U] (RCAEval/e2e/pc_pagerank.py:31-32,
+ * RCAEval/graph_heads/page_rank.py:85-89): A (device, m x m dense, lda) is the matrix
+ * passed to fit_transform. scores: device m doubles out. Returns PCG_ERR_INVALID
+ * ("The input matrix is empty.") when A has no non-zero (sknetwork check_format).       */
+int pcg_pagerank_dense(pcg_handle *h, const double *A, int64_t m, int64_t lda,
+                       double damping, int n_iter, double tol, double *scores);
+/* Same on a CSR input (device indptr[m+1], indices[nnz], data[nnz]).                   */
+int pcg_pagerank_csr(pcg_handle *h, const int32_t *indptr, const int32_t *indices,
+                     const double *data, int64_t m, int64_t nnz, double damping,
+                     int n_iter, double tol, double *scores);
+
+/* ---- random-walk head ------------------------------------------------------------
+ * Replaces RandomWalkScorer._walk (RCAEval/graph_heads/random_walk.py:179-186) for a
+ * column-stochastic transition matrix P (device, m x m, column c = distribution of the
+ * next node from c, as generate_transition_matrix :159-177 builds it): `num_loop` draws of
+ * numpy Generator(PCG64).choice(index, p=P[:, node]) from the given PCG64 state
+ * (state_hi/lo, inc_hi/lo: numpy's 128-bit state), start node `start`.
+ * counts: device m int64 out (visits per node).                                       */
+int pcg_random_walk(pcg_handle *h, const double *P, int64_t m, int64_t ldp, int64_t start,
+                    int64_t num_loop, uint64_t state_hi, uint64_t state_lo, uint64_t inc_hi,
+                    uint64_t inc_lo, int64_t *counts);
+
+/* ---- host orientation (C++, no device work) ----------------------------------------
+ * causal-learn UCSepset.uc_sepset(cg, priority=2) then Meek.meek(cg) [U] over the
+ * triple / triangle / kite enumerations of lib/causallearn/graph/GraphClass.py:108-188.
+ * adj: host n x n uint8 skeleton; sep_xy/sep_bits: host sepset-union rows as exported
+ * by pcg_sepset_export (count rows). graph: host n x n int32 endpoint codes out
+ * (TAIL=-1, ARROW=1; i->j <=> g[i,j]=-1, g[j,i]=1).                                     */
+int pcg_orient(int64_t n, const uint8_t *adj, const int32_t *sep_xy, const uint64_t *sep_bits,
+               int64_t count, int priority, int32_t *graph);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PCGPU_H */

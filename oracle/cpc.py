@@ -1,0 +1,99 @@
+"""ctypes binding of ``pc_oracle.c`` (C restatement of the stable PC-fisherz skeleton).
+
+TEST INFRASTRUCTURE ONLY — used by tests/, smoke() and bench.py's cpu_baseline leg.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+class OrcStats(ctypes.Structure):
+    _fields_ = [("tests", ctypes.c_int64 * 32), ("calls", ctypes.c_int64 * 32),
+                ("indep", ctypes.c_int64 * 32), ("levels", ctypes.c_int32),
+                ("error", ctypes.c_int32)]
+
+
+REC_DTYPE = np.dtype([("a", np.int32), ("b", np.int32), ("d", np.int32),
+                      ("s", np.int32, 5), ("p", np.float64)], align=True)
+
+
+def build() -> str:
+    path = os.path.join(_HERE, "liborc.so")
+    src = os.path.join(_HERE, "pc_oracle.c")
+    if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE, "liborc.so"])
+    return path
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        _LIB = ctypes.CDLL(build())
+        P = ctypes.c_void_p
+        _LIB.orc_skeleton.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                                      P, P, P, P, ctypes.c_int64, P, P, ctypes.c_int]
+        _LIB.orc_skeleton.restype = ctypes.c_int
+        _LIB.orc_fisherz_batch.argtypes = [P, ctypes.c_int, ctypes.c_int, P, P, ctypes.c_int,
+                                           ctypes.c_int64, P, P]
+        _LIB.orc_corrcoef.argtypes = [P, ctypes.c_int64, ctypes.c_int, P]
+    return _LIB
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+@dataclass
+class CSkeleton:
+    removed_level: np.ndarray    # n x n int8
+    deg_at_level: np.ndarray     # levels x n int32
+    side_union: np.ndarray       # n x n x W uint64 or None
+    records: np.ndarray          # REC_DTYPE or None
+    tests: list
+    calls: list
+    indep: list
+    levels: int
+    error: int
+
+    @property
+    def adj(self) -> np.ndarray:
+        n = self.removed_level.shape[0]
+        return (self.removed_level == -1) & ~np.eye(n, dtype=bool)
+
+
+def skeleton(C: np.ndarray, N: int, alpha: float = 0.05, max_depth: int = -1,
+             want_union: bool = True, record_cap: int = 0, nthreads: int = 0) -> CSkeleton:
+    C = np.ascontiguousarray(C, dtype=np.float64)
+    n = C.shape[0]
+    W = (n + 63) // 64
+    rl = np.empty((n, n), np.int8)
+    deg = np.zeros((32, n), np.int32)
+    su = np.empty((n, n, W), np.uint64) if want_union else None
+    rec = np.empty(record_cap, REC_DTYPE) if record_cap else None
+    cnt = np.zeros(1, np.int64)
+    st = OrcStats()
+    lib().orc_skeleton(_p(C), n, int(N), float(alpha), int(max_depth), _p(rl), _p(deg), _p(su),
+                       _p(rec), int(record_cap), _p(cnt), ctypes.byref(st), int(nthreads))
+    L = st.levels
+    if rec is not None:
+        if cnt[0] > record_cap:
+            raise RuntimeError(f"record buffer overflow: {cnt[0]} > {record_cap}")
+        rec = rec[: cnt[0]]
+    return CSkeleton(rl, deg[:L].copy(), su, rec, list(st.tests[:L]), list(st.calls[:L]),
+                     list(st.indep[:L]), L, st.error)
+
+
+def corrcoef(data: np.ndarray) -> np.ndarray:
+    X = np.ascontiguousarray(data, dtype=np.float64)
+    N, n = X.shape
+    C = np.empty((n, n), np.float64)
+    lib().orc_corrcoef(_p(X), N, n, _p(C))
+    return C

@@ -1,0 +1,288 @@
+/*
+ * pc_oracle.c — C restatement of stable PC-fisherz skeleton discovery.
+ * TEST INFRASTRUCTURE ONLY: linked by tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py (as the checker / CPU baseline), never by rcaeval_amd.
+ *
+ * Restates:
+ *   - lib/causallearn/utils/PCUtils/SkeletonDiscovery.py:70-144 (vendored; stable branch)
+ *       level loop `while max_degree()-1 > depth` (:72), node skip `len(Neigh_x) < depth-1`
+ *       (:83), `combinations(Neigh_x \ {y}, depth)` (:106), `p > alpha` -> deferred removal +
+ *       sepset union (:124-130, :135-136), removal at the level barrier (:141-144).
+ *   - lib/causallearn/graph/GraphClass.py:78-106: cache key (min, max, S) — here realised by
+ *       computing each unique test once on its canonical owner side, `neighbors`, `max_degree`.
+ *   - causal-learn 0.1.3.3 FisherZ.__call__ [U]: inv of the (d+2)x(d+2) sub-correlation by
+ *       LU with partial pivoting (LAPACK dgetf2/dgetrs order, as numpy.linalg.inv -> dgesv),
+ *       r = -inv01/sqrt(inv00*inv11), Z = 0.5*log((1+r)/(1-r)), X = sqrt(N-d-3)|Z|,
+ *       p = 2*(1 - ndtr(|X|)) with cephes ndtr's branch structure.
+ *
+ * Dedup rule (= the reference's memo): the test (min(x,y), max(x,y), S) is computed on
+ * node x's side unless y < x and S is a subset of adj(y) (then node y computes it). An
+ * independent result is OR-ed into x's side union, and into y's side union whenever
+ * S is a subset of adj(y) (the reference reaches the same cached p from both sides).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define ORC_MAXD 8
+
+typedef struct {
+    int64_t tests[32];   /* unique tests per depth            */
+    int64_t calls[32];   /* ci_test invocations per depth     */
+    int64_t indep[32];   /* unique tests with p > alpha       */
+    int32_t levels;      /* number of depths run              */
+    int32_t error;       /* 0 ok, 1 singular, 2 math domain   */
+} orc_stats;
+
+typedef struct {         /* one unique test (record mode) */
+    int32_t a, b;        /* a < b */
+    int32_t d;
+    int32_t s[5];        /* sorted conditioning set, -1 padded */
+    double p;
+} orc_record;
+
+/* cephes ndtr branch structure: p = 2*(1 - ndtr(|X|)). */
+static double pvalue_from_X(double X) {
+    double a = fabs(X);
+    double x = a * M_SQRT1_2;
+    double z = fabs(x), y;
+    if (z < M_SQRT1_2) {
+        y = 0.5 + 0.5 * erf(x);
+    } else {
+        y = 0.5 * erfc(z);
+        if (x > 0) y = 1.0 - y;
+    }
+    return 2.0 * (1.0 - y);
+}
+
+/* numpy.linalg.inv (dgesv with B = I) restricted to columns 0 and 1 of the inverse.
+ * Returns 0 ok, 1 exactly singular (LAPACK INFO > 0). */
+static int lu_inv01(double *A, int m, double *i00, double *i01, double *i11) {
+    int piv[ORC_MAXD + 2];
+    int info = 0;
+    for (int j = 0; j < m; ++j) {
+        int p = j;
+        double best = fabs(A[j * m + j]);
+        for (int i = j + 1; i < m; ++i) {
+            double v = fabs(A[i * m + j]);
+            if (v > best) { best = v; p = i; }
+        }
+        piv[j] = p;
+        if (A[p * m + j] != 0.0) {
+            if (p != j)
+                for (int k = 0; k < m; ++k) { double t = A[j * m + k]; A[j * m + k] = A[p * m + k]; A[p * m + k] = t; }
+            double rcp = 1.0 / A[j * m + j];
+            for (int i = j + 1; i < m; ++i) A[i * m + j] *= rcp;
+        } else if (!info) {
+            info = j + 1;
+        }
+        for (int i = j + 1; i < m; ++i) {
+            double l = A[i * m + j];
+            for (int k = j + 1; k < m; ++k) A[i * m + k] -= l * A[j * m + k];
+        }
+    }
+    if (info) return 1;
+    double B[2][ORC_MAXD + 2];
+    for (int c = 0; c < 2; ++c) {
+        for (int i = 0; i < m; ++i) B[c][i] = (i == c) ? 1.0 : 0.0;
+        for (int i = 0; i < m; ++i) { int p = piv[i]; if (p != i) { double t = B[c][i]; B[c][i] = B[c][p]; B[c][p] = t; } }
+        for (int i = 0; i < m; ++i) for (int k = 0; k < i; ++k) B[c][i] -= A[i * m + k] * B[c][k];
+        for (int i = m - 1; i >= 0; --i) {
+            for (int k = i + 1; k < m; ++k) B[c][i] -= A[i * m + k] * B[c][k];
+            B[c][i] /= A[i * m + i];
+        }
+    }
+    *i00 = B[0][0];
+    *i01 = B[1][0];   /* inv[0,1] = column 1, row 0 */
+    *i11 = B[1][1];
+    return 0;
+}
+
+/* One Fisher-z test on canonical (a<b, S sorted). err: 0 ok, 1 singular, 2 domain. */
+double orc_fisherz(const double *C, int n, int N, int a, int b, const int *S, int d, int *err) {
+    int var[ORC_MAXD + 2];
+    double A[(ORC_MAXD + 2) * (ORC_MAXD + 2)];
+    int m = d + 2;
+    var[0] = a; var[1] = b;
+    for (int k = 0; k < d; ++k) var[2 + k] = S[k];
+    for (int i = 0; i < m; ++i)
+        for (int j = 0; j < m; ++j) A[i * m + j] = C[(int64_t)var[i] * n + var[j]];
+    double i00, i01, i11;
+    *err = 0;
+    if (lu_inv01(A, m, &i00, &i01, &i11)) { *err = 1; return NAN; }
+    double prod = i00 * i11;
+    if (prod < 0) { *err = 2; return NAN; }            /* math.sqrt(negative) */
+    double r = -i01 / sqrt(prod);
+    double ratio = (1.0 + r) / (1.0 - r);               /* numpy scalar: x/0 -> inf */
+    if (ratio <= 0) { *err = 2; return NAN; }           /* math.log(<=0) */
+    double Z = 0.5 * log(ratio);
+    double dof = (double)N - d - 3;
+    if (dof < 0) { *err = 2; return NAN; }
+    double X = sqrt(dof) * fabs(Z);
+    return pvalue_from_X(X);
+}
+
+static inline int has_bit(const uint64_t *row, int j) { return (row[j >> 6] >> (j & 63)) & 1; }
+
+/*
+ * Stable skeleton. C: n x n row-major correlation. Outputs:
+ *   removed_level[n*n]   int8, -1 = survives, else depth at which the edge was removed
+ *   deg_at_level[32*n]   optional (NULL ok): degree of each node at the start of each depth
+ *   side_union[n*n*W]    optional (NULL ok), W = ceil(n/64): for a removed pair (x,y) the
+ *                        union of independent S on x's side at the removal depth
+ *   rec/rec_cap/rec_count optional: every unique test (record mode)
+ * max_depth < 0: unlimited. nthreads <= 0: all.
+ */
+int orc_skeleton(const double *C, int n, int N, double alpha, int max_depth,
+                 int8_t *removed_level, int32_t *deg_at_level, uint64_t *side_union,
+                 orc_record *rec, int64_t rec_cap, int64_t *rec_count,
+                 orc_stats *st, int nthreads) {
+    const int W = (n + 63) / 64;
+    uint64_t *adj = (uint64_t *)calloc((size_t)n * W, sizeof(uint64_t));
+    int32_t *deg = (int32_t *)malloc(sizeof(int32_t) * n);
+    int32_t *nbr = (int32_t *)malloc(sizeof(int32_t) * (size_t)n * n);
+    uint8_t *rm = (uint8_t *)calloc((size_t)n * n, 1);
+    if (!adj || !deg || !nbr || !rm) return -1;
+    memset(st, 0, sizeof(*st));
+    for (int64_t i = 0; i < (int64_t)n * n; ++i) removed_level[i] = -1;
+    for (int x = 0; x < n; ++x)
+        for (int y = 0; y < n; ++y)
+            if (x != y) adj[(size_t)x * W + (y >> 6)] |= 1ull << (y & 63);
+    if (side_union) memset(side_union, 0, sizeof(uint64_t) * (size_t)n * n * W);
+    if (rec_count) *rec_count = 0;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+    int depth = -1;
+    volatile int error = 0;
+    for (;;) {
+        int maxdeg = 0;
+        for (int x = 0; x < n; ++x) {
+            int c = 0;
+            for (int w = 0; w < W; ++w) c += __builtin_popcountll(adj[(size_t)x * W + w]);
+            deg[x] = c;
+            if (c > maxdeg) maxdeg = c;
+            int k = 0;
+            for (int y = 0; y < n; ++y) if (has_bit(adj + (size_t)x * W, y)) nbr[(size_t)x * n + k++] = y;
+        }
+        if (!(maxdeg - 1 > depth)) break;
+        if (max_depth >= 0 && depth >= max_depth) break;
+        ++depth;
+        if (depth >= 32 || depth > ORC_MAXD) break;
+        if (deg_at_level) memcpy(deg_at_level + (size_t)depth * n, deg, sizeof(int32_t) * n);
+        memset(rm, 0, (size_t)n * n);
+        int64_t tests = 0, calls = 0, indep = 0;
+        const int d = depth;
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : tests, calls, indep)
+        for (int x = 0; x < n; ++x) {
+            const int D = deg[x];
+            if (D < d - 1) continue;
+            const int32_t *nx = nbr + (size_t)x * n;
+            int idx[ORC_MAXD + 1], S[ORC_MAXD + 1], cand[1];
+            (void)cand;
+            for (int yi = 0; yi < D; ++yi) {
+                const int y = nx[yi];
+                const uint64_t *ady = adj + (size_t)y * W;
+                /* combinations of nx \ {y} of size d, lexicographic */
+                const int M = D - 1;
+                if (M < d) continue;
+                for (int k = 0; k < d; ++k) idx[k] = k;
+                for (;;) {
+                    int in_y = 1;
+                    for (int k = 0; k < d; ++k) {
+                        int li = idx[k] < yi ? idx[k] : idx[k] + 1;
+                        S[k] = nx[li];
+                        if (!has_bit(ady, S[k])) in_y = 0;
+                    }
+                    calls++;
+                    if (!(y < x && in_y)) {
+                        int a = x < y ? x : y, b = x < y ? y : x, err;
+                        double p = orc_fisherz(C, n, N, a, b, S, d, &err);
+                        if (err) error = err;
+                        tests++;
+                        if (rec) {
+                            int64_t slot = __atomic_fetch_add(rec_count, 1, __ATOMIC_RELAXED);
+                            if (slot < rec_cap) {
+                                orc_record *r = rec + slot;
+                                r->a = a; r->b = b; r->d = d;
+                                for (int k = 0; k < 5; ++k) r->s[k] = k < d ? S[k] : -1;
+                                r->p = p;
+                            }
+                        }
+                        if (p > alpha) {
+                            indep++;
+                            __atomic_store_n(&rm[(size_t)x * n + y], 1, __ATOMIC_RELAXED);
+                            __atomic_store_n(&rm[(size_t)y * n + x], 1, __ATOMIC_RELAXED);
+                            if (side_union) {
+                                uint64_t *ux = side_union + ((size_t)x * n + y) * W;
+                                uint64_t *uy = side_union + ((size_t)y * n + x) * W;
+                                for (int k = 0; k < d; ++k) {
+                                    __atomic_fetch_or(&ux[S[k] >> 6], 1ull << (S[k] & 63), __ATOMIC_RELAXED);
+                                    if (in_y) __atomic_fetch_or(&uy[S[k] >> 6], 1ull << (S[k] & 63), __ATOMIC_RELAXED);
+                                }
+                            }
+                        }
+                    }
+                    /* next combination */
+                    int k = d - 1;
+                    while (k >= 0 && idx[k] == M - d + k) --k;
+                    if (k < 0) break;
+                    idx[k]++;
+                    for (int j = k + 1; j < d; ++j) idx[j] = idx[j - 1] + 1;
+                }
+            }
+        }
+        st->tests[depth] = tests;
+        st->calls[depth] = calls;
+        st->indep[depth] = indep;
+        st->levels = depth + 1;
+        for (int x = 0; x < n; ++x)
+            for (int y = 0; y < n; ++y)
+                if (rm[(size_t)x * n + y]) {
+                    adj[(size_t)x * W + (y >> 6)] &= ~(1ull << (y & 63));
+                    removed_level[(size_t)x * n + y] = (int8_t)depth;
+                }
+        if (error) break;
+    }
+    st->error = error;
+    free(adj); free(deg); free(nbr); free(rm);
+    return error ? 1 : 0;
+}
+
+/* Fisher-z p-values for an explicit list of tests (used to cross-check the numpy oracle). */
+void orc_fisherz_batch(const double *C, int n, int N, const int32_t *ab, const int32_t *S, int d,
+                       int64_t count, double *p_out, int32_t *err_out) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < count; ++i) {
+        int err;
+        p_out[i] = orc_fisherz(C, n, N, ab[2 * i], ab[2 * i + 1], S + i * (d > 0 ? d : 1), d, &err);
+        err_out[i] = err;
+    }
+}
+
+/* Threaded np.corrcoef(data.T)-equivalent (numpy order: centre, dot, *1/(N-1), /s_i, /s_j, clip). */
+void orc_corrcoef(const double *X, int64_t N, int n, double *C) {
+    double *mean = (double *)calloc(n, sizeof(double));
+    for (int64_t t = 0; t < N; ++t) for (int j = 0; j < n; ++j) mean[j] += X[t * n + j];
+    for (int j = 0; j < n; ++j) mean[j] /= (double)N;
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int i = 0; i < n; ++i)
+        for (int j = i; j < n; ++j) {
+            double s = 0;
+            for (int64_t t = 0; t < N; ++t) s += (X[t * n + i] - mean[i]) * (X[t * n + j] - mean[j]);
+            C[(int64_t)i * n + j] = C[(int64_t)j * n + i] = s * (1.0 / (double)(N - 1));
+        }
+    double *sd = (double *)malloc(sizeof(double) * n);
+    for (int i = 0; i < n; ++i) sd[i] = sqrt(C[(int64_t)i * n + i]);
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) {
+            double v = C[(int64_t)i * n + j] / sd[i];
+            v = v / sd[j];
+            C[(int64_t)i * n + j] = v > 1 ? 1 : (v < -1 ? -1 : v);
+        }
+    free(mean); free(sd);
+}

@@ -1,0 +1,137 @@
+"""ctypes binding of ``libpcgpu.so`` (declared in ``include/pcgpu.h``).
+
+The library is built in-tree (``rcaeval_amd/libpcgpu.so``) by ``__graft_entry__.build()`` /
+``make -C rcaeval_amd/csrc``. There is no CPU fallback: if the library is missing or no
+GPU is visible, every engine entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpcgpu.so")
+
+PCG_OK = 0
+PCG_ERR_INVALID = -1
+PCG_ERR_OOM = -2
+PCG_ERR_HIP = -3
+PCG_ERR_SINGULAR = -4
+PCG_ERR_DOMAIN = -5
+PCG_ERR_RCCL = -6
+PCG_ERR_OVERFLOW = -7
+
+PCG_FLAG_FULL_P = 0x1
+PCG_FLAG_RECORD = 0x2
+PCG_FLAG_EXACT_ALL = 0x4
+
+PCG_MAX_LEVELS = 32
+PCG_MAX_DEPTH = 12
+
+I64 = ctypes.c_int64
+I32 = ctypes.c_int32
+P = ctypes.c_void_p
+D = ctypes.c_double
+
+
+class PcgStats(ctypes.Structure):
+    _fields_ = [
+        ("tests", I64 * PCG_MAX_LEVELS),
+        ("calls", I64 * PCG_MAX_LEVELS),
+        ("indep", I64 * PCG_MAX_LEVELS),
+        ("exact", I64 * PCG_MAX_LEVELS),
+        ("near_alpha", I64 * PCG_MAX_LEVELS),
+        ("edges_after", I64 * PCG_MAX_LEVELS),
+        ("max_degree", I32 * PCG_MAX_LEVELS),
+        ("level_ms", D * PCG_MAX_LEVELS),
+        ("kernel_ms", D * PCG_MAX_LEVELS),
+        ("levels", I32),
+        ("error", I32),
+    ]
+
+    def as_dict(self) -> dict:
+        L = self.levels
+        return {
+            "levels": L,
+            "error": self.error,
+            "tests": list(self.tests[:L]),
+            "calls": list(self.calls[:L]),
+            "indep": list(self.indep[:L]),
+            "exact": list(self.exact[:L]),
+            "near_alpha": list(self.near_alpha[:L]),
+            "edges_after": list(self.edges_after[:L]),
+            "max_degree": list(self.max_degree[:L]),
+            "level_ms": list(self.level_ms[:L]),
+            "kernel_ms": list(self.kernel_ms[:L]),
+        }
+
+
+class PcgRecord(ctypes.Structure):
+    _fields_ = [("a", I32), ("b", I32), ("d", I32), ("s", I32 * PCG_MAX_DEPTH), ("p", D)]
+
+
+# (name, restype, argtypes) — exactly the exports of include/pcgpu.h
+SIGNATURES = [
+    ("pcg_create", I32, [ctypes.c_int, ctypes.POINTER(P)]),
+    ("pcg_destroy", I32, [P]),
+    ("pcg_last_error", ctypes.c_char_p, [P]),
+    ("pcg_set_stream", I32, [P, P]),
+    ("pcg_set_capacity", I32, [P, I64, I64]),
+    ("pcg_corr", I32, [P, P, I64, I64, I64, P, I64]),
+    ("pcg_skeleton", I32, [P, P, I64, I64, I64, D, ctypes.c_int, ctypes.c_int, P, ctypes.POINTER(PcgStats)]),
+    ("pcg_degrees", I32, [P, P, I64]),
+    ("pcg_sepset_count", I32, [P, ctypes.POINTER(I64), ctypes.POINTER(I32)]),
+    ("pcg_sepset_export", I32, [P, P, P, I64]),
+    ("pcg_record_count", I32, [P, ctypes.POINTER(I64), ctypes.POINTER(I64)]),
+    ("pcg_record_export", I32, [P, P, I64, P, I64]),
+    ("pcg_skeleton_init", I32, [P, P, I64, I64, I64, D, ctypes.c_int, P]),
+    ("pcg_level_begin", I32, [P, ctypes.c_int, ctypes.POINTER(I64), ctypes.POINTER(I32), ctypes.POINTER(P)]),
+    ("pcg_level_run", I32, [P, I64, I64]),
+    ("pcg_level_end", I32, [P, ctypes.POINTER(PcgStats)]),
+    ("pcg_level_chunk_work", I32, [P, P, I64]),
+    ("pcg_pagerank_dense", I32, [P, P, I64, I64, D, ctypes.c_int, D, P]),
+    ("pcg_pagerank_csr", I32, [P, P, P, P, I64, I64, D, ctypes.c_int, D, P]),
+    ("pcg_random_walk", I32, [P, P, I64, I64, I64, I64, ctypes.c_uint64, ctypes.c_uint64,
+                              ctypes.c_uint64, ctypes.c_uint64, P]),
+    ("pcg_orient", I32, [I64, P, P, P, I64, ctypes.c_int, P]),
+]
+
+_lib = None
+
+
+class EngineUnavailable(RuntimeError):
+    """The HIP engine library is missing or unusable (no silent CPU fallback exists)."""
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise EngineUnavailable(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "or `make -C rcaeval_amd/csrc` (hipcc --offload-arch=gfx950)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class PcgError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[pcgpu {code}] {msg}")
+        self.code = code
+
+
+def check(handle, rc: int, what: str) -> int:
+    if rc < 0:
+        msg = load().pcg_last_error(handle)
+        msg = msg.decode() if msg else what
+        if rc in (PCG_ERR_SINGULAR, PCG_ERR_DOMAIN):
+            # causal-learn raises ValueError here [U]; @rca turns it into dummy ranks.
+            raise ValueError(msg)
+        raise PcgError(rc, f"{what}: {msg}")
+    return rc

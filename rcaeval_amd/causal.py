@@ -1,0 +1,194 @@
+"""Drop-in for causal-learn's ``pc(...)`` on the MI355X engine.
+
+Mirrors causal-learn 0.1.3.3 ``search/ConstraintBased/PC.py`` ``pc`` / ``pc_alg`` [U] as
+called by RCAEval (``RCAEval/e2e/pc_pagerank.py:19``, ``RCAEval/graph_construction/pc.py:15-20,
+46-56``): same arguments, same ``CausalGraph`` surface (``.G.graph`` endpoint codes,
+``.sepset`` n x n lists of tuples, ``.p_values``, ``.PC_elapsed``, ``.no_ci_tests``), same
+error behaviour (``ValueError`` on a singular sub-correlation matrix or a math domain error,
+``AssertionError`` on NaN/inf input).
+
+Pipeline: host → HBM once (X), K1 correlation (fp64 MFMA), K2/K3 level-synchronous
+skeleton on the device, sepset unions + removal depths back to the host, orientation
+(UCSepset priority 2 + Meek) in host C++ (``pcg_orient``).
+"""
+from __future__ import annotations
+
+import time
+import warnings
+
+import numpy as np
+
+from . import _lib
+from .engine import SkeletonOut, get_engine, orient
+
+fisherz = "fisherz"
+chisq = "chisq"
+gsq = "gsq"
+kci = "kci"
+mv_fisherz = "mv_fisherz"
+
+
+class GraphNode:
+    def __init__(self, name: str):
+        self.name = name
+
+    def get_name(self) -> str:
+        return self.name
+
+    def __repr__(self) -> str:
+        return self.name
+
+
+class GeneralGraph:
+    """Endpoint-code matrix holder (causal-learn ``GeneralGraph`` [U] subset)."""
+
+    def __init__(self, graph: np.ndarray, names):
+        self.graph = graph
+        self.nodes = [GraphNode(str(nm)) for nm in names]
+        self.num_vars = len(self.nodes)
+
+    def get_nodes(self):
+        return self.nodes
+
+    def get_node_names(self):
+        return [nd.get_name() for nd in self.nodes]
+
+    def get_num_edges(self) -> int:
+        return int(np.count_nonzero(np.triu((self.graph != 0) | (self.graph.T != 0), 1)))
+
+
+class SepsetArray:
+    """``cg.sepset`` (n x n object array of lists of tuples), materialised per entry.
+
+    Entry [a, b] follows ``SkeletonDiscovery.py:135-136``: for every depth at which the pair
+    was adjacent, one tuple from a's visit then one from b's visit (each visit skipped when
+    that node had fewer than depth-1 neighbours, ``:83``); the tuple is the union of all
+    independent S from that side (``:129-130``), empty unless the edge was removed there.
+    Tuple elements are ``np.int64``, inserted ascending into a set (the reference inserts in
+    the order the S sets are enumerated; only the tuple-internal order can differ).
+    """
+
+    def __init__(self, out: SkeletonOut):
+        self.shape = (out.n, out.n)
+        self._out = out
+        self._levels = out.levels
+        n = out.n
+        self._rl = out.removed_level
+        self._deg = out.deg_levels
+        self._rows: dict = {}
+        W = out.sep_bits.shape[1] if out.sep_bits.size else (n + 63) // 64
+        for r in range(len(out.sep_xy)):
+            x, y = int(out.sep_xy[r, 0]), int(out.sep_xy[r, 1])
+            bits = out.sep_bits[r]
+            members = []
+            for w in range(W):
+                v = int(bits[w])
+                while v:
+                    b = (v & -v).bit_length() - 1
+                    members.append(w * 64 + b)
+                    v &= v - 1
+            self._rows[(x, y)] = members
+
+    def _side(self, x: int, y: int) -> tuple:
+        mem = self._rows.get((x, y))
+        if not mem:
+            return ()
+        return tuple(set(np.int64(m) for m in mem))
+
+    def __getitem__(self, key):
+        if isinstance(key, tuple) and len(key) == 2:
+            i, j = int(key[0]), int(key[1])
+            if i == j:
+                return None
+            a, b = (i, j) if i < j else (j, i)
+            rl = int(self._rl[a, b])
+            last = rl if rl >= 0 else self._levels - 1
+            out = []
+            for d in range(0, last + 1):
+                for v, w in ((a, b), (b, a)):
+                    if self._deg[d, v] < d - 1:
+                        continue
+                    out.append(self._side(v, w) if d == rl else ())
+            return out if out else None
+        if isinstance(key, (int, np.integer)):
+            return [self[int(key), j] for j in range(self.shape[1])]
+        raise TypeError("SepsetArray supports [i, j] indexing")
+
+    def to_numpy(self) -> np.ndarray:
+        n = self.shape[0]
+        arr = np.empty((n, n), object)
+        for i in range(n):
+            for j in range(n):
+                arr[i, j] = self[i, j]
+        return arr
+
+
+class CausalGraph:
+    """causal-learn ``CausalGraph`` result surface [U] (``lib/causallearn/graph/GraphClass.py:19-60``)."""
+
+    def __init__(self, graph: np.ndarray, names, skeleton: SkeletonOut | None):
+        self.G = GeneralGraph(graph, names)
+        self.skeleton = skeleton
+        self.sepset = SepsetArray(skeleton) if skeleton is not None else np.empty(graph.shape, object)
+        self.p_values = np.empty(graph.shape, object)
+        self.PC_elapsed = -1
+        self.no_ci_tests = int(sum(skeleton.stats["calls"])) if skeleton is not None else 0
+        self.stats = skeleton.stats if skeleton is not None else {}
+
+
+def _check_supported(indep_test, stable, uc_rule, uc_priority, mvpc, background_knowledge):
+    name = indep_test if isinstance(indep_test, str) else getattr(indep_test, "__name__", str(indep_test))
+    if name != fisherz:
+        raise NotImplementedError(f"indep_test={name!r}: only fisherz runs on the MI355X engine")
+    if mvpc:
+        raise NotImplementedError("mvpc=True (missing-value PC) is not on the engine's path")
+    if not stable:
+        raise NotImplementedError("stable=False (order-dependent PC) is a later-round item (SURVEY §8(f) rank 3)")
+    if uc_rule != 0:
+        raise NotImplementedError("uc_rule != 0 is not on the pc_pagerank / pc_randomwalk path")
+    if uc_priority not in (2,):
+        raise NotImplementedError(f"uc_priority={uc_priority}: only priority 2 (the RCAEval default) is built")
+    if background_knowledge is not None:
+        raise NotImplementedError("background_knowledge is a later-round item")
+
+
+def skeleton_from_data(data: np.ndarray, alpha: float = 0.05, max_depth: int = -1, flags: int = 0,
+                       device: int | None = None, record_capacity: int = 0):
+    """Correlation + stable skeleton on the GPU; returns (SkeletonOut, C tensor)."""
+    eng = get_engine(device)
+    X = np.asarray(data, dtype=np.float64)
+    C = eng.corr(X)
+    out = eng.skeleton(C, X.shape[0], alpha=alpha, max_depth=max_depth, flags=flags,
+                       record_capacity=record_capacity)
+    return out, C
+
+
+def pc(data: np.ndarray, alpha: float = 0.05, indep_test=fisherz, stable: bool = True, uc_rule: int = 0,
+       uc_priority: int = 2, mvpc: bool = False, correction_name: str = "MV_Crtn_Fisher_Z",
+       background_knowledge=None, verbose: bool = False, show_progress: bool = True, node_names=None,
+       max_depth: int = -1, device: int | None = None, full_p: bool = False, **kwargs) -> CausalGraph:
+    """causal-learn ``pc`` [U] on the GPU (fisherz, stable, uc_rule 0, uc_priority 2)."""
+    assert type(data) == np.ndarray  # SkeletonDiscovery.py:47
+    assert 0 < alpha < 1
+    _check_supported(indep_test, stable, uc_rule, uc_priority, mvpc, background_knowledge)
+    if data.shape[0] < data.shape[1]:
+        warnings.warn("The number of features is much larger than the sample size!")
+    X = np.asarray(data, dtype=np.float64)
+    # CIT_Base.assert_input_data_is_valid [U]
+    assert not np.isnan(X).any(), "Input data contains NaN. Please check."
+    assert not np.isinf(X).any(), "Input data contains Inf. Please check."
+    n = X.shape[1]
+    names = node_names if node_names is not None else [f"X{i + 1}" for i in range(n)]
+    start = time.time()
+    if n == 0:
+        raise ValueError("max() arg is an empty sequence")
+    if n == 1:
+        cg = CausalGraph(np.zeros((1, 1), int), names, None)
+        cg.PC_elapsed = time.time() - start
+        return cg
+    flags = _lib.PCG_FLAG_FULL_P if full_p else 0
+    out, _ = skeleton_from_data(X, alpha=alpha, max_depth=max_depth, flags=flags, device=device)
+    graph = orient(out.adj, out.sep_xy, out.sep_bits, priority=2).astype(int)
+    cg = CausalGraph(graph, names, out)
+    cg.PC_elapsed = time.time() - start
+    return cg

@@ -1,0 +1,98 @@
+// api.hip — handle lifetime, error reporting and scratch management of libpcgpu.so.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include "handle.h"
+
+int pcg_fail(pcg_handle *h, int code, const char *fmt, ...) {
+    if (h) {
+        char buf[1024];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof(buf), fmt, ap);
+        va_end(ap);
+        h->err = buf;
+    }
+    return code;
+}
+
+bool pcg_ensure(pcg_handle *h, DevBuf &b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (b.bytes >= bytes) return true;
+    if (b.p) {
+        hipStreamSynchronize(h->stream);
+        hipFree(b.p);
+        b.p = nullptr;
+        b.bytes = 0;
+    }
+    const size_t want = bytes + bytes / 8;  // headroom for the next level / call
+    if (hipMalloc(&b.p, want) != hipSuccess) {
+        b.p = nullptr;
+        return false;
+    }
+    b.bytes = want;
+    return true;
+}
+
+extern "C" int pcg_create(int device, pcg_handle **out) {
+    if (!out) return PCG_ERR_INVALID;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return PCG_ERR_HIP;
+    if (device < 0 || device >= ndev) return PCG_ERR_INVALID;
+    if (hipSetDevice(device) != hipSuccess) return PCG_ERR_HIP;
+    pcg_handle *h = new pcg_handle();
+    h->device = device;
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return PCG_ERR_HIP;
+    }
+    h->own_stream = true;
+    for (auto &e : h->ev)
+        if (hipEventCreate(&e) != hipSuccess) {
+            delete h;
+            return PCG_ERR_HIP;
+        }
+    *out = h;
+    return PCG_OK;
+}
+
+extern "C" int pcg_destroy(pcg_handle *h) {
+    if (!h) return PCG_OK;
+    hipSetDevice(h->device);
+    if (h->stream) hipStreamSynchronize(h->stream);
+    DevBuf *bufs[] = {&h->adj, &h->deg, &h->off, &h->nbr, &h->rm, &h->ug, &h->cpre, &h->binom, &h->ctr,
+                      &h->deferred, &h->records, &h->nearbuf, &h->exportbuf, &h->export_xy, &h->diag,
+                      &h->colmean, &h->pr_scratch};
+    for (DevBuf *b : bufs)
+        if (b->p) hipFree(b->p);
+    for (auto &e : h->ev)
+        if (e) hipEventDestroy(e);
+    if (h->own_stream && h->stream) hipStreamDestroy(h->stream);
+    delete h;
+    return PCG_OK;
+}
+
+extern "C" const char *pcg_last_error(pcg_handle *h) { return h ? h->err.c_str() : "null handle"; }
+
+extern "C" int pcg_set_stream(pcg_handle *h, void *hip_stream) {
+    if (!h) return PCG_ERR_INVALID;
+    hipStreamSynchronize(h->stream);
+    if (h->own_stream && h->stream) hipStreamDestroy(h->stream);
+    if (hip_stream) {
+        h->stream = (hipStream_t)hip_stream;
+        h->own_stream = false;
+    } else {
+        if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) return PCG_ERR_HIP;
+        h->own_stream = true;
+    }
+    return PCG_OK;
+}
+
+extern "C" int pcg_set_capacity(pcg_handle *h, int64_t record_capacity, int64_t deferred_capacity) {
+    if (!h) return PCG_ERR_INVALID;
+    if (record_capacity > 0) h->rec_cap = record_capacity;
+    if (deferred_capacity > 0) h->def_cap = deferred_capacity;
+    return PCG_OK;
+}

@@ -1,0 +1,82 @@
+// handle.h — engine handle shared by the HIP translation units of libpcgpu.so.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "pcgpu.h"
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+
+// Device-side counters of one level (zeroed by pcg_level_begin).
+struct DevCounters {
+    unsigned long long tests;      // unique tests evaluated
+    unsigned long long indep;      // unique tests with p > alpha
+    unsigned long long deferred;   // tests pushed to the exact path (may exceed capacity)
+    unsigned long long exact;      // tests resolved by the exact path
+    unsigned long long records;    // records written (may exceed capacity)
+    unsigned long long near_alpha; // |p - alpha| < 1e-9 (may exceed capacity)
+    unsigned long long exported;   // sepset rows exported this level
+    unsigned long long error;      // PCG_ERR_* bits (1 singular, 2 domain)
+};
+
+struct DeferredEntry {             // one test routed to the exact (LU) path
+    int32_t x, y;                  // visiting node x, neighbour y
+    int32_t s[PCG_MAX_DEPTH];      // conditioning set (global ids)
+};
+
+struct pcg_handle {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    std::string err;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+
+    // scratch
+    DevBuf adj, deg, off, nbr, rm, ug, cpre, binom, ctr, deferred, records, nearbuf, exportbuf,
+        export_xy, diag, colmean, pr_scratch;
+    std::vector<uint64_t> binom_h;   // host copy of the binomial table
+    int64_t rec_cap = 0, def_cap = 1 << 16, near_cap = 1 << 16;
+    int64_t export_cap = 0;          // rows
+    int64_t export_rows = 0;         // rows exported so far (host mirror)
+    int binom_n = -1;                // binom table built for 0..binom_n
+
+    // skeleton state (single-GPU and level-step API)
+    const double *C = nullptr;
+    int64_t n = 0, ldc = 0, N = 0;
+    int W = 0;
+    double alpha = 0.05;
+    int flags = 0;
+    int8_t *rl = nullptr;
+    int depth = -1;                  // depth prepared by level_begin
+    int64_t total_chunks = 0;
+    int chunk = 256;                 // S ranks per block (= block size)
+    int32_t maxdeg = 0;
+    int64_t sumdeg = 0;
+    std::vector<int32_t> deg_h;      // degrees at the start of the current depth
+    std::vector<int32_t> deg_levels; // levels x n
+    std::vector<int64_t> cpre_h;     // chunk prefix (n + 1)
+    std::vector<int64_t> work_h;     // per-node tests estimate
+    std::vector<pcg_record> rec_h, near_h;
+    int64_t rec_total = 0, near_total = 0;
+    pcg_stats st{};
+    float run_ms = 0.f;              // CI-test kernel time of the current level
+};
+
+int pcg_fail(pcg_handle *h, int code, const char *fmt, ...);
+bool pcg_ensure(pcg_handle *h, DevBuf &b, size_t bytes);   // grow-only allocation
+
+#define PCG_HIP(h, expr)                                                                    \
+    do {                                                                                    \
+        hipError_t _e = (expr);                                                             \
+        if (_e != hipSuccess)                                                               \
+            return pcg_fail((h), PCG_ERR_HIP, "%s failed: %s (%s:%d)", #expr,               \
+                            hipGetErrorString(_e), __FILE__, __LINE__);                     \
+    } while (0)

@@ -1,0 +1,230 @@
+// orient.cpp — host orientation of the PC skeleton (no device work).
+//
+// Restates causal-learn 0.1.3.3 [U] (not on disk; pinned requirements.txt:20):
+//   pc_alg: cg_2 = UCSepset.uc_sepset(cg_1, uc_priority); cg = Meek.meek(cg_2)
+// over the enumerations of the vendored lib/causallearn/graph/GraphClass.py:
+//   find_tails / find_arrow_heads :108-116 (np.where row-major, entries (col, row))
+//   find_adj :145-147 (tails + arrow heads)
+//   find_unshielded_triples :157-165, find_triangles :167-176, find_kites :178-188
+//   (itertools.permutations order), and GeneralGraph [U] edge semantics:
+//   add_edge(Edge(i, j, TAIL, ARROW)) is a no-op on an existing non-bidirected edge, else
+//   g[i,j] = -1, g[j,i] = 1 and adjust_dpath(i, j); remove_edge of a fully directed edge
+//   calls reconstitute_dpath(get_graph_edges()); is_ancestor_of(a, b) = dpath[b, a] == 1.
+// uc_sepset(priority=2): for (x, y, z) in unshielded triples with x < z, if y is in no S of
+// sepset[x, z] (= the union of both sides' unions at the removal depth) and neither y->x nor
+// y->z is fully directed: re-orient x->y and z->y. Meek: R1 over triples, R2 over
+// triangles, R3 over kites until no change, skipping an orientation that would point at
+// an ancestor (is_ancestor_of check). Parity of these [U] details is unpinned offline.
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <unordered_map>
+#include <vector>
+
+#include "pcgpu.h"
+
+namespace {
+
+struct Graph {
+    int64_t n;
+    std::vector<int8_t> g;      // endpoint codes
+    std::vector<uint8_t> dpath; // dpath[j * n + i] == 1 <=> i is an ancestor of j
+
+    int8_t &at(int64_t i, int64_t j) { return g[i * n + j]; }
+    int8_t at(int64_t i, int64_t j) const { return g[i * n + j]; }
+
+    void adjust_dpath(int64_t i, int64_t j) {
+        uint8_t *dp = dpath.data();
+        dp[j * n + i] = 1;
+        for (int64_t k = 0; k < n; ++k) {
+            if (dp[i * n + k] == 1) dp[j * n + k] = 1;
+            if (dp[k * n + j] == 1) dp[k * n + i] = 1;
+        }
+    }
+    void reconstitute_dpath() {
+        for (int64_t i = 0; i < n; ++i) adjust_dpath(i, i);
+        // get_graph_edges(): i ascending, j > i ascending; Edge normalised tail-first for
+        // directed edges; edges.pop() consumes from the end.
+        std::vector<std::pair<int64_t, int64_t>> edges;
+        for (int64_t i = 0; i < n; ++i)
+            for (int64_t j = i + 1; j < n; ++j) {
+                const int8_t e1 = at(i, j), e2 = at(j, i);
+                if (e1 == 0 && e2 == 0) continue;
+                if (e1 == 1 && e2 == -1) edges.push_back({j, i});  // i <- j: node1 = j
+                else edges.push_back({i, j});
+            }
+        while (!edges.empty()) {
+            auto e = edges.back();
+            edges.pop_back();
+            adjust_dpath(e.first, e.second);
+        }
+    }
+    bool is_fully_directed(int64_t i, int64_t j) const { return at(i, j) == -1 && at(j, i) == 1; }
+    bool is_undirected(int64_t i, int64_t j) const { return at(i, j) == -1 && at(j, i) == -1; }
+    bool is_ancestor_of(int64_t a, int64_t b) const { return dpath[b * n + a] == 1; }
+    bool adjacent(int64_t i, int64_t j) const { return at(i, j) != 0; }
+
+    // remove the edge between i and j (GeneralGraph.remove_edge(get_edge(i, j)))
+    void remove_edge(int64_t i, int64_t j) {
+        const bool directed = is_fully_directed(i, j) || is_fully_directed(j, i);
+        at(i, j) = 0;
+        at(j, i) = 0;
+        if (directed) reconstitute_dpath();
+    }
+    // add_edge(Edge(i, j, TAIL, ARROW))
+    void add_directed(int64_t i, int64_t j) {
+        const int8_t e1 = at(i, j), e2 = at(j, i);
+        const bool bidirected = e1 == 1 && e2 == 1;
+        const bool existing = !bidirected && (e1 != 0 || e2 != 0);
+        if (existing) return;
+        if (bidirected) return;  // not produced by PC orientation
+        at(j, i) = 1;
+        at(i, j) = -1;
+        adjust_dpath(i, j);
+    }
+};
+
+// find_adj(): tails then arrow heads, each np.where row-major with entries (col, row)
+std::vector<std::pair<int32_t, int32_t>> find_adj(const Graph &G) {
+    std::vector<std::pair<int32_t, int32_t>> adj;
+    for (int code : {-1, 1})
+        for (int64_t r = 0; r < G.n; ++r)
+            for (int64_t c = 0; c < G.n; ++c)
+                if (G.at(r, c) == code) adj.push_back({(int32_t)c, (int32_t)r});
+    return adj;
+}
+
+struct Triple { int32_t i, j, k; };
+struct Kite { int32_t i, j, k, l; };
+
+// permutations(Adj, 2) filtered: pair0 = (i, j), pair1 = (j', k) with j' == j, i != k
+template <class Pred>
+std::vector<Triple> enumerate_triples(const Graph &G, const std::vector<std::pair<int32_t, int32_t>> &adj,
+                                      Pred keep) {
+    // positions of Adj entries by first element, ascending
+    std::vector<std::vector<int32_t>> by_first(G.n);
+    for (size_t b = 0; b < adj.size(); ++b) by_first[adj[b].first].push_back((int32_t)b);
+    std::vector<Triple> out;
+    for (size_t a = 0; a < adj.size(); ++a) {
+        const int32_t i = adj[a].first, j = adj[a].second;
+        for (int32_t b : by_first[j]) {
+            if ((size_t)b == a) continue;
+            const int32_t k = adj[b].second;
+            if (i != k && keep(i, j, k)) out.push_back({i, j, k});
+        }
+    }
+    return out;
+}
+
+}  // namespace
+
+extern "C" int pcg_orient(int64_t n, const uint8_t *adj, const int32_t *sep_xy, const uint64_t *sep_bits,
+                          int64_t count, int priority, int32_t *graph) {
+    if (n < 1 || !adj || !graph || (count > 0 && (!sep_xy || !sep_bits))) return PCG_ERR_INVALID;
+    if (priority != 2) return PCG_ERR_INVALID;  // the pc_pagerank / pc_randomwalk orientation
+    const int64_t W = (n + 63) / 64;
+    Graph G;
+    G.n = n;
+    G.g.assign(n * n, 0);
+    G.dpath.assign(n * n, 0);
+    for (int64_t i = 0; i < n; ++i)
+        for (int64_t j = 0; j < n; ++j)
+            if (i != j && adj[i * n + j]) G.at(i, j) = -1;
+    for (int64_t i = 0; i < n; ++i) G.adjust_dpath(i, i);  // GeneralGraph.__init__: reconstitute_dpath([])
+
+    // sepset membership: union over both sides of the removal depth, keyed by (min, max)
+    std::unordered_map<uint64_t, std::vector<uint64_t>> sep;
+    for (int64_t r = 0; r < count; ++r) {
+        const int64_t x = sep_xy[2 * r], y = sep_xy[2 * r + 1];
+        const uint64_t key = (uint64_t)std::min(x, y) * (uint64_t)n + (uint64_t)std::max(x, y);
+        auto &row = sep[key];
+        if (row.empty()) row.assign(W, 0);
+        for (int64_t w = 0; w < W; ++w) row[w] |= sep_bits[r * W + w];
+    }
+    auto in_sepset = [&](int64_t x, int64_t z, int64_t y) {
+        const uint64_t key = (uint64_t)std::min(x, z) * (uint64_t)n + (uint64_t)std::max(x, z);
+        auto it = sep.find(key);
+        if (it == sep.end()) return false;
+        return ((it->second[y >> 6] >> (y & 63)) & 1ull) != 0;
+    };
+
+    // ---- uc_sepset(priority = 2) on the skeleton (cg_new = deepcopy(cg))
+    {
+        const auto A = find_adj(G);
+        const auto UT = enumerate_triples(G, A, [&](int32_t i, int32_t, int32_t k) { return G.at(i, k) == 0; });
+        for (const Triple &t : UT) {
+            const int64_t x = t.i, y = t.j, z = t.k;
+            if (!(x < z)) continue;
+            if (in_sepset(x, z, y)) continue;
+            if (!G.is_fully_directed(y, x) && !G.is_fully_directed(y, z)) {
+                if (G.adjacent(x, y)) G.remove_edge(x, y);
+                G.add_directed(x, y);
+                if (G.adjacent(z, y)) G.remove_edge(z, y);
+                G.add_directed(z, y);
+            }
+        }
+    }
+    // ---- meek (lists computed once from cg_new = deepcopy(cg_2))
+    {
+        const auto A = find_adj(G);
+        const auto UT = enumerate_triples(G, A, [&](int32_t i, int32_t, int32_t k) { return G.at(i, k) == 0; });
+        // (i, k) in Adj  <=>  g[k, i] in {-1, 1}
+        const auto Tri = enumerate_triples(G, A, [&](int32_t i, int32_t, int32_t k) {
+            const int8_t v = G.at(k, i);
+            return v == -1 || v == 1;
+        });
+        // kites from permutations(Tri, 2)
+        std::vector<Kite> Kites;
+        {
+            std::unordered_map<uint64_t, std::vector<int32_t>> by_ik;
+            for (size_t b = 0; b < Tri.size(); ++b)
+                by_ik[(uint64_t)Tri[b].i * (uint64_t)n + (uint64_t)Tri[b].k].push_back((int32_t)b);
+            for (size_t a = 0; a < Tri.size(); ++a) {
+                const Triple &p0 = Tri[a];
+                auto it = by_ik.find((uint64_t)p0.i * (uint64_t)n + (uint64_t)p0.k);
+                for (int32_t b : it->second) {
+                    if ((size_t)b == a) continue;
+                    const Triple &p1 = Tri[b];
+                    if (p0.j < p1.j && G.at(p0.j, p1.j) == 0) Kites.push_back({p0.i, p0.j, p1.j, p0.k});
+                }
+            }
+        }
+        bool loop = true;
+        while (loop) {
+            loop = false;
+            for (const Triple &t : UT) {  // R1
+                const int64_t i = t.i, j = t.j, k = t.k;
+                if (G.is_fully_directed(i, j) && G.is_undirected(j, k)) {
+                    if (!G.adjacent(j, k)) continue;
+                    if (G.is_ancestor_of(k, j)) continue;
+                    G.remove_edge(j, k);
+                    G.add_directed(j, k);
+                    loop = true;
+                }
+            }
+            for (const Triple &t : Tri) {  // R2
+                const int64_t i = t.i, j = t.j, k = t.k;
+                if (G.is_fully_directed(i, j) && G.is_fully_directed(j, k) && G.is_undirected(i, k)) {
+                    if (!G.adjacent(i, k)) continue;
+                    if (G.is_ancestor_of(k, i)) continue;
+                    G.remove_edge(i, k);
+                    G.add_directed(i, k);
+                    loop = true;
+                }
+            }
+            for (const Kite &q : Kites) {  // R3
+                const int64_t i = q.i, j = q.j, k = q.k, l = q.l;
+                if (G.is_undirected(i, j) && G.is_undirected(i, k) && G.is_fully_directed(j, l) &&
+                    G.is_fully_directed(k, l) && G.is_undirected(i, l)) {
+                    if (!G.adjacent(i, l)) continue;
+                    if (G.is_ancestor_of(l, i)) continue;
+                    G.remove_edge(i, l);
+                    G.add_directed(i, l);
+                    loop = true;
+                }
+            }
+        }
+    }
+    for (int64_t i = 0; i < n * n; ++i) graph[i] = G.g[i];
+    return PCG_OK;
+}

@@ -1,0 +1,1047 @@
+// skeleton.hip — level-synchronous stable PC skeleton on MI355X (gfx950).
+//
+// Replaces causal-learn skeleton_discovery(stable=True) + FisherZ [U]; the loop it
+// restates is lib/causallearn/utils/PCUtils/SkeletonDiscovery.py:70-144 and the helpers
+// lib/causallearn/graph/GraphClass.py:78-106 (cache key, neighbors, max_degree).
+//
+// Device layout (HBM, all handle-owned except C and removed_level):
+//   C        n x n fp64 correlation (caller)           diag  n fp64 (C[i,i])
+//   adj      n x W u64 adjacency bitmask (W = ceil(n/64)); the level barrier state
+//   deg/off  n int32 degrees, n+1 int32 CSR offsets;   nbr   sum(deg) int32, ascending
+//   rm       n x n uint8 removal flags of the current depth (merged across ranks)
+//   ug       sum(deg) x W u64: per ordered adjacent pair (x -> y) the union of independent
+//            S seen from x's side (global node bits) — SkeletonDiscovery.py:129-130,135-136
+//   cpre     n+1 int64 chunk prefix: node x owns chunks [cpre[x], cpre[x+1])
+//
+// Work decomposition at depth d >= 1 ("x-side" order of the reference loop):
+//   a chunk = (node x, bs consecutive colex ranks of d-subsets S of adj(x)); one lane = one S.
+//   Each lane factors C_SS once (Cholesky in registers), u = L^-1 C_Sx, then sweeps every
+//   y in adj(x) \ S: v = L^-1 C_Sy, c_xx = 1-u.u, c_yy = C_yy - v.v, c_xy = C_xy - u.v, and
+//   r = c_xy / sqrt(c_xx c_yy) is the partial correlation (= -inv01/sqrt(inv00 inv11)).
+//   The block stages row C[y, adj(x)] + adj(y) in LDS (double-buffered, register prefetch),
+//   so every per-test operand comes from LDS; only the once-per-lane gathers hit L2/HBM.
+//   Dedup = the reference's memo: (x, y, S) is skipped on x's side when y < x and S is a
+//   subset of adj(y) — node y evaluates it and ORs the result into both sides' unions.
+//
+// Decision (default): p > alpha  <=>  r^2 < tanh(z_{1-a/2}/sqrt(N-d-3))^2; tests within a
+// relative 1e-6 band of the threshold, with a failed Cholesky, |r| ~ 1, NaN, or any other
+// edge case go to the exact path (LU like numpy.linalg.inv + the reference p expression).
+// PCG_FLAG_FULL_P computes the p-value of every test inline instead.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstring>
+
+#include "fisherz_dev.h"
+#include "handle.h"
+
+namespace {
+
+constexpr int MODE_DECIDE = 0;
+constexpr int MODE_FULLP = 1;
+constexpr int MODE_EXACT = 2;
+
+struct LevelArgs {
+    const double *C;
+    int64_t ldc;
+    const double *diag;
+    const uint64_t *adj;
+    int W;
+    int n;
+    int d;
+    int bs;                      // lanes (S ranks) per chunk
+    const int32_t *deg;
+    const int32_t *off;
+    const int32_t *nbr;
+    const int64_t *cpre;
+    const uint64_t *binom;
+    uint8_t *rm;
+    uint64_t *ug;
+    DevCounters *ctr;
+    DeferredEntry *deferred;
+    int64_t def_cap;
+    pcg_record *records;
+    int64_t rec_cap;
+    pcg_record *nearl;
+    int64_t near_cap;
+    double lo2, hi2, rmax2;      // decision band on r^2, |r| guard
+    double alpha, sqrt_dof;
+    int dof_negative;
+    int record;
+    int64_t chunk_lo;            // first chunk of this launch
+    int stage_cap;               // staged elements held in registers per thread
+};
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+__device__ __forceinline__ int find_in_sorted(const int32_t *a, int len, int v) {
+    int lo = 0, hi = len - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (a[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ void push_record(pcg_record *buf, int64_t cap, unsigned long long *ctr,
+                                            int a, int b, int d, const int *S, double p) {
+    const unsigned long long slot = atomicAdd(ctr, 1ull);
+    if ((int64_t)slot < cap) {
+        pcg_record &r = buf[slot];
+        r.a = a; r.b = b; r.d = d;
+        for (int i = 0; i < PCG_MAX_DEPTH; ++i) r.s[i] = i < d ? S[i] : -1;
+        r.p = p;
+    }
+}
+
+__device__ __forceinline__ void push_deferred(const LevelArgs &a, int x, int y, const int *S, int d) {
+    const unsigned long long slot = atomicAdd(&a.ctr->deferred, 1ull);
+    if ((int64_t)slot < a.def_cap) {
+        DeferredEntry &e = a.deferred[slot];
+        e.x = x; e.y = y;
+        for (int i = 0; i < PCG_MAX_DEPTH; ++i) e.s[i] = i < d ? S[i] : -1;
+    }
+}
+
+// 0 dependent, 1 independent, 2 exact path. p written in FULL_P mode.
+template <int MODE>
+__device__ __forceinline__ int decide(const LevelArgs &a, double cxy, double cxx, double cyy,
+                                      double *p) {
+    if (MODE == MODE_EXACT) return 2;
+    const double den = cxx * cyy;
+    if (!(den > 0.0)) return 2;
+    const double num = cxy * cxy;
+    if (MODE == MODE_DECIDE) {
+        if (num < a.lo2 * den) return 1;
+        if (num > a.hi2 * den && num < a.rmax2 * den) return 0;
+        return 2;
+    } else {
+        if (!(num < a.rmax2 * den)) return 2;
+        const double r = cxy / sqrt(den);
+        int err = 0;
+        const double pv = pcg_pvalue_from_r(r, a.sqrt_dof, &err);
+        if (err) return 2;
+        *p = pv;
+        return pv > a.alpha ? 1 : 0;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// utility kernels
+__global__ void k_init_adj(uint64_t *adj, int n, int W) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)n * W) return;
+    const int x = (int)(i / W), w = (int)(i % W);
+    const int base = w * 64;
+    const int rem = n - base;
+    uint64_t m = rem >= 64 ? ~0ull : ((1ull << rem) - 1ull);
+    if (x >= base && x < base + 64) m &= ~(1ull << (x - base));
+    adj[i] = m;
+}
+
+__global__ void k_diag(const double *C, int64_t ldc, int n, double *diag) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) diag[i] = C[(int64_t)i * ldc + i];
+}
+
+__global__ void k_degrees(const uint64_t *adj, int n, int W, int32_t *deg) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= n) return;
+    int c = 0;
+    for (int w = 0; w < W; ++w) c += __popcll(adj[(int64_t)x * W + w]);
+    deg[x] = c;
+}
+
+// one wave per node: ascending neighbour list from the bitmask (wave prefix scan)
+__global__ void k_fill_nbr(const uint64_t *adj, int n, int W, const int32_t *off, int32_t *nbr) {
+    const int x = blockIdx.x;
+    const int lane = threadIdx.x;
+    int base = off[x];
+    for (int w0 = 0; w0 < W; w0 += 64) {
+        const int w = w0 + lane;
+        uint64_t v = w < W ? adj[(int64_t)x * W + w] : 0ull;
+        const int c = __popcll(v);
+        int incl = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(incl, o);
+            if (lane >= o) incl += t;
+        }
+        const int tot = __shfl(incl, 63);
+        int pos = base + incl - c;
+        while (v) {
+            const int b = __ffsll((long long)v) - 1;
+            nbr[pos++] = w * 64 + b;
+            v &= v - 1;
+        }
+        base += tot;
+    }
+}
+
+// rm -> adjacency bitmask + removed_level (the level barrier, SkeletonDiscovery.py:141-144)
+__global__ void k_apply(const uint8_t *rm, uint64_t *adj, int8_t *rl, int n, int W, int d) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)n * W) return;
+    const int x = (int)(i / W), w = (int)(i % W);
+    uint64_t m = 0;
+    const int yend = min(n, w * 64 + 64);
+    for (int y = w * 64; y < yend; ++y)
+        if (rm[(int64_t)x * n + y]) {
+            m |= 1ull << (y - w * 64);
+            rl[(int64_t)x * n + y] = (int8_t)d;
+        }
+    if (m) adj[i] &= ~m;
+}
+
+// export non-empty union rows of removed ordered pairs
+__global__ void k_export(const int32_t *off, const int32_t *nbr, const uint8_t *rm,
+                         const uint64_t *ug, int n, int W, int64_t sumdeg, int32_t *xy,
+                         uint64_t *bits, int64_t cap, unsigned long long *ctr) {
+    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot >= sumdeg) return;
+    int lo = 0, hi = n;  // off[lo] <= slot < off[hi]
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (off[mid] <= slot) lo = mid; else hi = mid;
+    }
+    const int x = lo, y = nbr[slot];
+    if (!rm[(int64_t)x * n + y]) return;
+    const uint64_t *row = ug + slot * W;
+    uint64_t any = 0;
+    for (int w = 0; w < W; ++w) any |= row[w];
+    if (!any) return;
+    const unsigned long long r = atomicAdd(ctr, 1ull);
+    if ((int64_t)r >= cap) return;
+    xy[2 * r] = x;
+    xy[2 * r + 1] = y;
+    for (int w = 0; w < W; ++w) bits[(int64_t)r * W + w] = row[w];
+}
+
+// ---------------------------------------------------------------------------------------
+// depth 0: one chunk = one row x; tests (x, y) for y > x.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_level0(LevelArgs a) {
+    const int x = (int)(a.chunk_lo + blockIdx.x);
+    const double cxx = a.diag[x];
+    unsigned long long tests = 0, indep = 0;
+    const int S0[1] = {0};
+    for (int y = x + 1 + threadIdx.x; y < a.n; y += blockDim.x) {
+        const double cxy = a.C[(int64_t)x * a.ldc + y];
+        const double cyy = a.diag[y];
+        double p = 0.0;
+        const int dec = decide<MODE>(a, cxy, cxx, cyy, &p);
+        ++tests;
+        if (dec == 2) {
+            push_deferred(a, x, y, S0, 0);
+            continue;
+        }
+        if (MODE == MODE_FULLP) {
+            if (a.record) push_record(a.records, a.rec_cap, &a.ctr->records, x, y, 0, S0, p);
+            if (fabs(p - a.alpha) < 1e-9) push_record(a.nearl, a.near_cap, &a.ctr->near_alpha, x, y, 0, S0, p);
+        }
+        if (dec == 1) {
+            ++indep;
+            a.rm[(int64_t)x * a.n + y] = 1;
+            a.rm[(int64_t)y * a.n + x] = 1;
+        }
+    }
+    tests = wave_sum(tests);
+    indep = wave_sum(indep);
+    if ((threadIdx.x & 63) == 0) {
+        if (tests) atomicAdd(&a.ctr->tests, tests);
+        if (indep) atomicAdd(&a.ctr->indep, indep);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// depth d >= 1. DM = compile-time upper bound of d (exact for DM <= 4).
+template <int DM, int MODE>
+__global__ __launch_bounds__(256) void k_level(LevelArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int bs = blockDim.x;
+    const int64_t chunk = a.chunk_lo + blockIdx.x;
+
+    // node owning this chunk
+    int lo = 0, hi = a.n;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (a.cpre[mid] <= chunk) lo = mid; else hi = mid;
+    }
+    const int x = lo;
+    const int D = a.deg[x];
+    const int d = DM <= 4 ? DM : a.d;
+    const int W = a.W;
+    const int E = D + W + 2;                      // staged u64 per y: row, adj(y), Cxy, Cyy
+    const int32_t *nxg = a.nbr + a.off[x];
+
+    // LDS carve: nxs[D] int32 (padded to 8B) | sbuf[2][E] u64 | scratch[nwaves][2][W] u64
+    int32_t *nxs = reinterpret_cast<int32_t *>(smem);
+    uint64_t *sbuf = reinterpret_cast<uint64_t *>(smem + (((size_t)D * 4 + 15) & ~(size_t)15));
+    uint64_t *scr = sbuf + 2 * (size_t)E;
+    uint64_t *sc_self = scr + (size_t)wave * 2 * W;
+    uint64_t *sc_prop = sc_self + W;
+
+    for (int i = tid; i < D; i += bs) nxs[i] = nxg[i];
+    for (int i = lane; i < 2 * W; i += 64) sc_self[i] = 0;
+
+    const uint64_t nS = pcg_binom(a.binom, D, d);
+    const uint64_t rank = (uint64_t)(chunk - a.cpre[x]) * (uint64_t)bs + (uint64_t)tid;
+    const bool active = rank < nS;
+
+    int k[DM];      // local indices of S in adj(x), ascending
+    int sg[DM];     // global ids
+#pragma unroll
+    for (int i = 0; i < DM; ++i) { k[i] = -1; sg[i] = 0; }
+    if (active) pcg_unrank_colex<DM>(rank, d, D, a.binom, k);
+    __syncthreads();  // nxs ready
+#pragma unroll
+    for (int i = 0; i < DM; ++i)
+        if (i < d && active) sg[i] = nxs[k[i]];
+
+    // Cholesky of C_SS (lower, packed by row), u = L^-1 C_Sx, c_xx = C_xx - u.u
+    double L[DM][DM];
+    double rinv[DM];
+    double u[DM];
+    bool chol_ok = active;
+    double cxx = 0.0;
+    if (active) {
+#pragma unroll
+        for (int j = 0; j < DM; ++j) {
+            if (j < d) {
+                const double *Cj = a.C + (int64_t)sg[j] * a.ldc;
+                double s = a.diag[sg[j]];
+#pragma unroll
+                for (int q = 0; q < DM; ++q)
+                    if (q < j) s -= L[j][q] * L[j][q];
+                chol_ok = chol_ok && (s > 0.0);
+                const double ljj = sqrt(s);
+                rinv[j] = 1.0 / ljj;
+                L[j][j] = ljj;
+#pragma unroll
+                for (int i = 0; i < DM; ++i) {
+                    if (i > j && i < d) {
+                        double t = Cj[sg[i]];
+#pragma unroll
+                        for (int q = 0; q < DM; ++q)
+                            if (q < j) t -= L[i][q] * L[j][q];
+                        L[i][j] = t * rinv[j];
+                    }
+                }
+            }
+        }
+        const double *Cx = a.C + (int64_t)x * a.ldc;
+        double uu = 0.0;
+#pragma unroll
+        for (int i = 0; i < DM; ++i) {
+            if (i < d) {
+                double t = Cx[sg[i]];
+#pragma unroll
+                for (int q = 0; q < DM; ++q)
+                    if (q < i) t -= L[i][q] * u[q];
+                u[i] = t * rinv[i];
+                uu += u[i] * u[i];
+            }
+        }
+        cxx = a.diag[x] - uu;
+        chol_ok = chol_ok && (cxx == cxx);
+    }
+
+    unsigned long long tests = 0, indep = 0;
+    const int nstage = (E + bs - 1) / bs;          // staged elements per thread
+    constexpr int PF = 8;                          // held in registers (rest: direct)
+
+    auto stage_val = [&](int e, int yg) -> uint64_t {
+        if (e < D) return (uint64_t)__double_as_longlong(a.C[(int64_t)yg * a.ldc + nxs[e]]);
+        e -= D;
+        if (e < W) return a.adj[(int64_t)yg * W + e];
+        e -= W;
+        if (e == 0) return (uint64_t)__double_as_longlong(a.C[(int64_t)x * a.ldc + yg]);
+        return (uint64_t)__double_as_longlong(a.diag[yg]);
+    };
+
+    // prologue: stage y = nxs[0] into buffer 0
+    if (D > 0) {
+        const int yg0 = nxs[0];
+        for (int e = tid; e < E; e += bs) sbuf[e] = stage_val(e, yg0);
+    }
+    __syncthreads();
+
+    for (int t = 0; t < D; ++t) {
+        const uint64_t *cur = sbuf + (size_t)(t & 1) * E;
+        uint64_t *nxt = sbuf + (size_t)((t + 1) & 1) * E;
+        const bool more = t + 1 < D;
+        const int ygn = more ? nxs[t + 1] : 0;
+        uint64_t pf[PF];
+        if (more) {
+#pragma unroll
+            for (int j = 0; j < PF; ++j) {
+                const int e = tid + j * bs;
+                if (j < nstage && e < E) pf[j] = stage_val(e, ygn);
+            }
+        }
+        const int yg = nxs[t];
+        bool is_indep = false, prop = false;
+        if (active) {
+            bool skip = !active;
+#pragma unroll
+            for (int i = 0; i < DM; ++i)
+                if (i < d) skip = skip || (k[i] == t);
+            bool in_y = true;
+            if (!skip) {
+#pragma unroll
+                for (int i = 0; i < DM; ++i)
+                    if (i < d) in_y = in_y && ((cur[D + (sg[i] >> 6)] >> (sg[i] & 63)) & 1ull);
+                if (yg < x && in_y) skip = true;     // owned by node y (memo)
+            }
+            if (!skip) {
+                ++tests;
+                int dec = 2;
+                double p = 0.0;
+                if (chol_ok) {
+                    double vv = 0.0, uv = 0.0, v[DM];
+#pragma unroll
+                    for (int i = 0; i < DM; ++i) {
+                        if (i < d) {
+                            double tt = __longlong_as_double((long long)cur[k[i]]);
+#pragma unroll
+                            for (int q = 0; q < DM; ++q)
+                                if (q < i) tt -= L[i][q] * v[q];
+                            v[i] = tt * rinv[i];
+                            vv += v[i] * v[i];
+                            uv += u[i] * v[i];
+                        }
+                    }
+                    const double cxy = __longlong_as_double((long long)cur[D + W]) - uv;
+                    const double cyy = __longlong_as_double((long long)cur[D + W + 1]) - vv;
+                    dec = decide<MODE>(a, cxy, cxx, cyy, &p);
+                }
+                if (dec == 2) {
+                    push_deferred(a, x, yg, sg, d);
+                } else {
+                    if (MODE == MODE_FULLP) {
+                        const int lo_ = x < yg ? x : yg, hi_ = x < yg ? yg : x;
+                        if (a.record) push_record(a.records, a.rec_cap, &a.ctr->records, lo_, hi_, d, sg, p);
+                        if (fabs(p - a.alpha) < 1e-9)
+                            push_record(a.nearl, a.near_cap, &a.ctr->near_alpha, lo_, hi_, d, sg, p);
+                    }
+                    if (dec == 1) {
+                        is_indep = true;
+                        prop = in_y && (yg > x);
+                        ++indep;
+                    }
+                }
+            }
+        }
+        // sepset unions + removal flags (wave-uniform branch)
+        const unsigned long long bal = __ballot(is_indep);
+        if (bal) {
+            if (lane == __ffsll((long long)bal) - 1) {
+                a.rm[(int64_t)x * a.n + yg] = 1;
+                a.rm[(int64_t)yg * a.n + x] = 1;
+            }
+            if (is_indep) {
+#pragma unroll
+                for (int i = 0; i < DM; ++i)
+                    if (i < d) {
+                        atomicOr(&sc_self[sg[i] >> 6], 1ull << (sg[i] & 63));
+                        if (prop) atomicOr(&sc_prop[sg[i] >> 6], 1ull << (sg[i] & 63));
+                    }
+            }
+            const unsigned long long balp = __ballot(prop);
+            wave_sync();
+            uint64_t *row = a.ug + ((int64_t)a.off[x] + t) * W;
+            for (int w = lane; w < W; w += 64) {
+                const uint64_t vsw = sc_self[w];
+                if (vsw) { atomicOr(reinterpret_cast<unsigned long long *>(&row[w]), vsw); sc_self[w] = 0; }
+            }
+            if (balp) {
+                const int slot = a.off[yg] + find_in_sorted(a.nbr + a.off[yg], a.deg[yg], x);
+                uint64_t *rowy = a.ug + (int64_t)slot * W;
+                for (int w = lane; w < W; w += 64) {
+                    const uint64_t vpw = sc_prop[w];
+                    if (vpw) { atomicOr(reinterpret_cast<unsigned long long *>(&rowy[w]), vpw); sc_prop[w] = 0; }
+                }
+            }
+            wave_sync();
+        }
+        if (more) {
+#pragma unroll
+            for (int j = 0; j < PF; ++j) {
+                const int e = tid + j * bs;
+                if (j < nstage && e < E) nxt[e] = pf[j];
+            }
+            for (int e = tid + PF * bs; e < E; e += bs) nxt[e] = stage_val(e, ygn);
+        }
+        __syncthreads();
+    }
+
+    tests = wave_sum(tests);
+    indep = wave_sum(indep);
+    if (lane == 0) {
+        if (tests) atomicAdd(&a.ctr->tests, tests);
+        if (indep) atomicAdd(&a.ctr->indep, indep);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// exact path over the deferred list (LU like numpy.linalg.inv; the reference p expression)
+__global__ void k_exact(LevelArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int d = a.d;
+    const int m = d + 2;
+    const int per = m * m + 2 * m;
+    double *A = reinterpret_cast<double *>(smem) + (size_t)threadIdx.x * per;
+    double *B0 = A + m * m;
+    double *B1 = B0 + m;
+    int piv[PCG_MAX_DEPTH + 2];
+    const int64_t count = (int64_t)min((unsigned long long)a.def_cap, a.ctr->deferred);
+    unsigned long long nexact = 0, nindep = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const DeferredEntry e = a.deferred[i];
+        const int x = e.x, y = e.y;
+        const int lo_ = x < y ? x : y, hi_ = x < y ? y : x;
+        int var[PCG_MAX_DEPTH + 2];
+        var[0] = lo_; var[1] = hi_;
+        for (int q = 0; q < d; ++q) var[2 + q] = e.s[q];
+        for (int r = 0; r < m; ++r)
+            for (int c = 0; c < m; ++c) A[r * m + c] = a.C[(int64_t)var[r] * a.ldc + var[c]];
+        double i00, i01, i11, p = __builtin_nan("");
+        int err = 0;
+        if (pcg_lu_inv01(A, m, piv, B0, B1, &i00, &i01, &i11)) {
+            err = 1;
+        } else {
+            const double prod = i00 * i11;
+            if (prod < 0.0) err = 2;
+            else if (a.dof_negative) err = 2;
+            else {
+                const double r = -i01 / sqrt(prod);
+                p = pcg_pvalue_from_r(r, a.sqrt_dof, &err);
+            }
+        }
+        ++nexact;
+        if (err) { atomicOr(&a.ctr->error, (unsigned long long)err); continue; }
+        if (a.record) push_record(a.records, a.rec_cap, &a.ctr->records, lo_, hi_, d, e.s, p);
+        if (fabs(p - a.alpha) < 1e-9) push_record(a.nearl, a.near_cap, &a.ctr->near_alpha, lo_, hi_, d, e.s, p);
+        if (p > a.alpha) {
+            ++nindep;
+            a.rm[(int64_t)x * a.n + y] = 1;
+            a.rm[(int64_t)y * a.n + x] = 1;
+            if (d > 0) {
+                bool in_y = true;
+                for (int q = 0; q < d; ++q)
+                    in_y = in_y && ((a.adj[(int64_t)y * a.W + (e.s[q] >> 6)] >> (e.s[q] & 63)) & 1ull);
+                const int sx = a.off[x] + find_in_sorted(a.nbr + a.off[x], a.deg[x], y);
+                for (int q = 0; q < d; ++q)
+                    atomicOr(reinterpret_cast<unsigned long long *>(&a.ug[(int64_t)sx * a.W + (e.s[q] >> 6)]),
+                             1ull << (e.s[q] & 63));
+                if (in_y && y > x) {
+                    const int sy = a.off[y] + find_in_sorted(a.nbr + a.off[y], a.deg[y], x);
+                    for (int q = 0; q < d; ++q)
+                        atomicOr(reinterpret_cast<unsigned long long *>(&a.ug[(int64_t)sy * a.W + (e.s[q] >> 6)]),
+                                 1ull << (e.s[q] & 63));
+                }
+            }
+        }
+    }
+    if (nexact) atomicAdd(&a.ctr->exact, nexact);
+    if (nindep) atomicAdd(&a.ctr->indep, nindep);
+}
+
+// ---------------------------------------------------------------------------------------
+// host helpers
+uint64_t sat_add(uint64_t a, uint64_t b) { return (a > UINT64_MAX - b) ? UINT64_MAX : a + b; }
+
+void build_binom(pcg_handle *h, int n) {
+    h->binom_h.assign((size_t)(n + 1) * PCG_BK, 0);
+    for (int c = 0; c <= n; ++c) {
+        h->binom_h[(size_t)c * PCG_BK] = 1;
+        for (int k = 1; k < PCG_BK; ++k)
+            h->binom_h[(size_t)c * PCG_BK + k] =
+                c == 0 ? 0 : sat_add(h->binom_h[(size_t)(c - 1) * PCG_BK + k - 1],
+                                     h->binom_h[(size_t)(c - 1) * PCG_BK + k]);
+    }
+}
+
+uint64_t hbinom(const pcg_handle *h, int c, int k) {
+    if (c < k || c < 0) return 0;
+    return h->binom_h[(size_t)c * PCG_BK + k];
+}
+
+double threshold_r2(double alpha, double N, int d) {
+    // X_alpha = Phi^-1(1 - alpha/2) via Newton on the complementary error function
+    double target = alpha;                        // p(X) = erfc(X/sqrt2) == alpha
+    double X = 1.96;
+    for (int it = 0; it < 100; ++it) {
+        const double f = std::erfc(X * PCG_SQRT1_2) - target;
+        const double df = -std::sqrt(2.0 / M_PI) * std::exp(-0.5 * X * X);
+        const double step = f / df;
+        X -= step;
+        if (std::fabs(step) < 1e-15 * std::fabs(X)) break;
+    }
+    const double dof = N - d - 3;
+    const double r = std::tanh(X / std::sqrt(dof));
+    return r * r;
+}
+
+LevelArgs make_args(pcg_handle *h, int d, int mode_exact_all) {
+    LevelArgs a{};
+    a.C = h->C;
+    a.ldc = h->ldc;
+    a.diag = (const double *)h->diag.p;
+    a.adj = (const uint64_t *)h->adj.p;
+    a.W = h->W;
+    a.n = (int)h->n;
+    a.d = d;
+    a.bs = h->chunk;
+    a.deg = (const int32_t *)h->deg.p;
+    a.off = (const int32_t *)h->off.p;
+    a.nbr = (const int32_t *)h->nbr.p;
+    a.cpre = (const int64_t *)h->cpre.p;
+    a.binom = (const uint64_t *)h->binom.p;
+    a.rm = (uint8_t *)h->rm.p;
+    a.ug = (uint64_t *)h->ug.p;
+    a.ctr = (DevCounters *)h->ctr.p;
+    a.deferred = (DeferredEntry *)h->deferred.p;
+    a.def_cap = h->def_cap;
+    a.records = (pcg_record *)h->records.p;
+    a.rec_cap = h->rec_cap;
+    a.nearl = (pcg_record *)h->nearbuf.p;
+    a.near_cap = h->near_cap;
+    a.alpha = h->alpha;
+    const double dof = (double)h->N - d - 3;
+    a.dof_negative = dof < 0;
+    a.sqrt_dof = dof >= 0 ? std::sqrt(dof) : 0.0;
+    if (dof > 0) {
+        const double r2 = threshold_r2(h->alpha, (double)h->N, d);
+        a.lo2 = r2 * (1.0 - 1e-6);
+        a.hi2 = r2 * (1.0 + 1e-6);
+    } else {
+        a.lo2 = -1.0;  // never decides: every test to the exact path
+        a.hi2 = 1e300;
+    }
+    a.rmax2 = 1.0 - 2e-9;
+    a.record = (h->flags & PCG_FLAG_RECORD) ? 1 : 0;
+    (void)mode_exact_all;
+    return a;
+}
+
+template <int MODE>
+void launch_level_mode(pcg_handle *h, const LevelArgs &a, int64_t nchunks, size_t lds) {
+    const dim3 grid((unsigned)nchunks), block((unsigned)a.bs);
+    const int d = a.d;
+    if (d == 1) hipLaunchKernelGGL((k_level<1, MODE>), grid, block, lds, h->stream, a);
+    else if (d == 2) hipLaunchKernelGGL((k_level<2, MODE>), grid, block, lds, h->stream, a);
+    else if (d == 3) hipLaunchKernelGGL((k_level<3, MODE>), grid, block, lds, h->stream, a);
+    else if (d == 4) hipLaunchKernelGGL((k_level<4, MODE>), grid, block, lds, h->stream, a);
+    else if (d <= 6) hipLaunchKernelGGL((k_level<6, MODE>), grid, block, lds, h->stream, a);
+    else if (d <= 8) hipLaunchKernelGGL((k_level<8, MODE>), grid, block, lds, h->stream, a);
+    else hipLaunchKernelGGL((k_level<12, MODE>), grid, block, lds, h->stream, a);
+}
+
+int mode_of(const pcg_handle *h, int d) {
+    if ((h->flags & PCG_FLAG_EXACT_ALL) || (double)h->N - d - 3 <= 0) return MODE_EXACT;
+    if (h->flags & (PCG_FLAG_FULL_P | PCG_FLAG_RECORD)) return MODE_FULLP;
+    return MODE_DECIDE;
+}
+
+// degrees + CSR neighbour lists from the current adjacency; degrees copied to the host
+int refresh_graph(pcg_handle *h) {
+    const int n = (int)h->n, W = h->W;
+    hipLaunchKernelGGL(k_degrees, dim3((n + 255) / 256), dim3(256), 0, h->stream,
+                       (const uint64_t *)h->adj.p, n, W, (int32_t *)h->deg.p);
+    h->deg_h.resize(n);
+    PCG_HIP(h, hipMemcpyAsync(h->deg_h.data(), h->deg.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost,
+                              h->stream));
+    PCG_HIP(h, hipStreamSynchronize(h->stream));
+    std::vector<int32_t> off(n + 1, 0);
+    int64_t s = 0;
+    int32_t mx = 0;
+    for (int i = 0; i < n; ++i) {
+        off[i] = (int32_t)s;
+        s += h->deg_h[i];
+        mx = std::max(mx, h->deg_h[i]);
+    }
+    off[n] = (int32_t)s;
+    h->sumdeg = s;
+    h->maxdeg = mx;
+    if (!pcg_ensure(h, h->off, sizeof(int32_t) * (n + 1))) return PCG_ERR_OOM;
+    if (!pcg_ensure(h, h->nbr, sizeof(int32_t) * std::max<int64_t>(s, 1))) return PCG_ERR_OOM;
+    PCG_HIP(h, hipMemcpyAsync(h->off.p, off.data(), sizeof(int32_t) * (n + 1), hipMemcpyHostToDevice,
+                              h->stream));
+    hipLaunchKernelGGL(k_fill_nbr, dim3(n), dim3(64), 0, h->stream, (const uint64_t *)h->adj.p, n, W,
+                       (const int32_t *)h->off.p, (int32_t *)h->nbr.p);
+    PCG_HIP(h, hipGetLastError());
+    return PCG_OK;
+}
+
+size_t level_lds(const pcg_handle *h, int bs) {
+    const size_t D = (size_t)h->maxdeg, W = (size_t)h->W;
+    const size_t E = D + W + 2;
+    return ((D * 4 + 15) & ~(size_t)15) + 2 * E * 8 + (size_t)(bs / 64) * 2 * W * 8;
+}
+
+}  // namespace
+
+// ======================================================================================
+// C ABI
+extern "C" int pcg_skeleton_init(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N,
+                                 double alpha, int flags, int8_t *removed_level) {
+    if (!h || !C || !removed_level || n < 2 || ldc < n || !(alpha > 0 && alpha < 1))
+        return pcg_fail(h, PCG_ERR_INVALID, "pcg_skeleton_init: invalid arguments (n=%lld)", (long long)n);
+    if (n > INT32_MAX / 2) return pcg_fail(h, PCG_ERR_INVALID, "n too large");
+    PCG_HIP(h, hipSetDevice(h->device));
+    h->C = C; h->n = n; h->ldc = ldc; h->N = N; h->alpha = alpha; h->flags = flags;
+    h->rl = removed_level;
+    h->W = (int)((n + 63) / 64);
+    h->depth = -1;
+    h->deg_levels.clear();
+    h->export_rows = 0;
+    h->rec_h.clear(); h->near_h.clear();
+    h->rec_total = h->near_total = 0;
+    memset(&h->st, 0, sizeof(h->st));
+    const int W = h->W;
+    if (!pcg_ensure(h, h->adj, sizeof(uint64_t) * n * W) || !pcg_ensure(h, h->deg, sizeof(int32_t) * n) ||
+        !pcg_ensure(h, h->diag, sizeof(double) * n) || !pcg_ensure(h, h->rm, (size_t)n * n) ||
+        !pcg_ensure(h, h->ctr, sizeof(DevCounters)) ||
+        !pcg_ensure(h, h->deferred, sizeof(DeferredEntry) * h->def_cap) ||
+        !pcg_ensure(h, h->nearbuf, sizeof(pcg_record) * h->near_cap) ||
+        !pcg_ensure(h, h->records, sizeof(pcg_record) * std::max<int64_t>(h->rec_cap, 1)))
+        return pcg_fail(h, PCG_ERR_OOM, "device allocation failed (n=%lld)", (long long)n);
+    if (h->binom_n != (int)n) {
+        build_binom(h, (int)n);
+        if (!pcg_ensure(h, h->binom, sizeof(uint64_t) * h->binom_h.size())) return PCG_ERR_OOM;
+        PCG_HIP(h, hipMemcpyAsync(h->binom.p, h->binom_h.data(), sizeof(uint64_t) * h->binom_h.size(),
+                                  hipMemcpyHostToDevice, h->stream));
+        h->binom_n = (int)n;
+    }
+    const int64_t nw = n * W;
+    hipLaunchKernelGGL(k_init_adj, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, h->stream,
+                       (uint64_t *)h->adj.p, (int)n, W);
+    hipLaunchKernelGGL(k_diag, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream, C, ldc, (int)n,
+                       (double *)h->diag.p);
+    PCG_HIP(h, hipMemsetAsync(removed_level, 0xFF, (size_t)n * n, h->stream));
+    PCG_HIP(h, hipGetLastError());
+    return refresh_graph(h);
+}
+
+extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, int32_t *max_degree,
+                               uint8_t **rm_dev) {
+    if (!h || depth != h->depth + 1) return pcg_fail(h, PCG_ERR_INVALID, "pcg_level_begin: depth order");
+    if (max_degree) *max_degree = h->maxdeg;
+    if (rm_dev) *rm_dev = (uint8_t *)h->rm.p;
+    // reference loop condition: while max_degree() - 1 > depth_prev
+    if (!(h->maxdeg - 1 > depth - 1)) {
+        if (total_chunks) *total_chunks = 0;
+        return 1;  // done
+    }
+    if (depth >= PCG_MAX_LEVELS || depth > PCG_MAX_DEPTH)
+        return pcg_fail(h, PCG_ERR_INVALID, "conditioning depth %d exceeds PCG_MAX_DEPTH=%d", depth,
+                        PCG_MAX_DEPTH);
+    h->depth = depth;
+    const int n = (int)h->n;
+    h->deg_levels.insert(h->deg_levels.end(), h->deg_h.begin(), h->deg_h.end());
+    h->st.max_degree[depth] = h->maxdeg;
+    h->st.levels = depth + 1;
+    // calls-equivalent: sum_x D_x * C(D_x - 1, d) (ci_test invocations incl. cache hits)
+    int64_t calls = 0;
+    for (int x = 0; x < n; ++x) {
+        const int D = h->deg_h[x];
+        if (D < depth - 1) continue;
+        const uint64_t c = hbinom(h, D - 1, depth);
+        calls += (int64_t)std::min<uint64_t>(c, (uint64_t)INT64_MAX / 4096) * D;
+    }
+    h->st.calls[depth] = calls;
+    // work decomposition
+    h->cpre_h.assign(n + 1, 0);
+    h->work_h.assign(n, 0);
+    if (depth == 0) {
+        h->chunk = 256;
+        for (int x = 0; x <= n; ++x) h->cpre_h[x] = x;
+        for (int x = 0; x < n; ++x) h->work_h[x] = n - 1 - x;
+    } else {
+        // one block per node when C(D, d) is small; 256-rank chunks otherwise
+        double mean_s = 0.0;
+        int cnt = 0;
+        for (int x = 0; x < n; ++x) {
+            const int D = h->deg_h[x];
+            if (D >= depth + 1) { mean_s += (double)hbinom(h, D, depth); ++cnt; }
+        }
+        mean_s = cnt ? mean_s / cnt : 0.0;
+        h->chunk = mean_s <= 64 ? 64 : (mean_s <= 128 ? 128 : 256);
+        int64_t s = 0;
+        for (int x = 0; x < n; ++x) {
+            h->cpre_h[x] = s;
+            const int D = h->deg_h[x];
+            if (D >= depth + 1) {
+                const uint64_t ns = hbinom(h, D, depth);
+                if (ns > ((uint64_t)1 << 46))
+                    return pcg_fail(h, PCG_ERR_INVALID, "depth %d work too large at node %d (deg %d)", depth, x, D);
+                s += (int64_t)((ns + h->chunk - 1) / h->chunk);
+                h->work_h[x] = (int64_t)ns * (D - depth);
+            }
+        }
+        h->cpre_h[n] = s;
+    }
+    h->total_chunks = h->cpre_h[n];
+    if (total_chunks) *total_chunks = h->total_chunks;
+    if (!pcg_ensure(h, h->cpre, sizeof(int64_t) * (n + 1))) return PCG_ERR_OOM;
+    PCG_HIP(h, hipMemcpyAsync(h->cpre.p, h->cpre_h.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice,
+                              h->stream));
+    PCG_HIP(h, hipMemsetAsync(h->rm.p, 0, (size_t)n * n, h->stream));
+    PCG_HIP(h, hipMemsetAsync(h->ctr.p, 0, sizeof(DevCounters), h->stream));
+    if (depth >= 1) {
+        const size_t ugb = sizeof(uint64_t) * (size_t)std::max<int64_t>(h->sumdeg, 1) * h->W;
+        if (!pcg_ensure(h, h->ug, ugb)) return pcg_fail(h, PCG_ERR_OOM, "sepset union rows (%zu B)", ugb);
+        PCG_HIP(h, hipMemsetAsync(h->ug.p, 0, ugb, h->stream));
+        if (h->export_cap == 0) {  // every ordered pair is removed at most once
+            h->export_cap = std::max<int64_t>(h->sumdeg, 1);
+            if (!pcg_ensure(h, h->exportbuf, sizeof(uint64_t) * h->export_cap * h->W) ||
+                !pcg_ensure(h, h->export_xy, sizeof(int32_t) * 2 * h->export_cap))
+                return pcg_fail(h, PCG_ERR_OOM, "sepset export buffer");
+        } else if (h->export_rows + h->sumdeg > h->export_cap) {
+            // grow, preserving exported rows
+            const int64_t ncap = h->export_rows + h->sumdeg;
+            DevBuf nb, nx;
+            if (hipMalloc(&nb.p, sizeof(uint64_t) * ncap * h->W) != hipSuccess ||
+                hipMalloc(&nx.p, sizeof(int32_t) * 2 * ncap) != hipSuccess)
+                return pcg_fail(h, PCG_ERR_OOM, "sepset export buffer growth");
+            PCG_HIP(h, hipMemcpyAsync(nb.p, h->exportbuf.p, sizeof(uint64_t) * h->export_rows * h->W,
+                                      hipMemcpyDeviceToDevice, h->stream));
+            PCG_HIP(h, hipMemcpyAsync(nx.p, h->export_xy.p, sizeof(int32_t) * 2 * h->export_rows,
+                                      hipMemcpyDeviceToDevice, h->stream));
+            PCG_HIP(h, hipStreamSynchronize(h->stream));
+            hipFree(h->exportbuf.p);
+            hipFree(h->export_xy.p);
+            h->exportbuf = {nb.p, sizeof(uint64_t) * ncap * h->W};
+            h->export_xy = {nx.p, sizeof(int32_t) * 2 * ncap};
+            h->export_cap = ncap;
+        }
+    }
+    return PCG_OK;
+}
+
+extern "C" int pcg_level_chunk_work(pcg_handle *h, int64_t *prefix_host, int64_t capacity) {
+    if (!h || !prefix_host || capacity < h->total_chunks + 1)
+        return pcg_fail(h, PCG_ERR_INVALID, "pcg_level_chunk_work: capacity");
+    const int n = (int)h->n;
+    int64_t acc = 0;
+    prefix_host[0] = 0;
+    for (int x = 0; x < n; ++x) {
+        const int64_t c0 = h->cpre_h[x], c1 = h->cpre_h[x + 1];
+        if (c1 == c0) continue;
+        if (h->depth == 0) {
+            acc += h->work_h[x];
+            prefix_host[c0 + 1] = acc;
+            continue;
+        }
+        const int D = h->deg_h[x];
+        const uint64_t ns = hbinom(h, D, h->depth);
+        for (int64_t c = c0; c < c1; ++c) {
+            const uint64_t r0 = (uint64_t)(c - c0) * h->chunk;
+            const uint64_t r1 = std::min<uint64_t>(r0 + h->chunk, ns);
+            acc += (int64_t)(r1 - r0) * (D - h->depth) + 1;
+            prefix_host[c + 1] = acc;
+        }
+    }
+    return PCG_OK;
+}
+
+extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) {
+    if (!h || chunk_lo < 0 || chunk_hi > h->total_chunks || chunk_lo > chunk_hi)
+        return pcg_fail(h, PCG_ERR_INVALID, "pcg_level_run: chunk range");
+    const int d = h->depth;
+    const int mode = mode_of(h, d);
+    for (int attempt = 0; attempt < 8; ++attempt) {
+        LevelArgs a = make_args(h, d, mode == MODE_EXACT);
+        a.chunk_lo = chunk_lo;
+        const int64_t nch = chunk_hi - chunk_lo;
+        PCG_HIP(h, hipEventRecord(h->ev[2], h->stream));
+        if (nch > 0) {
+            if (d == 0) {
+                const dim3 grid((unsigned)nch), block(256);
+                if (mode == MODE_DECIDE) hipLaunchKernelGGL(k_level0<MODE_DECIDE>, grid, block, 0, h->stream, a);
+                else if (mode == MODE_FULLP) hipLaunchKernelGGL(k_level0<MODE_FULLP>, grid, block, 0, h->stream, a);
+                else hipLaunchKernelGGL(k_level0<MODE_EXACT>, grid, block, 0, h->stream, a);
+            } else {
+                const size_t lds = level_lds(h, a.bs);
+                if (lds > 160 * 1024)
+                    return pcg_fail(h, PCG_ERR_INVALID, "max degree %d too large for LDS staging", h->maxdeg);
+                if (mode == MODE_DECIDE) launch_level_mode<MODE_DECIDE>(h, a, nch, lds);
+                else if (mode == MODE_FULLP) launch_level_mode<MODE_FULLP>(h, a, nch, lds);
+                else launch_level_mode<MODE_EXACT>(h, a, nch, lds);
+            }
+        }
+        PCG_HIP(h, hipGetLastError());
+        PCG_HIP(h, hipEventRecord(h->ev[3], h->stream));
+        DevCounters c{};
+        PCG_HIP(h, hipMemcpyAsync(&c, h->ctr.p, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+        PCG_HIP(h, hipStreamSynchronize(h->stream));
+        PCG_HIP(h, hipEventElapsedTime(&h->run_ms, h->ev[2], h->ev[3]));
+        const bool def_over = (int64_t)c.deferred > h->def_cap;
+        const bool rec_over = a.record && (int64_t)c.records > h->rec_cap;
+        if (def_over || rec_over) {
+            if (def_over) {
+                h->def_cap = (int64_t)c.deferred + (int64_t)c.deferred / 4 + 1024;
+                if (!pcg_ensure(h, h->deferred, sizeof(DeferredEntry) * h->def_cap))
+                    return pcg_fail(h, PCG_ERR_OOM, "deferred list (%lld)", (long long)h->def_cap);
+            }
+            if (rec_over) {
+                h->rec_cap = (int64_t)c.records * 2 + 1024;
+                if (!pcg_ensure(h, h->records, sizeof(pcg_record) * h->rec_cap))
+                    return pcg_fail(h, PCG_ERR_OOM, "record buffer (%lld)", (long long)h->rec_cap);
+            }
+            // idempotent re-run: flags/unions are OR-only; counters restart
+            PCG_HIP(h, hipMemsetAsync(h->ctr.p, 0, sizeof(DevCounters), h->stream));
+            continue;
+        }
+        if (c.deferred > 0) {
+            a = make_args(h, d, mode == MODE_EXACT);
+            const int m = d + 2;
+            const int per = (m * m + 2 * m) * 8;
+            const int bs = per * 64 <= 64 * 1024 ? 64 : 32;
+            const int64_t nb = std::min<int64_t>(((int64_t)c.deferred + bs - 1) / bs, 4096);
+            hipLaunchKernelGGL(k_exact, dim3((unsigned)nb), dim3(bs), (size_t)per * bs, h->stream, a);
+            PCG_HIP(h, hipGetLastError());
+        }
+        return PCG_OK;
+    }
+    return pcg_fail(h, PCG_ERR_OVERFLOW, "level %d: list capacity kept overflowing", d);
+}
+
+extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
+    if (!h || h->depth < 0) return pcg_fail(h, PCG_ERR_INVALID, "pcg_level_end without begin");
+    const int d = h->depth, n = (int)h->n, W = h->W;
+    DevCounters c{};
+    PCG_HIP(h, hipMemcpyAsync(&c, h->ctr.p, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+    PCG_HIP(h, hipStreamSynchronize(h->stream));
+    // records / near-alpha to host
+    if ((h->flags & PCG_FLAG_RECORD) && c.records) {
+        const int64_t k = std::min<int64_t>((int64_t)c.records, h->rec_cap);
+        const size_t old = h->rec_h.size();
+        h->rec_h.resize(old + k);
+        PCG_HIP(h, hipMemcpy(h->rec_h.data() + old, h->records.p, sizeof(pcg_record) * k, hipMemcpyDeviceToHost));
+    }
+    if (c.near_alpha) {
+        const int64_t k = std::min<int64_t>((int64_t)c.near_alpha, h->near_cap);
+        const size_t old = h->near_h.size();
+        h->near_h.resize(old + k);
+        PCG_HIP(h, hipMemcpy(h->near_h.data() + old, h->nearbuf.p, sizeof(pcg_record) * k, hipMemcpyDeviceToHost));
+    }
+    h->st.tests[d] = (int64_t)c.tests;
+    h->st.indep[d] = (int64_t)c.indep;
+    h->st.exact[d] = (int64_t)c.exact;
+    h->st.near_alpha[d] = (int64_t)c.near_alpha;
+    h->st.kernel_ms[d] = h->run_ms;
+    if (c.error) {
+        h->st.error = (c.error & 1) ? PCG_ERR_SINGULAR : PCG_ERR_DOMAIN;
+        if (stats) *stats = h->st;
+        return pcg_fail(h, h->st.error,
+                        (c.error & 1) ? "Data correlation matrix is singular. Cannot run fisherz test. Please check your data."
+                                      : "math domain error");
+    }
+    // export unions of removed pairs, then apply the removals
+    if (d >= 1 && h->sumdeg > 0) {
+        PCG_HIP(h, hipMemsetAsync(&((DevCounters *)h->ctr.p)->exported, 0, sizeof(unsigned long long), h->stream));
+        const int64_t room = h->export_cap - h->export_rows;
+        hipLaunchKernelGGL(k_export, dim3((unsigned)((h->sumdeg + 255) / 256)), dim3(256), 0, h->stream,
+                           (const int32_t *)h->off.p, (const int32_t *)h->nbr.p, (const uint8_t *)h->rm.p,
+                           (const uint64_t *)h->ug.p, n, W, h->sumdeg,
+                           (int32_t *)h->export_xy.p + 2 * h->export_rows,
+                           (uint64_t *)h->exportbuf.p + h->export_rows * W, room,
+                           &((DevCounters *)h->ctr.p)->exported);
+        unsigned long long ex = 0;
+        PCG_HIP(h, hipMemcpyAsync(&ex, &((DevCounters *)h->ctr.p)->exported, sizeof(ex), hipMemcpyDeviceToHost,
+                                  h->stream));
+        PCG_HIP(h, hipStreamSynchronize(h->stream));
+        if ((int64_t)ex > room) return pcg_fail(h, PCG_ERR_OVERFLOW, "sepset export overflow");
+        h->export_rows += (int64_t)ex;
+    }
+    const int64_t nw = (int64_t)n * W;
+    hipLaunchKernelGGL(k_apply, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, h->stream,
+                       (const uint8_t *)h->rm.p, (uint64_t *)h->adj.p, h->rl, n, W, d);
+    PCG_HIP(h, hipGetLastError());
+    int rc = refresh_graph(h);
+    if (rc) return rc;
+    h->st.edges_after[d] = h->sumdeg / 2;
+    if (stats) *stats = h->st;
+    return PCG_OK;
+}
+
+extern "C" int pcg_skeleton(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N, double alpha,
+                            int max_depth, int flags, int8_t *removed_level, pcg_stats *stats) {
+    int rc = pcg_skeleton_init(h, C, n, ldc, N, alpha, flags, removed_level);
+    if (rc) return rc;
+    for (int depth = 0;; ++depth) {
+        if (max_depth >= 0 && depth > max_depth) break;
+        int64_t total = 0;
+        PCG_HIP(h, hipEventRecord(h->ev[0], h->stream));
+        rc = pcg_level_begin(h, depth, &total, nullptr, nullptr);
+        if (rc == 1) break;
+        if (rc) return rc;
+        rc = pcg_level_run(h, 0, total);
+        if (rc) return rc;
+        rc = pcg_level_end(h, nullptr);
+        if (rc) { if (stats) *stats = h->st; return rc; }
+        PCG_HIP(h, hipEventRecord(h->ev[1], h->stream));
+        PCG_HIP(h, hipEventSynchronize(h->ev[1]));
+        float ms = 0.f;
+        PCG_HIP(h, hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
+        h->st.level_ms[depth] = ms;
+    }
+    if (stats) *stats = h->st;
+    return PCG_OK;
+}
+
+extern "C" int pcg_degrees(pcg_handle *h, int32_t *deg_host, int64_t capacity) {
+    if (!h || !deg_host || capacity < (int64_t)h->deg_levels.size())
+        return pcg_fail(h, PCG_ERR_INVALID, "pcg_degrees: capacity %lld < %zu", (long long)capacity,
+                        h ? h->deg_levels.size() : 0);
+    memcpy(deg_host, h->deg_levels.data(), sizeof(int32_t) * h->deg_levels.size());
+    return PCG_OK;
+}
+
+extern "C" int pcg_sepset_count(pcg_handle *h, int64_t *count, int32_t *words_per_row) {
+    if (!h) return PCG_ERR_INVALID;
+    if (count) *count = h->export_rows;
+    if (words_per_row) *words_per_row = h->W;
+    return PCG_OK;
+}
+
+extern "C" int pcg_sepset_export(pcg_handle *h, int32_t *xy_host, uint64_t *bits_host, int64_t count) {
+    if (!h || count > h->export_rows) return pcg_fail(h, PCG_ERR_INVALID, "pcg_sepset_export: count");
+    if (count == 0) return PCG_OK;
+    PCG_HIP(h, hipMemcpy(xy_host, h->export_xy.p, sizeof(int32_t) * 2 * count, hipMemcpyDeviceToHost));
+    PCG_HIP(h, hipMemcpy(bits_host, h->exportbuf.p, sizeof(uint64_t) * count * h->W, hipMemcpyDeviceToHost));
+    return PCG_OK;
+}
+
+extern "C" int pcg_record_count(pcg_handle *h, int64_t *count, int64_t *near_count) {
+    if (!h) return PCG_ERR_INVALID;
+    if (count) *count = (int64_t)h->rec_h.size();
+    if (near_count) *near_count = (int64_t)h->near_h.size();
+    return PCG_OK;
+}
+
+extern "C" int pcg_record_export(pcg_handle *h, pcg_record *rec_host, int64_t count, pcg_record *near_host,
+                                 int64_t near_count) {
+    if (!h || count > (int64_t)h->rec_h.size() || near_count > (int64_t)h->near_h.size())
+        return pcg_fail(h, PCG_ERR_INVALID, "pcg_record_export: count");
+    if (count) memcpy(rec_host, h->rec_h.data(), sizeof(pcg_record) * count);
+    if (near_count) memcpy(near_host, h->near_h.data(), sizeof(pcg_record) * near_count);
+    return PCG_OK;
+}

@@ -1,0 +1,201 @@
+"""Device engine: thin Python owner of one ``pcg_handle`` per GPU.
+
+PyTorch-ROCm is used only as plumbing — device buffers (``tensor.data_ptr()``), the
+stream the handle runs on, and (in ``rcaeval_amd.dist``) ``torch.distributed``. All
+arithmetic runs in the HIP kernels of ``libpcgpu.so``.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from ._lib import PcgRecord, PcgStats, check
+
+_ENGINES: dict = {}
+
+RECORD_DTYPE = np.dtype([("a", np.int32), ("b", np.int32), ("d", np.int32),
+                         ("s", np.int32, _lib.PCG_MAX_DEPTH), ("p", np.float64)], align=True)
+assert RECORD_DTYPE.itemsize == ctypes.sizeof(PcgRecord)
+
+
+def _torch():
+    import torch
+    return torch
+
+
+@dataclass
+class SkeletonOut:
+    """Result of one device skeleton run (host copies)."""
+    n: int
+    removed_level: np.ndarray          # n x n int8, -1 = edge survives
+    deg_levels: np.ndarray             # levels x n int32, degrees at the start of each depth
+    sep_xy: np.ndarray                 # R x 2 int32, ordered removed pairs with a non-empty union
+    sep_bits: np.ndarray               # R x W uint64, x-side union (global node bits)
+    stats: dict
+    records: np.ndarray | None = None  # RECORD_DTYPE (PCG_FLAG_RECORD)
+    near_alpha: np.ndarray | None = None
+    device_ms: float = 0.0
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def levels(self) -> int:
+        return int(self.stats["levels"])
+
+    @property
+    def adj(self) -> np.ndarray:
+        a = self.removed_level == -1
+        np.fill_diagonal(a, False)
+        return a
+
+
+class Engine:
+    """One handle on one HIP device."""
+
+    def __init__(self, device: int = 0):
+        torch = _torch()
+        if not torch.cuda.is_available():
+            raise _lib.EngineUnavailable("no HIP device is visible (torch.cuda.is_available() is False)")
+        self.lib = _lib.load()
+        self.device_index = int(device)
+        self.device = torch.device("cuda", self.device_index)
+        h = ctypes.c_void_p()
+        rc = self.lib.pcg_create(self.device_index, ctypes.byref(h))
+        if rc != 0:
+            raise _lib.PcgError(rc, f"pcg_create(device={device}) failed")
+        self.h = h
+        with torch.cuda.device(self.device):
+            stream = torch.cuda.current_stream(self.device)
+        check(self.h, self.lib.pcg_set_stream(self.h, ctypes.c_void_p(stream.cuda_stream)), "pcg_set_stream")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.pcg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ helpers
+    def to_device(self, a) -> "object":
+        torch = _torch()
+        if isinstance(a, torch.Tensor):
+            return a.to(device=self.device, dtype=torch.float64).contiguous()
+        arr = np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+        return torch.from_numpy(arr).to(self.device)
+
+    def sync(self):
+        _torch().cuda.synchronize(self.device)
+
+    # ------------------------------------------------------------------ K1
+    def corr(self, X) -> "object":
+        """``np.corrcoef(X.T)`` of an N x n array on the GPU; returns an n x n fp64 tensor."""
+        torch = _torch()
+        Xd = self.to_device(X)
+        N, n = Xd.shape
+        C = torch.empty((n, n), dtype=torch.float64, device=self.device)
+        check(self.h, self.lib.pcg_corr(self.h, ctypes.c_void_p(Xd.data_ptr()), N, n, n,
+                                        ctypes.c_void_p(C.data_ptr()), n), "pcg_corr")
+        return C
+
+    # ------------------------------------------------------------------ K2/K3
+    def skeleton(self, C, N: int, alpha: float = 0.05, max_depth: int = -1, flags: int = 0,
+                 record_capacity: int = 0) -> SkeletonOut:
+        torch = _torch()
+        Cd = self.to_device(C)
+        n = Cd.shape[0]
+        rl = torch.empty((n, n), dtype=torch.int8, device=self.device)
+        if record_capacity:
+            check(self.h, self.lib.pcg_set_capacity(self.h, int(record_capacity), 0), "pcg_set_capacity")
+        st = PcgStats()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        rc = self.lib.pcg_skeleton(self.h, ctypes.c_void_p(Cd.data_ptr()), n, n, int(N), float(alpha),
+                                   int(max_depth), int(flags), ctypes.c_void_p(rl.data_ptr()),
+                                   ctypes.byref(st))
+        ev1.record()
+        check(self.h, rc, "pcg_skeleton")
+        self.sync()
+        return self._collect(n, rl, st, ev0.elapsed_time(ev1))
+
+    def _collect(self, n: int, rl, st: PcgStats, device_ms: float) -> SkeletonOut:
+        L = st.levels
+        deg = np.zeros((max(L, 1), n), np.int32)
+        if L:
+            check(self.h, self.lib.pcg_degrees(self.h, deg.ctypes.data_as(ctypes.c_void_p), deg.size),
+                  "pcg_degrees")
+        cnt, W = ctypes.c_int64(), ctypes.c_int32()
+        check(self.h, self.lib.pcg_sepset_count(self.h, ctypes.byref(cnt), ctypes.byref(W)), "pcg_sepset_count")
+        xy = np.zeros((cnt.value, 2), np.int32)
+        bits = np.zeros((cnt.value, W.value), np.uint64)
+        if cnt.value:
+            check(self.h, self.lib.pcg_sepset_export(self.h, xy.ctypes.data_as(ctypes.c_void_p),
+                                                     bits.ctypes.data_as(ctypes.c_void_p), cnt.value),
+                  "pcg_sepset_export")
+        rc_, nc_ = ctypes.c_int64(), ctypes.c_int64()
+        check(self.h, self.lib.pcg_record_count(self.h, ctypes.byref(rc_), ctypes.byref(nc_)), "pcg_record_count")
+        rec = np.zeros(rc_.value, RECORD_DTYPE)
+        near = np.zeros(nc_.value, RECORD_DTYPE)
+        if rc_.value or nc_.value:
+            check(self.h, self.lib.pcg_record_export(self.h, rec.ctypes.data_as(ctypes.c_void_p), rc_.value,
+                                                     near.ctypes.data_as(ctypes.c_void_p), nc_.value),
+                  "pcg_record_export")
+        return SkeletonOut(n=n, removed_level=rl.cpu().numpy(), deg_levels=deg[:L], sep_xy=xy, sep_bits=bits,
+                           stats=st.as_dict(), records=rec, near_alpha=near, device_ms=device_ms)
+
+    # ------------------------------------------------------------------ K4
+    def pagerank_dense(self, A, damping: float = 0.85, n_iter: int = 10, tol: float = 1e-6) -> np.ndarray:
+        torch = _torch()
+        Ad = self.to_device(A)
+        m = Ad.shape[0]
+        out = torch.empty(m, dtype=torch.float64, device=self.device)
+        check(self.h, self.lib.pcg_pagerank_dense(self.h, ctypes.c_void_p(Ad.data_ptr()), m, m, float(damping),
+                                                  int(n_iter), float(tol), ctypes.c_void_p(out.data_ptr())),
+              "pcg_pagerank_dense")
+        return out.cpu().numpy()
+
+    def random_walk_counts(self, P, start: int, num_loop: int, state: int, inc: int) -> np.ndarray:
+        torch = _torch()
+        Pd = self.to_device(P)
+        m = Pd.shape[0]
+        counts = torch.empty(m, dtype=torch.int64, device=self.device)
+        mask = (1 << 64) - 1
+        check(self.h, self.lib.pcg_random_walk(self.h, ctypes.c_void_p(Pd.data_ptr()), m, m, int(start),
+                                               int(num_loop), (state >> 64) & mask, state & mask,
+                                               (inc >> 64) & mask, inc & mask,
+                                               ctypes.c_void_p(counts.data_ptr())),
+              "pcg_random_walk")
+        return counts.cpu().numpy()
+
+
+def get_engine(device: int | None = None) -> Engine:
+    """Process-wide engine for ``device`` (default: LOCAL_RANK or 0)."""
+    import os
+    if device is None:
+        device = int(os.environ.get("LOCAL_RANK", "0"))
+    eng = _ENGINES.get(device)
+    if eng is None:
+        eng = Engine(device)
+        _ENGINES[device] = eng
+    return eng
+
+
+def orient(adj: np.ndarray, sep_xy: np.ndarray, sep_bits: np.ndarray, priority: int = 2) -> np.ndarray:
+    """Host C++ orientation (UCSepset priority 2 + Meek) → endpoint-code matrix."""
+    lib = _lib.load()
+    n = adj.shape[0]
+    a = np.ascontiguousarray(adj, dtype=np.uint8)
+    xy = np.ascontiguousarray(sep_xy, dtype=np.int32)
+    bits = np.ascontiguousarray(sep_bits, dtype=np.uint64)
+    g = np.zeros((n, n), np.int32)
+    rc = lib.pcg_orient(n, a.ctypes.data_as(ctypes.c_void_p), xy.ctypes.data_as(ctypes.c_void_p),
+                        bits.ctypes.data_as(ctypes.c_void_p), len(xy), int(priority),
+                        g.ctypes.data_as(ctypes.c_void_p))
+    if rc != 0:
+        raise _lib.PcgError(rc, f"pcg_orient(priority={priority}) failed")
+    return g

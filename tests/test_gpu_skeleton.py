@@ -1,0 +1,137 @@
+"""GPU parity: K1 correlation and K2/K3 skeleton vs the CPU oracle (C restatement).
+
+Tolerances (north_star): p-values |dp| <= 1e-9 |p_ref| + 2^-51 (fisherz.p_close);
+skeleton (removal depth of every pair) and sepset unions bit-identical; decisions may differ
+only for tests with |p - alpha| < 1e-9, which the engine enumerates (near_alpha list).
+"""
+import numpy as np
+import pytest
+
+from oracle import cpc, fisherz
+from rcaeval_amd import _lib, synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from rcaeval_amd.engine import get_engine
+    return get_engine(0)
+
+
+def _key(r):
+    return (int(r["a"]), int(r["b"]), tuple(int(v) for v in r["s"][: r["d"]]))
+
+
+def _unions_from_oracle(ref, n):
+    rows = {}
+    W = (n + 63) // 64
+    for x in range(n):
+        for y in range(n):
+            if x != y and ref.removed_level[x, y] > 0:
+                bits = ref.side_union[x, y]
+                if bits.any():
+                    rows[(x, y)] = tuple(int(b) for b in bits[:W])
+    return rows
+
+
+def _unions_from_engine(out):
+    return {(int(x), int(y)): tuple(int(b) for b in bits) for (x, y), bits in zip(out.sep_xy, out.sep_bits)}
+
+
+CASES = [  # (n, N, seed, w_low, w_high, edge_prob)
+    (8, 300, 0, 0.3, 0.9, None),
+    (20, 500, 1, 0.3, 0.9, None),
+    (30, 2000, 2, 0.1, 0.5, None),
+    (50, 600, 3, 0.3, 0.9, 0.1),
+    (64, 1000, 4, 0.2, 0.8, 0.08),
+    (65, 800, 5, 0.2, 0.8, 0.08),
+    (130, 3000, 6, 0.1, 0.5, None),
+]
+
+
+@pytest.mark.parametrize("n,N,seed,wl,wh,ep", CASES)
+def test_corr_matches_numpy(eng, n, N, seed, wl, wh, ep):
+    X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
+    C = eng.corr(X).cpu().numpy()
+    ref = np.corrcoef(X.T)
+    np.testing.assert_allclose(C, ref, rtol=0, atol=2e-14)
+
+
+@pytest.mark.parametrize("n,N,seed,wl,wh,ep", CASES)
+@pytest.mark.parametrize("flags", [0, _lib.PCG_FLAG_FULL_P | _lib.PCG_FLAG_RECORD])
+def test_skeleton_matches_oracle(eng, n, N, seed, wl, wh, ep, flags):
+    X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
+    C = np.corrcoef(X.T)
+    ref = cpc.skeleton(C, N, record_cap=2_000_000)
+    out = eng.skeleton(C, N, flags=flags, record_capacity=2_000_000)
+    near = {_key(r) for r in out.near_alpha}
+    if not near:
+        np.testing.assert_array_equal(out.removed_level, ref.removed_level)
+        assert _unions_from_engine(out) == _unions_from_oracle(ref, n)
+    assert out.stats["tests"] == ref.tests
+    if flags & _lib.PCG_FLAG_RECORD:
+        d = {_key(r): r["p"] for r in ref.records}
+        g = {_key(r): r["p"] for r in out.records}
+        assert set(g) == set(d)
+        keys = sorted(d)
+        ok = fisherz.p_close([g[k] for k in keys], [d[k] for k in keys])
+        assert ok.all(), [(keys[i], g[keys[i]], d[keys[i]]) for i in np.nonzero(~ok)[0][:5]]
+
+
+def test_decide_and_fullp_agree_2000_depth2(eng):
+    """Full-size (2000 vars) parity at depth <= 2 against the C oracle."""
+    X = synth.gaussian_sem(2000, 10000, seed=0)
+    C = eng.corr(X)
+    Ch = C.cpu().numpy()
+    ref = cpc.skeleton(Ch, 10000, max_depth=2, want_union=True)
+    a = eng.skeleton(C, 10000, max_depth=2, flags=0)
+    b = eng.skeleton(C, 10000, max_depth=2, flags=_lib.PCG_FLAG_FULL_P)
+    for out in (a, b):
+        assert out.stats["tests"] == ref.tests
+        if len(out.near_alpha) == 0:
+            np.testing.assert_array_equal(out.removed_level, ref.removed_level)
+            assert _unions_from_engine(out) == _unions_from_oracle(ref, 2000)
+
+
+def test_constant_column_nan_is_dependent(eng):
+    X = synth.gaussian_sem(12, 400, seed=7, w_low=0.3, w_high=0.9)
+    X[:, 5] = 3.0                                   # constant -> NaN correlations -> p NaN
+    with np.errstate(invalid="ignore", divide="ignore"):
+        C = np.corrcoef(X.T)
+    ref = cpc.skeleton(C, 400)
+    out = eng.skeleton(C, 400)
+    np.testing.assert_array_equal(out.removed_level, ref.removed_level)
+    assert (out.removed_level[5] == -1).sum() == 11   # NaN p never removes an edge
+
+
+def test_duplicate_column_singular_raises(eng):
+    X = synth.gaussian_sem(10, 300, seed=8, w_low=0.3, w_high=0.9)
+    X[:, 3] = X[:, 2]
+    C = np.corrcoef(X.T)
+    ref = cpc.skeleton(C, 300)
+    if ref.error:
+        with pytest.raises(ValueError):
+            eng.skeleton(C, 300)
+
+
+def test_tiny_sample_dof(eng):
+    X = synth.gaussian_sem(6, 6, seed=9, w_low=0.3, w_high=0.9)
+    C = np.corrcoef(X.T)
+    ref = cpc.skeleton(C, 6)
+    if ref.error:
+        with pytest.raises(ValueError):
+            eng.skeleton(C, 6)
+    else:
+        out = eng.skeleton(C, 6)
+        np.testing.assert_array_equal(out.removed_level, ref.removed_level)
+
+
+def test_max_depth_cap(eng):
+    X = synth.gaussian_sem(40, 1000, seed=10, w_low=0.2, w_high=0.8, edge_prob=0.1)
+    C = np.corrcoef(X.T)
+    for md in (0, 1, 2):
+        ref = cpc.skeleton(C, 1000, max_depth=md)
+        out = eng.skeleton(C, 1000, max_depth=md)
+        assert out.levels == ref.levels <= md + 1
+        np.testing.assert_array_equal(out.removed_level, ref.removed_level)

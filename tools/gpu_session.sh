@@ -1,0 +1,28 @@
+#!/bin/bash
+# Runs GPU steps one after another; each under its own time limit. Stops at the first
+# step that did not end normally (exit 0 = pass, 1 = test failures are tolerated).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+: > gpurun_out/status.log
+run() {
+  local name=$1 t=$2; shift 2
+  echo "[$(date +%T)] start $name" >> gpurun_out/status.log
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc" >> gpurun_out/status.log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stop after $name rc=$rc"; cat gpurun_out/status.log; exit $rc; fi
+  return 0
+}
+for step in "$@"; do
+  case $step in
+    smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    test)  run pytest_gpu 1200 python -m pytest tests -m gpu -q -x --timeout 600 ;;
+    testall) run pytest_gpu 1200 python -m pytest tests -m gpu -q --timeout 600 ;;
+    bench) run bench 900 python bench.py --steps 3 --warmup 1 ;;
+    benchfast) run bench 600 python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    *) echo "unknown step $step" ;;
+  esac
+done
+cat gpurun_out/status.log
