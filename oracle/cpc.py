@@ -22,7 +22,7 @@ class OrcStats(ctypes.Structure):
 
 
 REC_DTYPE = np.dtype([("a", np.int32), ("b", np.int32), ("d", np.int32),
-                      ("s", np.int32, 5), ("p", np.float64)], align=True)
+                      ("s", np.int32, 12), ("p", np.float64)], align=True)
 
 
 def build() -> str:

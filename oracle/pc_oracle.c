@@ -28,7 +28,7 @@
 #include <omp.h>
 #endif
 
-#define ORC_MAXD 8
+#define ORC_MAXD 12
 
 typedef struct {
     int64_t tests[32];   /* unique tests per depth            */
@@ -41,7 +41,7 @@ typedef struct {
 typedef struct {         /* one unique test (record mode) */
     int32_t a, b;        /* a < b */
     int32_t d;
-    int32_t s[5];        /* sorted conditioning set, -1 padded */
+    int32_t s[12];       /* sorted conditioning set, -1 padded */
     double p;
 } orc_record;
 
@@ -209,7 +209,7 @@ int orc_skeleton(const double *C, int n, int N, double alpha, int max_depth,
                             if (slot < rec_cap) {
                                 orc_record *r = rec + slot;
                                 r->a = a; r->b = b; r->d = d;
-                                for (int k = 0; k < 5; ++k) r->s[k] = k < d ? S[k] : -1;
+                                for (int k = 0; k < 12; ++k) r->s[k] = k < d ? S[k] : -1;
                                 r->p = p;
                             }
                         }

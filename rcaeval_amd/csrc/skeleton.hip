@@ -70,8 +70,8 @@ struct LevelArgs {
     double alpha, sqrt_dof;
     int dof_negative;
     int record;
-    int64_t chunk_lo;            // first chunk of this launch
-    int stage_cap;               // staged elements held in registers per thread
+    int64_t chunk_lo;            // first chunk of this launch (within its class)
+    int spl;                     // S ranks per lane (LDS-resident kernel)
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -498,6 +498,204 @@ __global__ __launch_bounds__(256) void k_level(LevelArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// depth d >= 1, nodes with D <= 64 neighbours: the node's whole local correlation block
+// M[t][k] = C[nbr t, nbr k] (D x D), C[x, nbr t], C[nbr t, nbr t] and the local adjacency
+// masks lmask[t] (bit k <=> nbr k in adj(nbr t)) are staged in LDS once per block; the
+// y sweep then runs barrier-free: skip = bit t of the lane's S mask, subset test
+// (S in adj(y)) = (lmask[t] & Smask) == Smask, memo ownership (y < x) = t < tx. Each lane
+// walks `spl` S ranks (stride = block size) so the staging is amortised over
+// spl * 256 * (D - d) tests. Sepset unions and removal flags accumulate in LDS (local bits)
+// and are flushed once per block.
+template <int DM, int MODE>
+__global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x;
+    const int bs = blockDim.x;
+    const int64_t chunk = a.chunk_lo + blockIdx.x;
+    int lo = 0, hi = a.n;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (a.cpre[mid] <= chunk) lo = mid; else hi = mid;
+    }
+    const int x = lo;
+    const int D = a.deg[x];
+    const int d = DM <= 4 ? DM : a.d;
+    const int32_t *nxg = a.nbr + a.off[x];
+
+    double *M = reinterpret_cast<double *>(smem);                 // D * D
+    double *Mx = M + D * D;                                       // D
+    double *Md = Mx + D;                                          // D
+    unsigned long long *lmask = reinterpret_cast<unsigned long long *>(Md + D);   // D
+    unsigned long long *uself = lmask + D;                        // D
+    unsigned long long *uprop = uself + D;                        // D
+    int32_t *nxs = reinterpret_cast<int32_t *>(uprop + D);       // D
+    int *s_tx = nxs + D;                                          // 1 (no static LDS: G17)
+
+    for (int i = tid; i < D; i += bs) nxs[i] = nxg[i];
+    __syncthreads();
+    for (int e = tid; e < D * D; e += bs) {
+        const int t = e / D, k = e - t * D;
+        M[e] = a.C[(int64_t)nxs[t] * a.ldc + nxs[k]];
+    }
+    for (int t = tid; t < D; t += bs) {
+        const int yg = nxs[t];
+        Mx[t] = a.C[(int64_t)x * a.ldc + yg];
+        Md[t] = a.diag[yg];
+        const uint64_t *ar = a.adj + (int64_t)yg * a.W;
+        unsigned long long m = 0;
+        for (int k = 0; k < D; ++k) m |= ((ar[nxs[k] >> 6] >> (nxs[k] & 63)) & 1ull) << k;
+        lmask[t] = m;
+        uself[t] = 0;
+        uprop[t] = 0;
+    }
+    if (tid == 0) {
+        int c = 0;
+        while (c < D && nxs[c] < x) ++c;
+        *s_tx = c;
+    }
+    __syncthreads();
+    const int tx = *s_tx;
+    const double Cxx = a.diag[x];
+    const uint64_t nS = pcg_binom(a.binom, D, d);
+    const uint64_t r0 = (uint64_t)(chunk - a.cpre[x]) * (uint64_t)bs * (uint64_t)a.spl;
+    const uint64_t r1 = min(nS, r0 + (uint64_t)bs * (uint64_t)a.spl);
+    unsigned long long tests = 0, indep = 0;
+
+    for (uint64_t rank = r0 + tid; rank < r1; rank += bs) {
+        int k[DM];
+#pragma unroll
+        for (int i = 0; i < DM; ++i) k[i] = 0;
+        pcg_unrank_colex<DM>(rank, d, D, a.binom, k);
+        unsigned long long Smask = 0;
+#pragma unroll
+        for (int i = 0; i < DM; ++i)
+            if (i < d) Smask |= 1ull << k[i];
+        // Cholesky of M_SS, u = L^-1 M_Sx
+        double L[DM][DM], rinv[DM], u[DM];
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < DM; ++j) {
+            if (j < d) {
+                double s = M[k[j] * D + k[j]];
+#pragma unroll
+                for (int q = 0; q < DM; ++q)
+                    if (q < j) s -= L[j][q] * L[j][q];
+                ok = ok && (s > 0.0);
+                const double ljj = sqrt(s);
+                rinv[j] = 1.0 / ljj;
+                L[j][j] = ljj;
+#pragma unroll
+                for (int i = 0; i < DM; ++i) {
+                    if (i > j && i < d) {
+                        double t = M[k[i] * D + k[j]];
+#pragma unroll
+                        for (int q = 0; q < DM; ++q)
+                            if (q < j) t -= L[i][q] * L[j][q];
+                        L[i][j] = t * rinv[j];
+                    }
+                }
+            }
+        }
+        double uu = 0.0;
+#pragma unroll
+        for (int i = 0; i < DM; ++i) {
+            if (i < d) {
+                double t = Mx[k[i]];
+#pragma unroll
+                for (int q = 0; q < DM; ++q)
+                    if (q < i) t -= L[i][q] * u[q];
+                u[i] = t * rinv[i];
+                uu += u[i] * u[i];
+            }
+        }
+        const double cxx = Cxx - uu;
+        ok = ok && (cxx == cxx);
+
+        for (int t = 0; t < D; ++t) {
+            if ((Smask >> t) & 1ull) continue;
+            const unsigned long long lm = lmask[t];
+            const bool in_y = (lm & Smask) == Smask;
+            if (t < tx && in_y) continue;          // node nbr[t] < x owns this test (memo)
+            ++tests;
+            int dec = 2;
+            double p = 0.0;
+            if (ok) {
+                const double *Mt = M + t * D;
+                double vv = 0.0, uv = 0.0, v[DM];
+#pragma unroll
+                for (int i = 0; i < DM; ++i) {
+                    if (i < d) {
+                        double tt = Mt[k[i]];
+#pragma unroll
+                        for (int q = 0; q < DM; ++q)
+                            if (q < i) tt -= L[i][q] * v[q];
+                        v[i] = tt * rinv[i];
+                        vv += v[i] * v[i];
+                        uv += u[i] * v[i];
+                    }
+                }
+                dec = decide<MODE>(a, Mx[t] - uv, cxx, Md[t] - vv, &p);
+            }
+            if (dec == 2 || (MODE == MODE_FULLP && (a.record || fabs(p - a.alpha) < 1e-9))) {
+                int sg[DM];
+#pragma unroll
+                for (int i = 0; i < DM; ++i) sg[i] = i < d ? nxs[k[i]] : 0;
+                const int yg = nxs[t];
+                if (dec == 2) {
+                    push_deferred(a, x, yg, sg, d);
+                    continue;
+                }
+                const int lo_ = x < yg ? x : yg, hi_ = x < yg ? yg : x;
+                if (a.record) push_record(a.records, a.rec_cap, &a.ctr->records, lo_, hi_, d, sg, p);
+                if (fabs(p - a.alpha) < 1e-9)
+                    push_record(a.nearl, a.near_cap, &a.ctr->near_alpha, lo_, hi_, d, sg, p);
+            }
+            if (dec == 1) {
+                ++indep;
+                atomicOr(&uself[t], Smask);
+                if (in_y && t >= tx) atomicOr(&uprop[t], Smask);
+            }
+        }
+    }
+    __syncthreads();
+    // flush unions (local bits -> global node bits) and removal flags
+    for (int t = tid; t < D; t += bs) {
+        const unsigned long long us = uself[t], up = uprop[t];
+        if (!(us | up)) continue;
+        const int yg = nxs[t];
+        a.rm[(int64_t)x * a.n + yg] = 1;
+        a.rm[(int64_t)yg * a.n + x] = 1;
+        if (us) {
+            unsigned long long *row = reinterpret_cast<unsigned long long *>(a.ug + ((int64_t)a.off[x] + t) * a.W);
+            unsigned long long m = us;
+            while (m) {
+                const int b = __ffsll((long long)m) - 1;
+                const int g = nxs[b];
+                atomicOr(&row[g >> 6], 1ull << (g & 63));
+                m &= m - 1;
+            }
+        }
+        if (up) {
+            const int slot = a.off[yg] + find_in_sorted(a.nbr + a.off[yg], a.deg[yg], x);
+            unsigned long long *row = reinterpret_cast<unsigned long long *>(a.ug + (int64_t)slot * a.W);
+            unsigned long long m = up;
+            while (m) {
+                const int b = __ffsll((long long)m) - 1;
+                const int g = nxs[b];
+                atomicOr(&row[g >> 6], 1ull << (g & 63));
+                m &= m - 1;
+            }
+        }
+    }
+    tests = wave_sum(tests);
+    indep = wave_sum(indep);
+    if ((tid & 63) == 0) {
+        if (tests) atomicAdd(&a.ctr->tests, tests);
+        if (indep) atomicAdd(&a.ctr->indep, indep);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // exact path over the deferred list (LU like numpy.linalg.inv; the reference p expression)
 __global__ void k_exact(LevelArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -636,6 +834,7 @@ LevelArgs make_args(pcg_handle *h, int d, int mode_exact_all) {
     }
     a.rmax2 = 1.0 - 2e-9;
     a.record = (h->flags & PCG_FLAG_RECORD) ? 1 : 0;
+    a.spl = h->spl;
     (void)mode_exact_all;
     return a;
 }
@@ -652,6 +851,23 @@ void launch_level_mode(pcg_handle *h, const LevelArgs &a, int64_t nchunks, size_
     else if (d <= 8) hipLaunchKernelGGL((k_level<8, MODE>), grid, block, lds, h->stream, a);
     else hipLaunchKernelGGL((k_level<12, MODE>), grid, block, lds, h->stream, a);
 }
+
+template <int MODE>
+void launch_lds_mode(pcg_handle *h, const LevelArgs &a, int64_t nchunks, size_t lds) {
+    const dim3 grid((unsigned)nchunks), block(256);
+    const int d = a.d;
+    if (d == 1) hipLaunchKernelGGL((k_level_lds<1, MODE>), grid, block, lds, h->stream, a);
+    else if (d == 2) hipLaunchKernelGGL((k_level_lds<2, MODE>), grid, block, lds, h->stream, a);
+    else if (d == 3) hipLaunchKernelGGL((k_level_lds<3, MODE>), grid, block, lds, h->stream, a);
+    else if (d == 4) hipLaunchKernelGGL((k_level_lds<4, MODE>), grid, block, lds, h->stream, a);
+    else if (d <= 6) hipLaunchKernelGGL((k_level_lds<6, MODE>), grid, block, lds, h->stream, a);
+    else if (d <= 8) hipLaunchKernelGGL((k_level_lds<8, MODE>), grid, block, lds, h->stream, a);
+    else hipLaunchKernelGGL((k_level_lds<12, MODE>), grid, block, lds, h->stream, a);
+}
+
+constexpr int SMALL_DEG = 64;        // LDS-resident kernel handles nodes with <= 64 neighbours
+
+size_t lds_small_bytes(int D) { return (size_t)D * D * 8 + (size_t)D * (2 * 8 + 3 * 8 + 4) + 16; }
 
 int mode_of(const pcg_handle *h, int d) {
     if ((h->flags & PCG_FLAG_EXACT_ALL) || (double)h->N - d - 3 <= 0) return MODE_EXACT;
@@ -766,41 +982,55 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
         calls += (int64_t)std::min<uint64_t>(c, (uint64_t)INT64_MAX / 4096) * D;
     }
     h->st.calls[depth] = calls;
-    // work decomposition
-    h->cpre_h.assign(n + 1, 0);
+    // work decomposition: depth 0 = one chunk per row; depth >= 1 = two node classes
+    h->cpre_h.assign(2 * (n + 1), 0);
     h->work_h.assign(n, 0);
+    int64_t *cs = h->cpre_h.data(), *cl = h->cpre_h.data() + (n + 1);
+    h->maxdeg_small = 0;
     if (depth == 0) {
         h->chunk = 256;
-        for (int x = 0; x <= n; ++x) h->cpre_h[x] = x;
+        h->spl = 1;
+        for (int x = 0; x <= n; ++x) cs[x] = x;
         for (int x = 0; x < n; ++x) h->work_h[x] = n - 1 - x;
+        h->total_small = n;
+        h->total_large = 0;
     } else {
-        // one block per node when C(D, d) is small; 256-rank chunks otherwise
-        double mean_s = 0.0;
-        int cnt = 0;
+        double sum_small = 0.0, sum_large = 0.0;
+        int cnt_large = 0;
         for (int x = 0; x < n; ++x) {
             const int D = h->deg_h[x];
-            if (D >= depth + 1) { mean_s += (double)hbinom(h, D, depth); ++cnt; }
+            if (D < depth + 1) continue;
+            const uint64_t ns = hbinom(h, D, depth);
+            if (ns > ((uint64_t)1 << 46))
+                return pcg_fail(h, PCG_ERR_INVALID, "depth %d work too large at node %d (deg %d)", depth, x, D);
+            h->work_h[x] = (int64_t)ns * (D - depth);
+            if (D <= SMALL_DEG) { sum_small += (double)ns; h->maxdeg_small = std::max(h->maxdeg_small, D); }
+            else { sum_large += (double)ns; ++cnt_large; }
         }
-        mean_s = cnt ? mean_s / cnt : 0.0;
-        h->chunk = mean_s <= 64 ? 64 : (mean_s <= 128 ? 128 : 256);
-        int64_t s = 0;
+        // ~4096 LDS-resident blocks per depth; each lane walks spl S ranks
+        h->spl = (int)std::min(64.0, std::max(1.0, std::floor(sum_small / (256.0 * 4096.0))));
+        const double mean_large = cnt_large ? sum_large / cnt_large : 0.0;
+        h->chunk = mean_large <= 64 ? 64 : (mean_large <= 128 ? 128 : 256);
+        const uint64_t csz = (uint64_t)256 * h->spl;
+        int64_t ss = 0, sl = 0;
         for (int x = 0; x < n; ++x) {
-            h->cpre_h[x] = s;
+            cs[x] = ss;
+            cl[x] = sl;
             const int D = h->deg_h[x];
-            if (D >= depth + 1) {
-                const uint64_t ns = hbinom(h, D, depth);
-                if (ns > ((uint64_t)1 << 46))
-                    return pcg_fail(h, PCG_ERR_INVALID, "depth %d work too large at node %d (deg %d)", depth, x, D);
-                s += (int64_t)((ns + h->chunk - 1) / h->chunk);
-                h->work_h[x] = (int64_t)ns * (D - depth);
-            }
+            if (D < depth + 1) continue;
+            const uint64_t ns = hbinom(h, D, depth);
+            if (D <= SMALL_DEG) ss += (int64_t)((ns + csz - 1) / csz);
+            else sl += (int64_t)((ns + h->chunk - 1) / h->chunk);
         }
-        h->cpre_h[n] = s;
+        cs[n] = ss;
+        cl[n] = sl;
+        h->total_small = ss;
+        h->total_large = sl;
     }
-    h->total_chunks = h->cpre_h[n];
+    h->total_chunks = h->total_small + h->total_large;
     if (total_chunks) *total_chunks = h->total_chunks;
-    if (!pcg_ensure(h, h->cpre, sizeof(int64_t) * (n + 1))) return PCG_ERR_OOM;
-    PCG_HIP(h, hipMemcpyAsync(h->cpre.p, h->cpre_h.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice,
+    if (!pcg_ensure(h, h->cpre, sizeof(int64_t) * 2 * (n + 1))) return PCG_ERR_OOM;
+    PCG_HIP(h, hipMemcpyAsync(h->cpre.p, h->cpre_h.data(), sizeof(int64_t) * 2 * (n + 1), hipMemcpyHostToDevice,
                               h->stream));
     PCG_HIP(h, hipMemsetAsync(h->rm.p, 0, (size_t)n * n, h->stream));
     PCG_HIP(h, hipMemsetAsync(h->ctr.p, 0, sizeof(DevCounters), h->stream));
@@ -841,21 +1071,26 @@ extern "C" int pcg_level_chunk_work(pcg_handle *h, int64_t *prefix_host, int64_t
     const int n = (int)h->n;
     int64_t acc = 0;
     prefix_host[0] = 0;
-    for (int x = 0; x < n; ++x) {
-        const int64_t c0 = h->cpre_h[x], c1 = h->cpre_h[x + 1];
-        if (c1 == c0) continue;
-        if (h->depth == 0) {
-            acc += h->work_h[x];
-            prefix_host[c0 + 1] = acc;
-            continue;
-        }
-        const int D = h->deg_h[x];
-        const uint64_t ns = hbinom(h, D, h->depth);
-        for (int64_t c = c0; c < c1; ++c) {
-            const uint64_t r0 = (uint64_t)(c - c0) * h->chunk;
-            const uint64_t r1 = std::min<uint64_t>(r0 + h->chunk, ns);
-            acc += (int64_t)(r1 - r0) * (D - h->depth) + 1;
-            prefix_host[c + 1] = acc;
+    for (int cls = 0; cls < 2; ++cls) {
+        const int64_t *cp = h->cpre_h.data() + cls * (n + 1);
+        const int64_t base = cls ? h->total_small : 0;
+        const uint64_t csz = cls ? (uint64_t)h->chunk : (uint64_t)256 * h->spl;
+        for (int x = 0; x < n; ++x) {
+            const int64_t c0 = cp[x], c1 = cp[x + 1];
+            if (c1 == c0) continue;
+            if (h->depth == 0) {
+                acc += h->work_h[x] + 1;
+                prefix_host[base + c0 + 1] = acc;
+                continue;
+            }
+            const int D = h->deg_h[x];
+            const uint64_t ns = hbinom(h, D, h->depth);
+            for (int64_t c = c0; c < c1; ++c) {
+                const uint64_t r0 = (uint64_t)(c - c0) * csz;
+                const uint64_t r1 = std::min<uint64_t>(r0 + csz, ns);
+                acc += (int64_t)(r1 - r0) * (D - h->depth) + 1;
+                prefix_host[base + c + 1] = acc;
+            }
         }
     }
     return PCG_OK;
@@ -878,12 +1113,29 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                 else if (mode == MODE_FULLP) hipLaunchKernelGGL(k_level0<MODE_FULLP>, grid, block, 0, h->stream, a);
                 else hipLaunchKernelGGL(k_level0<MODE_EXACT>, grid, block, 0, h->stream, a);
             } else {
-                const size_t lds = level_lds(h, a.bs);
-                if (lds > 160 * 1024)
-                    return pcg_fail(h, PCG_ERR_INVALID, "max degree %d too large for LDS staging", h->maxdeg);
-                if (mode == MODE_DECIDE) launch_level_mode<MODE_DECIDE>(h, a, nch, lds);
-                else if (mode == MODE_FULLP) launch_level_mode<MODE_FULLP>(h, a, nch, lds);
-                else launch_level_mode<MODE_EXACT>(h, a, nch, lds);
+                const int64_t s_lo = chunk_lo, s_hi = std::min(chunk_hi, h->total_small);
+                if (s_hi > s_lo) {
+                    LevelArgs as = a;
+                    as.chunk_lo = s_lo;
+                    as.bs = 256;
+                    const size_t lds = lds_small_bytes(h->maxdeg_small);
+                    if (mode == MODE_DECIDE) launch_lds_mode<MODE_DECIDE>(h, as, s_hi - s_lo, lds);
+                    else if (mode == MODE_FULLP) launch_lds_mode<MODE_FULLP>(h, as, s_hi - s_lo, lds);
+                    else launch_lds_mode<MODE_EXACT>(h, as, s_hi - s_lo, lds);
+                }
+                const int64_t l_lo = std::max(chunk_lo, h->total_small) - h->total_small;
+                const int64_t l_hi = chunk_hi - h->total_small;
+                if (l_hi > l_lo) {
+                    LevelArgs al = a;
+                    al.cpre = (const int64_t *)h->cpre.p + (h->n + 1);
+                    al.chunk_lo = l_lo;
+                    const size_t lds = level_lds(h, al.bs);
+                    if (lds > 160 * 1024)
+                        return pcg_fail(h, PCG_ERR_INVALID, "max degree %d too large for LDS staging", h->maxdeg);
+                    if (mode == MODE_DECIDE) launch_level_mode<MODE_DECIDE>(h, al, l_hi - l_lo, lds);
+                    else if (mode == MODE_FULLP) launch_level_mode<MODE_FULLP>(h, al, l_hi - l_lo, lds);
+                    else launch_level_mode<MODE_EXACT>(h, al, l_hi - l_lo, lds);
+                }
             }
         }
         PCG_HIP(h, hipGetLastError());

@@ -102,7 +102,7 @@ def test_constant_column_nan_is_dependent(eng):
     ref = cpc.skeleton(C, 400)
     out = eng.skeleton(C, 400)
     np.testing.assert_array_equal(out.removed_level, ref.removed_level)
-    assert (out.removed_level[5] == -1).sum() == 11   # NaN p never removes an edge
+    assert (out.removed_level[5] == -1).sum() == 12   # NaN p never removes an edge (+ diagonal)
 
 
 def test_duplicate_column_singular_raises(eng):
