@@ -117,8 +117,13 @@ def main():
     Xd = eng.to_device(X)                      # resident in HBM before timing
     torch.cuda.synchronize()
 
+    phases = []
+
     def one_step():
+        t0 = time.perf_counter()
         C = eng.corr(Xd)
+        torch.cuda.synchronize()
+        phases.append(("corr", time.perf_counter() - t0))
         if world > 1:
             from rcaeval_amd.dist import sharded_skeleton
             return sharded_skeleton(eng, C, args.samples, alpha=args.alpha, max_depth=args.max_depth,
@@ -173,6 +178,9 @@ def main():
                        "parallelism": f"edge-sharded x{world}" if world > 1 else "single GPU",
                        "decision": "full p-value" if args.full_p else "threshold + exact band"},
             "skeleton_ms": ms,
+            "step_ms_all": [round(1000 * t, 3) for t in times],
+            "corr_ms": [round(1000 * t, 3) for n_, t in phases if n_ == "corr"],
+            "engine_phases_ms": getattr(out, "extra", {}),
             "tests_per_level": st["tests"], "calls_per_level": st["calls"],
             "kernel_ms_per_level": [round(v, 3) for v in st["kernel_ms"]],
             "level_ms": [round(v, 3) for v in st["level_ms"]],

@@ -114,6 +114,8 @@ int pcg_degrees(pcg_handle *h, int32_t *deg_host, int64_t capacity);
 int pcg_sepset_count(pcg_handle *h, int64_t *count, int32_t *words_per_row);
 int pcg_sepset_export(pcg_handle *h, int32_t *xy_host /* 2*count */,
                       uint64_t *bits_host /* count*W */, int64_t count);
+/* Same, into caller-owned device buffers (stream-ordered copy, no host round trip).     */
+int pcg_sepset_export_device(pcg_handle *h, int32_t *xy_dev, uint64_t *bits_dev, int64_t count);
 
 /* Records of the last pcg_skeleton (PCG_FLAG_RECORD) and the near-alpha list.         */
 int pcg_record_count(pcg_handle *h, int64_t *count, int64_t *near_alpha_count);
@@ -135,6 +137,9 @@ int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi);
 int pcg_level_end(pcg_handle *h, pcg_stats *stats);
 /* Work weight of each chunk prefix (host out, total_chunks+1 int64) for load balance.  */
 int pcg_level_chunk_work(pcg_handle *h, int64_t *prefix_host, int64_t capacity);
+/* Use a caller-owned device buffer (n*n bytes, e.g. a torch tensor that the caller
+ * all-reduces) for the per-depth removal flags instead of the handle's own; NULL = own.   */
+int pcg_set_removal_buffer(pcg_handle *h, uint8_t *rm_dev, int64_t bytes);
 
 /* ---- K4: PageRank head -------------------------------------------------------------
  * Replaces scikit-network 0.31.0 PageRank(damping_factor, solver='piteration', n_iter,

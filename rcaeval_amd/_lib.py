@@ -82,6 +82,7 @@ SIGNATURES = [
     ("pcg_degrees", I32, [P, P, I64]),
     ("pcg_sepset_count", I32, [P, ctypes.POINTER(I64), ctypes.POINTER(I32)]),
     ("pcg_sepset_export", I32, [P, P, P, I64]),
+    ("pcg_sepset_export_device", I32, [P, P, P, I64]),
     ("pcg_record_count", I32, [P, ctypes.POINTER(I64), ctypes.POINTER(I64)]),
     ("pcg_record_export", I32, [P, P, I64, P, I64]),
     ("pcg_skeleton_init", I32, [P, P, I64, I64, I64, D, ctypes.c_int, P]),
@@ -89,6 +90,7 @@ SIGNATURES = [
     ("pcg_level_run", I32, [P, I64, I64]),
     ("pcg_level_end", I32, [P, ctypes.POINTER(PcgStats)]),
     ("pcg_level_chunk_work", I32, [P, P, I64]),
+    ("pcg_set_removal_buffer", I32, [P, P, I64]),
     ("pcg_pagerank_dense", I32, [P, P, I64, I64, D, ctypes.c_int, D, P]),
     ("pcg_pagerank_csr", I32, [P, P, P, P, I64, I64, D, ctypes.c_int, D, P]),
     ("pcg_random_walk", I32, [P, P, I64, I64, I64, I64, ctypes.c_uint64, ctypes.c_uint64,

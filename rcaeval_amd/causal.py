@@ -87,7 +87,8 @@ class SepsetArray:
                     b = (v & -v).bit_length() - 1
                     members.append(w * 64 + b)
                     v &= v - 1
-            self._rows[(x, y)] = members
+            prev = self._rows.get((x, y))          # several rows per pair when edge-sharded: OR
+            self._rows[(x, y)] = sorted(set(prev) | set(members)) if prev else members
 
     def _side(self, x: int, y: int) -> tuple:
         mem = self._rows.get((x, y))

@@ -43,6 +43,8 @@ struct pcg_handle {
     DevBuf adj, deg, off, nbr, rm, ug, cpre, binom, ctr, deferred, records, nearbuf, exportbuf,
         export_xy, diag, colmean, pr_scratch;
     std::vector<uint64_t> binom_h;   // host copy of the binomial table
+    uint8_t *rm_ext = nullptr;       // caller-owned removal-flag buffer (multi-GPU)
+    int64_t rm_ext_bytes = 0;
     int64_t rec_cap = 0, def_cap = 1 << 16, near_cap = 1 << 16;
     int64_t export_cap = 0;          // rows
     int64_t export_rows = 0;         // rows exported so far (host mirror)

@@ -561,99 +561,214 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
     const uint64_t r1 = min(nS, r0 + (uint64_t)bs * (uint64_t)a.spl);
     unsigned long long tests = 0, indep = 0;
 
-    for (uint64_t rank = r0 + tid; rank < r1; rank += bs) {
+    if constexpr (MODE == MODE_DECIDE && DM <= 4) {
+        // Each lane walks a contiguous run of spl colex ranks with the colex successor
+        // (no per-S unranking), factors M_SS once per S and sweeps y barrier-free.
+        const uint64_t q0 = r0 + (uint64_t)tid * (uint64_t)a.spl;
+        const uint64_t q1 = min(r1, q0 + (uint64_t)a.spl);
         int k[DM];
 #pragma unroll
-        for (int i = 0; i < DM; ++i) k[i] = 0;
-        pcg_unrank_colex<DM>(rank, d, D, a.binom, k);
-        unsigned long long Smask = 0;
+        for (int i = 0; i < DM; ++i) k[i] = i;
+        if (q0 < q1) pcg_unrank_colex<DM>(q0, d, D, a.binom, k);
+        for (uint64_t rank = q0; rank < q1; ++rank) {
+            if (rank > q0) {  // colex successor: bump the lowest k[i] that can grow, reset below
+                int i = 0;
 #pragma unroll
-        for (int i = 0; i < DM; ++i)
-            if (i < d) Smask |= 1ull << k[i];
-        // Cholesky of M_SS, u = L^-1 M_Sx
-        double L[DM][DM], rinv[DM], u[DM];
-        bool ok = true;
+                for (int j = 0; j < DM - 1; ++j)
+                    if (i == j && k[j] + 1 == k[j + 1]) i = j + 1;
 #pragma unroll
-        for (int j = 0; j < DM; ++j) {
-            if (j < d) {
-                double s = M[k[j] * D + k[j]];
-#pragma unroll
-                for (int q = 0; q < DM; ++q)
-                    if (q < j) s -= L[j][q] * L[j][q];
-                ok = ok && (s > 0.0);
-                const double ljj = sqrt(s);
-                rinv[j] = 1.0 / ljj;
-                L[j][j] = ljj;
-#pragma unroll
-                for (int i = 0; i < DM; ++i) {
-                    if (i > j && i < d) {
-                        double t = M[k[i] * D + k[j]];
-#pragma unroll
-                        for (int q = 0; q < DM; ++q)
-                            if (q < j) t -= L[i][q] * L[j][q];
-                        L[i][j] = t * rinv[j];
-                    }
+                for (int j = 0; j < DM; ++j) {
+                    if (j == i) k[j] += 1;
+                    else if (j < i) k[j] = j;
                 }
             }
-        }
-        double uu = 0.0;
+            unsigned long long Smask = 0;
 #pragma unroll
-        for (int i = 0; i < DM; ++i) {
-            if (i < d) {
-                double t = Mx[k[i]];
+            for (int i = 0; i < DM; ++i) Smask |= 1ull << k[i];
+            // L = chol(M_SS); Li = L^-1 (lower); u = Li M_Sx; w = Li^T u (so u.v = w.b)
+            double L[DM][DM], Li[DM][DM], u[DM], w[DM], b[DM];
+            bool ok = true;
 #pragma unroll
-                for (int q = 0; q < DM; ++q)
-                    if (q < i) t -= L[i][q] * u[q];
-                u[i] = t * rinv[i];
-                uu += u[i] * u[i];
+            for (int j = 0; j < DM; ++j) {
+                double sdiag = M[k[j] * D + k[j]];
+#pragma unroll
+                for (int q = 0; q < j; ++q) sdiag -= L[j][q] * L[j][q];
+                ok = ok && (sdiag > 0.0);
+                L[j][j] = sqrt(sdiag);
+                const double r = 1.0 / L[j][j];
+#pragma unroll
+                for (int i = j + 1; i < DM; ++i) {
+                    double t = M[k[i] * D + k[j]];
+#pragma unroll
+                    for (int q = 0; q < j; ++q) t -= L[i][q] * L[j][q];
+                    L[i][j] = t * r;
+                }
+                Li[j][j] = r;
             }
-        }
-        const double cxx = Cxx - uu;
-        ok = ok && (cxx == cxx);
-
-        for (int t = 0; t < D; ++t) {
-            if ((Smask >> t) & 1ull) continue;
-            const unsigned long long lm = lmask[t];
-            const bool in_y = (lm & Smask) == Smask;
-            if (t < tx && in_y) continue;          // node nbr[t] < x owns this test (memo)
-            ++tests;
-            int dec = 2;
-            double p = 0.0;
-            if (ok) {
+#pragma unroll
+            for (int i = 1; i < DM; ++i)
+#pragma unroll
+                for (int j = 0; j < i; ++j) {
+                    double t = 0.0;
+#pragma unroll
+                    for (int q = j; q < i; ++q) t += L[i][q] * Li[q][j];
+                    Li[i][j] = -t * Li[i][i];
+                }
+            double uu = 0.0;
+#pragma unroll
+            for (int i = 0; i < DM; ++i) b[i] = Mx[k[i]];
+#pragma unroll
+            for (int i = 0; i < DM; ++i) {
+                double t = 0.0;
+#pragma unroll
+                for (int j = 0; j <= i; ++j) t += Li[i][j] * b[j];
+                u[i] = t;
+                uu += t * t;
+            }
+#pragma unroll
+            for (int j = 0; j < DM; ++j) {
+                double t = 0.0;
+#pragma unroll
+                for (int i = j; i < DM; ++i) t += Li[i][j] * u[i];
+                w[j] = t;
+            }
+            const double cxx = Cxx - uu;
+            ok = ok && (cxx > 0.0);
+            const double hc = a.hi2 * cxx, lc = a.lo2 * cxx, rc = a.rmax2 * cxx;
+            for (int t = 0; t < D; ++t) {
                 const double *Mt = M + t * D;
-                double vv = 0.0, uv = 0.0, v[DM];
+#pragma unroll
+                for (int i = 0; i < DM; ++i) b[i] = Mt[k[i]];
+                double vv = 0.0, wb = 0.0;
 #pragma unroll
                 for (int i = 0; i < DM; ++i) {
-                    if (i < d) {
-                        double tt = Mt[k[i]];
+                    double v = 0.0;
 #pragma unroll
-                        for (int q = 0; q < DM; ++q)
-                            if (q < i) tt -= L[i][q] * v[q];
-                        v[i] = tt * rinv[i];
-                        vv += v[i] * v[i];
-                        uv += u[i] * v[i];
+                    for (int j = 0; j <= i; ++j) v += Li[i][j] * b[j];
+                    vv += v * v;
+                    wb += w[i] * b[i];
+                }
+                const double cxy = Mx[t] - wb;
+                const double cyy = Md[t] - vv;
+                const double num = cxy * cxy;
+                const bool dep = (num > hc * cyy) && (num < rc * cyy);
+                const unsigned long long lm = lmask[t];
+                const bool in_y = (lm & Smask) == Smask;
+                const bool live = !((Smask >> t) & 1ull) && !(t < tx && in_y);
+                tests += live;
+                const bool rare = live && !(ok && dep);
+                if (__ballot(rare)) {
+                    if (rare) {
+                        const bool ind = ok && (num < lc * cyy) && (cyy > 0.0);
+                        if (ind) {
+                            ++indep;
+                            atomicOr(&uself[t], Smask);
+                            if (in_y && t >= tx) atomicOr(&uprop[t], Smask);
+                        } else {
+                            int sg[DM];
+#pragma unroll
+                            for (int i = 0; i < DM; ++i) sg[i] = nxs[k[i]];
+                            push_deferred(a, x, nxs[t], sg, d);
+                        }
                     }
                 }
-                dec = decide<MODE>(a, Mx[t] - uv, cxx, Md[t] - vv, &p);
             }
-            if (dec == 2 || (MODE == MODE_FULLP && (a.record || fabs(p - a.alpha) < 1e-9))) {
-                int sg[DM];
-#pragma unroll
-                for (int i = 0; i < DM; ++i) sg[i] = i < d ? nxs[k[i]] : 0;
-                const int yg = nxs[t];
-                if (dec == 2) {
-                    push_deferred(a, x, yg, sg, d);
-                    continue;
+        }
+    } else {
+        for (uint64_t rank = r0 + tid; rank < r1; rank += bs) {
+            int k[DM];
+    #pragma unroll
+            for (int i = 0; i < DM; ++i) k[i] = 0;
+            pcg_unrank_colex<DM>(rank, d, D, a.binom, k);
+            unsigned long long Smask = 0;
+    #pragma unroll
+            for (int i = 0; i < DM; ++i)
+                if (i < d) Smask |= 1ull << k[i];
+            // Cholesky of M_SS, u = L^-1 M_Sx
+            double L[DM][DM], rinv[DM], u[DM];
+            bool ok = true;
+    #pragma unroll
+            for (int j = 0; j < DM; ++j) {
+                if (j < d) {
+                    double s = M[k[j] * D + k[j]];
+    #pragma unroll
+                    for (int q = 0; q < DM; ++q)
+                        if (q < j) s -= L[j][q] * L[j][q];
+                    ok = ok && (s > 0.0);
+                    const double ljj = sqrt(s);
+                    rinv[j] = 1.0 / ljj;
+                    L[j][j] = ljj;
+    #pragma unroll
+                    for (int i = 0; i < DM; ++i) {
+                        if (i > j && i < d) {
+                            double t = M[k[i] * D + k[j]];
+    #pragma unroll
+                            for (int q = 0; q < DM; ++q)
+                                if (q < j) t -= L[i][q] * L[j][q];
+                            L[i][j] = t * rinv[j];
+                        }
+                    }
                 }
-                const int lo_ = x < yg ? x : yg, hi_ = x < yg ? yg : x;
-                if (a.record) push_record(a.records, a.rec_cap, &a.ctr->records, lo_, hi_, d, sg, p);
-                if (fabs(p - a.alpha) < 1e-9)
-                    push_record(a.nearl, a.near_cap, &a.ctr->near_alpha, lo_, hi_, d, sg, p);
             }
-            if (dec == 1) {
-                ++indep;
-                atomicOr(&uself[t], Smask);
-                if (in_y && t >= tx) atomicOr(&uprop[t], Smask);
+            double uu = 0.0;
+    #pragma unroll
+            for (int i = 0; i < DM; ++i) {
+                if (i < d) {
+                    double t = Mx[k[i]];
+    #pragma unroll
+                    for (int q = 0; q < DM; ++q)
+                        if (q < i) t -= L[i][q] * u[q];
+                    u[i] = t * rinv[i];
+                    uu += u[i] * u[i];
+                }
+            }
+            const double cxx = Cxx - uu;
+            ok = ok && (cxx == cxx);
+
+            for (int t = 0; t < D; ++t) {
+                if ((Smask >> t) & 1ull) continue;
+                const unsigned long long lm = lmask[t];
+                const bool in_y = (lm & Smask) == Smask;
+                if (t < tx && in_y) continue;          // node nbr[t] < x owns this test (memo)
+                ++tests;
+                int dec = 2;
+                double p = 0.0;
+                if (ok) {
+                    const double *Mt = M + t * D;
+                    double vv = 0.0, uv = 0.0, v[DM];
+    #pragma unroll
+                    for (int i = 0; i < DM; ++i) {
+                        if (i < d) {
+                            double tt = Mt[k[i]];
+    #pragma unroll
+                            for (int q = 0; q < DM; ++q)
+                                if (q < i) tt -= L[i][q] * v[q];
+                            v[i] = tt * rinv[i];
+                            vv += v[i] * v[i];
+                            uv += u[i] * v[i];
+                        }
+                    }
+                    dec = decide<MODE>(a, Mx[t] - uv, cxx, Md[t] - vv, &p);
+                }
+                if (dec == 2 || (MODE == MODE_FULLP && (a.record || fabs(p - a.alpha) < 1e-9))) {
+                    int sg[DM];
+    #pragma unroll
+                    for (int i = 0; i < DM; ++i) sg[i] = i < d ? nxs[k[i]] : 0;
+                    const int yg = nxs[t];
+                    if (dec == 2) {
+                        push_deferred(a, x, yg, sg, d);
+                        continue;
+                    }
+                    const int lo_ = x < yg ? x : yg, hi_ = x < yg ? yg : x;
+                    if (a.record) push_record(a.records, a.rec_cap, &a.ctr->records, lo_, hi_, d, sg, p);
+                    if (fabs(p - a.alpha) < 1e-9)
+                        push_record(a.nearl, a.near_cap, &a.ctr->near_alpha, lo_, hi_, d, sg, p);
+                }
+                if (dec == 1) {
+                    ++indep;
+                    atomicOr(&uself[t], Smask);
+                    if (in_y && t >= tx) atomicOr(&uprop[t], Smask);
+                }
             }
         }
     }
@@ -811,7 +926,7 @@ LevelArgs make_args(pcg_handle *h, int d, int mode_exact_all) {
     a.nbr = (const int32_t *)h->nbr.p;
     a.cpre = (const int64_t *)h->cpre.p;
     a.binom = (const uint64_t *)h->binom.p;
-    a.rm = (uint8_t *)h->rm.p;
+    a.rm = h->rm_ext ? h->rm_ext : (uint8_t *)h->rm.p;
     a.ug = (uint64_t *)h->ug.p;
     a.ctr = (DevCounters *)h->ctr.p;
     a.deferred = (DeferredEntry *)h->deferred.p;
@@ -921,6 +1036,9 @@ extern "C" int pcg_skeleton_init(pcg_handle *h, const double *C, int64_t n, int6
         return pcg_fail(h, PCG_ERR_INVALID, "pcg_skeleton_init: invalid arguments (n=%lld)", (long long)n);
     if (n > INT32_MAX / 2) return pcg_fail(h, PCG_ERR_INVALID, "n too large");
     PCG_HIP(h, hipSetDevice(h->device));
+    if (h->rm_ext && h->rm_ext_bytes < n * n)
+        return pcg_fail(h, PCG_ERR_INVALID, "removal buffer too small (%lld < %lld)", (long long)h->rm_ext_bytes,
+                        (long long)(n * n));
     h->C = C; h->n = n; h->ldc = ldc; h->N = N; h->alpha = alpha; h->flags = flags;
     h->rl = removed_level;
     h->W = (int)((n + 63) / 64);
@@ -959,7 +1077,7 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
                                uint8_t **rm_dev) {
     if (!h || depth != h->depth + 1) return pcg_fail(h, PCG_ERR_INVALID, "pcg_level_begin: depth order");
     if (max_degree) *max_degree = h->maxdeg;
-    if (rm_dev) *rm_dev = (uint8_t *)h->rm.p;
+    if (rm_dev) *rm_dev = h->rm_ext ? h->rm_ext : (uint8_t *)h->rm.p;
     // reference loop condition: while max_degree() - 1 > depth_prev
     if (!(h->maxdeg - 1 > depth - 1)) {
         if (total_chunks) *total_chunks = 0;
@@ -1032,7 +1150,7 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
     if (!pcg_ensure(h, h->cpre, sizeof(int64_t) * 2 * (n + 1))) return PCG_ERR_OOM;
     PCG_HIP(h, hipMemcpyAsync(h->cpre.p, h->cpre_h.data(), sizeof(int64_t) * 2 * (n + 1), hipMemcpyHostToDevice,
                               h->stream));
-    PCG_HIP(h, hipMemsetAsync(h->rm.p, 0, (size_t)n * n, h->stream));
+    PCG_HIP(h, hipMemsetAsync(h->rm_ext ? (void *)h->rm_ext : h->rm.p, 0, (size_t)n * n, h->stream));
     PCG_HIP(h, hipMemsetAsync(h->ctr.p, 0, sizeof(DevCounters), h->stream));
     if (depth >= 1) {
         const size_t ugb = sizeof(uint64_t) * (size_t)std::max<int64_t>(h->sumdeg, 1) * h->W;
@@ -1062,6 +1180,13 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
             h->export_cap = ncap;
         }
     }
+    return PCG_OK;
+}
+
+extern "C" int pcg_set_removal_buffer(pcg_handle *h, uint8_t *rm_dev, int64_t bytes) {
+    if (!h) return PCG_ERR_INVALID;
+    h->rm_ext = rm_dev;
+    h->rm_ext_bytes = rm_dev ? bytes : 0;
     return PCG_OK;
 }
 
@@ -1211,7 +1336,8 @@ extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
         PCG_HIP(h, hipMemsetAsync(&((DevCounters *)h->ctr.p)->exported, 0, sizeof(unsigned long long), h->stream));
         const int64_t room = h->export_cap - h->export_rows;
         hipLaunchKernelGGL(k_export, dim3((unsigned)((h->sumdeg + 255) / 256)), dim3(256), 0, h->stream,
-                           (const int32_t *)h->off.p, (const int32_t *)h->nbr.p, (const uint8_t *)h->rm.p,
+                           (const int32_t *)h->off.p, (const int32_t *)h->nbr.p,
+                           h->rm_ext ? (const uint8_t *)h->rm_ext : (const uint8_t *)h->rm.p,
                            (const uint64_t *)h->ug.p, n, W, h->sumdeg,
                            (int32_t *)h->export_xy.p + 2 * h->export_rows,
                            (uint64_t *)h->exportbuf.p + h->export_rows * W, room,
@@ -1225,7 +1351,8 @@ extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
     }
     const int64_t nw = (int64_t)n * W;
     hipLaunchKernelGGL(k_apply, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, h->stream,
-                       (const uint8_t *)h->rm.p, (uint64_t *)h->adj.p, h->rl, n, W, d);
+                       h->rm_ext ? (const uint8_t *)h->rm_ext : (const uint8_t *)h->rm.p, (uint64_t *)h->adj.p,
+                       h->rl, n, W, d);
     PCG_HIP(h, hipGetLastError());
     int rc = refresh_graph(h);
     if (rc) return rc;
@@ -1279,6 +1406,16 @@ extern "C" int pcg_sepset_export(pcg_handle *h, int32_t *xy_host, uint64_t *bits
     if (count == 0) return PCG_OK;
     PCG_HIP(h, hipMemcpy(xy_host, h->export_xy.p, sizeof(int32_t) * 2 * count, hipMemcpyDeviceToHost));
     PCG_HIP(h, hipMemcpy(bits_host, h->exportbuf.p, sizeof(uint64_t) * count * h->W, hipMemcpyDeviceToHost));
+    return PCG_OK;
+}
+
+extern "C" int pcg_sepset_export_device(pcg_handle *h, int32_t *xy_dev, uint64_t *bits_dev, int64_t count) {
+    if (!h || count > h->export_rows) return pcg_fail(h, PCG_ERR_INVALID, "pcg_sepset_export_device: count");
+    if (count == 0) return PCG_OK;
+    PCG_HIP(h, hipMemcpyAsync(xy_dev, h->export_xy.p, sizeof(int32_t) * 2 * count, hipMemcpyDeviceToDevice,
+                              h->stream));
+    PCG_HIP(h, hipMemcpyAsync(bits_dev, h->exportbuf.p, sizeof(uint64_t) * count * h->W,
+                              hipMemcpyDeviceToDevice, h->stream));
     return PCG_OK;
 }
 

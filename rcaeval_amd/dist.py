@@ -1,0 +1,162 @@
+"""Edge-sharded stable-PC skeleton across GPUs (one process per GPU, RCCL over xGMI).
+
+Within one depth every (edge, S) test is independent — removals are deferred to the level
+barrier (``SkeletonDiscovery.py:141-144``) — so each rank evaluates an owner-disjoint,
+work-balanced slice of the depth's chunk list (a chunk = one node x and a run of S ranks;
+every test of a chunk, including both sepset sides, is evaluated by its owner). The only
+exchange is the removal flags: one ``all_reduce(MAX)`` of an n*n uint8 buffer per depth
+(RCCL has no bitwise OR; MAX over 0/1 bytes is the same merge). Every rank then applies the
+identical removals, so adjacency, degrees and the next depth's work list agree everywhere.
+Sepset-union rows stay on their owner until the end, then are all-gathered once.
+
+``LevelBackend`` abstracts one rank's device work so the protocol can be exercised on the
+CPU with ``gloo`` (tests/test_dist_cpu.py injects an oracle-backed backend).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import PcgStats, check
+
+
+def split_by_work(prefix: np.ndarray, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous chunk range of ``rank`` so that every rank gets ~1/world of the work.
+
+    ``prefix`` has total_chunks + 1 entries (prefix[0] = 0, non-decreasing).
+    Ranges of consecutive ranks tile [0, total_chunks) exactly.
+    """
+    total = len(prefix) - 1
+    if total <= 0:
+        return 0, 0
+    W = float(prefix[-1])
+
+    def cut(r: int) -> int:
+        if r <= 0:
+            return 0
+        if r >= world:
+            return total
+        return int(np.searchsorted(prefix, W * r / world, side="left"))
+
+    lo, hi = cut(rank), cut(rank + 1)
+    return min(lo, total), min(max(hi, lo), total)
+
+
+class GpuLevelBackend:
+    """One rank's device work through the C ABI (pcg_skeleton_init / pcg_level_*)."""
+
+    def __init__(self, eng, C, N: int, alpha: float, flags: int):
+        import torch
+        self.eng, self.lib, self.h = eng, eng.lib, eng.h
+        Cd = eng.to_device(C)
+        self.C = Cd
+        n = Cd.shape[0]
+        self.n = n
+        self.rl = torch.empty((n, n), dtype=torch.int8, device=eng.device)
+        self.rm = torch.zeros(n * n, dtype=torch.uint8, device=eng.device)
+        check(self.h, self.lib.pcg_set_removal_buffer(self.h, ctypes.c_void_p(self.rm.data_ptr()), n * n),
+              "pcg_set_removal_buffer")
+        check(self.h, self.lib.pcg_skeleton_init(self.h, ctypes.c_void_p(Cd.data_ptr()), n, n, int(N),
+                                                 float(alpha), int(flags), ctypes.c_void_p(self.rl.data_ptr())),
+              "pcg_skeleton_init")
+        self.stats = PcgStats()
+
+    def begin(self, depth: int):
+        total, maxdeg, rmp = ctypes.c_int64(), ctypes.c_int32(), ctypes.c_void_p()
+        rc = self.lib.pcg_level_begin(self.h, depth, ctypes.byref(total), ctypes.byref(maxdeg), ctypes.byref(rmp))
+        if rc == 1:
+            return None
+        check(self.h, rc, "pcg_level_begin")
+        prefix = np.zeros(total.value + 1, np.int64)
+        check(self.h, self.lib.pcg_level_chunk_work(self.h, prefix.ctypes.data_as(ctypes.c_void_p), len(prefix)),
+              "pcg_level_chunk_work")
+        return prefix
+
+    def run(self, lo: int, hi: int):
+        check(self.h, self.lib.pcg_level_run(self.h, int(lo), int(hi)), "pcg_level_run")
+
+    def removal_tensor(self):
+        return self.rm
+
+    def end(self):
+        check(self.h, self.lib.pcg_level_end(self.h, ctypes.byref(self.stats)), "pcg_level_end")
+
+    def finish(self):
+        self.lib.pcg_set_removal_buffer(self.h, None, 0)
+        return self.eng._collect(self.n, self.rl, self.stats, 0.0)
+
+
+def run_sharded_levels(backend, rank: int, world: int, max_depth: int = -1, group=None):
+    """The level loop shared by the GPU path and the CPU protocol test."""
+    import torch.distributed as dist
+    depth = 0
+    while True:
+        if max_depth >= 0 and depth > max_depth:
+            break
+        prefix = backend.begin(depth)
+        if prefix is None:
+            break
+        lo, hi = split_by_work(prefix, rank, world)
+        backend.run(lo, hi)
+        dist.all_reduce(backend.removal_tensor(), op=dist.ReduceOp.MAX, group=group)
+        backend.end()
+        depth += 1
+    return depth
+
+
+def _allgather_rows(xy, bits, group=None):
+    """All-gather variable-length (xy, bits) device tensors from every rank."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    cnt = torch.tensor([xy.shape[0]], dtype=torch.int64, device=xy.device)
+    counts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(counts, cnt, group=group)
+    counts = [int(c.item()) for c in counts]
+    mx = max(max(counts), 1)
+    W = bits.shape[1]
+    pad_xy = torch.zeros((mx, 2), dtype=xy.dtype, device=xy.device)
+    pad_bits = torch.zeros((mx, W), dtype=bits.dtype, device=bits.device)
+    pad_xy[: xy.shape[0]] = xy
+    pad_bits[: bits.shape[0]] = bits
+    all_xy = [torch.empty_like(pad_xy) for _ in range(world)]
+    all_bits = [torch.empty_like(pad_bits) for _ in range(world)]
+    dist.all_gather(all_xy, pad_xy, group=group)
+    dist.all_gather(all_bits, pad_bits, group=group)
+    xy_out = torch.cat([t[:c] for t, c in zip(all_xy, counts)])
+    bits_out = torch.cat([t[:c] for t, c in zip(all_bits, counts)])
+    return xy_out, bits_out
+
+
+def _allreduce_stats(stats: dict, device, group=None) -> dict:
+    import torch
+    import torch.distributed as dist
+    keys = ("tests", "indep", "exact", "near_alpha")
+    L = stats["levels"]
+    t = torch.tensor([stats[k][i] for k in keys for i in range(L)], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    vals = t.cpu().numpy().reshape(len(keys), L) if L else np.zeros((len(keys), 0), np.int64)
+    out = dict(stats)
+    for i, k in enumerate(keys):
+        out[k] = [int(v) for v in vals[i]]
+    return out
+
+
+def sharded_skeleton(eng, C, N: int, alpha: float = 0.05, max_depth: int = -1, flags: int = 0, group=None):
+    """Edge-sharded skeleton over the ranks of ``group``; every rank returns the full result."""
+    import torch.distributed as dist
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    backend = GpuLevelBackend(eng, C, N, alpha, flags)
+    run_sharded_levels(backend, rank, world, max_depth=max_depth, group=group)
+    out = backend.finish()
+    xy, bits = _allgather_rows(out.sep_xy_dev, out.sep_bits_dev, group=group)
+    out.sep_xy_dev, out.sep_bits_dev = xy, bits
+    out._host.clear()
+    out.stats = _allreduce_stats(out.stats, eng.device, group=group)
+    return out
+
+
+__all__ = ["split_by_work", "run_sharded_levels", "sharded_skeleton", "GpuLevelBackend"]
+_ = _lib

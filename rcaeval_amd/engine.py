@@ -7,7 +7,7 @@ arithmetic runs in the HIP kernels of ``libpcgpu.so``.
 from __future__ import annotations
 
 import ctypes
-from dataclasses import dataclass, field
+import time
 
 import numpy as np
 
@@ -26,19 +26,44 @@ def _torch():
     return torch
 
 
-@dataclass
 class SkeletonOut:
-    """Result of one device skeleton run (host copies)."""
-    n: int
-    removed_level: np.ndarray          # n x n int8, -1 = edge survives
-    deg_levels: np.ndarray             # levels x n int32, degrees at the start of each depth
-    sep_xy: np.ndarray                 # R x 2 int32, ordered removed pairs with a non-empty union
-    sep_bits: np.ndarray               # R x W uint64, x-side union (global node bits)
-    stats: dict
-    records: np.ndarray | None = None  # RECORD_DTYPE (PCG_FLAG_RECORD)
-    near_alpha: np.ndarray | None = None
-    device_ms: float = 0.0
-    extra: dict = field(default_factory=dict)
+    """Result of one device skeleton run.
+
+    The skeleton stays resident in HBM (``removed_level_dev``, ``sep_xy_dev``,
+    ``sep_bits_dev`` torch tensors); the numpy views (``removed_level``, ``sep_xy``,
+    ``sep_bits``) are copied to the host on first access.
+    """
+
+    def __init__(self, n, rl_dev, xy_dev, bits_dev, deg_levels, stats, records=None, near_alpha=None,
+                 device_ms=0.0):
+        self.n = n
+        self.removed_level_dev = rl_dev
+        self.sep_xy_dev = xy_dev
+        self.sep_bits_dev = bits_dev
+        self.deg_levels = deg_levels          # levels x n int32 (host)
+        self.stats = stats
+        self.records = records                # RECORD_DTYPE (PCG_FLAG_RECORD)
+        self.near_alpha = near_alpha
+        self.device_ms = device_ms
+        self.extra: dict = {}
+        self._host: dict = {}
+
+    def _h(self, key, t):
+        if key not in self._host:
+            self._host[key] = t.cpu().numpy()
+        return self._host[key]
+
+    @property
+    def removed_level(self) -> np.ndarray:      # n x n int8, -1 = edge survives
+        return self._h("rl", self.removed_level_dev)
+
+    @property
+    def sep_xy(self) -> np.ndarray:             # R x 2 int32, ordered removed pairs, non-empty union
+        return self._h("xy", self.sep_xy_dev)
+
+    @property
+    def sep_bits(self) -> np.ndarray:           # R x W uint64, x-side union (global node bits)
+        return self._h("bits", self.sep_bits_dev).view(np.uint64)
 
     @property
     def levels(self) -> int:
@@ -121,7 +146,11 @@ class Engine:
         ev1.record()
         check(self.h, rc, "pcg_skeleton")
         self.sync()
-        return self._collect(n, rl, st, ev0.elapsed_time(ev1))
+        t0 = time.perf_counter()
+        out = self._collect(n, rl, st, ev0.elapsed_time(ev1))
+        out.extra["collect_ms"] = 1000.0 * (time.perf_counter() - t0)
+        out.extra["device_ms"] = out.device_ms
+        return out
 
     def _collect(self, n: int, rl, st: PcgStats, device_ms: float) -> SkeletonOut:
         L = st.levels
@@ -129,14 +158,15 @@ class Engine:
         if L:
             check(self.h, self.lib.pcg_degrees(self.h, deg.ctypes.data_as(ctypes.c_void_p), deg.size),
                   "pcg_degrees")
+        torch = _torch()
         cnt, W = ctypes.c_int64(), ctypes.c_int32()
         check(self.h, self.lib.pcg_sepset_count(self.h, ctypes.byref(cnt), ctypes.byref(W)), "pcg_sepset_count")
-        xy = np.zeros((cnt.value, 2), np.int32)
-        bits = np.zeros((cnt.value, W.value), np.uint64)
+        xy = torch.empty((cnt.value, 2), dtype=torch.int32, device=self.device)
+        bits = torch.empty((cnt.value, W.value), dtype=torch.int64, device=self.device)
         if cnt.value:
-            check(self.h, self.lib.pcg_sepset_export(self.h, xy.ctypes.data_as(ctypes.c_void_p),
-                                                     bits.ctypes.data_as(ctypes.c_void_p), cnt.value),
-                  "pcg_sepset_export")
+            check(self.h, self.lib.pcg_sepset_export_device(self.h, ctypes.c_void_p(xy.data_ptr()),
+                                                            ctypes.c_void_p(bits.data_ptr()), cnt.value),
+                  "pcg_sepset_export_device")
         rc_, nc_ = ctypes.c_int64(), ctypes.c_int64()
         check(self.h, self.lib.pcg_record_count(self.h, ctypes.byref(rc_), ctypes.byref(nc_)), "pcg_record_count")
         rec = np.zeros(rc_.value, RECORD_DTYPE)
@@ -145,8 +175,8 @@ class Engine:
             check(self.h, self.lib.pcg_record_export(self.h, rec.ctypes.data_as(ctypes.c_void_p), rc_.value,
                                                      near.ctypes.data_as(ctypes.c_void_p), nc_.value),
                   "pcg_record_export")
-        return SkeletonOut(n=n, removed_level=rl.cpu().numpy(), deg_levels=deg[:L], sep_xy=xy, sep_bits=bits,
-                           stats=st.as_dict(), records=rec, near_alpha=near, device_ms=device_ms)
+        self.sync()
+        return SkeletonOut(n, rl, xy, bits, deg[:L].copy(), st.as_dict(), rec, near, device_ms)
 
     # ------------------------------------------------------------------ K4
     def pagerank_dense(self, A, damping: float = 0.85, n_iter: int = 10, tol: float = 1e-6) -> np.ndarray:

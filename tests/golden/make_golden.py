@@ -1,0 +1,176 @@
+"""Generate the committed golden fixtures (run in the build container, where /root/reference exists).
+
+  python tests/golden/make_golden.py
+
+Fixtures (data only — inputs and expected outputs):
+  random_walk.json  outputs of the REFERENCE ``RCAEval.graph_heads.random_walk.random_walk``
+                    (imported from /root/reference) on endpoint matrices / names / num_loop.
+  preprocess.npz    outputs of the REFERENCE ``RCAEval.io.time_series.preprocess`` on synthetic
+                    telemetry frames (columns kept + values).
+  fisherz.npz       Fisher-z p-values from causal-learn's [U] expression evaluated with the
+                    pinned libraries' own calls (np.corrcoef, np.linalg.inv, math.log,
+                    scipy.stats.norm.cdf) — oracle/fisherz.py — for every (x, y, S), |S| <= 3,
+                    on a 12-variable x 500-sample SEM.
+  orient.npz        skeleton + sepset-union + oriented graph from the Python orientation oracle
+                    (oracle/orient.py) on small SEMs — pins pcg_orient across rounds.
+  pagerank.npz      scikit-network-0.31.0-restated PageRank (oracle/pagerank.py, scipy CSR + numpy
+                    sums) on random 0/1 graphs — pins the GPU kernel bitwise.
+The reference code itself is never copied here; only its outputs are stored.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+from itertools import combinations
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, ROOT)
+
+
+def endpoint_cases():
+    from oracle import orient as oor
+    from oracle import skeleton as osk
+    from rcaeval_amd import synth
+    cases = []
+    for seed, (n, N, ep) in enumerate([(10, 500, 0.3), (38, 600, 0.08), (46, 600, 0.06), (49, 600, 0.06),
+                                       (50, 2000, 0.05), (12, 300, 0.4)]):
+        X = synth.gaussian_sem(n, N, seed=100 + seed, w_low=0.3, w_high=0.9, edge_prob=ep)
+        C = np.corrcoef(X.T)
+        r = osk.skeleton_discovery(C, N, max_depth=3)
+        g = oor.orient(r.adj, r.sepset)
+        cases.append((g, [f"svc{i // 3}_{['cpu', 'mem', 'latency'][i % 3]}" for i in range(n)]))
+    # an empty graph and a fully undirected one
+    cases.append((np.zeros((5, 5), int), [f"m{i}" for i in range(5)]))
+    u = -np.ones((6, 6), int)
+    np.fill_diagonal(u, 0)
+    cases.append((u, [f"u{i}" for i in range(6)]))
+    return cases
+
+
+def make_random_walk():
+    sys.path.insert(0, REF)
+    from RCAEval.graph_heads.random_walk import random_walk  # reference, imported (not copied)
+    out = []
+    for adj, names in endpoint_cases():
+        for num_loop in (None, len(names), 3 * len(names) + 1):
+            np.random.seed(1234)
+            res = random_walk(adj, names, num_loop=num_loop)
+            out.append({"adj": adj.tolist(), "names": names, "num_loop": num_loop,
+                        "ranks": [r[0] for r in res], "scores": [float(r[1]) for r in res]})
+    with open(os.path.join(HERE, "random_walk.json"), "w") as f:
+        json.dump(out, f)
+    print("random_walk.json", len(out))
+
+
+def telemetry_frames():
+    from rcaeval_amd import synth
+    frames = []
+    for seed, (m, rows) in enumerate([(12, 50), (30, 120), (49, 200)]):
+        df = synth.telemetry_frame(m, rows, n_constant=3, seed=seed)
+        df["frontend-external_cpu"] = np.linspace(0, 1, rows)
+        df["main_lat50"] = np.random.default_rng(seed).random(rows)
+        df["svc_x_lat50"] = np.random.default_rng(seed + 1).random(rows) * 10
+        df["time.1"] = df["time"]
+        frames.append(df)
+    return frames
+
+
+def make_preprocess():
+    sys.path.insert(0, REF)
+    from RCAEval.io.time_series import preprocess  # reference, imported (not copied)
+    arrays = {}
+    meta = []
+    for i, df in enumerate(telemetry_frames()):
+        arrays[f"in{i}_values"] = df.to_numpy(dtype=float)
+        arrays[f"in{i}_cols"] = np.array(df.columns.to_list())
+        for dataset in (None, "online-boutique", "causalrca-sock-shop"):
+            for dk in (False, True):
+                out = preprocess(data=df.copy(), dataset=dataset, dk_select_useful=dk)
+                key = f"{i}_{dataset}_{dk}"
+                arrays[f"out{key}_values"] = out.to_numpy(dtype=float)
+                arrays[f"out{key}_cols"] = np.array(out.columns.to_list())
+                meta.append(key)
+    arrays["keys"] = np.array(meta)
+    np.savez_compressed(os.path.join(HERE, "preprocess.npz"), **arrays)
+    print("preprocess.npz", len(meta))
+
+
+def make_fisherz():
+    from oracle import fisherz
+    from rcaeval_amd import synth
+    X = synth.gaussian_sem(12, 500, seed=42, w_low=0.3, w_high=0.9, edge_prob=0.3)
+    C = fisherz.corrcoef(X)
+    keys, ps = [], []
+    for d in range(4):
+        for x in range(12):
+            for y in range(x + 1, 12):
+                rest = [v for v in range(12) if v not in (x, y)]
+                for S in combinations(rest, d):
+                    keys.append([x, y] + list(S) + [-1] * (3 - d))
+                    ps.append(fisherz.pvalue(C, 500, x, y, S))
+    np.savez_compressed(os.path.join(HERE, "fisherz.npz"), X=X, C=C, keys=np.array(keys, np.int32),
+                        p=np.array(ps))
+    print("fisherz.npz", len(ps))
+
+
+def make_orient():
+    from oracle import orient as oor
+    from oracle import skeleton as osk
+    from rcaeval_amd import synth
+    arrays = {}
+    for i, (n, N, ep) in enumerate([(14, 800, 0.25), (20, 600, 0.2), (30, 1000, 0.12), (16, 400, 0.3)]):
+        X = synth.gaussian_sem(n, N, seed=200 + i, w_low=0.4, w_high=0.9, edge_prob=ep)
+        C = np.corrcoef(X.T)
+        r = osk.skeleton_discovery(C, N)
+        xy, bits = [], []
+        W = (n + 63) // 64
+        for x in range(n):
+            for y in range(n):
+                if x != y and r.removed_level[x, y] >= 1:
+                    lst = r.sepset[x, y]
+                    side = set(lst[-2]) if x < y else set(lst[-1])
+                    if side:
+                        row = [0] * W
+                        for s in side:
+                            row[int(s) >> 6] |= 1 << (int(s) & 63)
+                        xy.append((x, y))
+                        bits.append(row)
+        arrays[f"adj{i}"] = r.adj.astype(np.uint8)
+        arrays[f"xy{i}"] = np.array(xy, np.int32).reshape(-1, 2)
+        arrays[f"bits{i}"] = np.array(bits, np.uint64).reshape(-1, W)
+        arrays[f"graph{i}"] = oor.orient(r.adj, r.sepset).astype(np.int32)
+    np.savez_compressed(os.path.join(HERE, "orient.npz"), **arrays)
+    print("orient.npz")
+
+
+def make_pagerank():
+    from oracle import pagerank as opr
+    arrays = {}
+    rng = np.random.default_rng(7)
+    for i in range(12):
+        m = int(rng.integers(2, 400))
+        A = (rng.random((m, m)) < rng.uniform(0.003, 0.2)).astype(float)
+        np.fill_diagonal(A, 0)
+        if i == 0:
+            A[:] = 0
+            A[0, 1] = 1
+        arrays[f"A{i}"] = A
+        arrays[f"s{i}"] = opr.pagerank(A)
+    np.savez_compressed(os.path.join(HERE, "pagerank.npz"), **arrays)
+    print("pagerank.npz")
+
+
+if __name__ == "__main__":
+    make_fisherz()
+    make_orient()
+    make_pagerank()
+    if os.path.isdir(REF):
+        make_random_walk()
+        make_preprocess()
+    else:
+        print("reference not present: random_walk / preprocess goldens not regenerated")

@@ -1,0 +1,152 @@
+"""CPU: the edge-sharded level protocol of rcaeval_amd.dist with gloo, world_size 2.
+
+The GPU backend is replaced by an oracle-backed backend with the same begin/run/end
+contract (chunks = (node x, run of S ranks), owner-disjoint evaluation, removal flags
+merged with all_reduce(MAX)), so the partitioning, the merge and the level barrier are
+checked against the single-process oracle skeleton without a GPU.
+"""
+import os
+import socket
+from itertools import combinations
+
+import numpy as np
+import pytest
+
+from rcaeval_amd.dist import split_by_work
+
+
+def test_split_by_work_tiles_and_balances():
+    rng = np.random.default_rng(0)
+    for world in (1, 2, 3, 4, 8):
+        w = rng.integers(0, 100, 1000)
+        prefix = np.concatenate([[0], np.cumsum(w)])
+        ranges = [split_by_work(prefix, r, world) for r in range(world)]
+        assert ranges[0][0] == 0 and ranges[-1][1] == 1000
+        for (a, b), (c, d) in zip(ranges, ranges[1:]):
+            assert b == c
+        loads = [prefix[b] - prefix[a] for a, b in ranges]
+        assert max(loads) - min(loads) <= 2 * w.max()
+    assert split_by_work(np.array([0]), 0, 2) == (0, 0)
+
+
+class OracleLevelBackend:
+    """CPU stand-in for GpuLevelBackend (test only): same chunking and dedup rule."""
+
+    CH = 3  # S ranks per chunk
+
+    def __init__(self, C, N, alpha=0.05):
+        import torch
+        from oracle import fisherz
+        self.C, self.N, self.alpha = C, N, alpha
+        self.n = C.shape[0]
+        self.adj = ~np.eye(self.n, dtype=bool)
+        self.rl = np.full((self.n, self.n), -1, np.int64)
+        self.rm = torch.zeros(self.n * self.n, dtype=torch.uint8)
+        self.unions = {}
+        self.depth = -1
+        self.pv = lambda x, y, S: fisherz.pvalue(C, N, x, y, S)
+
+    def begin(self, depth):
+        deg = self.adj.sum(1)
+        if not (deg.max() - 1 > depth - 1):
+            return None
+        self.depth = depth
+        self.rm.zero_()
+        self.chunks = []
+        for x in range(self.n):
+            nb = list(np.nonzero(self.adj[x])[0])
+            if depth == 0:
+                self.chunks.append((x, None, [y for y in nb if y > x]))
+                continue
+            if len(nb) < depth + 1:
+                continue
+            subsets = list(combinations(range(len(nb)), depth))
+            for i in range(0, len(subsets), self.CH):
+                self.chunks.append((x, nb, subsets[i:i + self.CH]))
+        work = [len(c[2]) + 1 for c in self.chunks]
+        return np.concatenate([[0], np.cumsum(work)]).astype(np.int64)
+
+    def run(self, lo, hi):
+        d = self.depth
+        for x, nb, items in self.chunks[lo:hi]:
+            if d == 0:
+                for y in items:
+                    if self.pv(x, y, ()) > self.alpha:
+                        self.rm[x * self.n + y] = 1
+                        self.rm[y * self.n + x] = 1
+                continue
+            for ks in items:
+                S = [int(nb[k]) for k in ks]
+                for y in nb:
+                    if y in S:
+                        continue
+                    in_y = all(self.adj[y, s] for s in S)
+                    if y < x and in_y:
+                        continue
+                    if self.pv(x, y, S) > self.alpha:
+                        self.rm[x * self.n + y] = 1
+                        self.rm[y * self.n + x] = 1
+                        self.unions.setdefault((x, int(y), d), set()).update(S)
+                        if in_y and y > x:
+                            self.unions.setdefault((int(y), x, d), set()).update(S)
+
+    def removal_tensor(self):
+        return self.rm
+
+    def end(self):
+        rm = self.rm.numpy().reshape(self.n, self.n).astype(bool)
+        self.rl[rm] = self.depth
+        self.adj &= ~rm
+
+
+def _worker(rank, world, port, C, N, q):
+    import torch.distributed as dist
+    from rcaeval_amd.dist import run_sharded_levels
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    be = OracleLevelBackend(C, N)
+    run_sharded_levels(be, rank, world)
+    unions = [None] * world
+    dist.all_gather_object(unions, be.unions)
+    dist.destroy_process_group()
+    merged = {}
+    for u in unions:
+        for k, v in u.items():
+            merged.setdefault(k, set()).update(v)
+    q.put((rank, be.rl, merged))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_levels_match_single_process_oracle(world):
+    import multiprocessing as mp
+    from oracle import skeleton as osk
+    from rcaeval_amd import synth
+    n, N = 14, 600
+    X = synth.gaussian_sem(n, N, seed=11, w_low=0.3, w_high=0.9, edge_prob=0.25)
+    C = np.corrcoef(X.T)
+    ref = osk.skeleton_discovery(C, N)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, C, N, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, rl, merged in results:
+        np.testing.assert_array_equal(rl, ref.removed_level)
+        for (x, y, d), members in merged.items():
+            lst = ref.sepset[x, y]
+            side = set(int(v) for v in (lst[-2] if x < y else lst[-1]))
+            assert ref.removed_level[x, y] == d
+            assert members == side

@@ -1,0 +1,181 @@
+"""GPU parity for the ranking heads and the drop-in RCA methods, plus the sharded path.
+
+PageRank: bit-identical to the scikit-network restatement (golden).
+Random walk: identical ranks and scores to the REFERENCE module's outputs (golden).
+pc_pagerank / pc_randomwalk: identical rank lists to the oracle pipeline (numpy skeleton
+restatement + Python orientation restatement + scipy PageRank + the reference glue).
+"""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from rcaeval_amd import synth
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_pagerank_bitwise_golden():
+    from rcaeval_amd.graph_heads.page_rank import PageRank
+    g = np.load(os.path.join(GOLD, "pagerank.npz"))
+    for i in range(12):
+        np.testing.assert_array_equal(PageRank().fit_transform(g[f"A{i}"]), g[f"s{i}"])
+
+
+def test_pagerank_empty_input_raises():
+    from rcaeval_amd.graph_heads.page_rank import PageRank
+    with pytest.raises(ValueError):
+        PageRank().fit_transform(np.zeros((4, 4)))
+
+
+def test_random_walk_matches_reference_golden():
+    from rcaeval_amd.graph_heads.random_walk import random_walk
+    for c in json.load(open(os.path.join(GOLD, "random_walk.json"))):
+        res = random_walk(np.array(c["adj"]), c["names"], num_loop=c["num_loop"])
+        assert [r[0] for r in res] == c["ranks"]
+        np.testing.assert_array_equal([r[1] for r in res], c["scores"])
+
+
+def test_random_walk_serial_path_matches_numpy():
+    """Non-uniform transition columns take the sequential kernel; compare with numpy's choice."""
+    from oracle import random_walk as orw
+    from rcaeval_amd.engine import get_engine
+    rng = np.random.default_rng(5)
+    P = rng.random((9, 9))
+    P /= P.sum(0, keepdims=True)
+    st = np.random.default_rng(0).bit_generator.state["state"]
+    got = get_engine(0).random_walk_counts(P, 3, 500, st["state"], st["inc"])
+    np.testing.assert_array_equal(got, orw.walk_counts(P, 3, 500))
+
+
+def _oracle_pipeline(df, dataset, head):
+    """Reference-equivalent CPU pipeline built only from oracle restatements + reference glue."""
+    from oracle import orient as oor
+    from oracle import pagerank as opr
+    from oracle import random_walk as orw
+    from oracle import skeleton as osk
+    from rcaeval_amd.e2e.pc_pagerank import digraph_matrix
+    from rcaeval_amd.graph_heads.random_walk import transition_matrix
+    from rcaeval_amd.io.time_series import preprocess
+    data = preprocess(df, dataset=dataset)
+    names = data.columns.to_list()
+    X = data.to_numpy().astype(float)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        C = np.corrcoef(X.T)
+    r = osk.skeleton_discovery(C, X.shape[0])
+    g = oor.orient(r.adj, r.sepset)
+    if head == "pagerank":
+        M, _ = digraph_matrix(g)
+        scores = opr.pagerank(M.T)
+        ranked = sorted(zip(names, scores), key=lambda t: t[1], reverse=True)
+        return [n for n, _ in ranked], g
+    uniq = list(dict.fromkeys(names))
+    P = transition_matrix(g, names, uniq)
+    counts = orw.walk_counts(P, 0, len(names))
+    ranked = sorted([(nm, counts[i] / len(names)) for i, nm in enumerate(uniq)], key=lambda t: t[1], reverse=True)
+    return [n for n, _ in ranked], g
+
+
+@pytest.mark.parametrize("m,rows,seed", [(12, 200, 0), (38, 600, 1), (49, 600, 2)])
+def test_pc_pagerank_matches_oracle_pipeline(m, rows, seed):
+    from rcaeval_amd.e2e import pc_pagerank
+    df = synth.telemetry_frame(m, rows, n_constant=2, seed=seed)
+    out = pc_pagerank(df, 0, dataset="online-boutique")
+    ranks, g = _oracle_pipeline(df, "online-boutique", "pagerank")
+    assert out["ranks"] == ranks
+
+
+@pytest.mark.parametrize("m,rows,seed", [(12, 200, 3), (46, 600, 4)])
+def test_pc_randomwalk_matches_oracle_pipeline(m, rows, seed):
+    from rcaeval_amd.e2e import pc_randomwalk
+    from rcaeval_amd.graph_construction.pc import pc_default
+    df = synth.telemetry_frame(m, rows, n_constant=2, seed=seed)
+    out = pc_randomwalk(df, 0, dataset="online-boutique")
+    ranks, g = _oracle_pipeline(df, "online-boutique", "randomwalk")
+    assert out["ranks"] == ranks
+    from rcaeval_amd.io.time_series import preprocess
+    np.testing.assert_array_equal(pc_default(preprocess(df, dataset="online-boutique")), g)
+
+
+def test_pc_pagerank_readme_path_dataset_none_keeps_time_and_constants():
+    """dataset=None: preprocess is the identity, the time column and constant columns reach
+    PC (NaN correlations -> dependent), as in the README example."""
+    from rcaeval_amd.e2e import pc_pagerank
+    df = synth.telemetry_frame(20, 300, n_constant=2, seed=9)
+    out = pc_pagerank(df, 0)
+    ranks, _ = _oracle_pipeline(df, None, "pagerank")
+    assert out["ranks"] == ranks
+    assert out["node_names"] == df.columns.to_list()
+
+
+def test_causal_pc_sepset_surface():
+    from oracle import skeleton as osk
+    from rcaeval_amd.causal import pc
+    X = synth.gaussian_sem(16, 600, seed=21, w_low=0.3, w_high=0.9, edge_prob=0.25)
+    cg = pc(X)
+    r = osk.skeleton_discovery(np.corrcoef(X.T), 600)
+    n = 16
+    for i in range(n):
+        for j in range(n):
+            if i == j:
+                continue
+            mine, ref = cg.sepset[i, j], r.sepset[i, j]
+            assert len(mine) == len(ref)
+            assert [set(map(int, t)) for t in mine] == [set(map(int, t)) for t in ref]
+    assert cg.no_ci_tests == sum(r.calls_per_level)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _sharded_worker(rank, world, port, X, q):
+    import torch
+    import torch.distributed as dist
+    from rcaeval_amd.dist import sharded_skeleton
+    from rcaeval_amd.engine import get_engine
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = get_engine(0)
+    C = eng.corr(X)
+    out = sharded_skeleton(eng, C, X.shape[0], max_depth=3)
+    q.put((rank, out.removed_level.copy(), out.sep_xy.copy(), out.sep_bits.copy(), out.stats["tests"]))
+    dist.barrier()
+    dist.destroy_process_group()
+    torch.cuda.synchronize()
+
+
+def test_sharded_skeleton_two_ranks_one_gpu():
+    """The multi-GPU protocol with 2 ranks sharing cuda:0 (gloo all-reduce on device tensors)."""
+    import multiprocessing as mp
+    from rcaeval_amd.engine import get_engine
+    X = synth.gaussian_sem(300, 3000, seed=12)
+    eng = get_engine(0)
+    ref = eng.skeleton(eng.corr(X), 3000, max_depth=3)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, 2, port, X, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=600) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+
+    def unions(xy, bits):
+        d = {}
+        for (x, y), b in zip(xy, bits):
+            d[(int(x), int(y))] = d.get((int(x), int(y)), 0) | int.from_bytes(b.tobytes(), "little")
+        return d
+    for rank, rl, xy, bits, tests in res:
+        np.testing.assert_array_equal(rl, ref.removed_level)
+        assert unions(xy, bits) == unions(ref.sep_xy, ref.sep_bits)
+        assert tests == ref.stats["tests"]
