@@ -51,7 +51,10 @@ extern "C" {
                                  exact path                                            */
 
 #define PCG_MAX_LEVELS 32
-#define PCG_MAX_DEPTH 12      /* deepest conditioning-set size supported on device     */
+#define PCG_MAX_DEPTH 12      /* deepest conditioning set with the fast kernels and per-test
+                                 records; depths 13..PCG_MAX_LEVEL_DEPTH run on the generic
+                                 exact-path kernel (counts only, no records)            */
+#define PCG_MAX_LEVEL_DEPTH 30 /* deepest conditioning-set size supported at all          */
 
 typedef struct pcg_handle pcg_handle;
 

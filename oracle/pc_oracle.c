@@ -28,7 +28,7 @@
 #include <omp.h>
 #endif
 
-#define ORC_MAXD 12
+#define ORC_MAXD 32
 
 typedef struct {
     int64_t tests[32];   /* unique tests per depth            */

@@ -54,13 +54,17 @@ __device__ __forceinline__ void tile_of(int t, int T, int &bi, int &bj) {
 }
 
 __global__ __launch_bounds__(256) void k_xtx(const double *X, int64_t N, int n, int64_t ldx,
-                                            const double *mean, double scale, double *G,
-                                            int64_t ldg) {
+                                            const double *mean, int ntiles, int64_t kchunk, double *G,
+                                            int64_t ldg, int64_t slab_stride) {
     __shared__ double As[2][KT][TILE + PAD];
     __shared__ double Bs[2][KT][TILE + PAD];
     const int T = (n + TILE - 1) / TILE;
     int bi, bj;
-    tile_of(blockIdx.x, T, bi, bj);
+    tile_of(blockIdx.x % ntiles, T, bi, bj);
+    const int slab = blockIdx.x / ntiles;           // split-K slice
+    const int64_t kbeg = (int64_t)slab * kchunk;
+    const int64_t kend = std::min<int64_t>(N, kbeg + kchunk);
+    G += (int64_t)slab * slab_stride;
     const int i0 = bi * TILE, j0 = bj * TILE;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
@@ -83,7 +87,7 @@ __global__ __launch_bounds__(256) void k_xtx(const double *X, int64_t N, int n, 
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int64_t t = t0 + sr + 4 * q;
-            const bool vt = t < N;
+            const bool vt = t < kend;
             ra[q] = (vt && va) ? X[t * ldx + i0 + sc] - ma : 0.0;
             rb[q] = (vt && vb) ? X[t * ldx + j0 + sc] - mb : 0.0;
         }
@@ -96,14 +100,14 @@ __global__ __launch_bounds__(256) void k_xtx(const double *X, int64_t N, int n, 
         }
     };
 
-    const int64_t nk = (N + KT - 1) / KT;
-    load(0);
+    const int64_t nk = (kend - kbeg + KT - 1) / KT;
+    load(kbeg);
     store(0);
     __syncthreads();
     const int fr = lane & 15, fk = lane >> 4;
     for (int64_t kk = 0; kk < nk; ++kk) {
         const int buf = (int)(kk & 1);
-        if (kk + 1 < nk) load((kk + 1) * KT);
+        if (kk + 1 < nk) load(kbeg + (kk + 1) * KT);
 #pragma unroll
         for (int k4 = 0; k4 < KT; k4 += 4) {
             double a0 = As[buf][k4 + fk][wr + fr];
@@ -128,7 +132,7 @@ __global__ __launch_bounds__(256) void k_xtx(const double *X, int64_t N, int n, 
                 const int i = i0 + wr + 16 * a + (lane >> 4) + 4 * r;
                 const int j = j0 + wc + 16 * b + (lane & 15);
                 if (i < n && j < n) {
-                    const double v = acc[a][b][r] * scale;
+                    const double v = acc[a][b][r];
                     if (bi != bj) {
                         G[(int64_t)i * ldg + j] = v;
                         G[(int64_t)j * ldg + i] = v;
@@ -140,18 +144,27 @@ __global__ __launch_bounds__(256) void k_xtx(const double *X, int64_t N, int n, 
             }
 }
 
-__global__ void k_stddev(const double *G, int64_t ldg, int n, double *sd) {
+// sd_i = sqrt(c_ii) with c = (sum of split-K slabs) * 1/(N-1)
+__global__ void k_stddev(const double *G, int64_t ldg, int64_t slab_stride, int ks, int n, double scale,
+                         double *sd) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) sd[i] = sqrt(G[(int64_t)i * ldg + i]);
+    if (i >= n) return;
+    double v = 0.0;
+    for (int s = 0; s < ks; ++s) v += G[(int64_t)s * slab_stride + (int64_t)i * ldg + i];
+    sd[i] = sqrt(v * scale);
 }
 
-__global__ void k_normalize(double *G, int64_t ldg, int n, const double *sd) {
+// C_ij = clip(((sum_s G_s,ij) * 1/(N-1) / sd_i) / sd_j, -1, 1)   (numpy corrcoef order)
+__global__ void k_normalize(const double *G, int64_t ldg, int64_t slab_stride, int ks, double *C, int64_t ldc,
+                            int n, double scale, const double *sd) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     const int i = blockIdx.y;
     if (j >= n) return;
-    double v = G[(int64_t)i * ldg + j] / sd[i];
+    double g = 0.0;
+    for (int s = 0; s < ks; ++s) g += G[(int64_t)s * slab_stride + (int64_t)i * ldg + j];
+    double v = (g * scale) / sd[i];
     v = v / sd[j];
-    G[(int64_t)i * ldg + j] = v > 1.0 ? 1.0 : (v < -1.0 ? -1.0 : v);  // NaN passes through
+    C[(int64_t)i * ldc + j] = v > 1.0 ? 1.0 : (v < -1.0 ? -1.0 : v);  // NaN passes through
 }
 
 }  // namespace
@@ -173,10 +186,26 @@ extern "C" int pcg_corr(pcg_handle *h, const double *X, int64_t N, int64_t n, in
     hipLaunchKernelGGL(k_colmean, dim3((nn + 255) / 256), dim3(256), 0, h->stream, part, nchunks, nn, N, mean);
     const int T = (nn + TILE - 1) / TILE;
     const int ntiles = T * (T + 1) / 2;
-    hipLaunchKernelGGL(k_xtx, dim3(ntiles), dim3(256), 0, h->stream, X, N, nn, ldx, mean,
-                       1.0 / (double)(N - 1), C, ldc);
-    hipLaunchKernelGGL(k_stddev, dim3((nn + 255) / 256), dim3(256), 0, h->stream, C, ldc, nn, sd);
-    hipLaunchKernelGGL(k_normalize, dim3((nn + 255) / 256, nn), dim3(256), 0, h->stream, C, ldc, nn, sd);
+    // split K so that the grid covers the chip (~8 blocks per CU); slabs summed in order later
+    int ks = (int)std::min<int64_t>(std::max<int64_t>(1, (2048 + ntiles - 1) / ntiles), std::max<int64_t>(1, N / 512));
+    ks = std::min(ks, 16);
+    const int64_t kchunk = (((N + ks - 1) / ks) + KT - 1) / KT * KT;
+    ks = (int)((N + kchunk - 1) / kchunk);
+    double *G = C;
+    int64_t ldg = ldc, stride = 0;
+    if (ks > 1) {
+        stride = (int64_t)nn * nn;
+        if (!pcg_ensure(h, h->pr_scratch, sizeof(double) * (size_t)stride * ks))
+            return pcg_fail(h, PCG_ERR_OOM, "pcg_corr split-K slabs");
+        G = (double *)h->pr_scratch.p;
+        ldg = nn;
+    }
+    const double scale = 1.0 / (double)(N - 1);
+    hipLaunchKernelGGL(k_xtx, dim3(ntiles * ks), dim3(256), 0, h->stream, X, N, nn, ldx, mean, ntiles, kchunk, G,
+                       ldg, stride);
+    hipLaunchKernelGGL(k_stddev, dim3((nn + 255) / 256), dim3(256), 0, h->stream, G, ldg, stride, ks, nn, scale, sd);
+    hipLaunchKernelGGL(k_normalize, dim3((nn + 255) / 256, nn), dim3(256), 0, h->stream, G, ldg, stride, ks, C, ldc,
+                       nn, scale, sd);
     PCG_HIP(h, hipGetLastError());
     PCG_HIP(h, hipStreamSynchronize(h->stream));
     return PCG_OK;

@@ -94,7 +94,7 @@ __device__ inline int pcg_lu_inv01(double *A, int m, int *piv, double *B0, doubl
 }
 
 // Binomial table: binom[c * PCG_BK + k] = C(c, k), saturated at UINT64_MAX.
-#define PCG_BK (PCG_MAX_DEPTH + 1)
+#define PCG_BK (PCG_MAX_LEVEL_DEPTH + 1)
 
 __device__ __forceinline__ uint64_t pcg_binom(const uint64_t *tab, int c, int k) {
     return (c < k || c < 0) ? 0ull : tab[(int64_t)c * PCG_BK + k];

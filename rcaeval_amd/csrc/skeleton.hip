@@ -72,6 +72,7 @@ struct LevelArgs {
     int record;
     int64_t chunk_lo;            // first chunk of this launch (within its class)
     int spl;                     // S ranks per lane (LDS-resident kernel)
+    int lds_btab_off;            // byte offset of the LDS binomial table (LDS-resident kernel)
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -562,24 +563,30 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
     unsigned long long tests = 0, indep = 0;
 
     if constexpr (MODE == MODE_DECIDE && DM <= 4) {
-        // Each lane walks a contiguous run of spl colex ranks with the colex successor
-        // (no per-S unranking), factors M_SS once per S and sweeps y barrier-free.
-        const uint64_t q0 = r0 + (uint64_t)tid * (uint64_t)a.spl;
-        const uint64_t q1 = min(r1, q0 + (uint64_t)a.spl);
-        int k[DM];
+        // Lanes take consecutive colex ranks (stride = block size): within a wave the S sets
+        // share their high elements, so the per-y operand reads M[t][k_i] are broadcast or
+        // consecutive (bank-conflict-light). Unranking uses an LDS copy of C(c, i), c <= D.
+        unsigned long long *btab = reinterpret_cast<unsigned long long *>(smem + a.lds_btab_off);
+        for (int e = tid; e < (D + 1) * (DM + 1); e += bs) {
+            const int c = e / (DM + 1), i = e - c * (DM + 1);
+            btab[e] = pcg_binom(a.binom, c, i);
+        }
+        __syncthreads();
+        for (uint64_t rank = r0 + tid; rank < r1; rank += bs) {
+            int k[DM];
+            {
+                uint64_t rr = rank;
+                int hi_ = D;
 #pragma unroll
-        for (int i = 0; i < DM; ++i) k[i] = i;
-        if (q0 < q1) pcg_unrank_colex<DM>(q0, d, D, a.binom, k);
-        for (uint64_t rank = q0; rank < q1; ++rank) {
-            if (rank > q0) {  // colex successor: bump the lowest k[i] that can grow, reset below
-                int i = 0;
-#pragma unroll
-                for (int j = 0; j < DM - 1; ++j)
-                    if (i == j && k[j] + 1 == k[j + 1]) i = j + 1;
-#pragma unroll
-                for (int j = 0; j < DM; ++j) {
-                    if (j == i) k[j] += 1;
-                    else if (j < i) k[j] = j;
+                for (int ii = DM - 1; ii >= 0; --ii) {
+                    int lo_ = ii, up = hi_ - 1;
+                    while (lo_ < up) {
+                        const int mid = (lo_ + up + 1) >> 1;
+                        if (btab[mid * (DM + 1) + ii + 1] <= rr) lo_ = mid; else up = mid - 1;
+                    }
+                    k[ii] = lo_;
+                    rr -= btab[lo_ * (DM + 1) + ii + 1];
+                    hi_ = lo_;
                 }
             }
             unsigned long long Smask = 0;
@@ -811,6 +818,93 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// depths > PCG_MAX_DEPTH (degenerate graphs, e.g. constant columns whose NaN correlations
+// never separate): one thread per (x, S rank), exact LU path per test with per-thread
+// scratch in global memory. Throughput is not the goal here; semantics are.
+__global__ __launch_bounds__(64) void k_level_deep(LevelArgs a, double *scratch, int64_t nchunks) {
+    const int d = a.d;
+    const int m = d + 2;
+    const int per = m * m + 2 * m + (d + 2);      // doubles: A, B0, B1, then int space
+    const int64_t gtid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double *A = scratch + gtid * per;
+    double *B0 = A + m * m, *B1 = B0 + m;
+    int *kk = reinterpret_cast<int *>(B1 + m);   // d ints (fits in d+2 doubles)
+    int piv[PCG_MAX_LEVEL_DEPTH + 2];
+    int var[PCG_MAX_LEVEL_DEPTH + 2];
+    unsigned long long tests = 0, nindep = 0;
+    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+        const int64_t chunk = a.chunk_lo + c;
+        int lo = 0, hi = a.n;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (a.cpre[mid] <= chunk) lo = mid; else hi = mid;
+        }
+        const int x = lo;
+        const int D = a.deg[x];
+        const int32_t *nx = a.nbr + a.off[x];
+        const uint64_t nS = pcg_binom(a.binom, D, d);
+        const uint64_t rank = (uint64_t)(chunk - a.cpre[x]) * 64u + threadIdx.x;
+        if (rank >= nS) continue;
+        {   // colex unrank
+            uint64_t rr = rank;
+            int hi_ = D;
+            for (int ii = d - 1; ii >= 0; --ii) {
+                int lo_ = ii, up = hi_ - 1;
+                while (lo_ < up) {
+                    const int mid = (lo_ + up + 1) >> 1;
+                    if (pcg_binom(a.binom, mid, ii + 1) <= rr) lo_ = mid; else up = mid - 1;
+                }
+                kk[ii] = lo_;
+                rr -= pcg_binom(a.binom, lo_, ii + 1);
+                hi_ = lo_;
+            }
+        }
+        int p = 0;
+        for (int t = 0; t < D; ++t) {
+            if (p < d && kk[p] == t) { ++p; continue; }
+            const int yg = nx[t];
+            bool in_y = true;
+            for (int q = 0; q < d && in_y; ++q) {
+                const int s = nx[kk[q]];
+                in_y = (a.adj[(int64_t)yg * a.W + (s >> 6)] >> (s & 63)) & 1ull;
+            }
+            if (yg < x && in_y) continue;
+            ++tests;
+            var[0] = x < yg ? x : yg;
+            var[1] = x < yg ? yg : x;
+            for (int q = 0; q < d; ++q) var[2 + q] = nx[kk[q]];
+            for (int r = 0; r < m; ++r)
+                for (int c = 0; c < m; ++c) A[r * m + c] = a.C[(int64_t)var[r] * a.ldc + var[c]];
+            double i00, i01, i11, pv = __builtin_nan("");
+            int err = 0;
+            if (pcg_lu_inv01(A, m, piv, B0, B1, &i00, &i01, &i11)) err = 1;
+            else {
+                const double prod = i00 * i11;
+                if (prod < 0.0 || a.dof_negative) err = 2;
+                else pv = pcg_pvalue_from_r(-i01 / sqrt(prod), a.sqrt_dof, &err);
+            }
+            if (err) { atomicOr(&a.ctr->error, (unsigned long long)err); continue; }
+            if (fabs(pv - a.alpha) < 1e-9) atomicAdd(&a.ctr->near_alpha, 1ull);
+            if (pv > a.alpha) {
+                ++nindep;
+                a.rm[(int64_t)x * a.n + yg] = 1;
+                a.rm[(int64_t)yg * a.n + x] = 1;
+                unsigned long long *rx = reinterpret_cast<unsigned long long *>(a.ug + ((int64_t)a.off[x] + t) * a.W);
+                for (int q = 0; q < d; ++q) atomicOr(&rx[var[2 + q] >> 6], 1ull << (var[2 + q] & 63));
+                if (in_y && yg > x) {
+                    const int sy = a.off[yg] + find_in_sorted(a.nbr + a.off[yg], a.deg[yg], x);
+                    unsigned long long *ry = reinterpret_cast<unsigned long long *>(a.ug + (int64_t)sy * a.W);
+                    for (int q = 0; q < d; ++q) atomicOr(&ry[var[2 + q] >> 6], 1ull << (var[2 + q] & 63));
+                }
+            }
+        }
+    }
+    if (tests) atomicAdd(&a.ctr->tests, tests);
+    if (nindep) atomicAdd(&a.ctr->indep, nindep);
+    if (tests) atomicAdd(&a.ctr->exact, tests);
+}
+
+// ---------------------------------------------------------------------------------------
 // exact path over the deferred list (LU like numpy.linalg.inv; the reference p expression)
 __global__ void k_exact(LevelArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -982,7 +1076,8 @@ void launch_lds_mode(pcg_handle *h, const LevelArgs &a, int64_t nchunks, size_t 
 
 constexpr int SMALL_DEG = 64;        // LDS-resident kernel handles nodes with <= 64 neighbours
 
-size_t lds_small_bytes(int D) { return (size_t)D * D * 8 + (size_t)D * (2 * 8 + 3 * 8 + 4) + 16; }
+size_t lds_small_core(int D) { return ((size_t)D * D * 8 + (size_t)D * (2 * 8 + 3 * 8 + 4) + 16 + 15) & ~(size_t)15; }
+size_t lds_small_bytes(int D) { return lds_small_core(D) + (size_t)(D + 1) * 5 * 8; }
 
 int mode_of(const pcg_handle *h, int d) {
     if ((h->flags & PCG_FLAG_EXACT_ALL) || (double)h->N - d - 3 <= 0) return MODE_EXACT;
@@ -1083,9 +1178,9 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
         if (total_chunks) *total_chunks = 0;
         return 1;  // done
     }
-    if (depth >= PCG_MAX_LEVELS || depth > PCG_MAX_DEPTH)
-        return pcg_fail(h, PCG_ERR_INVALID, "conditioning depth %d exceeds PCG_MAX_DEPTH=%d", depth,
-                        PCG_MAX_DEPTH);
+    if (depth >= PCG_MAX_LEVELS || depth > PCG_MAX_LEVEL_DEPTH)
+        return pcg_fail(h, PCG_ERR_INVALID, "conditioning depth %d exceeds PCG_MAX_LEVEL_DEPTH=%d", depth,
+                        PCG_MAX_LEVEL_DEPTH);
     h->depth = depth;
     const int n = (int)h->n;
     h->deg_levels.insert(h->deg_levels.end(), h->deg_h.begin(), h->deg_h.end());
@@ -1122,13 +1217,16 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
             if (ns > ((uint64_t)1 << 46))
                 return pcg_fail(h, PCG_ERR_INVALID, "depth %d work too large at node %d (deg %d)", depth, x, D);
             h->work_h[x] = (int64_t)ns * (D - depth);
-            if (D <= SMALL_DEG) { sum_small += (double)ns; h->maxdeg_small = std::max(h->maxdeg_small, D); }
+            if (D <= SMALL_DEG && depth <= PCG_MAX_DEPTH) {
+                sum_small += (double)ns;
+                h->maxdeg_small = std::max(h->maxdeg_small, D);
+            }
             else { sum_large += (double)ns; ++cnt_large; }
         }
         // ~4096 LDS-resident blocks per depth; each lane walks spl S ranks
         h->spl = (int)std::min(64.0, std::max(1.0, std::floor(sum_small / (256.0 * 4096.0))));
         const double mean_large = cnt_large ? sum_large / cnt_large : 0.0;
-        h->chunk = mean_large <= 64 ? 64 : (mean_large <= 128 ? 128 : 256);
+        h->chunk = (depth > PCG_MAX_DEPTH || mean_large <= 64) ? 64 : (mean_large <= 128 ? 128 : 256);
         const uint64_t csz = (uint64_t)256 * h->spl;
         int64_t ss = 0, sl = 0;
         for (int x = 0; x < n; ++x) {
@@ -1137,7 +1235,7 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
             const int D = h->deg_h[x];
             if (D < depth + 1) continue;
             const uint64_t ns = hbinom(h, D, depth);
-            if (D <= SMALL_DEG) ss += (int64_t)((ns + csz - 1) / csz);
+            if (D <= SMALL_DEG && depth <= PCG_MAX_DEPTH) ss += (int64_t)((ns + csz - 1) / csz);
             else sl += (int64_t)((ns + h->chunk - 1) / h->chunk);
         }
         cs[n] = ss;
@@ -1243,6 +1341,7 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                     LevelArgs as = a;
                     as.chunk_lo = s_lo;
                     as.bs = 256;
+                    as.lds_btab_off = (int)lds_small_core(h->maxdeg_small);
                     const size_t lds = lds_small_bytes(h->maxdeg_small);
                     if (mode == MODE_DECIDE) launch_lds_mode<MODE_DECIDE>(h, as, s_hi - s_lo, lds);
                     else if (mode == MODE_FULLP) launch_lds_mode<MODE_FULLP>(h, as, s_hi - s_lo, lds);
@@ -1250,7 +1349,19 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                 }
                 const int64_t l_lo = std::max(chunk_lo, h->total_small) - h->total_small;
                 const int64_t l_hi = chunk_hi - h->total_small;
-                if (l_hi > l_lo) {
+                if (l_hi > l_lo && d > PCG_MAX_DEPTH) {
+                    LevelArgs al = a;
+                    al.cpre = (const int64_t *)h->cpre.p + (h->n + 1);
+                    const int64_t nch_deep = l_hi - l_lo;
+                    const int grid = (int)std::min<int64_t>(nch_deep, 512);
+                    const int m = d + 2;
+                    const size_t per = (size_t)(m * m + 2 * m + (d + 2));
+                    if (!pcg_ensure(h, h->pr_scratch, sizeof(double) * per * 64 * grid))
+                        return pcg_fail(h, PCG_ERR_OOM, "deep-level scratch");
+                    al.chunk_lo = l_lo;
+                    hipLaunchKernelGGL(k_level_deep, dim3(grid), dim3(64), 0, h->stream, al, (double *)h->pr_scratch.p,
+                                       nch_deep);
+                } else if (l_hi > l_lo) {
                     LevelArgs al = a;
                     al.cpre = (const int64_t *)h->cpre.p + (h->n + 1);
                     al.chunk_lo = l_lo;
