@@ -35,6 +35,23 @@ def flops_per_test(d: int) -> float:
     return (d + 2) ** 3 / 3.0 + 40.0
 
 
+def pmc_traffic(kernel_prefix: str):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC pass
+    (profiles/*_pmc_summary.json, same bench command): FETCH_SIZE (KB, x2 for the gfx950
+    half-count of wide reads, MI355X_MICROARCH.md §HBM) + WRITE_SIZE (KB). None if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
+    if not files:
+        return None, None
+    data = json.load(open(files[-1]))
+    for name, ctr in data.items():
+        if kernel_prefix in name and "FETCH_SIZE" in ctr and "WRITE_SIZE" in ctr:
+            fetch = ctr["FETCH_SIZE"]["per_dispatch_mean"] * 1024.0 * 2.0
+            write = ctr["WRITE_SIZE"]["per_dispatch_mean"] * 1024.0
+            return fetch + write, os.path.basename(files[-1])
+    return None, None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -165,6 +182,8 @@ def main():
     alg_flops = st["tests"][dmax] * flops_per_test(dmax)
     ach_gbs = alg_bytes / (k_ms / 1000.0) / 1e9 if k_ms > 0 else 0.0
     ach_tf = alg_flops / (k_ms / 1000.0) / 1e12 if k_ms > 0 else 0.0
+    kname = f"k_level_lds<{dmax}, {1 if args.full_p else 0}>" if dmax >= 1 else "k_level0"
+    traffic, traffic_src = pmc_traffic(kname)
 
     if rank == 0:
         line = {
@@ -186,8 +205,9 @@ def main():
             "level_ms": [round(v, 3) for v in st["level_ms"]],
             "edges_after": st["edges_after"], "exact_path": st["exact"], "near_alpha": st["near_alpha"],
             "roofline": {"bound": "hbm", "achieved": ach_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": ach_gbs / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": f"k_level<{dmax}> (depth {dmax})", "kernel_ms": k_ms,
+                         "frac": ach_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_src,
+                         "kernel": kname, "kernel_ms": k_ms,
                          "algorithmic_bytes_per_test": bytes_per_test(dmax),
                          "fp64_tflops_algorithmic": ach_tf, "fp64_peak_tflops": FP64_PEAK_TFLOPS},
         }
