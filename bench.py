@@ -123,11 +123,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs (default off): several ranks on one GPU need gloo + a shared device
+    device = int(os.environ.get("PCG_BENCH_DEVICE", local))
+    backend = os.environ.get("PCG_DIST_BACKEND", "nccl")
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    eng = get_engine(local)
+        torch.cuda.set_device(device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
+    eng = get_engine(device)
     flags = _lib.PCG_FLAG_FULL_P if args.full_p else 0
 
     X = synth.gaussian_sem(args.n, args.samples, seed=args.seed)
@@ -143,8 +149,13 @@ def main():
         phases.append(("corr", time.perf_counter() - t0))
         if world > 1:
             from rcaeval_amd.dist import sharded_skeleton
-            return sharded_skeleton(eng, C, args.samples, alpha=args.alpha, max_depth=args.max_depth,
-                                    flags=flags)
+            trace = [] if os.environ.get("PCG_DIST_TRACE") else None
+            out = sharded_skeleton(eng, C, args.samples, alpha=args.alpha, max_depth=args.max_depth,
+                                   flags=flags, trace=trace)
+            if trace is not None:
+                print(f"[rank {rank}] " + " ".join(f"{p}{d if d >= 0 else ''}={1000 * t:.2f}"
+                                                    for p, d, t in trace), file=sys.stderr, flush=True)
+            return out
         return eng.skeleton(C, args.samples, alpha=args.alpha, max_depth=args.max_depth, flags=flags)
 
     def barrier():
@@ -162,6 +173,8 @@ def main():
         out = one_step()
         barrier()
         dt = time.perf_counter() - t0
+        if os.environ.get("PCG_DIST_TRACE"):
+            print(f"[rank {rank}] step {1000 * dt:.2f} ms", file=sys.stderr, flush=True)
         if world > 1:
             t = torch.tensor([dt], dtype=torch.float64, device=eng.device)
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)

@@ -63,6 +63,7 @@ struct pcg_handle {
     int chunk = 256;                 // block size of the staged (large-degree) kernel
     int spl = 1;                     // S ranks per lane of the LDS-resident kernel
     int32_t maxdeg_small = 0;        // largest degree handled by the LDS-resident kernel
+    bool tgroup = false;             // small class runs k_level_lds_t this depth
     int32_t maxdeg = 0;
     int64_t sumdeg = 0;
     std::vector<int32_t> deg_h;      // degrees at the start of the current depth

@@ -42,6 +42,7 @@ namespace {
 constexpr int MODE_DECIDE = 0;
 constexpr int MODE_FULLP = 1;
 constexpr int MODE_EXACT = 2;
+#define PCG_TGROUP 4             // candidates c per lane task in k_level_lds_t
 
 struct LevelArgs {
     const double *C;
@@ -818,6 +819,285 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// depth 2..4, D <= 64, threshold decision: "T-group" form of the LDS-resident kernel.
+// A lane owns a (d-1)-subset T of adj(x) and a group of TG consecutive candidates c with
+// c < min(T) (S = {c} + T, ascending). Factoring T first and c last, per y it forms
+//   v_T = L_T^-1 M[T][y],  byy = M_yy - |v_T|^2,  bxy = M_xy - u_T.v_T     (once per y)
+// and per c only the last row of the triangular solve:
+//   v_c = (M[c][y] - l_c.v_T) / lambda_c,  c_yy = byy - v_c^2,  c_xy = bxy - u_c v_c
+// — the same partial correlation, ~9 fp64 ops per test instead of ~26. Tasks (g, T): group
+// g covers c in [g*TG, g*TG+TG), T ranges over (d-1)-subsets of [g*TG+1, D) in colex order.
+template <int DM>
+__global__ __launch_bounds__(256, 4) void k_level_lds_t(LevelArgs a) {
+    constexpr int DT = DM - 1;
+    constexpr int TG = PCG_TGROUP;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x;
+    const int bs = blockDim.x;
+    const int64_t chunk = a.chunk_lo + blockIdx.x;
+    int lo = 0, hi = a.n;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (a.cpre[mid] <= chunk) lo = mid; else hi = mid;
+    }
+    const int x = lo;
+    const int D = a.deg[x];
+    const int32_t *nxg = a.nbr + a.off[x];
+
+    double *M = reinterpret_cast<double *>(smem);                 // D * D
+    double *Mx = M + D * D;                                       // D
+    double *Md = Mx + D;                                          // D
+    unsigned long long *lmask = reinterpret_cast<unsigned long long *>(Md + D);   // D
+    unsigned long long *uself = lmask + D;                        // D
+    unsigned long long *uprop = uself + D;                        // D
+    int32_t *nxs = reinterpret_cast<int32_t *>(uprop + D);       // D
+    int *s_tx = nxs + D;                                          // 1
+    unsigned long long *btab = reinterpret_cast<unsigned long long *>(smem + a.lds_btab_off);
+    unsigned long long *gpre = btab + (D + 1) * (DM + 1);         // task prefix per group
+
+    for (int i = tid; i < D; i += bs) nxs[i] = nxg[i];
+    for (int e = tid; e < (D + 1) * (DM + 1); e += bs) {
+        const int c = e / (DM + 1), i = e - c * (DM + 1);
+        btab[e] = pcg_binom(a.binom, c, i);
+    }
+    __syncthreads();
+    for (int e = tid; e < D * D; e += bs) {
+        const int t = e / D, k = e - t * D;
+        M[e] = a.C[(int64_t)nxs[t] * a.ldc + nxs[k]];
+    }
+    for (int t = tid; t < D; t += bs) {
+        const int yg = nxs[t];
+        Mx[t] = a.C[(int64_t)x * a.ldc + yg];
+        Md[t] = a.diag[yg];
+        const uint64_t *ar = a.adj + (int64_t)yg * a.W;
+        unsigned long long m = 0;
+        for (int k = 0; k < D; ++k) m |= ((ar[nxs[k] >> 6] >> (nxs[k] & 63)) & 1ull) << k;
+        lmask[t] = m;
+        uself[t] = 0;
+        uprop[t] = 0;
+    }
+    const int ng = (D - DM) / TG + 1;     // groups with g*TG <= D - d
+    if (tid == 0) {
+        int c = 0;
+        while (c < D && nxs[c] < x) ++c;
+        *s_tx = c;
+        unsigned long long acc = 0;
+        for (int g = 0; g < ng; ++g) {
+            gpre[g] = acc;
+            const int Dp = D - g * TG - 1;
+            acc += (Dp >= DT) ? btab[Dp * (DM + 1) + DT] : 0ull;
+        }
+        gpre[ng] = acc;
+    }
+    __syncthreads();
+    const int tx = *s_tx;
+    const double Cxx = a.diag[x];
+    const uint64_t ntask = gpre[ng];
+    const uint64_t r0 = (uint64_t)(chunk - a.cpre[x]) * (uint64_t)bs * (uint64_t)a.spl;
+    const uint64_t r1 = min(ntask, r0 + (uint64_t)bs * (uint64_t)a.spl);
+    unsigned long long tests = 0, indep = 0;
+
+    for (uint64_t task = r0 + tid; task < r1; task += bs) {
+        int g = 0;
+        while (g + 1 < ng && gpre[g + 1] <= task) ++g;
+        const int cbase = g * TG;
+        int T[DT];
+        {   // colex unrank of the (d-1)-subset over [cbase+1, D)
+            uint64_t rr = task - gpre[g];
+            int hi_ = D - cbase - 1;
+#pragma unroll
+            for (int ii = DT - 1; ii >= 0; --ii) {
+                int lo_ = ii, up = hi_ - 1;
+                while (lo_ < up) {
+                    const int mid = (lo_ + up + 1) >> 1;
+                    if (btab[mid * (DM + 1) + ii + 1] <= rr) lo_ = mid; else up = mid - 1;
+                }
+                T[ii] = lo_;
+                rr -= btab[lo_ * (DM + 1) + ii + 1];
+                hi_ = lo_;
+            }
+#pragma unroll
+            for (int ii = 0; ii < DT; ++ii) T[ii] += cbase + 1;
+        }
+        unsigned long long Tmask = 0;
+#pragma unroll
+        for (int i = 0; i < DT; ++i) Tmask |= 1ull << T[i];
+        // T-info: L_T, Li_T = L_T^-1, u_T = Li_T M_Tx
+        double L[DT][DT], Li[DT][DT], uT[DT];
+        bool okT = true;
+#pragma unroll
+        for (int j = 0; j < DT; ++j) {
+            double s = M[T[j] * D + T[j]];
+#pragma unroll
+            for (int q = 0; q < j; ++q) s -= L[j][q] * L[j][q];
+            okT = okT && (s > 0.0);
+            L[j][j] = sqrt(s);
+            const double r = 1.0 / L[j][j];
+#pragma unroll
+            for (int i = j + 1; i < DT; ++i) {
+                double t = M[T[i] * D + T[j]];
+#pragma unroll
+                for (int q = 0; q < j; ++q) t -= L[i][q] * L[j][q];
+                L[i][j] = t * r;
+            }
+            Li[j][j] = r;
+        }
+#pragma unroll
+        for (int i = 1; i < DT; ++i)
+#pragma unroll
+            for (int j = 0; j < i; ++j) {
+                double t = 0.0;
+#pragma unroll
+                for (int q = j; q < i; ++q) t += L[i][q] * Li[q][j];
+                Li[i][j] = -t * Li[i][i];
+            }
+        double uuT = 0.0;
+#pragma unroll
+        for (int i = 0; i < DT; ++i) {
+            double t = 0.0;
+#pragma unroll
+            for (int j = 0; j <= i; ++j) t += Li[i][j] * Mx[T[j]];
+            uT[i] = t;
+            uuT += t * t;
+        }
+        // c-data for the group
+        double lc[TG][DT], rl[TG], uc[TG], hc[TG];
+        bool okc[TG];
+#pragma unroll
+        for (int jj = 0; jj < TG; ++jj) {
+            const int c = cbase + jj;
+            const bool valid = c < T[0];
+            const int cc = valid ? c : 0;
+            double ll = 0.0;
+#pragma unroll
+            for (int i = 0; i < DT; ++i) {
+                double t = 0.0;
+#pragma unroll
+                for (int j = 0; j <= i; ++j) t += Li[i][j] * M[T[j] * D + cc];
+                lc[jj][i] = t;
+                ll += t * t;
+            }
+            const double lam2 = M[cc * D + cc] - ll;
+            const double r = 1.0 / sqrt(lam2);
+            double lu = 0.0;
+#pragma unroll
+            for (int i = 0; i < DT; ++i) lu += lc[jj][i] * uT[i];
+            const double u = (Mx[cc] - lu) * r;
+            const double cxx = Cxx - uuT - u * u;
+            rl[jj] = r;
+            uc[jj] = u;
+            hc[jj] = a.hi2 * cxx;
+            okc[jj] = valid && okT && (lam2 > 0.0) && (cxx > 0.0);
+        }
+        const double rratio = a.rmax2 / a.hi2;     // rmax2*cxx*cyy = (hi2*cxx*cyy) * rratio
+        const int cend = min(T[0], cbase + TG);      // valid candidates: c in [cbase, cend)
+
+        for (int t = 0; t < D; ++t) {
+            if ((Tmask >> t) & 1ull) continue;
+            const unsigned long long lm = lmask[t];
+            const bool inT = (lm & Tmask) == Tmask;
+            const bool own = (t < tx) && inT;
+            const double *Mt = M + t * D;
+            double vT[DT];
+            double vv = 0.0, uv = 0.0;
+#pragma unroll
+            for (int i = 0; i < DT; ++i) {
+                double v = 0.0;
+#pragma unroll
+                for (int j = 0; j <= i; ++j) v += Li[i][j] * Mt[T[j]];
+                vT[i] = v;
+                vv += v * v;
+                uv += uT[i] * v;
+            }
+            const double byy = Md[t] - vv;
+            const double bxy = Mx[t] - uv;
+            bool rare[TG];
+            bool anyrare = false;
+            // candidates c in S-side adjacency of an owned y are skipped (dedup, see k_level_lds)
+            const unsigned skipc = own ? (unsigned)(lm >> cbase) : 0u;
+#pragma unroll
+            for (int jj = 0; jj < TG; ++jj) {
+                const int c = cbase + jj;
+                const bool valid = c < cend;
+                // branch-free: every lane evaluates all TG candidates (no exec-mask splits)
+                const bool live = valid & (t != c) & !((skipc >> jj) & 1u);
+                double s = Mt[valid ? c : 0];
+#pragma unroll
+                for (int i = 0; i < DT; ++i) s -= lc[jj][i] * vT[i];
+                const double vc = s * rl[jj];
+                const double cyy = byy - vc * vc;
+                const double cxy = bxy - uc[jj] * vc;
+                const double num = cxy * cxy;
+                const double th = hc[jj] * cyy;
+                const bool dep = (num > th) & (num < th * rratio);
+                tests += live;
+                rare[jj] = live & !(okc[jj] & dep);
+                anyrare = anyrare | rare[jj];
+            }
+            if (__ballot(anyrare)) {
+                if (anyrare) {
+#pragma unroll
+                    for (int jj = 0; jj < TG; ++jj) {
+                        if (!rare[jj]) continue;
+                        const int c = cbase + jj;
+                        // recompute the decision pieces for this c (rare path)
+                        double s = Mt[c];
+#pragma unroll
+                        for (int i = 0; i < DT; ++i) s -= lc[jj][i] * vT[i];
+                        const double vc = s * rl[jj];
+                        const double cyy = byy - vc * vc;
+                        const double cxy = bxy - uc[jj] * vc;
+                        const double cxx = hc[jj] / a.hi2;
+                        const bool ind = okc[jj] && (cxy * cxy < a.lo2 * cxx * cyy) && (cyy > 0.0);
+                        const unsigned long long Smask = Tmask | (1ull << c);
+                        if (ind) {
+                            ++indep;
+                            atomicOr(&uself[t], Smask);
+                            if (((lm & Smask) == Smask) && t >= tx) atomicOr(&uprop[t], Smask);
+                        } else {
+                            int sg[DM];
+                            sg[0] = nxs[c];
+#pragma unroll
+                            for (int i = 0; i < DT; ++i) sg[i + 1] = nxs[T[i]];
+                            push_deferred(a, x, nxs[t], sg, DM);
+                        }
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // flush unions (local bits -> global node bits) and removal flags
+    for (int t = tid; t < D; t += bs) {
+        const unsigned long long us = uself[t], up = uprop[t];
+        if (!(us | up)) continue;
+        const int yg = nxs[t];
+        a.rm[(int64_t)x * a.n + yg] = 1;
+        a.rm[(int64_t)yg * a.n + x] = 1;
+        for (int side = 0; side < 2; ++side) {
+            const unsigned long long bits = side ? up : us;
+            if (!bits) continue;
+            const int64_t slot = side ? (int64_t)a.off[yg] + find_in_sorted(a.nbr + a.off[yg], a.deg[yg], x)
+                                      : (int64_t)a.off[x] + t;
+            unsigned long long *row = reinterpret_cast<unsigned long long *>(a.ug + slot * a.W);
+            unsigned long long m = bits;
+            while (m) {
+                const int b = __ffsll((long long)m) - 1;
+                const int gid = nxs[b];
+                atomicOr(&row[gid >> 6], 1ull << (gid & 63));
+                m &= m - 1;
+            }
+        }
+    }
+    tests = wave_sum(tests);
+    indep = wave_sum(indep);
+    if ((tid & 63) == 0) {
+        if (tests) atomicAdd(&a.ctr->tests, tests);
+        if (indep) atomicAdd(&a.ctr->indep, indep);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // depths > PCG_MAX_DEPTH (degenerate graphs, e.g. constant columns whose NaN correlations
 // never separate): one thread per (x, S rank), exact LU path per test with per-thread
 // scratch in global memory. Throughput is not the goal here; semantics are.
@@ -1077,7 +1357,19 @@ void launch_lds_mode(pcg_handle *h, const LevelArgs &a, int64_t nchunks, size_t 
 constexpr int SMALL_DEG = 64;        // LDS-resident kernel handles nodes with <= 64 neighbours
 
 size_t lds_small_core(int D) { return ((size_t)D * D * 8 + (size_t)D * (2 * 8 + 3 * 8 + 4) + 16 + 15) & ~(size_t)15; }
-size_t lds_small_bytes(int D) { return lds_small_core(D) + (size_t)(D + 1) * 5 * 8; }
+size_t lds_small_bytes(int D) { return lds_small_core(D) + (size_t)(D + 1) * 5 * 8 + 24 * 8; }
+
+// lane tasks of k_level_lds_t for a node of degree D at depth d (see the kernel)
+uint64_t tgroup_tasks(const pcg_handle *h, int D, int d) {
+    uint64_t acc = 0;
+    for (int g = 0; g * PCG_TGROUP <= D - d; ++g) {
+        const int Dp = D - g * PCG_TGROUP - 1;
+        if (Dp >= d - 1) acc += hbinom(h, Dp, d - 1);
+    }
+    return acc;
+}
+
+bool use_tgroup(int mode, int d) { return mode == MODE_DECIDE && d >= 2 && d <= 4; }
 
 int mode_of(const pcg_handle *h, int d) {
     if ((h->flags & PCG_FLAG_EXACT_ALL) || (double)h->N - d - 3 <= 0) return MODE_EXACT;
@@ -1203,11 +1495,18 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
     if (depth == 0) {
         h->chunk = 256;
         h->spl = 1;
+        h->tgroup = false;
         for (int x = 0; x <= n; ++x) cs[x] = x;
         for (int x = 0; x < n; ++x) h->work_h[x] = n - 1 - x;
         h->total_small = n;
         h->total_large = 0;
     } else {
+        // small class units: T-group lane tasks (threshold mode, depth 2..4) or S ranks
+        const bool tg = use_tgroup(mode_of(h, depth), depth);
+        h->tgroup = tg;
+        auto small_units = [&](int D) -> uint64_t {
+            return tg ? tgroup_tasks(h, D, depth) : hbinom(h, D, depth);
+        };
         double sum_small = 0.0, sum_large = 0.0;
         int cnt_large = 0;
         for (int x = 0; x < n; ++x) {
@@ -1218,12 +1517,12 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
                 return pcg_fail(h, PCG_ERR_INVALID, "depth %d work too large at node %d (deg %d)", depth, x, D);
             h->work_h[x] = (int64_t)ns * (D - depth);
             if (D <= SMALL_DEG && depth <= PCG_MAX_DEPTH) {
-                sum_small += (double)ns;
+                sum_small += (double)small_units(D);
                 h->maxdeg_small = std::max(h->maxdeg_small, D);
             }
             else { sum_large += (double)ns; ++cnt_large; }
         }
-        // ~4096 LDS-resident blocks per depth; each lane walks spl S ranks
+        // ~4096 LDS-resident blocks per depth; each lane walks spl units
         h->spl = (int)std::min(64.0, std::max(1.0, std::floor(sum_small / (256.0 * 4096.0))));
         const double mean_large = cnt_large ? sum_large / cnt_large : 0.0;
         h->chunk = (depth > PCG_MAX_DEPTH || mean_large <= 64) ? 64 : (mean_large <= 128 ? 128 : 256);
@@ -1234,9 +1533,8 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
             cl[x] = sl;
             const int D = h->deg_h[x];
             if (D < depth + 1) continue;
-            const uint64_t ns = hbinom(h, D, depth);
-            if (D <= SMALL_DEG && depth <= PCG_MAX_DEPTH) ss += (int64_t)((ns + csz - 1) / csz);
-            else sl += (int64_t)((ns + h->chunk - 1) / h->chunk);
+            if (D <= SMALL_DEG && depth <= PCG_MAX_DEPTH) ss += (int64_t)((small_units(D) + csz - 1) / csz);
+            else sl += (int64_t)((hbinom(h, D, depth) + h->chunk - 1) / h->chunk);
         }
         cs[n] = ss;
         cl[n] = sl;
@@ -1307,11 +1605,13 @@ extern "C" int pcg_level_chunk_work(pcg_handle *h, int64_t *prefix_host, int64_t
                 continue;
             }
             const int D = h->deg_h[x];
-            const uint64_t ns = hbinom(h, D, h->depth);
+            const bool tg = (cls == 0) && h->tgroup;
+            const uint64_t ns = tg ? tgroup_tasks(h, D, h->depth) : hbinom(h, D, h->depth);
+            const int64_t per_unit = (int64_t)(D - h->depth) * (tg ? PCG_TGROUP : 1);
             for (int64_t c = c0; c < c1; ++c) {
                 const uint64_t r0 = (uint64_t)(c - c0) * csz;
                 const uint64_t r1 = std::min<uint64_t>(r0 + csz, ns);
-                acc += (int64_t)(r1 - r0) * (D - h->depth) + 1;
+                acc += (int64_t)(r1 - r0) * per_unit + 1;
                 prefix_host[base + c + 1] = acc;
             }
         }
@@ -1343,7 +1643,12 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                     as.bs = 256;
                     as.lds_btab_off = (int)lds_small_core(h->maxdeg_small);
                     const size_t lds = lds_small_bytes(h->maxdeg_small);
-                    if (mode == MODE_DECIDE) launch_lds_mode<MODE_DECIDE>(h, as, s_hi - s_lo, lds);
+                    if (h->tgroup) {
+                        const dim3 grid((unsigned)(s_hi - s_lo)), block(256);
+                        if (d == 2) hipLaunchKernelGGL(k_level_lds_t<2>, grid, block, lds, h->stream, as);
+                        else if (d == 3) hipLaunchKernelGGL(k_level_lds_t<3>, grid, block, lds, h->stream, as);
+                        else hipLaunchKernelGGL(k_level_lds_t<4>, grid, block, lds, h->stream, as);
+                    } else if (mode == MODE_DECIDE) launch_lds_mode<MODE_DECIDE>(h, as, s_hi - s_lo, lds);
                     else if (mode == MODE_FULLP) launch_lds_mode<MODE_FULLP>(h, as, s_hi - s_lo, lds);
                     else launch_lds_mode<MODE_EXACT>(h, as, s_hi - s_lo, lds);
                 }

@@ -88,20 +88,31 @@ class GpuLevelBackend:
         return self.eng._collect(self.n, self.rl, self.stats, 0.0)
 
 
-def run_sharded_levels(backend, rank: int, world: int, max_depth: int = -1, group=None):
-    """The level loop shared by the GPU path and the CPU protocol test."""
+def run_sharded_levels(backend, rank: int, world: int, max_depth: int = -1, group=None, trace=None):
+    """The level loop shared by the GPU path and the CPU protocol test. ``trace`` (a list)
+    collects (phase, depth, seconds) host timings of begin / run / all_reduce / end."""
+    import time
+
     import torch.distributed as dist
     depth = 0
+    clock = time.perf_counter
     while True:
         if max_depth >= 0 and depth > max_depth:
             break
+        t0 = clock()
         prefix = backend.begin(depth)
         if prefix is None:
             break
         lo, hi = split_by_work(prefix, rank, world)
+        t1 = clock()
         backend.run(lo, hi)
+        t2 = clock()
         dist.all_reduce(backend.removal_tensor(), op=dist.ReduceOp.MAX, group=group)
+        t3 = clock()
         backend.end()
+        if trace is not None:
+            trace.extend([("begin", depth, t1 - t0), ("run", depth, t2 - t1),
+                          ("allreduce", depth, t3 - t2), ("end", depth, clock() - t3)])
         depth += 1
     return depth
 
@@ -144,17 +155,26 @@ def _allreduce_stats(stats: dict, device, group=None) -> dict:
     return out
 
 
-def sharded_skeleton(eng, C, N: int, alpha: float = 0.05, max_depth: int = -1, flags: int = 0, group=None):
+def sharded_skeleton(eng, C, N: int, alpha: float = 0.05, max_depth: int = -1, flags: int = 0, group=None,
+                     trace=None):
     """Edge-sharded skeleton over the ranks of ``group``; every rank returns the full result."""
+    import time
+
     import torch.distributed as dist
     rank, world = dist.get_rank(group), dist.get_world_size(group)
+    t0 = time.perf_counter()
     backend = GpuLevelBackend(eng, C, N, alpha, flags)
-    run_sharded_levels(backend, rank, world, max_depth=max_depth, group=group)
+    if trace is not None:
+        trace.append(("init", -1, time.perf_counter() - t0))
+    run_sharded_levels(backend, rank, world, max_depth=max_depth, group=group, trace=trace)
+    t0 = time.perf_counter()
     out = backend.finish()
     xy, bits = _allgather_rows(out.sep_xy_dev, out.sep_bits_dev, group=group)
     out.sep_xy_dev, out.sep_bits_dev = xy, bits
     out._host.clear()
     out.stats = _allreduce_stats(out.stats, eng.device, group=group)
+    if trace is not None:
+        trace.append(("gather", -1, time.perf_counter() - t0))
     return out
 
 

@@ -22,6 +22,8 @@ for step in "$@"; do
     bench) run bench 900 python bench.py --steps 3 --warmup 1 ;;
     benchfast) run bench 600 python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    dist2) PCG_DIST_TRACE=1 PCG_BENCH_DEVICE=0 PCG_DIST_BACKEND=gloo run dist2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 2 --warmup 1 ;;
+    sim) run sim 600 python tools/shard_sim.py ;;
     *) echo "unknown step $step" ;;
   esac
 done
