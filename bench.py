@@ -35,7 +35,7 @@ def flops_per_test(d: int) -> float:
     return (d + 2) ** 3 / 3.0 + 40.0
 
 
-def pmc_traffic(kernel_prefix: str):
+def pmc_traffic(kernel_prefix: str):  # exact rocprof kernel name (template args kept)
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC pass
     (profiles/*_pmc_summary.json, same bench command): FETCH_SIZE (KB, x2 for the gfx950
     half-count of wide reads, MI355X_MICROARCH.md §HBM) + WRITE_SIZE (KB). None if absent."""
@@ -45,11 +45,22 @@ def pmc_traffic(kernel_prefix: str):
         return None, None
     data = json.load(open(files[-1]))
     for name, ctr in data.items():
-        if kernel_prefix in name and "FETCH_SIZE" in ctr and "WRITE_SIZE" in ctr:
+        if name == kernel_prefix and "FETCH_SIZE" in ctr and "WRITE_SIZE" in ctr:
             fetch = ctr["FETCH_SIZE"]["per_dispatch_mean"] * 1024.0 * 2.0
             write = ctr["WRITE_SIZE"]["per_dispatch_mean"] * 1024.0
             return fetch + write, os.path.basename(files[-1])
     return None, None
+
+
+def dominant_kernel(d: int, full_p: bool) -> str:
+    """Name (as rocprofv3 prints it, template args kept) of the CI-test kernel that runs
+    depth ``d`` for nodes of degree <= 64 — the host dispatch in skeleton.hip
+    (``use_tgroup``: threshold mode at depths 2..4 uses the T-group kernel)."""
+    if d == 0:
+        return f"k_level0<{1 if full_p else 0}>"
+    if not full_p and 2 <= d <= 4:
+        return f"k_level_lds_t<{d}>"
+    return f"k_level_lds<{d}, {1 if full_p else 0}>"
 
 
 def parse():
@@ -195,14 +206,14 @@ def main():
     alg_flops = st["tests"][dmax] * flops_per_test(dmax)
     ach_gbs = alg_bytes / (k_ms / 1000.0) / 1e9 if k_ms > 0 else 0.0
     ach_tf = alg_flops / (k_ms / 1000.0) / 1e12 if k_ms > 0 else 0.0
-    kname = f"k_level_lds<{dmax}, {1 if args.full_p else 0}>" if dmax >= 1 else "k_level0"
+    kname = dominant_kernel(dmax, args.full_p)
     traffic, traffic_src = pmc_traffic(kname)
 
     if rank == 0:
         line = {
             "metric": METRIC, "value": value, "unit": "CI tests/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
-            "scaling": "strong" if world > 1 else "weak", "vs_baseline": None, "dtype": "f64",
+            "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic Gaussian SEM (rcaeval_amd.synth.gaussian_sem), resident in HBM",
             "config": {"workload": f"stable PC-fisherz skeleton, {args.n} vars x {args.samples} samples, "
                                    f"max depth {args.max_depth}, alpha {args.alpha}, seed {args.seed}, "
