@@ -39,7 +39,8 @@ extern "C" {
 #define PCG_ERR_DOMAIN -5    /* math domain error in the Fisher-z expression
                                 (Python math.log/sqrt raise ValueError) [U]          */
 #define PCG_ERR_RCCL -6      /* reserved: collective failure                          */
-#define PCG_ERR_OVERFLOW -7  /* an internal list overflowed its capacity (retried)    */
+#define PCG_ERR_OVERFLOW -7  /* an internal list overflowed its capacity: capacities were
+                                enlarged, rerun the skeleton (pcg_skeleton does so itself) */
 
 /* skeleton flags */
 #define PCG_FLAG_FULL_P 0x1   /* compute the Fisher-z p-value of every test (reference
@@ -140,8 +141,13 @@ int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi);
 int pcg_level_end(pcg_handle *h, pcg_stats *stats);
 /* Work weight of each chunk prefix (host out, total_chunks+1 int64) for load balance.  */
 int pcg_level_chunk_work(pcg_handle *h, int64_t *prefix_host, int64_t capacity);
-/* Use a caller-owned device buffer (n*n bytes, e.g. a torch tensor that the caller
- * all-reduces) for the per-depth removal flags instead of the handle's own; NULL = own.   */
+/* Use a caller-owned device buffer (n*n + PCG_RM_STATUS bytes, e.g. a torch tensor that
+ * the caller all-reduces with MAX) for the per-depth removal flags instead of the handle's
+ * own; NULL = own. The PCG_RM_STATUS bytes after the n*n flags carry level status that the
+ * merge spreads to every rank: [0] an exact-path/record list overflowed (pcg_level_end
+ * returns PCG_ERR_OVERFLOW on every rank: grow nothing, rerun the skeleton — capacities
+ * have already been enlarged), [1] a singular sub-matrix, [2] a math domain error.      */
+#define PCG_RM_STATUS 64
 int pcg_set_removal_buffer(pcg_handle *h, uint8_t *rm_dev, int64_t bytes);
 
 /* ---- K4: PageRank head -------------------------------------------------------------

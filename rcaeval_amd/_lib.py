@@ -26,6 +26,7 @@ PCG_FLAG_RECORD = 0x2
 PCG_FLAG_EXACT_ALL = 0x4
 
 PCG_MAX_LEVELS = 32
+PCG_RM_STATUS = 64          # status bytes after the n*n removal flags (pcgpu.h)
 PCG_MAX_DEPTH = 12
 
 I64 = ctypes.c_int64

@@ -35,6 +35,23 @@ bool pcg_ensure(pcg_handle *h, DevBuf &b, size_t bytes) {
     return true;
 }
 
+bool pcg_ensure_pinned(pcg_handle *h, PinBuf &b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (b.bytes >= bytes) return true;
+    if (b.p) {
+        hipStreamSynchronize(h->stream);
+        hipHostFree(b.p);
+        b.p = nullptr;
+        b.bytes = 0;
+    }
+    if (hipHostMalloc(&b.p, bytes, hipHostMallocDefault) != hipSuccess) {
+        b.p = nullptr;
+        return false;
+    }
+    b.bytes = bytes;
+    return true;
+}
+
 extern "C" int pcg_create(int device, pcg_handle **out) {
     if (!out) return PCG_ERR_INVALID;
     *out = nullptr;
@@ -67,6 +84,9 @@ extern "C" int pcg_destroy(pcg_handle *h) {
                       &h->colmean, &h->pr_scratch};
     for (DevBuf *b : bufs)
         if (b->p) hipFree(b->p);
+    PinBuf *pins[] = {&h->ctr_pin, &h->deg_pin, &h->off_pin, &h->cpre_pin, &h->status_pin};
+    for (PinBuf *b : pins)
+        if (b->p) hipHostFree(b->p);
     for (auto &e : h->ev)
         if (e) hipEventDestroy(e);
     if (h->own_stream && h->stream) hipStreamDestroy(h->stream);

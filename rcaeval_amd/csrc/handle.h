@@ -15,6 +15,11 @@ struct DevBuf {
     size_t bytes = 0;
 };
 
+struct PinBuf {                    // page-locked host staging (async per-level transfers)
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+
 // Device-side counters of one level (zeroed by pcg_level_begin).
 struct DevCounters {
     unsigned long long tests;      // unique tests evaluated
@@ -42,10 +47,11 @@ struct pcg_handle {
     // scratch
     DevBuf adj, deg, off, nbr, rm, ug, cpre, binom, ctr, deferred, records, nearbuf, exportbuf,
         export_xy, diag, colmean, pr_scratch;
+    PinBuf ctr_pin, deg_pin, off_pin, cpre_pin, status_pin;
     std::vector<uint64_t> binom_h;   // host copy of the binomial table
     uint8_t *rm_ext = nullptr;       // caller-owned removal-flag buffer (multi-GPU)
     int64_t rm_ext_bytes = 0;
-    int64_t rec_cap = 0, def_cap = 1 << 16, near_cap = 1 << 16;
+    int64_t rec_cap = 0, def_cap = 1 << 20, near_cap = 1 << 16;
     int64_t export_cap = 0;          // rows
     int64_t export_rows = 0;         // rows exported so far (host mirror)
     int binom_n = -1;                // binom table built for 0..binom_n
@@ -74,10 +80,12 @@ struct pcg_handle {
     int64_t rec_total = 0, near_total = 0;
     pcg_stats st{};
     float run_ms = 0.f;              // CI-test kernel time of the current level
+    bool run_timed = false;          // ev[2]/ev[3] bracket this level's CI-test kernels
 };
 
 int pcg_fail(pcg_handle *h, int code, const char *fmt, ...);
 bool pcg_ensure(pcg_handle *h, DevBuf &b, size_t bytes);   // grow-only allocation
+bool pcg_ensure_pinned(pcg_handle *h, PinBuf &b, size_t bytes);   // grow-only, page-locked
 
 #define PCG_HIP(h, expr)                                                                    \
     do {                                                                                    \

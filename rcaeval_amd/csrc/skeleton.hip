@@ -116,6 +116,15 @@ __device__ __forceinline__ void push_deferred(const LevelArgs &a, int x, int y, 
     }
 }
 
+// error bits (1 singular, 2 domain) into the level counters and into the status bytes that
+// follow the n*n removal flags, so a multi-GPU merge spreads them to every rank
+__device__ __forceinline__ void flag_error(const LevelArgs &a, int err) {
+    atomicOr(&a.ctr->error, (unsigned long long)err);
+    uint8_t *status = a.rm + (int64_t)a.n * a.n;
+    if (err & 1) status[1] = 1;
+    if (err & 2) status[2] = 1;
+}
+
 // 0 dependent, 1 independent, 2 exact path. p written in FULL_P mode.
 template <int MODE>
 __device__ __forceinline__ int decide(const LevelArgs &a, double cxy, double cxx, double cyy,
@@ -206,28 +215,43 @@ __global__ void k_apply(const uint8_t *rm, uint64_t *adj, int8_t *rl, int n, int
     if (m) adj[i] &= ~m;
 }
 
-// export non-empty union rows of removed ordered pairs
-__global__ void k_export(const int32_t *off, const int32_t *nbr, const uint8_t *rm,
-                         const uint64_t *ug, int n, int W, int64_t sumdeg, int32_t *xy,
-                         uint64_t *bits, int64_t cap, unsigned long long *ctr) {
+// export non-empty union rows of removed ordered pairs: one lane per CSR slot; the wave
+// compacts its non-empty rows with one atomic (ballot + mbcnt), so appends never chain
+// atomics serially.
+__global__ __launch_bounds__(256) void k_export(const int32_t *off, const int32_t *nbr, const uint8_t *rm,
+                                                const uint64_t *ug, int n, int W, int64_t sumdeg, int32_t *xy,
+                                                uint64_t *bits, int64_t cap, unsigned long long *ctr) {
+    const int lane = threadIdx.x & 63;
     const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (slot >= sumdeg) return;
-    int lo = 0, hi = n;  // off[lo] <= slot < off[hi]
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (off[mid] <= slot) lo = mid; else hi = mid;
+    int x = -1, y = -1;
+    bool keep = false;
+    const uint64_t *row = nullptr;
+    if (slot < sumdeg) {
+        int lo = 0, hi = n;  // off[lo] <= slot < off[hi]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (off[mid] <= slot) lo = mid; else hi = mid;
+        }
+        x = lo;
+        y = nbr[slot];
+        if (rm[(int64_t)x * n + y]) {
+            row = ug + slot * W;
+            uint64_t any = 0;
+            for (int w = 0; w < W; ++w) any |= row[w];
+            keep = any != 0;
+        }
     }
-    const int x = lo, y = nbr[slot];
-    if (!rm[(int64_t)x * n + y]) return;
-    const uint64_t *row = ug + slot * W;
-    uint64_t any = 0;
-    for (int w = 0; w < W; ++w) any |= row[w];
-    if (!any) return;
-    const unsigned long long r = atomicAdd(ctr, 1ull);
-    if ((int64_t)r >= cap) return;
+    const unsigned long long m = __ballot(keep);
+    if (!m) return;
+    unsigned long long base = 0;
+    if (lane == __ffsll((long long)m) - 1) base = atomicAdd(ctr, (unsigned long long)__popcll(m));
+    base = __shfl(base, __ffsll((long long)m) - 1);
+    if (!keep) return;
+    const int64_t r = (int64_t)base + __popcll(m & ((1ull << lane) - 1ull));
+    if (r >= cap) return;
     xy[2 * r] = x;
     xy[2 * r + 1] = y;
-    for (int w = 0; w < W; ++w) bits[(int64_t)r * W + w] = row[w];
+    for (int w = 0; w < W; ++w) bits[r * W + w] = row[w];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -844,8 +868,9 @@ __global__ __launch_bounds__(256, 4) void k_level_lds_t(LevelArgs a) {
     const int D = a.deg[x];
     const int32_t *nxg = a.nbr + a.off[x];
 
-    double *M = reinterpret_cast<double *>(smem);                 // D * D
-    double *Mx = M + D * D;                                       // D
+    const int DS = (D + 3) & ~3;                                  // row stride: 32-B aligned rows
+    double *M = reinterpret_cast<double *>(smem);                 // D * DS (columns >= D zero)
+    double *Mx = M + D * DS;                                      // D
     double *Md = Mx + D;                                          // D
     unsigned long long *lmask = reinterpret_cast<unsigned long long *>(Md + D);   // D
     unsigned long long *uself = lmask + D;                        // D
@@ -861,9 +886,9 @@ __global__ __launch_bounds__(256, 4) void k_level_lds_t(LevelArgs a) {
         btab[e] = pcg_binom(a.binom, c, i);
     }
     __syncthreads();
-    for (int e = tid; e < D * D; e += bs) {
-        const int t = e / D, k = e - t * D;
-        M[e] = a.C[(int64_t)nxs[t] * a.ldc + nxs[k]];
+    for (int e = tid; e < D * DS; e += bs) {
+        const int t = e / DS, k = e - t * DS;
+        M[e] = k < D ? a.C[(int64_t)nxs[t] * a.ldc + nxs[k]] : 0.0;
     }
     for (int t = tid; t < D; t += bs) {
         const int yg = nxs[t];
@@ -896,6 +921,7 @@ __global__ __launch_bounds__(256, 4) void k_level_lds_t(LevelArgs a) {
     const uint64_t r0 = (uint64_t)(chunk - a.cpre[x]) * (uint64_t)bs * (uint64_t)a.spl;
     const uint64_t r1 = min(ntask, r0 + (uint64_t)bs * (uint64_t)a.spl);
     unsigned long long tests = 0, indep = 0;
+    unsigned tcount = 0;
 
     for (uint64_t task = r0 + tid; task < r1; task += bs) {
         int g = 0;
@@ -927,7 +953,7 @@ __global__ __launch_bounds__(256, 4) void k_level_lds_t(LevelArgs a) {
         bool okT = true;
 #pragma unroll
         for (int j = 0; j < DT; ++j) {
-            double s = M[T[j] * D + T[j]];
+            double s = M[T[j] * DS + T[j]];
 #pragma unroll
             for (int q = 0; q < j; ++q) s -= L[j][q] * L[j][q];
             okT = okT && (s > 0.0);
@@ -935,7 +961,7 @@ __global__ __launch_bounds__(256, 4) void k_level_lds_t(LevelArgs a) {
             const double r = 1.0 / L[j][j];
 #pragma unroll
             for (int i = j + 1; i < DT; ++i) {
-                double t = M[T[i] * D + T[j]];
+                double t = M[T[i] * DS + T[j]];
 #pragma unroll
                 for (int q = 0; q < j; ++q) t -= L[i][q] * L[j][q];
                 L[i][j] = t * r;
@@ -973,11 +999,11 @@ __global__ __launch_bounds__(256, 4) void k_level_lds_t(LevelArgs a) {
             for (int i = 0; i < DT; ++i) {
                 double t = 0.0;
 #pragma unroll
-                for (int j = 0; j <= i; ++j) t += Li[i][j] * M[T[j] * D + cc];
+                for (int j = 0; j <= i; ++j) t += Li[i][j] * M[T[j] * DS + cc];
                 lc[jj][i] = t;
                 ll += t * t;
             }
-            const double lam2 = M[cc * D + cc] - ll;
+            const double lam2 = M[cc * DS + cc] - ll;
             const double r = 1.0 / sqrt(lam2);
             double lu = 0.0;
 #pragma unroll
@@ -990,14 +1016,23 @@ __global__ __launch_bounds__(256, 4) void k_level_lds_t(LevelArgs a) {
             okc[jj] = valid && okT && (lam2 > 0.0) && (cxx > 0.0);
         }
         const double rratio = a.rmax2 / a.hi2;     // rmax2*cxx*cyy = (hi2*cxx*cyy) * rratio
-        const int cend = min(T[0], cbase + TG);      // valid candidates: c in [cbase, cend)
+        const int cend = min(T[0], cbase + TG);      // valid candidates: c in [cbase, cend), >= 1 of them
+        unsigned okm = 0;                            // candidates usable on the fast path
+#pragma unroll
+        for (int jj = 0; jj < TG; ++jj) okm |= (unsigned)okc[jj] << jj;
+        const unsigned vmask = (1u << (cend - cbase)) - 1u;
 
         for (int t = 0; t < D; ++t) {
-            if ((Tmask >> t) & 1ull) continue;
+            // t in T: the lane idles through this y (branch-free: no exec-mask split)
+            const bool inTset = (Tmask >> t) & 1ull;
             const unsigned long long lm = lmask[t];
-            const bool inT = (lm & Tmask) == Tmask;
-            const bool own = (t < tx) && inT;
-            const double *Mt = M + t * D;
+            const bool own = (t < tx) && ((lm & Tmask) == Tmask);
+            const double *Mt = M + t * DS;
+            // the TG candidate operands M[t][cbase .. cbase+TG) are contiguous and 32-B aligned
+            // (DS % 4 == 0, cbase % 4 == 0): two 16-B LDS reads, broadcast across the lanes of
+            // the wave that share the group
+            const double2 m01 = *reinterpret_cast<const double2 *>(Mt + cbase);
+            const double2 m23 = *reinterpret_cast<const double2 *>(Mt + cbase + 2);
             double vT[DT];
             double vv = 0.0, uv = 0.0;
 #pragma unroll
@@ -1011,34 +1046,33 @@ __global__ __launch_bounds__(256, 4) void k_level_lds_t(LevelArgs a) {
             }
             const double byy = Md[t] - vv;
             const double bxy = Mx[t] - uv;
-            bool rare[TG];
-            bool anyrare = false;
-            // candidates c in S-side adjacency of an owned y are skipped (dedup, see k_level_lds)
-            const unsigned skipc = own ? (unsigned)(lm >> cbase) : 0u;
+            // live candidates: valid, c != y, and not deduplicated onto y (S in adj(y), y < x)
+            const unsigned tb = ((unsigned)(t - cbase) < (unsigned)TG) ? (1u << (t - cbase)) : 0u;
+            const unsigned skip = own ? (unsigned)(lm >> cbase) : 0u;
+            const unsigned live = inTset ? 0u : (vmask & ~tb & ~skip);
+            double sc[TG] = {m01.x, m01.y, m23.x, m23.y};
+            // TG independent chains, interleaved
+#pragma unroll
+            for (int i = 0; i < DT; ++i)
+#pragma unroll
+                for (int jj = 0; jj < TG; ++jj) sc[jj] -= lc[jj][i] * vT[i];
+            unsigned dep = 0;
 #pragma unroll
             for (int jj = 0; jj < TG; ++jj) {
-                const int c = cbase + jj;
-                const bool valid = c < cend;
-                // branch-free: every lane evaluates all TG candidates (no exec-mask splits)
-                const bool live = valid & (t != c) & !((skipc >> jj) & 1u);
-                double s = Mt[valid ? c : 0];
-#pragma unroll
-                for (int i = 0; i < DT; ++i) s -= lc[jj][i] * vT[i];
-                const double vc = s * rl[jj];
+                const double vc = sc[jj] * rl[jj];
                 const double cyy = byy - vc * vc;
                 const double cxy = bxy - uc[jj] * vc;
                 const double num = cxy * cxy;
                 const double th = hc[jj] * cyy;
-                const bool dep = (num > th) & (num < th * rratio);
-                tests += live;
-                rare[jj] = live & !(okc[jj] & dep);
-                anyrare = anyrare | rare[jj];
+                dep |= (unsigned)((num > th) & (num < th * rratio)) << jj;
             }
-            if (__ballot(anyrare)) {
-                if (anyrare) {
+            tcount += __popc(live);
+            const unsigned rare = live & ~(dep & okm);
+            if (__ballot(rare != 0u)) {
+                if (rare) {
 #pragma unroll
                     for (int jj = 0; jj < TG; ++jj) {
-                        if (!rare[jj]) continue;
+                        if (!((rare >> jj) & 1u)) continue;
                         const int c = cbase + jj;
                         // recompute the decision pieces for this c (rare path)
                         double s = Mt[c];
@@ -1065,6 +1099,8 @@ __global__ __launch_bounds__(256, 4) void k_level_lds_t(LevelArgs a) {
                 }
             }
         }
+        tests += tcount;
+        tcount = 0;
     }
     __syncthreads();
     // flush unions (local bits -> global node bits) and removal flags
@@ -1163,7 +1199,7 @@ __global__ __launch_bounds__(64) void k_level_deep(LevelArgs a, double *scratch,
                 if (prod < 0.0 || a.dof_negative) err = 2;
                 else pv = pcg_pvalue_from_r(-i01 / sqrt(prod), a.sqrt_dof, &err);
             }
-            if (err) { atomicOr(&a.ctr->error, (unsigned long long)err); continue; }
+            if (err) { flag_error(a, err); continue; }
             if (fabs(pv - a.alpha) < 1e-9) atomicAdd(&a.ctr->near_alpha, 1ull);
             if (pv > a.alpha) {
                 ++nindep;
@@ -1195,7 +1231,11 @@ __global__ void k_exact(LevelArgs a) {
     double *B0 = A + m * m;
     double *B1 = B0 + m;
     int piv[PCG_MAX_DEPTH + 2];
-    const int64_t count = (int64_t)min((unsigned long long)a.def_cap, a.ctr->deferred);
+    const unsigned long long pushed = a.ctr->deferred;
+    const int64_t count = (int64_t)min((unsigned long long)a.def_cap, pushed);
+    if (blockIdx.x == 0 && threadIdx.x == 0 &&
+        ((int64_t)pushed > a.def_cap || (a.record && (int64_t)a.ctr->records > a.rec_cap)))
+        a.rm[(int64_t)a.n * a.n] = 1;      // overflow: every rank reruns (status byte 0)
     unsigned long long nexact = 0, nindep = 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count;
          i += (int64_t)gridDim.x * blockDim.x) {
@@ -1221,7 +1261,7 @@ __global__ void k_exact(LevelArgs a) {
             }
         }
         ++nexact;
-        if (err) { atomicOr(&a.ctr->error, (unsigned long long)err); continue; }
+        if (err) { flag_error(a, err); continue; }
         if (a.record) push_record(a.records, a.rec_cap, &a.ctr->records, lo_, hi_, d, e.s, p);
         if (fabs(p - a.alpha) < 1e-9) push_record(a.nearl, a.near_cap, &a.ctr->near_alpha, lo_, hi_, d, e.s, p);
         if (p > a.alpha) {
@@ -1356,7 +1396,8 @@ void launch_lds_mode(pcg_handle *h, const LevelArgs &a, int64_t nchunks, size_t 
 
 constexpr int SMALL_DEG = 64;        // LDS-resident kernel handles nodes with <= 64 neighbours
 
-size_t lds_small_core(int D) { return ((size_t)D * D * 8 + (size_t)D * (2 * 8 + 3 * 8 + 4) + 16 + 15) & ~(size_t)15; }
+size_t lds_small_core(int D) {  // k_level_lds_t is sized with D rounded up to 4 (its row stride)
+ return ((size_t)D * D * 8 + (size_t)D * (2 * 8 + 3 * 8 + 4) + 16 + 15) & ~(size_t)15; }
 size_t lds_small_bytes(int D) { return lds_small_core(D) + (size_t)(D + 1) * 5 * 8 + 24 * 8; }
 
 // lane tasks of k_level_lds_t for a node of degree D at depth d (see the kernel)
@@ -1377,30 +1418,36 @@ int mode_of(const pcg_handle *h, int d) {
     return MODE_DECIDE;
 }
 
-// degrees + CSR neighbour lists from the current adjacency; degrees copied to the host
-int refresh_graph(pcg_handle *h) {
+// degrees of the current adjacency -> page-locked host mirror (async; the caller syncs)
+int graph_launch(pcg_handle *h) {
     const int n = (int)h->n, W = h->W;
+    if (!pcg_ensure_pinned(h, h->deg_pin, sizeof(int32_t) * n)) return pcg_fail(h, PCG_ERR_OOM, "pinned degrees");
     hipLaunchKernelGGL(k_degrees, dim3((n + 255) / 256), dim3(256), 0, h->stream,
                        (const uint64_t *)h->adj.p, n, W, (int32_t *)h->deg.p);
-    h->deg_h.resize(n);
-    PCG_HIP(h, hipMemcpyAsync(h->deg_h.data(), h->deg.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost,
-                              h->stream));
-    PCG_HIP(h, hipStreamSynchronize(h->stream));
-    std::vector<int32_t> off(n + 1, 0);
+    PCG_HIP(h, hipMemcpyAsync(h->deg_pin.p, h->deg.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, h->stream));
+    return PCG_OK;
+}
+
+// after the sync: host degrees, CSR offsets (uploaded async), ascending neighbour lists
+int graph_finish(pcg_handle *h) {
+    const int n = (int)h->n, W = h->W;
+    const int32_t *dp = (const int32_t *)h->deg_pin.p;
+    h->deg_h.assign(dp, dp + n);
+    if (!pcg_ensure_pinned(h, h->off_pin, sizeof(int32_t) * (n + 1))) return pcg_fail(h, PCG_ERR_OOM, "pinned offsets");
+    int32_t *off = (int32_t *)h->off_pin.p;
     int64_t s = 0;
     int32_t mx = 0;
     for (int i = 0; i < n; ++i) {
         off[i] = (int32_t)s;
-        s += h->deg_h[i];
-        mx = std::max(mx, h->deg_h[i]);
+        s += dp[i];
+        mx = std::max(mx, dp[i]);
     }
     off[n] = (int32_t)s;
     h->sumdeg = s;
     h->maxdeg = mx;
     if (!pcg_ensure(h, h->off, sizeof(int32_t) * (n + 1))) return PCG_ERR_OOM;
     if (!pcg_ensure(h, h->nbr, sizeof(int32_t) * std::max<int64_t>(s, 1))) return PCG_ERR_OOM;
-    PCG_HIP(h, hipMemcpyAsync(h->off.p, off.data(), sizeof(int32_t) * (n + 1), hipMemcpyHostToDevice,
-                              h->stream));
+    PCG_HIP(h, hipMemcpyAsync(h->off.p, off, sizeof(int32_t) * (n + 1), hipMemcpyHostToDevice, h->stream));
     hipLaunchKernelGGL(k_fill_nbr, dim3(n), dim3(64), 0, h->stream, (const uint64_t *)h->adj.p, n, W,
                        (const int32_t *)h->off.p, (int32_t *)h->nbr.p);
     PCG_HIP(h, hipGetLastError());
@@ -1423,9 +1470,9 @@ extern "C" int pcg_skeleton_init(pcg_handle *h, const double *C, int64_t n, int6
         return pcg_fail(h, PCG_ERR_INVALID, "pcg_skeleton_init: invalid arguments (n=%lld)", (long long)n);
     if (n > INT32_MAX / 2) return pcg_fail(h, PCG_ERR_INVALID, "n too large");
     PCG_HIP(h, hipSetDevice(h->device));
-    if (h->rm_ext && h->rm_ext_bytes < n * n)
-        return pcg_fail(h, PCG_ERR_INVALID, "removal buffer too small (%lld < %lld)", (long long)h->rm_ext_bytes,
-                        (long long)(n * n));
+    if (h->rm_ext && h->rm_ext_bytes < n * n + PCG_RM_STATUS)
+        return pcg_fail(h, PCG_ERR_INVALID, "removal buffer too small (%lld < n*n + PCG_RM_STATUS = %lld)",
+                        (long long)h->rm_ext_bytes, (long long)(n * n + PCG_RM_STATUS));
     h->C = C; h->n = n; h->ldc = ldc; h->N = N; h->alpha = alpha; h->flags = flags;
     h->rl = removed_level;
     h->W = (int)((n + 63) / 64);
@@ -1437,7 +1484,7 @@ extern "C" int pcg_skeleton_init(pcg_handle *h, const double *C, int64_t n, int6
     memset(&h->st, 0, sizeof(h->st));
     const int W = h->W;
     if (!pcg_ensure(h, h->adj, sizeof(uint64_t) * n * W) || !pcg_ensure(h, h->deg, sizeof(int32_t) * n) ||
-        !pcg_ensure(h, h->diag, sizeof(double) * n) || !pcg_ensure(h, h->rm, (size_t)n * n) ||
+        !pcg_ensure(h, h->diag, sizeof(double) * n) || !pcg_ensure(h, h->rm, (size_t)n * n + PCG_RM_STATUS) ||
         !pcg_ensure(h, h->ctr, sizeof(DevCounters)) ||
         !pcg_ensure(h, h->deferred, sizeof(DeferredEntry) * h->def_cap) ||
         !pcg_ensure(h, h->nearbuf, sizeof(pcg_record) * h->near_cap) ||
@@ -1457,7 +1504,10 @@ extern "C" int pcg_skeleton_init(pcg_handle *h, const double *C, int64_t n, int6
                        (double *)h->diag.p);
     PCG_HIP(h, hipMemsetAsync(removed_level, 0xFF, (size_t)n * n, h->stream));
     PCG_HIP(h, hipGetLastError());
-    return refresh_graph(h);
+    int rc = graph_launch(h);
+    if (rc) return rc;
+    PCG_HIP(h, hipStreamSynchronize(h->stream));
+    return graph_finish(h);
 }
 
 extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, int32_t *max_degree,
@@ -1478,25 +1528,30 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
     h->deg_levels.insert(h->deg_levels.end(), h->deg_h.begin(), h->deg_h.end());
     h->st.max_degree[depth] = h->maxdeg;
     h->st.levels = depth + 1;
+    // per-degree tables: the decomposition below is O(n) lookups (it sits between two
+    // device phases of the level loop, so it is on the critical path)
+    const int maxd = h->maxdeg;
+    std::vector<int64_t> hist(maxd + 1, 0);
+    for (int x = 0; x < n; ++x) ++hist[h->deg_h[x]];
     // calls-equivalent: sum_x D_x * C(D_x - 1, d) (ci_test invocations incl. cache hits)
     int64_t calls = 0;
-    for (int x = 0; x < n; ++x) {
-        const int D = h->deg_h[x];
-        if (D < depth - 1) continue;
+    for (int D = std::max(depth - 1, 0); D <= maxd; ++D) {
+        if (!hist[D]) continue;
         const uint64_t c = hbinom(h, D - 1, depth);
-        calls += (int64_t)std::min<uint64_t>(c, (uint64_t)INT64_MAX / 4096) * D;
+        calls += (int64_t)std::min<uint64_t>(c, (uint64_t)INT64_MAX / 4096) * D * hist[D];
     }
     h->st.calls[depth] = calls;
     // work decomposition: depth 0 = one chunk per row; depth >= 1 = two node classes
-    h->cpre_h.assign(2 * (n + 1), 0);
+    if (!pcg_ensure_pinned(h, h->cpre_pin, sizeof(int64_t) * 2 * (n + 1)))
+        return pcg_fail(h, PCG_ERR_OOM, "pinned chunk prefix");
+    int64_t *cs = (int64_t *)h->cpre_pin.p, *cl = cs + (n + 1);
     h->work_h.assign(n, 0);
-    int64_t *cs = h->cpre_h.data(), *cl = h->cpre_h.data() + (n + 1);
     h->maxdeg_small = 0;
     if (depth == 0) {
         h->chunk = 256;
         h->spl = 1;
         h->tgroup = false;
-        for (int x = 0; x <= n; ++x) cs[x] = x;
+        for (int x = 0; x <= n; ++x) { cs[x] = x; cl[x] = 0; }
         for (int x = 0; x < n; ++x) h->work_h[x] = n - 1 - x;
         h->total_small = n;
         h->total_large = 0;
@@ -1504,37 +1559,45 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
         // small class units: T-group lane tasks (threshold mode, depth 2..4) or S ranks
         const bool tg = use_tgroup(mode_of(h, depth), depth);
         h->tgroup = tg;
-        auto small_units = [&](int D) -> uint64_t {
-            return tg ? tgroup_tasks(h, D, depth) : hbinom(h, D, depth);
-        };
+        std::vector<uint64_t> ns_of(maxd + 1, 0), units_of(maxd + 1, 0);
         double sum_small = 0.0, sum_large = 0.0;
         int cnt_large = 0;
-        for (int x = 0; x < n; ++x) {
-            const int D = h->deg_h[x];
-            if (D < depth + 1) continue;
+        for (int D = depth + 1; D <= maxd; ++D) {
             const uint64_t ns = hbinom(h, D, depth);
-            if (ns > ((uint64_t)1 << 46))
-                return pcg_fail(h, PCG_ERR_INVALID, "depth %d work too large at node %d (deg %d)", depth, x, D);
-            h->work_h[x] = (int64_t)ns * (D - depth);
-            if (D <= SMALL_DEG && depth <= PCG_MAX_DEPTH) {
-                sum_small += (double)small_units(D);
-                h->maxdeg_small = std::max(h->maxdeg_small, D);
+            if (hist[D] && ns > ((uint64_t)1 << 46))
+                return pcg_fail(h, PCG_ERR_INVALID, "depth %d work too large (deg %d)", depth, D);
+            ns_of[D] = ns;
+            const bool small = D <= SMALL_DEG && depth <= PCG_MAX_DEPTH;
+            units_of[D] = small ? (tg ? tgroup_tasks(h, D, depth) : ns) : ns;
+            if (!hist[D]) continue;
+            if (small) {
+                sum_small += (double)units_of[D] * hist[D];
+                h->maxdeg_small = D;
+            } else {
+                sum_large += (double)ns * hist[D];
+                cnt_large += (int)hist[D];
             }
-            else { sum_large += (double)ns; ++cnt_large; }
         }
         // ~4096 LDS-resident blocks per depth; each lane walks spl units
         h->spl = (int)std::min(64.0, std::max(1.0, std::floor(sum_small / (256.0 * 4096.0))));
         const double mean_large = cnt_large ? sum_large / cnt_large : 0.0;
         h->chunk = (depth > PCG_MAX_DEPTH || mean_large <= 64) ? 64 : (mean_large <= 128 ? 128 : 256);
         const uint64_t csz = (uint64_t)256 * h->spl;
+        std::vector<int64_t> nch_of(maxd + 1, 0);
+        for (int D = depth + 1; D <= maxd; ++D) {
+            const bool small = D <= SMALL_DEG && depth <= PCG_MAX_DEPTH;
+            nch_of[D] = small ? (int64_t)((units_of[D] + csz - 1) / csz)
+                              : (int64_t)((ns_of[D] + h->chunk - 1) / h->chunk);
+        }
         int64_t ss = 0, sl = 0;
         for (int x = 0; x < n; ++x) {
             cs[x] = ss;
             cl[x] = sl;
             const int D = h->deg_h[x];
             if (D < depth + 1) continue;
-            if (D <= SMALL_DEG && depth <= PCG_MAX_DEPTH) ss += (int64_t)((small_units(D) + csz - 1) / csz);
-            else sl += (int64_t)((hbinom(h, D, depth) + h->chunk - 1) / h->chunk);
+            h->work_h[x] = (int64_t)ns_of[D] * (D - depth);
+            if (D <= SMALL_DEG && depth <= PCG_MAX_DEPTH) ss += nch_of[D];
+            else sl += nch_of[D];
         }
         cs[n] = ss;
         cl[n] = sl;
@@ -1544,36 +1607,22 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
     h->total_chunks = h->total_small + h->total_large;
     if (total_chunks) *total_chunks = h->total_chunks;
     if (!pcg_ensure(h, h->cpre, sizeof(int64_t) * 2 * (n + 1))) return PCG_ERR_OOM;
-    PCG_HIP(h, hipMemcpyAsync(h->cpre.p, h->cpre_h.data(), sizeof(int64_t) * 2 * (n + 1), hipMemcpyHostToDevice,
+    PCG_HIP(h, hipMemcpyAsync(h->cpre.p, h->cpre_pin.p, sizeof(int64_t) * 2 * (n + 1), hipMemcpyHostToDevice,
                               h->stream));
-    PCG_HIP(h, hipMemsetAsync(h->rm_ext ? (void *)h->rm_ext : h->rm.p, 0, (size_t)n * n, h->stream));
+    PCG_HIP(h, hipMemsetAsync(h->rm_ext ? (void *)h->rm_ext : h->rm.p, 0, (size_t)n * n + PCG_RM_STATUS, h->stream));
     PCG_HIP(h, hipMemsetAsync(h->ctr.p, 0, sizeof(DevCounters), h->stream));
     if (depth >= 1) {
         const size_t ugb = sizeof(uint64_t) * (size_t)std::max<int64_t>(h->sumdeg, 1) * h->W;
         if (!pcg_ensure(h, h->ug, ugb)) return pcg_fail(h, PCG_ERR_OOM, "sepset union rows (%zu B)", ugb);
         PCG_HIP(h, hipMemsetAsync(h->ug.p, 0, ugb, h->stream));
-        if (h->export_cap == 0) {  // every ordered pair is removed at most once
-            h->export_cap = std::max<int64_t>(h->sumdeg, 1);
-            if (!pcg_ensure(h, h->exportbuf, sizeof(uint64_t) * h->export_cap * h->W) ||
-                !pcg_ensure(h, h->export_xy, sizeof(int32_t) * 2 * h->export_cap))
+        if (depth == 1 || h->export_cap == 0) {
+            // every ordered pair adjacent at depth 1 is exported at most once over all depths
+            // (depth-0 removals carry empty sepsets), so one allocation covers the run
+            const int64_t cap = std::max<int64_t>(h->sumdeg, 1);
+            if (!pcg_ensure(h, h->exportbuf, sizeof(uint64_t) * cap * h->W) ||
+                !pcg_ensure(h, h->export_xy, sizeof(int32_t) * 2 * cap))
                 return pcg_fail(h, PCG_ERR_OOM, "sepset export buffer");
-        } else if (h->export_rows + h->sumdeg > h->export_cap) {
-            // grow, preserving exported rows
-            const int64_t ncap = h->export_rows + h->sumdeg;
-            DevBuf nb, nx;
-            if (hipMalloc(&nb.p, sizeof(uint64_t) * ncap * h->W) != hipSuccess ||
-                hipMalloc(&nx.p, sizeof(int32_t) * 2 * ncap) != hipSuccess)
-                return pcg_fail(h, PCG_ERR_OOM, "sepset export buffer growth");
-            PCG_HIP(h, hipMemcpyAsync(nb.p, h->exportbuf.p, sizeof(uint64_t) * h->export_rows * h->W,
-                                      hipMemcpyDeviceToDevice, h->stream));
-            PCG_HIP(h, hipMemcpyAsync(nx.p, h->export_xy.p, sizeof(int32_t) * 2 * h->export_rows,
-                                      hipMemcpyDeviceToDevice, h->stream));
-            PCG_HIP(h, hipStreamSynchronize(h->stream));
-            hipFree(h->exportbuf.p);
-            hipFree(h->export_xy.p);
-            h->exportbuf = {nb.p, sizeof(uint64_t) * ncap * h->W};
-            h->export_xy = {nx.p, sizeof(int32_t) * 2 * ncap};
-            h->export_cap = ncap;
+            h->export_cap = cap;
         }
     }
     return PCG_OK;
@@ -1593,7 +1642,7 @@ extern "C" int pcg_level_chunk_work(pcg_handle *h, int64_t *prefix_host, int64_t
     int64_t acc = 0;
     prefix_host[0] = 0;
     for (int cls = 0; cls < 2; ++cls) {
-        const int64_t *cp = h->cpre_h.data() + cls * (n + 1);
+        const int64_t *cp = (const int64_t *)h->cpre_pin.p + cls * (n + 1);
         const int64_t base = cls ? h->total_small : 0;
         const uint64_t csz = cls ? (uint64_t)h->chunk : (uint64_t)256 * h->spl;
         for (int x = 0; x < n; ++x) {
@@ -1624,7 +1673,7 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
         return pcg_fail(h, PCG_ERR_INVALID, "pcg_level_run: chunk range");
     const int d = h->depth;
     const int mode = mode_of(h, d);
-    for (int attempt = 0; attempt < 8; ++attempt) {
+    {
         LevelArgs a = make_args(h, d, mode == MODE_EXACT);
         a.chunk_lo = chunk_lo;
         const int64_t nch = chunk_hi - chunk_lo;
@@ -1641,8 +1690,9 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                     LevelArgs as = a;
                     as.chunk_lo = s_lo;
                     as.bs = 256;
-                    as.lds_btab_off = (int)lds_small_core(h->maxdeg_small);
-                    const size_t lds = lds_small_bytes(h->maxdeg_small);
+                    const int dl = h->tgroup ? (h->maxdeg_small + 3) & ~3 : h->maxdeg_small;
+                    as.lds_btab_off = (int)lds_small_core(dl);
+                    const size_t lds = lds_small_bytes(dl);
                     if (h->tgroup) {
                         const dim3 grid((unsigned)(s_hi - s_lo)), block(256);
                         if (d == 2) hipLaunchKernelGGL(k_level_lds_t<2>, grid, block, lds, h->stream, as);
@@ -1681,53 +1731,57 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
         }
         PCG_HIP(h, hipGetLastError());
         PCG_HIP(h, hipEventRecord(h->ev[3], h->stream));
-        DevCounters c{};
-        PCG_HIP(h, hipMemcpyAsync(&c, h->ctr.p, sizeof(c), hipMemcpyDeviceToHost, h->stream));
-        PCG_HIP(h, hipStreamSynchronize(h->stream));
-        PCG_HIP(h, hipEventElapsedTime(&h->run_ms, h->ev[2], h->ev[3]));
-        const bool def_over = (int64_t)c.deferred > h->def_cap;
-        const bool rec_over = a.record && (int64_t)c.records > h->rec_cap;
-        if (def_over || rec_over) {
-            if (def_over) {
-                h->def_cap = (int64_t)c.deferred + (int64_t)c.deferred / 4 + 1024;
-                if (!pcg_ensure(h, h->deferred, sizeof(DeferredEntry) * h->def_cap))
-                    return pcg_fail(h, PCG_ERR_OOM, "deferred list (%lld)", (long long)h->def_cap);
-            }
-            if (rec_over) {
-                h->rec_cap = (int64_t)c.records * 2 + 1024;
-                if (!pcg_ensure(h, h->records, sizeof(pcg_record) * h->rec_cap))
-                    return pcg_fail(h, PCG_ERR_OOM, "record buffer (%lld)", (long long)h->rec_cap);
-            }
-            // idempotent re-run: flags/unions are OR-only; counters restart
-            PCG_HIP(h, hipMemsetAsync(h->ctr.p, 0, sizeof(DevCounters), h->stream));
-            continue;
-        }
-        if (c.deferred > 0) {
-            a = make_args(h, d, mode == MODE_EXACT);
-            const int m = d + 2;
-            const int per = (m * m + 2 * m) * 8;
-            const int bs = per * 64 <= 64 * 1024 ? 64 : 32;
-            const int64_t nb = std::min<int64_t>(((int64_t)c.deferred + bs - 1) / bs, 4096);
-            hipLaunchKernelGGL(k_exact, dim3((unsigned)nb), dim3(bs), (size_t)per * bs, h->stream, a);
-            PCG_HIP(h, hipGetLastError());
-        }
+        h->run_timed = true;
+        // exact path over the deferred list; the kernel reads the list length on the device
+        // (no host round trip) and raises the overflow status byte if the list overflowed
+        a = make_args(h, d, mode == MODE_EXACT);
+        const int m = d + 2;
+        const int per = (m * m + 2 * m) * 8;
+        const int bs = per * 64 <= 64 * 1024 ? 64 : 32;
+        hipLaunchKernelGGL(k_exact, dim3(512), dim3(bs), (size_t)per * bs, h->stream, a);
+        PCG_HIP(h, hipGetLastError());
         return PCG_OK;
     }
-    return pcg_fail(h, PCG_ERR_OVERFLOW, "level %d: list capacity kept overflowing", d);
 }
 
 extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
     if (!h || h->depth < 0) return pcg_fail(h, PCG_ERR_INVALID, "pcg_level_end without begin");
     const int d = h->depth, n = (int)h->n, W = h->W;
-    DevCounters c{};
-    PCG_HIP(h, hipMemcpyAsync(&c, h->ctr.p, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+    uint8_t *rmb = h->rm_ext ? h->rm_ext : (uint8_t *)h->rm.p;
+    DevCounters *ctr = (DevCounters *)h->ctr.p;
+    // everything below is stream-ordered; the level costs ONE host sync: export the unions of
+    // removed pairs (device-side append), apply the removals (SkeletonDiscovery.py:141-144),
+    // recount degrees, and fetch counters + status + degrees in one batch
+    const int64_t room = h->export_cap - h->export_rows;
+    if (d >= 1 && h->sumdeg > 0)
+        hipLaunchKernelGGL(k_export, dim3((unsigned)((h->sumdeg + 255) / 256)), dim3(256), 0, h->stream,
+                           (const int32_t *)h->off.p, (const int32_t *)h->nbr.p, (const uint8_t *)rmb,
+                           (const uint64_t *)h->ug.p, n, W, h->sumdeg,
+                           (int32_t *)h->export_xy.p + 2 * h->export_rows,
+                           (uint64_t *)h->exportbuf.p + h->export_rows * W, room, &ctr->exported);
+    const int64_t nw = (int64_t)n * W;
+    hipLaunchKernelGGL(k_apply, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, h->stream, (const uint8_t *)rmb,
+                       (uint64_t *)h->adj.p, h->rl, n, W, d);
+    PCG_HIP(h, hipGetLastError());
+    int rc = graph_launch(h);
+    if (rc) return rc;
+    if (!pcg_ensure_pinned(h, h->ctr_pin, sizeof(DevCounters)) || !pcg_ensure_pinned(h, h->status_pin, 16))
+        return pcg_fail(h, PCG_ERR_OOM, "pinned counters");
+    PCG_HIP(h, hipMemcpyAsync(h->ctr_pin.p, ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, h->stream));
+    PCG_HIP(h, hipMemcpyAsync(h->status_pin.p, rmb + (int64_t)n * n, 4, hipMemcpyDeviceToHost, h->stream));
     PCG_HIP(h, hipStreamSynchronize(h->stream));
-    // records / near-alpha to host
-    if ((h->flags & PCG_FLAG_RECORD) && c.records) {
-        const int64_t k = std::min<int64_t>((int64_t)c.records, h->rec_cap);
+    const DevCounters c = *(const DevCounters *)h->ctr_pin.p;
+    const uint8_t *status = (const uint8_t *)h->status_pin.p;
+    if (h->run_timed) {
+        PCG_HIP(h, hipEventElapsedTime(&h->run_ms, h->ev[2], h->ev[3]));
+        h->run_timed = false;
+    }
+    // records / near-alpha to host (parity runs; before the next level reuses the buffers)
+    if ((h->flags & PCG_FLAG_RECORD) && c.records && (int64_t)c.records <= h->rec_cap) {
         const size_t old = h->rec_h.size();
-        h->rec_h.resize(old + k);
-        PCG_HIP(h, hipMemcpy(h->rec_h.data() + old, h->records.p, sizeof(pcg_record) * k, hipMemcpyDeviceToHost));
+        h->rec_h.resize(old + c.records);
+        PCG_HIP(h, hipMemcpy(h->rec_h.data() + old, h->records.p, sizeof(pcg_record) * c.records,
+                             hipMemcpyDeviceToHost));
     }
     if (c.near_alpha) {
         const int64_t k = std::min<int64_t>((int64_t)c.near_alpha, h->near_cap);
@@ -1740,45 +1794,36 @@ extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
     h->st.exact[d] = (int64_t)c.exact;
     h->st.near_alpha[d] = (int64_t)c.near_alpha;
     h->st.kernel_ms[d] = h->run_ms;
-    if (c.error) {
-        h->st.error = (c.error & 1) ? PCG_ERR_SINGULAR : PCG_ERR_DOMAIN;
+    if (status[0]) {
+        // some rank's exact-path (or record) list overflowed: the level is incomplete on every
+        // rank. Enlarge and let the driver rerun the skeleton (pcg_skeleton does it itself).
+        h->def_cap = std::max<int64_t>(h->def_cap * 4, (int64_t)c.deferred * 2);
+        if (h->flags & PCG_FLAG_RECORD) h->rec_cap = std::max<int64_t>(h->rec_cap * 4, (int64_t)c.records * 2);
+        if (stats) *stats = h->st;
+        return pcg_fail(h, PCG_ERR_OVERFLOW, "level %d: exact-path list overflowed; capacity raised to %lld, rerun",
+                        d, (long long)h->def_cap);
+    }
+    if (c.error || status[1] || status[2]) {
+        const bool singular = (c.error & 1) || status[1];
+        h->st.error = singular ? PCG_ERR_SINGULAR : PCG_ERR_DOMAIN;
         if (stats) *stats = h->st;
         return pcg_fail(h, h->st.error,
-                        (c.error & 1) ? "Data correlation matrix is singular. Cannot run fisherz test. Please check your data."
-                                      : "math domain error");
+                        singular ? "Data correlation matrix is singular. Cannot run fisherz test. Please check your data."
+                                 : "math domain error");
     }
-    // export unions of removed pairs, then apply the removals
     if (d >= 1 && h->sumdeg > 0) {
-        PCG_HIP(h, hipMemsetAsync(&((DevCounters *)h->ctr.p)->exported, 0, sizeof(unsigned long long), h->stream));
-        const int64_t room = h->export_cap - h->export_rows;
-        hipLaunchKernelGGL(k_export, dim3((unsigned)((h->sumdeg + 255) / 256)), dim3(256), 0, h->stream,
-                           (const int32_t *)h->off.p, (const int32_t *)h->nbr.p,
-                           h->rm_ext ? (const uint8_t *)h->rm_ext : (const uint8_t *)h->rm.p,
-                           (const uint64_t *)h->ug.p, n, W, h->sumdeg,
-                           (int32_t *)h->export_xy.p + 2 * h->export_rows,
-                           (uint64_t *)h->exportbuf.p + h->export_rows * W, room,
-                           &((DevCounters *)h->ctr.p)->exported);
-        unsigned long long ex = 0;
-        PCG_HIP(h, hipMemcpyAsync(&ex, &((DevCounters *)h->ctr.p)->exported, sizeof(ex), hipMemcpyDeviceToHost,
-                                  h->stream));
-        PCG_HIP(h, hipStreamSynchronize(h->stream));
-        if ((int64_t)ex > room) return pcg_fail(h, PCG_ERR_OVERFLOW, "sepset export overflow");
-        h->export_rows += (int64_t)ex;
+        if ((int64_t)c.exported > room) return pcg_fail(h, PCG_ERR_OVERFLOW, "sepset export overflow");
+        h->export_rows += (int64_t)c.exported;
     }
-    const int64_t nw = (int64_t)n * W;
-    hipLaunchKernelGGL(k_apply, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, h->stream,
-                       h->rm_ext ? (const uint8_t *)h->rm_ext : (const uint8_t *)h->rm.p, (uint64_t *)h->adj.p,
-                       h->rl, n, W, d);
-    PCG_HIP(h, hipGetLastError());
-    int rc = refresh_graph(h);
+    rc = graph_finish(h);
     if (rc) return rc;
     h->st.edges_after[d] = h->sumdeg / 2;
     if (stats) *stats = h->st;
     return PCG_OK;
 }
 
-extern "C" int pcg_skeleton(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N, double alpha,
-                            int max_depth, int flags, int8_t *removed_level, pcg_stats *stats) {
+static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N, double alpha,
+                         int max_depth, int flags, int8_t *removed_level) {
     int rc = pcg_skeleton_init(h, C, n, ldc, N, alpha, flags, removed_level);
     if (rc) return rc;
     for (int depth = 0;; ++depth) {
@@ -1791,15 +1836,25 @@ extern "C" int pcg_skeleton(pcg_handle *h, const double *C, int64_t n, int64_t l
         rc = pcg_level_run(h, 0, total);
         if (rc) return rc;
         rc = pcg_level_end(h, nullptr);
-        if (rc) { if (stats) *stats = h->st; return rc; }
+        if (rc) return rc;
         PCG_HIP(h, hipEventRecord(h->ev[1], h->stream));
         PCG_HIP(h, hipEventSynchronize(h->ev[1]));
         float ms = 0.f;
         PCG_HIP(h, hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
         h->st.level_ms[depth] = ms;
     }
-    if (stats) *stats = h->st;
     return PCG_OK;
+}
+
+extern "C" int pcg_skeleton(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N, double alpha,
+                            int max_depth, int flags, int8_t *removed_level, pcg_stats *stats) {
+    int rc = PCG_OK;
+    for (int attempt = 0; attempt < 6; ++attempt) {
+        rc = skeleton_once(h, C, n, ldc, N, alpha, max_depth, flags, removed_level);
+        if (rc != PCG_ERR_OVERFLOW) break;
+    }
+    if (stats && h) *stats = h->st;
+    return rc;
 }
 
 extern "C" int pcg_degrees(pcg_handle *h, int32_t *deg_host, int64_t capacity) {

@@ -55,8 +55,11 @@ class GpuLevelBackend:
         n = Cd.shape[0]
         self.n = n
         self.rl = torch.empty((n, n), dtype=torch.int8, device=eng.device)
-        self.rm = torch.zeros(n * n, dtype=torch.uint8, device=eng.device)
-        check(self.h, self.lib.pcg_set_removal_buffer(self.h, ctypes.c_void_p(self.rm.data_ptr()), n * n),
+        # n*n removal flags + status bytes (overflow / singular / domain), merged by the same
+        # all-reduce so every rank takes the same branch at pcg_level_end
+        nb = n * n + _lib.PCG_RM_STATUS
+        self.rm = torch.zeros(nb, dtype=torch.uint8, device=eng.device)
+        check(self.h, self.lib.pcg_set_removal_buffer(self.h, ctypes.c_void_p(self.rm.data_ptr()), nb),
               "pcg_set_removal_buffer")
         check(self.h, self.lib.pcg_skeleton_init(self.h, ctypes.c_void_p(Cd.data_ptr()), n, n, int(N),
                                                  float(alpha), int(flags), ctypes.c_void_p(self.rl.data_ptr())),
@@ -162,11 +165,20 @@ def sharded_skeleton(eng, C, N: int, alpha: float = 0.05, max_depth: int = -1, f
 
     import torch.distributed as dist
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    t0 = time.perf_counter()
-    backend = GpuLevelBackend(eng, C, N, alpha, flags)
-    if trace is not None:
-        trace.append(("init", -1, time.perf_counter() - t0))
-    run_sharded_levels(backend, rank, world, max_depth=max_depth, group=group, trace=trace)
+    for attempt in range(6):
+        t0 = time.perf_counter()
+        backend = GpuLevelBackend(eng, C, N, alpha, flags)
+        if trace is not None:
+            trace.append(("init", -1, time.perf_counter() - t0))
+        try:
+            run_sharded_levels(backend, rank, world, max_depth=max_depth, group=group, trace=trace)
+            break
+        except _lib.PcgError as e:
+            # an exact-path list overflowed on some rank; the merged status byte makes every
+            # rank raise at the same level, capacities are already enlarged: rerun everywhere
+            if e.code != _lib.PCG_ERR_OVERFLOW or attempt == 5:
+                raise
+            eng.lib.pcg_set_removal_buffer(eng.h, None, 0)
     t0 = time.perf_counter()
     out = backend.finish()
     xy, bits = _allgather_rows(out.sep_xy_dev, out.sep_bits_dev, group=group)
