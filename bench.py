@@ -155,7 +155,11 @@ def main():
 
     def one_step():
         t0 = time.perf_counter()
-        C = eng.corr(Xd)
+        if world > 1:
+            from rcaeval_amd.dist import sharded_corr
+            C = sharded_corr(eng, Xd)
+        else:
+            C = eng.corr(Xd)
         torch.cuda.synchronize()
         phases.append(("corr", time.perf_counter() - t0))
         if world > 1:

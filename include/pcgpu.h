@@ -85,7 +85,10 @@ typedef struct {                       /* one unique CI test (PCG_FLAG_RECORD / 
 int pcg_create(int device, pcg_handle **out);
 int pcg_destroy(pcg_handle *h);
 const char *pcg_last_error(pcg_handle *h);
-/* Use an external HIP stream (e.g. torch.cuda.current_stream().cuda_stream); NULL = own. */
+/* Run every call on this HIP stream (e.g. torch.cuda.current_stream().cuda_stream) so the
+ * engine is stream-ordered with the caller's buffers. NULL = the device's default (null)
+ * stream — which is what torch's default current stream reports. A new handle starts on
+ * its own non-blocking stream until this is called.                                      */
 int pcg_set_stream(pcg_handle *h, void *hip_stream);
 /* Launch-shape knobs (0 = default). */
 int pcg_set_capacity(pcg_handle *h, int64_t record_capacity, int64_t deferred_capacity);
@@ -97,6 +100,19 @@ int pcg_set_capacity(pcg_handle *h, int64_t record_capacity, int64_t deferred_ca
  * X: device, N x n (ldx >= n). C: device, n x n (ldc >= n).                            */
 int pcg_corr(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx,
              double *C, int64_t ldc);
+
+/* ---- K1 sharded over ranks (multi-GPU) --------------------------------------------
+ * Rank `rank` of `world` computes the centred Gram sums of its share of the 64-row tile
+ * rows (zig-zag assignment, upper-triangle tiles only) into `packed` (device,
+ * rows_per_rank x n doubles, see pcg_corr_shard_rows). The caller all-gathers the packed
+ * buffers rank-major (RCCL over xGMI) and calls pcg_corr_shard_finish, which unpacks,
+ * mirrors and normalises: C is bitwise the single-GPU pcg_corr result (same split-K,
+ * same summation order) for every world size.                                          */
+int pcg_corr_shard_rows(int64_t n, int world, int64_t *rows_per_rank);
+int pcg_corr_shard(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx, int rank,
+                   int world, double *packed);
+int pcg_corr_shard_finish(pcg_handle *h, const double *gathered, int64_t N, int64_t n, int world,
+                          double *C, int64_t ldc);
 
 /* ---- K2/K3: stable PC skeleton ---------------------------------------------------
  * Replaces causal-learn skeleton_discovery(stable=True) with FisherZ
@@ -148,6 +164,9 @@ int pcg_level_chunk_work(pcg_handle *h, int64_t *prefix_host, int64_t capacity);
  * returns PCG_ERR_OVERFLOW on every rank: grow nothing, rerun the skeleton — capacities
  * have already been enlarged), [1] a singular sub-matrix, [2] a math domain error.      */
 #define PCG_RM_STATUS 64
+/* Number of ranks the level work lists are split over (default 1). The per-depth
+ * decomposition sizes its chunks so that each rank's slice still fills its GPU.          */
+int pcg_set_world_size(pcg_handle *h, int world);
 int pcg_set_removal_buffer(pcg_handle *h, uint8_t *rm_dev, int64_t bytes);
 
 /* ---- K4: PageRank head -------------------------------------------------------------

@@ -79,6 +79,9 @@ SIGNATURES = [
     ("pcg_set_stream", I32, [P, P]),
     ("pcg_set_capacity", I32, [P, I64, I64]),
     ("pcg_corr", I32, [P, P, I64, I64, I64, P, I64]),
+    ("pcg_corr_shard_rows", I32, [I64, ctypes.c_int, ctypes.POINTER(I64)]),
+    ("pcg_corr_shard", I32, [P, P, I64, I64, I64, ctypes.c_int, ctypes.c_int, P]),
+    ("pcg_corr_shard_finish", I32, [P, P, I64, I64, ctypes.c_int, P, I64]),
     ("pcg_skeleton", I32, [P, P, I64, I64, I64, D, ctypes.c_int, ctypes.c_int, P, ctypes.POINTER(PcgStats)]),
     ("pcg_degrees", I32, [P, P, I64]),
     ("pcg_sepset_count", I32, [P, ctypes.POINTER(I64), ctypes.POINTER(I32)]),
@@ -92,6 +95,7 @@ SIGNATURES = [
     ("pcg_level_end", I32, [P, ctypes.POINTER(PcgStats)]),
     ("pcg_level_chunk_work", I32, [P, P, I64]),
     ("pcg_set_removal_buffer", I32, [P, P, I64]),
+    ("pcg_set_world_size", I32, [P, ctypes.c_int]),
     ("pcg_pagerank_dense", I32, [P, P, I64, I64, D, ctypes.c_int, D, P]),
     ("pcg_pagerank_csr", I32, [P, P, P, P, I64, I64, D, ctypes.c_int, D, P]),
     ("pcg_random_walk", I32, [P, P, I64, I64, I64, I64, ctypes.c_uint64, ctypes.c_uint64,

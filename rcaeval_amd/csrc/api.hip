@@ -100,13 +100,11 @@ extern "C" int pcg_set_stream(pcg_handle *h, void *hip_stream) {
     if (!h) return PCG_ERR_INVALID;
     hipStreamSynchronize(h->stream);
     if (h->own_stream && h->stream) hipStreamDestroy(h->stream);
-    if (hip_stream) {
-        h->stream = (hipStream_t)hip_stream;
-        h->own_stream = false;
-    } else {
-        if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) return PCG_ERR_HIP;
-        h->own_stream = true;
-    }
+    // NULL is the default stream itself (not "make one"): torch's default current stream
+    // reports handle 0, and a private non-blocking stream would not be ordered after torch's
+    // writes to the buffers handed over
+    h->stream = (hipStream_t)hip_stream;
+    h->own_stream = false;
     return PCG_OK;
 }
 

@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <vector>
 
 #include "handle.h"
 
@@ -53,14 +54,23 @@ __device__ __forceinline__ void tile_of(int t, int T, int &bi, int &bj) {
     bj = row + rem;
 }
 
+// tl == nullptr: all upper-triangle tiles, mirrored into G (single GPU). Otherwise tl lists
+// (bi, bj, packed tile row) triples of one rank's share: rows go to packed position, no mirror.
 __global__ __launch_bounds__(256) void k_xtx(const double *X, int64_t N, int n, int64_t ldx,
                                             const double *mean, int ntiles, int64_t kchunk, double *G,
-                                            int64_t ldg, int64_t slab_stride) {
+                                            int64_t ldg, int64_t slab_stride, const int32_t *tl) {
     __shared__ double As[2][KT][TILE + PAD];
     __shared__ double Bs[2][KT][TILE + PAD];
     const int T = (n + TILE - 1) / TILE;
-    int bi, bj;
-    tile_of(blockIdx.x % ntiles, T, bi, bj);
+    int bi, bj, pbi = -1;
+    if (tl) {
+        const int t = blockIdx.x % ntiles;
+        bi = tl[3 * t];
+        bj = tl[3 * t + 1];
+        pbi = tl[3 * t + 2];
+    } else {
+        tile_of(blockIdx.x % ntiles, T, bi, bj);
+    }
     const int slab = blockIdx.x / ntiles;           // split-K slice
     const int64_t kbeg = (int64_t)slab * kchunk;
     const int64_t kend = std::min<int64_t>(N, kbeg + kchunk);
@@ -133,7 +143,9 @@ __global__ __launch_bounds__(256) void k_xtx(const double *X, int64_t N, int n, 
                 const int j = j0 + wc + 16 * b + (lane & 15);
                 if (i < n && j < n) {
                     const double v = acc[a][b][r];
-                    if (bi != bj) {
+                    if (pbi >= 0) {
+                        G[((int64_t)pbi * TILE + (i - i0)) * ldg + j] = v;
+                    } else if (bi != bj) {
                         G[(int64_t)i * ldg + j] = v;
                         G[(int64_t)j * ldg + i] = v;
                     } else if (i <= j) {
@@ -167,30 +179,170 @@ __global__ void k_normalize(const double *G, int64_t ldg, int64_t slab_stride, i
     C[(int64_t)i * ldc + j] = v > 1.0 ? 1.0 : (v < -1.0 ? -1.0 : v);  // NaN passes through
 }
 
+// packed[r][j] = sum_s G_s[r][j] in slab order (the order k_stddev / k_normalize use)
+__global__ void k_slab_sum(const double *G, int64_t slab_stride, int ks, int64_t count, double *out) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= count) return;
+    double g = 0.0;
+    for (int s = 0; s < ks; ++s) g += G[(int64_t)s * slab_stride + e];
+    out[e] = g;
+}
+
+// zig-zag owner of tile row r among `world` ranks (2 rows per rank per period of 2*world):
+// rank q owns rows m == q and m == 2*world-1-q of every period, so the upper-triangle work
+// (T - r tiles in row r) is balanced
+__host__ __device__ __forceinline__ void shard_slot(int r, int world, int &owner, int &local) {
+    const int period = 2 * world, q = r / period, m = r % period;
+    owner = m < world ? m : period - 1 - m;
+    local = 2 * q + (m < world ? 0 : 1);
+}
+
+// C from the gathered packed Gram rows of every rank: unpack (upper from the owner of the
+// smaller tile row), sd from the diagonal, normalize + clip in numpy.corrcoef order —
+// bitwise the single-GPU pcg_corr result (same slab split, same summation order)
+__global__ void k_gather_finish_sd(const double *Gg, int64_t rows_per_rank, int n, int world, double scale,
+                                   double *sd) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int owner, local;
+    shard_slot(i / TILE, world, owner, local);
+    const double g = Gg[((int64_t)owner * rows_per_rank + (int64_t)local * TILE + (i % TILE)) * n + i];
+    sd[i] = sqrt(g * scale);
+}
+
+__global__ void k_gather_finish(const double *Gg, int64_t rows_per_rank, int n, int world, double scale,
+                                const double *sd, double *C, int64_t ldc) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.y;
+    if (j >= n) return;
+    // (p, q) = the position the single-GPU path computes (upper tile, i <= j inside diagonal
+    // tiles) and mirrors
+    const bool up = (i / TILE) < (j / TILE) || ((i / TILE) == (j / TILE) && i <= j);
+    const int p = up ? i : j, q = up ? j : i;
+    int owner, local;
+    shard_slot(p / TILE, world, owner, local);
+    const double g = Gg[((int64_t)owner * rows_per_rank + (int64_t)local * TILE + (p % TILE)) * n + q];
+    double v = (g * scale) / sd[i];
+    v = v / sd[j];
+    C[(int64_t)i * ldc + j] = v > 1.0 ? 1.0 : (v < -1.0 ? -1.0 : v);
+}
+
+// split-K factor: a function of the problem only (n, N), so every world size sums the
+// same slabs in the same order; ~15 blocks per upper tile fills 256 CUs x 4 blocks with
+// little tail at 1..8 ranks
+int split_k(int n, int64_t N, int64_t *kchunk_out) {
+    const int T = (n + TILE - 1) / TILE;
+    const int ntiles = T * (T + 1) / 2;
+    int ks = (int)std::min<int64_t>(std::max<int64_t>(1, (7680 + ntiles - 1) / ntiles), std::max<int64_t>(1, N / 512));
+    ks = std::min(ks, 16);
+    const int64_t kchunk = (((N + ks - 1) / ks) + KT - 1) / KT * KT;
+    *kchunk_out = kchunk;
+    return (int)((N + kchunk - 1) / kchunk);
+}
+
+int column_means(pcg_handle *h, const double *X, int64_t N, int nn, int64_t ldx, double **mean_out, double **sd_out) {
+    const int nchunks = (int)((N + MEAN_ROWS - 1) / MEAN_ROWS);
+    if (!pcg_ensure(h, h->colmean, sizeof(double) * ((size_t)nn * (nchunks + 2))))
+        return pcg_fail(h, PCG_ERR_OOM, "pcg_corr scratch");
+    double *part = (double *)h->colmean.p;
+    double *mean = part + (size_t)nn * nchunks;
+    hipLaunchKernelGGL(k_colsum_partial, dim3((nn + 255) / 256, nchunks), dim3(256), 0, h->stream, X, N, nn,
+                       ldx, part);
+    hipLaunchKernelGGL(k_colmean, dim3((nn + 255) / 256), dim3(256), 0, h->stream, part, nchunks, nn, N, mean);
+    *mean_out = mean;
+    *sd_out = mean + nn;
+    return PCG_OK;
+}
+
 }  // namespace
+
+extern "C" int pcg_corr_shard_rows(int64_t n, int world, int64_t *rows_per_rank) {
+    if (n < 1 || world < 1 || !rows_per_rank) return PCG_ERR_INVALID;
+    const int64_t T = (n + TILE - 1) / TILE;
+    *rows_per_rank = (int64_t)TILE * 2 * ((T + 2 * world - 1) / (2 * world));
+    return PCG_OK;
+}
+
+extern "C" int pcg_corr_shard(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx, int rank,
+                              int world, double *packed) {
+    if (!h || !X || !packed || N < 2 || n < 1 || ldx < n || n > (1 << 24) || world < 1 || rank < 0 ||
+        rank >= world)
+        return pcg_fail(h, PCG_ERR_INVALID, "pcg_corr_shard: invalid arguments");
+    PCG_HIP(h, hipSetDevice(h->device));
+    const int nn = (int)n;
+    int64_t rows = 0;
+    pcg_corr_shard_rows(n, world, &rows);
+    PCG_HIP(h, hipMemsetAsync(packed, 0, sizeof(double) * rows * nn, h->stream));
+    const int T = (nn + TILE - 1) / TILE;
+    std::vector<int32_t> tl;
+    for (int bi = 0; bi < T; ++bi) {
+        int owner, local;
+        shard_slot(bi, world, owner, local);
+        if (owner != rank) continue;
+        for (int bj = bi; bj < T; ++bj) {
+            tl.push_back(bi);
+            tl.push_back(bj);
+            tl.push_back(local);
+        }
+    }
+    const int ntiles = (int)(tl.size() / 3);
+    if (ntiles == 0) return PCG_OK;
+    double *mean, *sd;
+    int rc = column_means(h, X, N, nn, ldx, &mean, &sd);
+    if (rc) return rc;
+    int64_t kchunk = 0;
+    const int ks = split_k(nn, N, &kchunk);
+    const int64_t stride = rows * nn;
+    if (!pcg_ensure(h, h->pr_scratch, sizeof(double) * ((size_t)stride * (ks > 1 ? ks : 0) + tl.size())))
+        return pcg_fail(h, PCG_ERR_OOM, "pcg_corr_shard slabs");
+    double *G = ks > 1 ? (double *)h->pr_scratch.p : packed;
+    int32_t *tld = reinterpret_cast<int32_t *>((double *)h->pr_scratch.p + (ks > 1 ? (size_t)stride * ks : 0));
+    PCG_HIP(h, hipMemcpyAsync(tld, tl.data(), sizeof(int32_t) * tl.size(), hipMemcpyHostToDevice, h->stream));
+    if (ks > 1) PCG_HIP(h, hipMemsetAsync(G, 0, sizeof(double) * (size_t)stride * ks, h->stream));
+    hipLaunchKernelGGL(k_xtx, dim3(ntiles * ks), dim3(256), 0, h->stream, X, N, nn, ldx, mean, ntiles, kchunk, G,
+                       (int64_t)nn, stride, (const int32_t *)tld);
+    if (ks > 1)
+        hipLaunchKernelGGL(k_slab_sum, dim3((unsigned)((stride + 255) / 256)), dim3(256), 0, h->stream, G, stride,
+                           ks, stride, packed);
+    PCG_HIP(h, hipGetLastError());
+    PCG_HIP(h, hipStreamSynchronize(h->stream));
+    return PCG_OK;
+}
+
+extern "C" int pcg_corr_shard_finish(pcg_handle *h, const double *gathered, int64_t N, int64_t n, int world,
+                                     double *C, int64_t ldc) {
+    if (!h || !gathered || !C || N < 2 || n < 1 || ldc < n || world < 1)
+        return pcg_fail(h, PCG_ERR_INVALID, "pcg_corr_shard_finish: invalid arguments");
+    PCG_HIP(h, hipSetDevice(h->device));
+    const int nn = (int)n;
+    int64_t rows = 0;
+    pcg_corr_shard_rows(n, world, &rows);
+    if (!pcg_ensure(h, h->colmean, sizeof(double) * ((size_t)nn * 2)))
+        return pcg_fail(h, PCG_ERR_OOM, "pcg_corr scratch");
+    double *sd = (double *)h->colmean.p;
+    const double scale = 1.0 / (double)(N - 1);
+    hipLaunchKernelGGL(k_gather_finish_sd, dim3((nn + 255) / 256), dim3(256), 0, h->stream, gathered, rows, nn,
+                       world, scale, sd);
+    hipLaunchKernelGGL(k_gather_finish, dim3((nn + 255) / 256, nn), dim3(256), 0, h->stream, gathered, rows, nn,
+                       world, scale, (const double *)sd, C, ldc);
+    PCG_HIP(h, hipGetLastError());
+    PCG_HIP(h, hipStreamSynchronize(h->stream));
+    return PCG_OK;
+}
 
 extern "C" int pcg_corr(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx, double *C,
                         int64_t ldc) {
     if (!h || !X || !C || N < 2 || n < 1 || ldx < n || ldc < n || n > (1 << 24))
         return pcg_fail(h, PCG_ERR_INVALID, "pcg_corr: invalid arguments");
     PCG_HIP(h, hipSetDevice(h->device));
-    const int nchunks = (int)((N + MEAN_ROWS - 1) / MEAN_ROWS);
-    if (!pcg_ensure(h, h->colmean, sizeof(double) * ((size_t)n * (nchunks + 2))))
-        return pcg_fail(h, PCG_ERR_OOM, "pcg_corr scratch");
-    double *part = (double *)h->colmean.p;
-    double *mean = part + (size_t)n * nchunks;
-    double *sd = mean + n;
     const int nn = (int)n;
-    hipLaunchKernelGGL(k_colsum_partial, dim3((nn + 255) / 256, nchunks), dim3(256), 0, h->stream, X, N, nn,
-                       ldx, part);
-    hipLaunchKernelGGL(k_colmean, dim3((nn + 255) / 256), dim3(256), 0, h->stream, part, nchunks, nn, N, mean);
+    double *mean, *sd;
+    int rc = column_means(h, X, N, nn, ldx, &mean, &sd);
+    if (rc) return rc;
     const int T = (nn + TILE - 1) / TILE;
     const int ntiles = T * (T + 1) / 2;
-    // split K so that the grid covers the chip (~8 blocks per CU); slabs summed in order later
-    int ks = (int)std::min<int64_t>(std::max<int64_t>(1, (2048 + ntiles - 1) / ntiles), std::max<int64_t>(1, N / 512));
-    ks = std::min(ks, 16);
-    const int64_t kchunk = (((N + ks - 1) / ks) + KT - 1) / KT * KT;
-    ks = (int)((N + kchunk - 1) / kchunk);
+    int64_t kchunk = 0;
+    const int ks = split_k(nn, N, &kchunk);
     double *G = C;
     int64_t ldg = ldc, stride = 0;
     if (ks > 1) {
@@ -202,7 +354,7 @@ extern "C" int pcg_corr(pcg_handle *h, const double *X, int64_t N, int64_t n, in
     }
     const double scale = 1.0 / (double)(N - 1);
     hipLaunchKernelGGL(k_xtx, dim3(ntiles * ks), dim3(256), 0, h->stream, X, N, nn, ldx, mean, ntiles, kchunk, G,
-                       ldg, stride);
+                       ldg, stride, (const int32_t *)nullptr);
     hipLaunchKernelGGL(k_stddev, dim3((nn + 255) / 256), dim3(256), 0, h->stream, G, ldg, stride, ks, nn, scale, sd);
     hipLaunchKernelGGL(k_normalize, dim3((nn + 255) / 256, nn), dim3(256), 0, h->stream, G, ldg, stride, ks, C, ldc,
                        nn, scale, sd);

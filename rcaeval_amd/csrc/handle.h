@@ -68,6 +68,7 @@ struct pcg_handle {
     int64_t total_small = 0, total_large = 0;
     int chunk = 256;                 // block size of the staged (large-degree) kernel
     int spl = 1;                     // S ranks per lane of the LDS-resident kernel
+    int world = 1;                   // ranks sharing each level's work list (pcg_set_world_size)
     int32_t maxdeg_small = 0;        // largest degree handled by the LDS-resident kernel
     bool tgroup = false;             // small class runs k_level_lds_t this depth
     int32_t maxdeg = 0;

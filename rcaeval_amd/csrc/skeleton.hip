@@ -1578,8 +1578,8 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
                 cnt_large += (int)hist[D];
             }
         }
-        // ~4096 LDS-resident blocks per depth; each lane walks spl units
-        h->spl = (int)std::min(64.0, std::max(1.0, std::floor(sum_small / (256.0 * 4096.0))));
+        // ~4096 LDS-resident blocks per depth and rank; each lane walks spl units
+        h->spl = (int)std::min(64.0, std::max(1.0, std::floor(sum_small / (256.0 * 4096.0 * h->world))));
         const double mean_large = cnt_large ? sum_large / cnt_large : 0.0;
         h->chunk = (depth > PCG_MAX_DEPTH || mean_large <= 64) ? 64 : (mean_large <= 128 ? 128 : 256);
         const uint64_t csz = (uint64_t)256 * h->spl;
@@ -1625,6 +1625,12 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
             h->export_cap = cap;
         }
     }
+    return PCG_OK;
+}
+
+extern "C" int pcg_set_world_size(pcg_handle *h, int world) {
+    if (!h || world < 1) return pcg_fail(h, PCG_ERR_INVALID, "pcg_set_world_size: world %d", world);
+    h->world = world;
     return PCG_OK;
 }
 

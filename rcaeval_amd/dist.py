@@ -47,7 +47,7 @@ def split_by_work(prefix: np.ndarray, rank: int, world: int) -> tuple[int, int]:
 class GpuLevelBackend:
     """One rank's device work through the C ABI (pcg_skeleton_init / pcg_level_*)."""
 
-    def __init__(self, eng, C, N: int, alpha: float, flags: int):
+    def __init__(self, eng, C, N: int, alpha: float, flags: int, world: int = 1):
         import torch
         self.eng, self.lib, self.h = eng, eng.lib, eng.h
         Cd = eng.to_device(C)
@@ -61,6 +61,7 @@ class GpuLevelBackend:
         self.rm = torch.zeros(nb, dtype=torch.uint8, device=eng.device)
         check(self.h, self.lib.pcg_set_removal_buffer(self.h, ctypes.c_void_p(self.rm.data_ptr()), nb),
               "pcg_set_removal_buffer")
+        check(self.h, self.lib.pcg_set_world_size(self.h, int(world)), "pcg_set_world_size")
         check(self.h, self.lib.pcg_skeleton_init(self.h, ctypes.c_void_p(Cd.data_ptr()), n, n, int(N),
                                                  float(alpha), int(flags), ctypes.c_void_p(self.rl.data_ptr())),
               "pcg_skeleton_init")
@@ -88,6 +89,7 @@ class GpuLevelBackend:
 
     def finish(self):
         self.lib.pcg_set_removal_buffer(self.h, None, 0)
+        self.lib.pcg_set_world_size(self.h, 1)
         return self.eng._collect(self.n, self.rl, self.stats, 0.0)
 
 
@@ -158,6 +160,26 @@ def _allreduce_stats(stats: dict, device, group=None) -> dict:
     return out
 
 
+def sharded_corr(eng, X, group=None):
+    """K1 sharded over the ranks of ``group``: each rank computes its zig-zag share of the
+    upper-triangle Gram tiles, one all-gather (RCCL over xGMI) assembles them, and every
+    rank normalises locally. Bitwise equal to the single-GPU ``eng.corr(X)``."""
+    import torch
+    import torch.distributed as dist
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    Xd = eng.to_device(X)
+    N, n = Xd.shape
+    packed = eng.corr_shard(Xd, rank, world)
+    if dist.get_backend(group) == "nccl":
+        gathered = torch.empty((world * packed.shape[0], n), dtype=torch.float64, device=eng.device)
+        dist.all_gather_into_tensor(gathered, packed, group=group)
+    else:   # gloo rehearsal (several ranks on one GPU)
+        parts = [torch.empty_like(packed) for _ in range(world)]
+        dist.all_gather(parts, packed, group=group)
+        gathered = torch.cat(parts)
+    return eng.corr_shard_finish(gathered, N, n, world)
+
+
 def sharded_skeleton(eng, C, N: int, alpha: float = 0.05, max_depth: int = -1, flags: int = 0, group=None,
                      trace=None):
     """Edge-sharded skeleton over the ranks of ``group``; every rank returns the full result."""
@@ -167,7 +189,7 @@ def sharded_skeleton(eng, C, N: int, alpha: float = 0.05, max_depth: int = -1, f
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     for attempt in range(6):
         t0 = time.perf_counter()
-        backend = GpuLevelBackend(eng, C, N, alpha, flags)
+        backend = GpuLevelBackend(eng, C, N, alpha, flags, world)
         if trace is not None:
             trace.append(("init", -1, time.perf_counter() - t0))
         try:
@@ -179,6 +201,7 @@ def sharded_skeleton(eng, C, N: int, alpha: float = 0.05, max_depth: int = -1, f
             if e.code != _lib.PCG_ERR_OVERFLOW or attempt == 5:
                 raise
             eng.lib.pcg_set_removal_buffer(eng.h, None, 0)
+            eng.lib.pcg_set_world_size(eng.h, 1)
     t0 = time.perf_counter()
     out = backend.finish()
     xy, bits = _allgather_rows(out.sep_xy_dev, out.sep_bits_dev, group=group)
@@ -190,5 +213,5 @@ def sharded_skeleton(eng, C, N: int, alpha: float = 0.05, max_depth: int = -1, f
     return out
 
 
-__all__ = ["split_by_work", "run_sharded_levels", "sharded_skeleton", "GpuLevelBackend"]
+__all__ = ["split_by_work", "run_sharded_levels", "sharded_skeleton", "sharded_corr", "GpuLevelBackend"]
 _ = _lib

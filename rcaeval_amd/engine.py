@@ -128,6 +128,28 @@ class Engine:
                                         ctypes.c_void_p(C.data_ptr()), n), "pcg_corr")
         return C
 
+    def corr_shard(self, X, rank: int, world: int):
+        """This rank's packed Gram rows of the sharded K1 (see ``pcg_corr_shard``)."""
+        torch = _torch()
+        Xd = self.to_device(X)
+        N, n = Xd.shape
+        rows = ctypes.c_int64()
+        check(self.h, self.lib.pcg_corr_shard_rows(n, int(world), ctypes.byref(rows)), "pcg_corr_shard_rows")
+        packed = torch.empty((rows.value, n), dtype=torch.float64, device=self.device)
+        check(self.h, self.lib.pcg_corr_shard(self.h, ctypes.c_void_p(Xd.data_ptr()), N, n, n, int(rank),
+                                              int(world), ctypes.c_void_p(packed.data_ptr())), "pcg_corr_shard")
+        return packed
+
+    def corr_shard_finish(self, gathered, N: int, n: int, world: int):
+        """C from the rank-major concatenation of every rank's packed rows."""
+        torch = _torch()
+        g = gathered.contiguous()
+        C = torch.empty((n, n), dtype=torch.float64, device=self.device)
+        check(self.h, self.lib.pcg_corr_shard_finish(self.h, ctypes.c_void_p(g.data_ptr()), int(N), int(n),
+                                                     int(world), ctypes.c_void_p(C.data_ptr()), n),
+              "pcg_corr_shard_finish")
+        return C
+
     # ------------------------------------------------------------------ K2/K3
     def skeleton(self, C, N: int, alpha: float = 0.05, max_depth: int = -1, flags: int = 0,
                  record_capacity: int = 0) -> SkeletonOut:

@@ -135,3 +135,18 @@ def test_max_depth_cap(eng):
         out = eng.skeleton(C, 1000, max_depth=md)
         assert out.levels == ref.levels <= md + 1
         np.testing.assert_array_equal(out.removed_level, ref.removed_level)
+
+
+@pytest.mark.parametrize("n,N,world", [(50, 600, 2), (130, 3000, 3), (300, 1200, 8), (2000, 10000, 8)])
+def test_sharded_corr_bitwise_equals_single_gpu(eng, n, N, world):
+    """K1 sharded over `world` ranks (each rank's packed share computed here in turn on one
+    GPU, then concatenated rank-major as the all-gather would) is bitwise pcg_corr."""
+    import torch
+    X = synth.gaussian_sem(n, N, seed=n, w_low=0.1, w_high=0.5)
+    Xd = eng.to_device(X)
+    C1 = eng.corr(Xd)
+    parts = [eng.corr_shard(Xd, r, world) for r in range(world)]
+    Cw = eng.corr_shard_finish(torch.cat(parts), N, n, world)
+    assert torch.equal(C1, Cw)
+    if n <= 300:
+        np.testing.assert_allclose(C1.cpu().numpy(), np.corrcoef(X.T), rtol=0, atol=2e-14)
