@@ -157,6 +157,9 @@ int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi);
 int pcg_level_end(pcg_handle *h, pcg_stats *stats);
 /* Work weight of each chunk prefix (host out, total_chunks+1 int64) for load balance.  */
 int pcg_level_chunk_work(pcg_handle *h, int64_t *prefix_host, int64_t capacity);
+/* The contiguous work-balanced chunk range [lo, hi) of `rank` (the same cut as
+ * searchsorted(prefix, total*r/world, 'left') over pcg_level_chunk_work's prefix).       */
+int pcg_level_split(pcg_handle *h, int rank, int world, int64_t *chunk_lo, int64_t *chunk_hi);
 /* Use a caller-owned device buffer (n*n + PCG_RM_STATUS bytes, e.g. a torch tensor that
  * the caller all-reduces with MAX) for the per-depth removal flags instead of the handle's
  * own; NULL = own. The PCG_RM_STATUS bytes after the n*n flags carry level status that the

@@ -94,6 +94,7 @@ SIGNATURES = [
     ("pcg_level_run", I32, [P, I64, I64]),
     ("pcg_level_end", I32, [P, ctypes.POINTER(PcgStats)]),
     ("pcg_level_chunk_work", I32, [P, P, I64]),
+    ("pcg_level_split", I32, [P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(I64), ctypes.POINTER(I64)]),
     ("pcg_set_removal_buffer", I32, [P, P, I64]),
     ("pcg_set_world_size", I32, [P, ctypes.c_int]),
     ("pcg_pagerank_dense", I32, [P, P, I64, I64, D, ctypes.c_int, D, P]),

@@ -1674,6 +1674,31 @@ extern "C" int pcg_level_chunk_work(pcg_handle *h, int64_t *prefix_host, int64_t
     return PCG_OK;
 }
 
+// contiguous, work-balanced chunk range of `rank`: the first chunk whose inclusive work
+// prefix reaches total*r/world (numpy searchsorted 'left' over the prefix), as
+// rcaeval_amd.dist.split_by_work computes it from pcg_level_chunk_work
+extern "C" int pcg_level_split(pcg_handle *h, int rank, int world, int64_t *chunk_lo, int64_t *chunk_hi) {
+    if (!h || world < 1 || rank < 0 || rank >= world || !chunk_lo || !chunk_hi)
+        return pcg_fail(h, PCG_ERR_INVALID, "pcg_level_split: rank %d world %d", rank, world);
+    const int64_t total = h->total_chunks;
+    std::vector<int64_t> prefix((size_t)total + 1);
+    int rc = pcg_level_chunk_work(h, prefix.data(), total + 1);
+    if (rc) return rc;
+    if (total <= 0) { *chunk_lo = *chunk_hi = 0; return PCG_OK; }
+    const double W = (double)prefix[total];
+    auto cut = [&](int r) -> int64_t {
+        if (r <= 0) return 0;
+        if (r >= world) return total;
+        const double target = W * r / world;
+        return (int64_t)(std::lower_bound(prefix.begin(), prefix.end(), target,
+                                          [](int64_t v, double t) { return (double)v < t; }) - prefix.begin());
+    };
+    const int64_t lo = std::min(cut(rank), total), hi = std::min(std::max(cut(rank + 1), lo), total);
+    *chunk_lo = lo;
+    *chunk_hi = hi;
+    return PCG_OK;
+}
+
 extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) {
     if (!h || chunk_lo < 0 || chunk_hi > h->total_chunks || chunk_lo > chunk_hi)
         return pcg_fail(h, PCG_ERR_INVALID, "pcg_level_run: chunk range");

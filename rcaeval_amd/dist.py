@@ -73,10 +73,21 @@ class GpuLevelBackend:
         if rc == 1:
             return None
         check(self.h, rc, "pcg_level_begin")
-        prefix = np.zeros(total.value + 1, np.int64)
+        return total.value
+
+    def prefix(self, total: int) -> np.ndarray:
+        """Work prefix of the current depth's chunks (pcg_level_chunk_work), for checks."""
+        prefix = np.zeros(total + 1, np.int64)
         check(self.h, self.lib.pcg_level_chunk_work(self.h, prefix.ctypes.data_as(ctypes.c_void_p), len(prefix)),
               "pcg_level_chunk_work")
         return prefix
+
+    def split(self, rank: int, world: int):
+        """This rank's chunk range, cut in C (pcg_level_split == split_by_work)."""
+        lo, hi = ctypes.c_int64(), ctypes.c_int64()
+        check(self.h, self.lib.pcg_level_split(self.h, rank, world, ctypes.byref(lo), ctypes.byref(hi)),
+              "pcg_level_split")
+        return lo.value, hi.value
 
     def run(self, lo: int, hi: int):
         check(self.h, self.lib.pcg_level_run(self.h, int(lo), int(hi)), "pcg_level_run")
@@ -105,10 +116,11 @@ def run_sharded_levels(backend, rank: int, world: int, max_depth: int = -1, grou
         if max_depth >= 0 and depth > max_depth:
             break
         t0 = clock()
-        prefix = backend.begin(depth)
-        if prefix is None:
+        work = backend.begin(depth)
+        if work is None:
             break
-        lo, hi = split_by_work(prefix, rank, world)
+        # GPU backend: the cut is made in C; the CPU protocol test hands back the prefix
+        lo, hi = backend.split(rank, world) if hasattr(backend, "split") else split_by_work(work, rank, world)
         t1 = clock()
         backend.run(lo, hi)
         t2 = clock()

@@ -206,3 +206,29 @@ def test_sharded_skeleton_two_ranks_one_gpu():
         np.testing.assert_array_equal(rl, ref.removed_level)
         assert unions(xy, bits) == unions(ref.sep_xy, ref.sep_bits)
         assert tests == ref.stats["tests"]
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_level_split_matches_split_by_work(world):
+    """pcg_level_split (the C cut the sharded loop uses) == split_by_work over the chunk work
+    prefix, at every depth of a real skeleton; the ranges tile [0, total)."""
+    from rcaeval_amd.dist import GpuLevelBackend, split_by_work
+    from rcaeval_amd.engine import get_engine
+    eng = get_engine(0)
+    X = synth.gaussian_sem(400, 2000, seed=21)
+    C = eng.corr(X)
+    be = GpuLevelBackend(eng, C, X.shape[0], 0.05, 0, world)
+    try:
+        for depth in range(4):
+            total = be.begin(depth)
+            if total is None:
+                break
+            prefix = be.prefix(total)
+            cuts = [be.split(r, world) for r in range(world)]
+            assert cuts == [split_by_work(prefix, r, world) for r in range(world)]
+            assert cuts[0][0] == 0 and cuts[-1][1] == total
+            assert all(cuts[r][1] == cuts[r + 1][0] for r in range(world - 1))
+            be.run(0, total)
+            be.end()
+    finally:
+        be.finish()
