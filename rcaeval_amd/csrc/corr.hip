@@ -6,9 +6,9 @@
 //   s = sqrt(diag(c)); c /= s[:, None]; c /= s[None, :]; clip(c, -1, 1)
 // X here is the caller's N x n (time x metrics) array, so c = Xc^T Xc.
 //
-// GEMM: 64 x 64 output tile per 256-thread block (4 waves, 32 x 32 per wave = 2 x 2
-// v_mfma_f64_16x16x4_f64 tiles), K (time) staged through LDS in 16-row slabs, double
-// buffered; the mean subtraction is fused into the staging load. Only upper-triangle
+// GEMM: 128 x 128 output tile per 256-thread block (4 waves, 64 x 64 per wave = 4 x 4
+// v_mfma_f64_16x16x4_f64 tiles, 64 accumulator doubles per lane), K (time) staged through
+// LDS in 8-row slabs, double buffered; the mean subtraction is fused into the staging load. Only upper-triangle
 // tiles are computed (c is symmetric); the epilogue mirrors them. Roofline: MFMA fp64
 // (2*N*n^2 flops); bytes 8*N*n*(n/64) staged per tile row, L2-served.
 #include <hip/hip_runtime.h>
@@ -22,10 +22,10 @@ namespace {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-constexpr int TILE = 64;
-constexpr int KT = 16;
+constexpr int TILE = 128;
+constexpr int KT = 8;
 constexpr int PAD = 1;  // LDS row padding (doubles) against bank conflicts
-constexpr int MEAN_ROWS = 256;
+constexpr int MEAN_ROWS = 32;   // rows per partial column sum: ~2500 blocks fill the chip
 
 // partial column sums over row chunks (deterministic two-pass mean)
 __global__ void k_colsum_partial(const double *X, int64_t N, int n, int64_t ldx, double *part) {
@@ -77,26 +77,28 @@ __global__ __launch_bounds__(256) void k_xtx(const double *X, int64_t N, int n, 
     G += (int64_t)slab * slab_stride;
     const int i0 = bi * TILE, j0 = bj * TILE;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
+    const int wr = (wave >> 1) * 64, wc = (wave & 1) * 64;
 
-    // staging: 16 x 64 slab = 1024 doubles per operand, 4 per thread
-    const int sc = tid & 63;          // column within the tile
-    const int sr = tid >> 6;          // rows sr, sr+4, sr+8, sr+12
+    // staging: KT x 128 slab = 1024 doubles per operand, 4 per thread (one 1-KiB row segment
+    // per wave and k-row: coalesced)
+    const int sc = tid & 127;         // column within the tile
+    const int sr = tid >> 7;          // rows sr, sr+2, sr+4, sr+6
     const double ma = (i0 + sc < n) ? mean[i0 + sc] : 0.0;
     const double mb = (j0 + sc < n) ? mean[j0 + sc] : 0.0;
     const bool va = i0 + sc < n, vb = j0 + sc < n;
 
-    d4 acc[2][2];
+    // each wave owns a 64 x 64 sub-tile = 4 x 4 MFMA 16x16 tiles (64 accumulator doubles)
+    d4 acc[4][4];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+        for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
 
     double ra[4], rb[4];
     auto load = [&](int64_t t0) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const int64_t t = t0 + sr + 4 * q;
+            const int64_t t = t0 + sr + 2 * q;
             const bool vt = t < kend;
             ra[q] = (vt && va) ? X[t * ldx + i0 + sc] - ma : 0.0;
             rb[q] = (vt && vb) ? X[t * ldx + j0 + sc] - mb : 0.0;
@@ -105,8 +107,8 @@ __global__ __launch_bounds__(256) void k_xtx(const double *X, int64_t N, int n, 
     auto store = [&](int buf) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            As[buf][sr + 4 * q][sc] = ra[q];
-            Bs[buf][sr + 4 * q][sc] = rb[q];
+            As[buf][sr + 2 * q][sc] = ra[q];
+            Bs[buf][sr + 2 * q][sc] = rb[q];
         }
     };
 
@@ -120,23 +122,26 @@ __global__ __launch_bounds__(256) void k_xtx(const double *X, int64_t N, int n, 
         if (kk + 1 < nk) load(kbeg + (kk + 1) * KT);
 #pragma unroll
         for (int k4 = 0; k4 < KT; k4 += 4) {
-            double a0 = As[buf][k4 + fk][wr + fr];
-            double a1 = As[buf][k4 + fk][wr + 16 + fr];
-            double b0 = Bs[buf][k4 + fk][wc + fr];
-            double b1 = Bs[buf][k4 + fk][wc + 16 + fr];
-            acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+            double av[4], bv[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                av[q] = As[buf][k4 + fk][wr + 16 * q + fr];
+                bv[q] = Bs[buf][k4 + fk][wc + 16 * q + fr];
+            }
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
         }
         if (kk + 1 < nk) store(buf ^ 1);
         __syncthreads();
     }
     // epilogue: C/D map of v_mfma_f64_16x16x4_f64: col = lane & 15, row = (lane >> 4) + 4 * r
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < 4; ++b)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int i = i0 + wr + 16 * a + (lane >> 4) + 4 * r;
@@ -228,12 +233,13 @@ __global__ void k_gather_finish(const double *Gg, int64_t rows_per_rank, int n, 
 }
 
 // split-K factor: a function of the problem only (n, N), so every world size sums the
-// same slabs in the same order; ~15 blocks per upper tile fills 256 CUs x 4 blocks with
+// same slabs in the same order; ~2048 blocks in all (n = 2000: 136 upper tiles x 15) fill
+// 256 CUs x 2 blocks in four even rounds, and 1/2/4/8 ranks in whole rounds, with
 // little tail at 1..8 ranks
 int split_k(int n, int64_t N, int64_t *kchunk_out) {
     const int T = (n + TILE - 1) / TILE;
     const int ntiles = T * (T + 1) / 2;
-    int ks = (int)std::min<int64_t>(std::max<int64_t>(1, (7680 + ntiles - 1) / ntiles), std::max<int64_t>(1, N / 512));
+    int ks = (int)std::min<int64_t>(std::max<int64_t>(1, (2048 + ntiles / 2) / ntiles), std::max<int64_t>(1, N / 512));
     ks = std::min(ks, 16);
     const int64_t kchunk = (((N + ks - 1) / ks) + KT - 1) / KT * KT;
     *kchunk_out = kchunk;

@@ -200,19 +200,22 @@ __global__ void k_fill_nbr(const uint64_t *adj, int n, int W, const int32_t *off
     }
 }
 
-// rm -> adjacency bitmask + removed_level (the level barrier, SkeletonDiscovery.py:141-144)
-__global__ void k_apply(const uint8_t *rm, uint64_t *adj, int8_t *rl, int n, int W, int d) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)n * W) return;
-    const int x = (int)(i / W), w = (int)(i % W);
-    uint64_t m = 0;
-    const int yend = min(n, w * 64 + 64);
-    for (int y = w * 64; y < yend; ++y)
-        if (rm[(int64_t)x * n + y]) {
-            m |= 1ull << (y - w * 64);
-            rl[(int64_t)x * n + y] = (int8_t)d;
-        }
-    if (m) adj[i] &= ~m;
+// rm -> adjacency bitmask + removed_level (the level barrier, SkeletonDiscovery.py:141-144).
+// One lane per removal byte (coalesced 64-byte row segments); the wave's ballot is the
+// 64-bit mask cleared from adjacency word (x, w).
+__global__ __launch_bounds__(256) void k_apply(const uint8_t *rm, uint64_t *adj, int8_t *rl, int n, int W, int d) {
+    const int lane = threadIdx.x & 63;
+    const int64_t word = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;   // wave-uniform
+    if (word >= (int64_t)n * W) return;
+    const int x = (int)(word / W), w = (int)(word % W);
+    const int y = w * 64 + lane;
+    bool removed = false;
+    if (y < n) {
+        removed = rm[(int64_t)x * n + y] != 0;
+        if (removed) rl[(int64_t)x * n + y] = (int8_t)d;
+    }
+    const unsigned long long m = __ballot(removed);
+    if (lane == 0 && m) adj[word] &= ~m;
 }
 
 // export non-empty union rows of removed ordered pairs: one lane per CSR slot; the wave
@@ -255,32 +258,56 @@ __global__ __launch_bounds__(256) void k_export(const int32_t *off, const int32_
 }
 
 // ---------------------------------------------------------------------------------------
-// depth 0: one chunk = one row x; tests (x, y) for y > x.
+// depth 0: one chunk = one 64 x 64 tile (bi <= bj) of the pair triangle; node bi*64 owns the
+// chunks of tile row bi. Decisions are staged in LDS so both rm[x][y] and its mirror
+// rm[y][x] are written as coalesced 64-byte row segments (every removal byte of the tile
+// pair is written, 0 or 1, by exactly this block).
 template <int MODE>
 __global__ __launch_bounds__(256) void k_level0(LevelArgs a) {
-    const int x = (int)(a.chunk_lo + blockIdx.x);
-    const double cxx = a.diag[x];
-    unsigned long long tests = 0, indep = 0;
+    __shared__ uint8_t flag[64][68];
+    const int64_t chunk = a.chunk_lo + blockIdx.x;
+    int lo = 0, hi = a.n;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (a.cpre[mid] <= chunk) lo = mid; else hi = mid;
+    }
+    const int bi = lo >> 6;
+    const int bj = bi + (int)(chunk - a.cpre[lo]);
+    const int x0 = bi * 64, y0 = bj * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     const int S0[1] = {0};
-    for (int y = x + 1 + threadIdx.x; y < a.n; y += blockDim.x) {
-        const double cxy = a.C[(int64_t)x * a.ldc + y];
-        const double cyy = a.diag[y];
-        double p = 0.0;
-        const int dec = decide<MODE>(a, cxy, cxx, cyy, &p);
-        ++tests;
-        if (dec == 2) {
-            push_deferred(a, x, y, S0, 0);
-            continue;
+    unsigned long long tests = 0, indep = 0;
+    const int y = y0 + tx;
+    const double cyy = y < a.n ? a.diag[y] : 0.0;
+#pragma unroll 4
+    for (int r = ty; r < 64; r += 4) {
+        const int x = x0 + r;
+        uint8_t f = 0;
+        if (x < a.n && y < a.n && y > x) {
+            const double cxy = a.C[(int64_t)x * a.ldc + y];
+            double p = 0.0;
+            const int dec = decide<MODE>(a, cxy, a.diag[x], cyy, &p);
+            ++tests;
+            if (dec == 2) {
+                push_deferred(a, x, y, S0, 0);
+            } else {
+                if (MODE == MODE_FULLP) {
+                    if (a.record) push_record(a.records, a.rec_cap, &a.ctr->records, x, y, 0, S0, p);
+                    if (fabs(p - a.alpha) < 1e-9) push_record(a.nearl, a.near_cap, &a.ctr->near_alpha, x, y, 0, S0, p);
+                }
+                if (dec == 1) { f = 1; ++indep; }
+            }
         }
-        if (MODE == MODE_FULLP) {
-            if (a.record) push_record(a.records, a.rec_cap, &a.ctr->records, x, y, 0, S0, p);
-            if (fabs(p - a.alpha) < 1e-9) push_record(a.nearl, a.near_cap, &a.ctr->near_alpha, x, y, 0, S0, p);
-        }
-        if (dec == 1) {
-            ++indep;
-            a.rm[(int64_t)x * a.n + y] = 1;
-            a.rm[(int64_t)y * a.n + x] = 1;
-        }
+        flag[r][tx] = f;
+    }
+    __syncthreads();
+    // rows x of the tile: rm[x][y0 + tx]; mirrored rows y: rm[y][x0 + tx] = flag[tx][y - y0]
+#pragma unroll 4
+    for (int r = ty; r < 64; r += 4) {
+        const int x = x0 + r, yy = y0 + tx;
+        if (x < a.n && yy < a.n && yy > x) a.rm[(int64_t)x * a.n + yy] = flag[r][tx];
+        const int ym = y0 + r, xm = x0 + tx;
+        if (ym < a.n && xm < a.n && ym > xm) a.rm[(int64_t)ym * a.n + xm] = flag[tx][r];
     }
     tests = wave_sum(tests);
     indep = wave_sum(indep);
@@ -1548,12 +1575,19 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
     h->work_h.assign(n, 0);
     h->maxdeg_small = 0;
     if (depth == 0) {
+        // 64 x 64 tiles of the pair triangle; node 64*bi owns the T - bi tiles of tile row bi
         h->chunk = 256;
         h->spl = 1;
         h->tgroup = false;
-        for (int x = 0; x <= n; ++x) { cs[x] = x; cl[x] = 0; }
+        const int T = (n + 63) / 64;
+        int64_t acc = 0;
+        for (int x = 0; x <= n; ++x) {
+            cs[x] = acc;
+            cl[x] = 0;
+            if (x < n && (x & 63) == 0) acc += T - (x >> 6);
+        }
         for (int x = 0; x < n; ++x) h->work_h[x] = n - 1 - x;
-        h->total_small = n;
+        h->total_small = acc;
         h->total_large = 0;
     } else {
         // small class units: T-group lane tasks (threshold mode, depth 2..4) or S ranks
@@ -1654,9 +1688,16 @@ extern "C" int pcg_level_chunk_work(pcg_handle *h, int64_t *prefix_host, int64_t
         for (int x = 0; x < n; ++x) {
             const int64_t c0 = cp[x], c1 = cp[x + 1];
             if (c1 == c0) continue;
-            if (h->depth == 0) {
-                acc += h->work_h[x] + 1;
-                prefix_host[base + c0 + 1] = acc;
+            if (h->depth == 0) {   // tile (x/64, x/64 + c - c0): its pair count
+                const int bi = x >> 6, T = (n + 63) / 64;
+                const int64_t ri = std::min<int64_t>(64, n - 64 * (int64_t)bi);
+                for (int64_t c = c0; c < c1; ++c) {
+                    const int bj = bi + (int)(c - c0);
+                    (void)T;
+                    const int64_t rj = std::min<int64_t>(64, n - 64 * (int64_t)bj);
+                    acc += (bj == bi ? ri * (ri - 1) / 2 : ri * rj) + 1;
+                    prefix_host[base + c + 1] = acc;
+                }
                 continue;
             }
             const int D = h->deg_h[x];
@@ -1791,7 +1832,7 @@ extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
                            (int32_t *)h->export_xy.p + 2 * h->export_rows,
                            (uint64_t *)h->exportbuf.p + h->export_rows * W, room, &ctr->exported);
     const int64_t nw = (int64_t)n * W;
-    hipLaunchKernelGGL(k_apply, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, h->stream, (const uint8_t *)rmb,
+    hipLaunchKernelGGL(k_apply, dim3((unsigned)((nw * 64 + 255) / 256)), dim3(256), 0, h->stream, (const uint8_t *)rmb,
                        (uint64_t *)h->adj.p, h->rl, n, W, d);
     PCG_HIP(h, hipGetLastError());
     int rc = graph_launch(h);
