@@ -77,6 +77,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-depth", type=int, default=2, help="depths timed for the CPU port baseline")
     ap.add_argument("--json-extra", action="store_true", help="print per-level detail to stderr")
+    ap.add_argument("--workload", choices=["skeleton", "rq2"], default="skeleton",
+                    help="skeleton: the headline line (config 5); rq2: every case of an Online-Boutique-shaped "
+                         "RQ2 tree through pc_pagerank, cases dealt one per GPU (config 2)")
+    ap.add_argument("--rq2-cases", type=int, default=125, help="cases in the synthetic RQ2 tree")
     return ap.parse_args()
 
 
@@ -125,8 +129,78 @@ def cpu_reference_equiv(X: np.ndarray, ref, budget_s: float = 4.0) -> dict:
     return {"value": count / dt, "cores": 1, "tests": count, "seconds": dt}
 
 
+OB_PC_PAGERANK_S_PER_CASE = 3.39   # paper Table 6, PC-PageRank, Online Boutique, 8-CPU machine
+
+
+def rq2_main(args):
+    """BASELINE config 2: the RQ2 loop (rcaeval_amd.rq2.run — read_csv, window, preprocess,
+    K1 + skeleton + orientation + PageRank, JSON dump) over a synthetic Online-Boutique-shaped
+    tree (44 metrics + time per case, 1200 s recorded, windowed to 300 + 300 rows by rq2).
+    Cases are dealt round-robin, one process per GPU; value = cases/s of the whole job."""
+    import shutil
+    import tempfile
+
+    import torch
+    from rcaeval_amd import rq2, synth
+    from rcaeval_amd.engine import get_engine
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("gloo")
+    get_engine(local)
+    base = os.environ.get("PCG_RQ2_DIR") or tempfile.mkdtemp(prefix="rq2_")
+    root = os.path.join(base, "data", "online-boutique")
+    services = [s for s in synth.OB_SERVICES if s not in ("frontend", "redis")]
+    faults = ("cpu", "mem", "delay", "loss", "disk")
+    per = max(1, args.rq2_cases // (len(services) * len(faults)))
+    if rank == 0 and not os.path.isdir(root):
+        synth.write_rq2_dataset(root, services=services, faults=faults, cases=per, rows=1200, seed=args.seed)
+    if world > 1:
+        torch.distributed.barrier()
+    out_dir = os.path.join(base, f"out_{rank}")
+    # warm-up on this rank's first case (engine, HIP module load), then the timed pass
+    first = rq2.list_cases(root)[rank::world][:1]
+    for p in first:
+        rq2.process(p, "pc_pagerank", "online-boutique", tempfile.mkdtemp(), length=None)
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    res = rq2.run(root, "pc_pagerank", "online-boutique", out_dir, rank=rank, world=world)
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+    if rank == 0:
+        n_cases = res["cases"]
+        s_per_case = dt / n_cases
+        print(json.dumps({
+            "metric": "PC-PageRank RQ2 cases/s (Online-Boutique-shaped, 44 metrics, cases dealt over GPUs)",
+            "value": n_cases / dt, "unit": "cases/s", "n_gpus": world, "steps": 1, "warmup": 1,
+            "ms_per_step": 1000.0 * dt, "higher_is_better": True, "scaling": "weak",
+            # whole-job cases/s over the published sequential rate (1 / 3.39 s per case)
+            "vs_baseline": (n_cases / dt) * OB_PC_PAGERANK_S_PER_CASE,
+            "dtype": "f64", "data": "synthetic RQ2 tree (rcaeval_amd.synth.write_rq2_dataset)",
+            "config": {"workload": f"rq2.run pc_pagerank over {n_cases} cases ({per} per service x fault), "
+                                   "read_csv + window + preprocess + PC + orientation + PageRank + JSON",
+                       "parallelism": f"cases round-robin over {world} GPU(s)"},
+            "seconds_per_case_per_gpu": s_per_case * world,
+            "published_seconds_per_case_cpu": OB_PC_PAGERANK_S_PER_CASE,
+            "summary": res["summary"]}), flush=True)
+    if not os.environ.get("PCG_RQ2_DIR") and rank == 0:
+        shutil.rmtree(base, ignore_errors=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.workload == "rq2":
+        return rq2_main(args)
     import torch
     from rcaeval_amd import _lib, synth
     from rcaeval_amd.engine import get_engine

@@ -76,3 +76,65 @@ def telemetry_frame(n_metrics: int = 49, n_rows: int = 600, n_constant: int = 2,
     df = pd.DataFrame(X, columns=cols)
     df.insert(0, "time", np.arange(1692569000, 1692569000 + n_rows))
     return df
+
+
+OB_SERVICES = ["adservice", "cartservice", "checkoutservice", "currencyservice", "emailservice", "frontend",
+               "paymentservice", "productcatalogservice", "recommendationservice", "shippingservice", "redis"]
+OB_METRICS = ["cpu", "mem", "latency-50", "latency-90"]
+FAULT_METRIC = {"cpu": "cpu", "mem": "mem", "delay": "latency-90", "loss": "latency-90", "disk": "mem"}
+
+
+def rq2_case_frame(services=None, metrics=None, rows: int = 1200, root_service: str = "cartservice",
+                   fault: str = "cpu", seed: int = 0, t0: int = 1692569000):
+    """One RCAEval-RQ2-shaped case: ``time`` + ``<service>_<metric>`` columns, ``rows``
+    one-second samples, a fault injected at the midpoint (returned as ``inject_time``):
+    the root-cause metric shifts by 4 sigma and the shift propagates to its SEM descendants.
+    Returns (DataFrame, inject_time)."""
+    import pandas as pd
+
+    services = services or OB_SERVICES
+    metrics = metrics or OB_METRICS
+    cols = [f"{s}_{m}" for s in services for m in metrics]
+    n = len(cols)
+    W, order, rng = sem_dag(n, edge_prob=3.0 / max(n - 1, 1), w_low=0.3, w_high=0.9, seed=seed)
+    E = rng.standard_normal((rows, n))
+    half = rows // 2
+    root = cols.index(f"{root_service}_{FAULT_METRIC[fault]}")
+    E[half:, root] += 4.0
+    X = np.zeros((rows, n))
+    for j in order:
+        parents = np.nonzero(W[:, j])[0]
+        col = E[:, j].copy()
+        if parents.size:
+            col += X[:, parents] @ W[parents, j]
+        X[:, j] = col
+    X = X * rng.uniform(0.5, 5.0, n) + rng.uniform(10, 100, n)
+    for j, c in enumerate(cols):
+        if c.endswith("_mem"):
+            X[:, j] = np.abs(X[:, j]) * 1e6
+    df = pd.DataFrame(X, columns=cols)
+    df.insert(0, "time", np.arange(t0, t0 + rows))
+    return df, t0 + half
+
+
+def write_rq2_dataset(root: str, services=None, faults=("cpu", "mem", "delay"), cases: int = 2,
+                      rows: int = 1200, seed: int = 0) -> list:
+    """An Online-Boutique-shaped RQ2 tree under ``root``:
+    ``<service>_<fault>/<case>/{data.csv, inject_time.txt}`` (``rq2.py:203-206,244-245``)."""
+    import os
+
+    services = services or [s for s in OB_SERVICES if s not in ("frontend", "redis")][:4]
+    paths = []
+    k = 0
+    for svc in services:
+        for fault in faults:
+            for case in range(1, cases + 1):
+                d = os.path.join(root, f"{svc}_{fault}", str(case))
+                os.makedirs(d, exist_ok=True)
+                df, inject = rq2_case_frame(root_service=svc, fault=fault, rows=rows, seed=seed + k)
+                df.to_csv(os.path.join(d, "data.csv"), index=False)
+                with open(os.path.join(d, "inject_time.txt"), "w") as f:
+                    f.write(f"{inject}\n")
+                paths.append(os.path.join(d, "data.csv"))
+                k += 1
+    return paths

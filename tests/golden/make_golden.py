@@ -15,6 +15,9 @@ Fixtures (data only — inputs and expected outputs):
                     (oracle/orient.py) on small SEMs — pins pcg_orient across rounds.
   pagerank.npz      scikit-network-0.31.0-restated PageRank (oracle/pagerank.py, scipy CSR + numpy
                     sums) on random 0/1 graphs — pins the GPU kernel bitwise.
+  evaluator.json    AC@k / Avg@k (service- and metric-level) of the REFERENCE
+                    ``RCAEval.benchmark.evaluation.Evaluator`` with ``RCAEval.classes.graph.Node``
+                    on seeded random rank lists (the RQ2 scorer, rq2.py:339-419).
 The reference code itself is never copied here; only its outputs are stored.
 """
 from __future__ import annotations
@@ -65,6 +68,39 @@ def make_random_walk():
     with open(os.path.join(HERE, "random_walk.json"), "w") as f:
         json.dump(out, f)
     print("random_walk.json", len(out))
+
+
+def evaluator_cases():
+    rng = np.random.default_rng(5)
+    services = ["cartservice", "adservice", "frontend", "redis", "emailservice", "paymentservice"]
+    metrics = ["cpu", "mem", "latency-90", "latency-50"]
+    cases = []
+    for _ in range(40):
+        names = [f"{services[i]}_{metrics[j]}" for i, j in zip(rng.integers(0, 6, 12), rng.integers(0, 4, 12))]
+        k = int(rng.integers(0, 12))
+        ans = (services[int(rng.integers(0, 6))], metrics[int(rng.integers(0, 3))])
+        cases.append({"ranks": names[:k + 1], "answer": list(ans)})
+    return cases
+
+
+def make_evaluator():
+    sys.path.insert(0, REF)
+    from RCAEval.benchmark.evaluation import Evaluator  # reference, imported (not copied)
+    from RCAEval.classes.graph import Node
+    cases = evaluator_cases()
+    s_ev, f_ev = Evaluator(), Evaluator()
+    for c in cases:
+        f_ev.add_case([Node(*x.split("_")[:2]) for x in c["ranks"]], Node(*c["answer"]))
+        s_ev.add_case([Node(x.split("_")[0], "unknown") for x in c["ranks"]], Node(c["answer"][0], "unknown"))
+    out = {"cases": cases,
+           "metric": {str(k): [f_ev.accuracy(k), f_ev.accuracy_service(k), f_ev.average(k), f_ev.average_service(k)]
+                      for k in range(0, 7)},
+           "service": {str(k): [s_ev.accuracy(k), s_ev.accuracy_service(k), s_ev.average(k), s_ev.average_service(k)]
+                       for k in range(0, 7)},
+           "empty": [Evaluator().accuracy(1), Evaluator().average(5)]}
+    with open(os.path.join(HERE, "evaluator.json"), "w") as f:
+        json.dump(out, f)
+    print("evaluator.json", len(cases))
 
 
 def telemetry_frames():
@@ -172,5 +208,6 @@ if __name__ == "__main__":
     if os.path.isdir(REF):
         make_random_walk()
         make_preprocess()
+        make_evaluator()
     else:
         print("reference not present: random_walk / preprocess goldens not regenerated")

@@ -232,3 +232,21 @@ def test_level_split_matches_split_by_work(world):
             be.end()
     finally:
         be.finish()
+
+
+def test_rq2_run_matches_oracle_per_case(tmp_path):
+    """the RQ2 loop over an Online-Boutique-shaped case tree; every
+    case's rank list equals the CPU oracle pipeline on the same window."""
+    from rcaeval_amd import rq2
+    root = os.path.join(str(tmp_path), "data", "online-boutique")
+    paths = synth.write_rq2_dataset(root, services=["cartservice", "adservice"], faults=("cpu", "delay"),
+                                    cases=1, rows=1200)
+    out_dir = os.path.join(str(tmp_path), "out")
+    res = rq2.run(root, "pc_pagerank", "online-boutique", out_dir)
+    assert res["cases"] == len(paths) == 4
+    for p in paths:
+        c = rq2.load_case(p)
+        ranks, _ = _oracle_pipeline(c["data"], "online-boutique", "pagerank")
+        got = rq2.load_json(os.path.join(out_dir, "results", c["result_name"]))["0"]
+        assert got == ranks
+    assert set(res["summary"]) >= {"Avg@5-CPU", "Avg@5-DELAY"}
