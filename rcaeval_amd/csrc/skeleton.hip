@@ -33,6 +33,7 @@
 #include <climits>
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 
 #include "fisherz_dev.h"
 #include "handle.h"
@@ -123,6 +124,17 @@ __device__ __forceinline__ void flag_error(const LevelArgs &a, int err) {
     uint8_t *status = a.rm + (int64_t)a.n * a.n;
     if (err & 1) status[1] = 1;
     if (err & 2) status[2] = 1;
+}
+
+// (group, t0) pairs of k_level_lds_t for a node of degree D at depth DM: t0 in
+// [g*TG + 1, D - DM + 1] for every group g with g*TG <= D - DM
+__host__ __device__ inline int tg_pairs(int D, int DM) {
+    int s = 0;
+    for (int cb = 0; cb <= D - DM; cb += PCG_TGROUP) {
+        const int m = D - (DM - 1) - cb;
+        if (m > 0) s += m;
+    }
+    return s;
 }
 
 // 0 dependent, 1 independent, 2 exact path. p written in FULL_P mode.
@@ -904,13 +916,15 @@ __global__ __launch_bounds__(256, 4) void k_level_lds_t(LevelArgs a) {
     unsigned long long *uprop = uself + D;                        // D
     int32_t *nxs = reinterpret_cast<int32_t *>(uprop + D);       // D
     int *s_tx = nxs + D;                                          // 1
-    unsigned long long *btab = reinterpret_cast<unsigned long long *>(smem + a.lds_btab_off);
-    unsigned long long *gpre = btab + (D + 1) * (DM + 1);         // task prefix per group
+    unsigned *btab = reinterpret_cast<unsigned *>(smem + a.lds_btab_off);   // C(c, i), c <= D, i <= DM
+    unsigned *ppre = btab + (D + 1) * (DM + 1);                   // task prefix per (g, t0) pair
+    unsigned short *pinfo = reinterpret_cast<unsigned short *>(ppre + tg_pairs(D, DM) + 1);  // g << 8 | t0
+    int *s_np = s_tx + 1;
 
     for (int i = tid; i < D; i += bs) nxs[i] = nxg[i];
     for (int e = tid; e < (D + 1) * (DM + 1); e += bs) {
         const int c = e / (DM + 1), i = e - c * (DM + 1);
-        btab[e] = pcg_binom(a.binom, c, i);
+        btab[e] = (unsigned)pcg_binom(a.binom, c, i);             // <= C(64, 4): fits 32 bits
     }
     __syncthreads();
     for (int e = tid; e < D * DS; e += bs) {
@@ -933,45 +947,62 @@ __global__ __launch_bounds__(256, 4) void k_level_lds_t(LevelArgs a) {
         int c = 0;
         while (c < D && nxs[c] < x) ++c;
         *s_tx = c;
-        unsigned long long acc = 0;
-        for (int g = 0; g < ng; ++g) {
-            gpre[g] = acc;
-            const int Dp = D - g * TG - 1;
-            acc += (Dp >= DT) ? btab[Dp * (DM + 1) + DT] : 0ull;
-        }
-        gpre[ng] = acc;
+        // tasks: group g, then t0 = min(T) ascending, then colex rank of T \ {t0} over (t0, D)
+        unsigned acc = 0;
+        int q = 0;
+        for (int g = 0; g < ng; ++g)
+            for (int t0 = g * TG + 1; t0 <= D - DT; ++t0) {
+                ppre[q] = acc;
+                pinfo[q] = (unsigned short)((g << 8) | t0);
+                acc += btab[(D - 1 - t0) * (DM + 1) + DT - 1];
+                ++q;
+            }
+        ppre[q] = acc;
+        *s_np = q;
     }
     __syncthreads();
     const int tx = *s_tx;
+    const int np = *s_np;
     const double Cxx = a.diag[x];
-    const uint64_t ntask = gpre[ng];
+    const uint64_t ntask = ppre[np];
     const uint64_t r0 = (uint64_t)(chunk - a.cpre[x]) * (uint64_t)bs * (uint64_t)a.spl;
     const uint64_t r1 = min(ntask, r0 + (uint64_t)bs * (uint64_t)a.spl);
     unsigned long long tests = 0, indep = 0;
     unsigned tcount = 0;
 
     for (uint64_t task = r0 + tid; task < r1; task += bs) {
-        int g = 0;
-        while (g + 1 < ng && gpre[g + 1] <= task) ++g;
-        const int cbase = g * TG;
+        // (g, t0) pair of this task: the last pair whose prefix is <= task
+        int lq = 0, hq = np;
+        while (hq - lq > 1) {
+            const int mid = (lq + hq) >> 1;
+            if (ppre[mid] <= task) lq = mid; else hq = mid;
+        }
+        const int info = pinfo[lq];
+        const int cbase = (info >> 8) * TG;
         int T[DT];
-        {   // colex unrank of the (d-1)-subset over [cbase+1, D)
-            uint64_t rr = task - gpre[g];
-            int hi_ = D - cbase - 1;
+        T[0] = info & 255;
+        {   // colex unrank of T \ {t0}, a (d-2)-subset of (t0, D)
+            unsigned rr = (unsigned)(task - ppre[lq]);
+            int hi_ = D - T[0] - 1;
 #pragma unroll
-            for (int ii = DT - 1; ii >= 0; --ii) {
+            for (int ii = DT - 2; ii >= 0; --ii) {
                 int lo_ = ii, up = hi_ - 1;
                 while (lo_ < up) {
                     const int mid = (lo_ + up + 1) >> 1;
                     if (btab[mid * (DM + 1) + ii + 1] <= rr) lo_ = mid; else up = mid - 1;
                 }
-                T[ii] = lo_;
+                T[ii + 1] = lo_;
                 rr -= btab[lo_ * (DM + 1) + ii + 1];
                 hi_ = lo_;
             }
 #pragma unroll
-            for (int ii = 0; ii < DT; ++ii) T[ii] += cbase + 1;
+            for (int ii = 1; ii < DT; ++ii) T[ii] += T[0] + 1;
         }
+        // candidates c in [cbase, min(t0, cbase + TG)): lanes of a wave share t0 except at pair
+        // boundaries, so the wave's largest candidate count bounds the sweep uniformly
+        const int nval = min(T[0] - cbase, TG);
+        const int nmax = __builtin_amdgcn_readfirstlane(
+            1 + (__ballot(nval >= 2) != 0) + (__ballot(nval >= 3) != 0) + (__ballot(nval >= 4) != 0));
         unsigned long long Tmask = 0;
 #pragma unroll
         for (int i = 0; i < DT; ++i) Tmask |= 1ull << T[i];
@@ -1018,6 +1049,11 @@ __global__ __launch_bounds__(256, 4) void k_level_lds_t(LevelArgs a) {
         bool okc[TG];
 #pragma unroll
         for (int jj = 0; jj < TG; ++jj) {
+            rl[jj] = uc[jj] = hc[jj] = 0.0;
+            okc[jj] = false;
+#pragma unroll
+            for (int i = 0; i < DT; ++i) lc[jj][i] = 0.0;
+            if (jj >= nmax) continue;                 // wave-uniform
             const int c = cbase + jj;
             const bool valid = c < T[0];
             const int cc = valid ? c : 0;
@@ -1049,83 +1085,92 @@ __global__ __launch_bounds__(256, 4) void k_level_lds_t(LevelArgs a) {
         for (int jj = 0; jj < TG; ++jj) okm |= (unsigned)okc[jj] << jj;
         const unsigned vmask = (1u << (cend - cbase)) - 1u;
 
-        for (int t = 0; t < D; ++t) {
-            // t in T: the lane idles through this y (branch-free: no exec-mask split)
-            const bool inTset = (Tmask >> t) & 1ull;
-            const unsigned long long lm = lmask[t];
-            const bool own = (t < tx) && ((lm & Tmask) == Tmask);
-            const double *Mt = M + t * DS;
-            // the TG candidate operands M[t][cbase .. cbase+TG) are contiguous and 32-B aligned
-            // (DS % 4 == 0, cbase % 4 == 0): two 16-B LDS reads, broadcast across the lanes of
-            // the wave that share the group
-            const double2 m01 = *reinterpret_cast<const double2 *>(Mt + cbase);
-            const double2 m23 = *reinterpret_cast<const double2 *>(Mt + cbase + 2);
-            double vT[DT];
-            double vv = 0.0, uv = 0.0;
-#pragma unroll
-            for (int i = 0; i < DT; ++i) {
-                double v = 0.0;
-#pragma unroll
-                for (int j = 0; j <= i; ++j) v += Li[i][j] * Mt[T[j]];
-                vT[i] = v;
-                vv += v * v;
-                uv += uT[i] * v;
-            }
-            const double byy = Md[t] - vv;
-            const double bxy = Mx[t] - uv;
-            // live candidates: valid, c != y, and not deduplicated onto y (S in adj(y), y < x)
-            const unsigned tb = ((unsigned)(t - cbase) < (unsigned)TG) ? (1u << (t - cbase)) : 0u;
-            const unsigned skip = own ? (unsigned)(lm >> cbase) : 0u;
-            const unsigned live = inTset ? 0u : (vmask & ~tb & ~skip);
-            double sc[TG] = {m01.x, m01.y, m23.x, m23.y};
-            // TG independent chains, interleaved
-#pragma unroll
-            for (int i = 0; i < DT; ++i)
-#pragma unroll
-                for (int jj = 0; jj < TG; ++jj) sc[jj] -= lc[jj][i] * vT[i];
-            unsigned dep = 0;
-#pragma unroll
-            for (int jj = 0; jj < TG; ++jj) {
-                const double vc = sc[jj] * rl[jj];
-                const double cyy = byy - vc * vc;
-                const double cxy = bxy - uc[jj] * vc;
-                const double num = cxy * cxy;
-                const double th = hc[jj] * cyy;
-                dep |= (unsigned)((num > th) & (num < th * rratio)) << jj;
-            }
-            tcount += __popc(live);
-            const unsigned rare = live & ~(dep & okm);
-            if (__ballot(rare != 0u)) {
-                if (rare) {
-#pragma unroll
-                    for (int jj = 0; jj < TG; ++jj) {
-                        if (!((rare >> jj) & 1u)) continue;
-                        const int c = cbase + jj;
-                        // recompute the decision pieces for this c (rare path)
-                        double s = Mt[c];
-#pragma unroll
-                        for (int i = 0; i < DT; ++i) s -= lc[jj][i] * vT[i];
-                        const double vc = s * rl[jj];
-                        const double cyy = byy - vc * vc;
-                        const double cxy = bxy - uc[jj] * vc;
-                        const double cxx = hc[jj] / a.hi2;
-                        const bool ind = okc[jj] && (cxy * cxy < a.lo2 * cxx * cyy) && (cyy > 0.0);
-                        const unsigned long long Smask = Tmask | (1ull << c);
-                        if (ind) {
-                            ++indep;
-                            atomicOr(&uself[t], Smask);
-                            if (((lm & Smask) == Smask) && t >= tx) atomicOr(&uprop[t], Smask);
-                        } else {
-                            int sg[DM];
-                            sg[0] = nxs[c];
-#pragma unroll
-                            for (int i = 0; i < DT; ++i) sg[i + 1] = nxs[T[i]];
-                            push_deferred(a, x, nxs[t], sg, DM);
+        // the y sweep, specialised on the wave-uniform candidate count so the NC chains stay
+        // branch-free and interleaved (candidates beyond the count are not evaluated at all)
+        auto sweep = [&](auto nc_tag) {
+            constexpr int NC = decltype(nc_tag)::value;
+            for (int t = 0; t < D; ++t) {
+                // t in T: the lane idles through this y (branch-free: no exec-mask split)
+                const bool inTset = (Tmask >> t) & 1ull;
+                const unsigned long long lm = lmask[t];
+                const bool own = (t < tx) && ((lm & Tmask) == Tmask);
+                const double *Mt = M + t * DS;
+                // the TG candidate operands M[t][cbase .. cbase+TG) are contiguous and 32-B aligned
+                // (DS % 4 == 0, cbase % 4 == 0): two 16-B LDS reads, broadcast across the lanes of
+                // the wave that share the group
+                const double2 m01 = *reinterpret_cast<const double2 *>(Mt + cbase);
+                const double2 m23 = *reinterpret_cast<const double2 *>(Mt + cbase + 2);
+                double vT[DT];
+                double vv = 0.0, uv = 0.0;
+    #pragma unroll
+                for (int i = 0; i < DT; ++i) {
+                    double v = 0.0;
+    #pragma unroll
+                    for (int j = 0; j <= i; ++j) v += Li[i][j] * Mt[T[j]];
+                    vT[i] = v;
+                    vv += v * v;
+                    uv += uT[i] * v;
+                }
+                const double byy = Md[t] - vv;
+                const double bxy = Mx[t] - uv;
+                // live candidates: valid, c != y, and not deduplicated onto y (S in adj(y), y < x)
+                const unsigned tb = ((unsigned)(t - cbase) < (unsigned)TG) ? (1u << (t - cbase)) : 0u;
+                const unsigned skip = own ? (unsigned)(lm >> cbase) : 0u;
+                const unsigned live = inTset ? 0u : (vmask & ~tb & ~skip);
+                double sc[TG] = {m01.x, m01.y, m23.x, m23.y};
+                // TG independent chains, interleaved
+    #pragma unroll
+                for (int i = 0; i < DT; ++i)
+    #pragma unroll
+                    for (int jj = 0; jj < NC; ++jj) sc[jj] -= lc[jj][i] * vT[i];
+                unsigned dep = 0;
+    #pragma unroll
+                for (int jj = 0; jj < NC; ++jj) {
+                    const double vc = sc[jj] * rl[jj];
+                    const double cyy = byy - vc * vc;
+                    const double cxy = bxy - uc[jj] * vc;
+                    const double num = cxy * cxy;
+                    const double th = hc[jj] * cyy;
+                    dep |= (unsigned)((num > th) & (num < th * rratio)) << jj;
+                }
+                tcount += __popc(live);
+                const unsigned rare = live & ~(dep & okm);
+                if (__ballot(rare != 0u)) {
+                    if (rare) {
+    #pragma unroll
+                        for (int jj = 0; jj < TG; ++jj) {
+                            if (!((rare >> jj) & 1u)) continue;
+                            const int c = cbase + jj;
+                            // recompute the decision pieces for this c (rare path)
+                            double s = Mt[c];
+    #pragma unroll
+                            for (int i = 0; i < DT; ++i) s -= lc[jj][i] * vT[i];
+                            const double vc = s * rl[jj];
+                            const double cyy = byy - vc * vc;
+                            const double cxy = bxy - uc[jj] * vc;
+                            const double cxx = hc[jj] / a.hi2;
+                            const bool ind = okc[jj] && (cxy * cxy < a.lo2 * cxx * cyy) && (cyy > 0.0);
+                            const unsigned long long Smask = Tmask | (1ull << c);
+                            if (ind) {
+                                ++indep;
+                                atomicOr(&uself[t], Smask);
+                                if (((lm & Smask) == Smask) && t >= tx) atomicOr(&uprop[t], Smask);
+                            } else {
+                                int sg[DM];
+                                sg[0] = nxs[c];
+    #pragma unroll
+                                for (int i = 0; i < DT; ++i) sg[i + 1] = nxs[T[i]];
+                                push_deferred(a, x, nxs[t], sg, DM);
+                            }
                         }
                     }
                 }
             }
-        }
+        };
+        if (nmax >= 4) sweep(std::integral_constant<int, 4>{});
+        else if (nmax == 3) sweep(std::integral_constant<int, 3>{});
+        else if (nmax == 2) sweep(std::integral_constant<int, 2>{});
+        else sweep(std::integral_constant<int, 1>{});
         tests += tcount;
         tcount = 0;
     }
@@ -1426,6 +1471,11 @@ constexpr int SMALL_DEG = 64;        // LDS-resident kernel handles nodes with <
 size_t lds_small_core(int D) {  // k_level_lds_t is sized with D rounded up to 4 (its row stride)
  return ((size_t)D * D * 8 + (size_t)D * (2 * 8 + 3 * 8 + 4) + 16 + 15) & ~(size_t)15; }
 size_t lds_small_bytes(int D) { return lds_small_core(D) + (size_t)(D + 1) * 5 * 8 + 24 * 8; }
+// k_level_lds_t: u32 binomial table + (g, t0) pair prefix (u32) and ids (u16)
+size_t lds_tgroup_bytes(int D, int DM) {
+    const size_t np = (size_t)tg_pairs(D, DM);
+    return lds_small_core(D) + (size_t)(D + 1) * (DM + 1) * 4 + (np + 1) * 4 + np * 2 + 16;
+}
 
 // lane tasks of k_level_lds_t for a node of degree D at depth d (see the kernel)
 uint64_t tgroup_tasks(const pcg_handle *h, int D, int d) {
@@ -1764,7 +1814,7 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                     as.bs = 256;
                     const int dl = h->tgroup ? (h->maxdeg_small + 3) & ~3 : h->maxdeg_small;
                     as.lds_btab_off = (int)lds_small_core(dl);
-                    const size_t lds = lds_small_bytes(dl);
+                    const size_t lds = h->tgroup ? lds_tgroup_bytes(dl, d) : lds_small_bytes(dl);
                     if (h->tgroup) {
                         const dim3 grid((unsigned)(s_hi - s_lo)), block(256);
                         if (d == 2) hipLaunchKernelGGL(k_level_lds_t<2>, grid, block, lds, h->stream, as);
