@@ -205,6 +205,33 @@ int pcg_random_walk(pcg_handle *h, const double *P, int64_t m, int64_t ldp, int6
 int pcg_orient(int64_t n, const uint8_t *adj, const int32_t *sep_xy, const uint64_t *sep_bits,
                int64_t count, int priority, int32_t *graph);
 
+/* The R0 list of UCSepset.uc_sepset [U]: unshielded triples (x, y, z), x < z, in
+ * find_unshielded_triples order (GraphClass.py:157-165), with y in no S of sepset[x, z].
+ * triples: host 3*capacity int32 out (x, y, z); total: host out (all candidates; call
+ * again with capacity >= total to get them all).                                       */
+int pcg_uc_candidates(int64_t n, const uint8_t *adj, const int32_t *sep_xy, const uint64_t *sep_bits,
+                      int64_t count, int32_t *triples, int64_t capacity, int64_t *total);
+/* uc_sepset's collider step over `triples` in the given order (priority 3/4: R0 sorted
+ * by the max CI p-value, ascending / descending — the caller computes those p with
+ * pcg_fisherz_batch), then Meek.meek [U]. graph: host n x n int32 endpoint codes out.  */
+int pcg_orient_triples(int64_t n, const uint8_t *adj, const int32_t *triples, int64_t tcount,
+                       int32_t *graph);
+
+/* ---- batched Fisher-z tests on caller-chosen (x, y, S) -----------------------------
+ * Replaces individual `cg.ci_test(x, y, S)` / FisherZ.__call__ [U] calls that do not come
+ * from the level enumeration (GraphClass.py:78-98): UCSepset priority 3/4 conditioning
+ * sets (GraphClass.py:190-204), the stable=False skeleton (SkeletonDiscovery.py:112-131),
+ * FCI possible-d-sep tests. tests: device count x stride int32 rows
+ * [a, b, d, s_0 .. s_{d-1}, pad], a < b and S sorted, distinct (the cache-key canonical
+ * form, GraphClass.py:87-88), d <= PCG_MAX_LEVEL_DEPTH, stride >= d + 3.
+ * p: device count doubles out (the reference p expression; LU like numpy.linalg.inv).
+ * status: device count int32 out: 0 ok, 1 singular sub-matrix (LinAlgError -> ValueError),
+ * 2 math domain error (ValueError), 3 malformed row (refused, never dereferenced).
+ * Synchronous on return.                                                                 */
+int pcg_fisherz_batch(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N,
+                      const int32_t *tests, int32_t stride, int64_t count, double *p,
+                      int32_t *status);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,4 +1,4 @@
-"""Orientation oracle — UCSepset(priority=2) + Meek [U], literal restatement (tests only).
+"""Orientation oracle — UCSepset(priority 2/3/4) + Meek [U], literal restatement (tests only).
 
 Follows the vendored enumerations in ``lib/causallearn/graph/GraphClass.py``:
 ``find_tails``/``find_arrow_heads`` (:108-116), ``find_adj`` (:145-147),
@@ -11,7 +11,7 @@ against this.
 """
 from __future__ import annotations
 
-from itertools import permutations
+from itertools import chain, combinations, permutations
 
 import numpy as np
 
@@ -114,6 +114,46 @@ def uc_sepset_priority2(G: _G, sepset_has) -> None:
             G.add_directed(z, y)
 
 
+def powerset(L):
+    """causal-learn ``PCUtils.Helper.powerset`` [U]: all subsets, by size, combinations order."""
+    s = list(L)
+    return list(chain.from_iterable(combinations(s, r) for r in range(len(s) + 1)))
+
+
+def list_union(L1, L2):
+    """``Helper.list_union`` [U]: L1 followed by the members of L2 not in L1."""
+    return L1 + [x for x in L2 if x not in L1]
+
+
+def find_cond_sets(G: _G, i, j):
+    """``GraphClass.find_cond_sets`` (:190-196): power sets of both neighbourhoods."""
+    ni = np.where(G.graph[i, :] != 0)[0]
+    nj = np.where(G.graph[j, :] != 0)[0]
+    return list_union(powerset(ni), powerset(nj))
+
+
+def uc_sepset_priority34(G: _G, sepset_has, ci_test, priority: int) -> None:
+    """uc_sepset(priority=3 | 4) [U]: R0 = candidates in UT order; score each by the max
+    p-value of ``ci_test(x, z, S)`` over ``find_cond_sets_without_mid`` (3) or
+    ``_with_mid`` (4) (GraphClass.py:198-204); stable sort ascending (3) / descending (4);
+    then the collider step in that order."""
+    UT = [(i, j, k) for (i, j, k) in G.find_unshielded_triples() if i < k]
+    R0 = [(x, y, z) for (x, y, z) in UT if not sepset_has(x, z, y)]
+    UC = {}
+    for (x, y, z) in R0:
+        cond = [S for S in find_cond_sets(G, x, z) if (y in S) == (priority == 4)]
+        UC[(x, y, z)] = max([ci_test(x, z, S) for S in cond])
+    UC = dict(sorted(UC.items(), key=lambda item: item[1], reverse=(priority == 4)))
+    for (x, y, z) in UC.keys():
+        if (not G.is_fully_directed(y, x)) and (not G.is_fully_directed(y, z)):
+            if G.graph[x, y] != 0:
+                G.remove_edge(x, y)
+            G.add_directed(x, y)
+            if G.graph[z, y] != 0:
+                G.remove_edge(z, y)
+            G.add_directed(z, y)
+
+
 def meek(G: _G) -> None:
     UT, Tri, Kite = G.find_unshielded_triples(), G.find_triangles(), G.find_kites()
     loop = True
@@ -143,13 +183,17 @@ def meek(G: _G) -> None:
                 loop = True
 
 
-def orient(skeleton_adj: np.ndarray, sepset) -> np.ndarray:
-    """``sepset``: n x n object array of lists of tuples (reference layout)."""
+def orient(skeleton_adj: np.ndarray, sepset, priority: int = 2, ci_test=None) -> np.ndarray:
+    """``sepset``: n x n object array of lists of tuples (reference layout);
+    ``ci_test(x, z, S) -> p`` is needed for priority 3 / 4."""
     G = _G(np.where(skeleton_adj, -1, 0))
 
     def has(x, z, y):
         return not all(y not in S for S in sepset[x, z])
 
-    uc_sepset_priority2(G, has)
+    if priority == 2:
+        uc_sepset_priority2(G, has)
+    else:
+        uc_sepset_priority34(G, has, ci_test, priority)
     meek(G)
     return G.graph

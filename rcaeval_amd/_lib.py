@@ -28,6 +28,7 @@ PCG_FLAG_EXACT_ALL = 0x4
 PCG_MAX_LEVELS = 32
 PCG_RM_STATUS = 64          # status bytes after the n*n removal flags (pcgpu.h)
 PCG_MAX_DEPTH = 12
+PCG_MAX_LEVEL_DEPTH = 30
 
 I64 = ctypes.c_int64
 I32 = ctypes.c_int32
@@ -102,6 +103,9 @@ SIGNATURES = [
     ("pcg_random_walk", I32, [P, P, I64, I64, I64, I64, ctypes.c_uint64, ctypes.c_uint64,
                               ctypes.c_uint64, ctypes.c_uint64, P]),
     ("pcg_orient", I32, [I64, P, P, P, I64, ctypes.c_int, P]),
+    ("pcg_uc_candidates", I32, [I64, P, P, P, I64, P, I64, ctypes.POINTER(I64)]),
+    ("pcg_orient_triples", I32, [I64, P, P, I64, P]),
+    ("pcg_fisherz_batch", I32, [P, P, I64, I64, I64, P, I32, I64, P, P]),
 ]
 
 _lib = None

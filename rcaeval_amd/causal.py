@@ -9,7 +9,8 @@ error behaviour (``ValueError`` on a singular sub-correlation matrix or a math d
 
 Pipeline: host → HBM once (X), K1 correlation (fp64 MFMA), K2/K3 level-synchronous
 skeleton on the device, sepset unions + removal depths back to the host, orientation
-(UCSepset priority 2 + Meek) in host C++ (``pcg_orient``).
+(UCSepset priority 2 + Meek) in host C++ (``pcg_orient``); priorities 3/4 score their
+collider candidates with batched device CI tests (``rcaeval_amd.citest``).
 """
 from __future__ import annotations
 
@@ -19,6 +20,7 @@ import warnings
 import numpy as np
 
 from . import _lib
+from .citest import CITester, uc_orient
 from .engine import SkeletonOut, get_engine, orient
 
 fisherz = "fisherz"
@@ -147,8 +149,8 @@ def _check_supported(indep_test, stable, uc_rule, uc_priority, mvpc, background_
         raise NotImplementedError("stable=False (order-dependent PC) is a later-round item (SURVEY §8(f) rank 3)")
     if uc_rule != 0:
         raise NotImplementedError("uc_rule != 0 is not on the pc_pagerank / pc_randomwalk path")
-    if uc_priority not in (2,):
-        raise NotImplementedError(f"uc_priority={uc_priority}: only priority 2 (the RCAEval default) is built")
+    if uc_priority not in (-1, 2, 3, 4):
+        raise NotImplementedError(f"uc_priority={uc_priority}: priorities 2, 3 (= -1, the default) and 4 are built")
     if background_knowledge is not None:
         raise NotImplementedError("background_knowledge is a later-round item")
 
@@ -168,7 +170,8 @@ def pc(data: np.ndarray, alpha: float = 0.05, indep_test=fisherz, stable: bool =
        uc_priority: int = 2, mvpc: bool = False, correction_name: str = "MV_Crtn_Fisher_Z",
        background_knowledge=None, verbose: bool = False, show_progress: bool = True, node_names=None,
        max_depth: int = -1, device: int | None = None, full_p: bool = False, **kwargs) -> CausalGraph:
-    """causal-learn ``pc`` [U] on the GPU (fisherz, stable, uc_rule 0, uc_priority 2)."""
+    """causal-learn ``pc`` [U] on the GPU (fisherz, stable, uc_rule 0, uc_priority 2/3/4; -1 means
+    uc_sepset's default priority 3, as ``pc_alg`` [U] calls ``uc_sepset(cg_1)`` then)."""
     assert type(data) == np.ndarray  # SkeletonDiscovery.py:47
     assert 0 < alpha < 1
     _check_supported(indep_test, stable, uc_rule, uc_priority, mvpc, background_knowledge)
@@ -188,8 +191,13 @@ def pc(data: np.ndarray, alpha: float = 0.05, indep_test=fisherz, stable: bool =
         cg.PC_elapsed = time.time() - start
         return cg
     flags = _lib.PCG_FLAG_FULL_P if full_p else 0
-    out, _ = skeleton_from_data(X, alpha=alpha, max_depth=max_depth, flags=flags, device=device)
-    graph = orient(out.adj, out.sep_xy, out.sep_bits, priority=2).astype(int)
+    out, C = skeleton_from_data(X, alpha=alpha, max_depth=max_depth, flags=flags, device=device)
+    priority = 3 if uc_priority == -1 else uc_priority
+    if priority == 2:
+        graph = orient(out.adj, out.sep_xy, out.sep_bits, priority=2).astype(int)
+    else:
+        ci = CITester(C, X.shape[0], device=device)
+        graph = uc_orient(out.adj, out.sep_xy, out.sep_bits, priority, ci).astype(int)
     cg = CausalGraph(graph, names, out)
     cg.PC_elapsed = time.time() - start
     return cg

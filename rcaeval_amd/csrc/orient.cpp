@@ -116,14 +116,26 @@ std::vector<Triple> enumerate_triples(const Graph &G, const std::vector<std::pai
     return out;
 }
 
-}  // namespace
+struct Sepsets {                        // sepset[x, z] membership: both sides' rows, keyed by (min, max)
+    int64_t n, W;
+    std::unordered_map<uint64_t, std::vector<uint64_t>> rows;
+    Sepsets(int64_t n_, const int32_t *sep_xy, const uint64_t *sep_bits, int64_t count) : n(n_), W((n_ + 63) / 64) {
+        for (int64_t r = 0; r < count; ++r) {
+            const int64_t x = sep_xy[2 * r], y = sep_xy[2 * r + 1];
+            auto &row = rows[key(x, y)];
+            if (row.empty()) row.assign(W, 0);
+            for (int64_t w = 0; w < W; ++w) row[w] |= sep_bits[r * W + w];
+        }
+    }
+    uint64_t key(int64_t a, int64_t b) const { return (uint64_t)std::min(a, b) * (uint64_t)n + (uint64_t)std::max(a, b); }
+    bool contains(int64_t x, int64_t z, int64_t y) const {   // y in some S of sepset[x, z]
+        auto it = rows.find(key(x, z));
+        if (it == rows.end()) return false;
+        return ((it->second[y >> 6] >> (y & 63)) & 1ull) != 0;
+    }
+};
 
-extern "C" int pcg_orient(int64_t n, const uint8_t *adj, const int32_t *sep_xy, const uint64_t *sep_bits,
-                          int64_t count, int priority, int32_t *graph) {
-    if (n < 1 || !adj || !graph || (count > 0 && (!sep_xy || !sep_bits))) return PCG_ERR_INVALID;
-    if (priority != 2) return PCG_ERR_INVALID;  // the pc_pagerank / pc_randomwalk orientation
-    const int64_t W = (n + 63) / 64;
-    Graph G;
+void init_graph(Graph &G, int64_t n, const uint8_t *adj) {
     G.n = n;
     G.g.assign(n * n, 0);
     G.dpath.assign(n * n, 0);
@@ -131,100 +143,142 @@ extern "C" int pcg_orient(int64_t n, const uint8_t *adj, const int32_t *sep_xy, 
         for (int64_t j = 0; j < n; ++j)
             if (i != j && adj[i * n + j]) G.at(i, j) = -1;
     for (int64_t i = 0; i < n; ++i) G.adjust_dpath(i, i);  // GeneralGraph.__init__: reconstitute_dpath([])
+}
 
-    // sepset membership: union over both sides of the removal depth, keyed by (min, max)
-    std::unordered_map<uint64_t, std::vector<uint64_t>> sep;
-    for (int64_t r = 0; r < count; ++r) {
-        const int64_t x = sep_xy[2 * r], y = sep_xy[2 * r + 1];
-        const uint64_t key = (uint64_t)std::min(x, y) * (uint64_t)n + (uint64_t)std::max(x, y);
-        auto &row = sep[key];
-        if (row.empty()) row.assign(W, 0);
-        for (int64_t w = 0; w < W; ++w) row[w] |= sep_bits[r * W + w];
-    }
-    auto in_sepset = [&](int64_t x, int64_t z, int64_t y) {
-        const uint64_t key = (uint64_t)std::min(x, z) * (uint64_t)n + (uint64_t)std::max(x, z);
-        auto it = sep.find(key);
-        if (it == sep.end()) return false;
-        return ((it->second[y >> 6] >> (y & 63)) & 1ull) != 0;
-    };
+// uc_sepset's R0 list: unshielded triples (x, y, z), x < z, in find_unshielded_triples order,
+// with y in no S of sepset[x, z]. The check does not depend on orientation, so priority 2's
+// in-loop test and priority 3/4's R0 filter select the same triples.
+std::vector<Triple> uc_candidates(const Graph &G, const Sepsets &sep) {
+    const auto A = find_adj(G);
+    const auto UT = enumerate_triples(G, A, [&](int32_t i, int32_t, int32_t k) { return G.at(i, k) == 0; });
+    std::vector<Triple> R0;
+    for (const Triple &t : UT)
+        if (t.i < t.k && !sep.contains(t.i, t.k, t.j)) R0.push_back(t);
+    return R0;
+}
 
-    // ---- uc_sepset(priority = 2) on the skeleton (cg_new = deepcopy(cg))
+// the collider step shared by priorities 2, 3 and 4: x->y<-z unless y->x or y->z is fully directed
+void apply_colliders(Graph &G, const Triple *T, int64_t count) {
+    for (int64_t q = 0; q < count; ++q) {
+        const int64_t x = T[q].i, y = T[q].j, z = T[q].k;
+        if (!G.is_fully_directed(y, x) && !G.is_fully_directed(y, z)) {
+            if (G.adjacent(x, y)) G.remove_edge(x, y);
+            G.add_directed(x, y);
+            if (G.adjacent(z, y)) G.remove_edge(z, y);
+            G.add_directed(z, y);
+        }
+    }
+}
+
+// Meek.meek [U]: triple / triangle / kite lists computed once from cg_new = deepcopy(cg_2)
+void meek(Graph &G) {
+    const int64_t n = G.n;
+    const auto A = find_adj(G);
+    const auto UT = enumerate_triples(G, A, [&](int32_t i, int32_t, int32_t k) { return G.at(i, k) == 0; });
+    // (i, k) in Adj  <=>  g[k, i] in {-1, 1}
+    const auto Tri = enumerate_triples(G, A, [&](int32_t i, int32_t, int32_t k) {
+        const int8_t v = G.at(k, i);
+        return v == -1 || v == 1;
+    });
+    // kites from permutations(Tri, 2)
+    std::vector<Kite> Kites;
     {
-        const auto A = find_adj(G);
-        const auto UT = enumerate_triples(G, A, [&](int32_t i, int32_t, int32_t k) { return G.at(i, k) == 0; });
-        for (const Triple &t : UT) {
-            const int64_t x = t.i, y = t.j, z = t.k;
-            if (!(x < z)) continue;
-            if (in_sepset(x, z, y)) continue;
-            if (!G.is_fully_directed(y, x) && !G.is_fully_directed(y, z)) {
-                if (G.adjacent(x, y)) G.remove_edge(x, y);
-                G.add_directed(x, y);
-                if (G.adjacent(z, y)) G.remove_edge(z, y);
-                G.add_directed(z, y);
+        std::unordered_map<uint64_t, std::vector<int32_t>> by_ik;
+        for (size_t b = 0; b < Tri.size(); ++b)
+            by_ik[(uint64_t)Tri[b].i * (uint64_t)n + (uint64_t)Tri[b].k].push_back((int32_t)b);
+        for (size_t a = 0; a < Tri.size(); ++a) {
+            const Triple &p0 = Tri[a];
+            auto it = by_ik.find((uint64_t)p0.i * (uint64_t)n + (uint64_t)p0.k);
+            for (int32_t b : it->second) {
+                if ((size_t)b == a) continue;
+                const Triple &p1 = Tri[b];
+                if (p0.j < p1.j && G.at(p0.j, p1.j) == 0) Kites.push_back({p0.i, p0.j, p1.j, p0.k});
             }
         }
     }
-    // ---- meek (lists computed once from cg_new = deepcopy(cg_2))
-    {
-        const auto A = find_adj(G);
-        const auto UT = enumerate_triples(G, A, [&](int32_t i, int32_t, int32_t k) { return G.at(i, k) == 0; });
-        // (i, k) in Adj  <=>  g[k, i] in {-1, 1}
-        const auto Tri = enumerate_triples(G, A, [&](int32_t i, int32_t, int32_t k) {
-            const int8_t v = G.at(k, i);
-            return v == -1 || v == 1;
-        });
-        // kites from permutations(Tri, 2)
-        std::vector<Kite> Kites;
-        {
-            std::unordered_map<uint64_t, std::vector<int32_t>> by_ik;
-            for (size_t b = 0; b < Tri.size(); ++b)
-                by_ik[(uint64_t)Tri[b].i * (uint64_t)n + (uint64_t)Tri[b].k].push_back((int32_t)b);
-            for (size_t a = 0; a < Tri.size(); ++a) {
-                const Triple &p0 = Tri[a];
-                auto it = by_ik.find((uint64_t)p0.i * (uint64_t)n + (uint64_t)p0.k);
-                for (int32_t b : it->second) {
-                    if ((size_t)b == a) continue;
-                    const Triple &p1 = Tri[b];
-                    if (p0.j < p1.j && G.at(p0.j, p1.j) == 0) Kites.push_back({p0.i, p0.j, p1.j, p0.k});
-                }
+    bool loop = true;
+    while (loop) {
+        loop = false;
+        for (const Triple &t : UT) {  // R1
+            const int64_t i = t.i, j = t.j, k = t.k;
+            if (G.is_fully_directed(i, j) && G.is_undirected(j, k)) {
+                if (!G.adjacent(j, k)) continue;
+                if (G.is_ancestor_of(k, j)) continue;
+                G.remove_edge(j, k);
+                G.add_directed(j, k);
+                loop = true;
             }
         }
-        bool loop = true;
-        while (loop) {
-            loop = false;
-            for (const Triple &t : UT) {  // R1
-                const int64_t i = t.i, j = t.j, k = t.k;
-                if (G.is_fully_directed(i, j) && G.is_undirected(j, k)) {
-                    if (!G.adjacent(j, k)) continue;
-                    if (G.is_ancestor_of(k, j)) continue;
-                    G.remove_edge(j, k);
-                    G.add_directed(j, k);
-                    loop = true;
-                }
+        for (const Triple &t : Tri) {  // R2
+            const int64_t i = t.i, j = t.j, k = t.k;
+            if (G.is_fully_directed(i, j) && G.is_fully_directed(j, k) && G.is_undirected(i, k)) {
+                if (!G.adjacent(i, k)) continue;
+                if (G.is_ancestor_of(k, i)) continue;
+                G.remove_edge(i, k);
+                G.add_directed(i, k);
+                loop = true;
             }
-            for (const Triple &t : Tri) {  // R2
-                const int64_t i = t.i, j = t.j, k = t.k;
-                if (G.is_fully_directed(i, j) && G.is_fully_directed(j, k) && G.is_undirected(i, k)) {
-                    if (!G.adjacent(i, k)) continue;
-                    if (G.is_ancestor_of(k, i)) continue;
-                    G.remove_edge(i, k);
-                    G.add_directed(i, k);
-                    loop = true;
-                }
-            }
-            for (const Kite &q : Kites) {  // R3
-                const int64_t i = q.i, j = q.j, k = q.k, l = q.l;
-                if (G.is_undirected(i, j) && G.is_undirected(i, k) && G.is_fully_directed(j, l) &&
-                    G.is_fully_directed(k, l) && G.is_undirected(i, l)) {
-                    if (!G.adjacent(i, l)) continue;
-                    if (G.is_ancestor_of(l, i)) continue;
-                    G.remove_edge(i, l);
-                    G.add_directed(i, l);
-                    loop = true;
-                }
+        }
+        for (const Kite &q : Kites) {  // R3
+            const int64_t i = q.i, j = q.j, k = q.k, l = q.l;
+            if (G.is_undirected(i, j) && G.is_undirected(i, k) && G.is_fully_directed(j, l) &&
+                G.is_fully_directed(k, l) && G.is_undirected(i, l)) {
+                if (!G.adjacent(i, l)) continue;
+                if (G.is_ancestor_of(l, i)) continue;
+                G.remove_edge(i, l);
+                G.add_directed(i, l);
+                loop = true;
             }
         }
     }
+}
+
+}  // namespace
+
+extern "C" int pcg_orient(int64_t n, const uint8_t *adj, const int32_t *sep_xy, const uint64_t *sep_bits,
+                          int64_t count, int priority, int32_t *graph) {
+    if (n < 1 || !adj || !graph || (count > 0 && (!sep_xy || !sep_bits))) return PCG_ERR_INVALID;
+    if (priority != 2) return PCG_ERR_INVALID;  // 3/4 need CI tests: pcg_uc_candidates + pcg_orient_triples
+    Graph G;
+    init_graph(G, n, adj);
+    const Sepsets sep(n, sep_xy, sep_bits, count);
+    const auto R0 = uc_candidates(G, sep);      // uc_sepset(priority = 2) on cg_new = deepcopy(cg)
+    apply_colliders(G, R0.data(), (int64_t)R0.size());
+    meek(G);
+    for (int64_t i = 0; i < n * n; ++i) graph[i] = G.g[i];
+    return PCG_OK;
+}
+
+extern "C" int pcg_uc_candidates(int64_t n, const uint8_t *adj, const int32_t *sep_xy, const uint64_t *sep_bits,
+                                 int64_t count, int32_t *triples, int64_t capacity, int64_t *total) {
+    if (n < 1 || !adj || !total || (count > 0 && (!sep_xy || !sep_bits)) || (capacity > 0 && !triples))
+        return PCG_ERR_INVALID;
+    Graph G;
+    init_graph(G, n, adj);
+    const auto R0 = uc_candidates(G, Sepsets(n, sep_xy, sep_bits, count));
+    *total = (int64_t)R0.size();
+    const int64_t m = std::min<int64_t>(capacity, (int64_t)R0.size());
+    for (int64_t q = 0; q < m; ++q) {
+        triples[3 * q] = R0[q].i;
+        triples[3 * q + 1] = R0[q].j;
+        triples[3 * q + 2] = R0[q].k;
+    }
+    return PCG_OK;
+}
+
+extern "C" int pcg_orient_triples(int64_t n, const uint8_t *adj, const int32_t *triples, int64_t tcount,
+                                  int32_t *graph) {
+    if (n < 1 || !adj || !graph || tcount < 0 || (tcount > 0 && !triples)) return PCG_ERR_INVALID;
+    std::vector<Triple> T((size_t)tcount);
+    for (int64_t q = 0; q < tcount; ++q) {
+        T[q] = {triples[3 * q], triples[3 * q + 1], triples[3 * q + 2]};
+        if (T[q].i < 0 || T[q].j < 0 || T[q].k < 0 || T[q].i >= n || T[q].j >= n || T[q].k >= n)
+            return PCG_ERR_INVALID;
+    }
+    Graph G;
+    init_graph(G, n, adj);
+    apply_colliders(G, T.data(), tcount);
+    meek(G);
     for (int64_t i = 0; i < n * n; ++i) graph[i] = G.g[i];
     return PCG_OK;
 }

@@ -200,6 +200,24 @@ class Engine:
         self.sync()
         return SkeletonOut(n, rl, xy, bits, deg[:L].copy(), st.as_dict(), rec, near, device_ms)
 
+    # ------------------------------------------------------------------ batched CI tests
+    def fisherz_batch(self, C, N: int, rows: np.ndarray):
+        """Fisher-z p of canonical rows ``[a, b, d, s_0..s_{d-1}, pad]`` (int32, count x stride)
+        on the device correlation ``C``; returns (p float64, status int32) host arrays."""
+        torch = _torch()
+        Cd = self.to_device(C)
+        n = Cd.shape[0]
+        rows = np.ascontiguousarray(rows, dtype=np.int32)
+        count, stride = rows.shape
+        t = torch.from_numpy(rows).to(self.device)
+        p = torch.empty(count, dtype=torch.float64, device=self.device)
+        st = torch.empty(count, dtype=torch.int32, device=self.device)
+        check(self.h, self.lib.pcg_fisherz_batch(self.h, ctypes.c_void_p(Cd.data_ptr()), n, n, int(N),
+                                                 ctypes.c_void_p(t.data_ptr()), int(stride), int(count),
+                                                 ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(st.data_ptr())),
+              "pcg_fisherz_batch")
+        return p.cpu().numpy(), st.cpu().numpy()
+
     # ------------------------------------------------------------------ K4
     def pagerank_dense(self, A, damping: float = 0.85, n_iter: int = 10, tol: float = 1e-6) -> np.ndarray:
         torch = _torch()
@@ -235,6 +253,41 @@ def get_engine(device: int | None = None) -> Engine:
         eng = Engine(device)
         _ENGINES[device] = eng
     return eng
+
+
+def uc_candidates(adj: np.ndarray, sep_xy: np.ndarray, sep_bits: np.ndarray) -> np.ndarray:
+    """UCSepset's R0 list (host C++ ``pcg_uc_candidates``): k x 3 int32 (x, y, z)."""
+    lib = _lib.load()
+    n = adj.shape[0]
+    a = np.ascontiguousarray(adj, dtype=np.uint8)
+    xy = np.ascontiguousarray(sep_xy, dtype=np.int32)
+    bits = np.ascontiguousarray(sep_bits, dtype=np.uint64)
+    total = ctypes.c_int64()
+    args = (n, a.ctypes.data_as(ctypes.c_void_p), xy.ctypes.data_as(ctypes.c_void_p),
+            bits.ctypes.data_as(ctypes.c_void_p), len(xy))
+    rc = lib.pcg_uc_candidates(*args, None, 0, ctypes.byref(total))
+    if rc != 0:
+        raise _lib.PcgError(rc, "pcg_uc_candidates failed")
+    out = np.zeros((total.value, 3), np.int32)
+    if total.value:
+        rc = lib.pcg_uc_candidates(*args, out.ctypes.data_as(ctypes.c_void_p), total.value, ctypes.byref(total))
+        if rc != 0:
+            raise _lib.PcgError(rc, "pcg_uc_candidates failed")
+    return out
+
+
+def orient_triples(adj: np.ndarray, triples: np.ndarray) -> np.ndarray:
+    """Collider step over ``triples`` in the given order, then Meek (``pcg_orient_triples``)."""
+    lib = _lib.load()
+    n = adj.shape[0]
+    a = np.ascontiguousarray(adj, dtype=np.uint8)
+    t = np.ascontiguousarray(np.asarray(triples, dtype=np.int32).reshape(-1, 3))
+    g = np.zeros((n, n), np.int32)
+    rc = lib.pcg_orient_triples(n, a.ctypes.data_as(ctypes.c_void_p), t.ctypes.data_as(ctypes.c_void_p), len(t),
+                                g.ctypes.data_as(ctypes.c_void_p))
+    if rc != 0:
+        raise _lib.PcgError(rc, "pcg_orient_triples failed")
+    return g
 
 
 def orient(adj: np.ndarray, sep_xy: np.ndarray, sep_bits: np.ndarray, priority: int = 2) -> np.ndarray:

@@ -20,10 +20,12 @@ def pc_default(data, show_progress=False, with_bg=False, **kwargs):
 
 
 def pc_fisherz_stable(data):
-    """``pc.py:42-57`` calls pc(..., uc_priority=-1): causal-learn's default priority 3
-    orientation, which issues extra CI tests over neighbour power sets — not built yet."""
-    raise NotImplementedError("pc_fisherz_stable (uc_priority=-1 -> priority 3) is a later-round item; "
-                              "use rcaeval_amd.causal.pc(data, uc_priority=2) for the RCAEval default")
+    """``pc.py:42-57``: stable PC with ``uc_priority=-1`` (uc_sepset's default priority 3: colliders
+    ordered by the max p over neighbour power sets without the middle node, scored with
+    batched device CI tests). Returns the ``CausalGraph``."""
+    node_names = data.columns.to_list()
+    return pc(data=data.to_numpy(), alpha=0.05, indep_test=fisherz, stable=True, uc_rule=0,
+              uc_priority=-1, background_knowledge=None, show_progress=False, node_names=node_names)
 
 
 def pc_fisherz(data):

@@ -1,0 +1,129 @@
+"""GPU parity: batched Fisher-z CI tests (pcg_fisherz_batch) and the orientation rules that use
+them (UCSepset priority 3 / 4, ``pc_fisherz_stable``) against the CPU oracle.
+
+Tolerance (north_star): p within |dp| <= 1e-9 |p_ref| + 2^-51 (fisherz.p_close); graphs identical.
+"""
+import numpy as np
+import pytest
+
+from oracle import cpc, fisherz
+from oracle import orient as oor
+from rcaeval_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from rcaeval_amd.engine import get_engine
+    return get_engine(0)
+
+
+def _rows(tests, stride):
+    rows = np.full((len(tests), stride), -1, np.int32)
+    for r, (a, b, S) in enumerate(tests):
+        rows[r, :3] = (a, b, len(S))
+        rows[r, 3:3 + len(S)] = S
+    return rows
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_fisherz_batch_matches_oracle_all_depths(eng, seed):
+    rng = np.random.default_rng(seed)
+    n, N = 40, 900
+    X = synth.gaussian_sem(n, N, seed=50 + seed, w_low=0.3, w_high=0.9)
+    C = np.corrcoef(X.T)
+    tests = []
+    for d in list(range(0, 31)) * 8:
+        v = rng.choice(n, size=d + 2, replace=False)
+        a, b = sorted(int(t) for t in v[:2])
+        tests.append((a, b, sorted(int(t) for t in v[2:])))
+    p, st = eng.fisherz_batch(C, N, _rows(tests, 33))
+    assert (st == 0).all()
+    ref = [fisherz.pvalue(C, N, a, b, S) for (a, b, S) in tests]
+    assert fisherz.p_close(p, ref).all()
+
+
+def test_fisherz_batch_errors(eng):
+    n = 8
+    X = synth.gaussian_sem(n, 60, seed=4)
+    C = np.corrcoef(X.T)
+    C[5, :] = C[3, :]                         # rows/cols 3 and 5 identical (C[3,5] = 1):
+    C[:, 5] = C[:, 3]                         # exactly singular in any elimination order
+    C[5, 5] = 1.0
+    tests = [(0, 1, [3, 5]),                  # singular -> 1
+             (0, 1, [2]),                     # fine
+             (0, 9, []),                      # index out of range -> 3 (refused)
+             (2, 2, []),                      # a == b -> 3
+             (0, 1, [1])]                     # y in S -> 3
+    p, st = eng.fisherz_batch(C, 60, _rows(tests, 6))
+    assert st.tolist() == [1, 0, 3, 3, 3]
+    with pytest.raises(ValueError):
+        fisherz.pvalue(C, 60, 0, 1, [3, 5])
+    assert fisherz.p_close([p[1]], [fisherz.pvalue(C, 60, 0, 1, [2])]).all()
+    small = [(0, 1, [2, 3, 4, 6, 7])]         # N - |S| - 3 < 0 -> math domain error
+    p, st = eng.fisherz_batch(C, 7, _rows(small, 8))
+    assert st.tolist() == [2]
+    with pytest.raises(ValueError):
+        fisherz.pvalue(C, 7, 0, 1, [2, 3, 4, 6, 7])
+
+
+def test_citester_memo_and_errors():
+    from rcaeval_amd.citest import CITester
+    X = synth.gaussian_sem(10, 300, seed=8)
+    C = np.corrcoef(X.T)
+    ci = CITester(C, 300)
+    p = ci.pvalues([(3, 1, (4, 2)), (1, 3, (2, 4)), (0, 5, ())])
+    assert p[0] == p[1] and len(ci.cache) == 2
+    assert fisherz.p_close(p, [fisherz.pvalue(C, 300, 1, 3, [2, 4])] * 2 + [fisherz.pvalue(C, 300, 0, 5, [])]).all()
+    with pytest.raises(AssertionError):
+        ci(1, 2, (2,))
+    C[7, :] = C[6, :]
+    C[:, 7] = C[:, 6]
+    C[7, 7] = 1.0
+    ci2 = CITester(C, 300)
+    with pytest.raises(ValueError):
+        ci2(0, 1, (6, 7))
+
+
+def _oracle_sepset(r, n):
+    sep = np.empty((n, n), object)
+    for a in range(n):
+        for b in range(n):
+            u = set()
+            if a != b and r.removed_level[a, b] >= 1:
+                for (p_, q_) in ((a, b), (b, a)):
+                    bits = r.side_union[p_, q_]
+                    u |= {j for j in range(n) if (int(bits[j >> 6]) >> (j & 63)) & 1}
+            sep[a, b] = [tuple(u)]
+    return sep
+
+
+@pytest.mark.parametrize("priority,n,seed", [(3, 12, 0), (3, 16, 1), (4, 12, 2), (-1, 14, 3)])
+def test_pc_uc_priority_matches_oracle(priority, n, seed):
+    from rcaeval_amd.causal import pc
+    N = 800
+    X = synth.gaussian_sem(n, N, seed=700 + seed, w_low=0.4, w_high=0.9, edge_prob=0.25)
+    cg = pc(X, uc_priority=priority, show_progress=False)
+    C = np.corrcoef(X.T)
+    r = cpc.skeleton(C, N)
+    pr = 3 if priority == -1 else priority
+    want = oor.orient(r.adj, _oracle_sepset(r, n), priority=pr,
+                      ci_test=lambda i, j, S: fisherz.pvalue(C, N, i, j, S))
+    np.testing.assert_array_equal(cg.G.graph, want)
+
+
+def test_pc_fisherz_stable_entry_point():
+    """RCAEval/graph_construction/pc.py:42-57 (uc_priority=-1 -> priority 3)."""
+    import pandas as pd
+    from rcaeval_amd.graph_construction.pc import pc_fisherz_stable
+    n, N = 13, 700
+    X = synth.gaussian_sem(n, N, seed=77, w_low=0.4, w_high=0.9, edge_prob=0.25)
+    df = pd.DataFrame(X, columns=[f"m{i}" for i in range(n)])
+    cg = pc_fisherz_stable(df)
+    C = np.corrcoef(X.T)
+    r = cpc.skeleton(C, N)
+    want = oor.orient(r.adj, _oracle_sepset(r, n), priority=3,
+                      ci_test=lambda i, j, S: fisherz.pvalue(C, N, i, j, S))
+    np.testing.assert_array_equal(cg.G.graph, want)
+    assert [nd.get_name() for nd in cg.G.nodes] == list(df.columns)

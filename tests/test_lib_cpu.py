@@ -135,3 +135,55 @@ def test_digraph_matrix_matches_networkx_semantics():
         M, mine = digraph_matrix(g)
         assert mine == nodes
         np.testing.assert_array_equal(M, ref)
+
+
+class _OracleCI:
+    """CPU stand-in for CITester (tests only): oracle Fisher-z p-values, same call surface."""
+
+    def __init__(self, C, N):
+        self.C, self.N = C, N
+
+    def pvalues(self, tests):
+        from oracle import fisherz as ofz
+        return [ofz.pvalue(self.C, self.N, i, j, S) for (i, j, S) in tests]
+
+    def __call__(self, i, j, S):
+        return self.pvalues([(i, j, S)])[0]
+
+
+@pytest.mark.parametrize("priority,seed", [(3, 0), (3, 1), (3, 2), (4, 0), (4, 1)])
+def test_uc_priority34_host_matches_python_oracle(priority, seed):
+    """UCSepset priority 3/4 [U]: C++ R0 candidates + ordered collider step + Meek against the
+    literal Python restatement, both scored with the oracle's Fisher-z p-values."""
+    from oracle import orient as oor
+    from oracle import skeleton as osk
+    from rcaeval_amd import synth
+    from rcaeval_amd.citest import uc_orient
+    n = 9 + seed
+    X = synth.gaussian_sem(n, 500, seed=900 + seed, w_low=0.4, w_high=0.9, edge_prob=0.3)
+    C = np.corrcoef(X.T)
+    r = osk.skeleton_discovery(C, 500)
+    xy, bits = [], []
+    for x in range(n):
+        for y in range(n):
+            if x != y and r.removed_level[x, y] >= 1:
+                lst = r.sepset[x, y]
+                side = set(lst[-2]) if x < y else set(lst[-1])
+                if side:
+                    xy.append((x, y))
+                    bits.append([sum(1 << int(s) for s in side)])
+    ci = _OracleCI(C, 500)
+    got = uc_orient(r.adj, np.array(xy, np.int32).reshape(-1, 2), np.array(bits, np.uint64).reshape(-1, 1),
+                    priority, ci)
+    want = oor.orient(r.adj, r.sepset, priority=priority, ci_test=ci)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_uc_candidates_match_priority2_order():
+    """Priority 2 == the collider step over R0 in find_unshielded_triples order."""
+    from rcaeval_amd.engine import orient, orient_triples, uc_candidates
+    g = np.load(os.path.join(GOLD, "orient.npz"))
+    for i in range(4):
+        R0 = uc_candidates(g[f"adj{i}"], g[f"xy{i}"], g[f"bits{i}"])
+        np.testing.assert_array_equal(orient_triples(g[f"adj{i}"], R0), g[f"graph{i}"])
+        np.testing.assert_array_equal(orient(g[f"adj{i}"], g[f"xy{i}"], g[f"bits{i}"]), g[f"graph{i}"])
