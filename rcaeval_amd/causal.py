@@ -22,6 +22,7 @@ import numpy as np
 from . import _lib
 from .citest import CITester, uc_orient
 from .engine import SkeletonOut, get_engine, orient
+from .skeleton_seq import skeleton_unstable
 
 fisherz = "fisherz"
 chisq = "chisq"
@@ -145,8 +146,6 @@ def _check_supported(indep_test, stable, uc_rule, uc_priority, mvpc, background_
         raise NotImplementedError(f"indep_test={name!r}: only fisherz runs on the MI355X engine")
     if mvpc:
         raise NotImplementedError("mvpc=True (missing-value PC) is not on the engine's path")
-    if not stable:
-        raise NotImplementedError("stable=False (order-dependent PC) is a later-round item (SURVEY §8(f) rank 3)")
     if uc_rule != 0:
         raise NotImplementedError("uc_rule != 0 is not on the pc_pagerank / pc_randomwalk path")
     if uc_priority not in (-1, 2, 3, 4):
@@ -190,9 +189,21 @@ def pc(data: np.ndarray, alpha: float = 0.05, indep_test=fisherz, stable: bool =
         cg = CausalGraph(np.zeros((1, 1), int), names, None)
         cg.PC_elapsed = time.time() - start
         return cg
+    priority = 3 if uc_priority == -1 else uc_priority
+    if not stable:
+        eng = get_engine(device)
+        ci = CITester(eng.corr(X), X.shape[0], device=device)
+        sk = skeleton_unstable(ci, alpha=alpha, max_depth=max_depth)
+        xy, bits = sk.sep_rows()
+        graph = uc_orient(sk.adj.astype(np.uint8), xy, bits, priority, ci).astype(int)
+        cg = CausalGraph(graph, names, None)
+        cg.sepset = sk.sepset
+        cg.no_ci_tests = int(sum(sk.calls))
+        cg.stats = {"levels": sk.levels, "calls": sk.calls}
+        cg.PC_elapsed = time.time() - start
+        return cg
     flags = _lib.PCG_FLAG_FULL_P if full_p else 0
     out, C = skeleton_from_data(X, alpha=alpha, max_depth=max_depth, flags=flags, device=device)
-    priority = 3 if uc_priority == -1 else uc_priority
     if priority == 2:
         graph = orient(out.adj, out.sep_xy, out.sep_bits, priority=2).astype(int)
     else:

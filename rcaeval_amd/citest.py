@@ -58,7 +58,26 @@ class CITester:
         return i, j, frozenset(int(s) for s in S)
 
     def pvalues(self, tests) -> list:
-        """p of every ``(i, j, S)`` in ``tests`` (cache misses evaluated in device batches)."""
+        """p of every ``(i, j, S)`` in ``tests`` (cache misses evaluated in device batches);
+        raises like the reference on the first failing test."""
+        p, st = self.pvalues_status(tests)
+        for s_ in st:
+            self.raise_for(s_)
+        return p
+
+    @staticmethod
+    def raise_for(status: int) -> None:
+        if status == 1:
+            raise ValueError("Data correlation matrix is singular. Cannot run fisherz test. "
+                             "Please check your data.")
+        if status == 2:
+            raise ValueError("math domain error")
+        if status != 0:
+            raise AssertionError("X, Y cannot be in condition_set.")
+
+    def pvalues_status(self, tests):
+        """(p list, status list) without raising: status 0 ok, 1 singular, 2 math domain, 3
+        malformed — for callers that must only fail on tests the reference would reach."""
         keys = [self.key(i, j, S) for (i, j, S) in tests]
         self.no_ci_tests += len(keys)
         todo = list(dict.fromkeys(k for k in keys if k not in self.cache))
@@ -69,22 +88,14 @@ class CITester:
                 raise NotImplementedError(f"conditioning set of size {dmax} > {_lib.PCG_MAX_LEVEL_DEPTH}")
             rows = np.full((len(part), 3 + max(dmax, 1)), -1, np.int32)
             for r, (a, b, S) in enumerate(part):
-                if a in S or b in S:
-                    raise AssertionError("X, Y cannot be in condition_set.")
                 s = sorted(S)
                 rows[r, 0], rows[r, 1], rows[r, 2] = a, b, len(s)
                 rows[r, 3:3 + len(s)] = s
             p, st = self.eng.fisherz_batch(self.C, self.N, rows)
             for r, k in enumerate(part):
-                if st[r] == 1:
-                    raise ValueError("Data correlation matrix is singular. Cannot run fisherz test. "
-                                     "Please check your data.")
-                if st[r] == 2:
-                    raise ValueError("math domain error")
-                if st[r] != 0:
-                    raise AssertionError(f"malformed CI test {k}")
-                self.cache[k] = float(p[r])
-        return [self.cache[k] for k in keys]
+                self.cache[k] = (float(p[r]), int(st[r]))
+        got = [self.cache[k] for k in keys]
+        return [g[0] for g in got], [g[1] for g in got]
 
     def __call__(self, i, j, S) -> float:
         return self.pvalues([(i, j, S)])[0]

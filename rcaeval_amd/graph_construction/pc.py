@@ -29,8 +29,11 @@ def pc_fisherz_stable(data):
 
 
 def pc_fisherz(data):
-    """``pc.py:24-39`` (stable=False) — order-dependent PC, a later-round item."""
-    raise NotImplementedError("stable=False PC is a later-round item (SURVEY §8(f) rank 3)")
+    """``pc.py:24-39``: order-dependent PC (stable=False, ``rcaeval_amd.skeleton_seq``) with
+    ``uc_priority=-1`` (priority 3). Returns the ``CausalGraph``."""
+    node_names = data.columns.to_list()
+    return pc(data=data.to_numpy(), alpha=0.05, indep_test=fisherz, stable=False, uc_rule=0,
+              uc_priority=-1, background_knowledge=None, show_progress=False, node_names=node_names)
 
 
 __all__ = ["pc_default", "pc_fisherz_stable", "pc_fisherz", "fisherz"]
