@@ -23,7 +23,10 @@ namespace {
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 constexpr int TILE = 128;
-constexpr int KT = 8;
+#ifndef PCG_K1_KT
+#define PCG_K1_KT 8
+#endif
+constexpr int KT = PCG_K1_KT;
 constexpr int PAD = 1;  // LDS row padding (doubles) against bank conflicts
 constexpr int MEAN_ROWS = 32;   // rows per partial column sum: ~2500 blocks fill the chip
 
@@ -79,10 +82,10 @@ __global__ __launch_bounds__(256) void k_xtx(const double *X, int64_t N, int n, 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = (wave >> 1) * 64, wc = (wave & 1) * 64;
 
-    // staging: KT x 128 slab = 1024 doubles per operand, 4 per thread (one 1-KiB row segment
-    // per wave and k-row: coalesced)
+    // staging: KT x 128 slab per operand, KT/2 per thread (one 1-KiB row segment per wave and
+    // k-row: coalesced)
     const int sc = tid & 127;         // column within the tile
-    const int sr = tid >> 7;          // rows sr, sr+2, sr+4, sr+6
+    const int sr = tid >> 7;          // rows sr, sr+2, ..., sr+KT-2
     const double ma = (i0 + sc < n) ? mean[i0 + sc] : 0.0;
     const double mb = (j0 + sc < n) ? mean[j0 + sc] : 0.0;
     const bool va = i0 + sc < n, vb = j0 + sc < n;
@@ -94,10 +97,10 @@ __global__ __launch_bounds__(256) void k_xtx(const double *X, int64_t N, int n, 
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
 
-    double ra[4], rb[4];
+    double ra[KT / 2], rb[KT / 2];
     auto load = [&](int64_t t0) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < KT / 2; ++q) {
             const int64_t t = t0 + sr + 2 * q;
             const bool vt = t < kend;
             ra[q] = (vt && va) ? X[t * ldx + i0 + sc] - ma : 0.0;
@@ -106,7 +109,7 @@ __global__ __launch_bounds__(256) void k_xtx(const double *X, int64_t N, int n, 
     };
     auto store = [&](int buf) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < KT / 2; ++q) {
             As[buf][sr + 2 * q][sc] = ra[q];
             Bs[buf][sr + 2 * q][sc] = rb[q];
         }
