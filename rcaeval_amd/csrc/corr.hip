@@ -9,7 +9,8 @@
 // GEMM: 128 x 128 output tile per 256-thread block (4 waves, 64 x 64 per wave = 4 x 4
 // v_mfma_f64_16x16x4_f64 tiles, 64 accumulator doubles per lane), K (time) staged through
 // LDS in 8-row slabs, double buffered; the mean subtraction is fused into the staging load. Only upper-triangle
-// tiles are computed (c is symmetric); the epilogue mirrors them. Roofline: MFMA fp64
+// tiles are computed (c is symmetric) and only their upper triangle is written; the
+// normalisation mirrors it (k_normalize_tiles). Roofline: MFMA fp64
 // (2*N*n^2 flops); bytes 8*N*n*(n/64) staged per tile row, L2-served.
 #include <hip/hip_runtime.h>
 
@@ -28,7 +29,7 @@ constexpr int TILE = 128;
 #endif
 constexpr int KT = PCG_K1_KT;
 constexpr int PAD = 1;  // LDS row padding (doubles) against bank conflicts
-constexpr int MEAN_ROWS = 32;   // rows per partial column sum: ~2500 blocks fill the chip
+constexpr int MEAN_ROWS = 256;  // rows per partial column sum (N = 10k: 40 chunks x 8 column blocks)
 
 // partial column sums over row chunks (deterministic two-pass mean)
 __global__ void k_colsum_partial(const double *X, int64_t N, int n, int64_t ldx, double *part) {
@@ -57,7 +58,7 @@ __device__ __forceinline__ void tile_of(int t, int T, int &bi, int &bj) {
     bj = row + rem;
 }
 
-// tl == nullptr: all upper-triangle tiles, mirrored into G (single GPU). Otherwise tl lists
+// tl == nullptr: all upper-triangle tiles, upper triangle into G (single GPU). Otherwise tl lists
 // (bi, bj, packed tile row) triples of one rank's share: rows go to packed position, no mirror.
 __global__ __launch_bounds__(256) void k_xtx(const double *X, int64_t N, int n, int64_t ldx,
                                             const double *mean, int ntiles, int64_t kchunk, double *G,
@@ -153,12 +154,8 @@ __global__ __launch_bounds__(256) void k_xtx(const double *X, int64_t N, int n, 
                     const double v = acc[a][b][r];
                     if (pbi >= 0) {
                         G[((int64_t)pbi * TILE + (i - i0)) * ldg + j] = v;
-                    } else if (bi != bj) {
-                        G[(int64_t)i * ldg + j] = v;
-                        G[(int64_t)j * ldg + i] = v;
-                    } else if (i <= j) {
-                        G[(int64_t)i * ldg + j] = v;
-                        G[(int64_t)j * ldg + i] = v;
+                    } else if (bi != bj || i <= j) {
+                        G[(int64_t)i * ldg + j] = v;   // upper triangle only: k_normalize_tiles mirrors
                     }
                 }
             }
@@ -175,19 +172,49 @@ __global__ void k_stddev(const double *G, int64_t ldg, int64_t slab_stride, int 
 }
 
 // C_ij = clip(((sum_s G_s,ij) * 1/(N-1) / sd_i) / sd_j, -1, 1)   (numpy corrcoef order)
-__global__ void k_normalize(const double *G, int64_t ldg, int64_t slab_stride, int ks, double *C, int64_t ldc,
-                            int n, double scale, const double *sd) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    const int i = blockIdx.y;
-    if (j >= n) return;
-    double g = 0.0;
-    for (int s = 0; s < ks; ++s) g += G[(int64_t)s * slab_stride + (int64_t)i * ldg + j];
-    double v = (g * scale) / sd[i];
-    v = v / sd[j];
-    C[(int64_t)i * ldc + j] = v > 1.0 ? 1.0 : (v < -1.0 ? -1.0 : v);  // NaN passes through
+// G holds the upper triangle only (i <= j). One block per 64 x 64 tile pair (bi <= bj): the
+// slab sums of the upper tile go through LDS so both C[i][j] and C[j][i] are written as
+// coalesced rows; each side keeps numpy's own division order ((g * scale) / sd_row) / sd_col,
+// so C is not forced to be bitwise symmetric (numpy's is not either).
+constexpr int NT = 64;
+__global__ __launch_bounds__(256) void k_normalize_tiles(const double *G, int64_t ldg, int64_t slab_stride, int ks,
+                                                         double *C, int64_t ldc, int n, double scale,
+                                                         const double *sd) {
+    __shared__ double t[NT][NT + 1];
+    const int T = (n + NT - 1) / NT;
+    int bi = 0, bj = 0;
+    {   // upper-triangle tile index -> (bi, bj), row-major over bi
+        int r = blockIdx.x;
+        while (r >= T - bi) { r -= T - bi; ++bi; }
+        bj = bi + r;
+    }
+    const int i0 = bi * NT, j0 = bj * NT;
+    const int c = threadIdx.x & 63, r4 = threadIdx.x >> 6;
+    for (int rr = r4; rr < NT; rr += 4) {
+        const int i = i0 + rr, j = j0 + c;
+        double g = 0.0;
+        if (i < n && j < n && (bi != bj || rr <= c))
+            for (int s = 0; s < ks; ++s) g += G[(int64_t)s * slab_stride + (int64_t)i * ldg + j];
+        t[rr][c] = g;
+    }
+    __syncthreads();
+    for (int rr = r4; rr < NT; rr += 4) {
+        const int i = i0 + rr, j = j0 + c;          // upper side: row i, column j
+        if (i < n && j < n && (bi != bj || rr <= c)) {
+            double v = (t[rr][c] * scale) / sd[i];
+            v = v / sd[j];
+            C[(int64_t)i * ldc + j] = v > 1.0 ? 1.0 : (v < -1.0 ? -1.0 : v);  // NaN passes through
+        }
+        const int p = j0 + rr, q = i0 + c;          // lower side: row p (tile bj), column q (tile bi)
+        if (p < n && q < n && (bi != bj || c < rr)) {
+            double v = (t[c][rr] * scale) / sd[p];
+            v = v / sd[q];
+            C[(int64_t)p * ldc + q] = v > 1.0 ? 1.0 : (v < -1.0 ? -1.0 : v);
+        }
+    }
 }
 
-// packed[r][j] = sum_s G_s[r][j] in slab order (the order k_stddev / k_normalize use)
+// packed[r][j] = sum_s G_s[r][j] in slab order (the order k_stddev / k_normalize_tiles use)
 __global__ void k_slab_sum(const double *G, int64_t slab_stride, int ks, int64_t count, double *out) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= count) return;
@@ -365,8 +392,9 @@ extern "C" int pcg_corr(pcg_handle *h, const double *X, int64_t N, int64_t n, in
     hipLaunchKernelGGL(k_xtx, dim3(ntiles * ks), dim3(256), 0, h->stream, X, N, nn, ldx, mean, ntiles, kchunk, G,
                        ldg, stride, (const int32_t *)nullptr);
     hipLaunchKernelGGL(k_stddev, dim3((nn + 255) / 256), dim3(256), 0, h->stream, G, ldg, stride, ks, nn, scale, sd);
-    hipLaunchKernelGGL(k_normalize, dim3((nn + 255) / 256, nn), dim3(256), 0, h->stream, G, ldg, stride, ks, C, ldc,
-                       nn, scale, sd);
+    const int T64 = (nn + NT - 1) / NT;
+    hipLaunchKernelGGL(k_normalize_tiles, dim3(T64 * (T64 + 1) / 2), dim3(256), 0, h->stream, G, ldg, stride, ks, C,
+                       ldc, nn, scale, sd);
     PCG_HIP(h, hipGetLastError());
     PCG_HIP(h, hipStreamSynchronize(h->stream));
     return PCG_OK;
