@@ -250,3 +250,40 @@ def test_rq2_run_matches_oracle_per_case(tmp_path):
         got = rq2.load_json(os.path.join(out_dir, "results", c["result_name"]))["0"]
         assert got == ranks
     assert set(res["summary"]) >= {"Avg@5-CPU", "Avg@5-DELAY"}
+
+
+def _sem_frame(X, prefix):
+    import pandas as pd
+    df = pd.DataFrame(X, columns=[f"{prefix}{i}_lat" for i in range(X.shape[1])])
+    df.insert(0, "time", np.arange(X.shape[0]))
+    return df
+
+
+@pytest.mark.parametrize("kind,seed", [("circa50", 5), ("circa50", 15), ("rcd50", 6)])
+def test_pc_randomwalk_config3_50_node_sem(kind, seed):
+    """BASELINE config 3: circa50 / rcd50-shaped 50-node SEMs (continuous, or discrete 0-5
+    levels for RCD) through pc_randomwalk — rank lists and endpoint graph identical to the
+    oracle pipeline."""
+    from rcaeval_amd.e2e import pc_randomwalk
+    if kind == "circa50":
+        X = synth.gaussian_sem(50, 3000, seed=seed, w_low=0.3, w_high=0.9)
+    else:
+        X = synth.discrete_sem(50, 3000, seed=seed).astype(float)
+    df = _sem_frame(X, "s")
+    out = pc_randomwalk(df, 0, dataset=kind)
+    ranks, g = _oracle_pipeline(df, kind, "randomwalk")
+    assert out["ranks"] == ranks
+    np.testing.assert_array_equal(out["adj"], g)
+
+
+def test_pc_pagerank_config4_train_ticket_212():
+    """BASELINE config 4: train-ticket-shaped frame (212 metrics x 600 rows, constant columns
+    dropped by preprocess) through pc_pagerank — identical rank list and endpoint graph."""
+    from rcaeval_amd.e2e import pc_pagerank
+    df = synth.telemetry_frame(212, 600, n_constant=4, seed=11)
+    out = pc_pagerank(df, 0, dataset="train-ticket")
+    ranks, g = _oracle_pipeline(df, "train-ticket", "pagerank")
+    assert out["ranks"] == ranks
+    from rcaeval_amd.io.time_series import preprocess
+    assert out["node_names"] == preprocess(df, dataset="train-ticket").columns.to_list()
+    assert len(out["node_names"]) == g.shape[0]
