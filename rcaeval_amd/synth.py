@@ -138,3 +138,31 @@ def write_rq2_dataset(root: str, services=None, faults=("cpu", "mem", "delay"), 
                 paths.append(os.path.join(d, "data.csv"))
                 k += 1
     return paths
+
+
+def write_rq1_dataset(root: str, num_node: int = 10, graphs: int = 2, cases: int = 2, rows: int = 600,
+                      seed: int = 0, edge_prob: float | None = None) -> list:
+    """A CIRCA-shaped RQ1 tree (``rq1.py:122,201-204,158-160``):
+    ``<root>/<num_node>/<graph_idx>/cases/<case_idx>/data.csv`` (no header row, one column per
+    node) and ``<root>/<num_node>/<graph_idx>/graph.json`` (``MemoryGraph.dump`` layout, nodes
+    ``Node("SIM", str(i))``, edges cause → effect as node indices)."""
+    import json
+    import os
+
+    paths = []
+    for g in range(graphs):
+        gdir = os.path.join(root, str(num_node), str(g))
+        os.makedirs(gdir, exist_ok=True)
+        W, _, _ = sem_dag(num_node, edge_prob, 0.3, 0.9, seed=seed + 1000 * g)
+        edges = [[int(i), int(j)] for i, j in zip(*np.nonzero(W))]
+        with open(os.path.join(gdir, "graph.json"), "w") as f:
+            json.dump({"nodes": [{"entity": "SIM", "metric": str(i)} for i in range(num_node)],
+                       "edges": edges}, f, indent=2, sort_keys=True)
+        for c in range(cases):
+            cdir = os.path.join(gdir, "cases", str(c))
+            os.makedirs(cdir, exist_ok=True)
+            X = gaussian_sem(num_node, rows, edge_prob, 0.3, 0.9, seed=seed + 1000 * g)
+            X += np.random.default_rng(seed + 1000 * g + c + 1).standard_normal(X.shape) * 0.1 * c
+            np.savetxt(os.path.join(cdir, "data.csv"), X, delimiter=",", fmt="%.17g")
+            paths.append(os.path.join(cdir, "data.csv"))
+    return paths

@@ -15,6 +15,9 @@ Fixtures (data only — inputs and expected outputs):
                     (oracle/orient.py) on small SEMs — pins pcg_orient across rounds.
   pagerank.npz      scikit-network-0.31.0-restated PageRank (oracle/pagerank.py, scipy CSR + numpy
                     sums) on random 0/1 graphs — pins the GPU kernel bitwise.
+  metrics.json      outputs of the REFERENCE ``finalize_directed_adj``, ``MemoryGraph.from_adj`` and
+                    ``RCAEval.benchmark.metrics`` F1 / F1_Skeleton / SHD (RQ1 scoring) on seeded
+                    random endpoint matrices and DAGs (Node-named and plain-int-named nodes).
   evaluator.json    AC@k / Avg@k (service- and metric-level) of the REFERENCE
                     ``RCAEval.benchmark.evaluation.Evaluator`` with ``RCAEval.classes.graph.Node``
                     on seeded random rank lists (the RQ2 scorer, rq2.py:339-419).
@@ -101,6 +104,66 @@ def make_evaluator():
     with open(os.path.join(HERE, "evaluator.json"), "w") as f:
         json.dump(out, f)
     print("evaluator.json", len(cases))
+
+
+def metrics_cases():
+    rng = np.random.default_rng(11)
+    pairs = [(0, 0), (-1, 1), (1, -1), (0, 1), (1, 0), (-1, -1), (1, 1), (2, 1), (1, 2), (2, 2)]
+    cases = []
+    for c in range(24):
+        n = int(rng.integers(2, 30))
+        adj = np.zeros((n, n), int)
+        for i in range(n):
+            for j in range(i + 1, n):
+                a, b = pairs[int(rng.integers(0, len(pairs)))] if rng.random() < 0.35 else (0, 0)
+                adj[i, j], adj[j, i] = a, b
+        if c % 7 == 3:                       # a diagonal entry (the reference maps it too)
+            adj[0, 0] = [-1, 1, 2][c % 3]
+        true_edges = [[int(i), int(j)] for i in range(n) for j in range(n)
+                      if i != j and rng.random() < 2.0 / n]
+        cases.append({"adj": adj.tolist(), "true_edges": true_edges, "named": bool(c % 2 == 0),
+                      "extra_true_nodes": int(rng.integers(0, 3)) if c % 5 == 1 else 0})
+    bad = np.zeros((4, 4), int)
+    bad[1, 2], bad[2, 1] = 3, 0
+    bad2 = np.zeros((4, 4), int)
+    bad2[2, 3], bad2[3, 2] = 2, -1
+    return cases, [bad.tolist(), bad2.tolist()]
+
+
+def make_metrics():
+    sys.path.insert(0, REF)
+    import networkx as nx
+    from RCAEval.benchmark.metrics import F1, SHD, F1_Skeleton  # reference, imported (not copied)
+    from RCAEval.classes.graph import MemoryGraph, Node
+    from RCAEval.graph_heads import finalize_directed_adj
+    cases, bad = metrics_cases()
+    out = []
+    for c in cases:
+        adj = np.array(c["adj"])
+        n = adj.shape[0]
+        nt = n + c["extra_true_nodes"]
+        nodes = [Node(f"svc{i % 5}", f"m{i}") for i in range(nt)] if c["named"] else list(range(nt))
+        est = MemoryGraph.from_adj(adj, nodes[:n])
+        tg = nx.DiGraph()
+        tg.add_nodes_from(nodes)
+        tg.add_edges_from((nodes[i], nodes[j]) for i, j in c["true_edges"])
+        true = MemoryGraph(tg)
+        pos = {v: k for k, v in enumerate(nodes)}
+        out.append({**c,
+                    "final": finalize_directed_adj(adj).tolist(),
+                    "est_edges": [[pos[u], pos[v]] for u, v in est._graph.edges],
+                    "F1": F1(true, est), "F1_Skeleton": F1_Skeleton(true, est),
+                    "SHD": SHD(true, est), "SHD_rev": SHD(est, true)})
+    errors = []
+    for b in bad:
+        try:
+            finalize_directed_adj(np.array(b))
+            errors.append(None)
+        except ValueError as e:
+            errors.append(str(e))
+    with open(os.path.join(HERE, "metrics.json"), "w") as f:
+        json.dump({"cases": out, "bad": bad, "bad_errors": errors}, f)
+    print("metrics.json", len(out))
 
 
 def telemetry_frames():
@@ -202,6 +265,10 @@ def make_pagerank():
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1:                   # regenerate only the named fixtures
+        for name in sys.argv[1:]:
+            globals()[f"make_{name}"]()
+        sys.exit(0)
     make_fisherz()
     make_orient()
     make_pagerank()
@@ -209,5 +276,6 @@ if __name__ == "__main__":
         make_random_walk()
         make_preprocess()
         make_evaluator()
+        make_metrics()
     else:
         print("reference not present: random_walk / preprocess goldens not regenerated")
