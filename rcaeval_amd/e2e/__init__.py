@@ -28,7 +28,8 @@ def rca(func):
     return wrapper
 
 
+from .cloudranger import cloudranger  # noqa: E402
 from .pc_pagerank import pc_pagerank  # noqa: E402
 from .pc_randomwalk import pc_randomwalk  # noqa: E402
 
-__all__ = ["rca", "pc_pagerank", "pc_randomwalk"]
+__all__ = ["rca", "cloudranger", "pc_pagerank", "pc_randomwalk"]

@@ -43,8 +43,8 @@ DATASET_MAP = {                                   # rq2.py:135-144
 
 def methods():
     """Methods this engine serves (``rq2.py:36-59`` resolves them by name)."""
-    from .e2e import pc_pagerank, pc_randomwalk
-    return {"pc_pagerank": pc_pagerank, "pc_randomwalk": pc_randomwalk}
+    from .e2e import cloudranger, pc_pagerank, pc_randomwalk
+    return {"pc_pagerank": pc_pagerank, "pc_randomwalk": pc_randomwalk, "cloudranger": cloudranger}
 
 
 def dump_json(filename: str, data) -> None:

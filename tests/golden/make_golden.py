@@ -18,6 +18,11 @@ Fixtures (data only — inputs and expected outputs):
   metrics.json      outputs of the REFERENCE ``finalize_directed_adj``, ``MemoryGraph.from_adj`` and
                     ``RCAEval.benchmark.metrics`` F1 / F1_Skeleton / SHD (RQ1 scoring) on seeded
                     random endpoint matrices and DAGs (Node-named and plain-int-named nodes).
+  cloudranger.npz   outputs of the REFERENCE ``relaToRank`` (+ ``guiyi``, ``secondorder_randomwalk``)
+                    from RCAEval/e2e/cloudranger.py — the three functions are read from the
+                    reference file and executed at generation time (the module itself needs
+                    pingouin / causal-learn / tigramite, absent here) — on seeded random
+                    dependency graphs and correlation rows, under ``np.random.seed``.
   evaluator.json    AC@k / Avg@k (service- and metric-level) of the REFERENCE
                     ``RCAEval.benchmark.evaluation.Evaluator`` with ``RCAEval.classes.graph.Node``
                     on seeded random rank lists (the RQ2 scorer, rq2.py:339-419).
@@ -166,6 +171,52 @@ def make_metrics():
     print("metrics.json", len(out))
 
 
+def _reference_functions(path, names):
+    """Execute only the named top-level functions of a reference file (not kept anywhere)."""
+    import ast
+    src = open(path).read()
+    tree = ast.parse(src)
+    keep = [node for node in tree.body if isinstance(node, ast.FunctionDef) and node.name in names]
+    ns = {"np": np}
+    exec(compile(ast.Module(body=keep, type_ignores=[]), path, "exec"), ns)
+    return ns
+
+
+def cloudranger_cases():
+    rng = np.random.default_rng(13)
+    cases = []
+    for c in range(14):
+        n = int(rng.integers(2, 26))
+        A = (rng.random((n, n)) < rng.uniform(0.05, 0.4)).astype(int)
+        np.fill_diagonal(A, 0)
+        if c == 1:
+            A[:] = 0                                   # no edges: walk breaks / self loops only
+        X = rng.standard_normal((200, n)) @ rng.standard_normal((n, n))
+        rela = np.corrcoef(X.T)
+        frontend = 0 if c % 4 == 0 else int(rng.integers(0, n))
+        beta, rho = (0.3, 0.2) if c % 2 == 0 else (0.1, 0.3)
+        cases.append((A, rela, frontend, beta, rho, 1000 + c))
+    return cases
+
+
+def make_cloudranger():
+    ref = _reference_functions(os.path.join(REF, "RCAEval", "e2e", "cloudranger.py"),
+                               {"guiyi", "relaToRank", "secondorder_randomwalk"})
+    arrays = {}
+    for k, (A, rela, frontend, beta, rho, seed) in enumerate(cloudranger_cases()):
+        np.random.seed(seed)
+        rank, P, M = ref["relaToRank"](rela.tolist(), A, 10, frontend, beta=beta, rho=rho)
+        arrays[f"A{k}"] = A
+        arrays[f"rela{k}"] = rela
+        arrays[f"params{k}"] = np.array([frontend, beta, rho, seed])
+        arrays[f"P{k}"] = np.array(P, dtype=float)
+        arrays[f"M{k}"] = M
+        arrays[f"rank{k}"] = np.array(rank, dtype=float)
+        arrays[f"next{k}"] = np.array([np.random.random_sample()])   # stream position after the walk
+    np.savez_compressed(os.path.join(HERE, "cloudranger.npz"), **arrays)
+    print("cloudranger.npz", len(arrays) // 7)
+
+
 def telemetry_frames():
     from rcaeval_amd import synth
     frames = []
@@ -277,5 +328,6 @@ if __name__ == "__main__":
         make_preprocess()
         make_evaluator()
         make_metrics()
+        make_cloudranger()
     else:
         print("reference not present: random_walk / preprocess goldens not regenerated")

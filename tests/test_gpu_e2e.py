@@ -51,7 +51,7 @@ def test_random_walk_serial_path_matches_numpy():
     np.testing.assert_array_equal(got, orw.walk_counts(P, 3, 500))
 
 
-def _oracle_pipeline(df, dataset, head):
+def _oracle_pipeline(df, dataset, head, alpha=0.05, sli=None):
     """Reference-equivalent CPU pipeline built only from oracle restatements + reference glue:
     C-restated skeleton (pc_oracle.c), Python-restated orientation, scipy PageRank."""
     from oracle import cpc
@@ -66,7 +66,7 @@ def _oracle_pipeline(df, dataset, head):
     X = data.to_numpy().astype(float)
     with np.errstate(invalid="ignore", divide="ignore"):
         C = np.corrcoef(X.T)
-    r = cpc.skeleton(C, X.shape[0])
+    r = cpc.skeleton(C, X.shape[0], alpha=alpha)
     n = C.shape[0]
     sep = np.empty((n, n), object)
     for a in range(n):
@@ -78,6 +78,12 @@ def _oracle_pipeline(df, dataset, head):
                     u |= {j for j in range(n) if (int(bits[j >> 6]) >> (j & 63)) & 1}
             sep[a, b] = [tuple(u)]
     g = oor.orient(r.adj, sep)
+    if head == "cloudranger":
+        from rcaeval_amd.graph_heads.finalize import finalize_directed_adj
+        from rcaeval_amd.graph_heads.relato_rank import relaToRank
+        rank, _, _ = relaToRank(np.corrcoef(data.to_numpy().T), finalize_directed_adj(g).T, 10,
+                                names.index(sli), beta=0.3, rho=0.2)
+        return [names[k - 1] for k, _ in rank], g
     if head == "pagerank":
         M, _ = digraph_matrix(g)
         scores = opr.pagerank(M.T)
@@ -287,3 +293,18 @@ def test_pc_pagerank_config4_train_ticket_212():
     from rcaeval_amd.io.time_series import preprocess
     assert out["node_names"] == preprocess(df, dataset="train-ticket").columns.to_list()
     assert len(out["node_names"]) == g.shape[0]
+
+
+@pytest.mark.parametrize("m,rows,seed", [(12, 200, 5), (38, 600, 6), (49, 600, 7)])
+def test_cloudranger_matches_oracle_pipeline(m, rows, seed):
+    """cloudranger.py:154-190: PC at alpha 0.1 on the engine + the second-order walk, under the
+    same np.random seed as the oracle pipeline (C-restated skeleton, Python orientation)."""
+    from rcaeval_amd.e2e import cloudranger
+    df = synth.telemetry_frame(m, rows, n_constant=2, seed=seed)
+    sli = [c for c in df.columns if c != "time"][seed % 5]
+    np.random.seed(seed)
+    out = cloudranger(df, 0, dataset="online-boutique", sli=sli)
+    np.random.seed(seed)
+    ranks, g = _oracle_pipeline(df, "online-boutique", "cloudranger", alpha=0.1, sli=sli)
+    np.testing.assert_array_equal(out["adj"], g)
+    assert out["ranks"] == ranks

@@ -96,3 +96,20 @@ def test_rq1_evaluate_layout_and_scores(tmp_path):
     assert out["summary"]["SHD"] == int(np.floor(np.mean(want_shd)))
     with pytest.raises(NotImplementedError):
         rq1.process(paths[0], res, method="fges")
+
+
+CR = np.load(os.path.join(os.path.dirname(__file__), "golden", "cloudranger.npz"))
+
+
+@pytest.mark.parametrize("k", range(14))
+def test_relato_rank_matches_reference_golden(k):
+    """CloudRanger head (cloudranger.py:69-148): P, M bitwise, the ranked visit counts and the
+    global RandomState position after the walk equal the reference's under the same seed."""
+    from rcaeval_amd.graph_heads.relato_rank import relaToRank
+    frontend, beta, rho, seed = CR[f"params{k}"]
+    np.random.seed(int(seed))
+    rank, P, M = relaToRank(CR[f"rela{k}"].tolist(), CR[f"A{k}"], 10, int(frontend), beta=beta, rho=rho)
+    np.testing.assert_array_equal(P, CR[f"P{k}"])
+    np.testing.assert_array_equal(M, CR[f"M{k}"])
+    np.testing.assert_array_equal(np.array(rank, dtype=float), CR[f"rank{k}"])
+    assert np.random.random_sample() == CR[f"next{k}"][0]
