@@ -301,7 +301,8 @@ def test_cloudranger_matches_oracle_pipeline(m, rows, seed):
     same np.random seed as the oracle pipeline (C-restated skeleton, Python orientation)."""
     from rcaeval_amd.e2e import cloudranger
     df = synth.telemetry_frame(m, rows, n_constant=2, seed=seed)
-    sli = [c for c in df.columns if c != "time"][seed % 5]
+    from rcaeval_amd.io.time_series import preprocess
+    sli = preprocess(df, dataset="online-boutique").columns[seed % 5]
     np.random.seed(seed)
     out = cloudranger(df, 0, dataset="online-boutique", sli=sli)
     np.random.seed(seed)
