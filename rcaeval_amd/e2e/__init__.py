@@ -28,8 +28,9 @@ def rca(func):
     return wrapper
 
 
+from .circa import circa  # noqa: E402
 from .cloudranger import cloudranger  # noqa: E402
 from .pc_pagerank import pc_pagerank  # noqa: E402
 from .pc_randomwalk import pc_randomwalk  # noqa: E402
 
-__all__ = ["rca", "cloudranger", "pc_pagerank", "pc_randomwalk"]
+__all__ = ["rca", "circa", "cloudranger", "pc_pagerank", "pc_randomwalk"]

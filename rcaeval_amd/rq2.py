@@ -43,8 +43,9 @@ DATASET_MAP = {                                   # rq2.py:135-144
 
 def methods():
     """Methods this engine serves (``rq2.py:36-59`` resolves them by name)."""
-    from .e2e import cloudranger, pc_pagerank, pc_randomwalk
-    return {"pc_pagerank": pc_pagerank, "pc_randomwalk": pc_randomwalk, "cloudranger": cloudranger}
+    from .e2e import circa, cloudranger, pc_pagerank, pc_randomwalk
+    return {"pc_pagerank": pc_pagerank, "pc_randomwalk": pc_randomwalk, "cloudranger": cloudranger,
+            "circa": circa}
 
 
 def dump_json(filename: str, data) -> None:

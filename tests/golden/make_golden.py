@@ -23,6 +23,9 @@ Fixtures (data only — inputs and expected outputs):
                     reference file and executed at generation time (the module itself needs
                     pingouin / causal-learn / tigramite, absent here) — on seeded random
                     dependency graphs and correlation rows, under ``np.random.seed``.
+  rht.json          outputs of the REFERENCE ``RCAEval.graph_heads.rht.rht`` (CIRCA's head, imported)
+                    on synthetic telemetry frames and random endpoint matrices, under
+                    ``np.random.seed`` (scores + the RandomState position afterwards).
   evaluator.json    AC@k / Avg@k (service- and metric-level) of the REFERENCE
                     ``RCAEval.benchmark.evaluation.Evaluator`` with ``RCAEval.classes.graph.Node``
                     on seeded random rank lists (the RQ2 scorer, rq2.py:339-419).
@@ -217,6 +220,44 @@ def make_cloudranger():
     print("cloudranger.npz", len(arrays) // 7)
 
 
+def rht_cases():
+    from rcaeval_amd import synth
+    rng = np.random.default_rng(17)
+    pairs = [(0, 0), (-1, -1), (-1, 1), (1, -1)]
+    cases = []
+    for c in range(8):
+        m = int(rng.integers(4, 20))
+        df = synth.telemetry_frame(m, 600, n_constant=1, seed=200 + c)
+        t = df.pop("time")
+        if c % 3 == 1:                                   # irregular sampling: drop rows, jitter
+            keep = np.sort(rng.choice(600, 450, replace=False))
+            df, t = df.iloc[keep].reset_index(drop=True), t.iloc[keep].reset_index(drop=True) + 0.25
+        if c % 4 == 2:
+            df.iloc[rng.integers(0, len(df), 20), int(rng.integers(0, m))] = np.nan
+        df["time"] = t                                   # circa puts time back last
+        adj = np.zeros((m, m), int)
+        for i in range(m):
+            for j in range(i + 1, m):
+                if rng.random() < 0.3:
+                    adj[i, j], adj[j, i] = pairs[int(rng.integers(1, 4))]
+        inject = int(df["time"].iloc[0]) + int(rng.integers(150, 250))
+        cases.append((df, adj, inject, 300 + c))
+    return cases
+
+
+def make_rht():
+    sys.path.insert(0, REF)
+    from RCAEval.graph_heads.rht import rht  # reference, imported (not copied)
+    out = []
+    for df, adj, inject, seed in rht_cases():
+        np.random.seed(seed)
+        r = rht(adj, inject, df.copy())
+        out.append({"ranks": [[a, float(b)] for a, b in r], "next": float(np.random.random_sample())})
+    with open(os.path.join(HERE, "rht.json"), "w") as f:
+        json.dump(out, f)
+    print("rht.json", len(out))
+
+
 def telemetry_frames():
     from rcaeval_amd import synth
     frames = []
@@ -329,5 +370,6 @@ if __name__ == "__main__":
         make_evaluator()
         make_metrics()
         make_cloudranger()
+        make_rht()
     else:
         print("reference not present: random_walk / preprocess goldens not regenerated")

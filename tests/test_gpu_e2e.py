@@ -309,3 +309,24 @@ def test_cloudranger_matches_oracle_pipeline(m, rows, seed):
     ranks, g = _oracle_pipeline(df, "online-boutique", "cloudranger", alpha=0.1, sli=sli)
     np.testing.assert_array_equal(out["adj"], g)
     assert out["ranks"] == ranks
+
+
+@pytest.mark.parametrize("m,rows,seed", [(12, 600, 8), (38, 600, 9)])
+def test_circa_matches_oracle_pipeline(m, rows, seed):
+    """circa.py:15-41: stable PC on the engine + the RHT head; the oracle pipeline's endpoint
+    matrix through the same head gives the same ranks."""
+    from rcaeval_amd.e2e import circa
+    from rcaeval_amd.graph_heads.rht import rht
+    from rcaeval_amd.io.time_series import preprocess
+    df = synth.telemetry_frame(m, rows, n_constant=2, seed=seed)
+    inject = int(df["time"].iloc[0]) + 200
+    np.random.seed(seed)
+    out = circa(df.copy(), inject, dataset="online-boutique")
+    _, g = _oracle_pipeline(df.copy(), "online-boutique", "pagerank")
+    np.testing.assert_array_equal(out["adj"], g)
+    data = preprocess(df.copy(), dataset="online-boutique")
+    data["time"] = df["time"]
+    np.random.seed(seed)
+    want = [n for n, _ in sorted(rht(g, inject, data), key=lambda x: x[1], reverse=True)]
+    assert out["ranks"] == want
+    assert len(out["ranks"]) > 0

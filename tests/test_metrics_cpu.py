@@ -113,3 +113,29 @@ def test_relato_rank_matches_reference_golden(k):
     np.testing.assert_array_equal(M, CR[f"M{k}"])
     np.testing.assert_array_equal(np.array(rank, dtype=float), CR[f"rank{k}"])
     assert np.random.random_sample() == CR[f"next{k}"][0]
+
+
+RHT = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "rht.json")))
+
+
+@pytest.mark.parametrize("k", range(len(RHT)))
+def test_rht_matches_reference_golden(k):
+    """CIRCA's RHT head (rht.py:331-403 + classes/data.py): node set, scores (1e-9 relative:
+    the reference's parent order follows string hashing) and the RandomState position."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden import rht_cases
+    from rcaeval_amd.graph_heads.rht import rht
+    df, adj, inject, seed = rht_cases()[k]
+    np.random.seed(seed)
+    got = rht(adj, inject, df.copy())
+    want = RHT[k]
+    assert np.random.random_sample() == want["next"]
+    assert sorted(n for n, _ in got) == sorted(n for n, _ in want["ranks"])
+    g, w = dict(got), dict(want["ranks"])
+    for name in w:
+        assert g[name] == pytest.approx(w[name], rel=1e-9, abs=1e-12), name
+    order_w = [n for n, _ in want["ranks"]]
+    vals = np.array([w[n] for n in order_w])
+    if np.all(np.diff(vals) < -1e-9):                    # no near-ties: identical rank list
+        assert [n for n, _ in got] == order_w
