@@ -52,6 +52,30 @@ def pmc_traffic(kernel_prefix: str):  # exact rocprof kernel name (template args
     return None, None
 
 
+def valu_issue_floor(kernel: str, tests: int):
+    """The resource that actually binds the CI-test kernels (their operands live in LDS, so the
+    §8(d) HBM-byte model overstates traffic ~10^3x): VALU issue. From the committed PMC pass
+    (same kernel, same workload): wave-instructions per launch, fp64 ones at 4 SIMD-cycles per
+    wave64 (78.6 TF/s fp64 = 16 lanes/cycle/SIMD) and the rest at 2 (32 lanes/cycle,
+    MI355X_MICROARCH.md), spread over 1024 SIMDs at 2.4 GHz. None if the pass is absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
+    if not files:
+        return None
+    data = json.load(open(files[-1]))
+    ctr = data.get(kernel, {})
+    need = ("SQ_INSTS_VALU", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64")
+    if not all(k in ctr for k in need):
+        return None
+    valu = ctr["SQ_INSTS_VALU"]["per_dispatch_mean"]
+    f64 = sum(ctr[k]["per_dispatch_mean"] for k in need[1:])
+    cycles = 4.0 * f64 + 2.0 * (valu - f64)
+    floor_ms = cycles / (1024 * 2.4e9) * 1e3
+    return {"resource": "VALU issue", "valu_instr_per_launch": valu, "fp64_instr_per_launch": f64,
+            "valu_instr_per_64_tests": valu / (tests / 64.0) if tests else None,
+            "issue_floor_ms": floor_ms, "source": os.path.basename(files[-1])}
+
+
 def dominant_kernel(d: int, full_p: bool) -> str:
     """Name (as rocprofv3 prints it, template args kept) of the CI-test kernel that runs
     depth ``d`` for nodes of degree <= 64 — the host dispatch in skeleton.hip
@@ -286,6 +310,9 @@ def main():
     ach_tf = alg_flops / (k_ms / 1000.0) / 1e12 if k_ms > 0 else 0.0
     kname = dominant_kernel(dmax, args.full_p)
     traffic, traffic_src = pmc_traffic(kname)
+    binding = valu_issue_floor(kname, int(st["tests"][dmax]))
+    if binding is not None:
+        binding["frac"] = binding["issue_floor_ms"] / k_ms if k_ms > 0 else None
 
     if rank == 0:
         line = {
@@ -311,7 +338,8 @@ def main():
                          "traffic_source": traffic_src,
                          "kernel": kname, "kernel_ms": k_ms,
                          "algorithmic_bytes_per_test": bytes_per_test(dmax),
-                         "fp64_tflops_algorithmic": ach_tf, "fp64_peak_tflops": FP64_PEAK_TFLOPS},
+                         "fp64_tflops_algorithmic": ach_tf, "fp64_peak_tflops": FP64_PEAK_TFLOPS,
+                         "binding": binding},
         }
         if not args.no_cpu_baseline and world == 1:
             cb = cpu_baseline(X, args.alpha, args.cpu_depth)

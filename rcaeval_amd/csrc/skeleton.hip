@@ -890,8 +890,11 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
 //   v_c = (M[c][y] - l_c.v_T) / lambda_c,  c_yy = byy - v_c^2,  c_xy = bxy - u_c v_c
 // — the same partial correlation, ~9 fp64 ops per test instead of ~26. Tasks (g, T): group
 // g covers c in [g*TG, g*TG+TG), T ranges over (d-1)-subsets of [g*TG+1, D) in colex order.
+#ifndef PCG_TG_MINB
+#define PCG_TG_MINB 4            // blocks per CU the depth-3/4 T-group kernel is register-sized for
+#endif
 template <int DM>
-__global__ __launch_bounds__(256, 4) void k_level_lds_t(LevelArgs a) {
+__global__ __launch_bounds__(256, (DM >= 3 ? PCG_TG_MINB : 4)) void k_level_lds_t(LevelArgs a) {
     constexpr int DT = DM - 1;
     constexpr int TG = PCG_TGROUP;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
