@@ -236,11 +236,14 @@ __global__ __launch_bounds__(256) void k_apply(const uint8_t *rm, uint64_t *adj,
 __global__ __launch_bounds__(256) void k_export(const int32_t *off, const int32_t *nbr, const uint8_t *rm,
                                                 const uint64_t *ug, int n, int W, int64_t sumdeg, int32_t *xy,
                                                 uint64_t *bits, int64_t cap, unsigned long long *ctr) {
+    // One lane per ordered adjacent pair (CSR slot) finds its (x, y) and whether the pair was
+    // removed; the wave then walks its removed pairs one by one and reads / copies each pair's
+    // W-word union row with all 64 lanes (coalesced), keeping the rows that are non-empty.
     const int lane = threadIdx.x & 63;
-    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t wave_base = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63);
+    const int64_t slot = wave_base + lane;
     int x = -1, y = -1;
-    bool keep = false;
-    const uint64_t *row = nullptr;
+    bool removed = false;
     if (slot < sumdeg) {
         int lo = 0, hi = n;  // off[lo] <= slot < off[hi]
         while (hi - lo > 1) {
@@ -249,24 +252,36 @@ __global__ __launch_bounds__(256) void k_export(const int32_t *off, const int32_
         }
         x = lo;
         y = nbr[slot];
-        if (rm[(int64_t)x * n + y]) {
-            row = ug + slot * W;
-            uint64_t any = 0;
-            for (int w = 0; w < W; ++w) any |= row[w];
-            keep = any != 0;
+        removed = rm[(int64_t)x * n + y] != 0;
+    }
+    const unsigned long long cand = __ballot(removed);
+    if (!cand) return;
+    unsigned long long keepm = 0;
+    for (unsigned long long mm = cand; mm; mm &= mm - 1) {
+        const int k = __ffsll((long long)mm) - 1;
+        const uint64_t *row = ug + (wave_base + k) * W;
+        uint64_t v = 0;
+        for (int w = lane; w < W; w += 64) v |= row[w];
+        if (__ballot(v != 0)) keepm |= 1ull << k;
+    }
+    if (!keepm) return;
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(ctr, (unsigned long long)__popcll(keepm));
+    base = __shfl(base, 0);
+    if ((keepm >> lane) & 1ull) {
+        const int64_t r = (int64_t)base + __popcll(keepm & ((1ull << lane) - 1ull));
+        if (r < cap) {
+            xy[2 * r] = x;
+            xy[2 * r + 1] = y;
         }
     }
-    const unsigned long long m = __ballot(keep);
-    if (!m) return;
-    unsigned long long base = 0;
-    if (lane == __ffsll((long long)m) - 1) base = atomicAdd(ctr, (unsigned long long)__popcll(m));
-    base = __shfl(base, __ffsll((long long)m) - 1);
-    if (!keep) return;
-    const int64_t r = (int64_t)base + __popcll(m & ((1ull << lane) - 1ull));
-    if (r >= cap) return;
-    xy[2 * r] = x;
-    xy[2 * r + 1] = y;
-    for (int w = 0; w < W; ++w) bits[r * W + w] = row[w];
+    for (unsigned long long mm = keepm; mm; mm &= mm - 1) {
+        const int k = __ffsll((long long)mm) - 1;
+        const int64_t r = (int64_t)base + __popcll(keepm & ((1ull << k) - 1ull));
+        if (r >= cap) break;
+        const uint64_t *row = ug + (wave_base + k) * W;
+        for (int w = lane; w < W; w += 64) bits[r * W + w] = row[w];
+    }
 }
 
 // ---------------------------------------------------------------------------------------
