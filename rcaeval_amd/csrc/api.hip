@@ -89,6 +89,8 @@ extern "C" int pcg_destroy(pcg_handle *h) {
         if (b->p) hipHostFree(b->p);
     for (auto &e : h->ev)
         if (e) hipEventDestroy(e);
+    for (auto &e : h->lev)
+        if (e) hipEventDestroy(e);
     if (h->own_stream && h->stream) hipStreamDestroy(h->stream);
     delete h;
     return PCG_OK;

@@ -29,7 +29,7 @@ constexpr int TILE = 128;
 #endif
 constexpr int KT = PCG_K1_KT;
 constexpr int PAD = 1;  // LDS row padding (doubles) against bank conflicts
-constexpr int MEAN_ROWS = 256;  // rows per partial column sum (N = 10k: 40 chunks x 8 column blocks)
+constexpr int MEAN_ROWS = 64;   // rows per partial column sum (N = 10k: 157 chunks x 8 column blocks)
 
 // partial column sums over row chunks (deterministic two-pass mean)
 __global__ void k_colsum_partial(const double *X, int64_t N, int n, int64_t ldx, double *part) {

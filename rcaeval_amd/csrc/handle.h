@@ -43,6 +43,7 @@ struct pcg_handle {
     bool own_stream = false;
     std::string err;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t lev[2 * PCG_MAX_LEVELS] = {};   // per-depth brackets, read once after the last depth
 
     // scratch
     DevBuf adj, deg, off, nbr, rm, ug, cpre, binom, ctr, deferred, records, nearbuf, exportbuf,

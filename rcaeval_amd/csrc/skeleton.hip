@@ -1966,10 +1966,16 @@ static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc,
                          int max_depth, int flags, int8_t *removed_level) {
     int rc = pcg_skeleton_init(h, C, n, ldc, N, alpha, flags, removed_level);
     if (rc) return rc;
+    // per-depth wall brackets are recorded on the stream and read after the last depth, so the
+    // level loop keeps its one host sync per depth (the one inside pcg_level_end)
+    int done = 0;
     for (int depth = 0;; ++depth) {
         if (max_depth >= 0 && depth > max_depth) break;
+        if (depth >= PCG_MAX_LEVELS) break;   // pcg_level_begin refuses deeper levels itself
+        for (int k = 0; k < 2; ++k)
+            if (!h->lev[2 * depth + k]) PCG_HIP(h, hipEventCreate(&h->lev[2 * depth + k]));
         int64_t total = 0;
-        PCG_HIP(h, hipEventRecord(h->ev[0], h->stream));
+        PCG_HIP(h, hipEventRecord(h->lev[2 * depth], h->stream));
         rc = pcg_level_begin(h, depth, &total, nullptr, nullptr);
         if (rc == 1) break;
         if (rc) return rc;
@@ -1977,10 +1983,13 @@ static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc,
         if (rc) return rc;
         rc = pcg_level_end(h, nullptr);
         if (rc) return rc;
-        PCG_HIP(h, hipEventRecord(h->ev[1], h->stream));
-        PCG_HIP(h, hipEventSynchronize(h->ev[1]));
+        PCG_HIP(h, hipEventRecord(h->lev[2 * depth + 1], h->stream));
+        done = depth + 1;
+    }
+    if (done) PCG_HIP(h, hipEventSynchronize(h->lev[2 * done - 1]));
+    for (int depth = 0; depth < done; ++depth) {
         float ms = 0.f;
-        PCG_HIP(h, hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
+        PCG_HIP(h, hipEventElapsedTime(&ms, h->lev[2 * depth], h->lev[2 * depth + 1]));
         h->st.level_ms[depth] = ms;
     }
     return PCG_OK;

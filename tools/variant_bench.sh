@@ -8,7 +8,7 @@ cp rcaeval_amd/libpcgpu.so /tmp/libpcgpu_base.so
 for v in /tmp/libpcgpu_base.so tools/micro/variants/libpcgpu_*.so; do
   name=$(basename "$v" .so)
   cp "$v" rcaeval_amd/libpcgpu.so
-  timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline > "gpurun_out/var_$name.log" 2>&1 || { echo "$name failed rc=$?"; tail -5 "gpurun_out/var_$name.log"; exit 1; }
+  timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline > "gpurun_out/var_$name.log" 2>&1 || { echo "$name failed rc=$?"; tail -5 "gpurun_out/var_$name.log"; exit 1; }
   python - "$name" "gpurun_out/var_$name.log" <<'PY'
 import json, sys
 l = [x for x in open(sys.argv[2]) if x.startswith("{")]
