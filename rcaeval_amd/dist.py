@@ -134,28 +134,42 @@ def run_sharded_levels(backend, rank: int, world: int, max_depth: int = -1, grou
     return depth
 
 
+def _gather_tensor(t, group=None):
+    """All-gather equal-shaped tensors into one (world * rows, ...) tensor: one RCCL
+    all-gather into a contiguous buffer under nccl, the list form under gloo."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    if dist.get_backend(group) == "nccl":
+        out = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous(), group=group)
+        return out
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t.contiguous(), group=group)
+    return torch.cat(parts)
+
+
 def _allgather_rows(xy, bits, group=None):
-    """All-gather variable-length (xy, bits) device tensors from every rank."""
+    """All-gather variable-length (xy, bits) device tensors from every rank: one count
+    exchange (one host sync), then ONE all-gather of rows packed as [x | y << 32, bits...]
+    (int64, padded to the longest rank)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     cnt = torch.tensor([xy.shape[0]], dtype=torch.int64, device=xy.device)
-    counts = [torch.zeros_like(cnt) for _ in range(world)]
-    dist.all_gather(counts, cnt, group=group)
-    counts = [int(c.item()) for c in counts]
+    counts = _gather_tensor(cnt, group=group).cpu().tolist()
     mx = max(max(counts), 1)
     W = bits.shape[1]
-    pad_xy = torch.zeros((mx, 2), dtype=xy.dtype, device=xy.device)
-    pad_bits = torch.zeros((mx, W), dtype=bits.dtype, device=bits.device)
-    pad_xy[: xy.shape[0]] = xy
-    pad_bits[: bits.shape[0]] = bits
-    all_xy = [torch.empty_like(pad_xy) for _ in range(world)]
-    all_bits = [torch.empty_like(pad_bits) for _ in range(world)]
-    dist.all_gather(all_xy, pad_xy, group=group)
-    dist.all_gather(all_bits, pad_bits, group=group)
-    xy_out = torch.cat([t[:c] for t, c in zip(all_xy, counts)])
-    bits_out = torch.cat([t[:c] for t, c in zip(all_bits, counts)])
-    return xy_out, bits_out
+    k = xy.shape[0]
+    pad = torch.zeros((mx, W + 1), dtype=torch.int64, device=xy.device)
+    if k:
+        xy64 = xy.to(torch.int64)
+        pad[:k, 0] = (xy64[:, 0] & 0xFFFFFFFF) | (xy64[:, 1] << 32)
+        pad[:k, 1:] = bits
+    allrows = _gather_tensor(pad, group=group).view(world, mx, W + 1)
+    rows = torch.cat([allrows[r, :c] for r, c in enumerate(counts)])
+    xy_out = torch.stack([rows[:, 0] & 0xFFFFFFFF, rows[:, 0] >> 32], dim=1).to(torch.int32)
+    return xy_out.contiguous(), rows[:, 1:].contiguous()
 
 
 def _allreduce_stats(stats: dict, device, group=None) -> dict:

@@ -150,3 +150,40 @@ def test_sharded_levels_match_single_process_oracle(world):
             side = set(int(v) for v in (lst[-2] if x < y else lst[-1]))
             assert ref.removed_level[x, y] == d
             assert members == side
+
+
+def _gather_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    from rcaeval_amd.dist import _allgather_rows
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = torch.Generator().manual_seed(rank)
+    k = [5, 0, 3][rank]                      # ragged, one rank empty
+    xy = torch.randint(0, 4000, (k, 2), generator=g, dtype=torch.int32)
+    bits = torch.randint(-2**62, 2**62, (k, 3), generator=g, dtype=torch.int64)
+    bits[:, 0] |= -2**63 if k else 0         # sign bit of the packed words survives
+    out_xy, out_bits = _allgather_rows(xy, bits)
+    dist.destroy_process_group()
+    q.put((rank, xy.numpy(), bits.numpy(), out_xy.numpy(), out_bits.numpy()))
+
+
+def test_allgather_rows_packs_ragged_ranks():
+    """The sepset-row gather of the sharded skeleton (dist._allgather_rows): rows of every rank
+    in rank order, (x, y) and all 64 bits of every union word preserved, empty ranks allowed."""
+    import multiprocessing as mp
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    want_xy = np.concatenate([r[1] for r in res])
+    want_bits = np.concatenate([r[2] for r in res])
+    for _, _, _, oxy, obits in res:
+        np.testing.assert_array_equal(oxy, want_xy)
+        np.testing.assert_array_equal(obits, want_bits)
