@@ -578,6 +578,109 @@ __global__ __launch_bounds__(256) void k_level(LevelArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// depth 1, nodes with 64 < D <= L1_MAXD neighbours, threshold decision. Both tests of a
+// neighbour pair {y, z} of x — (x, y | z) and (x, z | y) — read the same C[y][z] and the same
+// adjacency bit (adj is symmetric), so a lane takes one unordered pair and evaluates both:
+// half the scattered gathers of the per-test form, no barrier in the sweep. The node's
+// per-neighbour terms (C_xk, C_kk, 1/sqrt(C_kk), u_k = C_xk/sqrt(C_kk), c_xx|k, ok_k) are
+// staged in LDS once per block. Same arithmetic and decision as k_level<1, MODE_DECIDE>:
+// for (x, y | z): v = C_yz / sqrt(C_zz), c_xy = C_xy - u_z v, c_yy = C_yy - v^2.
+// A chunk is (x, a contiguous share of the D(D-1)/2 pairs, row-major over y < z).
+constexpr int L1_MAXD = 1024;
+__global__ __launch_bounds__(256) void k_level1_pairs(LevelArgs a) {
+    __shared__ int32_t s_nx[L1_MAXD];
+    __shared__ double s_cx[L1_MAXD], s_d[L1_MAXD], s_ri[L1_MAXD], s_u[L1_MAXD], s_cxx[L1_MAXD];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int64_t chunk = a.chunk_lo + blockIdx.x;
+    int lo = 0, hi = a.n;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (a.cpre[mid] <= chunk) lo = mid; else hi = mid;
+    }
+    const int x = lo;
+    const int D = a.deg[x];
+    const int W = a.W;
+    const int32_t *nx = a.nbr + a.off[x];
+    const double *Cx = a.C + (int64_t)x * a.ldc;
+    const double Cxx = a.diag[x];
+    for (int k = tid; k < D; k += blockDim.x) {
+        const int g = nx[k];
+        const double s = a.diag[g];
+        const double ri = 1.0 / sqrt(s);
+        const double cxk = Cx[g];
+        const double u = cxk * ri;
+        const double cxx = Cxx - u * u;
+        s_nx[k] = g;
+        s_cx[k] = cxk;
+        s_d[k] = s;
+        s_ri[k] = ri;
+        s_u[k] = u;
+        s_cxx[k] = ((s > 0.0) && (cxx == cxx)) ? cxx : __builtin_nan("");   // NaN marks !chol_ok
+    }
+    __syncthreads();
+    const int64_t npairs = (int64_t)D * (D - 1) / 2;
+    const int64_t nch = a.cpre[x + 1] - a.cpre[x];
+    const int64_t c = chunk - a.cpre[x];
+    const int64_t p0 = npairs * c / nch, p1 = npairs * (c + 1) / nch;
+    unsigned long long tests = 0, indep = 0;
+    const double twoD1 = 2.0 * D - 1.0;
+
+    for (int64_t p = p0 + tid; p < p1; p += blockDim.x) {
+        // pair p -> (y, z), y < z: row y starts at y(2D - 1 - y)/2
+        int y = (int)floor((twoD1 - sqrt(twoD1 * twoD1 - 8.0 * (double)p)) * 0.5);
+        auto rowstart = [&](int r) -> int64_t { return (int64_t)r * (2 * D - 1 - r) / 2; };
+        if (y < 0) y = 0;
+        while (y > 0 && rowstart(y) > p) --y;
+        while (rowstart(y + 1) <= p) ++y;
+        const int z = y + 1 + (int)(p - rowstart(y));
+        const int yg = s_nx[y], zg = s_nx[z];
+        const double cyz = a.C[(int64_t)yg * a.ldc + zg];
+        const bool adj_yz = (a.adj[(int64_t)yg * W + (zg >> 6)] >> (zg & 63)) & 1ull;
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            // side 0: test (x, y | z); side 1: test (x, z | y)
+            const int t = side ? z : y;        // the tested neighbour (local), S = {k}
+            const int k = side ? y : z;
+            const int tg = side ? zg : yg, kg = side ? yg : zg;
+            if (tg < x && adj_yz) continue;    // memo: node tg owns (tg, x, {kg})
+            ++tests;
+            const double cxx = s_cxx[k];
+            int dec = 2;
+            if (cxx == cxx) {
+                double pv = 0.0;
+                const double v = cyz * s_ri[k];
+                const double cxt = s_cx[t] - s_u[k] * v;
+                const double ctt = s_d[t] - v * v;
+                dec = decide<MODE_DECIDE>(a, cxt, cxx, ctt, &pv);
+            }
+            if (dec == 2) {
+                const int sg[1] = {kg};
+                push_deferred(a, x, tg, sg, 1);
+            } else if (dec == 1) {
+                ++indep;
+                a.rm[(int64_t)x * a.n + tg] = 1;
+                a.rm[(int64_t)tg * a.n + x] = 1;
+                unsigned long long *row = reinterpret_cast<unsigned long long *>(
+                    a.ug + ((int64_t)a.off[x] + t) * W);
+                atomicOr(&row[kg >> 6], 1ull << (kg & 63));
+                if (adj_yz && tg > x) {        // S in adj(tg): also tg's side of the pair
+                    const int slot = a.off[tg] + find_in_sorted(a.nbr + a.off[tg], a.deg[tg], x);
+                    unsigned long long *rowt = reinterpret_cast<unsigned long long *>(a.ug + (int64_t)slot * W);
+                    atomicOr(&rowt[kg >> 6], 1ull << (kg & 63));
+                }
+            }
+        }
+    }
+    tests = wave_sum(tests);
+    indep = wave_sum(indep);
+    if (lane == 0) {
+        if (tests) atomicAdd(&a.ctr->tests, tests);
+        if (indep) atomicAdd(&a.ctr->indep, indep);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // depth d >= 1, nodes with D <= 64 neighbours: the node's whole local correlation block
 // M[t][k] = C[nbr t, nbr k] (D x D), C[x, nbr t], C[nbr t, nbr t] and the local adjacency
 // masks lmask[t] (bit k <=> nbr k in adj(nbr t)) are staged in LDS once per block; the
@@ -1863,7 +1966,9 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                     const size_t lds = level_lds(h, al.bs);
                     if (lds > 160 * 1024)
                         return pcg_fail(h, PCG_ERR_INVALID, "max degree %d too large for LDS staging", h->maxdeg);
-                    if (mode == MODE_DECIDE) launch_level_mode<MODE_DECIDE>(h, al, l_hi - l_lo, lds);
+                    if (mode == MODE_DECIDE && d == 1 && h->maxdeg <= L1_MAXD)
+                        hipLaunchKernelGGL(k_level1_pairs, dim3((unsigned)(l_hi - l_lo)), dim3(256), 0, h->stream, al);
+                    else if (mode == MODE_DECIDE) launch_level_mode<MODE_DECIDE>(h, al, l_hi - l_lo, lds);
                     else if (mode == MODE_FULLP) launch_level_mode<MODE_FULLP>(h, al, l_hi - l_lo, lds);
                     else launch_level_mode<MODE_EXACT>(h, al, l_hi - l_lo, lds);
                 }
