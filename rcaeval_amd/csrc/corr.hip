@@ -38,7 +38,15 @@ __global__ void k_colsum_partial(const double *X, int64_t N, int n, int64_t ldx,
     if (j >= n) return;
     const int64_t r1 = std::min<int64_t>(r0 + MEAN_ROWS, N);
     double s = 0.0;
-    for (int64_t t = r0; t < r1; ++t) s += X[t * ldx + j];
+    int64_t t = r0;
+    for (; t + 8 <= r1; t += 8) {           // 8 loads in flight, summed in row order
+        double v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = X[(t + k) * ldx + j];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s += v[k];
+    }
+    for (; t < r1; ++t) s += X[t * ldx + j];
     part[(int64_t)blockIdx.y * n + j] = s;
 }
 
@@ -190,12 +198,24 @@ __global__ __launch_bounds__(256) void k_normalize_tiles(const double *G, int64_
     }
     const int i0 = bi * NT, j0 = bj * NT;
     const int c = threadIdx.x & 63, r4 = threadIdx.x >> 6;
-    for (int rr = r4; rr < NT; rr += 4) {
-        const int i = i0 + rr, j = j0 + c;
-        double g = 0.0;
-        if (i < n && j < n && (bi != bj || rr <= c))
-            for (int s = 0; s < ks; ++s) g += G[(int64_t)s * slab_stride + (int64_t)i * ldg + j];
-        t[rr][c] = g;
+    {   // all 16 rows of this thread in flight per slab; slabs summed in order 0..ks-1
+        constexpr int RPT = NT / 4;
+        double g[RPT];
+        bool live[RPT];
+#pragma unroll
+        for (int q = 0; q < RPT; ++q) {
+            const int rr = r4 + 4 * q, i = i0 + rr, j = j0 + c;
+            live[q] = i < n && j < n && (bi != bj || rr <= c);
+            g[q] = 0.0;
+        }
+        for (int s = 0; s < ks; ++s) {
+            const double *Gs = G + (int64_t)s * slab_stride;
+#pragma unroll
+            for (int q = 0; q < RPT; ++q)
+                if (live[q]) g[q] += Gs[(int64_t)(i0 + r4 + 4 * q) * ldg + j0 + c];
+        }
+#pragma unroll
+        for (int q = 0; q < RPT; ++q) t[r4 + 4 * q][c] = g[q];
     }
     __syncthreads();
     for (int rr = r4; rr < NT; rr += 4) {
