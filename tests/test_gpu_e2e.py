@@ -330,3 +330,24 @@ def test_circa_matches_oracle_pipeline(m, rows, seed):
     want = [n for n, _ in sorted(rht(g, inject, data), key=lambda x: x[1], reverse=True)]
     assert out["ranks"] == want
     assert len(out["ranks"]) > 0
+
+
+@pytest.mark.parametrize("method", ["circa", "cloudranger"])
+def test_rq2_run_other_pc_methods(tmp_path, method):
+    """rq2.py's loop with the other PC-based methods: every case's dumped
+    ranks equal a direct call of the method on the same window, in the harness's case order
+    and from the same np.random state (CloudRanger's walk and RHT's SLI draw use it)."""
+    from rcaeval_amd import e2e, rq2
+    root = os.path.join(str(tmp_path), "data", "online-boutique")
+    synth.write_rq2_dataset(root, services=["cartservice", "adservice"], faults=("cpu", "delay"), cases=1, rows=1200)
+    out_dir = os.path.join(str(tmp_path), "out")
+    np.random.seed(4)
+    res = rq2.run(root, method, "online-boutique", out_dir)
+    assert res["cases"] == 4
+    np.random.seed(4)
+    for p in rq2.list_cases(root):
+        c = rq2.load_case(p)
+        want = getattr(e2e, method)(c["data"], c["inject_time"], dataset="online-boutique", sli=c["sli"],
+                                    n_iter=c["num_node"])["ranks"]
+        got = rq2.load_json(os.path.join(out_dir, "results", c["result_name"]))["0"]
+        assert got == want and len(got) > 0
