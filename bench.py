@@ -251,15 +251,26 @@ def main():
 
     phases = []
 
+    # PCG_DIST_NATIVE=1: the level loop and its collectives run in C (pcg_skeleton_sharded on
+    # an RCCL communicator of the library's own); default: the torch.distributed driver
+    native = world > 1 and os.environ.get("PCG_DIST_NATIVE") == "1"
+    if native:
+        from rcaeval_amd.dist import native_comm
+        native_comm(eng)
+
     def one_step():
         t0 = time.perf_counter()
-        if world > 1:
+        if native:
+            C = eng.corr_sharded(Xd)
+        elif world > 1:
             from rcaeval_amd.dist import sharded_corr
             C = sharded_corr(eng, Xd)
         else:
             C = eng.corr(Xd)
         torch.cuda.synchronize()
         phases.append(("corr", time.perf_counter() - t0))
+        if native:
+            return eng.skeleton_sharded(C, args.samples, alpha=args.alpha, max_depth=args.max_depth, flags=flags)
         if world > 1:
             from rcaeval_amd.dist import sharded_skeleton
             trace = [] if os.environ.get("PCG_DIST_TRACE") else None
@@ -323,7 +334,8 @@ def main():
             "config": {"workload": f"stable PC-fisherz skeleton, {args.n} vars x {args.samples} samples, "
                                    f"max depth {args.max_depth}, alpha {args.alpha}, seed {args.seed}, "
                                    f"ER DAG p=2/(n-1), weights +-U(0.1,0.5)",
-                       "parallelism": f"edge-sharded x{world}" if world > 1 else "single GPU",
+                       "parallelism": (f"edge-sharded x{world}" + (" (native RCCL driver)" if native else ""))
+                                      if world > 1 else "single GPU",
                        "decision": "full p-value" if args.full_p else "threshold + exact band"},
             "skeleton_ms": ms,
             "step_ms_all": [round(1000 * t, 3) for t in times],

@@ -38,7 +38,7 @@ extern "C" {
                                 (causal-learn FisherZ raises ValueError) [U]         */
 #define PCG_ERR_DOMAIN -5    /* math domain error in the Fisher-z expression
                                 (Python math.log/sqrt raise ValueError) [U]          */
-#define PCG_ERR_RCCL -6      /* reserved: collective failure                          */
+#define PCG_ERR_RCCL -6      /* RCCL unavailable or a collective failed               */
 #define PCG_ERR_OVERFLOW -7  /* an internal list overflowed its capacity: capacities were
                                 enlarged, rerun the skeleton (pcg_skeleton does so itself) */
 
@@ -171,6 +171,31 @@ int pcg_level_split(pcg_handle *h, int rank, int world, int64_t *chunk_lo, int64
  * decomposition sizes its chunks so that each rank's slice still fills its GPU.          */
 int pcg_set_world_size(pcg_handle *h, int world);
 int pcg_set_removal_buffer(pcg_handle *h, uint8_t *rm_dev, int64_t bytes);
+
+/* ---- native multi-GPU driver (RCCL over xGMI, one process per GPU) -----------------
+ * SURVEY §8(b)'s pcg_comm_init / pcg_skeleton_sharded: the whole edge-sharded level loop
+ * runs in C with the collectives on the handle's stream — no host language between the
+ * per-depth steps. RCCL is resolved at run time (the copy the process already loaded, e.g.
+ * PyTorch's, else librccl.so.1), so one RCCL instance serves both.
+ * pcg_comm_unique_id: rank 0 creates the id (NCCL_UNIQUE_ID_BYTES = 128 bytes) and the
+ * caller hands the bytes to every rank; pcg_comm_init joins rank `rank` of `world`.      */
+#define PCG_COMM_ID_BYTES 128
+int pcg_comm_unique_id(void *id_out, int64_t bytes);
+int pcg_comm_init(pcg_handle *h, const void *unique_id, int rank, int world);
+int pcg_comm_destroy(pcg_handle *h);
+/* K1 on the communicator: pcg_corr_shard + RCCL all-gather + pcg_corr_shard_finish; C is
+ * bitwise the single-GPU pcg_corr result on every rank.                                   */
+int pcg_corr_sharded(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx,
+                     double *C, int64_t ldc);
+/* The edge-sharded stable skeleton on the communicator: per depth begin / split / run on
+ * this rank's work-balanced chunk range / RCCL all-reduce(MAX) of the removal flags and
+ * status bytes / end; then the per-level counters are summed over ranks and every rank's
+ * sepset rows are all-gathered, so pcg_sepset_* and removed_level describe the whole
+ * skeleton on every rank (a pair's row may appear once per rank that saw it: OR them).
+ * Same arguments and results as pcg_skeleton.                                              */
+int pcg_skeleton_sharded(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N,
+                         double alpha, int max_depth, int flags, int8_t *removed_level,
+                         pcg_stats *stats);
 
 /* ---- K4: PageRank head -------------------------------------------------------------
  * Replaces scikit-network 0.31.0 PageRank(damping_factor, solver='piteration', n_iter,

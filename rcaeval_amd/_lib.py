@@ -98,6 +98,11 @@ SIGNATURES = [
     ("pcg_level_split", I32, [P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(I64), ctypes.POINTER(I64)]),
     ("pcg_set_removal_buffer", I32, [P, P, I64]),
     ("pcg_set_world_size", I32, [P, ctypes.c_int]),
+    ("pcg_comm_unique_id", I32, [P, I64]),
+    ("pcg_comm_init", I32, [P, P, ctypes.c_int, ctypes.c_int]),
+    ("pcg_comm_destroy", I32, [P]),
+    ("pcg_corr_sharded", I32, [P, P, I64, I64, I64, P, I64]),
+    ("pcg_skeleton_sharded", I32, [P, P, I64, I64, I64, D, ctypes.c_int, ctypes.c_int, P, ctypes.POINTER(PcgStats)]),
     ("pcg_pagerank_dense", I32, [P, P, I64, I64, D, ctypes.c_int, D, P]),
     ("pcg_pagerank_csr", I32, [P, P, P, P, I64, I64, D, ctypes.c_int, D, P]),
     ("pcg_random_walk", I32, [P, P, I64, I64, I64, I64, ctypes.c_uint64, ctypes.c_uint64,

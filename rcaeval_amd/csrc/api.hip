@@ -79,6 +79,7 @@ extern "C" int pcg_destroy(pcg_handle *h) {
     if (!h) return PCG_OK;
     hipSetDevice(h->device);
     if (h->stream) hipStreamSynchronize(h->stream);
+    pcg_comm_release(h);
     DevBuf *bufs[] = {&h->adj, &h->deg, &h->off, &h->nbr, &h->rm, &h->ug, &h->cpre, &h->binom, &h->ctr,
                       &h->deferred, &h->records, &h->nearbuf, &h->exportbuf, &h->export_xy, &h->diag,
                       &h->colmean, &h->pr_scratch, &h->batch_scratch};

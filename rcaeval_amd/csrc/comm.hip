@@ -1,0 +1,290 @@
+// comm.hip — native multi-GPU driver of libpcgpu.so: RCCL over xGMI, one process per GPU.
+//
+// each PC depth's work list is split by work across the ranks (the same
+// pcg_level_split cut as the Python driver in rcaeval_amd/dist.py), every rank evaluates its
+// owner-disjoint chunk range, and the n*n removal flags + status bytes are merged with ONE
+// all-reduce(MAX, uint8) on the handle's stream (RCCL has no bitwise OR; MAX over 0/1 bytes is
+// the same merge) before pcg_level_end applies them identically everywhere. The loop runs in C:
+// no host-language round trip between the per-depth steps.
+//
+// RCCL is resolved at run time: first the copy the process has already loaded (PyTorch ships
+// one), else librccl.so.1 — so a process that also uses torch.distributed holds one RCCL.
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+
+#include "handle.h"
+
+namespace {
+
+struct Rccl {
+    bool ok = false;
+    std::string err;
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclAllGather) all_gather = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+};
+
+const Rccl &rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void *lib = nullptr;
+        for (const char *name : {"librccl.so.1", "librccl.so"}) {
+            lib = dlopen(name, RTLD_NOW | RTLD_NOLOAD);          // already in the process?
+            if (lib) break;
+        }
+        if (!lib) lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!lib) lib = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+        if (!lib) {
+            r.err = std::string("librccl not found: ") + dlerror();
+            return;
+        }
+        r.get_unique_id = (decltype(r.get_unique_id))dlsym(lib, "ncclGetUniqueId");
+        r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(lib, "ncclCommInitRank");
+        r.comm_destroy = (decltype(r.comm_destroy))dlsym(lib, "ncclCommDestroy");
+        r.all_reduce = (decltype(r.all_reduce))dlsym(lib, "ncclAllReduce");
+        r.all_gather = (decltype(r.all_gather))dlsym(lib, "ncclAllGather");
+        r.error_string = (decltype(r.error_string))dlsym(lib, "ncclGetErrorString");
+        r.ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.all_reduce && r.all_gather &&
+               r.error_string;
+        if (!r.ok) r.err = "librccl lacks an expected symbol";
+    });
+    return r;
+}
+
+#define PCG_NCCL(h, expr)                                                                   \
+    do {                                                                                    \
+        ncclResult_t _r = (expr);                                                           \
+        if (_r != ncclSuccess)                                                              \
+            return pcg_fail((h), PCG_ERR_RCCL, "%s failed: %s", #expr, rccl().error_string(_r)); \
+    } while (0)
+
+int need_comm(pcg_handle *h) {
+    if (!h) return PCG_ERR_INVALID;
+    if (!h->comm) return pcg_fail(h, PCG_ERR_INVALID, "no communicator: call pcg_comm_init first");
+    return PCG_OK;
+}
+
+// [x | y << 32, W union words] per exported row, zero-padded to `rows_out` rows
+__global__ void k_pack_rows(const int32_t *xy, const uint64_t *bits, int64_t rows, int W, int64_t rows_out,
+                            int64_t *out) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = rows_out * (W + 1);
+    if (e >= total) return;
+    const int64_t r = e / (W + 1);
+    const int c = (int)(e - r * (W + 1));
+    int64_t v = 0;
+    if (r < rows) {
+        if (c == 0) v = (int64_t)(uint32_t)xy[2 * r] | ((int64_t)(uint32_t)xy[2 * r + 1] << 32);
+        else v = (int64_t)bits[r * W + (c - 1)];
+    }
+    out[e] = v;
+}
+
+__global__ void k_unpack_rows(const int64_t *in, int64_t rows, int W, int32_t *xy, uint64_t *bits) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= rows * (W + 1)) return;
+    const int64_t r = e / (W + 1);
+    const int c = (int)(e - r * (W + 1));
+    const int64_t v = in[e];
+    if (c == 0) {
+        xy[2 * r] = (int32_t)(uint32_t)(v & 0xffffffffll);
+        xy[2 * r + 1] = (int32_t)(uint32_t)((uint64_t)v >> 32);
+    } else {
+        bits[r * W + (c - 1)] = (uint64_t)v;
+    }
+}
+
+int sharded_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N, double alpha,
+                 int max_depth, int flags, int8_t *removed_level) {
+    const int64_t nb = n * n + PCG_RM_STATUS;
+    if (!pcg_ensure(h, h->comm_rm, (size_t)nb)) return pcg_fail(h, PCG_ERR_OOM, "removal flags");
+    int rc = pcg_set_removal_buffer(h, (uint8_t *)h->comm_rm.p, nb);
+    if (!rc) rc = pcg_set_world_size(h, h->comm_world);
+    if (!rc) rc = pcg_skeleton_init(h, C, n, ldc, N, alpha, flags, removed_level);
+    ncclComm_t comm = (ncclComm_t)h->comm;
+    for (int depth = 0; !rc; ++depth) {
+        if (max_depth >= 0 && depth > max_depth) break;
+        int64_t total = 0, lo = 0, hi = 0;
+        rc = pcg_level_begin(h, depth, &total, nullptr, nullptr);
+        if (rc == 1) { rc = PCG_OK; break; }
+        if (rc) break;
+        rc = pcg_level_split(h, h->comm_rank, h->comm_world, &lo, &hi);
+        if (!rc) rc = pcg_level_run(h, lo, hi);
+        if (rc) break;
+        const ncclResult_t r = rccl().all_reduce(h->comm_rm.p, h->comm_rm.p, (size_t)nb, ncclUint8, ncclMax, comm,
+                                                 h->stream);
+        if (r != ncclSuccess) {
+            rc = pcg_fail(h, PCG_ERR_RCCL, "ncclAllReduce(removal flags) failed: %s", rccl().error_string(r));
+            break;
+        }
+        rc = pcg_level_end(h, nullptr);
+    }
+    pcg_set_removal_buffer(h, nullptr, 0);
+    pcg_set_world_size(h, 1);
+    return rc;
+}
+
+// per-depth counters summed over ranks (replicated quantities — calls, degrees, edges — are
+// identical on every rank already)
+int reduce_stats(pcg_handle *h) {
+    const int L = h->st.levels;
+    if (L <= 0) return PCG_OK;
+    std::vector<int64_t> v((size_t)4 * L);
+    for (int d = 0; d < L; ++d) {
+        v[d] = h->st.tests[d];
+        v[L + d] = h->st.indep[d];
+        v[2 * L + d] = h->st.exact[d];
+        v[3 * L + d] = h->st.near_alpha[d];
+    }
+    if (!pcg_ensure(h, h->comm_small, sizeof(int64_t) * v.size())) return pcg_fail(h, PCG_ERR_OOM, "stats");
+    PCG_HIP(h, hipMemcpyAsync(h->comm_small.p, v.data(), sizeof(int64_t) * v.size(), hipMemcpyHostToDevice,
+                              h->stream));
+    PCG_NCCL(h, rccl().all_reduce(h->comm_small.p, h->comm_small.p, v.size(), ncclInt64, ncclSum,
+                                  (ncclComm_t)h->comm, h->stream));
+    PCG_HIP(h, hipMemcpyAsync(v.data(), h->comm_small.p, sizeof(int64_t) * v.size(), hipMemcpyDeviceToHost,
+                              h->stream));
+    PCG_HIP(h, hipStreamSynchronize(h->stream));
+    for (int d = 0; d < L; ++d) {
+        h->st.tests[d] = v[d];
+        h->st.indep[d] = v[L + d];
+        h->st.exact[d] = v[2 * L + d];
+        h->st.near_alpha[d] = v[3 * L + d];
+    }
+    return PCG_OK;
+}
+
+// every rank's exported sepset rows -> the handle's export buffers on every rank
+int gather_sepsets(pcg_handle *h) {
+    const int world = h->comm_world, W = h->W;
+    ncclComm_t comm = (ncclComm_t)h->comm;
+    if (!pcg_ensure(h, h->comm_small, sizeof(int64_t) * (size_t)(world + 1)))
+        return pcg_fail(h, PCG_ERR_OOM, "row counts");
+    int64_t *cnt_d = (int64_t *)h->comm_small.p;
+    const int64_t mine = h->export_rows;
+    PCG_HIP(h, hipMemcpyAsync(cnt_d + world, &mine, sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
+    PCG_NCCL(h, rccl().all_gather(cnt_d + world, cnt_d, 1, ncclInt64, comm, h->stream));
+    std::vector<int64_t> cnt(world);
+    PCG_HIP(h, hipMemcpyAsync(cnt.data(), cnt_d, sizeof(int64_t) * world, hipMemcpyDeviceToHost, h->stream));
+    PCG_HIP(h, hipStreamSynchronize(h->stream));
+    int64_t mx = 1, total = 0;
+    for (int64_t c : cnt) {
+        mx = std::max(mx, c);
+        total += c;
+    }
+    const int64_t per = mx * (W + 1);
+    if (!pcg_ensure(h, h->comm_packed, sizeof(int64_t) * (size_t)per) ||
+        !pcg_ensure(h, h->comm_gathered, sizeof(int64_t) * (size_t)per * world))
+        return pcg_fail(h, PCG_ERR_OOM, "sepset row gather (%lld rows x %d words)", (long long)mx, W + 1);
+    hipLaunchKernelGGL(k_pack_rows, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, h->stream,
+                       (const int32_t *)h->export_xy.p, (const uint64_t *)h->exportbuf.p, mine, W, mx,
+                       (int64_t *)h->comm_packed.p);
+    PCG_NCCL(h, rccl().all_gather(h->comm_packed.p, h->comm_gathered.p, (size_t)per, ncclInt64, comm, h->stream));
+    const int64_t cap = std::max<int64_t>(total, 1);
+    if (!pcg_ensure(h, h->exportbuf, sizeof(uint64_t) * (size_t)cap * W) ||
+        !pcg_ensure(h, h->export_xy, sizeof(int32_t) * 2 * (size_t)cap))
+        return pcg_fail(h, PCG_ERR_OOM, "sepset export buffer");
+    int64_t at = 0;
+    for (int r = 0; r < world; ++r) {
+        if (!cnt[r]) continue;
+        const int64_t e = cnt[r] * (W + 1);
+        hipLaunchKernelGGL(k_unpack_rows, dim3((unsigned)((e + 255) / 256)), dim3(256), 0, h->stream,
+                           (const int64_t *)h->comm_gathered.p + (int64_t)r * per, cnt[r], W,
+                           (int32_t *)h->export_xy.p + 2 * at, (uint64_t *)h->exportbuf.p + at * W);
+        at += cnt[r];
+    }
+    PCG_HIP(h, hipGetLastError());
+    PCG_HIP(h, hipStreamSynchronize(h->stream));
+    h->export_rows = total;
+    h->export_cap = std::max(h->export_cap, cap);
+    return PCG_OK;
+}
+
+}  // namespace
+
+void pcg_comm_release(pcg_handle *h) {
+    if (!h) return;
+    if (h->comm && rccl().ok) rccl().comm_destroy((ncclComm_t)h->comm);
+    h->comm = nullptr;
+    for (DevBuf *b : {&h->comm_rm, &h->comm_packed, &h->comm_gathered, &h->comm_small})
+        if (b->p) {
+            (void)hipFree(b->p);
+            b->p = nullptr;
+            b->bytes = 0;
+        }
+}
+
+extern "C" int pcg_comm_unique_id(void *id_out, int64_t bytes) {
+    if (!id_out || bytes < (int64_t)sizeof(ncclUniqueId)) return PCG_ERR_INVALID;
+    if (!rccl().ok) return PCG_ERR_RCCL;
+    ncclUniqueId id;
+    if (rccl().get_unique_id(&id) != ncclSuccess) return PCG_ERR_RCCL;
+    std::memcpy(id_out, &id, sizeof(id));
+    return PCG_OK;
+}
+
+extern "C" int pcg_comm_init(pcg_handle *h, const void *unique_id, int rank, int world) {
+    if (!h || !unique_id || world < 1 || rank < 0 || rank >= world)
+        return pcg_fail(h, PCG_ERR_INVALID, "pcg_comm_init: rank %d of %d", rank, world);
+    if (!rccl().ok) return pcg_fail(h, PCG_ERR_RCCL, "%s", rccl().err.c_str());
+    pcg_comm_release(h);
+    PCG_HIP(h, hipSetDevice(h->device));
+    ncclUniqueId id;
+    std::memcpy(&id, unique_id, sizeof(id));
+    ncclComm_t comm = nullptr;
+    PCG_NCCL(h, rccl().comm_init_rank(&comm, world, id, rank));
+    h->comm = comm;
+    h->comm_rank = rank;
+    h->comm_world = world;
+    return PCG_OK;
+}
+
+extern "C" int pcg_comm_destroy(pcg_handle *h) {
+    if (!h) return PCG_ERR_INVALID;
+    pcg_comm_release(h);
+    h->comm_rank = 0;
+    h->comm_world = 1;
+    return PCG_OK;
+}
+
+extern "C" int pcg_corr_sharded(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx, double *C,
+                                int64_t ldc) {
+    int rc = need_comm(h);
+    if (rc) return rc;
+    int64_t rows = 0;
+    rc = pcg_corr_shard_rows(n, h->comm_world, &rows);
+    if (rc) return pcg_fail(h, rc, "pcg_corr_shard_rows");
+    const size_t per = (size_t)rows * (size_t)n;
+    if (!pcg_ensure(h, h->comm_packed, sizeof(double) * std::max<size_t>(per, 1)) ||
+        !pcg_ensure(h, h->comm_gathered, sizeof(double) * std::max<size_t>(per * h->comm_world, 1)))
+        return pcg_fail(h, PCG_ERR_OOM, "sharded K1 buffers");
+    rc = pcg_corr_shard(h, X, N, n, ldx, h->comm_rank, h->comm_world, (double *)h->comm_packed.p);
+    if (rc) return rc;
+    PCG_NCCL(h, rccl().all_gather(h->comm_packed.p, h->comm_gathered.p, per, ncclFloat64, (ncclComm_t)h->comm,
+                                  h->stream));
+    return pcg_corr_shard_finish(h, (const double *)h->comm_gathered.p, N, n, h->comm_world, C, ldc);
+}
+
+extern "C" int pcg_skeleton_sharded(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N,
+                                    double alpha, int max_depth, int flags, int8_t *removed_level,
+                                    pcg_stats *stats) {
+    int rc = need_comm(h);
+    if (rc) return rc;
+    for (int attempt = 0; attempt < 6; ++attempt) {
+        rc = sharded_once(h, C, n, ldc, N, alpha, max_depth, flags, removed_level);
+        if (rc != PCG_ERR_OVERFLOW) break;   // the merged status byte makes every rank rerun
+    }
+    // errors that the merged status bytes raise are raised on every rank at the same depth, so
+    // the collectives below are skipped consistently; a local HIP / argument error is not
+    if (!rc) rc = reduce_stats(h);
+    if (!rc) rc = gather_sepsets(h);
+    if (stats) *stats = h->st;
+    return rc;
+}

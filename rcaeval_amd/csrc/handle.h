@@ -83,7 +83,14 @@ struct pcg_handle {
     pcg_stats st{};
     float run_ms = 0.f;              // CI-test kernel time of the current level
     bool run_timed = false;          // ev[2]/ev[3] bracket this level's CI-test kernels
+
+    // RCCL communicator of pcg_comm_init (comm.hip): one per (process, device)
+    void *comm = nullptr;
+    int comm_rank = 0, comm_world = 1;
+    DevBuf comm_rm, comm_packed, comm_gathered, comm_small;
 };
+
+void pcg_comm_release(pcg_handle *h);      // comm.hip: destroy the communicator, free its buffers
 
 int pcg_fail(pcg_handle *h, int code, const char *fmt, ...);
 bool pcg_ensure(pcg_handle *h, DevBuf &b, size_t bytes);   // grow-only allocation

@@ -239,5 +239,32 @@ def sharded_skeleton(eng, C, N: int, alpha: float = 0.05, max_depth: int = -1, f
     return out
 
 
-__all__ = ["split_by_work", "run_sharded_levels", "sharded_skeleton", "sharded_corr", "GpuLevelBackend"]
+def native_comm(eng, group=None) -> None:
+    """Give ``eng`` an RCCL communicator over the ranks of ``group`` (pcg_comm_init): rank 0
+    makes the unique id, the existing process group broadcasts its 128 bytes."""
+    import torch
+    import torch.distributed as dist
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    dev = eng.device if dist.get_backend(group) == "nccl" else "cpu"
+    buf = torch.zeros(128, dtype=torch.uint8, device=dev)
+    if rank == 0:
+        buf.copy_(torch.frombuffer(bytearray(eng.comm_unique_id()), dtype=torch.uint8))
+    dist.broadcast(buf, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    eng.comm_init(bytes(buf.cpu().numpy().tobytes()), rank, world)
+
+
+def native_sharded_corr(eng, X):
+    """K1 sharded with the all-gather issued from C (needs ``native_comm`` first)."""
+    return eng.corr_sharded(X)
+
+
+def native_sharded_skeleton(eng, C, N: int, alpha: float = 0.05, max_depth: int = -1, flags: int = 0):
+    """The edge-sharded skeleton with the whole level loop in C: per depth begin / split / run /
+    RCCL all-reduce(MAX) / end on the handle's stream, then the counters summed and the sepset
+    rows all-gathered (pcg_skeleton_sharded). Same result as ``sharded_skeleton``."""
+    return eng.skeleton_sharded(C, N, alpha=alpha, max_depth=max_depth, flags=flags)
+
+
+__all__ = ["split_by_work", "run_sharded_levels", "sharded_skeleton", "sharded_corr", "GpuLevelBackend",
+           "native_comm", "native_sharded_corr", "native_sharded_skeleton"]
 _ = _lib

@@ -150,6 +150,41 @@ class Engine:
               "pcg_corr_shard_finish")
         return C
 
+    # ------------------------------------------------------------------ native multi-GPU
+    def comm_unique_id(self) -> bytes:
+        """RCCL unique id (PCG_COMM_ID_BYTES) for pcg_comm_init; rank 0 makes it."""
+        buf = ctypes.create_string_buffer(128)
+        check(self.h, self.lib.pcg_comm_unique_id(buf, 128), "pcg_comm_unique_id")
+        return buf.raw
+
+    def comm_init(self, unique_id: bytes, rank: int, world: int) -> None:
+        buf = ctypes.create_string_buffer(bytes(unique_id), 128)
+        check(self.h, self.lib.pcg_comm_init(self.h, buf, int(rank), int(world)), "pcg_comm_init")
+
+    def corr_sharded(self, X):
+        """K1 on the handle's communicator (pcg_corr_sharded): bitwise ``corr``."""
+        torch = _torch()
+        Xd = self.to_device(X)
+        N, n = Xd.shape
+        C = torch.empty((n, n), dtype=torch.float64, device=self.device)
+        check(self.h, self.lib.pcg_corr_sharded(self.h, ctypes.c_void_p(Xd.data_ptr()), N, n, n,
+                                                ctypes.c_void_p(C.data_ptr()), n), "pcg_corr_sharded")
+        return C
+
+    def skeleton_sharded(self, C, N: int, alpha: float = 0.05, max_depth: int = -1, flags: int = 0) -> SkeletonOut:
+        """The edge-sharded skeleton with the level loop in C (pcg_skeleton_sharded)."""
+        torch = _torch()
+        Cd = self.to_device(C)
+        n = Cd.shape[0]
+        rl = torch.empty((n, n), dtype=torch.int8, device=self.device)
+        st = PcgStats()
+        rc = self.lib.pcg_skeleton_sharded(self.h, ctypes.c_void_p(Cd.data_ptr()), n, n, int(N), float(alpha),
+                                           int(max_depth), int(flags), ctypes.c_void_p(rl.data_ptr()),
+                                           ctypes.byref(st))
+        check(self.h, rc, "pcg_skeleton_sharded")
+        self.sync()
+        return self._collect(n, rl, st, 0.0)
+
     # ------------------------------------------------------------------ K2/K3
     def skeleton(self, C, N: int, alpha: float = 0.05, max_depth: int = -1, flags: int = 0,
                  record_capacity: int = 0) -> SkeletonOut:

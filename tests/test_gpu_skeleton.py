@@ -150,3 +150,23 @@ def test_sharded_corr_bitwise_equals_single_gpu(eng, n, N, world):
     assert torch.equal(C1, Cw)
     if n <= 300:
         np.testing.assert_allclose(C1.cpu().numpy(), np.corrcoef(X.T), rtol=0, atol=2e-14)
+
+
+@pytest.mark.parametrize("n,N,max_depth", [(300, 1200, -1), (2000, 10000, 2)])
+def test_native_sharded_single_rank_equals_single_gpu(eng, n, N, max_depth):
+    """pcg_comm_init / pcg_corr_sharded / pcg_skeleton_sharded (the C-side RCCL driver) on a
+    one-rank communicator: every collective runs; C is bitwise pcg_corr's, the skeleton,
+    counters and sepset unions equal pcg_skeleton's."""
+    import torch
+    from rcaeval_amd._lib import check
+    X = synth.gaussian_sem(n, N, seed=21)
+    eng.comm_init(eng.comm_unique_id(), 0, 1)
+    C1 = eng.corr(X)
+    C2 = eng.corr_sharded(X)
+    assert torch.equal(C1, C2)
+    a = eng.skeleton(C1, N, max_depth=max_depth)
+    b = eng.skeleton_sharded(C1, N, max_depth=max_depth)
+    np.testing.assert_array_equal(a.removed_level, b.removed_level)
+    assert a.stats["tests"] == b.stats["tests"] and a.stats["indep"] == b.stats["indep"]
+    assert _unions_from_engine(a) == _unions_from_engine(b)
+    check(eng.h, eng.lib.pcg_comm_destroy(eng.h), "pcg_comm_destroy")
