@@ -92,6 +92,9 @@ extern "C" int pcg_destroy(pcg_handle *h) {
         if (e) hipEventDestroy(e);
     for (auto &e : h->lev)
         if (e) hipEventDestroy(e);
+    if (h->ev_fork) hipEventDestroy(h->ev_fork);
+    if (h->ev_join) hipEventDestroy(h->ev_join);
+    if (h->aux) hipStreamDestroy(h->aux);
     if (h->own_stream && h->stream) hipStreamDestroy(h->stream);
     delete h;
     return PCG_OK;

@@ -84,6 +84,10 @@ struct pcg_handle {
     float run_ms = 0.f;              // CI-test kernel time of the current level
     bool run_timed = false;          // ev[2]/ev[3] bracket this level's CI-test kernels
 
+    // second stream: a depth's large-degree class runs beside its LDS-resident class
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+
     // RCCL communicator of pcg_comm_init (comm.hip): one per (process, device)
     void *comm = nullptr;
     int comm_rank = 0, comm_world = 1;

@@ -1929,6 +1929,17 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                 else hipLaunchKernelGGL(k_level0<MODE_EXACT>, grid, block, 0, h->stream, a);
             } else {
                 const int64_t s_lo = chunk_lo, s_hi = std::min(chunk_hi, h->total_small);
+                // both classes present: the large-degree class runs on the aux stream beside
+                // the LDS-resident class, forked after everything already on the main stream
+                // and joined before the exact path
+                const bool fork = s_hi > s_lo && chunk_hi > h->total_small;
+                hipStream_t main_stream = h->stream;
+                if (fork) {
+                    if (!h->aux) PCG_HIP(h, hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking));
+                    if (!h->ev_fork) PCG_HIP(h, hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+                    if (!h->ev_join) PCG_HIP(h, hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+                    PCG_HIP(h, hipEventRecord(h->ev_fork, main_stream));
+                }
                 if (s_hi > s_lo) {
                     LevelArgs as = a;
                     as.chunk_lo = s_lo;
@@ -1947,6 +1958,14 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                 }
                 const int64_t l_lo = std::max(chunk_lo, h->total_small) - h->total_small;
                 const int64_t l_hi = chunk_hi - h->total_small;
+                struct StreamSwap {   // the large class launches on h->aux; restored on every exit
+                    pcg_handle *h; hipStream_t main; bool on;
+                    ~StreamSwap() { if (on) h->stream = main; }
+                } swap{h, main_stream, fork};
+                if (fork) {
+                    PCG_HIP(h, hipStreamWaitEvent(h->aux, h->ev_fork, 0));
+                    h->stream = h->aux;
+                }
                 if (l_hi > l_lo && d > PCG_MAX_DEPTH) {
                     LevelArgs al = a;
                     al.cpre = (const int64_t *)h->cpre.p + (h->n + 1);
@@ -1971,6 +1990,12 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                     else if (mode == MODE_DECIDE) launch_level_mode<MODE_DECIDE>(h, al, l_hi - l_lo, lds);
                     else if (mode == MODE_FULLP) launch_level_mode<MODE_FULLP>(h, al, l_hi - l_lo, lds);
                     else launch_level_mode<MODE_EXACT>(h, al, l_hi - l_lo, lds);
+                }
+                if (fork) {
+                    PCG_HIP(h, hipEventRecord(h->ev_join, h->aux));
+                    h->stream = main_stream;
+                    swap.on = false;
+                    PCG_HIP(h, hipStreamWaitEvent(main_stream, h->ev_join, 0));
                 }
             }
         }
