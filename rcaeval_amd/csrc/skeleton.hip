@@ -43,7 +43,10 @@ namespace {
 constexpr int MODE_DECIDE = 0;
 constexpr int MODE_FULLP = 1;
 constexpr int MODE_EXACT = 2;
-#define PCG_TGROUP 4             // candidates c per lane task in k_level_lds_t
+// candidates c per lane task in k_level_lds_t, per depth (measured, tools/variant_bench.sh):
+// groups of 8 halve the per-y shared work at depths 2 and 4 (depth 2 -28 %, depth 4 -3 % with
+// 2 waves/SIMD of 227 VGPRs); depth 3 keeps groups of 4 (4 waves/SIMD, 8 was +15 %)
+__host__ __device__ constexpr int tg_of_depth(int d) { return d == 3 ? 4 : 8; }
 
 struct LevelArgs {
     const double *C;
@@ -130,7 +133,7 @@ __device__ __forceinline__ void flag_error(const LevelArgs &a, int err) {
 // [g*TG + 1, D - DM + 1] for every group g with g*TG <= D - DM
 __host__ __device__ inline int tg_pairs(int D, int DM) {
     int s = 0;
-    for (int cb = 0; cb <= D - DM; cb += PCG_TGROUP) {
+    for (int cb = 0; cb <= D - DM; cb += tg_of_depth(DM)) {
         const int m = D - (DM - 1) - cb;
         if (m > 0) s += m;
     }
@@ -1008,13 +1011,13 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
 //   v_c = (M[c][y] - l_c.v_T) / lambda_c,  c_yy = byy - v_c^2,  c_xy = bxy - u_c v_c
 // — the same partial correlation, ~9 fp64 ops per test instead of ~26. Tasks (g, T): group
 // g covers c in [g*TG, g*TG+TG), T ranges over (d-1)-subsets of [g*TG+1, D) in colex order.
-#ifndef PCG_TG_MINB
-#define PCG_TG_MINB 4            // blocks per CU the depth-3/4 T-group kernel is register-sized for
-#endif
+// blocks per CU each depth's T-group kernel is register-sized for: 4 (128 VGPRs) for groups of
+// 4 and at depth 2; 2 (256 VGPRs, no spills) for depth 4's groups of 8
+__host__ __device__ constexpr int tg_minblocks(int DM) { return (tg_of_depth(DM) == 8 && DM >= 3) ? 2 : 4; }
 template <int DM>
-__global__ __launch_bounds__(256, (DM >= 3 ? PCG_TG_MINB : 4)) void k_level_lds_t(LevelArgs a) {
+__global__ __launch_bounds__(256, tg_minblocks(DM)) void k_level_lds_t(LevelArgs a) {
     constexpr int DT = DM - 1;
-    constexpr int TG = PCG_TGROUP;
+    constexpr int TG = tg_of_depth(DM);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x;
     const int bs = blockDim.x;
@@ -1122,8 +1125,10 @@ __global__ __launch_bounds__(256, (DM >= 3 ? PCG_TG_MINB : 4)) void k_level_lds_
         // candidates c in [cbase, min(t0, cbase + TG)): lanes of a wave share t0 except at pair
         // boundaries, so the wave's largest candidate count bounds the sweep uniformly
         const int nval = min(T[0] - cbase, TG);
-        const int nmax = __builtin_amdgcn_readfirstlane(
-            1 + (__ballot(nval >= 2) != 0) + (__ballot(nval >= 3) != 0) + (__ballot(nval >= 4) != 0));
+        int nmax_ = 1;
+#pragma unroll
+        for (int k = 2; k <= TG; ++k) nmax_ += (__ballot(nval >= k) != 0);
+        const int nmax = __builtin_amdgcn_readfirstlane(nmax_);
         unsigned long long Tmask = 0;
 #pragma unroll
         for (int i = 0; i < DT; ++i) Tmask |= 1ull << T[i];
@@ -1217,10 +1222,15 @@ __global__ __launch_bounds__(256, (DM >= 3 ? PCG_TG_MINB : 4)) void k_level_lds_
                 const bool own = (t < tx) && ((lm & Tmask) == Tmask);
                 const double *Mt = M + t * DS;
                 // the TG candidate operands M[t][cbase .. cbase+TG) are contiguous and 32-B aligned
-                // (DS % 4 == 0, cbase % 4 == 0): two 16-B LDS reads, broadcast across the lanes of
+                // (DS % 4 == 0, cbase % TG == 0): NC/2 16-B LDS reads, broadcast across the lanes of
                 // the wave that share the group
-                const double2 m01 = *reinterpret_cast<const double2 *>(Mt + cbase);
-                const double2 m23 = *reinterpret_cast<const double2 *>(Mt + cbase + 2);
+                double sc[TG];
+#pragma unroll
+                for (int q = 0; q < (NC + 1) / 2; ++q) {
+                    const double2 m = *reinterpret_cast<const double2 *>(Mt + cbase + 2 * q);
+                    sc[2 * q] = m.x;
+                    sc[2 * q + 1] = m.y;
+                }
                 double vT[DT];
                 double vv = 0.0, uv = 0.0;
     #pragma unroll
@@ -1238,7 +1248,6 @@ __global__ __launch_bounds__(256, (DM >= 3 ? PCG_TG_MINB : 4)) void k_level_lds_
                 const unsigned tb = ((unsigned)(t - cbase) < (unsigned)TG) ? (1u << (t - cbase)) : 0u;
                 const unsigned skip = own ? (unsigned)(lm >> cbase) : 0u;
                 const unsigned live = inTset ? 0u : (vmask & ~tb & ~skip);
-                double sc[TG] = {m01.x, m01.y, m23.x, m23.y};
                 // TG independent chains, interleaved
     #pragma unroll
                 for (int i = 0; i < DT; ++i)
@@ -1288,10 +1297,17 @@ __global__ __launch_bounds__(256, (DM >= 3 ? PCG_TG_MINB : 4)) void k_level_lds_
                 }
             }
         };
+        if constexpr (TG == 4) {
         if (nmax >= 4) sweep(std::integral_constant<int, 4>{});
         else if (nmax == 3) sweep(std::integral_constant<int, 3>{});
         else if (nmax == 2) sweep(std::integral_constant<int, 2>{});
         else sweep(std::integral_constant<int, 1>{});
+        } else {   // even counts: the slots past a lane's valid candidates are masked out of `live`
+        if (nmax > 6) sweep(std::integral_constant<int, 8>{});
+        else if (nmax > 4) sweep(std::integral_constant<int, 6>{});
+        else if (nmax > 2) sweep(std::integral_constant<int, 4>{});
+        else sweep(std::integral_constant<int, 2>{});
+        }
         tests += tcount;
         tcount = 0;
     }
@@ -1601,8 +1617,9 @@ size_t lds_tgroup_bytes(int D, int DM) {
 // lane tasks of k_level_lds_t for a node of degree D at depth d (see the kernel)
 uint64_t tgroup_tasks(const pcg_handle *h, int D, int d) {
     uint64_t acc = 0;
-    for (int g = 0; g * PCG_TGROUP <= D - d; ++g) {
-        const int Dp = D - g * PCG_TGROUP - 1;
+    const int TG = tg_of_depth(d);
+    for (int g = 0; g * TG <= D - d; ++g) {
+        const int Dp = D - g * TG - 1;
         if (Dp >= d - 1) acc += hbinom(h, Dp, d - 1);
     }
     return acc;
@@ -1874,7 +1891,7 @@ extern "C" int pcg_level_chunk_work(pcg_handle *h, int64_t *prefix_host, int64_t
             const int D = h->deg_h[x];
             const bool tg = (cls == 0) && h->tgroup;
             const uint64_t ns = tg ? tgroup_tasks(h, D, h->depth) : hbinom(h, D, h->depth);
-            const int64_t per_unit = (int64_t)(D - h->depth) * (tg ? PCG_TGROUP : 1);
+            const int64_t per_unit = (int64_t)(D - h->depth) * (tg ? tg_of_depth(h->depth) : 1);
             for (int64_t c = c0; c < c1; ++c) {
                 const uint64_t r0 = (uint64_t)(c - c0) * csz;
                 const uint64_t r1 = std::min<uint64_t>(r0 + csz, ns);
