@@ -46,7 +46,18 @@ constexpr int MODE_EXACT = 2;
 // candidates c per lane task in k_level_lds_t, per depth (measured, tools/variant_bench.sh):
 // groups of 8 halve the per-y shared work at depths 2 and 4 (depth 2 -28 %, depth 4 -3 % with
 // 2 waves/SIMD of 227 VGPRs); depth 3 keeps groups of 4 (4 waves/SIMD, 8 was +15 %)
-__host__ __device__ constexpr int tg_of_depth(int d) { return d == 3 ? 4 : 8; }
+#ifndef PCG_TG2
+#define PCG_TG2 8
+#endif
+#ifndef PCG_TG3
+#define PCG_TG3 4
+#endif
+#ifndef PCG_TG4
+#define PCG_TG4 8
+#endif
+__host__ __device__ constexpr int tg_of_depth(int d) { return d == 2 ? PCG_TG2 : (d == 3 ? PCG_TG3 : PCG_TG4); }
+static_assert((PCG_TG2 == 4 || PCG_TG2 == 8) && (PCG_TG3 == 4 || PCG_TG3 == 8) && (PCG_TG4 == 4 || PCG_TG4 == 8),
+              "k_level_lds_t candidate groups of 4 or 8");
 
 struct LevelArgs {
     const double *C;
@@ -1013,7 +1024,16 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
 // g covers c in [g*TG, g*TG+TG), T ranges over (d-1)-subsets of [g*TG+1, D) in colex order.
 // blocks per CU each depth's T-group kernel is register-sized for: 4 (128 VGPRs) for groups of
 // 4 and at depth 2; 2 (256 VGPRs, no spills) for depth 4's groups of 8
-__host__ __device__ constexpr int tg_minblocks(int DM) { return (tg_of_depth(DM) == 8 && DM >= 3) ? 2 : 4; }
+#ifndef PCG_MB2
+#define PCG_MB2 4
+#endif
+#ifndef PCG_MB3
+#define PCG_MB3 4
+#endif
+#ifndef PCG_MB4
+#define PCG_MB4 2
+#endif
+__host__ __device__ constexpr int tg_minblocks(int DM) { return DM == 2 ? PCG_MB2 : (DM == 3 ? PCG_MB3 : PCG_MB4); }
 template <int DM>
 __global__ __launch_bounds__(256, tg_minblocks(DM)) void k_level_lds_t(LevelArgs a) {
     constexpr int DT = DM - 1;
