@@ -24,6 +24,12 @@ namespace {
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 constexpr int TILE = 128;
+#ifndef PCG_K1_BLOCKS
+#define PCG_K1_BLOCKS 2048       // target k_xtx grid (tiles x split-K slabs)
+#endif
+#ifndef PCG_K1_MAXKS
+#define PCG_K1_MAXKS 16
+#endif
 #ifndef PCG_K1_KT
 #define PCG_K1_KT 8
 #endif
@@ -289,8 +295,9 @@ __global__ void k_gather_finish(const double *Gg, int64_t rows_per_rank, int n, 
 int split_k(int n, int64_t N, int64_t *kchunk_out) {
     const int T = (n + TILE - 1) / TILE;
     const int ntiles = T * (T + 1) / 2;
-    int ks = (int)std::min<int64_t>(std::max<int64_t>(1, (2048 + ntiles / 2) / ntiles), std::max<int64_t>(1, N / 512));
-    ks = std::min(ks, 16);
+    int ks = (int)std::min<int64_t>(std::max<int64_t>(1, (PCG_K1_BLOCKS + ntiles / 2) / ntiles),
+                                    std::max<int64_t>(1, N / 512));
+    ks = std::min(ks, PCG_K1_MAXKS);
     const int64_t kchunk = (((N + ks - 1) / ks) + KT - 1) / KT * KT;
     *kchunk_out = kchunk;
     return (int)((N + kchunk - 1) / kchunk);
