@@ -99,7 +99,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--full-p", action="store_true", help="compute every p-value (PCG_FLAG_FULL_P)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-depth", type=int, default=2, help="depths timed for the CPU port baseline")
+    ap.add_argument("--cpu-depth", type=int, default=3, help="depths timed for the CPU port baseline")
     ap.add_argument("--json-extra", action="store_true", help="print per-level detail to stderr")
     ap.add_argument("--workload", choices=["skeleton", "rq2"], default="skeleton",
                     help="skeleton: the headline line (config 5); rq2: every case of an Online-Boutique-shaped "
@@ -110,7 +110,7 @@ def parse():
 
 def cpu_baseline(X: np.ndarray, alpha: float, depth: int) -> dict:
     """Oracle C port (pc_oracle.c, OpenMP) on this host's cores: depths 0..depth of the same
-    workload (bounded sample: ~1.2e8 unique tests at depth 2), tests/s."""
+    workload (bounded sample: ~8.4e8 unique tests through depth 3, ~10 s on 16 threads), tests/s."""
     from oracle import cpc
     cores = len(os.sched_getaffinity(0))
     cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
