@@ -30,6 +30,12 @@ constexpr int TILE = 128;
 #ifndef PCG_K1_MAXKS
 #define PCG_K1_MAXKS 16
 #endif
+#ifndef PCG_K1_SLAB_BUDGET
+#define PCG_K1_SLAB_BUDGET (64ll << 20)   // bytes of split-K partial slabs beyond PCG_K1_MAXKS
+#endif
+#ifndef PCG_K1_MINROWS
+#define PCG_K1_MINROWS 32   // fewest rows per split-K slab
+#endif
 #ifndef PCG_K1_KT
 #define PCG_K1_KT 8
 #endif
@@ -214,11 +220,27 @@ __global__ __launch_bounds__(256) void k_normalize_tiles(const double *G, int64_
             live[q] = i < n && j < n && (bi != bj || rr <= c);
             g[q] = 0.0;
         }
-        for (int s = 0; s < ks; ++s) {
+        // four slabs' loads in flight at a time (small n splits K into up to 256 slabs); the adds
+        // stay in slab order
+        const int64_t off0 = (int64_t)(i0 + r4) * ldg + j0 + c;
+        int s = 0;
+        for (; s + 4 <= ks; s += 4) {
+            double v[4][RPT];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int q = 0; q < RPT; ++q)
+                    v[k][q] = live[q] ? G[(int64_t)(s + k) * slab_stride + off0 + (int64_t)4 * q * ldg] : 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int q = 0; q < RPT; ++q) g[q] += v[k][q];
+        }
+        for (; s < ks; ++s) {
             const double *Gs = G + (int64_t)s * slab_stride;
 #pragma unroll
             for (int q = 0; q < RPT; ++q)
-                if (live[q]) g[q] += Gs[(int64_t)(i0 + r4 + 4 * q) * ldg + j0 + c];
+                if (live[q]) g[q] += Gs[off0 + (int64_t)4 * q * ldg];
         }
 #pragma unroll
         for (int q = 0; q < RPT; ++q) t[r4 + 4 * q][c] = g[q];
@@ -295,9 +317,14 @@ __global__ void k_gather_finish(const double *Gg, int64_t rows_per_rank, int n, 
 int split_k(int n, int64_t N, int64_t *kchunk_out) {
     const int T = (n + TILE - 1) / TILE;
     const int ntiles = T * (T + 1) / 2;
+    // slab cap: PCG_K1_MAXKS for large n (each slab is a full n x n partial); small n (the RQ2
+    // cases: one tile, tens of variables) may split K much further so the grid is not a
+    // handful of blocks walking thousands of rows each
+    const int64_t slab_bytes = (int64_t)T * TILE * T * TILE * 8;
+    const int maxks = (int)std::min<int64_t>(256, std::max<int64_t>(PCG_K1_MAXKS, PCG_K1_SLAB_BUDGET / slab_bytes));
     int ks = (int)std::min<int64_t>(std::max<int64_t>(1, (PCG_K1_BLOCKS + ntiles / 2) / ntiles),
-                                    std::max<int64_t>(1, N / 512));
-    ks = std::min(ks, PCG_K1_MAXKS);
+                                    std::max<int64_t>(1, N / PCG_K1_MINROWS));
+    ks = std::min(ks, maxks);
     const int64_t kchunk = (((N + ks - 1) / ks) + KT - 1) / KT * KT;
     *kchunk_out = kchunk;
     return (int)((N + kchunk - 1) / kchunk);
