@@ -25,6 +25,7 @@ namespace {
 
 constexpr int PR_THREADS = 1024;
 constexpr int MAX_LEAVES = 1024;
+constexpr int PR_LDS_M = 1024;   // 5 * 1024 doubles = 40 KiB of dynamic LDS beside the 24 KiB static
 
 // numpy pairwise_sum leaf (n <= 128)
 __device__ double pw_leaf(const double *a, int n) {
@@ -120,6 +121,10 @@ __global__ __launch_bounds__(PR_THREADS) void k_pagerank(const double *A, int m,
     __shared__ Leaves L;
     __shared__ double leafsum[MAX_LEAVES];
     __shared__ int total_nnz;
+    // the five per-node vectors live in LDS for m <= PR_LDS_M (every iteration's sums and
+    // sweeps then avoid global round trips between barriers), else in the global scratch
+    extern __shared__ double pr_lds[];
+    if (m <= PR_LDS_M) work = pr_lds;
     double *b = work, *s = work + m, *s2 = work + 2 * m, *tmp = work + 3 * m, *inv = work + 4 * m;
     const int tid = threadIdx.x;
     if (tid == 0) pw_plan(L, m);
@@ -296,7 +301,9 @@ static int pagerank_common(pcg_handle *h, const double *A, const int32_t *indptr
     size_t offd = (size_t)(16 + sizeof(int32_t) * (m + 1 + nnz_cap) + 15) & ~(size_t)15;
     double *val = (double *)(base + offd);
     double *work = val + nnz_cap;
-    hipLaunchKernelGGL(k_pagerank, dim3(1), dim3(PR_THREADS), 0, h->stream, A, (int)m, lda, indptr, indices,
+    const size_t lds = m <= PR_LDS_M ? sizeof(double) * 5 * (size_t)m : 0;
+    const int threads = m <= 256 ? 256 : PR_THREADS;   // small graphs: cheaper block barriers
+    hipLaunchKernelGGL(k_pagerank, dim3(1), dim3(threads), lds, h->stream, A, (int)m, lda, indptr, indices,
                        data, damping, n_iter, tol, colptr, rowidx, val, work, scores, status);
     PCG_HIP(h, hipGetLastError());
     int st = 0;
