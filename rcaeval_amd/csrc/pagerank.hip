@@ -25,7 +25,7 @@ namespace {
 
 constexpr int PR_THREADS = 1024;
 constexpr int MAX_LEAVES = 1024;
-constexpr int PR_LDS_M = 1024;   // 5 * 1024 doubles = 40 KiB of dynamic LDS beside the 24 KiB static
+constexpr int PR_LDS_M = 768;    // 5 * 768 doubles + colptr = 33 KiB of dynamic LDS beside the ~25 KiB static (< 64 KiB)
 
 // numpy pairwise_sum leaf (n <= 128)
 __device__ double pw_leaf(const double *a, int n) {
@@ -124,7 +124,10 @@ __global__ __launch_bounds__(PR_THREADS) void k_pagerank(const double *A, int m,
     // the five per-node vectors live in LDS for m <= PR_LDS_M (every iteration's sums and
     // sweeps then avoid global round trips between barriers), else in the global scratch
     extern __shared__ double pr_lds[];
-    if (m <= PR_LDS_M) work = pr_lds;
+    if (m <= PR_LDS_M) {
+        work = pr_lds;
+        colptr = reinterpret_cast<int32_t *>(pr_lds + 5 * m);   // thread 0's prefix scan stays in LDS
+    }
     double *b = work, *s = work + m, *s2 = work + 2 * m, *tmp = work + 3 * m, *inv = work + 4 * m;
     const int tid = threadIdx.x;
     if (tid == 0) pw_plan(L, m);
@@ -301,7 +304,7 @@ static int pagerank_common(pcg_handle *h, const double *A, const int32_t *indptr
     size_t offd = (size_t)(16 + sizeof(int32_t) * (m + 1 + nnz_cap) + 15) & ~(size_t)15;
     double *val = (double *)(base + offd);
     double *work = val + nnz_cap;
-    const size_t lds = m <= PR_LDS_M ? sizeof(double) * 5 * (size_t)m : 0;
+    const size_t lds = m <= PR_LDS_M ? sizeof(double) * 5 * (size_t)m + sizeof(int32_t) * (size_t)(m + 1) : 0;
     const int threads = m <= 256 ? 256 : PR_THREADS;   // small graphs: cheaper block barriers
     hipLaunchKernelGGL(k_pagerank, dim3(1), dim3(threads), lds, h->stream, A, (int)m, lda, indptr, indices,
                        data, damping, n_iter, tol, colptr, rowidx, val, work, scores, status);
