@@ -58,6 +58,15 @@ def test_corr_matches_numpy(eng, n, N, seed, wl, wh, ep):
     np.testing.assert_allclose(C, ref, rtol=0, atol=2e-14)
 
 
+@pytest.mark.parametrize("n,N", [(44, 7000), (3, 40000), (130, 8193), (200, 33), (64, 32 * 256 + 5)])
+def test_corr_small_n_many_slabs(eng, n, N):
+    """Small n splits K into up to 256 slabs of >= 32 rows (RQ2-shaped cases); ragged N and the
+    single-slab tiny-N case included. Same tolerance as the numpy comparison above."""
+    X = synth.gaussian_sem(n, N, seed=n + N, w_low=0.1, w_high=0.5)
+    C = eng.corr(X).cpu().numpy()
+    np.testing.assert_allclose(C, np.corrcoef(X.T), rtol=0, atol=2e-14)
+
+
 @pytest.mark.parametrize("n,N,seed,wl,wh,ep", CASES)
 @pytest.mark.parametrize("flags", [0, _lib.PCG_FLAG_FULL_P | _lib.PCG_FLAG_RECORD])
 def test_skeleton_matches_oracle(eng, n, N, seed, wl, wh, ep, flags):
