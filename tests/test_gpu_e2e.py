@@ -25,6 +25,18 @@ def test_pagerank_bitwise_golden():
         np.testing.assert_array_equal(PageRank().fit_transform(g[f"A{i}"]), g[f"s{i}"])
 
 
+@pytest.mark.parametrize("m,n_iter", [(5, 10), (300, 10), (800, 30), (1100, 10)])
+def test_pagerank_sizes_vs_oracle(m, n_iter):
+    """Each layout of k_pagerank: LDS vectors with a 256-thread block (m <= 256), LDS with
+    1024 threads (m <= 768), global scratch (m > 768) — bitwise the scipy/numpy oracle."""
+    from oracle import pagerank as opr
+    from rcaeval_amd.graph_heads.page_rank import PageRank
+    rng = np.random.default_rng(m)
+    A = (rng.random((m, m)) < min(1.0, 6.0 / m)) * rng.random((m, m))
+    A[rng.integers(0, m, size=max(1, m // 10))] = 0.0   # dangling nodes
+    np.testing.assert_array_equal(PageRank(n_iter=n_iter).fit_transform(A), opr.pagerank(A, n_iter=n_iter))
+
+
 def test_pagerank_empty_input_raises():
     from rcaeval_amd.graph_heads.page_rank import PageRank
     with pytest.raises(ValueError):
