@@ -30,50 +30,73 @@ def bytes_per_test(d: int) -> int:
     return 8 * (d + 2) * (d + 3) // 2 + 4 * (d + 2) + 8
 
 
-def flops_per_test(d: int) -> float:
-    """(d+2)^3/3 + ~40 (factor + Fisher-z tail) per test."""
-    return (d + 2) ** 3 / 3.0 + 40.0
-
-
-def pmc_traffic(kernel_prefix: str):  # exact rocprof kernel name (template args kept)
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC pass
-    (profiles/*_pmc_summary.json, same bench command): FETCH_SIZE (KB, x2 for the gfx950
-    half-count of wide reads, MI355X_MICROARCH.md §HBM) + WRITE_SIZE (KB). None if absent."""
+def _pmc(kernel: str):
+    """Per-dispatch PMC counters of ``kernel`` (rocprof name, template args kept) from the latest
+    committed rocprofv3 pass over this same bench command (profiles/r*_pmc_summary.json)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
     if not files:
-        return None, None
-    data = json.load(open(files[-1]))
-    for name, ctr in data.items():
-        if name == kernel_prefix and "FETCH_SIZE" in ctr and "WRITE_SIZE" in ctr:
-            fetch = ctr["FETCH_SIZE"]["per_dispatch_mean"] * 1024.0 * 2.0
-            write = ctr["WRITE_SIZE"]["per_dispatch_mean"] * 1024.0
-            return fetch + write, os.path.basename(files[-1])
-    return None, None
-
-
-def valu_issue_floor(kernel: str, tests: int):
-    """The resource that actually binds the CI-test kernels (their operands live in LDS, so the
-    §8(d) HBM-byte model overstates traffic ~10^3x): VALU issue. From the committed PMC pass
-    (same kernel, same workload): wave-instructions per launch, fp64 ones at 4 SIMD-cycles per
-    wave64 (78.6 TF/s fp64 = 16 lanes/cycle/SIMD) and the rest at 2 (32 lanes/cycle,
-    MI355X_MICROARCH.md), spread over 1024 SIMDs at 2.4 GHz. None if the pass is absent."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
-    if not files:
-        return None
+        return {}, None
     data = json.load(open(files[-1]))
     ctr = data.get(kernel, {})
+    return {k: v["per_dispatch_mean"] for k, v in ctr.items()}, os.path.basename(files[-1])
+
+
+def roofline_of(kernel: str, tests: int, d: int, k_ms: float) -> dict:
+    """Roofline of the dominant CI-test kernel.
+
+    Binding resource: VALU issue. The kernel stages each node's correlation block in LDS, so
+    its HBM traffic (PMC) is ~10^3 below SURVEY §8(d)'s per-test byte model and HBM is not what
+    binds. Issue floor, from the committed PMC pass of the same kernel and workload: fp64
+    wave-instructions at 4 SIMD-cycles (78.6 TF/s fp64 = 16 FMA lanes/cycle/SIMD) and every
+    other VALU wave-instruction at 2 (32 lanes/cycle, MI355X_MICROARCH.md), over 1024 SIMDs at
+    the 2.4 GHz max clock. achieved = the issue cycles the launch needs / its live duration;
+    frac = floor / live duration. The HBM figures (measured and §8(d) algorithmic) and the
+    fp64 rate are secondary keys."""
+    ctr, src = _pmc(kernel)
+    peak_gcyc = 1024 * 2.4   # G SIMD-cycles/s
+    line = {"bound": "valu", "unit": "G SIMD-issue-cycles/s", "peak": peak_gcyc, "achieved": None,
+            "frac": None, "traffic": None, "kernel": kernel, "kernel_ms": k_ms, "pmc_source": src}
+    alg = tests * bytes_per_test(d)
+    sec = {"hbm_contract_bytes_per_test": bytes_per_test(d),
+           "hbm_contract_gbs": alg / (k_ms / 1e3) / 1e9 if k_ms > 0 else None,
+           "note": "SURVEY 8(d) per-test byte model; operands are LDS-resident, so it is not a traffic figure"}
     need = ("SQ_INSTS_VALU", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64")
-    if not all(k in ctr for k in need):
-        return None
-    valu = ctr["SQ_INSTS_VALU"]["per_dispatch_mean"]
-    f64 = sum(ctr[k]["per_dispatch_mean"] for k in need[1:])
-    cycles = 4.0 * f64 + 2.0 * (valu - f64)
-    floor_ms = cycles / (1024 * 2.4e9) * 1e3
-    return {"resource": "VALU issue", "valu_instr_per_launch": valu, "fp64_instr_per_launch": f64,
-            "valu_instr_per_64_tests": valu / (tests / 64.0) if tests else None,
-            "issue_floor_ms": floor_ms, "source": os.path.basename(files[-1])}
+    if k_ms > 0 and all(k in ctr for k in need):
+        valu = ctr["SQ_INSTS_VALU"]
+        f64 = sum(ctr[k] for k in need[1:])
+        cycles = 4.0 * f64 + 2.0 * (valu - f64)
+        floor_ms = cycles / (peak_gcyc * 1e9) * 1e3
+        line["achieved"] = cycles / (k_ms / 1e3) / 1e9
+        line["frac"] = floor_ms / k_ms
+        line["issue_floor_ms"] = floor_ms
+        sec["valu_instr_per_64_tests"] = valu / (tests / 64.0) if tests else None
+        sec["fp64_instr_per_64_tests"] = f64 / (tests / 64.0) if tests else None
+        if "SQ_INSTS_VALU_FLOPS_FP64" in ctr:     # per wave-instruction flops -> x64 lanes
+            tf = 64.0 * ctr["SQ_INSTS_VALU_FLOPS_FP64"] / (k_ms / 1e3) / 1e12
+            sec["fp64_tflops_executed"] = tf
+            sec["fp64_frac"] = tf / FP64_PEAK_TFLOPS
+    if k_ms > 0 and "FETCH_SIZE" in ctr and "WRITE_SIZE" in ctr:
+        # FETCH_SIZE counts KiB with gfx950's wide reads at half weight (MI355X_MICROARCH.md HBM
+        # section): x2; WRITE_SIZE KiB as is
+        traffic = ctr["FETCH_SIZE"] * 1024.0 * 2.0 + ctr["WRITE_SIZE"] * 1024.0
+        line["traffic"] = traffic
+        sec["hbm_measured_gbs"] = traffic / (k_ms / 1e3) / 1e9
+        sec["hbm_measured_frac"] = sec["hbm_measured_gbs"] / HBM_PEAK_GBS
+    line["secondary"] = sec
+    return line
+
+
+def k1_roofline(n: int, N: int, corr_ms: float) -> dict:
+    """K1 (np.corrcoef) on fp64 MFMA: 2 N n^2 algorithmic flop; the kernel multiplies the
+    upper-triangle 128 x 128 tiles only (T(T+1)/2 tiles, T = ceil(n/128))."""
+    T = (n + 127) // 128
+    mfma_flop = T * (T + 1) // 2 * 128 * 128 * 2.0 * N
+    return {"bound": "mfma", "unit": "TFLOP/s", "peak": FP64_PEAK_TFLOPS, "ms": corr_ms,
+            "achieved_algorithmic": 2.0 * N * n * n / (corr_ms / 1e3) / 1e12,
+            "achieved_executed": mfma_flop / (corr_ms / 1e3) / 1e12,
+            "frac": mfma_flop / (corr_ms / 1e3) / 1e12 / FP64_PEAK_TFLOPS,
+            "what": "pcg_corr end to end (column means, split-K k_xtx, fused normalisation)"}
 
 
 def dominant_kernel(d: int, full_p: bool) -> str:
@@ -108,21 +131,41 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(X: np.ndarray, alpha: float, depth: int) -> dict:
-    """Oracle C port (pc_oracle.c, OpenMP) on this host's cores: depths 0..depth of the same
-    workload (bounded sample: ~8.4e8 unique tests through depth 3, ~10 s on 16 threads), tests/s."""
+def cpu_baseline(X: np.ndarray, alpha: float, depth: int, gpu_tests: list, gpu_removed: np.ndarray,
+                 stride: int = 20) -> dict:
+    """Oracle C port (pc_oracle.c: LU per test, OpenMP) on this host's cores, on the SAME depth
+    mix as the GPU line: depths 0..``depth`` run in full (their removals and per-level test
+    counts are checked against the GPU's), each deeper depth timed on a node sample (every
+    ``stride``-th node's visits on the graph at the start of that depth — the GPU's, which the
+    full-size parity test pins to the oracle's). value = all of the GPU line's unique tests
+    over the CPU time projected from the per-depth rates."""
     from oracle import cpc
     cores = len(os.sched_getaffinity(0))
     cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+    N = X.shape[0]
     C = np.corrcoef(X.T)
     t0 = time.perf_counter()
-    ref = cpc.skeleton(C, X.shape[0], alpha=alpha, max_depth=depth, want_union=False, nthreads=cores)
-    dt = time.perf_counter() - t0
-    tests = int(sum(ref.tests))
-    return {"value": tests / dt, "unit": "CI tests/s", "cores": cores, "kind": "port",
-            "sample": f"same SEM, depths 0..{depth} in full ({tests} unique tests, {dt:.2f} s), "
-                      f"oracle/pc_oracle.c (LU per test, OpenMP)",
-            "seconds": dt, "tests": tests, "_ref": ref}
+    ref = cpc.skeleton(C, N, alpha=alpha, max_depth=depth, want_union=False, nthreads=cores)
+    full_s = time.perf_counter() - t0
+    per_level = []
+    est_s = 0.0
+    for d, tests in enumerate(gpu_tests):
+        if d < ref.levels:
+            rate = ref.tests[d] / ref.secs[d]
+            per_level.append({"depth": d, "tests": ref.tests[d], "seconds": ref.secs[d], "rate": rate,
+                              "how": "full depth"})
+        else:
+            t_s, sec = cpc.level_sample(C, N, gpu_removed, d, 0, stride, alpha=alpha, nthreads=cores)
+            rate = t_s / sec
+            per_level.append({"depth": d, "tests": t_s, "seconds": sec, "rate": rate,
+                              "how": f"nodes x = 0 mod {stride}"})
+        est_s += tests / rate
+    total = int(sum(gpu_tests))
+    return {"value": total / est_s, "unit": "CI tests/s", "cores": cores, "kind": "port",
+            "sample": f"same SEM and depth mix as the GPU line: depths 0..{ref.levels - 1} in full "
+                      f"({sum(ref.tests)} unique tests, {full_s:.1f} s), deeper depths on every {stride}-th "
+                      f"node's visits; CPU time projected per depth = {est_s:.1f} s for {total} tests",
+            "per_level": per_level, "projected_seconds": est_s, "_ref": ref}
 
 
 def cpu_reference_equiv(X: np.ndarray, ref, budget_s: float = 4.0) -> dict:
@@ -312,18 +355,24 @@ def main():
     value = tests_total / (ms / 1000.0)
 
     # dominant kernel: the CI-test kernel of the deepest, largest level
-    L = st["levels"]
     dmax = int(np.argmax(st["tests"]))
     k_ms = st["kernel_ms"][dmax]
-    alg_bytes = st["tests"][dmax] * bytes_per_test(dmax)
-    alg_flops = st["tests"][dmax] * flops_per_test(dmax)
-    ach_gbs = alg_bytes / (k_ms / 1000.0) / 1e9 if k_ms > 0 else 0.0
-    ach_tf = alg_flops / (k_ms / 1000.0) / 1e12 if k_ms > 0 else 0.0
     kname = dominant_kernel(dmax, args.full_p)
-    traffic, traffic_src = pmc_traffic(kname)
-    binding = valu_issue_floor(kname, int(st["tests"][dmax]))
-    if binding is not None:
-        binding["frac"] = binding["issue_floor_ms"] / k_ms if k_ms > 0 else None
+    roof = roofline_of(kname, int(st["tests"][dmax]), dmax, k_ms)
+    corr_med = float(np.median([1000 * t for n_, t in phases if n_ == "corr"][args.warmup:] or [0.0]))
+    roof["k1"] = k1_roofline(args.n, args.samples, corr_med) if corr_med > 0 else None
+
+    # the same skeleton with every p-value computed (PCG_FLAG_FULL_P), once, after the timed
+    # steps: the reference-arithmetic mode beside the threshold headline
+    full_p = None
+    if not args.full_p and world == 1:
+        C = eng.corr(Xd)
+        o = eng.skeleton(C, args.samples, alpha=args.alpha, max_depth=args.max_depth, flags=_lib.PCG_FLAG_FULL_P)
+        fp_ms = float(sum(o.stats["level_ms"]))
+        same = bool(np.array_equal(o.removed_level, out.removed_level)) and o.stats["tests"] == st["tests"]
+        full_p = {"skeleton_device_ms": fp_ms, "tests_per_s": sum(o.stats["tests"]) / (fp_ms / 1e3),
+                  "kernel_ms_per_level": [round(v, 3) for v in o.stats["kernel_ms"]],
+                  "same_skeleton_as_threshold": same}
 
     if rank == 0:
         line = {
@@ -345,16 +394,11 @@ def main():
             "kernel_ms_per_level": [round(v, 3) for v in st["kernel_ms"]],
             "level_ms": [round(v, 3) for v in st["level_ms"]],
             "edges_after": st["edges_after"], "exact_path": st["exact"], "near_alpha": st["near_alpha"],
-            "roofline": {"bound": "hbm", "achieved": ach_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": ach_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_source": traffic_src,
-                         "kernel": kname, "kernel_ms": k_ms,
-                         "algorithmic_bytes_per_test": bytes_per_test(dmax),
-                         "fp64_tflops_algorithmic": ach_tf, "fp64_peak_tflops": FP64_PEAK_TFLOPS,
-                         "binding": binding},
+            "roofline": roof,
+            "full_p": full_p,
         }
         if not args.no_cpu_baseline and world == 1:
-            cb = cpu_baseline(X, args.alpha, args.cpu_depth)
+            cb = cpu_baseline(X, args.alpha, args.cpu_depth, st["tests"], out.removed_level)
             ref = cb.pop("_ref")
             # parity of the timed GPU run on the CPU-sampled depths
             Lc = ref.levels

@@ -92,6 +92,9 @@ const char *pcg_last_error(pcg_handle *h);
 int pcg_set_stream(pcg_handle *h, void *hip_stream);
 /* Launch-shape knobs (0 = default). */
 int pcg_set_capacity(pcg_handle *h, int64_t record_capacity, int64_t deferred_capacity);
+/* PCG_FLAG_RECORD on a fixed sample (full-size parity runs): keep only the unique tests whose
+ * canonical pair (a < b) has (a*n + b) % modulus == residue; modulus 0 or 1 = every test.  */
+int pcg_set_record_sample(pcg_handle *h, int64_t modulus, int64_t residue);
 
 /* ---- K1: correlation -------------------------------------------------------------
  * Replaces FisherZ.__init__'s `np.corrcoef(data.T)` [U]: column means,

@@ -18,7 +18,7 @@ _LIB = None
 class OrcStats(ctypes.Structure):
     _fields_ = [("tests", ctypes.c_int64 * 32), ("calls", ctypes.c_int64 * 32),
                 ("indep", ctypes.c_int64 * 32), ("levels", ctypes.c_int32),
-                ("error", ctypes.c_int32)]
+                ("error", ctypes.c_int32), ("secs", ctypes.c_double * 32)]
 
 
 REC_DTYPE = np.dtype([("a", np.int32), ("b", np.int32), ("d", np.int32),
@@ -39,11 +39,14 @@ def lib():
         _LIB = ctypes.CDLL(build())
         P = ctypes.c_void_p
         _LIB.orc_skeleton.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int,
-                                      P, P, P, P, ctypes.c_int64, P, P, ctypes.c_int]
+                                      P, P, P, P, ctypes.c_int64, P, P, ctypes.c_int64, P, P, ctypes.c_int]
         _LIB.orc_skeleton.restype = ctypes.c_int
         _LIB.orc_fisherz_batch.argtypes = [P, ctypes.c_int, ctypes.c_int, P, P, ctypes.c_int,
                                            ctypes.c_int64, P, P]
         _LIB.orc_corrcoef.argtypes = [P, ctypes.c_int64, ctypes.c_int, P]
+        _LIB.orc_level_sample.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_double, P, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P]
+        _LIB.orc_level_sample.restype = ctypes.c_int
     return _LIB
 
 
@@ -57,11 +60,13 @@ class CSkeleton:
     deg_at_level: np.ndarray     # levels x n int32
     side_union: np.ndarray       # n x n x W uint64 or None
     records: np.ndarray          # REC_DTYPE or None
+    near_alpha: np.ndarray       # REC_DTYPE: every unique test with |p - alpha| < 1e-9
     tests: list
     calls: list
     indep: list
     levels: int
     error: int
+    secs: list = None            # wall seconds per depth
 
     @property
     def adj(self) -> np.ndarray:
@@ -79,16 +84,37 @@ def skeleton(C: np.ndarray, N: int, alpha: float = 0.05, max_depth: int = -1,
     su = np.empty((n, n, W), np.uint64) if want_union else None
     rec = np.empty(record_cap, REC_DTYPE) if record_cap else None
     cnt = np.zeros(1, np.int64)
+    near_cap = 1 << 16
+    near = np.empty(near_cap, REC_DTYPE)
+    ncnt = np.zeros(1, np.int64)
     st = OrcStats()
     lib().orc_skeleton(_p(C), n, int(N), float(alpha), int(max_depth), _p(rl), _p(deg), _p(su),
-                       _p(rec), int(record_cap), _p(cnt), ctypes.byref(st), int(nthreads))
+                       _p(rec), int(record_cap), _p(cnt), _p(near), near_cap, _p(ncnt),
+                       ctypes.byref(st), int(nthreads))
     L = st.levels
     if rec is not None:
         if cnt[0] > record_cap:
             raise RuntimeError(f"record buffer overflow: {cnt[0]} > {record_cap}")
         rec = rec[: cnt[0]]
-    return CSkeleton(rl, deg[:L].copy(), su, rec, list(st.tests[:L]), list(st.calls[:L]),
-                     list(st.indep[:L]), L, st.error)
+    if ncnt[0] > near_cap:
+        raise RuntimeError(f"near-alpha buffer overflow: {ncnt[0]} > {near_cap}")
+    return CSkeleton(rl, deg[:L].copy(), su, rec, near[: ncnt[0]].copy(), list(st.tests[:L]),
+                     list(st.calls[:L]), list(st.indep[:L]), L, st.error, list(st.secs[:L]))
+
+
+def level_sample(C: np.ndarray, N: int, removed_level: np.ndarray, d: int, x0: int = 0, xstep: int = 1,
+                 alpha: float = 0.05, nthreads: int = 0):
+    """Time depth ``d``'s visits of nodes x0, x0+xstep, ... on the graph at the start of
+    depth d (pairs with removed_level -1 or >= d): (unique tests, seconds)."""
+    C = np.ascontiguousarray(C, dtype=np.float64)
+    rl = np.ascontiguousarray(removed_level, dtype=np.int8)
+    tests = np.zeros(1, np.int64)
+    secs = np.zeros(1, np.float64)
+    err = lib().orc_level_sample(_p(C), C.shape[0], int(N), float(alpha), _p(rl), int(d), int(x0), int(xstep),
+                                 int(nthreads), _p(tests), _p(secs))
+    if err:
+        raise RuntimeError(f"orc_level_sample error {err}")
+    return int(tests[0]), float(secs[0])
 
 
 def corrcoef(data: np.ndarray) -> np.ndarray:
@@ -97,3 +123,15 @@ def corrcoef(data: np.ndarray) -> np.ndarray:
     C = np.empty((n, n), np.float64)
     lib().orc_corrcoef(_p(X), N, n, _p(C))
     return C
+
+
+def fisherz_batch(C: np.ndarray, N: int, ab: np.ndarray, S: np.ndarray, d: int):
+    """FisherZ p of explicit canonical tests (a < b, S sorted, all of size d): (p, err)."""
+    C = np.ascontiguousarray(C, dtype=np.float64)
+    ab = np.ascontiguousarray(ab, dtype=np.int32).reshape(-1, 2)
+    count = len(ab)
+    S = np.ascontiguousarray(S, dtype=np.int32).reshape(count, max(d, 1))
+    p = np.empty(count, np.float64)
+    err = np.empty(count, np.int32)
+    lib().orc_fisherz_batch(_p(C), C.shape[0], int(N), _p(ab), _p(S), int(d), count, _p(p), _p(err))
+    return p, err

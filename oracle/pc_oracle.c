@@ -24,6 +24,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -36,6 +37,7 @@ typedef struct {
     int64_t indep[32];   /* unique tests with p > alpha       */
     int32_t levels;      /* number of depths run              */
     int32_t error;       /* 0 ok, 1 singular, 2 math domain   */
+    double secs[32];     /* wall seconds per depth            */
 } orc_stats;
 
 typedef struct {         /* one unique test (record mode) */
@@ -128,6 +130,121 @@ double orc_fisherz(const double *C, int n, int N, int a, int b, const int *S, in
 
 static inline int has_bit(const uint64_t *row, int j) { return (row[j >> 6] >> (j & 63)) & 1; }
 
+typedef struct {            /* one depth of the x-side loop (SkeletonDiscovery.py:77-136) */
+    const double *C;
+    int n, N, W, d;
+    double alpha;
+    const uint64_t *adj;    /* n x W adjacency at the start of the depth */
+    const int32_t *deg, *nbr;
+    uint8_t *rm;            /* n x n removal flags (NULL: count only) */
+    uint64_t *side_union;
+    orc_record *rec, *nearl;
+    int64_t rec_cap, near_cap, *rec_count, *near_count;
+    int x0, xstep;          /* nodes x = x0, x0 + xstep, ... (a node sample when xstep > 1) */
+} orc_level;
+
+/* Runs the visits of the selected nodes; returns the error code (0 ok). */
+static int level_pass(const orc_level *L, int64_t *tests_out, int64_t *calls_out, int64_t *indep_out) {
+    const int n = L->n, W = L->W, d = L->d;
+    int64_t tests = 0, calls = 0, indep = 0;
+    volatile int error = 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : tests, calls, indep)
+    for (int x = L->x0; x < n; x += L->xstep) {
+        const int D = L->deg[x];
+        if (D < d - 1) continue;
+        const int32_t *nx = L->nbr + (size_t)x * n;
+        int idx[ORC_MAXD + 1], S[ORC_MAXD + 1];
+        for (int yi = 0; yi < D; ++yi) {
+            const int y = nx[yi];
+            const uint64_t *ady = L->adj + (size_t)y * W;
+            /* combinations of nx \ {y} of size d, lexicographic */
+            const int M = D - 1;
+            if (M < d) continue;
+            for (int k = 0; k < d; ++k) idx[k] = k;
+            for (;;) {
+                int in_y = 1;
+                for (int k = 0; k < d; ++k) {
+                    int li = idx[k] < yi ? idx[k] : idx[k] + 1;
+                    S[k] = nx[li];
+                    if (!has_bit(ady, S[k])) in_y = 0;
+                }
+                calls++;
+                if (!(y < x && in_y)) {
+                    int a = x < y ? x : y, b = x < y ? y : x, err;
+                    double p = orc_fisherz(L->C, n, L->N, a, b, S, d, &err);
+                    if (err) error = err;
+                    tests++;
+                    if (L->rec) {
+                        int64_t slot = __atomic_fetch_add(L->rec_count, 1, __ATOMIC_RELAXED);
+                        if (slot < L->rec_cap) {
+                            orc_record *r = L->rec + slot;
+                            r->a = a; r->b = b; r->d = d;
+                            for (int k = 0; k < 12; ++k) r->s[k] = k < d ? S[k] : -1;
+                            r->p = p;
+                        }
+                    }
+                    if (L->nearl && fabs(p - L->alpha) < 1e-9) {
+                        int64_t slot = __atomic_fetch_add(L->near_count, 1, __ATOMIC_RELAXED);
+                        if (slot < L->near_cap) {
+                            orc_record *r = L->nearl + slot;
+                            r->a = a; r->b = b; r->d = d;
+                            for (int k = 0; k < 12; ++k) r->s[k] = k < d ? S[k] : -1;
+                            r->p = p;
+                        }
+                    }
+                    if (p > L->alpha) {
+                        indep++;
+                        if (L->rm) {
+                            __atomic_store_n(&L->rm[(size_t)x * n + y], 1, __ATOMIC_RELAXED);
+                            __atomic_store_n(&L->rm[(size_t)y * n + x], 1, __ATOMIC_RELAXED);
+                        }
+                        if (L->side_union) {
+                            uint64_t *ux = L->side_union + ((size_t)x * n + y) * W;
+                            uint64_t *uy = L->side_union + ((size_t)y * n + x) * W;
+                            for (int k = 0; k < d; ++k) {
+                                __atomic_fetch_or(&ux[S[k] >> 6], 1ull << (S[k] & 63), __ATOMIC_RELAXED);
+                                if (in_y) __atomic_fetch_or(&uy[S[k] >> 6], 1ull << (S[k] & 63), __ATOMIC_RELAXED);
+                            }
+                        }
+                    }
+                }
+                /* next combination */
+                int k = d - 1;
+                while (k >= 0 && idx[k] == M - d + k) --k;
+                if (k < 0) break;
+                idx[k]++;
+                for (int j = k + 1; j < d; ++j) idx[j] = idx[j - 1] + 1;
+            }
+        }
+    }
+    *tests_out = tests;
+    *calls_out = calls;
+    *indep_out = indep;
+    return error;
+}
+
+static double now_s(void) {
+#ifdef _OPENMP
+    return omp_get_wtime();
+#else
+    return (double)clock() / CLOCKS_PER_SEC;
+#endif
+}
+
+/* degrees + ascending neighbour lists of the adjacency bitmask; returns the max degree */
+static int build_lists(const uint64_t *adj, int n, int W, int32_t *deg, int32_t *nbr) {
+    int maxdeg = 0;
+    for (int x = 0; x < n; ++x) {
+        int c = 0;
+        for (int w = 0; w < W; ++w) c += __builtin_popcountll(adj[(size_t)x * W + w]);
+        deg[x] = c;
+        if (c > maxdeg) maxdeg = c;
+        int k = 0;
+        for (int y = 0; y < n; ++y) if (has_bit(adj + (size_t)x * W, y)) nbr[(size_t)x * n + k++] = y;
+    }
+    return maxdeg;
+}
+
 /*
  * Stable skeleton. C: n x n row-major correlation. Outputs:
  *   removed_level[n*n]   int8, -1 = survives, else depth at which the edge was removed
@@ -135,11 +252,14 @@ static inline int has_bit(const uint64_t *row, int j) { return (row[j >> 6] >> (
  *   side_union[n*n*W]    optional (NULL ok), W = ceil(n/64): for a removed pair (x,y) the
  *                        union of independent S on x's side at the removal depth
  *   rec/rec_cap/rec_count optional: every unique test (record mode)
- * max_depth < 0: unlimited. nthreads <= 0: all.
+ *   nearl/near_cap/near_count optional: every unique test with |p - alpha| < 1e-9 (the tests
+ *                        whose decision north_star allows to differ; enumerated like the engine)
+ * max_depth < 0: unlimited. nthreads <= 0: all. st->secs: wall time per depth.
  */
 int orc_skeleton(const double *C, int n, int N, double alpha, int max_depth,
                  int8_t *removed_level, int32_t *deg_at_level, uint64_t *side_union,
                  orc_record *rec, int64_t rec_cap, int64_t *rec_count,
+                 orc_record *nearl, int64_t near_cap, int64_t *near_count,
                  orc_stats *st, int nthreads) {
     const int W = (n + 63) / 64;
     uint64_t *adj = (uint64_t *)calloc((size_t)n * W, sizeof(uint64_t));
@@ -154,88 +274,25 @@ int orc_skeleton(const double *C, int n, int N, double alpha, int max_depth,
             if (x != y) adj[(size_t)x * W + (y >> 6)] |= 1ull << (y & 63);
     if (side_union) memset(side_union, 0, sizeof(uint64_t) * (size_t)n * n * W);
     if (rec_count) *rec_count = 0;
+    if (near_count) *near_count = 0;
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #endif
-    int depth = -1;
-    volatile int error = 0;
+    int depth = -1, error = 0;
     for (;;) {
-        int maxdeg = 0;
-        for (int x = 0; x < n; ++x) {
-            int c = 0;
-            for (int w = 0; w < W; ++w) c += __builtin_popcountll(adj[(size_t)x * W + w]);
-            deg[x] = c;
-            if (c > maxdeg) maxdeg = c;
-            int k = 0;
-            for (int y = 0; y < n; ++y) if (has_bit(adj + (size_t)x * W, y)) nbr[(size_t)x * n + k++] = y;
-        }
+        const int maxdeg = build_lists(adj, n, W, deg, nbr);
         if (!(maxdeg - 1 > depth)) break;
         if (max_depth >= 0 && depth >= max_depth) break;
         ++depth;
         if (depth >= 32 || depth > ORC_MAXD) break;
         if (deg_at_level) memcpy(deg_at_level + (size_t)depth * n, deg, sizeof(int32_t) * n);
         memset(rm, 0, (size_t)n * n);
-        int64_t tests = 0, calls = 0, indep = 0;
-        const int d = depth;
-#pragma omp parallel for schedule(dynamic, 1) reduction(+ : tests, calls, indep)
-        for (int x = 0; x < n; ++x) {
-            const int D = deg[x];
-            if (D < d - 1) continue;
-            const int32_t *nx = nbr + (size_t)x * n;
-            int idx[ORC_MAXD + 1], S[ORC_MAXD + 1], cand[1];
-            (void)cand;
-            for (int yi = 0; yi < D; ++yi) {
-                const int y = nx[yi];
-                const uint64_t *ady = adj + (size_t)y * W;
-                /* combinations of nx \ {y} of size d, lexicographic */
-                const int M = D - 1;
-                if (M < d) continue;
-                for (int k = 0; k < d; ++k) idx[k] = k;
-                for (;;) {
-                    int in_y = 1;
-                    for (int k = 0; k < d; ++k) {
-                        int li = idx[k] < yi ? idx[k] : idx[k] + 1;
-                        S[k] = nx[li];
-                        if (!has_bit(ady, S[k])) in_y = 0;
-                    }
-                    calls++;
-                    if (!(y < x && in_y)) {
-                        int a = x < y ? x : y, b = x < y ? y : x, err;
-                        double p = orc_fisherz(C, n, N, a, b, S, d, &err);
-                        if (err) error = err;
-                        tests++;
-                        if (rec) {
-                            int64_t slot = __atomic_fetch_add(rec_count, 1, __ATOMIC_RELAXED);
-                            if (slot < rec_cap) {
-                                orc_record *r = rec + slot;
-                                r->a = a; r->b = b; r->d = d;
-                                for (int k = 0; k < 12; ++k) r->s[k] = k < d ? S[k] : -1;
-                                r->p = p;
-                            }
-                        }
-                        if (p > alpha) {
-                            indep++;
-                            __atomic_store_n(&rm[(size_t)x * n + y], 1, __ATOMIC_RELAXED);
-                            __atomic_store_n(&rm[(size_t)y * n + x], 1, __ATOMIC_RELAXED);
-                            if (side_union) {
-                                uint64_t *ux = side_union + ((size_t)x * n + y) * W;
-                                uint64_t *uy = side_union + ((size_t)y * n + x) * W;
-                                for (int k = 0; k < d; ++k) {
-                                    __atomic_fetch_or(&ux[S[k] >> 6], 1ull << (S[k] & 63), __ATOMIC_RELAXED);
-                                    if (in_y) __atomic_fetch_or(&uy[S[k] >> 6], 1ull << (S[k] & 63), __ATOMIC_RELAXED);
-                                }
-                            }
-                        }
-                    }
-                    /* next combination */
-                    int k = d - 1;
-                    while (k >= 0 && idx[k] == M - d + k) --k;
-                    if (k < 0) break;
-                    idx[k]++;
-                    for (int j = k + 1; j < d; ++j) idx[j] = idx[j - 1] + 1;
-                }
-            }
-        }
+        orc_level L = {C, n, N, W, depth, alpha, adj, deg, nbr, rm, side_union, rec, nearl,
+                       rec_cap, near_cap, rec_count, near_count, 0, 1};
+        const double t0 = now_s();
+        int64_t tests, calls, indep;
+        error = level_pass(&L, &tests, &calls, &indep);
+        st->secs[depth] = now_s() - t0;
         st->tests[depth] = tests;
         st->calls[depth] = calls;
         st->indep[depth] = indep;
@@ -251,6 +308,36 @@ int orc_skeleton(const double *C, int n, int N, double alpha, int max_depth,
     st->error = error;
     free(adj); free(deg); free(nbr); free(rm);
     return error ? 1 : 0;
+}
+
+/* CPU-baseline sample of one depth: the visits of nodes x0, x0+xstep, ... at depth d on the
+ * adjacency {(x, y): removed_level[x,y] == -1 or >= d} (the graph at the start of depth d).
+ * Counts only (no removal, no sepsets). Returns the error code; tests/seconds out. */
+int orc_level_sample(const double *C, int n, int N, double alpha, const int8_t *removed_level, int d,
+                     int x0, int xstep, int nthreads, int64_t *tests_out, double *seconds_out) {
+    const int W = (n + 63) / 64;
+    uint64_t *adj = (uint64_t *)calloc((size_t)n * W, sizeof(uint64_t));
+    int32_t *deg = (int32_t *)malloc(sizeof(int32_t) * n);
+    int32_t *nbr = (int32_t *)malloc(sizeof(int32_t) * (size_t)n * n);
+    if (!adj || !deg || !nbr) return -1;
+    for (int x = 0; x < n; ++x)
+        for (int y = 0; y < n; ++y) {
+            const int8_t r = removed_level[(size_t)x * n + y];
+            if (x != y && (r < 0 || r >= d)) adj[(size_t)x * W + (y >> 6)] |= 1ull << (y & 63);
+        }
+    build_lists(adj, n, W, deg, nbr);
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+    orc_level L = {C, n, N, W, d, alpha, adj, deg, nbr, NULL, NULL, NULL, NULL, 0, 0, NULL, NULL,
+                   x0, xstep > 0 ? xstep : 1};
+    const double t0 = now_s();
+    int64_t tests, calls, indep;
+    const int err = level_pass(&L, &tests, &calls, &indep);
+    *seconds_out = now_s() - t0;
+    *tests_out = tests;
+    free(adj); free(deg); free(nbr);
+    return err;
 }
 
 /* Fisher-z p-values for an explicit list of tests (used to cross-check the numpy oracle). */

@@ -79,6 +79,7 @@ SIGNATURES = [
     ("pcg_last_error", ctypes.c_char_p, [P]),
     ("pcg_set_stream", I32, [P, P]),
     ("pcg_set_capacity", I32, [P, I64, I64]),
+    ("pcg_set_record_sample", I32, [P, I64, I64]),
     ("pcg_corr", I32, [P, P, I64, I64, I64, P, I64]),
     ("pcg_corr_shard_rows", I32, [I64, ctypes.c_int, ctypes.POINTER(I64)]),
     ("pcg_corr_shard", I32, [P, P, I64, I64, I64, ctypes.c_int, ctypes.c_int, P]),

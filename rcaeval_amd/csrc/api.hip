@@ -120,3 +120,12 @@ extern "C" int pcg_set_capacity(pcg_handle *h, int64_t record_capacity, int64_t 
     if (deferred_capacity > 0) h->def_cap = deferred_capacity;
     return PCG_OK;
 }
+
+extern "C" int pcg_set_record_sample(pcg_handle *h, int64_t modulus, int64_t residue) {
+    if (!h || modulus < 0 || (modulus > 1 && (residue < 0 || residue >= modulus)))
+        return pcg_fail(h, PCG_ERR_INVALID, "pcg_set_record_sample: modulus %lld residue %lld", (long long)modulus,
+                        (long long)residue);
+    h->rec_mod = modulus;
+    h->rec_res = residue;
+    return PCG_OK;
+}

@@ -53,6 +53,7 @@ struct pcg_handle {
     uint8_t *rm_ext = nullptr;       // caller-owned removal-flag buffer (multi-GPU)
     int64_t rm_ext_bytes = 0;
     int64_t rec_cap = 0, def_cap = 1 << 20, near_cap = 1 << 16;
+    int64_t rec_mod = 0, rec_res = 0;  // pcg_set_record_sample (0/1 = record every test)
     int64_t export_cap = 0;          // rows
     int64_t export_rows = 0;         // rows exported so far (host mirror)
     int binom_n = -1;                // binom table built for 0..binom_n

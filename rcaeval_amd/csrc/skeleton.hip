@@ -41,6 +41,9 @@
 namespace {
 
 constexpr int MODE_DECIDE = 0;
+#ifndef PCG_COND_TAU
+#define PCG_COND_TAU 1e-4     // conditioning guard of the fast paths (see decide)
+#endif
 constexpr int MODE_FULLP = 1;
 constexpr int MODE_EXACT = 2;
 // candidates c per lane task in k_level_lds_t, per depth (measured, tools/variant_bench.sh):
@@ -82,10 +85,12 @@ struct LevelArgs {
     int64_t rec_cap;
     pcg_record *nearl;
     int64_t near_cap;
-    double lo2, hi2, rmax2;      // decision band on r^2, |r| guard
+    double lo2, hi2;             // decision band on r^2
+    double tau;                  // conditioning guard (see decide)
     double alpha, sqrt_dof;
     int dof_negative;
     int record;
+    int64_t rec_mod, rec_res;    // record sample: canonical pair (a, b) with (a*n + b) % rec_mod == rec_res
     int64_t chunk_lo;            // first chunk of this launch (within its class)
     int spl;                     // S ranks per lane (LDS-resident kernel)
     int lds_btab_off;            // byte offset of the LDS binomial table (LDS-resident kernel)
@@ -122,6 +127,11 @@ __device__ __forceinline__ void push_record(pcg_record *buf, int64_t cap, unsign
     }
 }
 
+// PCG_FLAG_RECORD keeps every unique test, or the fixed pair sample of pcg_set_record_sample
+__device__ __forceinline__ bool rec_on(const LevelArgs &a, int lo, int hi) {
+    return a.record && (a.rec_mod <= 1 || ((int64_t)lo * a.n + hi) % a.rec_mod == a.rec_res);
+}
+
 __device__ __forceinline__ void push_deferred(const LevelArgs &a, int x, int y, const int *S, int d) {
     const unsigned long long slot = atomicAdd(&a.ctr->deferred, 1ull);
     if ((int64_t)slot < a.def_cap) {
@@ -152,19 +162,26 @@ __host__ __device__ inline int tg_pairs(int D, int DM) {
 }
 
 // 0 dependent, 1 independent, 2 exact path. p written in FULL_P mode.
+// Conditioning guard: the Cholesky-based partial correlation is trusted only when
+//   g * min(c_xx, c_yy) * (1 - r^2) >= tau,   g = the smallest pivot^2 of C_SS,
+// i.e. c_xx c_yy - c_xy^2 > kg with kg = tau / g (correlation diagonals are 1). Below it
+// (near-collinear S, x or y given S nearly determined, |r| ~ 1) the test goes to the exact LU
+// path, so decisions never rest on a cancellation-dominated r^2: with tau = 1e-4 the
+// backward-error bound of the factorisation keeps r^2 within ~1e-8 relative of the LU value,
+// far inside the +-1e-6 band (a test with near-duplicate columns pins this).
 template <int MODE>
-__device__ __forceinline__ int decide(const LevelArgs &a, double cxy, double cxx, double cyy,
+__device__ __forceinline__ int decide(const LevelArgs &a, double cxy, double cxx, double cyy, double kg,
                                       double *p) {
     if (MODE == MODE_EXACT) return 2;
     const double den = cxx * cyy;
     if (!(den > 0.0)) return 2;
     const double num = cxy * cxy;
+    if (!(den - num > kg)) return 2;
     if (MODE == MODE_DECIDE) {
         if (num < a.lo2 * den) return 1;
-        if (num > a.hi2 * den && num < a.rmax2 * den) return 0;
+        if (num > a.hi2 * den) return 0;
         return 2;
     } else {
-        if (!(num < a.rmax2 * den)) return 2;
         const double r = cxy / sqrt(den);
         int err = 0;
         const double pv = pcg_pvalue_from_r(r, a.sqrt_dof, &err);
@@ -327,13 +344,13 @@ __global__ __launch_bounds__(256) void k_level0(LevelArgs a) {
         if (x < a.n && y < a.n && y > x) {
             const double cxy = a.C[(int64_t)x * a.ldc + y];
             double p = 0.0;
-            const int dec = decide<MODE>(a, cxy, a.diag[x], cyy, &p);
+            const int dec = decide<MODE>(a, cxy, a.diag[x], cyy, a.tau, &p);
             ++tests;
             if (dec == 2) {
                 push_deferred(a, x, y, S0, 0);
             } else {
                 if (MODE == MODE_FULLP) {
-                    if (a.record) push_record(a.records, a.rec_cap, &a.ctr->records, x, y, 0, S0, p);
+                    if (rec_on(a, x, y)) push_record(a.records, a.rec_cap, &a.ctr->records, x, y, 0, S0, p);
                     if (fabs(p - a.alpha) < 1e-9) push_record(a.nearl, a.near_cap, &a.ctr->near_alpha, x, y, 0, S0, p);
                 }
                 if (dec == 1) { f = 1; ++indep; }
@@ -412,6 +429,7 @@ __global__ __launch_bounds__(256) void k_level(LevelArgs a) {
     double u[DM];
     bool chol_ok = active;
     double cxx = 0.0;
+    double gmin = 1.0;   // smallest pivot^2 of C_SS (conditioning guard, see decide)
     if (active) {
 #pragma unroll
         for (int j = 0; j < DM; ++j) {
@@ -422,6 +440,7 @@ __global__ __launch_bounds__(256) void k_level(LevelArgs a) {
                 for (int q = 0; q < DM; ++q)
                     if (q < j) s -= L[j][q] * L[j][q];
                 chol_ok = chol_ok && (s > 0.0);
+                gmin = fmin(gmin, s);
                 const double ljj = sqrt(s);
                 rinv[j] = 1.0 / ljj;
                 L[j][j] = ljj;
@@ -453,6 +472,7 @@ __global__ __launch_bounds__(256) void k_level(LevelArgs a) {
         cxx = a.diag[x] - uu;
         chol_ok = chol_ok && (cxx == cxx);
     }
+    const double kg = a.tau / gmin;
 
     unsigned long long tests = 0, indep = 0;
     const int nstage = (E + bs - 1) / bs;          // staged elements per thread
@@ -521,14 +541,14 @@ __global__ __launch_bounds__(256) void k_level(LevelArgs a) {
                     }
                     const double cxy = __longlong_as_double((long long)cur[D + W]) - uv;
                     const double cyy = __longlong_as_double((long long)cur[D + W + 1]) - vv;
-                    dec = decide<MODE>(a, cxy, cxx, cyy, &p);
+                    dec = decide<MODE>(a, cxy, cxx, cyy, kg, &p);
                 }
                 if (dec == 2) {
                     push_deferred(a, x, yg, sg, d);
                 } else {
                     if (MODE == MODE_FULLP) {
                         const int lo_ = x < yg ? x : yg, hi_ = x < yg ? yg : x;
-                        if (a.record) push_record(a.records, a.rec_cap, &a.ctr->records, lo_, hi_, d, sg, p);
+                        if (rec_on(a, lo_, hi_)) push_record(a.records, a.rec_cap, &a.ctr->records, lo_, hi_, d, sg, p);
                         if (fabs(p - a.alpha) < 1e-9)
                             push_record(a.nearl, a.near_cap, &a.ctr->near_alpha, lo_, hi_, d, sg, p);
                     }
@@ -666,7 +686,7 @@ __global__ __launch_bounds__(256) void k_level1_pairs(LevelArgs a) {
                 const double v = cyz * s_ri[k];
                 const double cxt = s_cx[t] - s_u[k] * v;
                 const double ctt = s_d[t] - v * v;
-                dec = decide<MODE_DECIDE>(a, cxt, cxx, ctt, &pv);
+                dec = decide<MODE_DECIDE>(a, cxt, cxx, ctt, a.tau * s_ri[k] * s_ri[k], &pv);
             }
             if (dec == 2) {
                 const int sg[1] = {kg};
@@ -791,12 +811,14 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
             // L = chol(M_SS); Li = L^-1 (lower); u = Li M_Sx; w = Li^T u (so u.v = w.b)
             double L[DM][DM], Li[DM][DM], u[DM], w[DM], b[DM];
             bool ok = true;
+            double gmin = 1.0;
 #pragma unroll
             for (int j = 0; j < DM; ++j) {
                 double sdiag = M[k[j] * D + k[j]];
 #pragma unroll
                 for (int q = 0; q < j; ++q) sdiag -= L[j][q] * L[j][q];
                 ok = ok && (sdiag > 0.0);
+                gmin = fmin(gmin, sdiag);
                 L[j][j] = sqrt(sdiag);
                 const double r = 1.0 / L[j][j];
 #pragma unroll
@@ -837,7 +859,7 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
             }
             const double cxx = Cxx - uu;
             ok = ok && (cxx > 0.0);
-            const double hc = a.hi2 * cxx, lc = a.lo2 * cxx, rc = a.rmax2 * cxx;
+            const double hc = a.hi2 * cxx, lc = a.lo2 * cxx, kg = a.tau / gmin;
             for (int t = 0; t < D; ++t) {
                 const double *Mt = M + t * D;
 #pragma unroll
@@ -854,7 +876,8 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
                 const double cxy = Mx[t] - wb;
                 const double cyy = Md[t] - vv;
                 const double num = cxy * cxy;
-                const bool dep = (num > hc * cyy) && (num < rc * cyy);
+                const double cond = fma(cxx, cyy, -num);   // c_xx c_yy (1 - r^2): guard, see decide
+                const bool dep = (num > hc * cyy) && (cond > kg);
                 const unsigned long long lm = lmask[t];
                 const bool in_y = (lm & Smask) == Smask;
                 const bool live = !((Smask >> t) & 1ull) && !(t < tx && in_y);
@@ -862,7 +885,7 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
                 const bool rare = live && !(ok && dep);
                 if (__ballot(rare)) {
                     if (rare) {
-                        const bool ind = ok && (num < lc * cyy) && (cyy > 0.0);
+                        const bool ind = ok && (num < lc * cyy) && (cyy > 0.0) && (cond > kg);
                         if (ind) {
                             ++indep;
                             atomicOr(&uself[t], Smask);
@@ -890,6 +913,7 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
             // Cholesky of M_SS, u = L^-1 M_Sx
             double L[DM][DM], rinv[DM], u[DM];
             bool ok = true;
+            double gmin = 1.0;
     #pragma unroll
             for (int j = 0; j < DM; ++j) {
                 if (j < d) {
@@ -898,6 +922,7 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
                     for (int q = 0; q < DM; ++q)
                         if (q < j) s -= L[j][q] * L[j][q];
                     ok = ok && (s > 0.0);
+                    gmin = fmin(gmin, s);
                     const double ljj = sqrt(s);
                     rinv[j] = 1.0 / ljj;
                     L[j][j] = ljj;
@@ -951,7 +976,7 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
                             uv += u[i] * v[i];
                         }
                     }
-                    dec = decide<MODE>(a, Mx[t] - uv, cxx, Md[t] - vv, &p);
+                    dec = decide<MODE>(a, Mx[t] - uv, cxx, Md[t] - vv, a.tau / gmin, &p);
                 }
                 if (dec == 2 || (MODE == MODE_FULLP && (a.record || fabs(p - a.alpha) < 1e-9))) {
                     int sg[DM];
@@ -963,7 +988,7 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
                         continue;
                     }
                     const int lo_ = x < yg ? x : yg, hi_ = x < yg ? yg : x;
-                    if (a.record) push_record(a.records, a.rec_cap, &a.ctr->records, lo_, hi_, d, sg, p);
+                    if (rec_on(a, lo_, hi_)) push_record(a.records, a.rec_cap, &a.ctr->records, lo_, hi_, d, sg, p);
                     if (fabs(p - a.alpha) < 1e-9)
                         push_record(a.nearl, a.near_cap, &a.ctr->near_alpha, lo_, hi_, d, sg, p);
                 }
@@ -1155,12 +1180,14 @@ __global__ __launch_bounds__(256, tg_minblocks(DM)) void k_level_lds_t(LevelArgs
         // T-info: L_T, Li_T = L_T^-1, u_T = Li_T M_Tx
         double L[DT][DT], Li[DT][DT], uT[DT];
         bool okT = true;
+        double gmin = 1.0;   // smallest pivot^2 over T and the group's valid candidates (guard)
 #pragma unroll
         for (int j = 0; j < DT; ++j) {
             double s = M[T[j] * DS + T[j]];
 #pragma unroll
             for (int q = 0; q < j; ++q) s -= L[j][q] * L[j][q];
             okT = okT && (s > 0.0);
+            gmin = fmin(gmin, s);
             L[j][j] = sqrt(s);
             const double r = 1.0 / L[j][j];
 #pragma unroll
@@ -1223,8 +1250,12 @@ __global__ __launch_bounds__(256, tg_minblocks(DM)) void k_level_lds_t(LevelArgs
             uc[jj] = u;
             hc[jj] = a.hi2 * cxx;
             okc[jj] = valid && okT && (lam2 > 0.0) && (cxx > 0.0);
+            if (valid) gmin = fmin(gmin, lam2);
         }
-        const double rratio = a.rmax2 / a.hi2;     // rmax2*cxx*cyy = (hi2*cxx*cyy) * rratio
+        // conditioning guard (see decide): c_xx c_yy - c_xy^2 > tau / g, with c_xx c_yy
+        // recovered from the threshold product th = hi2 c_xx c_yy the sweep forms anyway
+        const double inv_hi2 = 1.0 / a.hi2;
+        const double kg = a.tau / gmin;
         const int cend = min(T[0], cbase + TG);      // valid candidates: c in [cbase, cend), >= 1 of them
         unsigned okm = 0;                            // candidates usable on the fast path
 #pragma unroll
@@ -1281,7 +1312,7 @@ __global__ __launch_bounds__(256, tg_minblocks(DM)) void k_level_lds_t(LevelArgs
                     const double cxy = bxy - uc[jj] * vc;
                     const double num = cxy * cxy;
                     const double th = hc[jj] * cyy;
-                    dep |= (unsigned)((num > th) & (num < th * rratio)) << jj;
+                    dep |= (unsigned)((num > th) & (fma(th, inv_hi2, -kg) > num)) << jj;
                 }
                 tcount += __popc(live);
                 const unsigned rare = live & ~(dep & okm);
@@ -1299,7 +1330,8 @@ __global__ __launch_bounds__(256, tg_minblocks(DM)) void k_level_lds_t(LevelArgs
                             const double cyy = byy - vc * vc;
                             const double cxy = bxy - uc[jj] * vc;
                             const double cxx = hc[jj] / a.hi2;
-                            const bool ind = okc[jj] && (cxy * cxy < a.lo2 * cxx * cyy) && (cyy > 0.0);
+                            const bool ind = okc[jj] && (cxy * cxy < a.lo2 * cxx * cyy) && (cyy > 0.0) &&
+                                             (cxx * cyy - cxy * cxy > kg);
                             const unsigned long long Smask = Tmask | (1ull << c);
                             if (ind) {
                                 ++indep;
@@ -1491,7 +1523,7 @@ __global__ void k_exact(LevelArgs a) {
         }
         ++nexact;
         if (err) { flag_error(a, err); continue; }
-        if (a.record) push_record(a.records, a.rec_cap, &a.ctr->records, lo_, hi_, d, e.s, p);
+        if (rec_on(a, lo_, hi_)) push_record(a.records, a.rec_cap, &a.ctr->records, lo_, hi_, d, e.s, p);
         if (fabs(p - a.alpha) < 1e-9) push_record(a.nearl, a.near_cap, &a.ctr->near_alpha, lo_, hi_, d, e.s, p);
         if (p > a.alpha) {
             ++nindep;
@@ -1590,8 +1622,10 @@ LevelArgs make_args(pcg_handle *h, int d, int mode_exact_all) {
         a.lo2 = -1.0;  // never decides: every test to the exact path
         a.hi2 = 1e300;
     }
-    a.rmax2 = 1.0 - 2e-9;
+    a.tau = PCG_COND_TAU;
     a.record = (h->flags & PCG_FLAG_RECORD) ? 1 : 0;
+    a.rec_mod = h->rec_mod;
+    a.rec_res = h->rec_res;
     a.spl = h->spl;
     (void)mode_exact_all;
     return a;

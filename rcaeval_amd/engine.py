@@ -187,13 +187,17 @@ class Engine:
 
     # ------------------------------------------------------------------ K2/K3
     def skeleton(self, C, N: int, alpha: float = 0.05, max_depth: int = -1, flags: int = 0,
-                 record_capacity: int = 0) -> SkeletonOut:
+                 record_capacity: int = 0, record_sample: tuple = (0, 0)) -> SkeletonOut:
+        """``record_sample=(modulus, residue)``: with PCG_FLAG_RECORD keep only the tests of the
+        canonical pairs (a, b) with (a*n + b) % modulus == residue (full-size parity samples)."""
         torch = _torch()
         Cd = self.to_device(C)
         n = Cd.shape[0]
         rl = torch.empty((n, n), dtype=torch.int8, device=self.device)
         if record_capacity:
             check(self.h, self.lib.pcg_set_capacity(self.h, int(record_capacity), 0), "pcg_set_capacity")
+        check(self.h, self.lib.pcg_set_record_sample(self.h, int(record_sample[0]), int(record_sample[1])),
+              "pcg_set_record_sample")
         st = PcgStats()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()

@@ -9,6 +9,7 @@ import pytest
 
 from oracle import cpc, fisherz
 from rcaeval_amd import _lib, synth
+from tests_support import assert_skeleton_matches, unions_from_engine
 
 pytestmark = pytest.mark.gpu
 
@@ -21,22 +22,6 @@ def eng():
 
 def _key(r):
     return (int(r["a"]), int(r["b"]), tuple(int(v) for v in r["s"][: r["d"]]))
-
-
-def _unions_from_oracle(ref, n):
-    rows = {}
-    W = (n + 63) // 64
-    for x in range(n):
-        for y in range(n):
-            if x != y and ref.removed_level[x, y] > 0:
-                bits = ref.side_union[x, y]
-                if bits.any():
-                    rows[(x, y)] = tuple(int(b) for b in bits[:W])
-    return rows
-
-
-def _unions_from_engine(out):
-    return {(int(x), int(y)): tuple(int(b) for b in bits) for (x, y), bits in zip(out.sep_xy, out.sep_bits)}
 
 
 CASES = [  # (n, N, seed, w_low, w_high, edge_prob)
@@ -74,11 +59,36 @@ def test_skeleton_matches_oracle(eng, n, N, seed, wl, wh, ep, flags):
     C = np.corrcoef(X.T)
     ref = cpc.skeleton(C, N, record_cap=2_000_000)
     out = eng.skeleton(C, N, flags=flags, record_capacity=2_000_000)
-    near = {_key(r) for r in out.near_alpha}
-    if not near:
-        np.testing.assert_array_equal(out.removed_level, ref.removed_level)
-        assert _unions_from_engine(out) == _unions_from_oracle(ref, n)
-    assert out.stats["tests"] == ref.tests
+    assert_skeleton_matches(out, ref, n)
+    if flags & _lib.PCG_FLAG_RECORD:
+        d = {_key(r): r["p"] for r in ref.records}
+        g = {_key(r): r["p"] for r in out.records}
+        assert set(g) == set(d)
+        keys = sorted(d)
+        ok = fisherz.p_close([g[k] for k in keys], [d[k] for k in keys])
+        assert ok.all(), [(keys[i], g[keys[i]], d[keys[i]]) for i in np.nonzero(~ok)[0][:5]]
+
+
+@pytest.mark.parametrize("noise", [1e-2, 1e-4, 1e-6, 1e-7])
+@pytest.mark.parametrize("flags", [0, _lib.PCG_FLAG_FULL_P | _lib.PCG_FLAG_RECORD])
+def test_near_collinear_columns_match_lu_oracle(eng, noise, flags):
+    """Ill-conditioned sub-matrices (near-duplicate columns and a near linear combination, as
+    RCAEval metric sets have them): the fast Cholesky paths must hand these tests to the exact
+    LU path (conditioning guard, skeleton.hip decide) so that every decision and p-value is
+    numpy.linalg.inv's (the C oracle's LU)."""
+    rng = np.random.default_rng(11)
+    X = synth.gaussian_sem(40, 800, seed=12, w_low=0.2, w_high=0.8, edge_prob=0.1)
+    for j, i in ((5, 3), (17, 9), (30, 31), (22, 5)):
+        X[:, j] = X[:, i] + noise * rng.standard_normal(len(X))
+    X[:, 38] = X[:, 1] - 0.5 * X[:, 2] + noise * rng.standard_normal(len(X))
+    C = np.corrcoef(X.T)
+    ref = cpc.skeleton(C, 800, record_cap=2_000_000)
+    if ref.error:
+        with pytest.raises(ValueError):
+            eng.skeleton(C, 800, flags=flags, record_capacity=2_000_000)
+        return
+    out = eng.skeleton(C, 800, flags=flags, record_capacity=2_000_000)
+    assert_skeleton_matches(out, ref, 40)
     if flags & _lib.PCG_FLAG_RECORD:
         d = {_key(r): r["p"] for r in ref.records}
         g = {_key(r): r["p"] for r in out.records}
@@ -89,7 +99,7 @@ def test_skeleton_matches_oracle(eng, n, N, seed, wl, wh, ep, flags):
 
 
 def test_decide_and_fullp_agree_2000_depth2(eng):
-    """Full-size (2000 vars) parity at depth <= 2 against the C oracle."""
+    """Full-size (2000 vars) parity at depth <= 2 against the C oracle, threshold and full-p."""
     X = synth.gaussian_sem(2000, 10000, seed=0)
     C = eng.corr(X)
     Ch = C.cpu().numpy()
@@ -97,10 +107,48 @@ def test_decide_and_fullp_agree_2000_depth2(eng):
     a = eng.skeleton(C, 10000, max_depth=2, flags=0)
     b = eng.skeleton(C, 10000, max_depth=2, flags=_lib.PCG_FLAG_FULL_P)
     for out in (a, b):
-        assert out.stats["tests"] == ref.tests
-        if len(out.near_alpha) == 0:
-            np.testing.assert_array_equal(out.removed_level, ref.removed_level)
-            assert _unions_from_engine(out) == _unions_from_oracle(ref, 2000)
+        assert_skeleton_matches(out, ref, 2000)
+
+
+@pytest.mark.timeout(900)
+def test_config5_full_depth4_matches_oracle(eng):
+    """BASELINE config 5 at full size and full depth: 2000 vars x 10 000 samples, seed 0,
+    max_depth 4 — the benchmarked workload, whose depth 4 (83 % of the 4.9e9 unique tests) runs
+    on the dominant k_level_lds_t<4> kernel. Threshold-mode removal depth of every pair,
+    per-level unique-test counts and sepset unions against the C oracle on the same C
+    (only pairs touched by an enumerated |p - alpha| < 1e-9 test are exempt); then the
+    full-p kernels on the same graph, with recorded p of a fixed pair sample (1 in 4099 pairs,
+    every depth) within 1e-9 relative (+2^-51) of the oracle's FisherZ."""
+    import sys
+    import time
+    X = synth.gaussian_sem(2000, 10000, seed=0)
+    C = eng.corr(X)
+    Ch = C.cpu().numpy()
+    a = eng.skeleton(C, 10000, max_depth=4, flags=0)
+    assert a.levels == 5 and sum(a.stats["tests"]) > 4.5e9
+    b = eng.skeleton(C, 10000, max_depth=4, flags=_lib.PCG_FLAG_FULL_P | _lib.PCG_FLAG_RECORD,
+                     record_capacity=4_000_000, record_sample=(4099, 17))
+    t0 = time.perf_counter()
+    print("oracle: config 5 to depth 4 ...", file=sys.stderr, flush=True)
+    ref = cpc.skeleton(Ch, 10000, max_depth=4, want_union=True)
+    print(f"oracle done in {time.perf_counter() - t0:.1f} s: tests {ref.tests}, "
+          f"near-alpha {len(ref.near_alpha)} / engine {len(a.near_alpha)}", file=sys.stderr, flush=True)
+    flips = assert_skeleton_matches(a, ref, 2000)
+    flips_b = assert_skeleton_matches(b, ref, 2000)
+    print(f"near-alpha flips: threshold {flips}, full-p {flips_b}", file=sys.stderr, flush=True)
+    rec = b.records
+    per_depth = np.bincount(rec["d"], minlength=5)
+    assert (per_depth[:5] > 100).all(), per_depth
+    p_ref = np.empty(len(rec))
+    for d in range(5):
+        sel = np.nonzero(rec["d"] == d)[0]
+        ab = np.ascontiguousarray(np.stack([rec["a"][sel], rec["b"][sel]], 1), dtype=np.int32)
+        S = np.ascontiguousarray(rec["s"][sel, :max(d, 1)], dtype=np.int32)
+        pr, err = cpc.fisherz_batch(Ch, 10000, ab, S, d)
+        assert not err.any()
+        p_ref[sel] = pr
+    ok = fisherz.p_close(rec["p"], p_ref)
+    assert ok.all(), [(rec[i], p_ref[i]) for i in np.nonzero(~ok)[0][:3]]
 
 
 def test_constant_column_nan_is_dependent(eng):
@@ -177,5 +225,5 @@ def test_native_sharded_single_rank_equals_single_gpu(eng, n, N, max_depth):
     b = eng.skeleton_sharded(C1, N, max_depth=max_depth)
     np.testing.assert_array_equal(a.removed_level, b.removed_level)
     assert a.stats["tests"] == b.stats["tests"] and a.stats["indep"] == b.stats["indep"]
-    assert _unions_from_engine(a) == _unions_from_engine(b)
+    assert unions_from_engine(a) == unions_from_engine(b)
     check(eng.h, eng.lib.pcg_comm_destroy(eng.h), "pcg_comm_destroy")
