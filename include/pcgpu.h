@@ -41,6 +41,8 @@ extern "C" {
 #define PCG_ERR_RCCL -6      /* RCCL unavailable or a collective failed               */
 #define PCG_ERR_OVERFLOW -7  /* an internal list overflowed its capacity: capacities were
                                 enlarged, rerun the skeleton (pcg_skeleton does so itself) */
+#define PCG_ERR_PEER -8      /* another rank failed at this depth (edge-sharded skeleton):
+                                every rank leaves the level loop at the same depth         */
 
 /* skeleton flags */
 #define PCG_FLAG_FULL_P 0x1   /* compute the Fisher-z p-value of every test (reference
@@ -170,6 +172,17 @@ int pcg_level_split(pcg_handle *h, int rank, int world, int64_t *chunk_lo, int64
  * returns PCG_ERR_OVERFLOW on every rank: grow nothing, rerun the skeleton — capacities
  * have already been enlarged), [1] a singular sub-matrix, [2] a math domain error.      */
 #define PCG_RM_STATUS 64
+/* Bit-packed level barrier (replaces the n*n-byte all-reduce): pcg_level_pack writes this
+ * rank's removal flags as upper-triangle bits plus one status word (`words` u64 from
+ * pcg_level_packed_words; 256 KB at n = 2000) into packed_dev — local_error != 0 contributes
+ * no flags and marks "this rank failed" so its peers do not wait in the collective; the caller
+ * all-gathers the packed words of every rank (RCCL over xGMI, rank-major) and
+ * pcg_level_merge ORs the `world` copies back into the removal flags and status bytes;
+ * pcg_level_end then returns PCG_ERR_PEER on every rank if any rank failed.
+ * Both are stream-ordered on the handle's stream.                                          */
+int pcg_level_packed_words(int64_t n, int64_t *words);
+int pcg_level_pack(pcg_handle *h, uint64_t *packed_dev, int local_error);
+int pcg_level_merge(pcg_handle *h, const uint64_t *gathered_dev, int world);
 /* Number of ranks the level work lists are split over (default 1). The per-depth
  * decomposition sizes its chunks so that each rank's slice still fills its GPU.          */
 int pcg_set_world_size(pcg_handle *h, int world);
@@ -191,8 +204,9 @@ int pcg_comm_destroy(pcg_handle *h);
 int pcg_corr_sharded(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx,
                      double *C, int64_t ldc);
 /* The edge-sharded stable skeleton on the communicator: per depth begin / split / run on
- * this rank's work-balanced chunk range / RCCL all-reduce(MAX) of the removal flags and
- * status bytes / end; then the per-level counters are summed over ranks and every rank's
+ * this rank's work-balanced chunk range / pack / RCCL all-gather of the packed removal bits
+ * and status word / merge / end (a rank that fails locally still joins the all-gather, and
+ * its peers return PCG_ERR_PEER at the same depth); then the per-level counters are summed over ranks and every rank's
  * sepset rows are all-gathered, so pcg_sepset_* and removed_level describe the whole
  * skeleton on every rank (a pair's row may appear once per rank that saw it: OR them).
  * Same arguments and results as pcg_skeleton.                                              */

@@ -20,6 +20,7 @@ PCG_ERR_SINGULAR = -4
 PCG_ERR_DOMAIN = -5
 PCG_ERR_RCCL = -6
 PCG_ERR_OVERFLOW = -7
+PCG_ERR_PEER = -8
 
 PCG_FLAG_FULL_P = 0x1
 PCG_FLAG_RECORD = 0x2
@@ -98,6 +99,9 @@ SIGNATURES = [
     ("pcg_level_chunk_work", I32, [P, P, I64]),
     ("pcg_level_split", I32, [P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(I64), ctypes.POINTER(I64)]),
     ("pcg_set_removal_buffer", I32, [P, P, I64]),
+    ("pcg_level_packed_words", I32, [I64, ctypes.POINTER(I64)]),
+    ("pcg_level_pack", I32, [P, P, ctypes.c_int]),
+    ("pcg_level_merge", I32, [P, P, ctypes.c_int]),
     ("pcg_set_world_size", I32, [P, ctypes.c_int]),
     ("pcg_comm_unique_id", I32, [P, I64]),
     ("pcg_comm_init", I32, [P, P, ctypes.c_int, ctypes.c_int]),

@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import time
 import warnings
+from itertools import combinations
 
 import numpy as np
 
@@ -67,18 +68,26 @@ class SepsetArray:
     was adjacent, one tuple from a's visit then one from b's visit (each visit skipped when
     that node had fewer than depth-1 neighbours, ``:83``); the tuple is the union of all
     independent S from that side (``:129-130``), empty unless the edge was removed there.
-    Tuple elements are ``np.int64``, inserted ascending into a set (the reference inserts in
-    the order the S sets are enumerated; only the tuple-internal order can differ).
+
+    The tuple is ``tuple(sepsets)`` of the reference's ``set`` of ``np.int64``, so its order is
+    CPython's set order for the reference's insertion sequence: the members of each
+    independent S, S in ``combinations`` order (``:109,129-130``). A union of exactly d
+    members came from one S (inserted ascending); a larger union is ordered by deciding the
+    d-subsets of the union in ``combinations`` order on the device (``pcg_fisherz_batch``,
+    LU path) — all of them at once, on first access of such an entry.
     """
 
-    def __init__(self, out: SkeletonOut):
+    def __init__(self, out: SkeletonOut, ci: "CITester | None" = None, alpha: float = 0.05):
         self.shape = (out.n, out.n)
         self._out = out
         self._levels = out.levels
         n = out.n
         self._rl = out.removed_level
         self._deg = out.deg_levels
+        self._ci = ci
+        self._alpha = float(alpha)
         self._rows: dict = {}
+        self._order: dict | None = None
         W = out.sep_bits.shape[1] if out.sep_bits.size else (n + 63) // 64
         for r in range(len(out.sep_xy)):
             x, y = int(out.sep_xy[r, 0]), int(out.sep_xy[r, 1])
@@ -93,11 +102,44 @@ class SepsetArray:
             prev = self._rows.get((x, y))          # several rows per pair when edge-sharded: OR
             self._rows[(x, y)] = sorted(set(prev) | set(members)) if prev else members
 
+    def _resolve_order(self) -> dict:
+        """First-insertion order of every union with more members than its depth."""
+        order: dict = {}
+        todo = []
+        for (x, y), mem in self._rows.items():
+            a, b = (x, y) if x < y else (y, x)
+            d = int(self._rl[a, b])
+            if 0 < d < len(mem):
+                todo.append((x, y, d, mem))
+        if not todo:
+            return order
+        if self._ci is None:
+            raise RuntimeError("sepset insertion order needs the CI tester of the run")
+        tests, spans = [], []
+        for (x, y, d, mem) in todo:
+            subs = list(combinations(mem, d))
+            spans.append((len(tests), subs))
+            tests.extend((x, y, S) for S in subs)
+        p, _ = self._ci.pvalues_status(tests)
+        for (x, y, d, mem), (lo, subs) in zip(todo, spans):
+            seq: list = []
+            for q, S in enumerate(subs):
+                if p[lo + q] > self._alpha:
+                    seq.extend(s for s in S if s not in seq)
+            seq.extend(s for s in mem if s not in seq)    # decisions within the LU band: ascending
+            order[(x, y)] = seq
+        return order
+
     def _side(self, x: int, y: int) -> tuple:
         mem = self._rows.get((x, y))
         if not mem:
             return ()
-        return tuple(set(np.int64(m) for m in mem))
+        a, b = (x, y) if x < y else (y, x)
+        if len(mem) > max(int(self._rl[a, b]), 0):
+            if self._order is None:
+                self._order = self._resolve_order()
+            mem = self._order.get((x, y), mem)
+        return tuple(set(np.int64(m) for m in mem))    # CPython set order for this insertion order
 
     def __getitem__(self, key):
         if isinstance(key, tuple) and len(key) == 2:
@@ -127,17 +169,101 @@ class SepsetArray:
         return arr
 
 
-class CausalGraph:
-    """causal-learn ``CausalGraph`` result surface [U] (``lib/causallearn/graph/GraphClass.py:19-60``)."""
+# p_values materialises one float per reference ci_test call that returned p <= alpha; past
+# this many calls (RCAEval graphs are far below it) the lists would not fit a host anyway
+MAX_P_VALUE_CALLS = 20_000_000
 
-    def __init__(self, graph: np.ndarray, names, skeleton: SkeletonOut | None):
+
+def p_values_from_run(out: SkeletonOut, C, N: int, alpha: float, device: int | None = None) -> np.ndarray:
+    """``cg.p_values`` of a stable run (``SkeletonDiscovery.py:131-132``): for every visit of
+    x -> y at every depth, the p of each dependent S in ``combinations`` order.
+
+    The p-values come from a ``PCG_FLAG_FULL_P | PCG_FLAG_RECORD`` rerun of the skeleton on the
+    same C (every unique test recorded with the reference's p); the enumeration replays the
+    reference loop on the recorded adjacency of each depth (``removed_level``), so cache hits
+    repeat the cached p exactly as ``GraphClass.py:89-90`` returns it. Tests deeper than the
+    record depth (degenerate graphs) are evaluated by ``pcg_fisherz_batch``.
+    """
+    n = out.n
+    calls = int(sum(out.stats["calls"]))
+    if calls > MAX_P_VALUE_CALLS:
+        raise NotImplementedError(f"cg.p_values of {calls} ci_test calls (> {MAX_P_VALUE_CALLS}): "
+                                  "use the record path (Engine.skeleton(..., flags=PCG_FLAG_RECORD))")
+    eng = get_engine(device)
+    L = out.levels
+    rer = eng.skeleton(C, N, alpha=alpha, max_depth=L - 1,
+                       flags=_lib.PCG_FLAG_FULL_P | _lib.PCG_FLAG_RECORD,
+                       record_capacity=max(int(sum(out.stats["tests"])), 1))
+    cache: dict = {}
+    for r in rer.records:
+        d = int(r["d"])
+        cache[(int(r["a"]), int(r["b"]), tuple(int(s) for s in r["s"][:d]))] = float(r["p"])
+    rl = out.removed_level
+    pv = np.empty((n, n), object)
+    ci = None
+    for d in range(L):
+        A = (rl == -1) | (rl >= d)
+        np.fill_diagonal(A, False)
+        nbrs = [np.flatnonzero(A[x]).tolist() for x in range(n)]
+        miss = []
+        for x in range(n):
+            Nx = nbrs[x]
+            if len(Nx) < d - 1:
+                continue
+            for y in Nx:
+                a, b = (x, y) if x < y else (y, x)
+                for S in combinations([v for v in Nx if v != y], d):
+                    if (a, b, S) not in cache:
+                        miss.append((a, b, S))
+        if miss:
+            if ci is None:
+                ci = CITester(C, N, device=device)
+            p, _ = ci.pvalues_status(miss)
+            cache.update(zip(miss, p))
+        for x in range(n):
+            Nx = nbrs[x]
+            if len(Nx) < d - 1:
+                continue
+            for y in Nx:
+                a, b = (x, y) if x < y else (y, x)
+                for S in combinations([v for v in Nx if v != y], d):
+                    p = cache[(a, b, S)]
+                    if not p > alpha:
+                        if pv[x, y] is None:
+                            pv[x, y] = [p]
+                        else:
+                            pv[x, y].append(p)
+    return pv
+
+
+class CausalGraph:
+    """causal-learn ``CausalGraph`` result surface [U] (``lib/causallearn/graph/GraphClass.py:19-60``).
+
+    ``p_values`` is built on first access (``p_values_from_run``) for stable runs."""
+
+    def __init__(self, graph: np.ndarray, names, skeleton: SkeletonOut | None, C=None, N: int = 0,
+                 alpha: float = 0.05, device: int | None = None):
         self.G = GeneralGraph(graph, names)
         self.skeleton = skeleton
-        self.sepset = SepsetArray(skeleton) if skeleton is not None else np.empty(graph.shape, object)
-        self.p_values = np.empty(graph.shape, object)
+        self._run = (C, int(N), float(alpha), device)
+        ci = CITester(C, N, device=device) if (skeleton is not None and C is not None) else None
+        self.sepset = (SepsetArray(skeleton, ci, alpha) if skeleton is not None
+                       else np.empty(graph.shape, object))
+        self._p_values = None if (skeleton is not None and C is not None) else np.empty(graph.shape, object)
         self.PC_elapsed = -1
         self.no_ci_tests = int(sum(skeleton.stats["calls"])) if skeleton is not None else 0
         self.stats = skeleton.stats if skeleton is not None else {}
+
+    @property
+    def p_values(self) -> np.ndarray:
+        if self._p_values is None:
+            C, N, alpha, device = self._run
+            self._p_values = p_values_from_run(self.skeleton, C, N, alpha, device)
+        return self._p_values
+
+    @p_values.setter
+    def p_values(self, value) -> None:
+        self._p_values = value
 
 
 def _check_supported(indep_test, stable, uc_rule, uc_priority, mvpc, background_knowledge):
@@ -198,6 +324,7 @@ def pc(data: np.ndarray, alpha: float = 0.05, indep_test=fisherz, stable: bool =
         graph = uc_orient(sk.adj.astype(np.uint8), xy, bits, priority, ci).astype(int)
         cg = CausalGraph(graph, names, None)
         cg.sepset = sk.sepset
+        cg.p_values = sk.p_values
         cg.no_ci_tests = int(sum(sk.calls))
         cg.stats = {"levels": sk.levels, "calls": sk.calls}
         cg.PC_elapsed = time.time() - start
@@ -209,6 +336,6 @@ def pc(data: np.ndarray, alpha: float = 0.05, indep_test=fisherz, stable: bool =
     else:
         ci = CITester(C, X.shape[0], device=device)
         graph = uc_orient(out.adj, out.sep_xy, out.sep_bits, priority, ci).astype(int)
-    cg = CausalGraph(graph, names, out)
+    cg = CausalGraph(graph, names, out, C=C, N=X.shape[0], alpha=alpha, device=device)
     cg.PC_elapsed = time.time() - start
     return cg

@@ -2,10 +2,10 @@
 //
 // each PC depth's work list is split by work across the ranks (the same
 // pcg_level_split cut as the Python driver in rcaeval_amd/dist.py), every rank evaluates its
-// owner-disjoint chunk range, and the n*n removal flags + status bytes are merged with ONE
-// all-reduce(MAX, uint8) on the handle's stream (RCCL has no bitwise OR; MAX over 0/1 bytes is
-// the same merge) before pcg_level_end applies them identically everywhere. The loop runs in C:
-// no host-language round trip between the per-depth steps.
+// owner-disjoint chunk range, and the removal flags + status are merged with ONE all-gather of
+// bit-packed upper-triangle flags on the handle's stream (barrier.hip: RCCL has no bitwise OR,
+// so every rank ORs the gathered copies itself) before pcg_level_end applies them identically
+// everywhere. The loop runs in C: no host-language round trip between the per-depth steps.
 //
 // RCCL is resolved at run time: first the copy the process has already loaded (PyTorch ships
 // one), else librccl.so.1 — so a process that also uses torch.distributed holds one RCCL.
@@ -104,30 +104,45 @@ __global__ void k_unpack_rows(const int64_t *in, int64_t rows, int W, int32_t *x
 
 int sharded_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N, double alpha,
                  int max_depth, int flags, int8_t *removed_level) {
-    const int64_t nb = n * n + PCG_RM_STATUS;
-    if (!pcg_ensure(h, h->comm_rm, (size_t)nb)) return pcg_fail(h, PCG_ERR_OOM, "removal flags");
-    int rc = pcg_set_removal_buffer(h, (uint8_t *)h->comm_rm.p, nb);
-    if (!rc) rc = pcg_set_world_size(h, h->comm_world);
+    int64_t P = 0;
+    int rc = pcg_level_packed_words(n, &P);
+    if (rc) return pcg_fail(h, PCG_ERR_INVALID, "n = %lld", (long long)n);
+    const int world = h->comm_world;
+    if (!pcg_ensure(h, h->comm_packed, sizeof(uint64_t) * (size_t)P) ||
+        !pcg_ensure(h, h->comm_gathered, sizeof(uint64_t) * (size_t)P * world))
+        return pcg_fail(h, PCG_ERR_OOM, "packed removal flags");
+    rc = pcg_set_removal_buffer(h, nullptr, 0);   // the handle's own flags
+    if (!rc) rc = pcg_set_world_size(h, world);
     if (!rc) rc = pcg_skeleton_init(h, C, n, ldc, N, alpha, flags, removed_level);
     ncclComm_t comm = (ncclComm_t)h->comm;
+    uint64_t *packed = (uint64_t *)h->comm_packed.p, *gathered = (uint64_t *)h->comm_gathered.p;
     for (int depth = 0; !rc; ++depth) {
         if (max_depth >= 0 && depth > max_depth) break;
         int64_t total = 0, lo = 0, hi = 0;
-        rc = pcg_level_begin(h, depth, &total, nullptr, nullptr);
-        if (rc == 1) { rc = PCG_OK; break; }
-        if (rc) break;
-        rc = pcg_level_split(h, h->comm_rank, h->comm_world, &lo, &hi);
-        if (!rc) rc = pcg_level_run(h, lo, hi);
-        if (rc) break;
-        const ncclResult_t r = rccl().all_reduce(h->comm_rm.p, h->comm_rm.p, (size_t)nb, ncclUint8, ncclMax, comm,
-                                                 h->stream);
+        // begin is deterministic over the replicated adjacency ("done" agrees on every rank);
+        // a local failure of begin / split / run still joins the all-gather below, flagged in
+        // the status word, so no peer waits in the collective for this rank
+        int local = pcg_level_begin(h, depth, &total, nullptr, nullptr);
+        if (local == 1) break;
+        if (!local) local = pcg_level_split(h, h->comm_rank, world, &lo, &hi);
+        if (!local) local = pcg_level_run(h, lo, hi);
+        const std::string local_err = local ? h->err : std::string();
+        rc = pcg_level_pack(h, packed, local != 0);
+        if (rc) break;   // a launch failure here leaves nothing sane to send
+        const ncclResult_t r = rccl().all_gather(packed, gathered, (size_t)P, ncclUint64, comm, h->stream);
         if (r != ncclSuccess) {
-            rc = pcg_fail(h, PCG_ERR_RCCL, "ncclAllReduce(removal flags) failed: %s", rccl().error_string(r));
+            rc = pcg_fail(h, PCG_ERR_RCCL, "ncclAllGather(packed removal flags) failed: %s", rccl().error_string(r));
+            break;
+        }
+        rc = pcg_level_merge(h, gathered, world);
+        if (rc) break;
+        if (local) {   // this rank's own error, raised after its peers got the verdict
+            h->err = local_err;
+            rc = local;
             break;
         }
         rc = pcg_level_end(h, nullptr);
     }
-    pcg_set_removal_buffer(h, nullptr, 0);
     pcg_set_world_size(h, 1);
     return rc;
 }
@@ -281,8 +296,8 @@ extern "C" int pcg_skeleton_sharded(pcg_handle *h, const double *C, int64_t n, i
         rc = sharded_once(h, C, n, ldc, N, alpha, max_depth, flags, removed_level);
         if (rc != PCG_ERR_OVERFLOW) break;   // the merged status byte makes every rank rerun
     }
-    // errors that the merged status bytes raise are raised on every rank at the same depth, so
-    // the collectives below are skipped consistently; a local HIP / argument error is not
+    // level errors (singular, domain, a peer's local failure) end every rank at the same depth
+    // through the merged status word, so the collectives below are skipped consistently
     if (!rc) rc = reduce_stats(h);
     if (!rc) rc = gather_sepsets(h);
     if (stats) *stats = h->st;

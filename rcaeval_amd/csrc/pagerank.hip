@@ -52,6 +52,11 @@ struct Leaves {
     int nprog;
     int prog[2 * MAX_LEAVES];
 };
+// k_pagerank's LDS: static (Leaves, leaf sums, total_nnz, block_pw_sum's result) + the dynamic
+// per-node vectors and column pointers for m <= PR_LDS_M must fit one workgroup's 64 KiB
+static_assert(sizeof(Leaves) + MAX_LEAVES * sizeof(double) + 32 + 5 * PR_LDS_M * sizeof(double) +
+                      (PR_LDS_M + 1) * sizeof(int32_t) <= 65536,
+              "k_pagerank LDS budget");
 
 __device__ void pw_plan(Leaves &L, int n) {  // thread 0 only
     int st_s[64], st_n[64], st_state[64], sp = 0;
@@ -117,10 +122,11 @@ __global__ __launch_bounds__(PR_THREADS) void k_pagerank(const double *A, int m,
                                                          const double *data, double damping, int n_iter,
                                                          double tol, int32_t *colptr, int32_t *rowidx,
                                                          double *val, double *work, double *scores,
-                                                         int *status) {
+                                                         int64_t nnz_cap, int *status) {
     __shared__ Leaves L;
     __shared__ double leafsum[MAX_LEAVES];
     __shared__ int total_nnz;
+    __shared__ int bad_csr;
     // the five per-node vectors live in LDS for m <= PR_LDS_M (every iteration's sums and
     // sweeps then avoid global round trips between barriers), else in the global scratch
     extern __shared__ double pr_lds[];
@@ -152,12 +158,23 @@ __global__ __launch_bounds__(PR_THREADS) void k_pagerank(const double *A, int m,
         }
     } else {
         for (int i = tid; i <= m; i += blockDim.x) colptr[i] = 0;
+        if (tid == 0) bad_csr = 0;
         __syncthreads();
-        for (int j = tid; j < m; j += blockDim.x)
+        for (int j = tid; j < m; j += blockDim.x) {
+            if (indptr[j + 1] < indptr[j] || indptr[j] < 0) { bad_csr = 1; continue; }
             for (int q = indptr[j]; q < indptr[j + 1]; ++q)
-                if (data[q] != 0.0) atomicAdd(&colptr[indices[q] + 1], 1);
+                if (data[q] != 0.0) {
+                    const int c = indices[q];
+                    if ((unsigned)c < (unsigned)m) atomicAdd(&colptr[c + 1], 1);
+                    else bad_csr = 1;
+                }
+        }
     }
     __syncthreads();
+    if (!A && bad_csr) {   // malformed CSR (decreasing indptr, column out of range): refuse
+        if (tid == 0) *status = 3;
+        return;
+    }
     if (tid == 0) {
         colptr[0] = 0;
         for (int i = 0; i < m; ++i) colptr[i + 1] += colptr[i];
@@ -166,6 +183,10 @@ __global__ __launch_bounds__(PR_THREADS) void k_pagerank(const double *A, int m,
     __syncthreads();
     if (total_nnz == 0) {  // sknetwork check_format: "The input matrix is empty."
         if (tid == 0) *status = 1;
+        return;
+    }
+    if ((int64_t)total_nnz > nnz_cap) {   // CSR caller understated nnz: refuse before the fill
+        if (tid == 0) *status = 2;
         return;
     }
     if (A) {
@@ -307,12 +328,14 @@ static int pagerank_common(pcg_handle *h, const double *A, const int32_t *indptr
     const size_t lds = m <= PR_LDS_M ? sizeof(double) * 5 * (size_t)m + sizeof(int32_t) * (size_t)(m + 1) : 0;
     const int threads = m <= 256 ? 256 : PR_THREADS;   // small graphs: cheaper block barriers
     hipLaunchKernelGGL(k_pagerank, dim3(1), dim3(threads), lds, h->stream, A, (int)m, lda, indptr, indices,
-                       data, damping, n_iter, tol, colptr, rowidx, val, work, scores, status);
+                       data, damping, n_iter, tol, colptr, rowidx, val, work, scores, nnz_cap, status);
     PCG_HIP(h, hipGetLastError());
     int st = 0;
     PCG_HIP(h, hipMemcpyAsync(&st, status, sizeof(int), hipMemcpyDeviceToHost, h->stream));
     PCG_HIP(h, hipStreamSynchronize(h->stream));
     if (st == 1) return pcg_fail(h, PCG_ERR_INVALID, "The input matrix is empty.");
+    if (st == 3) return pcg_fail(h, PCG_ERR_INVALID, "pcg_pagerank_csr: malformed CSR (indptr order or column index)");
+    if (st == 2) return pcg_fail(h, PCG_ERR_INVALID, "pcg_pagerank_csr: nnz is smaller than the non-zeros in indptr");
     return PCG_OK;
 }
 
@@ -326,7 +349,7 @@ extern "C" int pcg_pagerank_dense(pcg_handle *h, const double *A, int64_t m, int
 
 extern "C" int pcg_pagerank_csr(pcg_handle *h, const int32_t *indptr, const int32_t *indices, const double *data,
                                 int64_t m, int64_t nnz, double damping, int n_iter, double tol, double *scores) {
-    if (!h || !indptr || !indices || !data || !scores || m < 1 || m > (1 << 15))
+    if (!h || !indptr || !indices || !data || !scores || m < 1 || m > (1 << 15) || nnz < 0)
         return pcg_fail(h, PCG_ERR_INVALID, "pcg_pagerank_csr: invalid arguments");
     return pagerank_common(h, nullptr, indptr, indices, data, m, 0, nnz, damping, n_iter, tol, scores);
 }

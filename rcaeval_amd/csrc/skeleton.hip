@@ -2135,6 +2135,10 @@ extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
     h->st.exact[d] = (int64_t)c.exact;
     h->st.near_alpha[d] = (int64_t)c.near_alpha;
     h->st.kernel_ms[d] = h->run_ms;
+    if (status[3]) {   // checked first: the failed rank will not rerun, so nobody may
+        if (stats) *stats = h->st;
+        return pcg_fail(h, PCG_ERR_PEER, "level %d: another rank failed at this depth", d);
+    }
     if (status[0]) {
         // some rank's exact-path (or record) list overflowed: the level is incomplete on every
         // rank. Enlarge and let the driver rerun the skeleton (pcg_skeleton does it itself).

@@ -4,10 +4,14 @@ Within one depth every (edge, S) test is independent — removals are deferred t
 barrier (``SkeletonDiscovery.py:141-144``) — so each rank evaluates an owner-disjoint,
 work-balanced slice of the depth's chunk list (a chunk = one node x and a run of S ranks;
 every test of a chunk, including both sepset sides, is evaluated by its owner). The only
-exchange is the removal flags: one ``all_reduce(MAX)`` of an n*n uint8 buffer per depth
-(RCCL has no bitwise OR; MAX over 0/1 bytes is the same merge). Every rank then applies the
-identical removals, so adjacency, degrees and the next depth's work list agree everywhere.
-Sepset-union rows stay on their owner until the end, then are all-gathered once.
+exchange is the removal flags: each rank packs its upper-triangle flags into bits plus one
+status word (``pcg_level_pack``: 256 KB at n = 2000 instead of 4 MB of bytes), ONE
+all-gather (RCCL over xGMI) collects every rank's words, and ``pcg_level_merge`` ORs them
+(RCCL has no bitwise OR). Every rank then applies the identical removals, so adjacency,
+degrees and the next depth's work list agree everywhere. A rank whose begin / run fails still
+joins the all-gather with its "failed" status bit set, so its peers leave the depth with
+``PCG_ERR_PEER`` instead of waiting in the collective. Sepset-union rows stay on their owner
+until the end, then are all-gathered once.
 
 ``LevelBackend`` abstracts one rank's device work so the protocol can be exercised on the
 CPU with ``gloo`` (tests/test_dist_cpu.py injects an oracle-backed backend).
@@ -55,12 +59,10 @@ class GpuLevelBackend:
         n = Cd.shape[0]
         self.n = n
         self.rl = torch.empty((n, n), dtype=torch.int8, device=eng.device)
-        # n*n removal flags + status bytes (overflow / singular / domain), merged by the same
-        # all-reduce so every rank takes the same branch at pcg_level_end
-        nb = n * n + _lib.PCG_RM_STATUS
-        self.rm = torch.zeros(nb, dtype=torch.uint8, device=eng.device)
-        check(self.h, self.lib.pcg_set_removal_buffer(self.h, ctypes.c_void_p(self.rm.data_ptr()), nb),
-              "pcg_set_removal_buffer")
+        words = ctypes.c_int64()
+        check(self.h, self.lib.pcg_level_packed_words(n, ctypes.byref(words)), "pcg_level_packed_words")
+        self.packed = torch.zeros(words.value, dtype=torch.int64, device=eng.device)
+        check(self.h, self.lib.pcg_set_removal_buffer(self.h, None, 0), "pcg_set_removal_buffer")
         check(self.h, self.lib.pcg_set_world_size(self.h, int(world)), "pcg_set_world_size")
         check(self.h, self.lib.pcg_skeleton_init(self.h, ctypes.c_void_p(Cd.data_ptr()), n, n, int(N),
                                                  float(alpha), int(flags), ctypes.c_void_p(self.rl.data_ptr())),
@@ -92,44 +94,65 @@ class GpuLevelBackend:
     def run(self, lo: int, hi: int):
         check(self.h, self.lib.pcg_level_run(self.h, int(lo), int(hi)), "pcg_level_run")
 
-    def removal_tensor(self):
-        return self.rm
+    def pack(self, local_error: bool):
+        """This rank's removal flags as packed upper-triangle bits + status word (device)."""
+        check(self.h, self.lib.pcg_level_pack(self.h, ctypes.c_void_p(self.packed.data_ptr()), int(local_error)),
+              "pcg_level_pack")
+        return self.packed
+
+    def merge(self, gathered, world: int):
+        """OR of every rank's packed words (rank-major) back into the removal flags."""
+        g = gathered.contiguous()
+        check(self.h, self.lib.pcg_level_merge(self.h, ctypes.c_void_p(g.data_ptr()), int(world)), "pcg_level_merge")
+        self._keep = g            # the merge is stream-ordered: keep the buffer alive until end()
 
     def end(self):
         check(self.h, self.lib.pcg_level_end(self.h, ctypes.byref(self.stats)), "pcg_level_end")
+        self._keep = None
 
     def finish(self):
-        self.lib.pcg_set_removal_buffer(self.h, None, 0)
         self.lib.pcg_set_world_size(self.h, 1)
         return self.eng._collect(self.n, self.rl, self.stats, 0.0)
 
 
 def run_sharded_levels(backend, rank: int, world: int, max_depth: int = -1, group=None, trace=None):
     """The level loop shared by the GPU path and the CPU protocol test. ``trace`` (a list)
-    collects (phase, depth, seconds) host timings of begin / run / all_reduce / end."""
+    collects (phase, depth, seconds) host timings of begin / run / exchange / end.
+
+    Per depth: begin (identical on every rank: the adjacency is replicated) / split / run on
+    this rank's slice / pack / ONE all-gather / merge / end. A local failure of begin, split
+    or run is carried through the all-gather as the rank's "failed" status bit and re-raised
+    afterwards; its peers raise ``PCG_ERR_PEER`` from end at the same depth."""
     import time
 
-    import torch.distributed as dist
-    depth = 0
     clock = time.perf_counter
+    depth = 0
     while True:
         if max_depth >= 0 and depth > max_depth:
             break
         t0 = clock()
-        work = backend.begin(depth)
-        if work is None:
-            break
-        # GPU backend: the cut is made in C; the CPU protocol test hands back the prefix
-        lo, hi = backend.split(rank, world) if hasattr(backend, "split") else split_by_work(work, rank, world)
-        t1 = clock()
-        backend.run(lo, hi)
+        local_err = None
+        t1 = t0
+        try:
+            work = backend.begin(depth)
+            if work is None:
+                break                # "done" is decided on replicated state: every rank agrees
+            # GPU backend: the cut is made in C; the CPU protocol test hands back the prefix
+            lo, hi = backend.split(rank, world) if hasattr(backend, "split") else split_by_work(work, rank, world)
+            t1 = clock()
+            backend.run(lo, hi)
+        except Exception as e:   # noqa: BLE001 - any local failure must still reach the collective
+            local_err = e
         t2 = clock()
-        dist.all_reduce(backend.removal_tensor(), op=dist.ReduceOp.MAX, group=group)
+        gathered = _gather_tensor(backend.pack(local_err is not None), group=group)
+        backend.merge(gathered, world)
         t3 = clock()
+        if local_err is not None:
+            raise local_err
         backend.end()
         if trace is not None:
             trace.extend([("begin", depth, t1 - t0), ("run", depth, t2 - t1),
-                          ("allreduce", depth, t3 - t2), ("end", depth, clock() - t3)])
+                          ("exchange", depth, t3 - t2), ("end", depth, clock() - t3)])
         depth += 1
     return depth
 
@@ -226,7 +249,6 @@ def sharded_skeleton(eng, C, N: int, alpha: float = 0.05, max_depth: int = -1, f
             # rank raise at the same level, capacities are already enlarged: rerun everywhere
             if e.code != _lib.PCG_ERR_OVERFLOW or attempt == 5:
                 raise
-            eng.lib.pcg_set_removal_buffer(eng.h, None, 0)
             eng.lib.pcg_set_world_size(eng.h, 1)
     t0 = time.perf_counter()
     out = backend.finish()
@@ -260,8 +282,8 @@ def native_sharded_corr(eng, X):
 
 def native_sharded_skeleton(eng, C, N: int, alpha: float = 0.05, max_depth: int = -1, flags: int = 0):
     """The edge-sharded skeleton with the whole level loop in C: per depth begin / split / run /
-    RCCL all-reduce(MAX) / end on the handle's stream, then the counters summed and the sepset
-    rows all-gathered (pcg_skeleton_sharded). Same result as ``sharded_skeleton``."""
+    pack / RCCL all-gather / merge / end on the handle's stream, then the counters summed and
+    the sepset rows all-gathered (pcg_skeleton_sharded). Same result as ``sharded_skeleton``."""
     return eng.skeleton_sharded(C, N, alpha=alpha, max_depth=max_depth, flags=flags)
 
 

@@ -268,6 +268,21 @@ class Engine:
               "pcg_pagerank_dense")
         return out.cpu().numpy()
 
+    def pagerank_csr(self, indptr, indices, data, m: int, damping: float = 0.85, n_iter: int = 10,
+                     tol: float = 1e-6, nnz: int | None = None) -> np.ndarray:
+        """PageRank of a CSR matrix (``pcg_pagerank_csr``); ``nnz`` defaults to len(indices)."""
+        torch = _torch()
+        ip = torch.from_numpy(np.ascontiguousarray(indptr, dtype=np.int32)).to(self.device)
+        ix = torch.from_numpy(np.ascontiguousarray(indices, dtype=np.int32)).to(self.device)
+        dv = self.to_device(data)
+        out = torch.empty(int(m), dtype=torch.float64, device=self.device)
+        nnz = len(ix) if nnz is None else int(nnz)
+        check(self.h, self.lib.pcg_pagerank_csr(self.h, ctypes.c_void_p(ip.data_ptr()), ctypes.c_void_p(ix.data_ptr()),
+                                                ctypes.c_void_p(dv.data_ptr()), int(m), nnz, float(damping),
+                                                int(n_iter), float(tol), ctypes.c_void_p(out.data_ptr())),
+              "pcg_pagerank_csr")
+        return out.cpu().numpy()
+
     def random_walk_counts(self, P, start: int, num_loop: int, state: int, inc: int) -> np.ndarray:
         torch = _torch()
         Pd = self.to_device(P)

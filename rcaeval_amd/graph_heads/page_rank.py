@@ -27,6 +27,22 @@ class PageRank:
         self.scores_ = None
 
     def fit(self, input_matrix, device: int | None = None) -> "PageRank":
+        """Dense arrays run ``pcg_pagerank_dense``; scipy sparse input (sknetwork's other
+        accepted format) runs ``pcg_pagerank_csr`` on its CSR form."""
+        try:
+            from scipy import sparse
+        except ImportError:  # pragma: no cover - scipy is in the image
+            sparse = None
+        if sparse is not None and sparse.issparse(input_matrix):
+            A = sparse.csr_matrix(input_matrix, dtype=np.float64)
+            if A.shape[0] != A.shape[1]:
+                raise ValueError("PageRank expects a square adjacency matrix (bipartite input not built)")
+            if not A.count_nonzero():
+                raise ValueError("The input matrix is empty.")   # sknetwork check_format [U]
+            A.sort_indices()
+            self.scores_ = get_engine(device).pagerank_csr(A.indptr, A.indices, A.data, A.shape[0],
+                                                           self.damping_factor, self.n_iter, self.tol)
+            return self
         A = np.asarray(input_matrix, dtype=np.float64)
         if A.ndim != 2 or A.shape[0] != A.shape[1]:
             raise ValueError("PageRank expects a square adjacency matrix (bipartite input not built)")
@@ -44,25 +60,29 @@ _PAIR_RULES = {
     (0, 0): None, (-1, -1): (1, 1), (1, -1): (1, None), (-1, 1): (None, 1), (0, 1): (0, 1),
     (1, 0): (1, 0), (1, 1): (1, 1), (2, 1): (1, 0), (1, 2): (0, 1), (2, 2): (1, 1),
 }
+# every rule is its own mirror (rule(u, v) == reversed rule(v, u)), so both visits of a pair
+# write the same value and pr[a, b] depends only on (adj[a,b], adj[b,a]): this table
+_PAIR_VALUE = {k: (r[0] if r is not None and r[0] is not None else 0) for k, r in _PAIR_RULES.items()}
 
 
 def page_rank_preprocess(adj: np.ndarray) -> np.ndarray:
-    """Endpoint codes -> 0/1 matrix, pair rules of ``page_rank.py:7-63`` (same visit order)."""
+    """Endpoint codes -> 0/1 matrix, pair rules of ``page_rank.py:7-63``, as one table lookup
+    per cell; an unknown pair raises at the first row-major cell, like the reference loop."""
     adj = np.asarray(adj)
     out = np.zeros_like(adj)
     m = len(adj)
-    for a in range(m):
-        for b in range(m):
-            key = (int(adj[a, b]), int(adj[b, a]))
-            if key not in _PAIR_RULES:
-                raise ValueError(f"Unexpected value: {adj[a, b]}, {adj[b, a]}")
-            rule = _PAIR_RULES[key]
-            if rule is None:
-                continue
-            if rule[0] is not None:
-                out[a, b] = rule[0]
-            if rule[1] is not None:
-                out[b, a] = rule[1]
+    if m == 0:
+        return out
+    A = adj.astype(np.int64, copy=False)
+    known = np.zeros((m, m), bool)
+    for (u, v), val in _PAIR_VALUE.items():
+        hit = (A == u) & (A.T == v)
+        known |= hit
+        if val:
+            out[hit] = val
+    if not known.all():
+        a, b = np.argwhere(~known)[0]
+        raise ValueError(f"Unexpected value: {adj[a, b]}, {adj[b, a]}")
     return out
 
 

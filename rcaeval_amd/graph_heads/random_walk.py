@@ -18,30 +18,34 @@ from ..engine import get_engine
 _RHO = 0.5
 
 
-def _edges_from_adj(adj: np.ndarray, m: int):
-    """Directed edges (u, v) of the nx graph before ``graph.reverse()`` (``:267-291``)."""
-    edges = []
-    for a in range(m):
-        for b in range(m):
-            ab, ba = int(adj[a, b]), int(adj[b, a])
-            if ab == ba == 0:
-                continue
-            if ab == ba == -1:
-                edges.append((b, a))
-            elif ab == 1 and ba == -1:
-                edges.append((b, a))
-            elif ab == -1 and ba == 1:
-                edges.append((a, b))
-            elif ab == 0 and ba == 1:
-                edges.append((a, b))
-            elif ab == 1 and ba == 0:
-                edges.append((b, a))
-            elif ab == 1 and ba == 1:
-                edges.append((a, b))
-                edges.append((b, a))
-            else:
-                raise ValueError(f"Unexpected value: {adj[a, b]}, {adj[b, a]}")
-    return edges
+# endpoint-code pairs (adj[a, b], adj[b, a]) the reference's edge loop accepts (:271-294)
+_VALID_PAIRS = {(0, 0), (-1, -1), (1, -1), (-1, 1), (0, 1), (1, 0), (1, 1)}
+
+
+def _check_codes(adj: np.ndarray) -> None:
+    """Raise like ``random_walk.py:293-294`` at the first (row-major) unknown code pair."""
+    m = len(adj)
+    if m == 0:
+        return
+    A = adj.astype(np.int64, copy=False)
+    ok = np.zeros((m, m), bool)
+    for u, v in _VALID_PAIRS:
+        ok |= (A == u) & (A.T == v)
+    if not ok.all():
+        a, b = np.argwhere(~ok)[0]
+        raise ValueError(f"Unexpected value: {adj[a, b]}, {adj[b, a]}")
+
+
+def edge_matrix(adj: np.ndarray) -> np.ndarray:
+    """E[u, v]: the nx edge u -> v before ``graph.reverse()`` (``:267-291``), as a bool matrix.
+
+    Visit (a, b) adds b -> a for the pairs (-1,-1), (1,-1), (1,0), (1,1) and a -> b for (-1,1),
+    (0,1), (1,1); over both visits of a pair that is a -> b  <=>  adj[b,a] == 1 or both are -1.
+    """
+    adj = np.asarray(adj)
+    _check_codes(adj)
+    A = adj.astype(np.int64, copy=False)
+    return (A.T == 1) | ((A == -1) & (A.T == -1))
 
 
 def transition_matrix(adj, node_names, names, score_values=None) -> np.ndarray:
@@ -49,34 +53,31 @@ def transition_matrix(adj, node_names, names, score_values=None) -> np.ndarray:
 
     ``node_names[a]`` names row/column a of ``adj``; ``names`` are the unique names in
     ``scores`` order (Node equality is by name); returns size x size with column c = the
-    distribution of the next node from node c.
+    distribution of the next node from node c. Array form of the reference's per-node loop:
+    on the reversed graph, children(c) = {u : u -> v in E, v ~ c} and parents(c) = {v : u -> v
+    in E, u ~ c}; parents are written after children (``:160-169``), and each column's
+    diagonal sees that column's max before it is set (``:171``).
     """
     adj = np.asarray(adj)
     m = len(adj)
     idx = {nm: i for i, nm in enumerate(names)}
     size = len(names)
     score = np.zeros(size) if score_values is None else np.asarray(score_values, dtype=float)
-    # graph on Node(name): node a of adj maps to names index of its (deduplicated) name
-    children = [set() for _ in range(size)]
-    parents = [set() for _ in range(size)]
-    node_of = [idx[node_names[a]] for a in range(m)]
-    for u, v in _edges_from_adj(adj, m):
-        # reversed graph: edge v -> u; children(v) gets u, parents(u) gets v
-        cu, cv = node_of[u], node_of[v]
-        children[cv].add(cu)
-        parents[cu].add(cv)
+    E = edge_matrix(adj).astype(np.int64)
+    Q = np.zeros((m, size), np.int64)
+    Q[np.arange(m), [idx[node_names[a]] for a in range(m)]] = 1
+    child = (Q.T @ E @ Q) > 0          # child[ch, c]: reversed edge c -> ch
+    parent = (Q.T @ E.T @ Q) > 0       # parent[pa, c]: reversed edge pa -> c
+    s = np.abs(score)
     M = np.zeros((size, size))
-    for c in range(size):
-        for ch in children[c]:
-            M[ch, c] = _RHO * abs(score[ch])
-        for pa in parents[c]:
-            M[pa, c] = abs(score[pa])
-        M[c, c] = max(abs(score[c]) - M[:, c].max(), 0)
-        tot = M[:, c].sum()
-        if tot > 0:
-            M[:, c] = M[:, c] / tot
-        else:
-            M[:, c] = 1 / size
+    M = np.where(child, _RHO * s[:, None], M)
+    M = np.where(parent, s[:, None], M)
+    diag = np.maximum(s - M.max(axis=0), 0.0) if size else s
+    M[np.arange(size), np.arange(size)] = diag
+    tot = np.ascontiguousarray(M.T).sum(axis=1)      # per-column pairwise sums, like Series.sum
+    pos = tot > 0
+    M[:, pos] = M[:, pos] / tot[pos]
+    M[:, ~pos] = 1 / size
     return M
 
 
@@ -86,7 +87,7 @@ def random_walk(adj: np.ndarray, node_names=None, sli=None, num_loop=None, previ
     adj = np.asarray(adj)
     if node_names is None:
         node_names = [f"X{i}" for i in range(len(adj))]
-    _edges_from_adj(adj, len(adj))            # raises on unknown endpoint pairs, like :293-294
+    _check_codes(adj)                         # raises on unknown endpoint pairs, like :293-294
     # sli = np.random.choice(nodes): same draw from numpy's global RandomState (:301)
     start_pos = int(np.random.choice(len(node_names)))
     uniq = list(dict.fromkeys(node_names))    # {Node(name): Score} dict semantics

@@ -43,6 +43,7 @@ class SeqSkeleton:
     def __init__(self, n: int):
         self.adj = ~np.eye(n, dtype=bool)
         self.sepset = np.empty((n, n), object)
+        self.p_values = np.empty((n, n), object)       # dependent p per (x, y), :131-132
         self.removed_level = np.full((n, n), -1, np.int64)
         self.calls: list = []
         self.levels = 0
@@ -105,6 +106,8 @@ def skeleton_unstable(ci: CITester, alpha: float = 0.05, max_depth: int = -1) ->
                         if pv > alpha:
                             first[y] = S
                             del its[y]
+                        else:
+                            append_value(out.p_values, x, y, pv)
                 k = min(4 * k, _MAX_CHUNK)
             for y in nb:
                 y = int(y)

@@ -1,9 +1,10 @@
 """CPU: the edge-sharded level protocol of rcaeval_amd.dist with gloo, world_size 2.
 
-The GPU backend is replaced by an oracle-backed backend with the same begin/run/end
-contract (chunks = (node x, run of S ranks), owner-disjoint evaluation, removal flags
-merged with all_reduce(MAX)), so the partitioning, the merge and the level barrier are
-checked against the single-process oracle skeleton without a GPU.
+The GPU backend is replaced by an oracle-backed backend with the same begin/run/pack/merge/end
+contract (chunks = (node x, run of S ranks), owner-disjoint evaluation, removal flags packed
+as upper-triangle bits + a status word, all-gathered and OR-merged), so the partitioning, the
+merge, the level barrier and the failure protocol are checked against the single-process
+oracle skeleton without a GPU.
 """
 import os
 import socket
@@ -90,13 +91,46 @@ class OracleLevelBackend:
                         if in_y and y > x:
                             self.unions.setdefault((int(y), x, d), set()).update(S)
 
-    def removal_tensor(self):
-        return self.rm
+    def pack(self, local_error):
+        """Upper-triangle bits of the flags (row-major pairs x < y) + one status byte."""
+        import torch
+        rm = self.rm.numpy().reshape(self.n, self.n).astype(bool)
+        iu = np.triu_indices(self.n, 1)
+        bits = np.packbits(rm[iu]) if not local_error else np.zeros((len(iu[0]) + 7) // 8, np.uint8)
+        return torch.from_numpy(np.concatenate([bits, [8 if local_error else 0]]).astype(np.uint8))
+
+    def merge(self, gathered, world):
+        g = gathered.numpy().reshape(world, -1)
+        merged = np.bitwise_or.reduce(g, axis=0)
+        self.status = int(merged[-1])
+        iu = np.triu_indices(self.n, 1)
+        up = np.unpackbits(merged[:-1])[:len(iu[0])].astype(bool)
+        rm = np.zeros((self.n, self.n), bool)
+        rm[iu] = up
+        rm |= rm.T
+        self.rm.copy_(__import__("torch").from_numpy(rm.reshape(-1).astype(np.uint8)))
 
     def end(self):
+        from rcaeval_amd import _lib
+        if self.status & 8:
+            raise _lib.PcgError(_lib.PCG_ERR_PEER, "another rank failed at this depth")
         rm = self.rm.numpy().reshape(self.n, self.n).astype(bool)
         self.rl[rm] = self.depth
         self.adj &= ~rm
+
+
+class FailingBackend(OracleLevelBackend):
+    """Raises inside run() at one depth on one rank (failure-protocol test)."""
+
+    def __init__(self, C, N, fail_rank, rank, fail_depth=1):
+        super().__init__(C, N)
+        self.fail = rank == fail_rank
+        self.fail_depth = fail_depth
+
+    def run(self, lo, hi):
+        if self.fail and self.depth == self.fail_depth:
+            raise MemoryError("injected local failure")
+        super().run(lo, hi)
 
 
 def _worker(rank, world, port, C, N, q):
@@ -124,7 +158,7 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_sharded_levels_match_single_process_oracle(world):
     import multiprocessing as mp
     from oracle import skeleton as osk
@@ -150,6 +184,49 @@ def test_sharded_levels_match_single_process_oracle(world):
             side = set(int(v) for v in (lst[-2] if x < y else lst[-1]))
             assert ref.removed_level[x, y] == d
             assert members == side
+
+
+def _fail_worker(rank, world, port, C, N, q):
+    import torch.distributed as dist
+    from rcaeval_amd import _lib
+    from rcaeval_amd.dist import run_sharded_levels
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    be = FailingBackend(C, N, fail_rank=1, rank=rank)
+    try:
+        run_sharded_levels(be, rank, world)
+        out = ("ok", be.depth)
+    except MemoryError:
+        out = ("own", be.depth)
+    except _lib.PcgError as e:
+        out = ("peer" if e.code == _lib.PCG_ERR_PEER else "other", be.depth)
+    dist.destroy_process_group()
+    q.put((rank, out))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_local_failure_reaches_every_rank_without_hanging(world):
+    """A rank that fails inside its slice still joins the level's all-gather: it re-raises its
+    own error and every peer raises PCG_ERR_PEER at the same depth (nobody waits forever)."""
+    import multiprocessing as mp
+    from rcaeval_amd import synth
+    n, N = 12, 500
+    X = synth.gaussian_sem(n, N, seed=4, w_low=0.3, w_high=0.9, edge_prob=0.3)
+    C = np.corrcoef(X.T)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fail_worker, args=(r, world, port, C, N, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        kind, depth = res[r]
+        assert kind == ("own" if r == 1 else "peer"), res
+        assert depth == 1
 
 
 def _gather_worker(rank, world, port, q):

@@ -25,16 +25,39 @@ def test_pagerank_bitwise_golden():
         np.testing.assert_array_equal(PageRank().fit_transform(g[f"A{i}"]), g[f"s{i}"])
 
 
-@pytest.mark.parametrize("m,n_iter", [(5, 10), (300, 10), (800, 30), (1100, 10)])
+@pytest.mark.parametrize("m,n_iter", [(5, 10), (256, 10), (257, 10), (300, 10), (768, 12), (769, 12), (800, 30),
+                                      (1100, 10)])
 def test_pagerank_sizes_vs_oracle(m, n_iter):
-    """Each layout of k_pagerank: LDS vectors with a 256-thread block (m <= 256), LDS with
-    1024 threads (m <= 768), global scratch (m > 768) — bitwise the scipy/numpy oracle."""
+    """Each layout of k_pagerank and its switch points: LDS vectors with a 256-thread block
+    (m <= 256), LDS vectors with 1024 threads (m <= 768), global scratch (m > 768) — bitwise the
+    scipy/numpy oracle, through both the dense and the CSR entry (pcg_pagerank_csr)."""
+    from scipy import sparse
     from oracle import pagerank as opr
     from rcaeval_amd.graph_heads.page_rank import PageRank
     rng = np.random.default_rng(m)
     A = (rng.random((m, m)) < min(1.0, 6.0 / m)) * rng.random((m, m))
     A[rng.integers(0, m, size=max(1, m // 10))] = 0.0   # dangling nodes
-    np.testing.assert_array_equal(PageRank(n_iter=n_iter).fit_transform(A), opr.pagerank(A, n_iter=n_iter))
+    ref = opr.pagerank(A, n_iter=n_iter)
+    np.testing.assert_array_equal(PageRank(n_iter=n_iter).fit_transform(A), ref)
+    np.testing.assert_array_equal(PageRank(n_iter=n_iter).fit_transform(sparse.csr_matrix(A)), ref)
+
+
+def test_pagerank_csr_refuses_understated_nnz_and_bad_columns():
+    from scipy import sparse
+    from rcaeval_amd._lib import PcgError
+    from rcaeval_amd.engine import get_engine
+    rng = np.random.default_rng(1)
+    A = sparse.csr_matrix((rng.random((50, 50)) < 0.2) * 1.0)
+    eng = get_engine(0)
+    with pytest.raises(PcgError):
+        eng.pagerank_csr(A.indptr, A.indices, A.data, 50, nnz=A.nnz // 2)
+    bad = A.indices.copy()
+    bad[3] = 77
+    with pytest.raises(PcgError):
+        eng.pagerank_csr(A.indptr, bad, A.data, 50)
+    # the handle stays usable after a refusal
+    np.testing.assert_array_equal(eng.pagerank_csr(A.indptr, A.indices, A.data, 50),
+                                  eng.pagerank_dense(A.toarray()))
 
 
 def test_pagerank_empty_input_raises():
@@ -156,21 +179,53 @@ def test_deep_levels_constant_column_vs_c_oracle():
     np.testing.assert_array_equal(out.removed_level, ref.removed_level)
 
 
-def test_causal_pc_sepset_surface():
+@pytest.mark.parametrize("n,N,seed,prob", [(16, 600, 21, 0.25), (24, 300, 5, 0.35), (30, 2000, 8, 0.3)])
+def test_causal_pc_sepset_and_p_values_surface(n, N, seed, prob):
+    """cg.sepset element for element (tuples in the reference's set order, not as sets) and
+    cg.p_values (every dependent p per visit, enumeration order) against oracle/skeleton.py."""
     from oracle import skeleton as osk
     from rcaeval_amd.causal import pc
-    X = synth.gaussian_sem(16, 600, seed=21, w_low=0.3, w_high=0.9, edge_prob=0.25)
+    X = synth.gaussian_sem(n, N, seed=seed, w_low=0.3, w_high=0.9, edge_prob=prob)
     cg = pc(X)
-    r = osk.skeleton_discovery(np.corrcoef(X.T), 600)
-    n = 16
+    r = osk.skeleton_discovery(np.corrcoef(X.T), N)
+    multi = 0
     for i in range(n):
         for j in range(n):
             if i == j:
                 continue
             mine, ref = cg.sepset[i, j], r.sepset[i, j]
             assert len(mine) == len(ref)
-            assert [set(map(int, t)) for t in mine] == [set(map(int, t)) for t in ref]
+            assert [tuple(map(int, t)) for t in mine] == [tuple(map(int, t)) for t in ref], (i, j)
+            multi += any(len(t) > max(int(r.removed_level[i, j]), 0) for t in ref)
+            pm, pr = cg.p_values[i, j], r.p_values[i, j]
+            if pr is None:
+                assert pm is None, (i, j)
+                continue
+            assert len(pm) == len(pr), (i, j)
+            pm, pr = np.asarray(pm), np.asarray(pr)
+            assert np.all(np.abs(pm - pr) <= 1e-9 * np.abs(pr) + 2.0 ** -51), (i, j)
     assert cg.no_ci_tests == sum(r.calls_per_level)
+    assert multi > 0          # unions from several S: the insertion order is exercised
+
+
+def test_sepset_order_matches_cpython_set_for_multi_s_unions():
+    """A union assembled from several independent S (|union| > depth) keeps the reference's
+    first-insertion order through CPython's set layout (members >= 8 collide in small tables)."""
+    from oracle import skeleton as osk
+    from rcaeval_amd.causal import pc
+    X = synth.gaussian_sem(40, 400, seed=3, w_low=0.1, w_high=0.3, edge_prob=0.3)
+    cg = pc(X)
+    r = osk.skeleton_discovery(np.corrcoef(X.T), 400)
+    seen = 0
+    for i in range(40):
+        for j in range(40):
+            if i == j or r.sepset[i, j] is None:
+                continue
+            rl = int(r.removed_level[i, j])
+            for t_m, t_r in zip(cg.sepset[i, j], r.sepset[i, j]):
+                assert tuple(map(int, t_m)) == tuple(map(int, t_r)), (i, j)
+                seen += rl > 0 and len(t_r) > rl
+    assert seen > 0
 
 
 def _free_port():

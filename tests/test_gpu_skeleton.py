@@ -227,3 +227,55 @@ def test_native_sharded_single_rank_equals_single_gpu(eng, n, N, max_depth):
     assert a.stats["tests"] == b.stats["tests"] and a.stats["indep"] == b.stats["indep"]
     assert unions_from_engine(a) == unions_from_engine(b)
     check(eng.h, eng.lib.pcg_comm_destroy(eng.h), "pcg_comm_destroy")
+
+
+@pytest.mark.parametrize("n", [2, 63, 64, 65, 130, 2000])
+def test_packed_barrier_or_merges_ranks(eng, n):
+    """pcg_level_pack / pcg_level_merge: the OR of three ranks' symmetric removal flags (and
+    their status bytes) comes back byte-exact in both triangles; a rank that reports a local
+    failure contributes no flags and sets status byte 3 (pcg_level_end -> PCG_ERR_PEER)."""
+    import ctypes
+    import torch
+    lib, h = eng.lib, eng.h
+    C = torch.eye(n, dtype=torch.float64, device=eng.device)
+    rl = torch.empty((n, n), dtype=torch.int8, device=eng.device)
+    rm = torch.zeros(n * n + _lib.PCG_RM_STATUS, dtype=torch.uint8, device=eng.device)
+    _lib.check(h, lib.pcg_set_removal_buffer(h, ctypes.c_void_p(rm.data_ptr()), rm.numel()), "rm")
+    try:
+        _lib.check(h, lib.pcg_skeleton_init(h, ctypes.c_void_p(C.data_ptr()), n, n, 100, 0.05, 0,
+                                            ctypes.c_void_p(rl.data_ptr())), "init")
+        total = ctypes.c_int64()
+        assert lib.pcg_level_begin(h, 0, ctypes.byref(total), None, None) == 0
+        words = ctypes.c_int64()
+        _lib.check(h, lib.pcg_level_packed_words(n, ctypes.byref(words)), "words")
+        rng = np.random.default_rng(n)
+        want = np.zeros((n, n), bool)
+        parts = []
+        for r in range(3):
+            f = np.triu(rng.random((n, n)) < 0.1, 1)
+            f |= f.T
+            status = np.zeros(_lib.PCG_RM_STATUS, np.uint8)
+            status[r % 3] = r == 2            # rank 2 raises the domain-error byte
+            rm.copy_(torch.from_numpy(np.concatenate([f.reshape(-1).astype(np.uint8), status])))
+            packed = torch.empty(words.value, dtype=torch.int64, device=eng.device)
+            _lib.check(h, lib.pcg_level_pack(h, ctypes.c_void_p(packed.data_ptr()), 0), "pack")
+            parts.append(packed)
+            want |= f
+        failed = torch.empty(words.value, dtype=torch.int64, device=eng.device)
+        _lib.check(h, lib.pcg_level_pack(h, ctypes.c_void_p(failed.data_ptr()), 1), "pack failed rank")
+        rm.fill_(7)
+        g = torch.cat(parts)
+        _lib.check(h, lib.pcg_level_merge(h, ctypes.c_void_p(g.data_ptr()), 3), "merge")
+        eng.sync()
+        got = rm[:n * n].cpu().numpy().reshape(n, n)
+        np.testing.assert_array_equal(got, want.astype(np.uint8))
+        st = rm[n * n:n * n + 8].cpu().numpy()
+        assert list(st[:4]) == [0, 0, 1, 0]
+        g2 = torch.cat(parts + [failed])
+        _lib.check(h, lib.pcg_level_merge(h, ctypes.c_void_p(g2.data_ptr()), 4), "merge with failed rank")
+        eng.sync()
+        np.testing.assert_array_equal(rm[:n * n].cpu().numpy().reshape(n, n), want.astype(np.uint8))
+        assert rm[n * n + 3].item() == 1
+        assert lib.pcg_level_end(h, None) == _lib.PCG_ERR_PEER
+    finally:
+        lib.pcg_set_removal_buffer(h, None, 0)

@@ -17,8 +17,8 @@ run() {
 for step in "$@"; do
   case $step in
     smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    test)  run pytest_gpu 1200 python -m pytest tests -m gpu -q -x --timeout 600 ;;
-    testall) run pytest_gpu 1200 python -m pytest tests -m gpu -q --timeout 600 ;;
+    test)  run pytest_gpu 1200 python -u -m pytest tests -m gpu -q -x --timeout 600 --timeout-method thread ;;
+    testall) run pytest_gpu 1200 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread ;;
     bench) run bench 900 python bench.py --steps 3 --warmup 1 ;;
     benchfast) run bench 600 python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
