@@ -183,6 +183,10 @@ int pcg_level_split(pcg_handle *h, int rank, int world, int64_t *chunk_lo, int64
 int pcg_level_packed_words(int64_t n, int64_t *words);
 int pcg_level_pack(pcg_handle *h, uint64_t *packed_dev, int local_error);
 int pcg_level_merge(pcg_handle *h, const uint64_t *gathered_dev, int world);
+/* Testing knob: nodes with more than `max_degree` (default and cap 64) neighbours leave the
+ * narrow LDS-resident class, so the wide T-group kernel (64-bit masks -> 128-bit) and the
+ * staged kernels can be checked on small graphs. Results are identical for any value.      */
+int pcg_set_narrow_degree(pcg_handle *h, int max_degree);
 /* Number of ranks the level work lists are split over (default 1). The per-depth
  * decomposition sizes its chunks so that each rank's slice still fills its GPU.          */
 int pcg_set_world_size(pcg_handle *h, int world);

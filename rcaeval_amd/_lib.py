@@ -103,6 +103,7 @@ SIGNATURES = [
     ("pcg_level_pack", I32, [P, P, ctypes.c_int]),
     ("pcg_level_merge", I32, [P, P, ctypes.c_int]),
     ("pcg_set_world_size", I32, [P, ctypes.c_int]),
+    ("pcg_set_narrow_degree", I32, [P, ctypes.c_int]),
     ("pcg_comm_unique_id", I32, [P, I64]),
     ("pcg_comm_init", I32, [P, P, ctypes.c_int, ctypes.c_int]),
     ("pcg_comm_destroy", I32, [P]),

@@ -66,18 +66,21 @@ struct pcg_handle {
     int flags = 0;
     int8_t *rl = nullptr;
     int depth = -1;                  // depth prepared by level_begin
-    int64_t total_chunks = 0;        // small-class + large-class chunks of the current depth
-    int64_t total_small = 0, total_large = 0;
+    int64_t total_chunks = 0;        // narrow + wide + large class chunks of the current depth
+    int64_t total_small = 0, total_wide = 0, total_large = 0;
     int chunk = 256;                 // block size of the staged (large-degree) kernel
     int spl = 1;                     // S ranks per lane of the LDS-resident kernel
     int world = 1;                   // ranks sharing each level's work list (pcg_set_world_size)
     int32_t maxdeg_small = 0;        // largest degree handled by the LDS-resident kernel
+    int32_t maxdeg_wide = 0;         // largest degree of the wide (128-bit mask) T-group class
+    int spl_w = 1;                   // tasks per lane of the wide class
+    int narrow_deg = 64;             // pcg_set_narrow_degree (testing: route more nodes to the wide class)
     bool tgroup = false;             // small class runs k_level_lds_t this depth
     int32_t maxdeg = 0;
     int64_t sumdeg = 0;
     std::vector<int32_t> deg_h;      // degrees at the start of the current depth
     std::vector<int32_t> deg_levels; // levels x n
-    std::vector<int64_t> cpre_h;     // 2 x (n + 1): small-class chunk prefix, then large-class
+    std::vector<int64_t> cpre_h;     // 3 x (n + 1): narrow, wide, large class chunk prefixes
     std::vector<int64_t> work_h;     // per-node tests estimate
     std::vector<pcg_record> rec_h, near_h;
     int64_t rec_total = 0, near_total = 0;

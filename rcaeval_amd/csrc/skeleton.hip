@@ -1059,8 +1059,26 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
 #define PCG_MB4 2
 #endif
 __host__ __device__ constexpr int tg_minblocks(int DM) { return DM == 2 ? PCG_MB2 : (DM == 3 ? PCG_MB3 : PCG_MB4); }
-template <int DM>
-__global__ __launch_bounds__(256, tg_minblocks(DM)) void k_level_lds_t(LevelArgs a) {
+// WIDE: nodes with 64 < D <= WIDE_DEG (128) — the same kernel with 128-bit local masks (the
+// few high-degree nodes of depths 2-3 that the staged generic kernel used to take)
+template <bool WIDE>
+using LMask = std::conditional_t<WIDE, unsigned __int128, unsigned long long>;
+
+template <bool WIDE>
+__device__ __forceinline__ void lmask_atomic_or(LMask<WIDE> *p, LMask<WIDE> v) {
+    if constexpr (WIDE) {
+        unsigned long long *q = reinterpret_cast<unsigned long long *>(p);
+        const unsigned long long lo = (unsigned long long)v, hi = (unsigned long long)(v >> 64);
+        if (lo) atomicOr(q, lo);
+        if (hi) atomicOr(q + 1, hi);
+    } else {
+        atomicOr(p, v);
+    }
+}
+
+template <int DM, bool WIDE>
+__global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_t(LevelArgs a) {
+    using Mask = LMask<WIDE>;
     constexpr int DT = DM - 1;
     constexpr int TG = tg_of_depth(DM);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1080,9 +1098,9 @@ __global__ __launch_bounds__(256, tg_minblocks(DM)) void k_level_lds_t(LevelArgs
     double *M = reinterpret_cast<double *>(smem);                 // D * DS (columns >= D zero)
     double *Mx = M + D * DS;                                      // D
     double *Md = Mx + D;                                          // D
-    unsigned long long *lmask = reinterpret_cast<unsigned long long *>(Md + D);   // D
-    unsigned long long *uself = lmask + D;                        // D
-    unsigned long long *uprop = uself + D;                        // D
+    Mask *lmask = reinterpret_cast<Mask *>(Md + D);              // D (16-B aligned: DS % 4 == 0)
+    Mask *uself = lmask + D;                                      // D
+    Mask *uprop = uself + D;                                      // D
     int32_t *nxs = reinterpret_cast<int32_t *>(uprop + D);       // D
     int *s_tx = nxs + D;                                          // 1
     unsigned *btab = reinterpret_cast<unsigned *>(smem + a.lds_btab_off);   // C(c, i), c <= D, i <= DM
@@ -1105,8 +1123,8 @@ __global__ __launch_bounds__(256, tg_minblocks(DM)) void k_level_lds_t(LevelArgs
         Mx[t] = a.C[(int64_t)x * a.ldc + yg];
         Md[t] = a.diag[yg];
         const uint64_t *ar = a.adj + (int64_t)yg * a.W;
-        unsigned long long m = 0;
-        for (int k = 0; k < D; ++k) m |= ((ar[nxs[k] >> 6] >> (nxs[k] & 63)) & 1ull) << k;
+        Mask m = 0;
+        for (int k = 0; k < D; ++k) m |= (Mask)((ar[nxs[k] >> 6] >> (nxs[k] & 63)) & 1ull) << k;
         lmask[t] = m;
         uself[t] = 0;
         uprop[t] = 0;
@@ -1174,9 +1192,9 @@ __global__ __launch_bounds__(256, tg_minblocks(DM)) void k_level_lds_t(LevelArgs
 #pragma unroll
         for (int k = 2; k <= TG; ++k) nmax_ += (__ballot(nval >= k) != 0);
         const int nmax = __builtin_amdgcn_readfirstlane(nmax_);
-        unsigned long long Tmask = 0;
+        Mask Tmask = 0;
 #pragma unroll
-        for (int i = 0; i < DT; ++i) Tmask |= 1ull << T[i];
+        for (int i = 0; i < DT; ++i) Tmask |= (Mask)1 << T[i];
         // T-info: L_T, Li_T = L_T^-1, u_T = Li_T M_Tx
         double L[DT][DT], Li[DT][DT], uT[DT];
         bool okT = true;
@@ -1268,8 +1286,8 @@ __global__ __launch_bounds__(256, tg_minblocks(DM)) void k_level_lds_t(LevelArgs
             constexpr int NC = decltype(nc_tag)::value;
             for (int t = 0; t < D; ++t) {
                 // t in T: the lane idles through this y (branch-free: no exec-mask split)
-                const bool inTset = (Tmask >> t) & 1ull;
-                const unsigned long long lm = lmask[t];
+                const bool inTset = (bool)((Tmask >> t) & 1u);
+                const Mask lm = lmask[t];
                 const bool own = (t < tx) && ((lm & Tmask) == Tmask);
                 const double *Mt = M + t * DS;
                 // the TG candidate operands M[t][cbase .. cbase+TG) are contiguous and 32-B aligned
@@ -1332,11 +1350,11 @@ __global__ __launch_bounds__(256, tg_minblocks(DM)) void k_level_lds_t(LevelArgs
                             const double cxx = hc[jj] / a.hi2;
                             const bool ind = okc[jj] && (cxy * cxy < a.lo2 * cxx * cyy) && (cyy > 0.0) &&
                                              (cxx * cyy - cxy * cxy > kg);
-                            const unsigned long long Smask = Tmask | (1ull << c);
+                            const Mask Smask = Tmask | ((Mask)1 << c);
                             if (ind) {
                                 ++indep;
-                                atomicOr(&uself[t], Smask);
-                                if (((lm & Smask) == Smask) && t >= tx) atomicOr(&uprop[t], Smask);
+                                lmask_atomic_or<WIDE>(&uself[t], Smask);
+                                if (((lm & Smask) == Smask) && t >= tx) lmask_atomic_or<WIDE>(&uprop[t], Smask);
                             } else {
                                 int sg[DM];
                                 sg[0] = nxs[c];
@@ -1366,23 +1384,25 @@ __global__ __launch_bounds__(256, tg_minblocks(DM)) void k_level_lds_t(LevelArgs
     __syncthreads();
     // flush unions (local bits -> global node bits) and removal flags
     for (int t = tid; t < D; t += bs) {
-        const unsigned long long us = uself[t], up = uprop[t];
+        const Mask us = uself[t], up = uprop[t];
         if (!(us | up)) continue;
         const int yg = nxs[t];
         a.rm[(int64_t)x * a.n + yg] = 1;
         a.rm[(int64_t)yg * a.n + x] = 1;
         for (int side = 0; side < 2; ++side) {
-            const unsigned long long bits = side ? up : us;
+            const Mask bits = side ? up : us;
             if (!bits) continue;
             const int64_t slot = side ? (int64_t)a.off[yg] + find_in_sorted(a.nbr + a.off[yg], a.deg[yg], x)
                                       : (int64_t)a.off[x] + t;
             unsigned long long *row = reinterpret_cast<unsigned long long *>(a.ug + slot * a.W);
-            unsigned long long m = bits;
-            while (m) {
-                const int b = __ffsll((long long)m) - 1;
-                const int gid = nxs[b];
-                atomicOr(&row[gid >> 6], 1ull << (gid & 63));
-                m &= m - 1;
+            for (int half = 0; half < (WIDE ? 2 : 1); ++half) {
+                unsigned long long m = (unsigned long long)(bits >> (64 * half));
+                while (m) {
+                    const int b = 64 * half + __ffsll((long long)m) - 1;
+                    const int gid = nxs[b];
+                    atomicOr(&row[gid >> 6], 1ull << (gid & 63));
+                    m &= m - 1;
+                }
             }
         }
     }
@@ -1657,16 +1677,19 @@ void launch_lds_mode(pcg_handle *h, const LevelArgs &a, int64_t nchunks, size_t 
     else hipLaunchKernelGGL((k_level_lds<12, MODE>), grid, block, lds, h->stream, a);
 }
 
-constexpr int SMALL_DEG = 64;        // LDS-resident kernel handles nodes with <= 64 neighbours
+constexpr int SMALL_DEG = 64;        // LDS-resident kernels handle nodes with <= 64 neighbours
+constexpr int WIDE_DEG = 128;        // ... and the T-group kernel's WIDE form nodes with <= 128
 
-size_t lds_small_core(int D) {  // k_level_lds_t is sized with D rounded up to 4 (its row stride)
- return ((size_t)D * D * 8 + (size_t)D * (2 * 8 + 3 * 8 + 4) + 16 + 15) & ~(size_t)15; }
+// mask_bytes: 8 (64-bit local masks) or 16 (WIDE); D rounded up to 4 (the T-group row stride)
+size_t lds_small_core(int D, int mask_bytes = 8) {
+ return ((size_t)D * D * 8 + (size_t)D * (2 * 8 + 3 * mask_bytes + 4) + 16 + 15) & ~(size_t)15; }
 size_t lds_small_bytes(int D) { return lds_small_core(D) + (size_t)(D + 1) * 5 * 8 + 24 * 8; }
 // k_level_lds_t: u32 binomial table + (g, t0) pair prefix (u32) and ids (u16)
-size_t lds_tgroup_bytes(int D, int DM) {
+size_t lds_tgroup_bytes(int D, int DM, int mask_bytes = 8) {
     const size_t np = (size_t)tg_pairs(D, DM);
-    return lds_small_core(D) + (size_t)(D + 1) * (DM + 1) * 4 + (np + 1) * 4 + np * 2 + 16;
+    return lds_small_core(D, mask_bytes) + (size_t)(D + 1) * (DM + 1) * 4 + (np + 1) * 4 + np * 2 + 16;
 }
+constexpr size_t LDS_MAX = 160 * 1024;   // gfx950 LDS per workgroup
 
 // lane tasks of k_level_lds_t for a node of degree D at depth d (see the kernel)
 uint64_t tgroup_tasks(const pcg_handle *h, int D, int d) {
@@ -1680,6 +1703,13 @@ uint64_t tgroup_tasks(const pcg_handle *h, int D, int d) {
 }
 
 bool use_tgroup(int mode, int d) { return mode == MODE_DECIDE && d >= 2 && d <= 4; }
+
+// node class of a degree-D node at depth d: 0 narrow, 1 wide (T-group depths only), 2 large
+int level_class(const pcg_handle *h, int D, int d, bool tg) {
+    if (D <= std::min(SMALL_DEG, h->narrow_deg) && d <= PCG_MAX_DEPTH) return 0;
+    if (tg && D <= WIDE_DEG && lds_tgroup_bytes((D + 3) & ~3, d, 16) <= LDS_MAX) return 1;
+    return 2;
+}
 
 int mode_of(const pcg_handle *h, int d) {
     if ((h->flags & PCG_FLAG_EXACT_ALL) || (double)h->N - d - 3 <= 0) return MODE_EXACT;
@@ -1810,12 +1840,17 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
         calls += (int64_t)std::min<uint64_t>(c, (uint64_t)INT64_MAX / 4096) * D * hist[D];
     }
     h->st.calls[depth] = calls;
-    // work decomposition: depth 0 = one chunk per row; depth >= 1 = two node classes
-    if (!pcg_ensure_pinned(h, h->cpre_pin, sizeof(int64_t) * 2 * (n + 1)))
+    // work decomposition: depth 0 = one chunk per row; depth >= 1 = three node classes:
+    // narrow (D <= 64: LDS-resident kernels), wide (64 < D <= 128 at the T-group depths: the
+    // T-group kernel with 128-bit masks), large (the rest: staged generic kernels)
+    if (!pcg_ensure_pinned(h, h->cpre_pin, sizeof(int64_t) * 3 * (n + 1)))
         return pcg_fail(h, PCG_ERR_OOM, "pinned chunk prefix");
-    int64_t *cs = (int64_t *)h->cpre_pin.p, *cl = cs + (n + 1);
+    int64_t *cs = (int64_t *)h->cpre_pin.p, *cw = cs + (n + 1), *cl = cw + (n + 1);
     h->work_h.assign(n, 0);
     h->maxdeg_small = 0;
+    h->maxdeg_wide = 0;
+    h->total_wide = 0;
+    h->spl_w = 1;
     if (depth == 0) {
         // 64 x 64 tiles of the pair triangle; node 64*bi owns the T - bi tiles of tile row bi
         h->chunk = 256;
@@ -1825,6 +1860,7 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
         int64_t acc = 0;
         for (int x = 0; x <= n; ++x) {
             cs[x] = acc;
+            cw[x] = 0;
             cl[x] = 0;
             if (x < n && (x & 63) == 0) acc += T - (x >> 6);
         }
@@ -1836,54 +1872,64 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
         const bool tg = use_tgroup(mode_of(h, depth), depth);
         h->tgroup = tg;
         std::vector<uint64_t> ns_of(maxd + 1, 0), units_of(maxd + 1, 0);
-        double sum_small = 0.0, sum_large = 0.0;
+        std::vector<int> cls_of(maxd + 1, 2);
+        double sum_small = 0.0, sum_wide = 0.0, sum_large = 0.0;
         int cnt_large = 0;
         for (int D = depth + 1; D <= maxd; ++D) {
             const uint64_t ns = hbinom(h, D, depth);
             if (hist[D] && ns > ((uint64_t)1 << 46))
                 return pcg_fail(h, PCG_ERR_INVALID, "depth %d work too large (deg %d)", depth, D);
             ns_of[D] = ns;
-            const bool small = D <= SMALL_DEG && depth <= PCG_MAX_DEPTH;
-            units_of[D] = small ? (tg ? tgroup_tasks(h, D, depth) : ns) : ns;
+            cls_of[D] = level_class(h, D, depth, tg);
+            units_of[D] = cls_of[D] < 2 ? (tg ? tgroup_tasks(h, D, depth) : ns) : ns;
             if (!hist[D]) continue;
-            if (small) {
+            if (cls_of[D] == 0) {
                 sum_small += (double)units_of[D] * hist[D];
                 h->maxdeg_small = D;
+            } else if (cls_of[D] == 1) {
+                sum_wide += (double)units_of[D] * hist[D];
+                h->maxdeg_wide = D;
             } else {
                 sum_large += (double)ns * hist[D];
                 cnt_large += (int)hist[D];
             }
         }
-        // ~4096 LDS-resident blocks per depth and rank; each lane walks spl units
+        // ~4096 LDS-resident blocks per depth and rank; each lane walks spl units. The wide class
+        // (a few nodes) aims at ~512 blocks so its nodes are spread over the chip
         h->spl = (int)std::min(64.0, std::max(1.0, std::floor(sum_small / (256.0 * 4096.0 * h->world))));
+        h->spl_w = (int)std::min(64.0, std::max(1.0, std::floor(sum_wide / (256.0 * 512.0 * h->world))));
         const double mean_large = cnt_large ? sum_large / cnt_large : 0.0;
         h->chunk = (depth > PCG_MAX_DEPTH || mean_large <= 64) ? 64 : (mean_large <= 128 ? 128 : 256);
-        const uint64_t csz = (uint64_t)256 * h->spl;
+        const uint64_t csz = (uint64_t)256 * h->spl, cszw = (uint64_t)256 * h->spl_w;
         std::vector<int64_t> nch_of(maxd + 1, 0);
         for (int D = depth + 1; D <= maxd; ++D) {
-            const bool small = D <= SMALL_DEG && depth <= PCG_MAX_DEPTH;
-            nch_of[D] = small ? (int64_t)((units_of[D] + csz - 1) / csz)
-                              : (int64_t)((ns_of[D] + h->chunk - 1) / h->chunk);
+            const int c = cls_of[D];
+            nch_of[D] = c == 0 ? (int64_t)((units_of[D] + csz - 1) / csz)
+                               : c == 1 ? (int64_t)((units_of[D] + cszw - 1) / cszw)
+                                        : (int64_t)((ns_of[D] + h->chunk - 1) / h->chunk);
         }
-        int64_t ss = 0, sl = 0;
+        int64_t ss = 0, sw = 0, sl = 0;
         for (int x = 0; x < n; ++x) {
             cs[x] = ss;
+            cw[x] = sw;
             cl[x] = sl;
             const int D = h->deg_h[x];
             if (D < depth + 1) continue;
             h->work_h[x] = (int64_t)ns_of[D] * (D - depth);
-            if (D <= SMALL_DEG && depth <= PCG_MAX_DEPTH) ss += nch_of[D];
-            else sl += nch_of[D];
+            const int c = cls_of[D];
+            (c == 0 ? ss : c == 1 ? sw : sl) += nch_of[D];
         }
         cs[n] = ss;
+        cw[n] = sw;
         cl[n] = sl;
         h->total_small = ss;
+        h->total_wide = sw;
         h->total_large = sl;
     }
-    h->total_chunks = h->total_small + h->total_large;
+    h->total_chunks = h->total_small + h->total_wide + h->total_large;
     if (total_chunks) *total_chunks = h->total_chunks;
-    if (!pcg_ensure(h, h->cpre, sizeof(int64_t) * 2 * (n + 1))) return PCG_ERR_OOM;
-    PCG_HIP(h, hipMemcpyAsync(h->cpre.p, h->cpre_pin.p, sizeof(int64_t) * 2 * (n + 1), hipMemcpyHostToDevice,
+    if (!pcg_ensure(h, h->cpre, sizeof(int64_t) * 3 * (n + 1))) return PCG_ERR_OOM;
+    PCG_HIP(h, hipMemcpyAsync(h->cpre.p, h->cpre_pin.p, sizeof(int64_t) * 3 * (n + 1), hipMemcpyHostToDevice,
                               h->stream));
     PCG_HIP(h, hipMemsetAsync(h->rm_ext ? (void *)h->rm_ext : h->rm.p, 0, (size_t)n * n + PCG_RM_STATUS, h->stream));
     PCG_HIP(h, hipMemsetAsync(h->ctr.p, 0, sizeof(DevCounters), h->stream));
@@ -1901,6 +1947,12 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
             h->export_cap = cap;
         }
     }
+    return PCG_OK;
+}
+
+extern "C" int pcg_set_narrow_degree(pcg_handle *h, int max_degree) {
+    if (!h || max_degree < 1) return pcg_fail(h, PCG_ERR_INVALID, "pcg_set_narrow_degree: %d", max_degree);
+    h->narrow_deg = max_degree;
     return PCG_OK;
 }
 
@@ -1923,19 +1975,19 @@ extern "C" int pcg_level_chunk_work(pcg_handle *h, int64_t *prefix_host, int64_t
     const int n = (int)h->n;
     int64_t acc = 0;
     prefix_host[0] = 0;
-    for (int cls = 0; cls < 2; ++cls) {
+    for (int cls = 0; cls < 3; ++cls) {
         const int64_t *cp = (const int64_t *)h->cpre_pin.p + cls * (n + 1);
-        const int64_t base = cls ? h->total_small : 0;
-        const uint64_t csz = cls ? (uint64_t)h->chunk : (uint64_t)256 * h->spl;
+        const int64_t base = cls == 0 ? 0 : cls == 1 ? h->total_small : h->total_small + h->total_wide;
+        const uint64_t csz = cls == 0 ? (uint64_t)256 * h->spl : cls == 1 ? (uint64_t)256 * h->spl_w
+                                                                        : (uint64_t)h->chunk;
         for (int x = 0; x < n; ++x) {
             const int64_t c0 = cp[x], c1 = cp[x + 1];
             if (c1 == c0) continue;
             if (h->depth == 0) {   // tile (x/64, x/64 + c - c0): its pair count
-                const int bi = x >> 6, T = (n + 63) / 64;
+                const int bi = x >> 6;
                 const int64_t ri = std::min<int64_t>(64, n - 64 * (int64_t)bi);
                 for (int64_t c = c0; c < c1; ++c) {
                     const int bj = bi + (int)(c - c0);
-                    (void)T;
                     const int64_t rj = std::min<int64_t>(64, n - 64 * (int64_t)bj);
                     acc += (bj == bi ? ri * (ri - 1) / 2 : ri * rj) + 1;
                     prefix_host[base + c + 1] = acc;
@@ -1943,7 +1995,7 @@ extern "C" int pcg_level_chunk_work(pcg_handle *h, int64_t *prefix_host, int64_t
                 continue;
             }
             const int D = h->deg_h[x];
-            const bool tg = (cls == 0) && h->tgroup;
+            const bool tg = (cls < 2) && h->tgroup;
             const uint64_t ns = tg ? tgroup_tasks(h, D, h->depth) : hbinom(h, D, h->depth);
             const int64_t per_unit = (int64_t)(D - h->depth) * (tg ? tg_of_depth(h->depth) : 1);
             for (int64_t c = c0; c < c1; ++c) {
@@ -1999,11 +2051,15 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                 else if (mode == MODE_FULLP) hipLaunchKernelGGL(k_level0<MODE_FULLP>, grid, block, 0, h->stream, a);
                 else hipLaunchKernelGGL(k_level0<MODE_EXACT>, grid, block, 0, h->stream, a);
             } else {
-                const int64_t s_lo = chunk_lo, s_hi = std::min(chunk_hi, h->total_small);
-                // both classes present: the large-degree class runs on the aux stream beside
-                // the LDS-resident class, forked after everything already on the main stream
-                // and joined before the exact path
-                const bool fork = s_hi > s_lo && chunk_hi > h->total_small;
+                const int64_t S = h->total_small, Wd = h->total_wide;
+                const int64_t s_lo = chunk_lo, s_hi = std::min(chunk_hi, S);
+                const int64_t w_lo = std::max(chunk_lo, S) - S, w_hi = std::max(std::min(chunk_hi, S + Wd) - S, w_lo);
+                const int64_t l_lo = std::max(chunk_lo, S + Wd) - (S + Wd);
+                const int64_t l_hi = std::max(chunk_hi - (S + Wd), l_lo);
+                // narrow and (wide or large) present: the wide / large classes run on the aux
+                // stream beside the narrow class, forked after everything already on the main
+                // stream and joined before the exact path
+                const bool fork = s_hi > s_lo && (w_hi > w_lo || l_hi > l_lo);
                 hipStream_t main_stream = h->stream;
                 if (fork) {
                     if (!h->aux) PCG_HIP(h, hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking));
@@ -2020,16 +2076,14 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                     const size_t lds = h->tgroup ? lds_tgroup_bytes(dl, d) : lds_small_bytes(dl);
                     if (h->tgroup) {
                         const dim3 grid((unsigned)(s_hi - s_lo)), block(256);
-                        if (d == 2) hipLaunchKernelGGL(k_level_lds_t<2>, grid, block, lds, h->stream, as);
-                        else if (d == 3) hipLaunchKernelGGL(k_level_lds_t<3>, grid, block, lds, h->stream, as);
-                        else hipLaunchKernelGGL(k_level_lds_t<4>, grid, block, lds, h->stream, as);
+                        if (d == 2) hipLaunchKernelGGL((k_level_lds_t<2, false>), grid, block, lds, h->stream, as);
+                        else if (d == 3) hipLaunchKernelGGL((k_level_lds_t<3, false>), grid, block, lds, h->stream, as);
+                        else hipLaunchKernelGGL((k_level_lds_t<4, false>), grid, block, lds, h->stream, as);
                     } else if (mode == MODE_DECIDE) launch_lds_mode<MODE_DECIDE>(h, as, s_hi - s_lo, lds);
                     else if (mode == MODE_FULLP) launch_lds_mode<MODE_FULLP>(h, as, s_hi - s_lo, lds);
                     else launch_lds_mode<MODE_EXACT>(h, as, s_hi - s_lo, lds);
                 }
-                const int64_t l_lo = std::max(chunk_lo, h->total_small) - h->total_small;
-                const int64_t l_hi = chunk_hi - h->total_small;
-                struct StreamSwap {   // the large class launches on h->aux; restored on every exit
+                struct StreamSwap {   // the wide / large classes launch on h->aux; restored on every exit
                     pcg_handle *h; hipStream_t main; bool on;
                     ~StreamSwap() { if (on) h->stream = main; }
                 } swap{h, main_stream, fork};
@@ -2037,9 +2091,23 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                     PCG_HIP(h, hipStreamWaitEvent(h->aux, h->ev_fork, 0));
                     h->stream = h->aux;
                 }
+                if (w_hi > w_lo) {
+                    LevelArgs aw = a;
+                    aw.cpre = (const int64_t *)h->cpre.p + (h->n + 1);
+                    aw.chunk_lo = w_lo;
+                    aw.bs = 256;
+                    aw.spl = h->spl_w;
+                    const int dl = (h->maxdeg_wide + 3) & ~3;
+                    aw.lds_btab_off = (int)lds_small_core(dl, 16);
+                    const size_t lds = lds_tgroup_bytes(dl, d, 16);
+                    const dim3 grid((unsigned)(w_hi - w_lo)), block(256);
+                    if (d == 2) hipLaunchKernelGGL((k_level_lds_t<2, true>), grid, block, lds, h->stream, aw);
+                    else if (d == 3) hipLaunchKernelGGL((k_level_lds_t<3, true>), grid, block, lds, h->stream, aw);
+                    else hipLaunchKernelGGL((k_level_lds_t<4, true>), grid, block, lds, h->stream, aw);
+                }
                 if (l_hi > l_lo && d > PCG_MAX_DEPTH) {
                     LevelArgs al = a;
-                    al.cpre = (const int64_t *)h->cpre.p + (h->n + 1);
+                    al.cpre = (const int64_t *)h->cpre.p + 2 * (h->n + 1);
                     const int64_t nch_deep = l_hi - l_lo;
                     const int grid = (int)std::min<int64_t>(nch_deep, 512);
                     const int m = d + 2;
@@ -2051,10 +2119,10 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                                        nch_deep);
                 } else if (l_hi > l_lo) {
                     LevelArgs al = a;
-                    al.cpre = (const int64_t *)h->cpre.p + (h->n + 1);
+                    al.cpre = (const int64_t *)h->cpre.p + 2 * (h->n + 1);
                     al.chunk_lo = l_lo;
                     const size_t lds = level_lds(h, al.bs);
-                    if (lds > 160 * 1024)
+                    if (lds > LDS_MAX)
                         return pcg_fail(h, PCG_ERR_INVALID, "max degree %d too large for LDS staging", h->maxdeg);
                     if (mode == MODE_DECIDE && d == 1 && h->maxdeg <= L1_MAXD)
                         hipLaunchKernelGGL(k_level1_pairs, dim3((unsigned)(l_hi - l_lo)), dim3(256), 0, h->stream, al);

@@ -69,6 +69,23 @@ def test_skeleton_matches_oracle(eng, n, N, seed, wl, wh, ep, flags):
         assert ok.all(), [(keys[i], g[keys[i]], d[keys[i]]) for i in np.nonzero(~ok)[0][:5]]
 
 
+@pytest.mark.parametrize("narrow", [4, 16])
+@pytest.mark.parametrize("n,N,seed,wl,wh,ep", CASES)
+def test_wide_and_large_classes_match_oracle(eng, n, N, seed, wl, wh, ep, narrow):
+    """Nodes above `narrow` neighbours leave the LDS-resident class: at the T-group depths they
+    run the WIDE (128-bit mask) T-group kernel, elsewhere the staged kernels — the skeleton,
+    the unions and the per-level test counts stay the oracle's."""
+    X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
+    C = np.corrcoef(X.T)
+    ref = cpc.skeleton(C, N)
+    _lib.check(eng.h, eng.lib.pcg_set_narrow_degree(eng.h, narrow), "pcg_set_narrow_degree")
+    try:
+        out = eng.skeleton(C, N)
+    finally:
+        eng.lib.pcg_set_narrow_degree(eng.h, 64)
+    assert_skeleton_matches(out, ref, n)
+
+
 @pytest.mark.parametrize("noise", [1e-2, 1e-4, 1e-6, 1e-7])
 @pytest.mark.parametrize("flags", [0, _lib.PCG_FLAG_FULL_P | _lib.PCG_FLAG_RECORD])
 def test_near_collinear_columns_match_lu_oracle(eng, noise, flags):
