@@ -278,6 +278,20 @@ int pcg_fisherz_batch(pcg_handle *h, const double *C, int64_t n, int64_t ldc, in
                       const int32_t *tests, int32_t stride, int64_t count, double *p,
                       int32_t *status);
 
+/* ---- batched discrete CI tests (RCD) ----------------------------------------------
+ * Replaces causal-learn's chisq / gsq [U] (utils/cit.py chisq_or_gsq_test, causal-learn
+ * 0.1.2.3 of RCAEval's RCD environment) as called from SkeletonDiscovery.py:152-210 /
+ * :70-144 by RCAEval/e2e/rcd.py:72-102. data: device n x N int32, variable-major (data[v*N+i]
+ * in [0, card[v])); card: device n int32; tests: device count x stride int32 rows
+ * [a, b, d, s_0 .. s_{d-1}, pad] (a < b). Per test: the contingency table over the strata of
+ * S (empty strata dropped), the chi-square (g_sq = 0) or G-square (g_sq = 1) statistic summed
+ * like numpy (bitwise), and its degrees of freedom. stat: device count doubles; df: device count
+ * int64; status: device count int32 (0 ok, 3 malformed row or sample, 4 table larger than
+ * max_cells). The caller takes p = chi2.sf(stat, df) (p = 1 when df <= 0). Synchronous.  */
+int pcg_chisq_batch(pcg_handle *h, const int32_t *data, int64_t N, int64_t n, const int32_t *card,
+                    const int32_t *tests, int32_t stride, int64_t count, int g_sq, int64_t max_cells,
+                    double *stat, int64_t *df, int32_t *status);
+
 #ifdef __cplusplus
 }
 #endif

@@ -47,7 +47,7 @@ struct pcg_handle {
 
     // scratch
     DevBuf adj, deg, off, nbr, rm, ug, cpre, binom, ctr, deferred, records, nearbuf, exportbuf,
-        export_xy, diag, colmean, pr_scratch, batch_scratch;
+        export_xy, diag, colmean, pr_scratch, batch_scratch, chisq_scratch;
     PinBuf ctr_pin, deg_pin, off_pin, cpre_pin, status_pin;
     std::vector<uint64_t> binom_h;   // host copy of the binomial table
     uint8_t *rm_ext = nullptr;       // caller-owned removal-flag buffer (multi-GPU)

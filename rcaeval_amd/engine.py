@@ -257,6 +257,23 @@ class Engine:
               "pcg_fisherz_batch")
         return p.cpu().numpy(), st.cpu().numpy()
 
+    def chisq_batch(self, data_dev, card_dev, N: int, n: int, rows: np.ndarray, g_sq: bool, max_cells: int):
+        """Contingency statistics of canonical rows ``[a, b, d, s..]`` (``pcg_chisq_batch``) on
+        variable-major int32 codes ``data_dev`` (n x N); returns (stat, df, status) host arrays."""
+        torch = _torch()
+        rows = np.ascontiguousarray(rows, dtype=np.int32)
+        count, stride = rows.shape
+        t = torch.from_numpy(rows).to(self.device)
+        stat = torch.empty(count, dtype=torch.float64, device=self.device)
+        df = torch.empty(count, dtype=torch.int64, device=self.device)
+        st = torch.empty(count, dtype=torch.int32, device=self.device)
+        check(self.h, self.lib.pcg_chisq_batch(self.h, ctypes.c_void_p(data_dev.data_ptr()), int(N), int(n),
+                                               ctypes.c_void_p(card_dev.data_ptr()), ctypes.c_void_p(t.data_ptr()),
+                                               int(stride), int(count), int(bool(g_sq)), int(max_cells),
+                                               ctypes.c_void_p(stat.data_ptr()), ctypes.c_void_p(df.data_ptr()),
+                                               ctypes.c_void_p(st.data_ptr())), "pcg_chisq_batch")
+        return stat.cpu().numpy(), df.cpu().numpy(), st.cpu().numpy()
+
     # ------------------------------------------------------------------ K4
     def pagerank_dense(self, A, damping: float = 0.85, n_iter: int = 10, tol: float = 1e-6) -> np.ndarray:
         torch = _torch()
