@@ -128,6 +128,8 @@ def parse():
                     help="skeleton: the headline line (config 5); rq2: every case of an Online-Boutique-shaped "
                          "RQ2 tree through pc_pagerank, cases dealt one per GPU (config 2)")
     ap.add_argument("--rq2-cases", type=int, default=125, help="cases in the synthetic RQ2 tree")
+    ap.add_argument("--rq2-dataset", choices=["online-boutique", "sock-shop"], default="online-boutique",
+                    help="shape of the synthetic RQ2 tree (config 2 names both)")
     return ap.parse_args()
 
 
@@ -220,23 +222,27 @@ def rq2_main(args):
         dist.init_process_group("gloo")
     get_engine(local)
     base = os.environ.get("PCG_RQ2_DIR") or tempfile.mkdtemp(prefix="rq2_")
-    root = os.path.join(base, "data", "online-boutique")
-    services = [s for s in synth.OB_SERVICES if s not in ("frontend", "redis")]
-    faults = ("cpu", "mem", "delay", "loss", "disk")
+    dataset = args.rq2_dataset
+    root = os.path.join(base, "data", dataset)
+    ss = dataset == "sock-shop"
+    services = [s for s in (synth.SS_SERVICES if ss else synth.OB_SERVICES)
+                if s not in (("front-end",) if ss else ("frontend", "redis"))]
+    faults = ("cpu", "mem", "delay", "loss") if ss else ("cpu", "mem", "delay", "loss", "disk")
     per = max(1, args.rq2_cases // (len(services) * len(faults)))
     if rank == 0 and not os.path.isdir(root):
-        synth.write_rq2_dataset(root, services=services, faults=faults, cases=per, rows=1200, seed=args.seed)
+        synth.write_rq2_dataset(root, services=services, faults=faults, cases=per, rows=1200, seed=args.seed,
+                                flavor=dataset)
     if world > 1:
         torch.distributed.barrier()
     out_dir = os.path.join(base, f"out_{rank}")
     # warm-up on this rank's first case (engine, HIP module load), then the timed pass
     first = rq2.list_cases(root)[rank::world][:1]
     for p in first:
-        rq2.process(p, "pc_pagerank", "online-boutique", tempfile.mkdtemp(), length=None)
+        rq2.process(p, "pc_pagerank", dataset, tempfile.mkdtemp(), length=None)
     if world > 1:
         torch.distributed.barrier()
     t0 = time.perf_counter()
-    res = rq2.run(root, "pc_pagerank", "online-boutique", out_dir, rank=rank, world=world)
+    res = rq2.run(root, "pc_pagerank", dataset, out_dir, rank=rank, world=world)
     dt = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64)
@@ -246,12 +252,12 @@ def rq2_main(args):
         n_cases = res["cases"]
         s_per_case = dt / n_cases
         print(json.dumps({
-            "metric": "PC-PageRank RQ2 cases/s (Online-Boutique-shaped, 44 metrics, cases dealt over GPUs)",
+            "metric": f"PC-PageRank RQ2 cases/s ({dataset}-shaped, cases dealt over GPUs)",
             "value": n_cases / dt, "unit": "cases/s", "n_gpus": world, "steps": 1, "warmup": 1,
             "ms_per_step": 1000.0 * dt, "higher_is_better": True, "scaling": "weak",
-            # whole-job cases/s over the published sequential rate (1 / 3.39 s per case)
-            "vs_baseline": (n_cases / dt) * OB_PC_PAGERANK_S_PER_CASE,
-            "dtype": "f64", "data": "synthetic RQ2 tree (rcaeval_amd.synth.write_rq2_dataset)",
+            # whole-job cases/s over the published sequential rate (1 / 3.39 s per OB case)
+            "vs_baseline": (n_cases / dt) * OB_PC_PAGERANK_S_PER_CASE if not ss else None,
+            "dtype": "f64", "data": f"synthetic {dataset}-shaped RQ2 tree (rcaeval_amd.synth.write_rq2_dataset)",
             "config": {"workload": f"rq2.run pc_pagerank over {n_cases} cases ({per} per service x fault), "
                                    "read_csv + window + preprocess + PC + orientation + PageRank + JSON",
                        "parallelism": f"cases round-robin over {world} GPU(s)"},

@@ -82,10 +82,16 @@ OB_SERVICES = ["adservice", "cartservice", "checkoutservice", "currencyservice",
                "paymentservice", "productcatalogservice", "recommendationservice", "shippingservice", "redis"]
 OB_METRICS = ["cpu", "mem", "latency-50", "latency-90"]
 FAULT_METRIC = {"cpu": "cpu", "mem": "mem", "delay": "latency-90", "loss": "latency-90", "disk": "mem"}
+# Sock Shop: <svc>_{cpu,mem,lat_50,lat_90,lat_99}; rq2.py:228-230 drops lat_50 / lat_99 columns
+# and takes <svc>_lat_90 (else front-end_cpu) as the SLI (:259-262)
+SS_SERVICES = ["carts", "catalogue", "front-end", "orders", "payment", "shipping", "user", "carts-db",
+               "orders-db", "user-db"]
+SS_METRICS = ["cpu", "mem", "lat_50", "lat_90", "lat_99"]
+SS_FAULT_METRIC = {"cpu": "cpu", "mem": "mem", "delay": "lat_90", "loss": "lat_90", "disk": "mem"}
 
 
 def rq2_case_frame(services=None, metrics=None, rows: int = 1200, root_service: str = "cartservice",
-                   fault: str = "cpu", seed: int = 0, t0: int = 1692569000):
+                   fault: str = "cpu", seed: int = 0, t0: int = 1692569000, fault_metric=None):
     """One RCAEval-RQ2-shaped case: ``time`` + ``<service>_<metric>`` columns, ``rows``
     one-second samples, a fault injected at the midpoint (returned as ``inject_time``):
     the root-cause metric shifts by 4 sigma and the shift propagates to its SEM descendants.
@@ -99,7 +105,7 @@ def rq2_case_frame(services=None, metrics=None, rows: int = 1200, root_service: 
     W, order, rng = sem_dag(n, edge_prob=3.0 / max(n - 1, 1), w_low=0.3, w_high=0.9, seed=seed)
     E = rng.standard_normal((rows, n))
     half = rows // 2
-    root = cols.index(f"{root_service}_{FAULT_METRIC[fault]}")
+    root = cols.index(f"{root_service}_{(fault_metric or FAULT_METRIC)[fault]}")
     E[half:, root] += 4.0
     X = np.zeros((rows, n))
     for j in order:
@@ -118,12 +124,17 @@ def rq2_case_frame(services=None, metrics=None, rows: int = 1200, root_service: 
 
 
 def write_rq2_dataset(root: str, services=None, faults=("cpu", "mem", "delay"), cases: int = 2,
-                      rows: int = 1200, seed: int = 0) -> list:
-    """An Online-Boutique-shaped RQ2 tree under ``root``:
-    ``<service>_<fault>/<case>/{data.csv, inject_time.txt}`` (``rq2.py:203-206,244-245``)."""
+                      rows: int = 1200, seed: int = 0, flavor: str = "online-boutique") -> list:
+    """An RQ2 case tree under ``root``: ``<service>_<fault>/<case>/{data.csv, inject_time.txt}``
+    (``rq2.py:203-206,244-245``), Online-Boutique-shaped (``<svc>_{cpu,mem,latency-50,latency-90}``)
+    or, with ``flavor="sock-shop"``, Sock-Shop-shaped (``<svc>_{cpu,mem,lat_50,lat_90,lat_99}``)."""
     import os
 
-    services = services or [s for s in OB_SERVICES if s not in ("frontend", "redis")][:4]
+    ss = flavor == "sock-shop"
+    all_services = SS_SERVICES if ss else OB_SERVICES
+    kw = {"services": SS_SERVICES, "metrics": SS_METRICS, "fault_metric": SS_FAULT_METRIC} if ss else {}
+    skip = ("front-end",) if ss else ("frontend", "redis")
+    services = services or [s for s in all_services if s not in skip][:4]
     paths = []
     k = 0
     for svc in services:
@@ -131,7 +142,7 @@ def write_rq2_dataset(root: str, services=None, faults=("cpu", "mem", "delay"), 
             for case in range(1, cases + 1):
                 d = os.path.join(root, f"{svc}_{fault}", str(case))
                 os.makedirs(d, exist_ok=True)
-                df, inject = rq2_case_frame(root_service=svc, fault=fault, rows=rows, seed=seed + k)
+                df, inject = rq2_case_frame(root_service=svc, fault=fault, rows=rows, seed=seed + k, **kw)
                 df.to_csv(os.path.join(d, "data.csv"), index=False)
                 with open(os.path.join(d, "inject_time.txt"), "w") as f:
                     f.write(f"{inject}\n")

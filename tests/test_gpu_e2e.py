@@ -307,19 +307,25 @@ def test_level_split_matches_split_by_work(world):
         be.finish()
 
 
-def test_rq2_run_matches_oracle_per_case(tmp_path):
-    """the RQ2 loop over an Online-Boutique-shaped case tree; every
-    case's rank list equals the CPU oracle pipeline on the same window."""
+@pytest.mark.parametrize("dataset,services", [("online-boutique", ["cartservice", "adservice"]),
+                                              ("sock-shop", ["carts", "orders"])])
+def test_rq2_run_matches_oracle_per_case(tmp_path, dataset, services):
+    """the RQ2 loop over an Online-Boutique- or Sock-Shop-shaped case tree
+    (sock-shop: lat_50 / lat_99 dropped, lat_90 SLI, rq2.py:228-230,259-262); every case's rank
+    list equals the CPU oracle pipeline on the same window."""
     from rcaeval_amd import rq2
-    root = os.path.join(str(tmp_path), "data", "online-boutique")
-    paths = synth.write_rq2_dataset(root, services=["cartservice", "adservice"], faults=("cpu", "delay"),
-                                    cases=1, rows=1200)
+    root = os.path.join(str(tmp_path), "data", dataset)
+    paths = synth.write_rq2_dataset(root, services=services, faults=("cpu", "delay"), cases=1, rows=1200,
+                                    flavor=dataset)
     out_dir = os.path.join(str(tmp_path), "out")
-    res = rq2.run(root, "pc_pagerank", "online-boutique", out_dir)
+    res = rq2.run(root, "pc_pagerank", dataset, out_dir)
     assert res["cases"] == len(paths) == 4
     for p in paths:
         c = rq2.load_case(p)
-        ranks, _ = _oracle_pipeline(c["data"], "online-boutique", "pagerank")
+        if dataset == "sock-shop":
+            assert not any(col.endswith(("_lat_50", "_lat_99")) for col in c["data"].columns)
+            assert c["sli"] == f"{c['service']}_lat_90"
+        ranks, _ = _oracle_pipeline(c["data"], dataset, "pagerank")
         got = rq2.load_json(os.path.join(out_dir, "results", c["result_name"]))["0"]
         assert got == ranks
     assert set(res["summary"]) >= {"Avg@5-CPU", "Avg@5-DELAY"}
