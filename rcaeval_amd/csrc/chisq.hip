@@ -10,8 +10,9 @@
 // with no samples are dropped (`SMarginalCounts != 0`); expected E = Sx * Sy / Sm (int64
 // products, float64 division); statistic = sum over the kept (k, x, y) cells in C order of
 // (T - E)^2 / (E == 0 ? 1 : E) (chi-square) or 2 * T * log(T / E) (G-square, ratio 0 -> 1),
-// summed with numpy's pairwise summation (8 accumulators, 128-element leaves), so the
-// statistic is bitwise numpy's; df = sum_k (cX - 1 - zero rows_k) * (cY - 1 - zero cols_k).
+// summed like numpy's sum (pairwise: 8 accumulators, 128-element leaves, inside blocks of 8192
+// elements accumulated in order), so the chi-square statistic is bitwise numpy's (G-square up to
+// the last bit of the device log); df = sum_k (cX - 1 - zero rows_k) * (cY - 1 - zero cols_k).
 // The tail probability chi2.sf(stat, df) is left to the caller (scipy's chdtrc on the host:
 // one vectorised call per batch), p = 1 when df <= 0.
 //
@@ -235,7 +236,11 @@ __global__ __launch_bounds__(CHI_BLOCK) void k_chisq(const int32_t *data, int64_
             int64_t df = 0, kept = 0;
             for (int k = 0; k < CHI_BLOCK; ++k) df += part_cnt[k];
             for (int64_t s = 0; s < cS; ++s) kept += Sm[s] != 0;
-            double v = np_pairwise_sum(terms, kept * cX * cY);
+            // numpy reduces a contiguous array in buffer-sized blocks of 8192 elements: pairwise
+            // inside a block, blocks accumulated in order onto 0.0
+            const int64_t total = kept * cX * cY;
+            double v = 0.0;
+            for (int64_t b0 = 0; b0 < total; b0 += 8192) v += np_pairwise_sum(terms + b0, min((int64_t)8192, total - b0));
             if (g_sq) v = 2.0 * v;
             stat[t] = v;
             dfout[t] = df;

@@ -47,20 +47,29 @@ constexpr int MODE_DECIDE = 0;
 constexpr int MODE_FULLP = 1;
 constexpr int MODE_EXACT = 2;
 // candidates c per lane task in k_level_lds_t, per depth (measured, tools/variant_bench.sh):
-// groups of 8 halve the per-y shared work at depths 2 and 4 (depth 2 -28 %, depth 4 -3 % with
-// 2 waves/SIMD of 227 VGPRs); depth 3 keeps groups of 4 (4 waves/SIMD, 8 was +15 %)
+// depth 2 groups of 8 (-28 % vs 4); depth 3 groups of 4 (4 waves/SIMD, 8 was +15 %, 6 equal);
+// depth 4 groups of 6 at 3 waves/SIMD (168 VGPRs): fp64 VALU from one wave issues at most every
+// ~8 cycles with a ~50-cycle dependent latency (tools/micro/valu_occ.hip), so a third wave of 6
+// chains beats two waves of 8 (4.03 vs 4.29 ms; groups of 4 at 3 waves 4.46 ms)
 #ifndef PCG_TG2
 #define PCG_TG2 8
+#endif
+#ifndef PCG_TG_WC
+#define PCG_TG_WC 0   // T-group sweep: project candidates with w_c = C_TT^-1 M[T][c] (see k_level_lds_t)
+#endif
+#ifndef PCG_TG_Y2
+#define PCG_TG_Y2 0   // T-group sweep: two y per iteration at the depths whose bit is set (1 << d)
 #endif
 #ifndef PCG_TG3
 #define PCG_TG3 4
 #endif
 #ifndef PCG_TG4
-#define PCG_TG4 8
+#define PCG_TG4 6
 #endif
 __host__ __device__ constexpr int tg_of_depth(int d) { return d == 2 ? PCG_TG2 : (d == 3 ? PCG_TG3 : PCG_TG4); }
-static_assert((PCG_TG2 == 4 || PCG_TG2 == 8) && (PCG_TG3 == 4 || PCG_TG3 == 8) && (PCG_TG4 == 4 || PCG_TG4 == 8),
-              "k_level_lds_t candidate groups of 4 or 8");
+static_assert((PCG_TG2 == 4 || PCG_TG2 == 6 || PCG_TG2 == 8) && (PCG_TG3 == 4 || PCG_TG3 == 6 || PCG_TG3 == 8) &&
+                  (PCG_TG4 == 4 || PCG_TG4 == 6 || PCG_TG4 == 8),
+              "k_level_lds_t candidate groups of 4, 6 or 8");
 
 struct LevelArgs {
     const double *C;
@@ -1047,8 +1056,8 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
 //   v_c = (M[c][y] - l_c.v_T) / lambda_c,  c_yy = byy - v_c^2,  c_xy = bxy - u_c v_c
 // — the same partial correlation, ~9 fp64 ops per test instead of ~26. Tasks (g, T): group
 // g covers c in [g*TG, g*TG+TG), T ranges over (d-1)-subsets of [g*TG+1, D) in colex order.
-// blocks per CU each depth's T-group kernel is register-sized for: 4 (128 VGPRs) for groups of
-// 4 and at depth 2; 2 (256 VGPRs, no spills) for depth 4's groups of 8
+// blocks per CU each depth's T-group kernel is register-sized for: 4 (128 VGPRs) at depths 2-3,
+// 3 (168 VGPRs) for depth 4's groups of 6
 #ifndef PCG_MB2
 #define PCG_MB2 4
 #endif
@@ -1056,7 +1065,7 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
 #define PCG_MB3 4
 #endif
 #ifndef PCG_MB4
-#define PCG_MB4 2
+#define PCG_MB4 3
 #endif
 __host__ __device__ constexpr int tg_minblocks(int DM) { return DM == 2 ? PCG_MB2 : (DM == 3 ? PCG_MB3 : PCG_MB4); }
 // WIDE: nodes with 64 < D <= WIDE_DEG (128) — the same kernel with 128-bit local masks (the
@@ -1270,6 +1279,23 @@ __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_
             okc[jj] = valid && okT && (lam2 > 0.0) && (cxx > 0.0);
             if (valid) gmin = fmin(gmin, lam2);
         }
+#if PCG_TG_WC
+        // w_c = L_T^-T l_c = C_TT^-1 M[T][c]: then l_c . v_T = w_c . M[T][y], so each candidate's
+        // chain starts from the row loads instead of waiting for v_T (same count of FMAs)
+#pragma unroll
+        for (int jj = 0; jj < TG; ++jj) {
+            double w[DT];
+#pragma unroll
+            for (int i = 0; i < DT; ++i) {
+                double t = 0.0;
+#pragma unroll
+                for (int k = i; k < DT; ++k) t += Li[k][i] * lc[jj][k];
+                w[i] = t;
+            }
+#pragma unroll
+            for (int i = 0; i < DT; ++i) lc[jj][i] = w[i];
+        }
+#endif
         // conditioning guard (see decide): c_xx c_yy - c_xy^2 > tau / g, with c_xx c_yy
         // recovered from the threshold product th = hi2 c_xx c_yy the sweep forms anyway
         const double inv_hi2 = 1.0 / a.hi2;
@@ -1284,83 +1310,107 @@ __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_
         // branch-free and interleaved (candidates beyond the count are not evaluated at all)
         auto sweep = [&](auto nc_tag) {
             constexpr int NC = decltype(nc_tag)::value;
-            for (int t = 0; t < D; ++t) {
-                // t in T: the lane idles through this y (branch-free: no exec-mask split)
-                const bool inTset = (bool)((Tmask >> t) & 1u);
-                const Mask lm = lmask[t];
-                const bool own = (t < tx) && ((lm & Tmask) == Tmask);
-                const double *Mt = M + t * DS;
-                // the TG candidate operands M[t][cbase .. cbase+TG) are contiguous and 32-B aligned
-                // (DS % 4 == 0, cbase % TG == 0): NC/2 16-B LDS reads, broadcast across the lanes of
-                // the wave that share the group
-                double sc[TG];
+            // YU consecutive y per iteration: their chains are independent, so the in-order issue of
+            // one wave has twice the fp64 work in flight (PCG_TG_Y2)
+            constexpr int YU = ((PCG_TG_Y2 >> DM) & 1) ? 2 : 1;
+            for (int t0y = 0; t0y < D; t0y += YU) {
+                int tt[YU];
+                Mask lmv[YU];
+                double byy[YU], bxy[YU], projv[YU][DT];
+                unsigned live[YU], dep[YU];
 #pragma unroll
-                for (int q = 0; q < (NC + 1) / 2; ++q) {
-                    const double2 m = *reinterpret_cast<const double2 *>(Mt + cbase + 2 * q);
-                    sc[2 * q] = m.x;
-                    sc[2 * q + 1] = m.y;
+                for (int k = 0; k < YU; ++k) {
+                    const int t = min(t0y + k, D - 1);
+                    tt[k] = t;
+                    // t in T: the lane idles through this y (branch-free: no exec-mask split)
+                    const bool inTset = (bool)((Tmask >> t) & 1u) || (t0y + k >= D);
+                    const Mask lm = lmask[t];
+                    lmv[k] = lm;
+                    const bool own = (t < tx) && ((lm & Tmask) == Tmask);
+                    const double *Mt = M + t * DS;
+                    // the TG candidate operands M[t][cbase .. cbase+TG) are contiguous and 32-B aligned
+                    // (DS % 4 == 0, cbase % TG == 0): NC/2 16-B LDS reads, broadcast across the lanes
+                    // of the wave that share the group
+                    double sc[TG];
+#pragma unroll
+                    for (int q = 0; q < (NC + 1) / 2; ++q) {
+                        const double2 m = *reinterpret_cast<const double2 *>(Mt + cbase + 2 * q);
+                        sc[2 * q] = m.x;
+                        sc[2 * q + 1] = m.y;
+                    }
+                    double vT[DT], mT[DT];
+                    double vv = 0.0, uv = 0.0;
+#pragma unroll
+                    for (int j = 0; j < DT; ++j) mT[j] = Mt[T[j]];
+#pragma unroll
+                    for (int i = 0; i < DT; ++i) {
+                        double v = 0.0;
+#pragma unroll
+                        for (int j = 0; j <= i; ++j) v += Li[i][j] * mT[j];
+                        vT[i] = v;
+                        vv += v * v;
+                        uv += uT[i] * v;
+                    }
+#pragma unroll
+                    for (int i = 0; i < DT; ++i) projv[k][i] = PCG_TG_WC ? mT[i] : vT[i];   // w_c.M[T][y] or l_c.v_T
+                    byy[k] = Md[t] - vv;
+                    bxy[k] = Mx[t] - uv;
+                    // live candidates: valid, c != y, and not deduplicated onto y (S in adj(y), y < x)
+                    const unsigned tb = ((unsigned)(t - cbase) < (unsigned)TG) ? (1u << (t - cbase)) : 0u;
+                    const unsigned skip = own ? (unsigned)(lm >> cbase) : 0u;
+                    live[k] = inTset ? 0u : (vmask & ~tb & ~skip);
+                    // TG independent chains, interleaved
+#pragma unroll
+                    for (int i = 0; i < DT; ++i)
+#pragma unroll
+                        for (int jj = 0; jj < NC; ++jj) sc[jj] -= lc[jj][i] * projv[k][i];
+                    unsigned dp = 0;
+#pragma unroll
+                    for (int jj = 0; jj < NC; ++jj) {
+                        const double vc = sc[jj] * rl[jj];
+                        const double cyy = byy[k] - vc * vc;
+                        const double cxy = bxy[k] - uc[jj] * vc;
+                        const double num = cxy * cxy;
+                        const double th = hc[jj] * cyy;
+                        dp |= (unsigned)((num > th) & (fma(th, inv_hi2, -kg) > num)) << jj;
+                    }
+                    dep[k] = dp;
                 }
-                double vT[DT];
-                double vv = 0.0, uv = 0.0;
-    #pragma unroll
-                for (int i = 0; i < DT; ++i) {
-                    double v = 0.0;
-    #pragma unroll
-                    for (int j = 0; j <= i; ++j) v += Li[i][j] * Mt[T[j]];
-                    vT[i] = v;
-                    vv += v * v;
-                    uv += uT[i] * v;
-                }
-                const double byy = Md[t] - vv;
-                const double bxy = Mx[t] - uv;
-                // live candidates: valid, c != y, and not deduplicated onto y (S in adj(y), y < x)
-                const unsigned tb = ((unsigned)(t - cbase) < (unsigned)TG) ? (1u << (t - cbase)) : 0u;
-                const unsigned skip = own ? (unsigned)(lm >> cbase) : 0u;
-                const unsigned live = inTset ? 0u : (vmask & ~tb & ~skip);
-                // TG independent chains, interleaved
-    #pragma unroll
-                for (int i = 0; i < DT; ++i)
-    #pragma unroll
-                    for (int jj = 0; jj < NC; ++jj) sc[jj] -= lc[jj][i] * vT[i];
-                unsigned dep = 0;
-    #pragma unroll
-                for (int jj = 0; jj < NC; ++jj) {
-                    const double vc = sc[jj] * rl[jj];
-                    const double cyy = byy - vc * vc;
-                    const double cxy = bxy - uc[jj] * vc;
-                    const double num = cxy * cxy;
-                    const double th = hc[jj] * cyy;
-                    dep |= (unsigned)((num > th) & (fma(th, inv_hi2, -kg) > num)) << jj;
-                }
-                tcount += __popc(live);
-                const unsigned rare = live & ~(dep & okm);
-                if (__ballot(rare != 0u)) {
-                    if (rare) {
-    #pragma unroll
-                        for (int jj = 0; jj < TG; ++jj) {
-                            if (!((rare >> jj) & 1u)) continue;
-                            const int c = cbase + jj;
-                            // recompute the decision pieces for this c (rare path)
-                            double s = Mt[c];
-    #pragma unroll
-                            for (int i = 0; i < DT; ++i) s -= lc[jj][i] * vT[i];
-                            const double vc = s * rl[jj];
-                            const double cyy = byy - vc * vc;
-                            const double cxy = bxy - uc[jj] * vc;
-                            const double cxx = hc[jj] / a.hi2;
-                            const bool ind = okc[jj] && (cxy * cxy < a.lo2 * cxx * cyy) && (cyy > 0.0) &&
-                                             (cxx * cyy - cxy * cxy > kg);
-                            const Mask Smask = Tmask | ((Mask)1 << c);
-                            if (ind) {
-                                ++indep;
-                                lmask_atomic_or<WIDE>(&uself[t], Smask);
-                                if (((lm & Smask) == Smask) && t >= tx) lmask_atomic_or<WIDE>(&uprop[t], Smask);
-                            } else {
-                                int sg[DM];
-                                sg[0] = nxs[c];
-    #pragma unroll
-                                for (int i = 0; i < DT; ++i) sg[i + 1] = nxs[T[i]];
-                                push_deferred(a, x, nxs[t], sg, DM);
+#pragma unroll
+                for (int k = 0; k < YU; ++k) {
+                    const int t = tt[k];
+                    tcount += __popc(live[k]);
+                    const unsigned rare = live[k] & ~(dep[k] & okm);
+                    if (__ballot(rare != 0u)) {
+                        if (rare) {
+                            const double *Mt = M + t * DS;
+                            const Mask lm = lmv[k];
+#pragma unroll
+                            for (int jj = 0; jj < TG; ++jj) {
+                                if (!((rare >> jj) & 1u)) continue;
+                                const int c = cbase + jj;
+                                // recompute the decision pieces for this c (rare path)
+                                double s = Mt[c];
+#pragma unroll
+                                for (int i = 0; i < DT; ++i) s -= lc[jj][i] * projv[k][i];
+                                const double vc = s * rl[jj];
+                                const double cyy = byy[k] - vc * vc;
+                                const double cxy = bxy[k] - uc[jj] * vc;
+                                const double cxx = hc[jj] / a.hi2;
+                                const bool ind = okc[jj] && (cxy * cxy < a.lo2 * cxx * cyy) && (cyy > 0.0) &&
+                                                 (cxx * cyy - cxy * cxy > kg);
+                                const Mask Smask = Tmask | ((Mask)1 << c);
+                                if (ind) {
+                                    ++indep;
+                                    lmask_atomic_or<WIDE>(&uself[t], Smask);
+                                    if (((lm & Smask) == Smask) && t >= tx) lmask_atomic_or<WIDE>(&uprop[t], Smask);
+                                } else {
+                                    int sg[DM];
+                                    sg[0] = nxs[c];
+#pragma unroll
+                                    for (int i = 0; i < DT; ++i) sg[i + 1] = nxs[T[i]];
+                                    push_deferred(a, x, nxs[t], sg, DM);
+                                }
                             }
                         }
                     }
@@ -1372,7 +1422,11 @@ __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_
         else if (nmax == 3) sweep(std::integral_constant<int, 3>{});
         else if (nmax == 2) sweep(std::integral_constant<int, 2>{});
         else sweep(std::integral_constant<int, 1>{});
-        } else {   // even counts: the slots past a lane's valid candidates are masked out of `live`
+        } else if constexpr (TG == 6) {   // even counts: slots past a lane's candidates are not `live`
+        if (nmax > 4) sweep(std::integral_constant<int, 6>{});
+        else if (nmax > 2) sweep(std::integral_constant<int, 4>{});
+        else sweep(std::integral_constant<int, 2>{});
+        } else {
         if (nmax > 6) sweep(std::integral_constant<int, 8>{});
         else if (nmax > 4) sweep(std::integral_constant<int, 6>{});
         else if (nmax > 2) sweep(std::integral_constant<int, 4>{});

@@ -23,7 +23,7 @@ def _rows(rng, n, count, dmax):
 
 
 @pytest.mark.parametrize("n,N,cmax,dmax,gsq", [(8, 1500, 5, 3, False), (12, 4000, 3, 4, False), (6, 800, 5, 2, True),
-                                               (7, 3000, 6, 4, False)])
+                                               (7, 3000, 6, 4, False), (9, 20000, 8, 4, False)])
 def test_chisq_batch_matches_oracle(n, N, cmax, dmax, gsq):
     import torch
     from rcaeval_amd.engine import get_engine
@@ -41,7 +41,10 @@ def test_chisq_batch_matches_oracle(n, N, cmax, dmax, gsq):
     for r, (a, b, S) in enumerate(keys):
         want, wdf = och.chisq_or_gsq_stat(codes[:, S + [a, b]].T, card[S + [a, b]], gsq)
         assert df[r] == wdf
-        assert stat[r] == want or abs(stat[r] - want) <= 1e-13 * abs(want), (r, stat[r], want)
+        if gsq:   # the device log may differ from glibc's in the last bit
+            assert abs(stat[r] - want) <= 1e-13 * abs(want), (r, stat[r], want)
+        else:     # numpy's blocked pairwise order: bitwise
+            assert stat[r] == want, (r, stat[r], want)
 
 
 def test_chisq_batch_refuses_bad_rows():

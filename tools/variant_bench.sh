@@ -13,7 +13,7 @@ for v in /tmp/libpcgpu_base.so tools/micro/variants/libpcgpu_*.so; do
 import json, sys
 l = [x for x in open(sys.argv[2]) if x.startswith("{")]
 d = json.loads(l[-1])
-print("%-24s value %.3e  ms %.3f  kernel_ms %s corr %s" % (sys.argv[1], d["value"], d["ms_per_step"], d["kernel_ms_per_level"], d["corr_ms"][-4:]))
+print("%-24s value %.3e  ms %.3f  kernel_ms %s level_ms %s corr %s edges %s same_fullp %s" % (sys.argv[1], d["value"], d["ms_per_step"], d["kernel_ms_per_level"], d["level_ms"], d["corr_ms"][-2:], d["edges_after"], (d.get("full_p") or {}).get("same_skeleton_as_threshold")))
 PY
 done
 cp /tmp/libpcgpu_base.so rcaeval_amd/libpcgpu.so
