@@ -47,29 +47,33 @@ def roofline_of(kernel: str, tests: int, d: int, k_ms: float) -> dict:
 
     Binding resource: VALU issue. The kernel stages each node's correlation block in LDS, so
     its HBM traffic (PMC) is ~10^3 below SURVEY §8(d)'s per-test byte model and HBM is not what
-    binds. Issue floor, from the committed PMC pass of the same kernel and workload: fp64
-    wave-instructions at 4 SIMD-cycles (78.6 TF/s fp64 = 16 FMA lanes/cycle/SIMD) and every
-    other VALU wave-instruction at 2 (32 lanes/cycle, MI355X_MICROARCH.md), over 1024 SIMDs at
-    the 2.4 GHz max clock. achieved = the issue cycles the launch needs / its live duration;
-    frac = floor / live duration. The HBM figures (measured and §8(d) algorithmic) and the
-    fp64 rate are secondary keys."""
+    binds. Measured from the committed PMC pass of the same kernel and workload:
+    ``SQ_ACTIVE_INST_VALU`` counts, per wave, the quad-cycles (4 shader cycles,
+    MI355X_MICROARCH.md constants table) in which the wave's VALU instructions occupy its SIMD;
+    summed over waves it is the SIMD-cycles the VALUs were busy. achieved = those cycles / the
+    live kernel time; peak = 1024 SIMDs x 2.4 GHz; frac = achieved / peak (the VALU-busy share
+    of the chip over the kernel). The issue-cost model it agrees with — every wave64 VALU
+    instruction, fp64 or not, 4 SIMD-cycles (tools/micro/valu_occ.hip, profiles/r02_valu_occ.log)
+    — and the HBM / fp64 figures are secondary keys."""
     ctr, src = _pmc(kernel)
     peak_gcyc = 1024 * 2.4   # G SIMD-cycles/s
-    line = {"bound": "valu", "unit": "G SIMD-issue-cycles/s", "peak": peak_gcyc, "achieved": None,
+    line = {"bound": "valu", "unit": "G SIMD-cycles/s (VALU busy)", "peak": peak_gcyc, "achieved": None,
             "frac": None, "traffic": None, "kernel": kernel, "kernel_ms": k_ms, "pmc_source": src}
     alg = tests * bytes_per_test(d)
     sec = {"hbm_contract_bytes_per_test": bytes_per_test(d),
            "hbm_contract_gbs": alg / (k_ms / 1e3) / 1e9 if k_ms > 0 else None,
            "note": "SURVEY 8(d) per-test byte model; operands are LDS-resident, so it is not a traffic figure"}
+    if k_ms > 0 and "SQ_ACTIVE_INST_VALU" in ctr:
+        busy = 4.0 * ctr["SQ_ACTIVE_INST_VALU"]
+        line["achieved"] = busy / (k_ms / 1e3) / 1e9
+        line["frac"] = line["achieved"] / peak_gcyc
+        line["valu_busy_ms_per_simd"] = busy / 1024 / 2.4e9 * 1e3
     need = ("SQ_INSTS_VALU", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64")
     if k_ms > 0 and all(k in ctr for k in need):
         valu = ctr["SQ_INSTS_VALU"]
         f64 = sum(ctr[k] for k in need[1:])
-        cycles = 4.0 * f64 + 2.0 * (valu - f64)
-        floor_ms = cycles / (peak_gcyc * 1e9) * 1e3
-        line["achieved"] = cycles / (k_ms / 1e3) / 1e9
-        line["frac"] = floor_ms / k_ms
-        line["issue_floor_ms"] = floor_ms
+        sec["issue_model_4cyc_frac"] = 4.0 * valu / (peak_gcyc * 1e9) / (k_ms / 1e3)
+        sec["issue_model_4cyc_fp64_2cyc_other_frac"] = (4.0 * f64 + 2.0 * (valu - f64)) / (peak_gcyc * 1e9) / (k_ms / 1e3)
         sec["valu_instr_per_64_tests"] = valu / (tests / 64.0) if tests else None
         sec["fp64_instr_per_64_tests"] = f64 / (tests / 64.0) if tests else None
         if "SQ_INSTS_VALU_FLOPS_FP64" in ctr:     # per wave-instruction flops -> x64 lanes
@@ -106,7 +110,7 @@ def dominant_kernel(d: int, full_p: bool) -> str:
     if d == 0:
         return f"k_level0<{1 if full_p else 0}>"
     if not full_p and 2 <= d <= 4:
-        return f"k_level_lds_t<{d}>"
+        return f"k_level_lds_t<{d}, false>"
     return f"k_level_lds<{d}, {1 if full_p else 0}>"
 
 
