@@ -130,6 +130,14 @@ int pcg_skeleton(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t
                  double alpha, int max_depth, int flags, int8_t *removed_level,
                  pcg_stats *stats);
 
+/* K1 + skeleton in one call: pcg_corr's kernels then pcg_skeleton's on the same stream, with
+ * no host round trip between them (the path pc(data) takes: FisherZ.__init__'s corrcoef, then
+ * skeleton_discovery). X: device N x n (ldx); C: device n x n out (ldc). Same results as the
+ * two calls.                                                                              */
+int pcg_pc_skeleton(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx, double *C,
+                    int64_t ldc, double alpha, int max_depth, int flags, int8_t *removed_level,
+                    pcg_stats *stats);
+
 /* Degrees at the start of each depth of the last pcg_skeleton (host out, levels x n). */
 int pcg_degrees(pcg_handle *h, int32_t *deg_host, int64_t capacity);
 

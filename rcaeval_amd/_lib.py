@@ -86,6 +86,8 @@ SIGNATURES = [
     ("pcg_corr_shard", I32, [P, P, I64, I64, I64, ctypes.c_int, ctypes.c_int, P]),
     ("pcg_corr_shard_finish", I32, [P, P, I64, I64, ctypes.c_int, P, I64]),
     ("pcg_skeleton", I32, [P, P, I64, I64, I64, D, ctypes.c_int, ctypes.c_int, P, ctypes.POINTER(PcgStats)]),
+    ("pcg_pc_skeleton", I32, [P, P, I64, I64, I64, P, I64, D, ctypes.c_int, ctypes.c_int, P,
+                          ctypes.POINTER(PcgStats)]),
     ("pcg_degrees", I32, [P, P, I64]),
     ("pcg_sepset_count", I32, [P, ctypes.POINTER(I64), ctypes.POINTER(I32)]),
     ("pcg_sepset_export", I32, [P, P, P, I64]),

@@ -285,10 +285,7 @@ def skeleton_from_data(data: np.ndarray, alpha: float = 0.05, max_depth: int = -
     """Correlation + stable skeleton on the GPU; returns (SkeletonOut, C tensor)."""
     eng = get_engine(device)
     X = np.asarray(data, dtype=np.float64)
-    C = eng.corr(X)
-    out = eng.skeleton(C, X.shape[0], alpha=alpha, max_depth=max_depth, flags=flags,
-                       record_capacity=record_capacity)
-    return out, C
+    return eng.corr_skeleton(X, alpha=alpha, max_depth=max_depth, flags=flags, record_capacity=record_capacity)
 
 
 def pc(data: np.ndarray, alpha: float = 0.05, indep_test=fisherz, stable: bool = True, uc_rule: int = 0,

@@ -82,12 +82,13 @@ extern "C" int pcg_destroy(pcg_handle *h) {
     pcg_comm_release(h);
     DevBuf *bufs[] = {&h->adj, &h->deg, &h->off, &h->nbr, &h->rm, &h->ug, &h->cpre, &h->binom, &h->ctr,
                       &h->deferred, &h->records, &h->nearbuf, &h->exportbuf, &h->export_xy, &h->diag,
-                      &h->colmean, &h->pr_scratch, &h->batch_scratch, &h->chisq_scratch};
+                      &h->colmean, &h->pr_scratch, &h->batch_scratch, &h->chisq_scratch, &h->done_ctr};
     for (DevBuf *b : bufs)
         if (b->p) hipFree(b->p);
     PinBuf *pins[] = {&h->ctr_pin, &h->deg_pin, &h->off_pin, &h->cpre_pin, &h->status_pin};
     for (PinBuf *b : pins)
         if (b->p) hipHostFree(b->p);
+    if (h->summary) hipHostFree(h->summary);
     for (auto &e : h->ev)
         if (e) hipEventDestroy(e);
     for (auto &e : h->lev)

@@ -420,8 +420,8 @@ extern "C" int pcg_corr_shard_finish(pcg_handle *h, const double *gathered, int6
     return PCG_OK;
 }
 
-extern "C" int pcg_corr(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx, double *C,
-                        int64_t ldc) {
+// K1 launched on the handle's stream without a host sync (the fused pcg_pc_skeleton path)
+int pcg_corr_launch(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx, double *C, int64_t ldc) {
     if (!h || !X || !C || N < 2 || n < 1 || ldx < n || ldc < n || n > (1 << 24))
         return pcg_fail(h, PCG_ERR_INVALID, "pcg_corr: invalid arguments");
     PCG_HIP(h, hipSetDevice(h->device));
@@ -450,6 +450,13 @@ extern "C" int pcg_corr(pcg_handle *h, const double *X, int64_t N, int64_t n, in
     hipLaunchKernelGGL(k_normalize_tiles, dim3(T64 * (T64 + 1) / 2), dim3(256), 0, h->stream, G, ldg, stride, ks, C,
                        ldc, nn, scale, sd);
     PCG_HIP(h, hipGetLastError());
+    return PCG_OK;
+}
+
+extern "C" int pcg_corr(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx, double *C,
+                        int64_t ldc) {
+    const int rc = pcg_corr_launch(h, X, N, n, ldx, C, ldc);
+    if (rc) return rc;
     PCG_HIP(h, hipStreamSynchronize(h->stream));
     return PCG_OK;
 }

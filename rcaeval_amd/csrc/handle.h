@@ -32,6 +32,13 @@ struct DevCounters {
     unsigned long long error;      // PCG_ERR_* bits (1 singular, 2 domain)
 };
 
+// host-mapped per-level summary (k_level_summary); n int32 degrees follow the struct
+struct LevelSummary {
+    DevCounters ctr;
+    uint8_t status[8];
+    unsigned long long seq;        // written last, after a system-scope fence
+};
+
 struct DeferredEntry {             // one test routed to the exact (LU) path
     int32_t x, y;                  // visiting node x, neighbour y
     int32_t s[PCG_MAX_DEPTH];      // conditioning set (global ids)
@@ -78,6 +85,11 @@ struct pcg_handle {
     bool tgroup = false;             // small class runs k_level_lds_t this depth
     int32_t maxdeg = 0;
     int64_t sumdeg = 0;
+    LevelSummary *summary = nullptr;    // host-mapped, coherent (graph_launch / level_wait)
+    size_t summary_bytes = 0;
+    unsigned long long summary_seq = 0;
+    DevBuf done_ctr;                    // k_level_summary's last-block counter
+    bool done_ready = false;
     std::vector<int32_t> deg_h;      // degrees at the start of the current depth
     std::vector<int32_t> deg_levels; // levels x n
     std::vector<int64_t> cpre_h;     // 3 x (n + 1): narrow, wide, large class chunk prefixes
@@ -99,6 +111,8 @@ struct pcg_handle {
 };
 
 void pcg_comm_release(pcg_handle *h);      // comm.hip: destroy the communicator, free its buffers
+// corr.hip: K1 queued on h->stream without the host sync of pcg_corr (pcg_pc_skeleton)
+int pcg_corr_launch(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx, double *C, int64_t ldc);
 
 int pcg_fail(pcg_handle *h, int code, const char *fmt, ...);
 bool pcg_ensure(pcg_handle *h, DevBuf &b, size_t bytes);   // grow-only allocation

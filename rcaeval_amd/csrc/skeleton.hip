@@ -218,12 +218,56 @@ __global__ void k_diag(const double *C, int64_t ldc, int n, double *diag) {
     if (i < n) diag[i] = C[(int64_t)i * ldc + i];
 }
 
-__global__ void k_degrees(const uint64_t *adj, int n, int W, int32_t *deg) {
+// The level barrier's host summary, written by the device straight into host-mapped memory:
+// degrees (also kept on the device for the next depth), the level counters, the merged status
+// bytes, then — after every block's writes are visible system-wide — the sequence number the host
+// spins on. Replaces three device-to-host copies and a stream synchronisation per depth.
+__global__ __launch_bounds__(256) void k_level_summary(const uint64_t *adj, int n, int W, int32_t *deg,
+                                                       const DevCounters *ctr, const uint8_t *status,
+                                                       LevelSummary *out, int32_t *out_deg, unsigned *done,
+                                                       unsigned long long seq) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= n) return;
-    int c = 0;
-    for (int w = 0; w < W; ++w) c += __popcll(adj[(int64_t)x * W + w]);
-    deg[x] = c;
+    if (x < n) {
+        int c = 0;
+        for (int w = 0; w < W; ++w) c += __popcll(adj[(int64_t)x * W + w]);
+        deg[x] = c;
+        out_deg[x] = c;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        out->ctr = *ctr;
+        for (int k = 0; k < 8; ++k) out->status[k] = status ? status[k] : 0;
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned prev = atomicAdd(done, 1u);
+        if (prev == gridDim.x - 1) {        // the last block: every block's writes are fenced
+            __threadfence_system();
+            atomicExch(done, 0u);
+            __atomic_store_n(&out->seq, seq, __ATOMIC_RELEASE);
+        }
+    }
+}
+
+// CSR offsets off[0..n] = exclusive prefix of deg (one block, 1024 threads, chunked scan)
+__global__ __launch_bounds__(1024) void k_offsets(const int32_t *deg, int n, int32_t *off) {
+    __shared__ int32_t part[1024];
+    const int tid = threadIdx.x;
+    const int per = (n + 1023) / 1024;
+    const int lo = min(n, tid * per), hi = min(n, lo + per);
+    int32_t s = 0;
+    for (int i = lo; i < hi; ++i) s += deg[i];
+    part[tid] = s;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {       // inclusive Hillis-Steele scan of the chunk sums
+        const int32_t v = tid >= o ? part[tid - o] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    int32_t acc = tid ? part[tid - 1] : 0;
+    for (int i = lo; i < hi; ++i) { off[i] = acc; acc += deg[i]; }
+    if (tid == 1023) off[n] = part[1023];
 }
 
 // one wave per node: ascending neighbour list from the bitmask (wave prefix scan)
@@ -763,14 +807,18 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
         const int t = e / D, k = e - t * D;
         M[e] = a.C[(int64_t)nxs[t] * a.ldc + nxs[k]];
     }
+    // local adjacency masks: one wave per row t, the wave's ballot over lanes k (D <= 64)
+    for (int t = tid >> 6; t < D; t += bs >> 6) {
+        const int k = tid & 63;
+        const uint64_t *ar = a.adj + (int64_t)nxs[t] * a.W;
+        const bool bit = k < D && ((ar[nxs[k] >> 6] >> (nxs[k] & 63)) & 1ull);
+        const unsigned long long m = __ballot(bit);
+        if (k == 0) lmask[t] = m;
+    }
     for (int t = tid; t < D; t += bs) {
         const int yg = nxs[t];
         Mx[t] = a.C[(int64_t)x * a.ldc + yg];
         Md[t] = a.diag[yg];
-        const uint64_t *ar = a.adj + (int64_t)yg * a.W;
-        unsigned long long m = 0;
-        for (int k = 0; k < D; ++k) m |= ((ar[nxs[k] >> 6] >> (nxs[k] & 63)) & 1ull) << k;
-        lmask[t] = m;
         uself[t] = 0;
         uprop[t] = 0;
     }
@@ -1127,14 +1175,22 @@ __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_
         const int t = e / DS, k = e - t * DS;
         M[e] = k < D ? a.C[(int64_t)nxs[t] * a.ldc + nxs[k]] : 0.0;
     }
+    // local adjacency masks: one wave per row t, lane k reads the bit adj(nxs[t], nxs[k]) and the
+    // wave's ballot is the row's 64-bit word (64 independent loads in flight per row)
+    for (int t = tid >> 6; t < D; t += bs >> 6) {
+        const uint64_t *ar = a.adj + (int64_t)nxs[t] * a.W;
+        Mask m = 0;
+        for (int k0 = 0; k0 < D; k0 += 64) {
+            const int k = k0 + (tid & 63);
+            const bool bit = k < D && ((ar[nxs[k] >> 6] >> (nxs[k] & 63)) & 1ull);
+            m |= (Mask)__ballot(bit) << k0;
+        }
+        if ((tid & 63) == 0) lmask[t] = m;
+    }
     for (int t = tid; t < D; t += bs) {
         const int yg = nxs[t];
         Mx[t] = a.C[(int64_t)x * a.ldc + yg];
         Md[t] = a.diag[yg];
-        const uint64_t *ar = a.adj + (int64_t)yg * a.W;
-        Mask m = 0;
-        for (int k = 0; k < D; ++k) m |= (Mask)((ar[nxs[k] >> 6] >> (nxs[k] & 63)) & 1ull) << k;
-        lmask[t] = m;
         uself[t] = 0;
         uprop[t] = 0;
     }
@@ -1771,36 +1827,75 @@ int mode_of(const pcg_handle *h, int d) {
     return MODE_DECIDE;
 }
 
-// degrees of the current adjacency -> page-locked host mirror (async; the caller syncs)
+// the level summary (degrees, counters, status) of the current adjacency -> host-mapped memory;
+// level_wait() spins until the device has written it
 int graph_launch(pcg_handle *h) {
     const int n = (int)h->n, W = h->W;
-    if (!pcg_ensure_pinned(h, h->deg_pin, sizeof(int32_t) * n)) return pcg_fail(h, PCG_ERR_OOM, "pinned degrees");
-    hipLaunchKernelGGL(k_degrees, dim3((n + 255) / 256), dim3(256), 0, h->stream,
-                       (const uint64_t *)h->adj.p, n, W, (int32_t *)h->deg.p);
-    PCG_HIP(h, hipMemcpyAsync(h->deg_pin.p, h->deg.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, h->stream));
+    const size_t bytes = sizeof(LevelSummary) + sizeof(int32_t) * (size_t)n;
+    if (!h->summary || h->summary_bytes < bytes) {
+        if (h->summary) { (void)hipStreamSynchronize(h->stream); (void)hipHostFree(h->summary); }
+        h->summary = nullptr;
+        h->summary_bytes = 0;
+        void *p = nullptr;
+        if (hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+            return pcg_fail(h, PCG_ERR_OOM, "host-mapped level summary");
+        h->summary = (LevelSummary *)p;
+        h->summary_bytes = bytes;
+        h->summary->seq = 0;
+        h->summary_seq = 0;
+    }
+    if (!pcg_ensure(h, h->done_ctr, 16)) return pcg_fail(h, PCG_ERR_OOM, "summary counter");
+    if (!h->done_ready) {
+        PCG_HIP(h, hipMemsetAsync(h->done_ctr.p, 0, 16, h->stream));
+        h->done_ready = true;
+    }
+    void *dsum = nullptr;
+    PCG_HIP(h, hipHostGetDevicePointer(&dsum, h->summary, 0));
+    LevelSummary *ds = (LevelSummary *)dsum;
+    const uint8_t *status = h->depth >= 0 ? (h->rm_ext ? h->rm_ext : (const uint8_t *)h->rm.p) + (int64_t)n * n : nullptr;
+    const unsigned long long seq = ++h->summary_seq;
+    hipLaunchKernelGGL(k_level_summary, dim3((n + 255) / 256), dim3(256), 0, h->stream, (const uint64_t *)h->adj.p, n,
+                       W, (int32_t *)h->deg.p, (const DevCounters *)h->ctr.p, status, ds,
+                       reinterpret_cast<int32_t *>(ds + 1), (unsigned *)h->done_ctr.p, seq);
+    PCG_HIP(h, hipGetLastError());
     return PCG_OK;
 }
 
-// after the sync: host degrees, CSR offsets (uploaded async), ascending neighbour lists
+// spin until the summary of the last graph_launch is visible (a stream error or a stream that
+// finished without it ends the wait with an error instead of hanging)
+int level_wait(pcg_handle *h) {
+    const unsigned long long want = h->summary_seq;
+    unsigned spins = 0;
+    while (__atomic_load_n(&h->summary->seq, __ATOMIC_ACQUIRE) != want) {
+        if ((++spins & 1023) == 0) {
+            const hipError_t e = hipStreamQuery(h->stream);
+            if (e == hipSuccess) {
+                if (__atomic_load_n(&h->summary->seq, __ATOMIC_ACQUIRE) == want) break;
+                return pcg_fail(h, PCG_ERR_HIP, "level summary not written (seq %llu)", want);
+            }
+            if (e != hipErrorNotReady) return pcg_fail(h, PCG_ERR_HIP, "stream error: %s", hipGetErrorString(e));
+        }
+        __builtin_ia32_pause();
+    }
+    return PCG_OK;
+}
+
+// after the wait: host degrees, CSR offsets (device scan), ascending neighbour lists
 int graph_finish(pcg_handle *h) {
     const int n = (int)h->n, W = h->W;
-    const int32_t *dp = (const int32_t *)h->deg_pin.p;
+    const int32_t *dp = reinterpret_cast<const int32_t *>(h->summary + 1);
     h->deg_h.assign(dp, dp + n);
-    if (!pcg_ensure_pinned(h, h->off_pin, sizeof(int32_t) * (n + 1))) return pcg_fail(h, PCG_ERR_OOM, "pinned offsets");
-    int32_t *off = (int32_t *)h->off_pin.p;
     int64_t s = 0;
     int32_t mx = 0;
     for (int i = 0; i < n; ++i) {
-        off[i] = (int32_t)s;
         s += dp[i];
         mx = std::max(mx, dp[i]);
     }
-    off[n] = (int32_t)s;
     h->sumdeg = s;
     h->maxdeg = mx;
     if (!pcg_ensure(h, h->off, sizeof(int32_t) * (n + 1))) return PCG_ERR_OOM;
     if (!pcg_ensure(h, h->nbr, sizeof(int32_t) * std::max<int64_t>(s, 1))) return PCG_ERR_OOM;
-    PCG_HIP(h, hipMemcpyAsync(h->off.p, off, sizeof(int32_t) * (n + 1), hipMemcpyHostToDevice, h->stream));
+    hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, h->stream, (const int32_t *)h->deg.p, n, (int32_t *)h->off.p);
     hipLaunchKernelGGL(k_fill_nbr, dim3(n), dim3(64), 0, h->stream, (const uint64_t *)h->adj.p, n, W,
                        (const int32_t *)h->off.p, (int32_t *)h->nbr.p);
     PCG_HIP(h, hipGetLastError());
@@ -1858,8 +1953,8 @@ extern "C" int pcg_skeleton_init(pcg_handle *h, const double *C, int64_t n, int6
     PCG_HIP(h, hipMemsetAsync(removed_level, 0xFF, (size_t)n * n, h->stream));
     PCG_HIP(h, hipGetLastError());
     int rc = graph_launch(h);
+    if (!rc) rc = level_wait(h);
     if (rc) return rc;
-    PCG_HIP(h, hipStreamSynchronize(h->stream));
     return graph_finish(h);
 }
 
@@ -2226,17 +2321,19 @@ extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
     hipLaunchKernelGGL(k_apply, dim3((unsigned)((nw * 64 + 255) / 256)), dim3(256), 0, h->stream, (const uint8_t *)rmb,
                        (uint64_t *)h->adj.p, h->rl, n, W, d);
     PCG_HIP(h, hipGetLastError());
-    int rc = graph_launch(h);
+    int rc = graph_launch(h);            // degrees + counters + status -> host-mapped summary
+    if (!rc) rc = level_wait(h);
     if (rc) return rc;
-    if (!pcg_ensure_pinned(h, h->ctr_pin, sizeof(DevCounters)) || !pcg_ensure_pinned(h, h->status_pin, 16))
-        return pcg_fail(h, PCG_ERR_OOM, "pinned counters");
-    PCG_HIP(h, hipMemcpyAsync(h->ctr_pin.p, ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, h->stream));
-    PCG_HIP(h, hipMemcpyAsync(h->status_pin.p, rmb + (int64_t)n * n, 4, hipMemcpyDeviceToHost, h->stream));
-    PCG_HIP(h, hipStreamSynchronize(h->stream));
-    const DevCounters c = *(const DevCounters *)h->ctr_pin.p;
-    const uint8_t *status = (const uint8_t *)h->status_pin.p;
+    const DevCounters c = h->summary->ctr;
+    uint8_t status[8];
+    for (int k = 0; k < 8; ++k) status[k] = h->summary->status[k];
     if (h->run_timed) {
-        PCG_HIP(h, hipEventElapsedTime(&h->run_ms, h->ev[2], h->ev[3]));
+        hipError_t e = hipEventElapsedTime(&h->run_ms, h->ev[2], h->ev[3]);
+        if (e == hipErrorNotReady) {        // the summary can land before the runtime marks the event
+            PCG_HIP(h, hipEventSynchronize(h->ev[3]));
+            e = hipEventElapsedTime(&h->run_ms, h->ev[2], h->ev[3]);
+        }
+        PCG_HIP(h, e);
         h->run_timed = false;
     }
     // records / near-alpha to host (parity runs; before the next level reuses the buffers)
@@ -2331,6 +2428,14 @@ extern "C" int pcg_skeleton(pcg_handle *h, const double *C, int64_t n, int64_t l
     }
     if (stats && h) *stats = h->st;
     return rc;
+}
+
+extern "C" int pcg_pc_skeleton(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx, double *C,
+                               int64_t ldc, double alpha, int max_depth, int flags, int8_t *removed_level,
+                               pcg_stats *stats) {
+    const int rc = pcg_corr_launch(h, X, N, n, ldx, C, ldc);     // stream-ordered: no host sync between
+    if (rc) return rc;
+    return pcg_skeleton(h, C, n, ldc, N, alpha, max_depth, flags, removed_level, stats);
 }
 
 extern "C" int pcg_degrees(pcg_handle *h, int32_t *deg_host, int64_t capacity) {

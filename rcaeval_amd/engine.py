@@ -213,6 +213,31 @@ class Engine:
         out.extra["device_ms"] = out.device_ms
         return out
 
+    def corr_skeleton(self, X, alpha: float = 0.05, max_depth: int = -1, flags: int = 0, record_capacity: int = 0):
+        """K1 + stable skeleton in one C call (``pcg_pc_skeleton``); returns (SkeletonOut, C)."""
+        torch = _torch()
+        Xd = self.to_device(X)
+        N, n = Xd.shape
+        C = torch.empty((n, n), dtype=torch.float64, device=self.device)
+        rl = torch.empty((n, n), dtype=torch.int8, device=self.device)
+        if record_capacity:
+            check(self.h, self.lib.pcg_set_capacity(self.h, int(record_capacity), 0), "pcg_set_capacity")
+        check(self.h, self.lib.pcg_set_record_sample(self.h, 0, 0), "pcg_set_record_sample")
+        st = PcgStats()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        rc = self.lib.pcg_pc_skeleton(self.h, ctypes.c_void_p(Xd.data_ptr()), N, n, n, ctypes.c_void_p(C.data_ptr()),
+                                      n, float(alpha), int(max_depth), int(flags), ctypes.c_void_p(rl.data_ptr()),
+                                      ctypes.byref(st))
+        ev1.record()
+        check(self.h, rc, "pcg_pc_skeleton")
+        self.sync()
+        t0 = time.perf_counter()
+        out = self._collect(n, rl, st, ev0.elapsed_time(ev1))
+        out.extra["collect_ms"] = 1000.0 * (time.perf_counter() - t0)
+        out.extra["device_ms"] = out.device_ms
+        return out, C
+
     def _collect(self, n: int, rl, st: PcgStats, device_ms: float) -> SkeletonOut:
         L = st.levels
         deg = np.zeros((max(L, 1), n), np.int32)
