@@ -92,15 +92,20 @@ def roofline_of(kernel: str, tests: int, d: int, k_ms: float) -> dict:
     return line
 
 
+K1_TILE = 64                  # corr.hip PCG_K1_TILE
+MFMA_F64_MEASURED_TFLOPS = 47.9   # v_mfma_f64_16x16x4_f64 at 4 waves/SIMD, tools/micro/mfma_f64.hip (profiles/r02_mfma_f64.log)
+
+
 def k1_roofline(n: int, N: int, corr_ms: float) -> dict:
     """K1 (np.corrcoef) on fp64 MFMA: 2 N n^2 algorithmic flop; the kernel multiplies the
-    upper-triangle 128 x 128 tiles only (T(T+1)/2 tiles, T = ceil(n/128))."""
-    T = (n + 127) // 128
-    mfma_flop = T * (T + 1) // 2 * 128 * 128 * 2.0 * N
+    upper-triangle K1_TILE-square tiles only (T(T+1)/2 tiles, T = ceil(n/K1_TILE))."""
+    T = (n + K1_TILE - 1) // K1_TILE
+    mfma_flop = T * (T + 1) // 2 * K1_TILE * K1_TILE * 2.0 * N
+    ex = mfma_flop / (corr_ms / 1e3) / 1e12
     return {"bound": "mfma", "unit": "TFLOP/s", "peak": FP64_PEAK_TFLOPS, "ms": corr_ms,
             "achieved_algorithmic": 2.0 * N * n * n / (corr_ms / 1e3) / 1e12,
-            "achieved_executed": mfma_flop / (corr_ms / 1e3) / 1e12,
-            "frac": mfma_flop / (corr_ms / 1e3) / 1e12 / FP64_PEAK_TFLOPS,
+            "achieved_executed": ex, "frac": ex / FP64_PEAK_TFLOPS,
+            "frac_of_measured_instruction_ceiling": ex / MFMA_F64_MEASURED_TFLOPS,
             "what": "pcg_corr end to end (column means, split-K k_xtx, fused normalisation)"}
 
 

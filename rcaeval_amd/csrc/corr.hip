@@ -6,12 +6,17 @@
 //   s = sqrt(diag(c)); c /= s[:, None]; c /= s[None, :]; clip(c, -1, 1)
 // X here is the caller's N x n (time x metrics) array, so c = Xc^T Xc.
 //
-// GEMM: 128 x 128 output tile per 256-thread block (4 waves, 64 x 64 per wave = 4 x 4
-// v_mfma_f64_16x16x4_f64 tiles, 64 accumulator doubles per lane), K (time) staged through
-// LDS in 8-row slabs, double buffered; the mean subtraction is fused into the staging load. Only upper-triangle
-// tiles are computed (c is symmetric) and only their upper triangle is written; the
-// normalisation mirrors it (k_normalize_tiles). Roofline: MFMA fp64
-// (2*N*n^2 flops); bytes 8*N*n*(n/64) staged per tile row, L2-served.
+// GEMM: 64 x 64 output tile per 256-thread block (2 x 2 waves, 32 x 32 per wave = 2 x 2
+// v_mfma_f64_16x16x4_f64 tiles), K (time) staged through LDS in 4-row slabs, double buffered,
+// with the mean subtraction fused into the staging load. Only upper-triangle tiles are computed
+// (c is symmetric) and only their upper triangle is written; the normalisation mirrors it
+// (k_normalize_tiles, which also takes sd from the slab diagonals). K is split into fixed slabs
+// (a function of n and N only, so every world size sums the same slabs in the same order);
+// ~4096 blocks at n = 2000 (528 tiles x 8 slabs) keep ~8 small blocks resident per CU, which
+// hides the staging latency far better than 128 x 128 tiles at 2 blocks per CU. Blocks are
+// ordered XCD-major (blockIdx % 8 is the XCD the dispatcher picks), so each XCD walks whole
+// slabs and reads its rows of X from HBM about once instead of once per XCD.
+// Roofline: MFMA fp64 (2*N*n^2 algorithmic flops; the upper-tile work 528 * 16 * N/4 MFMAs).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -23,9 +28,20 @@ namespace {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-constexpr int TILE = 128;
+#ifndef PCG_K1_TILE
+#define PCG_K1_TILE 64
+#endif
+#ifndef PCG_K1_XCD
+#define PCG_K1_XCD 1        // 1: XCD-major block order (each XCD walks whole split-K slabs)
+#endif
+#ifndef PCG_K1_KS
+#define PCG_K1_KS 0         // >0: force the split-K slab count (experiments)
+#endif
+constexpr int TILE = PCG_K1_TILE;
+constexpr int WT = TILE / 32;          // 16x16 MFMA tiles per wave dimension (2 x 2 waves per block)
+constexpr int RS = 256 / TILE;         // staging row step
 #ifndef PCG_K1_BLOCKS
-#define PCG_K1_BLOCKS 2048       // target k_xtx grid (tiles x split-K slabs)
+#define PCG_K1_BLOCKS 4096       // target k_xtx grid (tiles x split-K slabs)
 #endif
 #ifndef PCG_K1_MAXKS
 #define PCG_K1_MAXKS 16
@@ -37,14 +53,14 @@ constexpr int TILE = 128;
 #define PCG_K1_MINROWS 32   // fewest rows per split-K slab
 #endif
 #ifndef PCG_K1_KT
-#define PCG_K1_KT 8
+#define PCG_K1_KT 4
 #endif
 constexpr int KT = PCG_K1_KT;
 constexpr int PAD = 1;  // LDS row padding (doubles) against bank conflicts
 constexpr int MEAN_ROWS = 64;   // rows per partial column sum (N = 10k: 157 chunks x 8 column blocks)
 
 // partial column sums over row chunks (deterministic two-pass mean)
-__global__ void k_colsum_partial(const double *X, int64_t N, int n, int64_t ldx, double *part) {
+__global__ __launch_bounds__(256) void k_colsum_partial(const double *X, int64_t N, int n, int64_t ldx, double *part) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t r0 = (int64_t)blockIdx.y * MEAN_ROWS;
     if (j >= n) return;
@@ -62,12 +78,29 @@ __global__ void k_colsum_partial(const double *X, int64_t N, int n, int64_t ldx,
     part[(int64_t)blockIdx.y * n + j] = s;
 }
 
-__global__ void k_colmean(const double *part, int nchunks, int n, int64_t N, double *mean) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
+// mean_j = (sum of the chunk partials) / N: 64 columns per block, the 4 waves take contiguous
+// quarters of the chunk list (8 loads in flight each), quarters added in order through LDS
+__global__ __launch_bounds__(256) void k_colmean(const double *part, int nchunks, int n, int64_t N, double *mean) {
+    __shared__ double q4[4][64];
+    const int c = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int j = blockIdx.x * 64 + c;
+    const int per = (nchunks + 3) / 4;
+    const int lo = std::min(nchunks, w * per), hi = std::min(nchunks, lo + per);
     double s = 0.0;
-    for (int c = 0; c < nchunks; ++c) s += part[(int64_t)c * n + j];
-    mean[j] = s / (double)N;
+    if (j < n) {
+        int k = lo;
+        for (; k + 8 <= hi; k += 8) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(k + u) * n + j];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += v[u];
+        }
+        for (; k < hi; ++k) s += part[(int64_t)k * n + j];
+    }
+    q4[w][c] = s;
+    __syncthreads();
+    if (w == 0 && j < n) mean[j] = (((q4[0][c] + q4[1][c]) + q4[2][c]) + q4[3][c]) / (double)N;
 }
 
 __device__ __forceinline__ void tile_of(int t, int T, int &bi, int &bj) {
@@ -81,48 +114,53 @@ __device__ __forceinline__ void tile_of(int t, int T, int &bi, int &bj) {
 // tl == nullptr: all upper-triangle tiles, upper triangle into G (single GPU). Otherwise tl lists
 // (bi, bj, packed tile row) triples of one rank's share: rows go to packed position, no mirror.
 __global__ __launch_bounds__(256) void k_xtx(const double *X, int64_t N, int n, int64_t ldx,
-                                            const double *mean, int ntiles, int64_t kchunk, double *G,
-                                            int64_t ldg, int64_t slab_stride, const int32_t *tl) {
+                                            const double *mean, int ntiles, int nslabs, int64_t kchunk,
+                                            double *G, int64_t ldg, int64_t slab_stride, const int32_t *tl) {
     __shared__ double As[2][KT][TILE + PAD];
     __shared__ double Bs[2][KT][TILE + PAD];
     const int T = (n + TILE - 1) / TILE;
     int bi, bj, pbi = -1;
+    int lin = blockIdx.x;
+    if (PCG_K1_XCD) {       // blocks go round-robin over the 8 XCDs: give XCD x a contiguous run
+        const int per = gridDim.x / 8;
+        lin = (blockIdx.x % 8) * per + blockIdx.x / 8;
+        if (lin >= ntiles * nslabs) return;
+    }
     if (tl) {
-        const int t = blockIdx.x % ntiles;
+        const int t = lin % ntiles;
         bi = tl[3 * t];
         bj = tl[3 * t + 1];
         pbi = tl[3 * t + 2];
     } else {
-        tile_of(blockIdx.x % ntiles, T, bi, bj);
+        tile_of(lin % ntiles, T, bi, bj);
     }
-    const int slab = blockIdx.x / ntiles;           // split-K slice
+    const int slab = lin / ntiles;                  // split-K slice
     const int64_t kbeg = (int64_t)slab * kchunk;
     const int64_t kend = std::min<int64_t>(N, kbeg + kchunk);
     G += (int64_t)slab * slab_stride;
     const int i0 = bi * TILE, j0 = bj * TILE;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wr = (wave >> 1) * 64, wc = (wave & 1) * 64;
+    const int wr = (wave >> 1) * (TILE / 2), wc = (wave & 1) * (TILE / 2);
 
-    // staging: KT x 128 slab per operand, KT/2 per thread (one 1-KiB row segment per wave and
-    // k-row: coalesced)
-    const int sc = tid & 127;         // column within the tile
-    const int sr = tid >> 7;          // rows sr, sr+2, ..., sr+KT-2
+    // staging: KT x TILE slab per operand, KT/RS rows per thread (coalesced row segments)
+    const int sc = tid % TILE;        // column within the tile
+    const int sr = tid / TILE;        // rows sr, sr+RS, ...
     const double ma = (i0 + sc < n) ? mean[i0 + sc] : 0.0;
     const double mb = (j0 + sc < n) ? mean[j0 + sc] : 0.0;
     const bool va = i0 + sc < n, vb = j0 + sc < n;
 
-    // each wave owns a 64 x 64 sub-tile = 4 x 4 MFMA 16x16 tiles (64 accumulator doubles)
-    d4 acc[4][4];
+    // each wave owns a TILE/2 square sub-tile = WT x WT MFMA 16x16 tiles
+    d4 acc[WT][WT];
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < WT; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+        for (int b = 0; b < WT; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
 
-    double ra[KT / 2], rb[KT / 2];
+    double ra[KT / RS], rb[KT / RS];
     auto load = [&](int64_t t0) {
 #pragma unroll
-        for (int q = 0; q < KT / 2; ++q) {
-            const int64_t t = t0 + sr + 2 * q;
+        for (int q = 0; q < KT / RS; ++q) {
+            const int64_t t = t0 + sr + RS * q;
             const bool vt = t < kend;
             ra[q] = (vt && va) ? X[t * ldx + i0 + sc] - ma : 0.0;
             rb[q] = (vt && vb) ? X[t * ldx + j0 + sc] - mb : 0.0;
@@ -130,9 +168,9 @@ __global__ __launch_bounds__(256) void k_xtx(const double *X, int64_t N, int n, 
     };
     auto store = [&](int buf) {
 #pragma unroll
-        for (int q = 0; q < KT / 2; ++q) {
-            As[buf][sr + 2 * q][sc] = ra[q];
-            Bs[buf][sr + 2 * q][sc] = rb[q];
+        for (int q = 0; q < KT / RS; ++q) {
+            As[buf][sr + RS * q][sc] = ra[q];
+            Bs[buf][sr + RS * q][sc] = rb[q];
         }
     };
 
@@ -146,16 +184,16 @@ __global__ __launch_bounds__(256) void k_xtx(const double *X, int64_t N, int n, 
         if (kk + 1 < nk) load(kbeg + (kk + 1) * KT);
 #pragma unroll
         for (int k4 = 0; k4 < KT; k4 += 4) {
-            double av[4], bv[4];
+            double av[WT], bv[WT];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < WT; ++q) {
                 av[q] = As[buf][k4 + fk][wr + 16 * q + fr];
                 bv[q] = Bs[buf][k4 + fk][wc + 16 * q + fr];
             }
 #pragma unroll
-            for (int a = 0; a < 4; ++a)
+            for (int a = 0; a < WT; ++a)
 #pragma unroll
-                for (int b = 0; b < 4; ++b)
+                for (int b = 0; b < WT; ++b)
                     acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
         }
         if (kk + 1 < nk) store(buf ^ 1);
@@ -163,9 +201,9 @@ __global__ __launch_bounds__(256) void k_xtx(const double *X, int64_t N, int n, 
     }
     // epilogue: C/D map of v_mfma_f64_16x16x4_f64: col = lane & 15, row = (lane >> 4) + 4 * r
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < WT; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b)
+        for (int b = 0; b < WT; ++b)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int i = i0 + wr + 16 * a + (lane >> 4) + 4 * r;
@@ -181,26 +219,23 @@ __global__ __launch_bounds__(256) void k_xtx(const double *X, int64_t N, int n, 
             }
 }
 
-// sd_i = sqrt(c_ii) with c = (sum of split-K slabs) * 1/(N-1)
-__global__ void k_stddev(const double *G, int64_t ldg, int64_t slab_stride, int ks, int n, double scale,
-                         double *sd) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    double v = 0.0;
-    for (int s = 0; s < ks; ++s) v += G[(int64_t)s * slab_stride + (int64_t)i * ldg + i];
-    sd[i] = sqrt(v * scale);
-}
-
 // C_ij = clip(((sum_s G_s,ij) * 1/(N-1) / sd_i) / sd_j, -1, 1)   (numpy corrcoef order)
 // G holds the upper triangle only (i <= j). One block per 64 x 64 tile pair (bi <= bj): the
 // slab sums of the upper tile go through LDS so both C[i][j] and C[j][i] are written as
 // coalesced rows; each side keeps numpy's own division order ((g * scale) / sd_row) / sd_col,
 // so C is not forced to be bitwise symmetric (numpy's is not either).
 constexpr int NT = 64;
+__device__ __forceinline__ double slab_diag_sd(const double *G, int64_t ldg, int64_t slab_stride, int ks, int i,
+                                               double scale) {
+    double v = 0.0;    // sd_i = sqrt(c_ii), c = (sum of split-K slabs in slab order) * 1/(N-1)
+    for (int s = 0; s < ks; ++s) v += G[(int64_t)s * slab_stride + (int64_t)i * ldg + i];
+    return sqrt(v * scale);
+}
+
 __global__ __launch_bounds__(256) void k_normalize_tiles(const double *G, int64_t ldg, int64_t slab_stride, int ks,
-                                                         double *C, int64_t ldc, int n, double scale,
-                                                         const double *sd) {
+                                                         double *C, int64_t ldc, int n, double scale) {
     __shared__ double t[NT][NT + 1];
+    __shared__ double sdr[NT], sdc[NT];
     const int T = (n + NT - 1) / NT;
     int bi = 0, bj = 0;
     {   // upper-triangle tile index -> (bi, bj), row-major over bi
@@ -210,6 +245,8 @@ __global__ __launch_bounds__(256) void k_normalize_tiles(const double *G, int64_
     }
     const int i0 = bi * NT, j0 = bj * NT;
     const int c = threadIdx.x & 63, r4 = threadIdx.x >> 6;
+    if (r4 == 0 && i0 + c < n) sdr[c] = slab_diag_sd(G, ldg, slab_stride, ks, i0 + c, scale);
+    if (r4 == 1 && j0 + c < n) sdc[c] = slab_diag_sd(G, ldg, slab_stride, ks, j0 + c, scale);
     {   // all 16 rows of this thread in flight per slab; slabs summed in order 0..ks-1
         constexpr int RPT = NT / 4;
         double g[RPT];
@@ -249,20 +286,20 @@ __global__ __launch_bounds__(256) void k_normalize_tiles(const double *G, int64_
     for (int rr = r4; rr < NT; rr += 4) {
         const int i = i0 + rr, j = j0 + c;          // upper side: row i, column j
         if (i < n && j < n && (bi != bj || rr <= c)) {
-            double v = (t[rr][c] * scale) / sd[i];
-            v = v / sd[j];
+            double v = (t[rr][c] * scale) / sdr[rr];
+            v = v / sdc[c];
             C[(int64_t)i * ldc + j] = v > 1.0 ? 1.0 : (v < -1.0 ? -1.0 : v);  // NaN passes through
         }
         const int p = j0 + rr, q = i0 + c;          // lower side: row p (tile bj), column q (tile bi)
         if (p < n && q < n && (bi != bj || c < rr)) {
-            double v = (t[c][rr] * scale) / sd[p];
-            v = v / sd[q];
+            double v = (t[c][rr] * scale) / sdc[rr];
+            v = v / sdr[c];
             C[(int64_t)p * ldc + q] = v > 1.0 ? 1.0 : (v < -1.0 ? -1.0 : v);
         }
     }
 }
 
-// packed[r][j] = sum_s G_s[r][j] in slab order (the order k_stddev / k_normalize_tiles use)
+// packed[r][j] = sum_s G_s[r][j] in slab order (the order k_normalize_tiles uses)
 __global__ void k_slab_sum(const double *G, int64_t slab_stride, int ks, int64_t count, double *out) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= count) return;
@@ -325,22 +362,24 @@ int split_k(int n, int64_t N, int64_t *kchunk_out) {
     int ks = (int)std::min<int64_t>(std::max<int64_t>(1, (PCG_K1_BLOCKS + ntiles / 2) / ntiles),
                                     std::max<int64_t>(1, N / PCG_K1_MINROWS));
     ks = std::min(ks, maxks);
+    if (PCG_K1_KS > 0) ks = (int)std::min<int64_t>(PCG_K1_KS, std::max<int64_t>(1, N / KT));
     const int64_t kchunk = (((N + ks - 1) / ks) + KT - 1) / KT * KT;
     *kchunk_out = kchunk;
     return (int)((N + kchunk - 1) / kchunk);
 }
 
-int column_means(pcg_handle *h, const double *X, int64_t N, int nn, int64_t ldx, double **mean_out, double **sd_out) {
+unsigned xtx_grid(int blocks) { return PCG_K1_XCD ? (unsigned)((blocks + 7) / 8 * 8) : (unsigned)blocks; }
+
+int column_means(pcg_handle *h, const double *X, int64_t N, int nn, int64_t ldx, double **mean_out) {
     const int nchunks = (int)((N + MEAN_ROWS - 1) / MEAN_ROWS);
-    if (!pcg_ensure(h, h->colmean, sizeof(double) * ((size_t)nn * (nchunks + 2))))
+    if (!pcg_ensure(h, h->colmean, sizeof(double) * ((size_t)nn * (nchunks + 1))))
         return pcg_fail(h, PCG_ERR_OOM, "pcg_corr scratch");
     double *part = (double *)h->colmean.p;
     double *mean = part + (size_t)nn * nchunks;
-    hipLaunchKernelGGL(k_colsum_partial, dim3((nn + 255) / 256, nchunks), dim3(256), 0, h->stream, X, N, nn,
-                       ldx, part);
-    hipLaunchKernelGGL(k_colmean, dim3((nn + 255) / 256), dim3(256), 0, h->stream, part, nchunks, nn, N, mean);
+    hipLaunchKernelGGL(k_colsum_partial, dim3((nn + 255) / 256, nchunks), dim3(256), 0, h->stream, X, N, nn, ldx,
+                       part);
+    hipLaunchKernelGGL(k_colmean, dim3((nn + 63) / 64), dim3(256), 0, h->stream, part, nchunks, nn, N, mean);
     *mean_out = mean;
-    *sd_out = mean + nn;
     return PCG_OK;
 }
 
@@ -377,8 +416,8 @@ extern "C" int pcg_corr_shard(pcg_handle *h, const double *X, int64_t N, int64_t
     }
     const int ntiles = (int)(tl.size() / 3);
     if (ntiles == 0) return PCG_OK;
-    double *mean, *sd;
-    int rc = column_means(h, X, N, nn, ldx, &mean, &sd);
+    double *mean;
+    int rc = column_means(h, X, N, nn, ldx, &mean);
     if (rc) return rc;
     int64_t kchunk = 0;
     const int ks = split_k(nn, N, &kchunk);
@@ -389,8 +428,8 @@ extern "C" int pcg_corr_shard(pcg_handle *h, const double *X, int64_t N, int64_t
     int32_t *tld = reinterpret_cast<int32_t *>((double *)h->pr_scratch.p + (ks > 1 ? (size_t)stride * ks : 0));
     PCG_HIP(h, hipMemcpyAsync(tld, tl.data(), sizeof(int32_t) * tl.size(), hipMemcpyHostToDevice, h->stream));
     if (ks > 1) PCG_HIP(h, hipMemsetAsync(G, 0, sizeof(double) * (size_t)stride * ks, h->stream));
-    hipLaunchKernelGGL(k_xtx, dim3(ntiles * ks), dim3(256), 0, h->stream, X, N, nn, ldx, mean, ntiles, kchunk, G,
-                       (int64_t)nn, stride, (const int32_t *)tld);
+    hipLaunchKernelGGL(k_xtx, dim3(xtx_grid(ntiles * ks)), dim3(256), 0, h->stream, X, N, nn, ldx, mean, ntiles, ks,
+                       kchunk, G, (int64_t)nn, stride, (const int32_t *)tld);
     if (ks > 1)
         hipLaunchKernelGGL(k_slab_sum, dim3((unsigned)((stride + 255) / 256)), dim3(256), 0, h->stream, G, stride,
                            ks, stride, packed);
@@ -426,8 +465,8 @@ int pcg_corr_launch(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_
         return pcg_fail(h, PCG_ERR_INVALID, "pcg_corr: invalid arguments");
     PCG_HIP(h, hipSetDevice(h->device));
     const int nn = (int)n;
-    double *mean, *sd;
-    int rc = column_means(h, X, N, nn, ldx, &mean, &sd);
+    double *mean;
+    int rc = column_means(h, X, N, nn, ldx, &mean);
     if (rc) return rc;
     const int T = (nn + TILE - 1) / TILE;
     const int ntiles = T * (T + 1) / 2;
@@ -443,12 +482,11 @@ int pcg_corr_launch(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_
         ldg = nn;
     }
     const double scale = 1.0 / (double)(N - 1);
-    hipLaunchKernelGGL(k_xtx, dim3(ntiles * ks), dim3(256), 0, h->stream, X, N, nn, ldx, mean, ntiles, kchunk, G,
-                       ldg, stride, (const int32_t *)nullptr);
-    hipLaunchKernelGGL(k_stddev, dim3((nn + 255) / 256), dim3(256), 0, h->stream, G, ldg, stride, ks, nn, scale, sd);
+    hipLaunchKernelGGL(k_xtx, dim3(xtx_grid(ntiles * ks)), dim3(256), 0, h->stream, X, N, nn, ldx, mean, ntiles, ks,
+                       kchunk, G, ldg, stride, (const int32_t *)nullptr);
     const int T64 = (nn + NT - 1) / NT;
     hipLaunchKernelGGL(k_normalize_tiles, dim3(T64 * (T64 + 1) / 2), dim3(256), 0, h->stream, G, ldg, stride, ks, C,
-                       ldc, nn, scale, sd);
+                       ldc, nn, scale);
     PCG_HIP(h, hipGetLastError());
     return PCG_OK;
 }
