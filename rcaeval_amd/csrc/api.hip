@@ -44,7 +44,7 @@ bool pcg_ensure_pinned(pcg_handle *h, PinBuf &b, size_t bytes) {
         b.p = nullptr;
         b.bytes = 0;
     }
-    if (hipHostMalloc(&b.p, bytes, hipHostMallocDefault) != hipSuccess) {
+    if (hipHostMalloc(&b.p, bytes, hipHostMallocMapped) != hipSuccess) {   // device-readable (k_copy_i64)
         b.p = nullptr;
         return false;
     }
@@ -82,7 +82,7 @@ extern "C" int pcg_destroy(pcg_handle *h) {
     pcg_comm_release(h);
     DevBuf *bufs[] = {&h->adj, &h->deg, &h->off, &h->nbr, &h->rm, &h->ug, &h->cpre, &h->binom, &h->ctr,
                       &h->deferred, &h->records, &h->nearbuf, &h->exportbuf, &h->export_xy, &h->diag,
-                      &h->colmean, &h->pr_scratch, &h->batch_scratch, &h->chisq_scratch, &h->done_ctr};
+                      &h->colmean, &h->pr_scratch, &h->batch_scratch, &h->chisq_scratch};
     for (DevBuf *b : bufs)
         if (b->p) hipFree(b->p);
     PinBuf *pins[] = {&h->ctr_pin, &h->deg_pin, &h->off_pin, &h->cpre_pin, &h->status_pin};

@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <string>
 #include <vector>
+#include <chrono>
 
 #include "pcgpu.h"
 
@@ -43,6 +44,12 @@ struct DeferredEntry {             // one test routed to the exact (LU) path
     int32_t x, y;                  // visiting node x, neighbour y
     int32_t s[PCG_MAX_DEPTH];      // conditioning set (global ids)
 };
+
+inline double pcg_now_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+#define PCG_HT(h, label) \
+    do { if ((h)->htrace_on) (h)->htrace.emplace_back((label), pcg_now_us()); } while (0)
 
 struct pcg_handle {
     int device = 0;
@@ -88,8 +95,10 @@ struct pcg_handle {
     LevelSummary *summary = nullptr;    // host-mapped, coherent (graph_launch / level_wait)
     size_t summary_bytes = 0;
     unsigned long long summary_seq = 0;
-    DevBuf done_ctr;                    // k_level_summary's last-block counter
-    bool done_ready = false;
+    bool ug_clean = false;
+    // PCG_HOST_TRACE=1: host timestamps of the level loop's steps, printed after each skeleton
+    bool htrace_on = false;
+    std::vector<std::pair<const char *, double>> htrace;              // the union rows of the current CSR are all zero
     std::vector<int32_t> deg_h;      // degrees at the start of the current depth
     std::vector<int32_t> deg_levels; // levels x n
     std::vector<int64_t> cpre_h;     // 3 x (n + 1): narrow, wide, large class chunk prefixes

@@ -29,6 +29,9 @@
 // PCG_FLAG_FULL_P computes the p-value of every test inline instead.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include <algorithm>
 #include <climits>
 #include <cmath>
@@ -213,50 +216,32 @@ __global__ void k_init_adj(uint64_t *adj, int n, int W) {
     adj[i] = m;
 }
 
-__global__ void k_diag(const double *C, int64_t ldc, int n, double *diag) {
+__global__ void k_diag(const double *C, int64_t ldc, int n, double *diag, int32_t *deg) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) diag[i] = C[(int64_t)i * ldc + i];
-}
-
-// The level barrier's host summary, written by the device straight into host-mapped memory:
-// degrees (also kept on the device for the next depth), the level counters, the merged status
-// bytes, then — after every block's writes are visible system-wide — the sequence number the host
-// spins on. Replaces three device-to-host copies and a stream synchronisation per depth.
-__global__ __launch_bounds__(256) void k_level_summary(const uint64_t *adj, int n, int W, int32_t *deg,
-                                                       const DevCounters *ctr, const uint8_t *status,
-                                                       LevelSummary *out, int32_t *out_deg, unsigned *done,
-                                                       unsigned long long seq) {
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    if (x < n) {
-        int c = 0;
-        for (int w = 0; w < W; ++w) c += __popcll(adj[(int64_t)x * W + w]);
-        deg[x] = c;
-        out_deg[x] = c;
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        out->ctr = *ctr;
-        for (int k = 0; k < 8; ++k) out->status[k] = status ? status[k] : 0;
-    }
-    __threadfence_system();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned prev = atomicAdd(done, 1u);
-        if (prev == gridDim.x - 1) {        // the last block: every block's writes are fenced
-            __threadfence_system();
-            atomicExch(done, 0u);
-            __atomic_store_n(&out->seq, seq, __ATOMIC_RELEASE);
-        }
+    if (i < n) {
+        diag[i] = C[(int64_t)i * ldc + i];
+        deg[i] = n - 1;                  // the complete graph k_init_adj builds
     }
 }
 
-// CSR offsets off[0..n] = exclusive prefix of deg (one block, 1024 threads, chunked scan)
-__global__ __launch_bounds__(1024) void k_offsets(const int32_t *deg, int n, int32_t *off) {
+// The level barrier's host summary, one block: the CSR offsets of the new graph (exclusive
+// scan of the degrees k_apply keeps current), the degrees, level counters and merged status
+// bytes written straight into host-mapped memory, then — after a system-scope fence — the
+// sequence number the host spins on. Replaces three device-to-host copies and a stream
+// synchronisation per depth; the counters and status bytes are cleared once copied.
+__global__ __launch_bounds__(1024) void k_level_summary(const int32_t *deg, int n, int32_t *off, DevCounters *ctr,
+                                                        uint8_t *status, LevelSummary *out, int32_t *out_deg,
+                                                        unsigned long long seq) {
     __shared__ int32_t part[1024];
     const int tid = threadIdx.x;
     const int per = (n + 1023) / 1024;
     const int lo = min(n, tid * per), hi = min(n, lo + per);
     int32_t s = 0;
-    for (int i = lo; i < hi; ++i) s += deg[i];
+    for (int i = lo; i < hi; ++i) {
+        const int32_t v = deg[i];
+        out_deg[i] = v;
+        s += v;
+    }
     part[tid] = s;
     __syncthreads();
     for (int o = 1; o < 1024; o <<= 1) {       // inclusive Hillis-Steele scan of the chunk sums
@@ -268,13 +253,31 @@ __global__ __launch_bounds__(1024) void k_offsets(const int32_t *deg, int n, int
     int32_t acc = tid ? part[tid - 1] : 0;
     for (int i = lo; i < hi; ++i) { off[i] = acc; acc += deg[i]; }
     if (tid == 1023) off[n] = part[1023];
+    if (tid == 0) {
+        out->ctr = *ctr;
+        *ctr = DevCounters{};
+        for (int k = 0; k < 8; ++k) out->status[k] = status ? status[k] : 0;
+        if (status)
+            for (int k = 0; k < PCG_RM_STATUS; ++k) status[k] = 0;
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (tid == 0) {
+        __threadfence_system();
+        __atomic_store_n(&out->seq, seq, __ATOMIC_RELEASE);
+    }
 }
 
-// one wave per node: ascending neighbour list from the bitmask (wave prefix scan)
-__global__ void k_fill_nbr(const uint64_t *adj, int n, int W, const int32_t *off, int32_t *nbr) {
+// one wave per node: ascending neighbour list from the bitmask (wave prefix scan); with ug,
+// also clears the node's union rows (one W-word row per CSR slot) for the coming depth
+__global__ void k_fill_nbr(const uint64_t *adj, int n, int W, const int32_t *off, int32_t *nbr, uint64_t *ug) {
     const int x = blockIdx.x;
     const int lane = threadIdx.x;
     int base = off[x];
+    if (ug) {
+        const int64_t lo = (int64_t)base * W, hi = (int64_t)off[x + 1] * W;
+        for (int64_t e = lo + lane; e < hi; e += 64) ug[e] = 0ull;
+    }
     for (int w0 = 0; w0 < W; w0 += 64) {
         const int w = w0 + lane;
         uint64_t v = w < W ? adj[(int64_t)x * W + w] : 0ull;
@@ -297,32 +300,49 @@ __global__ void k_fill_nbr(const uint64_t *adj, int n, int W, const int32_t *off
 }
 
 // rm -> adjacency bitmask + removed_level (the level barrier, SkeletonDiscovery.py:141-144).
-// One lane per removal byte (coalesced 64-byte row segments); the wave's ballot is the
-// 64-bit mask cleared from adjacency word (x, w).
-__global__ __launch_bounds__(256) void k_apply(const uint8_t *rm, uint64_t *adj, int8_t *rl, int n, int W, int d) {
-    const int lane = threadIdx.x & 63;
-    const int64_t word = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;   // wave-uniform
-    if (word >= (int64_t)n * W) return;
-    const int x = (int)(word / W), w = (int)(word % W);
-    const int y = w * 64 + lane;
-    bool removed = false;
-    if (y < n) {
-        removed = rm[(int64_t)x * n + y] != 0;
-        if (removed) rl[(int64_t)x * n + y] = (int8_t)d;
+// One block per row x, one lane per removal byte (coalesced 64-byte row segments, the 4 waves
+// take every 4th adjacency word); a wave's ballot is the 64-bit mask cleared from adjacency
+// word (x, w), and the row's removed count lowers deg[x] once (degrees stay current for
+// k_level_summary). rm is the last read here: set bytes are cleared for the next depth.
+__global__ __launch_bounds__(256) void k_apply(uint8_t *rm, uint64_t *adj, int32_t *deg, int8_t *rl, int n, int W,
+                                               int d) {
+    __shared__ int cleared[4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int x = blockIdx.x;
+    int mine = 0;
+    for (int w = wave; w < W; w += 4) {
+        const int y = w * 64 + lane;
+        bool removed = false;
+        if (y < n) {
+            removed = rm[(int64_t)x * n + y] != 0;
+            if (removed) {
+                rl[(int64_t)x * n + y] = (int8_t)d;
+                rm[(int64_t)x * n + y] = 0;
+            }
+        }
+        const unsigned long long m = __ballot(removed);
+        if (lane == 0 && m) {
+            const uint64_t old = adj[(int64_t)x * W + w];
+            adj[(int64_t)x * W + w] = old & ~m;
+            mine += __popcll(old & m);
+        }
     }
-    const unsigned long long m = __ballot(removed);
-    if (lane == 0 && m) adj[word] &= ~m;
+    if (lane == 0) cleared[wave] = mine;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int c = cleared[0] + cleared[1] + cleared[2] + cleared[3];
+        if (c) deg[x] -= c;
+    }
 }
 
-// export non-empty union rows of removed ordered pairs: one lane per CSR slot; the wave
-// compacts its non-empty rows with one atomic (ballot + mbcnt), so appends never chain
-// atomics serially.
+// export non-empty union rows of removed ordered pairs: one lane per CSR slot finds its (x, y)
+// and whether the pair was removed; the wave then reads its removed pairs' W-word rows with all
+// 64 lanes (coalesced), eight rows' loads in flight at a time, keeps the non-empty ones and
+// compacts them with one atomic (ballot + mbcnt).
+constexpr int EXPORT_GROUP = 8;
 __global__ __launch_bounds__(256) void k_export(const int32_t *off, const int32_t *nbr, const uint8_t *rm,
                                                 const uint64_t *ug, int n, int W, int64_t sumdeg, int32_t *xy,
                                                 uint64_t *bits, int64_t cap, unsigned long long *ctr) {
-    // One lane per ordered adjacent pair (CSR slot) finds its (x, y) and whether the pair was
-    // removed; the wave then walks its removed pairs one by one and reads / copies each pair's
-    // W-word union row with all 64 lanes (coalesced), keeping the rows that are non-empty.
     const int lane = threadIdx.x & 63;
     const int64_t wave_base = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63);
     const int64_t slot = wave_base + lane;
@@ -341,12 +361,24 @@ __global__ __launch_bounds__(256) void k_export(const int32_t *off, const int32_
     const unsigned long long cand = __ballot(removed);
     if (!cand) return;
     unsigned long long keepm = 0;
-    for (unsigned long long mm = cand; mm; mm &= mm - 1) {
-        const int k = __ffsll((long long)mm) - 1;
-        const uint64_t *row = ug + (wave_base + k) * W;
-        uint64_t v = 0;
-        for (int w = lane; w < W; w += 64) v |= row[w];
-        if (__ballot(v != 0)) keepm |= 1ull << k;
+    for (unsigned long long mm = cand; mm;) {
+        int ks[EXPORT_GROUP];
+        int cnt = 0;
+#pragma unroll
+        for (int g = 0; g < EXPORT_GROUP; ++g) {
+            ks[g] = mm ? __ffsll((long long)mm) - 1 : 0;
+            if (mm) { mm &= mm - 1; ++cnt; }
+        }
+        uint64_t v[EXPORT_GROUP];
+#pragma unroll
+        for (int g = 0; g < EXPORT_GROUP; ++g) v[g] = 0;
+        for (int w = lane; w < W; w += 64)
+#pragma unroll
+            for (int g = 0; g < EXPORT_GROUP; ++g)
+                if (g < cnt) v[g] |= ug[(wave_base + ks[g]) * W + w];
+#pragma unroll
+        for (int g = 0; g < EXPORT_GROUP; ++g)
+            if (g < cnt && __ballot(v[g] != 0)) keepm |= 1ull << ks[g];
     }
     if (!keepm) return;
     unsigned long long base = 0;
@@ -359,12 +391,25 @@ __global__ __launch_bounds__(256) void k_export(const int32_t *off, const int32_
             xy[2 * r + 1] = y;
         }
     }
-    for (unsigned long long mm = keepm; mm; mm &= mm - 1) {
-        const int k = __ffsll((long long)mm) - 1;
-        const int64_t r = (int64_t)base + __popcll(keepm & ((1ull << k) - 1ull));
-        if (r >= cap) break;
-        const uint64_t *row = ug + (wave_base + k) * W;
-        for (int w = lane; w < W; w += 64) bits[r * W + w] = row[w];
+    for (unsigned long long mm = keepm; mm;) {
+        int ks[EXPORT_GROUP];
+        int cnt = 0;
+#pragma unroll
+        for (int g = 0; g < EXPORT_GROUP; ++g) {
+            ks[g] = mm ? __ffsll((long long)mm) - 1 : 0;
+            if (mm) { mm &= mm - 1; ++cnt; }
+        }
+        for (int w = lane; w < W; w += 64) {
+            uint64_t v[EXPORT_GROUP];
+#pragma unroll
+            for (int g = 0; g < EXPORT_GROUP; ++g) v[g] = g < cnt ? ug[(wave_base + ks[g]) * W + w] : 0ull;
+#pragma unroll
+            for (int g = 0; g < EXPORT_GROUP; ++g) {
+                if (g >= cnt) break;
+                const int64_t r = (int64_t)base + __popcll(keepm & ((1ull << ks[g]) - 1ull));
+                if (r < cap) bits[r * W + w] = v[g];
+            }
+        }
     }
 }
 
@@ -1613,12 +1658,16 @@ __global__ __launch_bounds__(64) void k_level_deep(LevelArgs a, double *scratch,
 
 // ---------------------------------------------------------------------------------------
 // exact path over the deferred list (LU like numpy.linalg.inv; the reference p expression)
-__global__ void k_exact(LevelArgs a) {
+// One wave per deferred test: the lanes gather the (d+2)^2 correlation entries in parallel
+// into the wave's LDS slot (a single lane's rolled gather would wait out one HBM latency per
+// entry), then lane 0 factors and decides.
+__global__ __launch_bounds__(256) void k_exact(LevelArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int d = a.d;
     const int m = d + 2;
     const int per = m * m + 2 * m;
-    double *A = reinterpret_cast<double *>(smem) + (size_t)threadIdx.x * per;
+    const int lane = threadIdx.x & 63;
+    double *A = reinterpret_cast<double *>(smem) + (size_t)(threadIdx.x >> 6) * per;
     double *B0 = A + m * m;
     double *B1 = B0 + m;
     int piv[PCG_MAX_DEPTH + 2];
@@ -1628,16 +1677,27 @@ __global__ void k_exact(LevelArgs a) {
         ((int64_t)pushed > a.def_cap || (a.record && (int64_t)a.ctr->records > a.rec_cap)))
         a.rm[(int64_t)a.n * a.n] = 1;      // overflow: every rank reruns (status byte 0)
     unsigned long long nexact = 0, nindep = 0;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count;
-         i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < count; i += waves) {
         const DeferredEntry e = a.deferred[i];
         const int x = e.x, y = e.y;
         const int lo_ = x < y ? x : y, hi_ = x < y ? y : x;
         int var[PCG_MAX_DEPTH + 2];
         var[0] = lo_; var[1] = hi_;
         for (int q = 0; q < d; ++q) var[2 + q] = e.s[q];
-        for (int r = 0; r < m; ++r)
-            for (int c = 0; c < m; ++c) A[r * m + c] = a.C[(int64_t)var[r] * a.ldc + var[c]];
+        for (int k = lane; k < m * m; k += 64) {
+            const int r = k / m, c = k - r * m;
+            int vr = lo_, vc = lo_;
+            for (int q = 0; q < m; ++q) {      // register-indexed var[] without dynamic indexing
+                if (q == r) vr = var[q];
+                if (q == c) vc = var[q];
+            }
+            A[k] = a.C[(int64_t)vr * a.ldc + vc];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane != 0) continue;
         double i00, i01, i11, p = __builtin_nan("");
         int err = 0;
         if (pcg_lu_inv01(A, m, piv, B0, B1, &i00, &i01, &i11)) {
@@ -1844,21 +1904,36 @@ int graph_launch(pcg_handle *h) {
         h->summary->seq = 0;
         h->summary_seq = 0;
     }
-    if (!pcg_ensure(h, h->done_ctr, 16)) return pcg_fail(h, PCG_ERR_OOM, "summary counter");
-    if (!h->done_ready) {
-        PCG_HIP(h, hipMemsetAsync(h->done_ctr.p, 0, 16, h->stream));
-        h->done_ready = true;
-    }
     void *dsum = nullptr;
     PCG_HIP(h, hipHostGetDevicePointer(&dsum, h->summary, 0));
     LevelSummary *ds = (LevelSummary *)dsum;
-    const uint8_t *status = h->depth >= 0 ? (h->rm_ext ? h->rm_ext : (const uint8_t *)h->rm.p) + (int64_t)n * n : nullptr;
+    uint8_t *status = h->depth >= 0 ? (h->rm_ext ? h->rm_ext : (uint8_t *)h->rm.p) + (int64_t)n * n : nullptr;
     const unsigned long long seq = ++h->summary_seq;
-    hipLaunchKernelGGL(k_level_summary, dim3((n + 255) / 256), dim3(256), 0, h->stream, (const uint64_t *)h->adj.p, n,
-                       W, (int32_t *)h->deg.p, (const DevCounters *)h->ctr.p, status, ds,
-                       reinterpret_cast<int32_t *>(ds + 1), (unsigned *)h->done_ctr.p, seq);
+    // the next depth's CSR is built from the device degrees while the host waits for the
+    // summary; nbr is sized by the current graph (degrees only fall), and the union rows are
+    // cleared along with it when the buffer already covers that bound
+    const int64_t bound = h->depth < 0 ? (int64_t)n * (n - 1) : h->sumdeg;
+    if (!pcg_ensure(h, h->off, sizeof(int32_t) * (n + 1)) ||
+        !pcg_ensure(h, h->nbr, sizeof(int32_t) * std::max<int64_t>(bound, 1)))
+        return pcg_fail(h, PCG_ERR_OOM, "neighbour lists");
+    hipLaunchKernelGGL(k_level_summary, dim3(1), dim3(1024), 0, h->stream, (const int32_t *)h->deg.p, n,
+                       (int32_t *)h->off.p, (DevCounters *)h->ctr.p, status, ds, reinterpret_cast<int32_t *>(ds + 1),
+                       seq);
+    uint64_t *ug = nullptr;
+    if (h->depth >= 0 && h->ug.p && h->ug.bytes >= sizeof(uint64_t) * (size_t)std::max<int64_t>(bound, 1) * W)
+        ug = (uint64_t *)h->ug.p;
+    h->ug_clean = ug != nullptr;
+    hipLaunchKernelGGL(k_fill_nbr, dim3(n), dim3(64), 0, h->stream, (const uint64_t *)h->adj.p, n, W,
+                       (const int32_t *)h->off.p, (int32_t *)h->nbr.p, ug);
     PCG_HIP(h, hipGetLastError());
     return PCG_OK;
+}
+
+// chunk prefix (host-mapped, written by the decomposition) -> device, by a kernel on the
+// handle's stream (no DMA-engine round trip in the level's launch burst)
+__global__ void k_copy_i64(const int64_t *src, int64_t count, int64_t *dst) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) dst[i] = src[i];
 }
 
 // spin until the summary of the last graph_launch is visible (a stream error or a stream that
@@ -1880,9 +1955,9 @@ int level_wait(pcg_handle *h) {
     return PCG_OK;
 }
 
-// after the wait: host degrees, CSR offsets (device scan), ascending neighbour lists
-int graph_finish(pcg_handle *h) {
-    const int n = (int)h->n, W = h->W;
+// after the wait: host degrees and their sum / maximum
+void graph_finish(pcg_handle *h) {
+    const int n = (int)h->n;
     const int32_t *dp = reinterpret_cast<const int32_t *>(h->summary + 1);
     h->deg_h.assign(dp, dp + n);
     int64_t s = 0;
@@ -1893,13 +1968,6 @@ int graph_finish(pcg_handle *h) {
     }
     h->sumdeg = s;
     h->maxdeg = mx;
-    if (!pcg_ensure(h, h->off, sizeof(int32_t) * (n + 1))) return PCG_ERR_OOM;
-    if (!pcg_ensure(h, h->nbr, sizeof(int32_t) * std::max<int64_t>(s, 1))) return PCG_ERR_OOM;
-    hipLaunchKernelGGL(k_offsets, dim3(1), dim3(1024), 0, h->stream, (const int32_t *)h->deg.p, n, (int32_t *)h->off.p);
-    hipLaunchKernelGGL(k_fill_nbr, dim3(n), dim3(64), 0, h->stream, (const uint64_t *)h->adj.p, n, W,
-                       (const int32_t *)h->off.p, (int32_t *)h->nbr.p);
-    PCG_HIP(h, hipGetLastError());
-    return PCG_OK;
 }
 
 size_t level_lds(const pcg_handle *h, int bs) {
@@ -1949,13 +2017,15 @@ extern "C" int pcg_skeleton_init(pcg_handle *h, const double *C, int64_t n, int6
     hipLaunchKernelGGL(k_init_adj, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, h->stream,
                        (uint64_t *)h->adj.p, (int)n, W);
     hipLaunchKernelGGL(k_diag, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream, C, ldc, (int)n,
-                       (double *)h->diag.p);
+                       (double *)h->diag.p, (int32_t *)h->deg.p);
     PCG_HIP(h, hipMemsetAsync(removed_level, 0xFF, (size_t)n * n, h->stream));
     PCG_HIP(h, hipGetLastError());
-    int rc = graph_launch(h);
+    PCG_HIP(h, hipMemsetAsync(h->rm_ext ? (void *)h->rm_ext : h->rm.p, 0, (size_t)n * n + PCG_RM_STATUS, h->stream));
+    int rc = graph_launch(h);            // also clears the counters
     if (!rc) rc = level_wait(h);
     if (rc) return rc;
-    return graph_finish(h);
+    graph_finish(h);
+    return PCG_OK;
 }
 
 extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, int32_t *max_degree,
@@ -2077,15 +2147,25 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
     }
     h->total_chunks = h->total_small + h->total_wide + h->total_large;
     if (total_chunks) *total_chunks = h->total_chunks;
+    PCG_HT(h, "begin:decomposed");
     if (!pcg_ensure(h, h->cpre, sizeof(int64_t) * 3 * (n + 1))) return PCG_ERR_OOM;
-    PCG_HIP(h, hipMemcpyAsync(h->cpre.p, h->cpre_pin.p, sizeof(int64_t) * 3 * (n + 1), hipMemcpyHostToDevice,
-                              h->stream));
-    PCG_HIP(h, hipMemsetAsync(h->rm_ext ? (void *)h->rm_ext : h->rm.p, 0, (size_t)n * n + PCG_RM_STATUS, h->stream));
-    PCG_HIP(h, hipMemsetAsync(h->ctr.p, 0, sizeof(DevCounters), h->stream));
+    // rm, the counters and the status bytes were cleared by the previous depth's k_apply /
+    // k_level_summary (or at init); the union rows by k_fill_nbr (or here, on first use)
+    {
+        void *src = nullptr;
+        PCG_HIP(h, hipHostGetDevicePointer(&src, h->cpre_pin.p, 0));
+        const int64_t cnt = 3 * (int64_t)(n + 1);
+        hipLaunchKernelGGL(k_copy_i64, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, h->stream,
+                           (const int64_t *)src, cnt, (int64_t *)h->cpre.p);
+        PCG_HIP(h, hipGetLastError());
+    }
+    PCG_HT(h, "begin:prefix-copy-launched");
     if (depth >= 1) {
         const size_t ugb = sizeof(uint64_t) * (size_t)std::max<int64_t>(h->sumdeg, 1) * h->W;
+        void *before = h->ug.p;
         if (!pcg_ensure(h, h->ug, ugb)) return pcg_fail(h, PCG_ERR_OOM, "sepset union rows (%zu B)", ugb);
-        PCG_HIP(h, hipMemsetAsync(h->ug.p, 0, ugb, h->stream));
+        if (h->ug.p != before || !h->ug_clean) PCG_HIP(h, hipMemsetAsync(h->ug.p, 0, ugb, h->stream));
+        h->ug_clean = false;
         if (depth == 1 || h->export_cap == 0) {
             // every ordered pair adjacent at depth 1 is exported at most once over all depths
             // (depth-0 removals carry empty sepsets), so one allocation covers the run
@@ -2188,6 +2268,7 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
         return pcg_fail(h, PCG_ERR_INVALID, "pcg_level_run: chunk range");
     const int d = h->depth;
     const int mode = mode_of(h, d);
+    PCG_HT(h, "run:start");
     {
         LevelArgs a = make_args(h, d, mode == MODE_EXACT);
         a.chunk_lo = chunk_lo;
@@ -2290,13 +2371,13 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
         PCG_HIP(h, hipGetLastError());
         PCG_HIP(h, hipEventRecord(h->ev[3], h->stream));
         h->run_timed = true;
+        PCG_HT(h, "run:launched");
         // exact path over the deferred list; the kernel reads the list length on the device
         // (no host round trip) and raises the overflow status byte if the list overflowed
         a = make_args(h, d, mode == MODE_EXACT);
         const int m = d + 2;
-        const int per = (m * m + 2 * m) * 8;
-        const int bs = per * 64 <= 64 * 1024 ? 64 : 32;
-        hipLaunchKernelGGL(k_exact, dim3(512), dim3(bs), (size_t)per * bs, h->stream, a);
+        const int per = (m * m + 2 * m) * 8;      // one LDS slot per wave
+        hipLaunchKernelGGL(k_exact, dim3(256), dim3(256), (size_t)per * 4, h->stream, a);
         PCG_HIP(h, hipGetLastError());
         return PCG_OK;
     }
@@ -2311,19 +2392,22 @@ extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
     // removed pairs (device-side append), apply the removals (SkeletonDiscovery.py:141-144),
     // recount degrees, and fetch counters + status + degrees in one batch
     const int64_t room = h->export_cap - h->export_rows;
+    (void)W;
     if (d >= 1 && h->sumdeg > 0)
         hipLaunchKernelGGL(k_export, dim3((unsigned)((h->sumdeg + 255) / 256)), dim3(256), 0, h->stream,
                            (const int32_t *)h->off.p, (const int32_t *)h->nbr.p, (const uint8_t *)rmb,
                            (const uint64_t *)h->ug.p, n, W, h->sumdeg,
                            (int32_t *)h->export_xy.p + 2 * h->export_rows,
                            (uint64_t *)h->exportbuf.p + h->export_rows * W, room, &ctr->exported);
-    const int64_t nw = (int64_t)n * W;
-    hipLaunchKernelGGL(k_apply, dim3((unsigned)((nw * 64 + 255) / 256)), dim3(256), 0, h->stream, (const uint8_t *)rmb,
-                       (uint64_t *)h->adj.p, h->rl, n, W, d);
+    hipLaunchKernelGGL(k_apply, dim3((unsigned)n), dim3(256), 0, h->stream, rmb,
+                       (uint64_t *)h->adj.p, (int32_t *)h->deg.p, h->rl, n, W, d);
     PCG_HIP(h, hipGetLastError());
+    PCG_HT(h, "end:tail-launched");
     int rc = graph_launch(h);            // degrees + counters + status -> host-mapped summary
+    PCG_HT(h, "end:summary-launched");
     if (!rc) rc = level_wait(h);
     if (rc) return rc;
+    PCG_HT(h, "end:summary-seen");
     const DevCounters c = h->summary->ctr;
     uint8_t status[8];
     for (int k = 0; k < 8; ++k) status[k] = h->summary->status[k];
@@ -2336,6 +2420,7 @@ extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
         PCG_HIP(h, e);
         h->run_timed = false;
     }
+    PCG_HT(h, "end:kernel-ms-read");
     // records / near-alpha to host (parity runs; before the next level reuses the buffers)
     if ((h->flags & PCG_FLAG_RECORD) && c.records && (int64_t)c.records <= h->rec_cap) {
         const size_t old = h->rec_h.size();
@@ -2379,17 +2464,21 @@ extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
         if ((int64_t)c.exported > room) return pcg_fail(h, PCG_ERR_OVERFLOW, "sepset export overflow");
         h->export_rows += (int64_t)c.exported;
     }
-    rc = graph_finish(h);
-    if (rc) return rc;
+    graph_finish(h);
     h->st.edges_after[d] = h->sumdeg / 2;
+    PCG_HT(h, "end:done");
     if (stats) *stats = h->st;
     return PCG_OK;
 }
 
 static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N, double alpha,
                          int max_depth, int flags, int8_t *removed_level) {
+    h->htrace_on = getenv("PCG_HOST_TRACE") != nullptr;
+    h->htrace.clear();
+    PCG_HT(h, "init:start");
     int rc = pcg_skeleton_init(h, C, n, ldc, N, alpha, flags, removed_level);
     if (rc) return rc;
+    PCG_HT(h, "init:done");
     // per-depth wall brackets are recorded on the stream and read after the last depth, so the
     // level loop keeps its one host sync per depth (the one inside pcg_level_end)
     int done = 0;
@@ -2400,6 +2489,7 @@ static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc,
             if (!h->lev[2 * depth + k]) PCG_HIP(h, hipEventCreate(&h->lev[2 * depth + k]));
         int64_t total = 0;
         PCG_HIP(h, hipEventRecord(h->lev[2 * depth], h->stream));
+        PCG_HT(h, "loop:begin");
         rc = pcg_level_begin(h, depth, &total, nullptr, nullptr);
         if (rc == 1) break;
         if (rc) return rc;
@@ -2415,6 +2505,14 @@ static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc,
         float ms = 0.f;
         PCG_HIP(h, hipEventElapsedTime(&ms, h->lev[2 * depth], h->lev[2 * depth + 1]));
         h->st.level_ms[depth] = ms;
+    }
+    if (h->htrace_on && !h->htrace.empty()) {
+        const double t0 = h->htrace.front().second;
+        double prev = t0;
+        for (auto &e : h->htrace) {
+            fprintf(stderr, "[pcg host] %9.1f us  +%7.1f  %s\n", e.second - t0, e.second - prev, e.first);
+            prev = e.second;
+        }
     }
     return PCG_OK;
 }
