@@ -294,7 +294,9 @@ def main():
     # rehearsal knobs (default off): several ranks on one GPU need gloo + a shared device
     device = int(os.environ.get("PCG_BENCH_DEVICE", local))
     backend = os.environ.get("PCG_DIST_BACKEND", "nccl")
-    if world > 1:
+    # PCG_BENCH_FORCE_DIST=1: run the sharded driver even at world 1 (its overhead, measured)
+    dist_path = world > 1 or os.environ.get("PCG_BENCH_FORCE_DIST") == "1"
+    if dist_path:
         import torch.distributed as dist
         torch.cuda.set_device(device)
         if backend == "nccl":
@@ -312,7 +314,7 @@ def main():
 
     # PCG_DIST_NATIVE=1: the level loop and its collectives run in C (pcg_skeleton_sharded on
     # an RCCL communicator of the library's own); default: the torch.distributed driver
-    native = world > 1 and os.environ.get("PCG_DIST_NATIVE") == "1"
+    native = dist_path and os.environ.get("PCG_DIST_NATIVE") == "1"
     if native:
         from rcaeval_amd.dist import native_comm
         native_comm(eng)
@@ -321,7 +323,7 @@ def main():
         t0 = time.perf_counter()
         if native:
             C = eng.corr_sharded(Xd)
-        elif world > 1:
+        elif dist_path:
             from rcaeval_amd.dist import sharded_corr
             C = sharded_corr(eng, Xd)
         else:   # single GPU: K1 + skeleton in one C call (pcg_pc_skeleton), no host round trip between
@@ -330,7 +332,7 @@ def main():
         phases.append(("corr", time.perf_counter() - t0))
         if native:
             return eng.skeleton_sharded(C, args.samples, alpha=args.alpha, max_depth=args.max_depth, flags=flags)
-        if world > 1:
+        if dist_path:
             from rcaeval_amd.dist import sharded_skeleton
             trace = [] if os.environ.get("PCG_DIST_TRACE") else None
             out = sharded_skeleton(eng, C, args.samples, alpha=args.alpha, max_depth=args.max_depth,
@@ -343,7 +345,7 @@ def main():
 
     def barrier():
         torch.cuda.synchronize()
-        if world > 1:
+        if dist_path:
             torch.distributed.barrier()
         torch.cuda.synchronize()
 

@@ -63,6 +63,13 @@ constexpr int MODE_EXACT = 2;
 #ifndef PCG_TG_Y2
 #define PCG_TG_Y2 0   // T-group sweep: two y per iteration at the depths whose bit is set (1 << d)
 #endif
+#ifndef PCG_TG_SGPR
+#define PCG_TG_SGPR 0x18 // T-group sweep, depths whose bit (1 << d) is set: per-y bookkeeping as wave
+                         // lane masks (SALU) instead of per-lane bits
+#endif
+#ifndef PCG_TG_SPLIT
+#define PCG_TG_SPLIT 0   // lane-mask sweep: split the y range around a shared candidate window (spills: slower)
+#endif
 #ifndef PCG_TG3
 #define PCG_TG3 4
 #endif
@@ -1406,11 +1413,143 @@ __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_
 #pragma unroll
         for (int jj = 0; jj < TG; ++jj) okm |= (unsigned)okc[jj] << jj;
         const unsigned vmask = (1u << (cend - cbase)) - 1u;
+        constexpr bool SG = (PCG_TG_SGPR >> DM) & 1;
+        // lane-mask form of the sweep's bookkeeping. Tests per task are counted in closed form:
+        // every valid candidate meets every y outside T except itself, minus the dedup skips of
+        // "own" y (counted in the rare path below). okv[jj]: lanes whose candidate jj is valid
+        // and fast-path usable; notok: lanes with a valid candidate that is not (every y of such
+        // a lane takes the rare path); uni: the wave's lanes share one candidate window, so the
+        // y equal to a candidate is masked by a scalar index instead of the rare path.
+        unsigned long long okv[TG], notok = 0ull, lanebit = 0ull;
+        int cb0 = 0;
+        bool uni = false;
+        if constexpr (SG) {
+            tcount += (unsigned)(nval * (D - DT - 1));     // nval = cend - cbase
+#pragma unroll
+            for (int jj = 0; jj < TG; ++jj) okv[jj] = __builtin_amdgcn_ballot_w64(okc[jj]);
+            notok = __builtin_amdgcn_ballot_w64((vmask & ~okm) != 0u);
+            cb0 = __builtin_amdgcn_readfirstlane(cbase);
+            uni = __builtin_amdgcn_ballot_w64(cbase != cb0) == 0ull;
+            lanebit = 1ull << (tid & 63);
+        }
 
         // the y sweep, specialised on the wave-uniform candidate count so the NC chains stay
         // branch-free and interleaved (candidates beyond the count are not evaluated at all)
         auto sweep = [&](auto nc_tag) {
             constexpr int NC = decltype(nc_tag)::value;
+            if constexpr (SG) {
+            auto ystep = [&](int t, auto ym_tag) {
+                constexpr int YM = decltype(ym_tag)::value;
+                const Mask lm = lmask[t];
+                const double *Mt = M + t * DS;
+                double sc[TG];
+#pragma unroll
+                for (int q = 0; q < (NC + 1) / 2; ++q) {
+                    const double2 m = *reinterpret_cast<const double2 *>(Mt + cbase + 2 * q);
+                    sc[2 * q] = m.x;
+                    sc[2 * q + 1] = m.y;
+                }
+                double vT[DT], mT[DT];
+                double vv = 0.0, uv = 0.0;
+#pragma unroll
+                for (int j = 0; j < DT; ++j) mT[j] = Mt[T[j]];
+#pragma unroll
+                for (int i = 0; i < DT; ++i) {
+                    double v = 0.0;
+#pragma unroll
+                    for (int j = 0; j <= i; ++j) v += Li[i][j] * mT[j];
+                    vT[i] = v;
+                    vv += v * v;
+                    uv += uT[i] * v;
+                }
+                double projv[DT];
+#pragma unroll
+                for (int i = 0; i < DT; ++i) projv[i] = PCG_TG_WC ? mT[i] : vT[i];
+                const double byy = Md[t] - vv;
+                const double bxy = Mx[t] - uv;
+#pragma unroll
+                for (int i = 0; i < DT; ++i)
+#pragma unroll
+                    for (int jj = 0; jj < NC; ++jj) sc[jj] -= lc[jj][i] * projv[i];
+                // lanes whose usable candidates are not all dependent at this y
+                // YM 0: no candidate equals y for any lane (a shared window outside y); 1: shared
+                // window holding y (candidate t - cb0 is y: masked by its scalar index); 2: lanes
+                // with different windows (a lane whose window holds y takes the rare path)
+                const int jdead = YM == 1 ? t - cb0 : -1;
+                unsigned long long bad = 0ull;
+#pragma unroll
+                for (int jj = 0; jj < NC; ++jj) {
+                    const double vc = sc[jj] * rl[jj];
+                    const double cyy = byy - vc * vc;
+                    const double cxy = bxy - uc[jj] * vc;
+                    const double num = cxy * cxy;
+                    const double th = hc[jj] * cyy;
+                    const unsigned long long keep = jj == jdead ? 0ull : okv[jj];
+                    // one ballot per compare: each is the compare's own lane mask (no VGPR round trip)
+                    bad |= keep & ~(__builtin_amdgcn_ballot_w64(num > th) &
+                                    __builtin_amdgcn_ballot_w64(fma(th, inv_hi2, -kg) > num));
+                }
+                const unsigned long long inT = __builtin_amdgcn_ballot_w64((bool)((Tmask >> t) & 1u));
+                unsigned long long rarel = (bad | notok) & ~inT;
+                if (YM == 2) rarel |= __builtin_amdgcn_ballot_w64((unsigned)(t - cbase) < (unsigned)nval);
+                if (t < tx) rarel |= __builtin_amdgcn_ballot_w64((lm & Tmask) == Tmask) & ~inT;
+                if (!rarel) return;
+                if (!(rarel & lanebit)) return;
+                // rare path (this lane): the exact live set, the dedup skips, then the per-lane
+                // decision bits from the wave masks
+                const bool own = (t < tx) && ((lm & Tmask) == Tmask);
+                const unsigned tb = ((unsigned)(t - cbase) < (unsigned)TG) ? (1u << (t - cbase)) : 0u;
+                const unsigned skip = own ? (unsigned)(lm >> cbase) : 0u;
+                if ((Tmask >> t) & 1u) return;
+                const unsigned live = vmask & ~tb & ~skip;
+                tcount -= __popc(vmask & ~tb & skip);
+#pragma unroll
+                for (int jj = 0; jj < TG; ++jj) {
+                    if (!((live >> jj) & 1u)) continue;
+                    const int c = cbase + jj;
+                    double s_ = Mt[c];
+#pragma unroll
+                    for (int i = 0; i < DT; ++i) s_ -= lc[jj][i] * projv[i];
+                    const double vc = s_ * rl[jj];
+                    const double cyy = byy - vc * vc;
+                    const double cxy = bxy - uc[jj] * vc;
+                    {   // the fast path's decision, recomputed in the same operation order
+                        const double num = cxy * cxy;
+                        const double th = hc[jj] * cyy;
+                        if (okc[jj] && (num > th) && (fma(th, inv_hi2, -kg) > num)) continue;
+                    }
+                    const double cxx = hc[jj] / a.hi2;
+                    const bool ind = okc[jj] && (cxy * cxy < a.lo2 * cxx * cyy) && (cyy > 0.0) &&
+                                     (cxx * cyy - cxy * cxy > kg);
+                    const Mask Smask = Tmask | ((Mask)1 << c);
+                    if (ind) {
+                        ++indep;
+                        lmask_atomic_or<WIDE>(&uself[t], Smask);
+                        if (((lm & Smask) == Smask) && t >= tx) lmask_atomic_or<WIDE>(&uprop[t], Smask);
+                    } else {
+                        int sg[DM];
+                        sg[0] = nxs[c];
+#pragma unroll
+                        for (int i = 0; i < DT; ++i) sg[i + 1] = nxs[T[i]];
+                        push_deferred(a, x, nxs[t], sg, DM);
+                    }
+                }
+            };
+            using Y0 = std::integral_constant<int, 0>;
+            using Y1 = std::integral_constant<int, 1>;
+            using Y2 = std::integral_constant<int, 2>;
+            if (PCG_TG_SPLIT && uni) {
+                const int w0 = min(cb0, D), w1 = min(cb0 + TG, D);
+                for (int t = 0; t < w0; ++t) ystep(t, Y0{});
+                for (int t = w0; t < w1; ++t) ystep(t, Y1{});
+                for (int t = w1; t < D; ++t) ystep(t, Y0{});
+            } else if (uni) {
+                for (int t = 0; t < D; ++t) ystep(t, Y1{});
+            } else {
+                for (int t = 0; t < D; ++t) ystep(t, Y2{});
+            }
+            return;
+            }
             // YU consecutive y per iteration: their chains are independent, so the in-order issue of
             // one wave has twice the fp64 work in flight (PCG_TG_Y2)
             constexpr int YU = ((PCG_TG_Y2 >> DM) & 1) ? 2 : 1;

@@ -25,8 +25,18 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--no-gpu", action="store_true")
     args = ap.parse_args()
+    import threading
+
     import numpy as np
     from oracle import skeleton as osk
+
+    def heartbeat():      # the GPU pool kills commands silent for 3 minutes
+        t0 = time.perf_counter()
+        while True:
+            time.sleep(20)
+            print(f"[cpu_ref_e2e] {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=heartbeat, daemon=True).start()
     from rcaeval_amd import synth
     rows = []
     for n in args.ns:
