@@ -312,12 +312,23 @@ def main():
 
     phases = []
 
-    # PCG_DIST_NATIVE=1: the level loop and its collectives run in C (pcg_skeleton_sharded on
-    # an RCCL communicator of the library's own); default: the torch.distributed driver
-    native = dist_path and os.environ.get("PCG_DIST_NATIVE") == "1"
+    # default for N > 1: the level loop and its collectives run in C (pcg_skeleton_sharded on an
+    # RCCL communicator of the library's own: one host round trip per depth, no Python in the
+    # loop; at world 1 it adds 0.56 ms per step to the single-GPU call where the torch.distributed
+    # driver adds 1.58 ms). PCG_DIST_NATIVE=0 selects the torch.distributed driver; so does a
+    # communicator that fails to come up on any rank (agreed collectively, no rank left waiting).
+    native = dist_path and os.environ.get("PCG_DIST_NATIVE", "1") == "1"
     if native:
         from rcaeval_amd.dist import native_comm
-        native_comm(eng)
+        ok = 1
+        try:
+            native_comm(eng)
+        except Exception as e:   # noqa: BLE001 - fall back to the torch.distributed driver
+            print(f"[rank {rank}] native RCCL driver unavailable ({e}); using torch.distributed", file=sys.stderr)
+            ok = 0
+        flag = torch.tensor([ok], dtype=torch.int32, device=eng.device if backend == "nccl" else "cpu")
+        torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MIN)
+        native = bool(flag.item())
 
     def one_step():
         t0 = time.perf_counter()
