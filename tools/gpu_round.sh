@@ -25,7 +25,9 @@ step pmc_fetch 200 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-
 step pmc_write 200 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- $B
 step pmc_sq1 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/pmc_sq1 -o run --output-format csv -- $B
 step pmc_sq2 200 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_FLOPS_FP64 SQ_WAVES SQ_INSTS_SALU SQ_ACTIVE_INST_ANY -d $OUT/pmc_sq2 -o run --output-format csv -- $B
+step pmc_mfma 200 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_VALU GRBM_GUI_ACTIVE -d $OUT/pmc_mfma -o run --output-format csv -- $B
 python tools/pmc_summary.py profiles/${TAG}_pmc_summary.json $OUT > $OUT/pmc_summary.log 2>&1 && cp profiles/${TAG}_pmc_summary.json $OUT/
+python tools/timeline.py $OUT/prof/run_kernel_trace.csv > $OUT/${TAG}_timeline.txt 2>&1
 step valu_occ 120 ./tools/micro/valu_occ
 step bench 900 python bench.py --steps 20 --warmup 3
 cat $OUT/round_status.log
