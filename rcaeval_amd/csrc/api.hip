@@ -80,7 +80,9 @@ extern "C" int pcg_destroy(pcg_handle *h) {
     hipSetDevice(h->device);
     if (h->stream) hipStreamSynchronize(h->stream);
     pcg_comm_release(h);
-    DevBuf *bufs[] = {&h->adj, &h->deg, &h->off, &h->nbr, &h->rm, &h->ug, &h->cpre, &h->binom, &h->ctr,
+    if (h->xs) hipStreamSynchronize(h->xs);
+    DevBuf *bufs[] = {&h->adj, &h->deg, &h->off2[0], &h->off2[1], &h->nbr2[0], &h->nbr2[1], &h->rm, &h->ug2[0],
+                      &h->ug2[1], &h->exp_ctr, &h->cpre, &h->binom, &h->ctr,
                       &h->deferred, &h->records, &h->nearbuf, &h->exportbuf, &h->export_xy, &h->diag,
                       &h->colmean, &h->pr_scratch, &h->batch_scratch, &h->chisq_scratch};
     for (DevBuf *b : bufs)
@@ -96,6 +98,10 @@ extern "C" int pcg_destroy(pcg_handle *h) {
     if (h->ev_fork) hipEventDestroy(h->ev_fork);
     if (h->ev_join) hipEventDestroy(h->ev_join);
     if (h->aux) hipStreamDestroy(h->aux);
+    if (h->xs) hipStreamDestroy(h->xs);
+    if (h->ev_xready) hipEventDestroy(h->ev_xready);
+    for (auto &e : h->ev_xdone)
+        if (e) hipEventDestroy(e);
     if (h->own_stream && h->stream) hipStreamDestroy(h->stream);
     delete h;
     return PCG_OK;

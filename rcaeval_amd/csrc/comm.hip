@@ -180,6 +180,8 @@ int reduce_stats(pcg_handle *h) {
 int gather_sepsets(pcg_handle *h) {
     const int world = h->comm_world, W = h->W;
     ncclComm_t comm = (ncclComm_t)h->comm;
+    int rc0 = export_sync(h);
+    if (rc0) return rc0;
     if (!pcg_ensure(h, h->comm_small, sizeof(int64_t) * (size_t)(world + 1)))
         return pcg_fail(h, PCG_ERR_OOM, "row counts");
     int64_t *cnt_d = (int64_t *)h->comm_small.p;

@@ -57,11 +57,23 @@ struct pcg_handle {
     bool own_stream = false;
     std::string err;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    hipEvent_t lev[2 * PCG_MAX_LEVELS] = {};   // per-depth brackets, read once after the last depth
+    hipEvent_t lev[2 * PCG_MAX_LEVELS] = {};   // depth-boundary events (skeleton_once), read after the last depth
+    bool lev_on = false;
+    int lev_n = 0;
 
     // scratch
-    DevBuf adj, deg, off, nbr, rm, ug, cpre, binom, ctr, deferred, records, nearbuf, exportbuf,
-        export_xy, diag, colmean, pr_scratch, batch_scratch, chisq_scratch;
+    DevBuf adj, deg, rm, cpre, binom, ctr, deferred, records, nearbuf, exportbuf, export_xy, diag, colmean,
+        pr_scratch, batch_scratch, chisq_scratch;
+    // CSR (offsets, neighbour lists) and sepset union rows, double-buffered: depth d's sepset
+    // export reads buffer set cb on the export stream while depth d + 1 runs on set 1 - cb
+    DevBuf off2[2], nbr2[2], ug2[2];
+    int cb = 0;                      // buffer set of the current graph
+    bool ug_clean2[2] = {false, false};   // the union rows of set i's CSR are all zero
+    hipStream_t xs = nullptr;        // sepset export stream
+    hipEvent_t ev_xready = nullptr, ev_xdone[2] = {nullptr, nullptr};
+    bool xpending[2] = {false, false};    // an export reading set i is queued on xs
+    bool xany = false;               // exports queued since the last export_sync
+    DevBuf exp_ctr;                  // rows exported so far (device, persists across depths)
     PinBuf ctr_pin, deg_pin, off_pin, cpre_pin, status_pin;
     std::vector<uint64_t> binom_h;   // host copy of the binomial table
     uint8_t *rm_ext = nullptr;       // caller-owned removal-flag buffer (multi-GPU)
@@ -95,10 +107,9 @@ struct pcg_handle {
     LevelSummary *summary = nullptr;    // host-mapped, coherent (graph_launch / level_wait)
     size_t summary_bytes = 0;
     unsigned long long summary_seq = 0;
-    bool ug_clean = false;
     // PCG_HOST_TRACE=1: host timestamps of the level loop's steps, printed after each skeleton
     bool htrace_on = false;
-    std::vector<std::pair<const char *, double>> htrace;              // the union rows of the current CSR are all zero
+    std::vector<std::pair<const char *, double>> htrace;
     std::vector<int32_t> deg_h;      // degrees at the start of the current depth
     std::vector<int32_t> deg_levels; // levels x n
     std::vector<int64_t> cpre_h;     // 3 x (n + 1): narrow, wide, large class chunk prefixes
@@ -121,6 +132,7 @@ struct pcg_handle {
 
 void pcg_comm_release(pcg_handle *h);      // comm.hip: destroy the communicator, free its buffers
 // corr.hip: K1 queued on h->stream without the host sync of pcg_corr (pcg_pc_skeleton)
+int export_sync(pcg_handle *h);   // skeleton.hip: wait for the sepset exports, take their row count
 int pcg_corr_launch(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx, double *C, int64_t ldc);
 
 int pcg_fail(pcg_handle *h, int code, const char *fmt, ...);

@@ -231,88 +231,112 @@ __global__ void k_diag(const double *C, int64_t ldc, int n, double *diag, int32_
     }
 }
 
-// The level barrier's host summary, one block: the CSR offsets of the new graph (exclusive
-// scan of the degrees k_apply keeps current), the degrees, level counters and merged status
-// bytes written straight into host-mapped memory, then — after a system-scope fence — the
-// sequence number the host spins on. Replaces three device-to-host copies and a stream
-// synchronisation per depth; the counters and status bytes are cleared once copied.
-__global__ __launch_bounds__(1024) void k_level_summary(const int32_t *deg, int n, int32_t *off, DevCounters *ctr,
-                                                        uint8_t *status, LevelSummary *out, int32_t *out_deg,
-                                                        unsigned long long seq) {
-    __shared__ int32_t part[1024];
-    const int tid = threadIdx.x;
-    const int per = (n + 1023) / 1024;
-    const int lo = min(n, tid * per), hi = min(n, lo + per);
-    int32_t s = 0;
-    for (int i = lo; i < hi; ++i) {
-        const int32_t v = deg[i];
-        out_deg[i] = v;
-        s += v;
-    }
-    part[tid] = s;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {       // inclusive Hillis-Steele scan of the chunk sums
-        const int32_t v = tid >= o ? part[tid - o] : 0;
-        __syncthreads();
-        part[tid] += v;
-        __syncthreads();
-    }
-    int32_t acc = tid ? part[tid - 1] : 0;
-    for (int i = lo; i < hi; ++i) { off[i] = acc; acc += deg[i]; }
-    if (tid == 1023) off[n] = part[1023];
-    if (tid == 0) {
-        out->ctr = *ctr;
-        *ctr = DevCounters{};
-        for (int k = 0; k < 8; ++k) out->status[k] = status ? status[k] : 0;
-        if (status)
-            for (int k = 0; k < PCG_RM_STATUS; ++k) status[k] = 0;
-    }
-    __threadfence_system();
-    __syncthreads();
-    if (tid == 0) {
-        __threadfence_system();
-        __atomic_store_n(&out->seq, seq, __ATOMIC_RELEASE);
-    }
-}
+constexpr int EXPORT_GROUP = 8;     // union rows in flight per wave in the sepset export
 
-// one wave per node: ascending neighbour list from the bitmask (wave prefix scan); with ug,
-// also clears the node's union rows (one W-word row per CSR slot) for the coming depth
-__global__ void k_fill_nbr(const uint64_t *adj, int n, int W, const int32_t *off, int32_t *nbr, uint64_t *ug) {
-    const int x = blockIdx.x;
-    const int lane = threadIdx.x;
-    int base = off[x];
-    if (ug) {
-        const int64_t lo = (int64_t)base * W, hi = (int64_t)off[x + 1] * W;
-        for (int64_t e = lo + lane; e < hi; e += 64) ug[e] = 0ull;
-    }
-    for (int w0 = 0; w0 < W; w0 += 64) {
-        const int w = w0 + lane;
-        uint64_t v = w < W ? adj[(int64_t)x * W + w] : 0ull;
-        const int c = __popcll(v);
-        int incl = c;
+// sepset export helpers: lane k of a wave owns CSR slot slot0 + k of node x; rows of removed
+// slots are read with all 64 lanes, eight rows' loads in flight
+// pass 1: the mask of the wave's removed slots whose W-word union row is non-empty
+__device__ __forceinline__ unsigned long long export_keep(int64_t slot0, bool removed, const uint64_t *ug, int W,
+                                                         int wid = 0, int nw = 1) {
+    const int lane = threadIdx.x & 63;
+    unsigned long long keepm = 0;
+    int gi = 0;     // groups of eight candidates are dealt round-robin over nw waves; this is wave wid
+    for (unsigned long long mm = __ballot(removed); mm; ++gi) {
+        int ks[EXPORT_GROUP];
+        int cnt = 0;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int t = __shfl_up(incl, o);
-            if (lane >= o) incl += t;
+        for (int g = 0; g < EXPORT_GROUP; ++g) {
+            ks[g] = mm ? __ffsll((long long)mm) - 1 : 0;
+            if (mm) { mm &= mm - 1; ++cnt; }
         }
-        const int tot = __shfl(incl, 63);
-        int pos = base + incl - c;
-        while (v) {
-            const int b = __ffsll((long long)v) - 1;
-            nbr[pos++] = w * 64 + b;
-            v &= v - 1;
+        if (gi % nw != wid) continue;
+        uint64_t v[EXPORT_GROUP];
+#pragma unroll
+        for (int g = 0; g < EXPORT_GROUP; ++g) v[g] = 0ull;
+        for (int w = lane; w < W; w += 64)
+#pragma unroll
+            for (int g = 0; g < EXPORT_GROUP; ++g)
+                if (g < cnt) v[g] |= ug[(slot0 + ks[g]) * W + w];
+#pragma unroll
+        for (int g = 0; g < EXPORT_GROUP; ++g)
+            if (g < cnt && __ballot(v[g] != 0ull)) keepm |= 1ull << ks[g];
+    }
+    return keepm;
+}
+
+// pass 2: copy the kept rows (already L2-resident from pass 1) to rows base, base + 1, ...
+__device__ __forceinline__ void export_copy(int64_t slot0, unsigned long long keepm, int64_t base, int x, int y,
+                                            const uint64_t *ug, int W, int32_t *xy, uint64_t *bits, int64_t cap,
+                                            int wid = 0, int nw = 1) {
+    const int lane = threadIdx.x & 63;
+    if (wid == 0 && ((keepm >> lane) & 1ull)) {      // the lane owning the slot writes its (x, y)
+        const int64_t r = base + __popcll(keepm & ((1ull << lane) - 1ull));
+        if (r < cap) {
+            xy[2 * r] = x;
+            xy[2 * r + 1] = y;
         }
-        base += tot;
+    }
+    int gi = 0;
+    for (unsigned long long mm = keepm; mm; ++gi) {
+        int ks[EXPORT_GROUP];
+        int cnt = 0;
+#pragma unroll
+        for (int g = 0; g < EXPORT_GROUP; ++g) {
+            ks[g] = mm ? __ffsll((long long)mm) - 1 : 0;
+            if (mm) { mm &= mm - 1; ++cnt; }
+        }
+        if (gi % nw != wid) continue;
+        for (int w = lane; w < W; w += 64) {
+            uint64_t v[EXPORT_GROUP];
+#pragma unroll
+            for (int g = 0; g < EXPORT_GROUP; ++g) v[g] = g < cnt ? ug[(slot0 + ks[g]) * W + w] : 0ull;
+#pragma unroll
+            for (int g = 0; g < EXPORT_GROUP; ++g) {
+                if (g >= cnt) break;
+                const int64_t r = base + __popcll(keepm & ((1ull << ks[g]) - 1ull));
+                if (r < cap) bits[r * W + w] = v[g];
+            }
+        }
     }
 }
 
-// rm -> adjacency bitmask + removed_level (the level barrier, SkeletonDiscovery.py:141-144).
-// One block per row x, one lane per removal byte (coalesced 64-byte row segments, the 4 waves
-// take every 4th adjacency word); a wave's ballot is the 64-bit mask cleared from adjacency
-// word (x, w), and the row's removed count lowers deg[x] once (degrees stay current for
-// k_level_summary). rm is the last read here: set bytes are cleared for the next depth.
-__global__ __launch_bounds__(256) void k_apply(uint8_t *rm, uint64_t *adj, int32_t *deg, int8_t *rl, int n, int W,
-                                               int d) {
+// The sepset export of depth d, off the level loop's critical path (export stream, double-
+// buffered CSR and union rows): one lane per CSR slot (x, y) of depth d's graph finds x, keeps
+// the slot if the pair was removed at this depth (removed_level == d) and its union row is
+// non-empty, and the wave appends its kept rows with one atomic on a counter that persists
+// across depths (rows are read with all 64 lanes, eight in flight).
+__global__ __launch_bounds__(256) void k_export(const int32_t *off, const int32_t *nbr, const int8_t *rl, int d,
+                                                const uint64_t *ug, int n, int W, int64_t sumdeg, int32_t *xy,
+                                                uint64_t *bits, int64_t cap, unsigned long long *ctr) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave_base = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63);
+    const int64_t slot = wave_base + lane;
+    int x = -1, y = -1;
+    bool removed = false;
+    if (slot < sumdeg) {
+        int lo = 0, hi = n;  // off[lo] <= slot < off[hi]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (off[mid] <= slot) lo = mid; else hi = mid;
+        }
+        x = lo;
+        y = nbr[slot];
+        removed = rl[(int64_t)x * n + y] == (int8_t)d;
+    }
+    const unsigned long long keepm = export_keep(wave_base, removed, ug, W);
+    if (!keepm) return;
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(ctr, (unsigned long long)__popcll(keepm));
+    base = __shfl(base, 0);
+    export_copy(wave_base, keepm, (int64_t)base, x, y, ug, W, xy, bits, cap);
+}
+
+// The level barrier (SkeletonDiscovery.py:141-144), one 256-thread block per row x: rm row x ->
+// adjacency words (a wave's ballot is the mask cleared from word (x, w)) + removed_level, deg[x]
+// lowered by the row's removed count; rm is the last read here, so set bytes are cleared for the
+// next depth.
+__global__ __launch_bounds__(256) void k_level_close(uint8_t *rm, uint64_t *adj, int32_t *deg, int8_t *rl, int n,
+                                                     int W, int d) {
     __shared__ int cleared[4];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x = blockIdx.x;
@@ -342,81 +366,85 @@ __global__ __launch_bounds__(256) void k_apply(uint8_t *rm, uint64_t *adj, int32
     }
 }
 
-// export non-empty union rows of removed ordered pairs: one lane per CSR slot finds its (x, y)
-// and whether the pair was removed; the wave then reads its removed pairs' W-word rows with all
-// 64 lanes (coalesced), eight rows' loads in flight at a time, keeps the non-empty ones and
-// compacts them with one atomic (ballot + mbcnt).
-constexpr int EXPORT_GROUP = 8;
-__global__ __launch_bounds__(256) void k_export(const int32_t *off, const int32_t *nbr, const uint8_t *rm,
-                                                const uint64_t *ug, int n, int W, int64_t sumdeg, int32_t *xy,
-                                                uint64_t *bits, int64_t cap, unsigned long long *ctr) {
-    const int lane = threadIdx.x & 63;
-    const int64_t wave_base = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63);
-    const int64_t slot = wave_base + lane;
-    int x = -1, y = -1;
-    bool removed = false;
-    if (slot < sumdeg) {
-        int lo = 0, hi = n;  // off[lo] <= slot < off[hi]
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (off[mid] <= slot) lo = mid; else hi = mid;
+// The level barrier's summary and the next depth's CSR in one launch. Blocks 0 .. ceil(n/4)-1:
+// one wave per node x builds its ascending neighbour list from the adjacency row at offset
+// sum(deg[0..x)) (each wave sums the prefix itself, so no grid-wide scan is waited for) and, with
+// ug, clears the node's union rows. The last block: the CSR offsets (exclusive scan of deg), the
+// degrees, level counters and merged status bytes written into host-mapped memory, then — after
+// a system-scope fence — the sequence number the host spins on (the host then enqueues work that
+// the stream orders after the whole grid). Counters and status bytes are cleared once copied.
+__global__ __launch_bounds__(256) void k_summary_fill(const int32_t *deg, int n, int W, const uint64_t *adj,
+                                                      int32_t *off, int32_t *nbr, uint64_t *ug, DevCounters *ctr,
+                                                      uint8_t *status, LevelSummary *out, int32_t *out_deg,
+                                                      unsigned long long seq) {
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int nfill = (n + 3) / 4;
+    if ((int)blockIdx.x < nfill) {
+        const int x = blockIdx.x * 4 + (tid >> 6);
+        if (x >= n) return;
+        int ps = 0;
+        for (int i = lane; i < x; i += 64) ps += deg[i];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) ps += __shfl_xor(ps, o);
+        int base = ps;
+        if (ug) {
+            const int64_t lo = (int64_t)base * W, hi = (int64_t)(base + deg[x]) * W;
+            for (int64_t e = lo + lane; e < hi; e += 64) ug[e] = 0ull;
         }
-        x = lo;
-        y = nbr[slot];
-        removed = rm[(int64_t)x * n + y] != 0;
-    }
-    const unsigned long long cand = __ballot(removed);
-    if (!cand) return;
-    unsigned long long keepm = 0;
-    for (unsigned long long mm = cand; mm;) {
-        int ks[EXPORT_GROUP];
-        int cnt = 0;
+        for (int w0 = 0; w0 < W; w0 += 64) {
+            const int w = w0 + lane;
+            uint64_t v = w < W ? adj[(int64_t)x * W + w] : 0ull;
+            const int c = __popcll(v);
+            int incl = c;
 #pragma unroll
-        for (int g = 0; g < EXPORT_GROUP; ++g) {
-            ks[g] = mm ? __ffsll((long long)mm) - 1 : 0;
-            if (mm) { mm &= mm - 1; ++cnt; }
-        }
-        uint64_t v[EXPORT_GROUP];
-#pragma unroll
-        for (int g = 0; g < EXPORT_GROUP; ++g) v[g] = 0;
-        for (int w = lane; w < W; w += 64)
-#pragma unroll
-            for (int g = 0; g < EXPORT_GROUP; ++g)
-                if (g < cnt) v[g] |= ug[(wave_base + ks[g]) * W + w];
-#pragma unroll
-        for (int g = 0; g < EXPORT_GROUP; ++g)
-            if (g < cnt && __ballot(v[g] != 0)) keepm |= 1ull << ks[g];
-    }
-    if (!keepm) return;
-    unsigned long long base = 0;
-    if (lane == 0) base = atomicAdd(ctr, (unsigned long long)__popcll(keepm));
-    base = __shfl(base, 0);
-    if ((keepm >> lane) & 1ull) {
-        const int64_t r = (int64_t)base + __popcll(keepm & ((1ull << lane) - 1ull));
-        if (r < cap) {
-            xy[2 * r] = x;
-            xy[2 * r + 1] = y;
-        }
-    }
-    for (unsigned long long mm = keepm; mm;) {
-        int ks[EXPORT_GROUP];
-        int cnt = 0;
-#pragma unroll
-        for (int g = 0; g < EXPORT_GROUP; ++g) {
-            ks[g] = mm ? __ffsll((long long)mm) - 1 : 0;
-            if (mm) { mm &= mm - 1; ++cnt; }
-        }
-        for (int w = lane; w < W; w += 64) {
-            uint64_t v[EXPORT_GROUP];
-#pragma unroll
-            for (int g = 0; g < EXPORT_GROUP; ++g) v[g] = g < cnt ? ug[(wave_base + ks[g]) * W + w] : 0ull;
-#pragma unroll
-            for (int g = 0; g < EXPORT_GROUP; ++g) {
-                if (g >= cnt) break;
-                const int64_t r = (int64_t)base + __popcll(keepm & ((1ull << ks[g]) - 1ull));
-                if (r < cap) bits[r * W + w] = v[g];
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(incl, o);
+                if (lane >= o) incl += t;
             }
+            const int tot = __shfl(incl, 63);
+            int pos = base + incl - c;
+            while (v) {
+                const int b = __ffsll((long long)v) - 1;
+                nbr[pos++] = w * 64 + b;
+                v &= v - 1;
+            }
+            base += tot;
         }
+        return;
+    }
+    __shared__ int32_t part[256];
+    const int per = (n + 255) / 256;
+    const int lo = min(n, tid * per), hi = min(n, lo + per);
+    int32_t sum = 0;
+    for (int i = lo; i < hi; ++i) {
+        const int32_t v = deg[i];
+        out_deg[i] = v;
+        sum += v;
+    }
+    part[tid] = sum;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {        // inclusive Hillis-Steele scan of the chunk sums
+        const int32_t v = tid >= o ? part[tid - o] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    int32_t acc = tid ? part[tid - 1] : 0;
+    for (int i = lo; i < hi; ++i) { off[i] = acc; acc += deg[i]; }
+    if (tid == 255) off[n] = part[255];
+    if (tid == 0) {
+        out->ctr = *ctr;
+        *ctr = DevCounters{};
+        for (int k = 0; k < 8; ++k) out->status[k] = status ? status[k] : 0;
+        if (status)
+            for (int k = 0; k < PCG_RM_STATUS; ++k) status[k] = 0;
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (tid == 0) {
+        __threadfence_system();
+        __atomic_store_n(&out->seq, seq, __ATOMIC_RELEASE);
     }
 }
 
@@ -1926,12 +1954,12 @@ LevelArgs make_args(pcg_handle *h, int d, int mode_exact_all) {
     a.d = d;
     a.bs = h->chunk;
     a.deg = (const int32_t *)h->deg.p;
-    a.off = (const int32_t *)h->off.p;
-    a.nbr = (const int32_t *)h->nbr.p;
+    a.off = (const int32_t *)h->off2[h->cb].p;
+    a.nbr = (const int32_t *)h->nbr2[h->cb].p;
     a.cpre = (const int64_t *)h->cpre.p;
     a.binom = (const uint64_t *)h->binom.p;
     a.rm = h->rm_ext ? h->rm_ext : (uint8_t *)h->rm.p;
-    a.ug = (uint64_t *)h->ug.p;
+    a.ug = (uint64_t *)h->ug2[h->cb].p;
     a.ctr = (DevCounters *)h->ctr.p;
     a.deferred = (DeferredEntry *)h->deferred.p;
     a.def_cap = h->def_cap;
@@ -2052,19 +2080,32 @@ int graph_launch(pcg_handle *h) {
     // summary; nbr is sized by the current graph (degrees only fall), and the union rows are
     // cleared along with it when the buffer already covers that bound
     const int64_t bound = h->depth < 0 ? (int64_t)n * (n - 1) : h->sumdeg;
-    if (!pcg_ensure(h, h->off, sizeof(int32_t) * (n + 1)) ||
-        !pcg_ensure(h, h->nbr, sizeof(int32_t) * std::max<int64_t>(bound, 1)))
+    // the new graph's CSR goes to the other buffer set; an export still reading that set (depth
+    // d - 1's) is waited for on the device first
+    const int t = h->depth < 0 ? 0 : 1 - h->cb;
+    if (h->xpending[t]) {
+        PCG_HIP(h, hipStreamWaitEvent(h->stream, h->ev_xdone[t], 0));
+        h->xpending[t] = false;
+    }
+    if (!pcg_ensure(h, h->off2[t], sizeof(int32_t) * (n + 1)) ||
+        !pcg_ensure(h, h->nbr2[t], sizeof(int32_t) * std::max<int64_t>(bound, 1)))
         return pcg_fail(h, PCG_ERR_OOM, "neighbour lists");
-    hipLaunchKernelGGL(k_level_summary, dim3(1), dim3(1024), 0, h->stream, (const int32_t *)h->deg.p, n,
-                       (int32_t *)h->off.p, (DevCounters *)h->ctr.p, status, ds, reinterpret_cast<int32_t *>(ds + 1),
-                       seq);
     uint64_t *ug = nullptr;
-    if (h->depth >= 0 && h->ug.p && h->ug.bytes >= sizeof(uint64_t) * (size_t)std::max<int64_t>(bound, 1) * W)
-        ug = (uint64_t *)h->ug.p;
-    h->ug_clean = ug != nullptr;
-    hipLaunchKernelGGL(k_fill_nbr, dim3(n), dim3(64), 0, h->stream, (const uint64_t *)h->adj.p, n, W,
-                       (const int32_t *)h->off.p, (int32_t *)h->nbr.p, ug);
+    if (h->depth >= 0 && h->ug2[t].p &&
+        h->ug2[t].bytes >= sizeof(uint64_t) * (size_t)std::max<int64_t>(bound, 1) * W)
+        ug = (uint64_t *)h->ug2[t].p;
+    h->ug_clean2[t] = ug != nullptr;
+    hipLaunchKernelGGL(k_summary_fill, dim3((unsigned)((n + 3) / 4 + 1)), dim3(256), 0, h->stream,
+                       (const int32_t *)h->deg.p, n, W, (const uint64_t *)h->adj.p, (int32_t *)h->off2[t].p,
+                       (int32_t *)h->nbr2[t].p, ug, (DevCounters *)h->ctr.p, status, ds,
+                       reinterpret_cast<int32_t *>(ds + 1), seq);
+    h->cb = t;
     PCG_HIP(h, hipGetLastError());
+    if (h->lev_on && h->lev_n < 2 * PCG_MAX_LEVELS) {   // depth boundary (skeleton_once), off the host's critical path
+        hipEvent_t &e = h->lev[h->lev_n++];
+        if (!e) PCG_HIP(h, hipEventCreate(&e));
+        PCG_HIP(h, hipEventRecord(e, h->stream));
+    }
     return PCG_OK;
 }
 
@@ -2133,6 +2174,10 @@ extern "C" int pcg_skeleton_init(pcg_handle *h, const double *C, int64_t n, int6
     h->W = (int)((n + 63) / 64);
     h->depth = -1;
     h->deg_levels.clear();
+    if (h->xs) PCG_HIP(h, hipStreamSynchronize(h->xs));   // a previous run's exports are done
+    h->xpending[0] = h->xpending[1] = false;
+    h->xany = false;
+    h->cb = 0;
     h->export_rows = 0;
     h->rec_h.clear(); h->near_h.clear();
     h->rec_total = h->near_total = 0;
@@ -2140,7 +2185,7 @@ extern "C" int pcg_skeleton_init(pcg_handle *h, const double *C, int64_t n, int6
     const int W = h->W;
     if (!pcg_ensure(h, h->adj, sizeof(uint64_t) * n * W) || !pcg_ensure(h, h->deg, sizeof(int32_t) * n) ||
         !pcg_ensure(h, h->diag, sizeof(double) * n) || !pcg_ensure(h, h->rm, (size_t)n * n + PCG_RM_STATUS) ||
-        !pcg_ensure(h, h->ctr, sizeof(DevCounters)) ||
+        !pcg_ensure(h, h->ctr, sizeof(DevCounters)) || !pcg_ensure(h, h->exp_ctr, sizeof(unsigned long long)) ||
         !pcg_ensure(h, h->deferred, sizeof(DeferredEntry) * h->def_cap) ||
         !pcg_ensure(h, h->nearbuf, sizeof(pcg_record) * h->near_cap) ||
         !pcg_ensure(h, h->records, sizeof(pcg_record) * std::max<int64_t>(h->rec_cap, 1)))
@@ -2160,6 +2205,7 @@ extern "C" int pcg_skeleton_init(pcg_handle *h, const double *C, int64_t n, int6
     PCG_HIP(h, hipMemsetAsync(removed_level, 0xFF, (size_t)n * n, h->stream));
     PCG_HIP(h, hipGetLastError());
     PCG_HIP(h, hipMemsetAsync(h->rm_ext ? (void *)h->rm_ext : h->rm.p, 0, (size_t)n * n + PCG_RM_STATUS, h->stream));
+    PCG_HIP(h, hipMemsetAsync(h->exp_ctr.p, 0, sizeof(unsigned long long), h->stream));
     int rc = graph_launch(h);            // also clears the counters
     if (!rc) rc = level_wait(h);
     if (rc) return rc;
@@ -2301,10 +2347,11 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
     PCG_HT(h, "begin:prefix-copy-launched");
     if (depth >= 1) {
         const size_t ugb = sizeof(uint64_t) * (size_t)std::max<int64_t>(h->sumdeg, 1) * h->W;
-        void *before = h->ug.p;
-        if (!pcg_ensure(h, h->ug, ugb)) return pcg_fail(h, PCG_ERR_OOM, "sepset union rows (%zu B)", ugb);
-        if (h->ug.p != before || !h->ug_clean) PCG_HIP(h, hipMemsetAsync(h->ug.p, 0, ugb, h->stream));
-        h->ug_clean = false;
+        DevBuf &ugb_ = h->ug2[h->cb];
+        void *before = ugb_.p;
+        if (!pcg_ensure(h, ugb_, ugb)) return pcg_fail(h, PCG_ERR_OOM, "sepset union rows (%zu B)", ugb);
+        if (ugb_.p != before || !h->ug_clean2[h->cb]) PCG_HIP(h, hipMemsetAsync(ugb_.p, 0, ugb, h->stream));
+        h->ug_clean2[h->cb] = false;
         if (depth == 1 || h->export_cap == 0) {
             // every ordered pair adjacent at depth 1 is exported at most once over all depths
             // (depth-0 removals carry empty sepsets), so one allocation covers the run
@@ -2526,23 +2573,33 @@ extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
     if (!h || h->depth < 0) return pcg_fail(h, PCG_ERR_INVALID, "pcg_level_end without begin");
     const int d = h->depth, n = (int)h->n, W = h->W;
     uint8_t *rmb = h->rm_ext ? h->rm_ext : (uint8_t *)h->rm.p;
-    DevCounters *ctr = (DevCounters *)h->ctr.p;
     // everything below is stream-ordered; the level costs ONE host sync: export the unions of
     // removed pairs (device-side append), apply the removals (SkeletonDiscovery.py:141-144),
     // recount degrees, and fetch counters + status + degrees in one batch
-    const int64_t room = h->export_cap - h->export_rows;
-    (void)W;
-    if (d >= 1 && h->sumdeg > 0)
-        hipLaunchKernelGGL(k_export, dim3((unsigned)((h->sumdeg + 255) / 256)), dim3(256), 0, h->stream,
-                           (const int32_t *)h->off.p, (const int32_t *)h->nbr.p, (const uint8_t *)rmb,
-                           (const uint64_t *)h->ug.p, n, W, h->sumdeg,
-                           (int32_t *)h->export_xy.p + 2 * h->export_rows,
-                           (uint64_t *)h->exportbuf.p + h->export_rows * W, room, &ctr->exported);
-    hipLaunchKernelGGL(k_apply, dim3((unsigned)n), dim3(256), 0, h->stream, rmb,
-                       (uint64_t *)h->adj.p, (int32_t *)h->deg.p, h->rl, n, W, d);
+    hipLaunchKernelGGL(k_level_close, dim3((unsigned)n), dim3(256), 0, h->stream, rmb, (uint64_t *)h->adj.p,
+                       (int32_t *)h->deg.p, h->rl, n, W, d);
     PCG_HIP(h, hipGetLastError());
     PCG_HT(h, "end:tail-launched");
+    const int xcb = h->cb;               // depth d's CSR / union buffer set (graph_launch flips cb)
+    const int64_t xsum = h->sumdeg;
     int rc = graph_launch(h);            // degrees + counters + status -> host-mapped summary
+    if (!rc && d >= 1 && xsum > 0) {
+        // depth d's sepset export on the export stream, queued behind the barrier (removed_level
+        // written); it reads buffer set xcb while the next depth runs on the other set
+        if (!h->xs) PCG_HIP(h, hipStreamCreateWithFlags(&h->xs, hipStreamNonBlocking));
+        if (!h->ev_xready) PCG_HIP(h, hipEventCreateWithFlags(&h->ev_xready, hipEventDisableTiming));
+        if (!h->ev_xdone[xcb]) PCG_HIP(h, hipEventCreateWithFlags(&h->ev_xdone[xcb], hipEventDisableTiming));
+        PCG_HIP(h, hipEventRecord(h->ev_xready, h->stream));
+        PCG_HIP(h, hipStreamWaitEvent(h->xs, h->ev_xready, 0));
+        hipLaunchKernelGGL(k_export, dim3((unsigned)((xsum + 255) / 256)), dim3(256), 0, h->xs,
+                           (const int32_t *)h->off2[xcb].p, (const int32_t *)h->nbr2[xcb].p,
+                           (const int8_t *)h->rl, d, (const uint64_t *)h->ug2[xcb].p, n, W, xsum,
+                           (int32_t *)h->export_xy.p, (uint64_t *)h->exportbuf.p, h->export_cap,
+                           (unsigned long long *)h->exp_ctr.p);
+        PCG_HIP(h, hipEventRecord(h->ev_xdone[xcb], h->xs));
+        h->xpending[xcb] = true;
+        h->xany = true;
+    }
     PCG_HT(h, "end:summary-launched");
     if (!rc) rc = level_wait(h);
     if (rc) return rc;
@@ -2599,10 +2656,6 @@ extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
                         singular ? "Data correlation matrix is singular. Cannot run fisherz test. Please check your data."
                                  : "math domain error");
     }
-    if (d >= 1 && h->sumdeg > 0) {
-        if ((int64_t)c.exported > room) return pcg_fail(h, PCG_ERR_OVERFLOW, "sepset export overflow");
-        h->export_rows += (int64_t)c.exported;
-    }
     graph_finish(h);
     h->st.edges_after[d] = h->sumdeg / 2;
     PCG_HT(h, "end:done");
@@ -2615,35 +2668,36 @@ static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc,
     h->htrace_on = getenv("PCG_HOST_TRACE") != nullptr;
     h->htrace.clear();
     PCG_HT(h, "init:start");
+    // level d's wall time = between the depth-boundary events graph_launch records after init's
+    // and after each depth's barrier launches (lev[d], lev[d + 1]), read after the last depth
+    h->lev_on = true;
+    h->lev_n = 0;
     int rc = pcg_skeleton_init(h, C, n, ldc, N, alpha, flags, removed_level);
-    if (rc) return rc;
+    if (rc) { h->lev_on = false; return rc; }
     PCG_HT(h, "init:done");
-    // per-depth wall brackets are recorded on the stream and read after the last depth, so the
-    // level loop keeps its one host sync per depth (the one inside pcg_level_end)
     int done = 0;
     for (int depth = 0;; ++depth) {
         if (max_depth >= 0 && depth > max_depth) break;
         if (depth >= PCG_MAX_LEVELS) break;   // pcg_level_begin refuses deeper levels itself
-        for (int k = 0; k < 2; ++k)
-            if (!h->lev[2 * depth + k]) PCG_HIP(h, hipEventCreate(&h->lev[2 * depth + k]));
         int64_t total = 0;
-        PCG_HIP(h, hipEventRecord(h->lev[2 * depth], h->stream));
         PCG_HT(h, "loop:begin");
         rc = pcg_level_begin(h, depth, &total, nullptr, nullptr);
         if (rc == 1) break;
-        if (rc) return rc;
-        rc = pcg_level_run(h, 0, total);
-        if (rc) return rc;
-        rc = pcg_level_end(h, nullptr);
-        if (rc) return rc;
-        PCG_HIP(h, hipEventRecord(h->lev[2 * depth + 1], h->stream));
+        if (!rc) rc = pcg_level_run(h, 0, total);
+        if (!rc) rc = pcg_level_end(h, nullptr);
+        if (rc) { h->lev_on = false; return rc; }
         done = depth + 1;
     }
-    if (done) PCG_HIP(h, hipEventSynchronize(h->lev[2 * done - 1]));
-    for (int depth = 0; depth < done; ++depth) {
-        float ms = 0.f;
-        PCG_HIP(h, hipEventElapsedTime(&ms, h->lev[2 * depth], h->lev[2 * depth + 1]));
-        h->st.level_ms[depth] = ms;
+    h->lev_on = false;
+    rc = export_sync(h);                 // the last depth's export (the skeleton's sepset rows)
+    if (rc) return rc;
+    if (done && h->lev_n > done) {
+        PCG_HIP(h, hipEventSynchronize(h->lev[done]));
+        for (int depth = 0; depth < done; ++depth) {
+            float ms = 0.f;
+            PCG_HIP(h, hipEventElapsedTime(&ms, h->lev[depth], h->lev[depth + 1]));
+            h->st.level_ms[depth] = ms;
+        }
     }
     if (h->htrace_on && !h->htrace.empty()) {
         const double t0 = h->htrace.front().second;
@@ -2675,6 +2729,21 @@ extern "C" int pcg_pc_skeleton(pcg_handle *h, const double *X, int64_t N, int64_
     return pcg_skeleton(h, C, n, ldc, N, alpha, max_depth, flags, removed_level, stats);
 }
 
+// wait for the queued sepset exports and take their row count (the export stream's counter)
+int export_sync(pcg_handle *h) {
+    if (!h->xany) return PCG_OK;
+    PCG_HIP(h, hipStreamSynchronize(h->xs));
+    unsigned long long rows = 0;
+    PCG_HIP(h, hipMemcpy(&rows, h->exp_ctr.p, sizeof(rows), hipMemcpyDeviceToHost));
+    h->xany = false;
+    h->xpending[0] = h->xpending[1] = false;
+    if ((int64_t)rows > h->export_cap)
+        return pcg_fail(h, PCG_ERR_OVERFLOW, "sepset export overflow (%llu rows > %lld)", rows,
+                        (long long)h->export_cap);
+    h->export_rows = (int64_t)rows;
+    return PCG_OK;
+}
+
 extern "C" int pcg_degrees(pcg_handle *h, int32_t *deg_host, int64_t capacity) {
     if (!h || !deg_host || capacity < (int64_t)h->deg_levels.size())
         return pcg_fail(h, PCG_ERR_INVALID, "pcg_degrees: capacity %lld < %zu", (long long)capacity,
@@ -2685,13 +2754,18 @@ extern "C" int pcg_degrees(pcg_handle *h, int32_t *deg_host, int64_t capacity) {
 
 extern "C" int pcg_sepset_count(pcg_handle *h, int64_t *count, int32_t *words_per_row) {
     if (!h) return PCG_ERR_INVALID;
+    const int rc = export_sync(h);
+    if (rc) return rc;
     if (count) *count = h->export_rows;
     if (words_per_row) *words_per_row = h->W;
     return PCG_OK;
 }
 
 extern "C" int pcg_sepset_export(pcg_handle *h, int32_t *xy_host, uint64_t *bits_host, int64_t count) {
-    if (!h || count > h->export_rows) return pcg_fail(h, PCG_ERR_INVALID, "pcg_sepset_export: count");
+    if (!h) return PCG_ERR_INVALID;
+    const int rc = export_sync(h);
+    if (rc) return rc;
+    if (count > h->export_rows) return pcg_fail(h, PCG_ERR_INVALID, "pcg_sepset_export: count");
     if (count == 0) return PCG_OK;
     PCG_HIP(h, hipMemcpy(xy_host, h->export_xy.p, sizeof(int32_t) * 2 * count, hipMemcpyDeviceToHost));
     PCG_HIP(h, hipMemcpy(bits_host, h->exportbuf.p, sizeof(uint64_t) * count * h->W, hipMemcpyDeviceToHost));
@@ -2699,7 +2773,10 @@ extern "C" int pcg_sepset_export(pcg_handle *h, int32_t *xy_host, uint64_t *bits
 }
 
 extern "C" int pcg_sepset_export_device(pcg_handle *h, int32_t *xy_dev, uint64_t *bits_dev, int64_t count) {
-    if (!h || count > h->export_rows) return pcg_fail(h, PCG_ERR_INVALID, "pcg_sepset_export_device: count");
+    if (!h) return PCG_ERR_INVALID;
+    const int rc = export_sync(h);
+    if (rc) return rc;
+    if (count > h->export_rows) return pcg_fail(h, PCG_ERR_INVALID, "pcg_sepset_export_device: count");
     if (count == 0) return PCG_OK;
     PCG_HIP(h, hipMemcpyAsync(xy_dev, h->export_xy.p, sizeof(int32_t) * 2 * count, hipMemcpyDeviceToDevice,
                               h->stream));
