@@ -236,12 +236,10 @@ constexpr int EXPORT_GROUP = 8;     // union rows in flight per wave in the seps
 // sepset export helpers: lane k of a wave owns CSR slot slot0 + k of node x; rows of removed
 // slots are read with all 64 lanes, eight rows' loads in flight
 // pass 1: the mask of the wave's removed slots whose W-word union row is non-empty
-__device__ __forceinline__ unsigned long long export_keep(int64_t slot0, bool removed, const uint64_t *ug, int W,
-                                                         int wid = 0, int nw = 1) {
+__device__ __forceinline__ unsigned long long export_keep(int64_t slot0, bool removed, const uint64_t *ug, int W) {
     const int lane = threadIdx.x & 63;
     unsigned long long keepm = 0;
-    int gi = 0;     // groups of eight candidates are dealt round-robin over nw waves; this is wave wid
-    for (unsigned long long mm = __ballot(removed); mm; ++gi) {
+    for (unsigned long long mm = __ballot(removed); mm;) {
         int ks[EXPORT_GROUP];
         int cnt = 0;
 #pragma unroll
@@ -249,7 +247,6 @@ __device__ __forceinline__ unsigned long long export_keep(int64_t slot0, bool re
             ks[g] = mm ? __ffsll((long long)mm) - 1 : 0;
             if (mm) { mm &= mm - 1; ++cnt; }
         }
-        if (gi % nw != wid) continue;
         uint64_t v[EXPORT_GROUP];
 #pragma unroll
         for (int g = 0; g < EXPORT_GROUP; ++g) v[g] = 0ull;
@@ -266,18 +263,16 @@ __device__ __forceinline__ unsigned long long export_keep(int64_t slot0, bool re
 
 // pass 2: copy the kept rows (already L2-resident from pass 1) to rows base, base + 1, ...
 __device__ __forceinline__ void export_copy(int64_t slot0, unsigned long long keepm, int64_t base, int x, int y,
-                                            const uint64_t *ug, int W, int32_t *xy, uint64_t *bits, int64_t cap,
-                                            int wid = 0, int nw = 1) {
+                                            const uint64_t *ug, int W, int32_t *xy, uint64_t *bits, int64_t cap) {
     const int lane = threadIdx.x & 63;
-    if (wid == 0 && ((keepm >> lane) & 1ull)) {      // the lane owning the slot writes its (x, y)
+    if ((keepm >> lane) & 1ull) {      // the lane owning the slot writes its (x, y)
         const int64_t r = base + __popcll(keepm & ((1ull << lane) - 1ull));
         if (r < cap) {
             xy[2 * r] = x;
             xy[2 * r + 1] = y;
         }
     }
-    int gi = 0;
-    for (unsigned long long mm = keepm; mm; ++gi) {
+    for (unsigned long long mm = keepm; mm;) {
         int ks[EXPORT_GROUP];
         int cnt = 0;
 #pragma unroll
@@ -285,7 +280,6 @@ __device__ __forceinline__ void export_copy(int64_t slot0, unsigned long long ke
             ks[g] = mm ? __ffsll((long long)mm) - 1 : 0;
             if (mm) { mm &= mm - 1; ++cnt; }
         }
-        if (gi % nw != wid) continue;
         for (int w = lane; w < W; w += 64) {
             uint64_t v[EXPORT_GROUP];
 #pragma unroll
