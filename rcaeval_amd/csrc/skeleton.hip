@@ -67,6 +67,9 @@ constexpr int MODE_EXACT = 2;
 #define PCG_TG_SGPR 0x18 // T-group sweep, depths whose bit (1 << d) is set: per-y bookkeeping as wave
                          // lane masks (SALU) instead of per-lane bits
 #endif
+#ifndef PCG_TG_SGPR_WIDE
+#define PCG_TG_SGPR_WIDE PCG_TG_SGPR   // the same for the wide (128-bit mask) class
+#endif
 #ifndef PCG_TG_SPLIT
 #define PCG_TG_SPLIT 0   // lane-mask sweep: split the y range around a shared candidate window (spills: slower)
 #endif
@@ -1435,7 +1438,7 @@ __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_
 #pragma unroll
         for (int jj = 0; jj < TG; ++jj) okm |= (unsigned)okc[jj] << jj;
         const unsigned vmask = (1u << (cend - cbase)) - 1u;
-        constexpr bool SG = (PCG_TG_SGPR >> DM) & 1;
+        constexpr bool SG = ((WIDE ? PCG_TG_SGPR_WIDE : PCG_TG_SGPR) >> DM) & 1;
         // lane-mask form of the sweep's bookkeeping. Tests per task are counted in closed form:
         // every valid candidate meets every y outside T except itself, minus the dedup skips of
         // "own" y (counted in the rare path below). okv[jj]: lanes whose candidate jj is valid
