@@ -100,6 +100,96 @@ __device__ inline int pcg_lu_inv01(double *A, int m, int *piv, double *B0, doubl
     return 0;
 }
 
+// pcg_lu_inv01 with the matrix in registers (M = d + 2 known at compile time): the same
+// operations in the same order (pivot search, row swap, scaling, elimination, dgetrs
+// substitutions), the dynamic pivot row selected instead of indexed — bitwise the same result.
+template <int M>
+__device__ inline int pcg_lu_inv01_reg(double (&A)[M][M], double *i00, double *i01, double *i11) {
+#pragma clang fp contract(off)
+    int info = 0;
+    int piv[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        int p = j;
+        double best = fabs(A[j][j]);
+#pragma unroll
+        for (int i = j + 1; i < M; ++i) {
+            const double v = fabs(A[i][j]);
+            if (v > best) { best = v; p = i; }
+        }
+        piv[j] = p;
+        double rp[M];
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+            double t = A[j][k];
+#pragma unroll
+            for (int i = j + 1; i < M; ++i)
+                if (p == i) t = A[i][k];
+            rp[k] = t;
+        }
+        if (rp[j] != 0.0) {
+            if (p != j) {
+#pragma unroll
+                for (int k = 0; k < M; ++k) {
+#pragma unroll
+                    for (int i = j + 1; i < M; ++i)
+                        if (p == i) A[i][k] = A[j][k];
+                    A[j][k] = rp[k];
+                }
+            }
+            const double rcp = 1.0 / A[j][j];
+#pragma unroll
+            for (int i = j + 1; i < M; ++i) A[i][j] *= rcp;
+        } else if (!info) {
+            info = j + 1;
+        }
+#pragma unroll
+        for (int i = j + 1; i < M; ++i) {
+            const double l = A[i][j];
+#pragma unroll
+            for (int k = j + 1; k < M; ++k) A[i][k] -= l * A[j][k];
+        }
+    }
+    if (info) return 1;
+    double B0[M], B1[M];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        double B[M];
+#pragma unroll
+        for (int i = 0; i < M; ++i) B[i] = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+            const int p = piv[i];
+            if (p != i) {
+                double bp = B[i];
+#pragma unroll
+                for (int q = i + 1; q < M; ++q)
+                    if (p == q) bp = B[q];
+#pragma unroll
+                for (int q = i + 1; q < M; ++q)
+                    if (p == q) B[q] = B[i];
+                B[i] = bp;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < M; ++i)
+#pragma unroll
+            for (int k = 0; k < i; ++k) B[i] -= A[i][k] * B[k];
+#pragma unroll
+        for (int i = M - 1; i >= 0; --i) {
+#pragma unroll
+            for (int k = i + 1; k < M; ++k) B[i] -= A[i][k] * B[k];
+            B[i] /= A[i][i];
+        }
+#pragma unroll
+        for (int i = 0; i < M; ++i) (c ? B1 : B0)[i] = B[i];
+    }
+    *i00 = B0[0];
+    *i01 = B1[0];
+    *i11 = B1[1];
+    return 0;
+}
+
 // Binomial table: binom[c * PCG_BK + k] = C(c, k), saturated at UINT64_MAX.
 #define PCG_BK (PCG_MAX_LEVEL_DEPTH + 1)
 

@@ -363,7 +363,8 @@ __global__ __launch_bounds__(256) void k_level_close(uint8_t *rm, uint64_t *adj,
     }
 }
 
-// The level barrier's summary and the next depth's CSR in one launch. Blocks 0 .. ceil(n/4)-1:
+// The level barrier's summary and the next depth's CSR in one launch. Blocks 0 .. nfill-1
+// (nfill = ceil(n/4); 0 at init: depth 0 reads no CSR):
 // one wave per node x builds its ascending neighbour list from the adjacency row at offset
 // sum(deg[0..x)) (each wave sums the prefix itself, so no grid-wide scan is waited for) and, with
 // ug, clears the node's union rows. The last block: the CSR offsets (exclusive scan of deg), the
@@ -373,10 +374,9 @@ __global__ __launch_bounds__(256) void k_level_close(uint8_t *rm, uint64_t *adj,
 __global__ __launch_bounds__(256) void k_summary_fill(const int32_t *deg, int n, int W, const uint64_t *adj,
                                                       int32_t *off, int32_t *nbr, uint64_t *ug, DevCounters *ctr,
                                                       uint8_t *status, LevelSummary *out, int32_t *out_deg,
-                                                      unsigned long long seq) {
+                                                      unsigned long long seq, int nfill) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int nfill = (n + 3) / 4;
     if ((int)blockIdx.x < nfill) {
         const int x = blockIdx.x * 4 + (tid >> 6);
         if (x >= n) return;
@@ -1822,6 +1822,16 @@ __global__ __launch_bounds__(64) void k_level_deep(LevelArgs a, double *scratch,
 
 // ---------------------------------------------------------------------------------------
 // exact path over the deferred list (LU like numpy.linalg.inv; the reference p expression)
+template <int M>
+__device__ __forceinline__ int lu_from_lds(const double *A, double *i00, double *i01, double *i11) {
+    double R[M][M];
+#pragma unroll
+    for (int r = 0; r < M; ++r)
+#pragma unroll
+        for (int c = 0; c < M; ++c) R[r][c] = A[r * M + c];
+    return pcg_lu_inv01_reg<M>(R, i00, i01, i11);
+}
+
 // One wave per deferred test: the lanes gather the (d+2)^2 correlation entries in parallel
 // into the wave's LDS slot (a single lane's rolled gather would wait out one HBM latency per
 // entry), then lane 0 factors and decides.
@@ -1864,7 +1874,16 @@ __global__ __launch_bounds__(256) void k_exact(LevelArgs a) {
         if (lane != 0) continue;
         double i00, i01, i11, p = __builtin_nan("");
         int err = 0;
-        if (pcg_lu_inv01(A, m, piv, B0, B1, &i00, &i01, &i11)) {
+        int sing;
+        switch (m) {     // depths 0..4: the factorisation in registers; deeper: in the LDS slot
+        case 2: sing = lu_from_lds<2>(A, &i00, &i01, &i11); break;
+        case 3: sing = lu_from_lds<3>(A, &i00, &i01, &i11); break;
+        case 4: sing = lu_from_lds<4>(A, &i00, &i01, &i11); break;
+        case 5: sing = lu_from_lds<5>(A, &i00, &i01, &i11); break;
+        case 6: sing = lu_from_lds<6>(A, &i00, &i01, &i11); break;
+        default: sing = pcg_lu_inv01(A, m, piv, B0, B1, &i00, &i01, &i11);
+        }
+        if (sing) {
             err = 1;
         } else {
             const double prod = i00 * i11;
@@ -2084,18 +2103,20 @@ int graph_launch(pcg_handle *h) {
         PCG_HIP(h, hipStreamWaitEvent(h->stream, h->ev_xdone[t], 0));
         h->xpending[t] = false;
     }
+    // depth 0 (the complete graph) reads no neighbour lists: init builds only the summary
+    const int nfill = h->depth < 0 ? 0 : (n + 3) / 4;
     if (!pcg_ensure(h, h->off2[t], sizeof(int32_t) * (n + 1)) ||
-        !pcg_ensure(h, h->nbr2[t], sizeof(int32_t) * std::max<int64_t>(bound, 1)))
+        (nfill && !pcg_ensure(h, h->nbr2[t], sizeof(int32_t) * std::max<int64_t>(bound, 1))))
         return pcg_fail(h, PCG_ERR_OOM, "neighbour lists");
     uint64_t *ug = nullptr;
     if (h->depth >= 0 && h->ug2[t].p &&
         h->ug2[t].bytes >= sizeof(uint64_t) * (size_t)std::max<int64_t>(bound, 1) * W)
         ug = (uint64_t *)h->ug2[t].p;
     h->ug_clean2[t] = ug != nullptr;
-    hipLaunchKernelGGL(k_summary_fill, dim3((unsigned)((n + 3) / 4 + 1)), dim3(256), 0, h->stream,
+    hipLaunchKernelGGL(k_summary_fill, dim3((unsigned)(nfill + 1)), dim3(256), 0, h->stream,
                        (const int32_t *)h->deg.p, n, W, (const uint64_t *)h->adj.p, (int32_t *)h->off2[t].p,
                        (int32_t *)h->nbr2[t].p, ug, (DevCounters *)h->ctr.p, status, ds,
-                       reinterpret_cast<int32_t *>(ds + 1), seq);
+                       reinterpret_cast<int32_t *>(ds + 1), seq, nfill);
     h->cb = t;
     PCG_HIP(h, hipGetLastError());
     if (h->lev_on && h->lev_n < 2 * PCG_MAX_LEVELS) {   // depth boundary (skeleton_once), off the host's critical path
