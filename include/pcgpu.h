@@ -74,6 +74,7 @@ typedef struct {
     double kernel_ms[PCG_MAX_LEVELS];  /* time of the CI-test kernel alone per depth        */
     int32_t levels;                    /* depths run                                        */
     int32_t error;                     /* 0 or PCG_ERR_SINGULAR / PCG_ERR_DOMAIN            */
+    int64_t screened[PCG_MAX_LEVELS];  /* tests the fp32 sweep left to its fp64 screen      */
 } pcg_stats;
 
 typedef struct {                       /* one unique CI test (PCG_FLAG_RECORD / near-alpha) */
@@ -195,6 +196,10 @@ int pcg_level_merge(pcg_handle *h, const uint64_t *gathered_dev, int world);
  * narrow LDS-resident class, so the wide T-group kernel (64-bit masks -> 128-bit) and the
  * staged kernels can be checked on small graphs. Results are identical for any value.      */
 int pcg_set_narrow_degree(pcg_handle *h, int max_degree);
+/* Testing knob: 1 (default) runs the threshold-mode T-group sweep of depths 2..4 in packed
+ * fp32 with an a-priori error bound (tests it cannot make certain are evaluated in fp64:
+ * k_level_lds_f); 0 runs the all-fp64 sweep (k_level_lds_t). Results are identical.      */
+int pcg_set_screen_precision(pcg_handle *h, int fp32);
 /* Number of ranks the level work lists are split over (default 1). The per-depth
  * decomposition sizes its chunks so that each rank's slice still fills its GPU.          */
 int pcg_set_world_size(pcg_handle *h, int world);

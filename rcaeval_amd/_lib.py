@@ -50,6 +50,7 @@ class PcgStats(ctypes.Structure):
         ("kernel_ms", D * PCG_MAX_LEVELS),
         ("levels", I32),
         ("error", I32),
+        ("screened", I64 * PCG_MAX_LEVELS),
     ]
 
     def as_dict(self) -> dict:
@@ -66,6 +67,7 @@ class PcgStats(ctypes.Structure):
             "max_degree": list(self.max_degree[:L]),
             "level_ms": list(self.level_ms[:L]),
             "kernel_ms": list(self.kernel_ms[:L]),
+            "screened": list(self.screened[:L]),
         }
 
 
@@ -106,6 +108,7 @@ SIGNATURES = [
     ("pcg_level_merge", I32, [P, P, ctypes.c_int]),
     ("pcg_set_world_size", I32, [P, ctypes.c_int]),
     ("pcg_set_narrow_degree", I32, [P, ctypes.c_int]),
+    ("pcg_set_screen_precision", I32, [P, ctypes.c_int]),
     ("pcg_comm_unique_id", I32, [P, I64]),
     ("pcg_comm_init", I32, [P, P, ctypes.c_int, ctypes.c_int]),
     ("pcg_comm_destroy", I32, [P]),

@@ -83,7 +83,7 @@ extern "C" int pcg_destroy(pcg_handle *h) {
     if (h->xs) hipStreamSynchronize(h->xs);
     DevBuf *bufs[] = {&h->adj, &h->deg, &h->off2[0], &h->off2[1], &h->nbr2[0], &h->nbr2[1], &h->rm, &h->ug2[0],
                       &h->ug2[1], &h->exp_ctr, &h->cpre, &h->binom, &h->ctr,
-                      &h->deferred, &h->records, &h->nearbuf, &h->exportbuf, &h->export_xy, &h->diag,
+                      &h->deferred, &h->screenq, &h->records, &h->nearbuf, &h->exportbuf, &h->export_xy, &h->diag,
                       &h->colmean, &h->pr_scratch, &h->batch_scratch, &h->chisq_scratch};
     for (DevBuf *b : bufs)
         if (b->p) hipFree(b->p);

@@ -152,12 +152,13 @@ int sharded_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t
 int reduce_stats(pcg_handle *h) {
     const int L = h->st.levels;
     if (L <= 0) return PCG_OK;
-    std::vector<int64_t> v((size_t)4 * L);
+    std::vector<int64_t> v((size_t)5 * L);
     for (int d = 0; d < L; ++d) {
         v[d] = h->st.tests[d];
         v[L + d] = h->st.indep[d];
         v[2 * L + d] = h->st.exact[d];
         v[3 * L + d] = h->st.near_alpha[d];
+        v[4 * L + d] = h->st.screened[d];
     }
     if (!pcg_ensure(h, h->comm_small, sizeof(int64_t) * v.size())) return pcg_fail(h, PCG_ERR_OOM, "stats");
     PCG_HIP(h, hipMemcpyAsync(h->comm_small.p, v.data(), sizeof(int64_t) * v.size(), hipMemcpyHostToDevice,
@@ -172,6 +173,7 @@ int reduce_stats(pcg_handle *h) {
         h->st.indep[d] = v[L + d];
         h->st.exact[d] = v[2 * L + d];
         h->st.near_alpha[d] = v[3 * L + d];
+        h->st.screened[d] = v[4 * L + d];
     }
     return PCG_OK;
 }

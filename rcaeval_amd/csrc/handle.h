@@ -31,6 +31,7 @@ struct DevCounters {
     unsigned long long near_alpha; // |p - alpha| < 1e-9 (may exceed capacity)
     unsigned long long exported;   // sepset rows exported this level
     unsigned long long error;      // PCG_ERR_* bits (1 singular, 2 domain)
+    unsigned long long screened;   // tests the fp32 sweep handed to the fp64 screen list (may exceed capacity)
 };
 
 // host-mapped per-level summary (k_level_summary); n int32 degrees follow the struct
@@ -38,6 +39,11 @@ struct LevelSummary {
     DevCounters ctr;
     uint8_t status[8];
     unsigned long long seq;        // written last, after a system-scope fence
+};
+
+struct ScreenEntry {               // one test the fp32 sweep could not decide (k_screen: fp64)
+    int32_t x, y;
+    int32_t s[4];                  // conditioning set (global ids, ascending), depths 2..4
 };
 
 struct DeferredEntry {             // one test routed to the exact (LU) path
@@ -62,6 +68,7 @@ struct pcg_handle {
     int lev_n = 0;
 
     // scratch
+    DevBuf screenq;                 // fp32 sweep -> fp64 screen list (k_level_lds_f -> k_screen)
     DevBuf adj, deg, rm, cpre, binom, ctr, deferred, records, nearbuf, exportbuf, export_xy, diag, colmean,
         pr_scratch, batch_scratch, chisq_scratch;
     // CSR (offsets, neighbour lists) and sepset union rows, double-buffered: depth d's sepset
@@ -78,7 +85,7 @@ struct pcg_handle {
     std::vector<uint64_t> binom_h;   // host copy of the binomial table
     uint8_t *rm_ext = nullptr;       // caller-owned removal-flag buffer (multi-GPU)
     int64_t rm_ext_bytes = 0;
-    int64_t rec_cap = 0, def_cap = 1 << 20, near_cap = 1 << 16;
+    int64_t rec_cap = 0, def_cap = 1 << 20, near_cap = 1 << 16, scr_cap = 1 << 20;
     int64_t rec_mod = 0, rec_res = 0;  // pcg_set_record_sample (0/1 = record every test)
     int64_t export_cap = 0;          // rows
     int64_t export_rows = 0;         // rows exported so far (host mirror)
@@ -102,6 +109,7 @@ struct pcg_handle {
     int spl_w = 1;                   // tasks per lane of the wide class
     int narrow_deg = 64;             // pcg_set_narrow_degree (testing: route more nodes to the wide class)
     bool tgroup = false;             // small class runs k_level_lds_t this depth
+    bool screen32 = true;            // pcg_set_screen_precision: fp32-screened T-group sweep (k_level_lds_f)
     int32_t maxdeg = 0;
     int64_t sumdeg = 0;
     LevelSummary *summary = nullptr;    // host-mapped, coherent (graph_launch / level_wait)

@@ -103,12 +103,15 @@ struct LevelArgs {
     DevCounters *ctr;
     DeferredEntry *deferred;
     int64_t def_cap;
+    ScreenEntry *screen;         // fp32 sweep -> fp64 screen list
+    int64_t scr_cap;
     pcg_record *records;
     int64_t rec_cap;
     pcg_record *nearl;
     int64_t near_cap;
     double lo2, hi2;             // decision band on r^2
     double tau;                  // conditioning guard (see decide)
+    double s_amgm, inv_s;        // fp32 screen: AM-GM scale ~ |c_xy| at the threshold (k_level_lds_f)
     double alpha, sqrt_dof;
     int dof_negative;
     int record;
@@ -160,6 +163,15 @@ __device__ __forceinline__ void push_deferred(const LevelArgs &a, int x, int y, 
         DeferredEntry &e = a.deferred[slot];
         e.x = x; e.y = y;
         for (int i = 0; i < PCG_MAX_DEPTH; ++i) e.s[i] = i < d ? S[i] : -1;
+    }
+}
+
+__device__ __forceinline__ void push_screen(const LevelArgs &a, int x, int y, const int *S, int d) {
+    const unsigned long long slot = atomicAdd(&a.ctr->screened, 1ull);
+    if ((int64_t)slot < a.scr_cap) {
+        ScreenEntry &e = a.screen[slot];
+        e.x = x; e.y = y;
+        for (int i = 0; i < 4; ++i) e.s[i] = i < d ? S[i] : -1;
     }
 }
 
@@ -1734,6 +1746,559 @@ __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_
 }
 
 // ---------------------------------------------------------------------------------------
+// fp32-screened T-group sweep (threshold mode; the default form of k_level_lds_t).
+//
+// The block stages A~ = fp32(C) restricted to adj(x) (half the LDS of the fp64 form). Per
+// lane task the setup (L_T, L_T^-1, u_T, l_c, 1/lambda_c, u_c, c_xx) runs in fp64 on A~ and
+// is rounded to fp32 once; the y sweep runs in packed fp32 (v_pk_fma_f32: two candidates per
+// instruction). A test is decided "dependent" in fp32 only when that is certain for the
+// fp64 C: with nu_c = ||L_S^-1||_F (S = T + {c}),
+//     E_c = KE * u32 * (1 + nu_c)^2,   u32 = 2^-24,
+// bounds |c^ - c| for each of c_xx, c_yy, c_xy (the sweep's rounding plus the input rounding
+// C -> A~ propagated through the Schur complement, whose regression weights are bounded by
+// nu_c; tools/f32_screen_study.py measures max|err| / E_c ~ 2e-3 on config 5 with KE = 64).
+// Certain dependence needs (|c_xy^| - E)^2 > hi2 (c_xx^ + E)(c_yy^ + E) and the fp64 paths'
+// conditioning guard c_xx c_yy - c_xy^2 > tau / g on the true values; with 2E|c_xy| <=
+// E (c_xy^2 / s + s) (s = a.s_amgm ~ |c_xy| at the threshold) both become linear in c_yy^:
+//     alpha c_yy^ + beta  <  c_xy^2  <  gamma c_yy^ - kappa
+// (per-candidate constants, every rounding of the fp32 evaluation folded in as a margin),
+// evaluated as one compare |c_xy^2 - k1 - m c_yy^| < hh c_yy^ - k2. Every other test (the
+// independent ones, the band around the threshold, unusable candidates: 6e-5 of depth 4's
+// tests on config 5) takes the rare path, which evaluates it in fp64 from the C in HBM and
+// decides it like the fp64 kernels (band -> exact path). Decisions are therefore the fp64
+// kernels' decisions; only where the fp32 sweep is certain does it decide.
+typedef float f2v __attribute__((ext_vector_type(2)));
+constexpr double F32_U = 5.9604644775390625e-08;   // 2^-24
+#ifndef PCG_F32_KE
+#define PCG_F32_KE 64.0
+#endif
+#ifndef PCG_TG_F32
+#define PCG_TG_F32 0x1c   // depths (bit 1 << d) whose T-group sweep is fp32-screened by default
+#endif
+#ifndef PCG_MBF2
+#define PCG_MBF2 4
+#endif
+#ifndef PCG_MBF3
+#define PCG_MBF3 4
+#endif
+#ifndef PCG_MBF4
+#define PCG_MBF4 4
+#endif
+__host__ __device__ constexpr int tgf_minblocks(int DM) { return DM == 2 ? PCG_MBF2 : (DM == 3 ? PCG_MBF3 : PCG_MBF4); }
+
+// (x, y | S) in fp64 from the C in HBM (Cholesky of C_SS, the fp64 kernels' guard and band):
+// 0 dependent, 1 independent, 2 exact path
+template <int DM>
+__device__ int eval_test_global(const LevelArgs &a, int x, int y, const int *Sg) {
+    double L[DM][DM], rinv[DM], u[DM], v[DM];
+    double gmin = 1.0;
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < DM; ++j) {
+        double s = a.diag[Sg[j]];
+#pragma unroll
+        for (int q = 0; q < j; ++q) s -= L[j][q] * L[j][q];
+        ok = ok && (s > 0.0);
+        gmin = fmin(gmin, s);
+        L[j][j] = sqrt(s);
+        rinv[j] = 1.0 / L[j][j];
+#pragma unroll
+        for (int i = j + 1; i < DM; ++i) {
+            double t = a.C[(int64_t)Sg[i] * a.ldc + Sg[j]];
+#pragma unroll
+            for (int q = 0; q < j; ++q) t -= L[i][q] * L[j][q];
+            L[i][j] = t * rinv[j];
+        }
+    }
+    double uu = 0.0, vv = 0.0, uv = 0.0;
+#pragma unroll
+    for (int i = 0; i < DM; ++i) {
+        double tu = a.C[(int64_t)Sg[i] * a.ldc + x], tv = a.C[(int64_t)Sg[i] * a.ldc + y];
+#pragma unroll
+        for (int q = 0; q < i; ++q) {
+            tu -= L[i][q] * u[q];
+            tv -= L[i][q] * v[q];
+        }
+        u[i] = tu * rinv[i];
+        v[i] = tv * rinv[i];
+        uu += u[i] * u[i];
+        vv += v[i] * v[i];
+        uv += u[i] * v[i];
+    }
+    if (!ok) return 2;
+    return decide<MODE_DECIDE>(a, a.C[(int64_t)x * a.ldc + y] - uv, a.diag[x] - uu, a.diag[y] - vv, a.tau / gmin,
+                               nullptr);
+}
+
+template <int DM, bool WIDE>
+__global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds_f(LevelArgs a) {
+    using Mask = LMask<WIDE>;
+    constexpr int DT = DM - 1;
+    constexpr int TG = tg_of_depth(DM);
+    constexpr int NP = TG / 2;                                    // candidate pairs
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x;
+    const int bs = blockDim.x;
+    const int64_t chunk = a.chunk_lo + blockIdx.x;
+    int lo = 0, hi = a.n;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (a.cpre[mid] <= chunk) lo = mid; else hi = mid;
+    }
+    const int x = lo;
+    const int D = a.deg[x];
+    const int32_t *nxg = a.nbr + a.off[x];
+
+    const int DS = (D + 3) & ~3;                                  // padded length / row stride
+    Mask *lmask = reinterpret_cast<Mask *>(smem);                 // DS
+    Mask *uself = lmask + DS;                                     // DS
+    Mask *uprop = uself + DS;                                     // DS
+    float *M = reinterpret_cast<float *>(uprop + DS);             // D * DS (columns >= D zero)
+    float *Mx = M + D * DS;                                       // DS
+    float *Md = Mx + DS;                                          // DS
+    int32_t *nxs = reinterpret_cast<int32_t *>(Md + DS);         // DS
+    int *s_tx = nxs + DS;                                         // 1
+    int *s_np = s_tx + 1;                                         // 1
+    unsigned *btab = reinterpret_cast<unsigned *>(smem + a.lds_btab_off);   // C(c, i), c <= D, i <= DM
+    unsigned *ppre = btab + (D + 1) * (DM + 1);                   // task prefix per (g, t0) pair
+    unsigned short *pinfo = reinterpret_cast<unsigned short *>(ppre + tg_pairs(D, DM) + 1);  // g << 8 | t0
+
+    for (int i = tid; i < D; i += bs) nxs[i] = nxg[i];
+    for (int e = tid; e < (D + 1) * (DM + 1); e += bs) {
+        const int c = e / (DM + 1), i = e - c * (DM + 1);
+        btab[e] = (unsigned)pcg_binom(a.binom, c, i);
+    }
+    __syncthreads();
+    for (int e = tid; e < D * DS; e += bs) {
+        const int t = e / DS, k = e - t * DS;
+        M[e] = k < D ? (float)a.C[(int64_t)nxs[t] * a.ldc + nxs[k]] : 0.0f;
+    }
+    for (int t = tid >> 6; t < D; t += bs >> 6) {
+        const uint64_t *ar = a.adj + (int64_t)nxs[t] * a.W;
+        Mask m = 0;
+        for (int k0 = 0; k0 < D; k0 += 64) {
+            const int k = k0 + (tid & 63);
+            const bool bit = k < D && ((ar[nxs[k] >> 6] >> (nxs[k] & 63)) & 1ull);
+            m |= (Mask)__ballot(bit) << k0;
+        }
+        if ((tid & 63) == 0) lmask[t] = m;
+    }
+    for (int t = tid; t < D; t += bs) {
+        const int yg = nxs[t];
+        Mx[t] = (float)a.C[(int64_t)x * a.ldc + yg];
+        Md[t] = (float)a.diag[yg];
+        uself[t] = 0;
+        uprop[t] = 0;
+    }
+    const int ng = (D - DM) / TG + 1;
+    if (tid == 0) {
+        int c = 0;
+        while (c < D && nxs[c] < x) ++c;
+        *s_tx = c;
+        unsigned acc = 0;
+        int q = 0;
+        for (int g = 0; g < ng; ++g)
+            for (int t0 = g * TG + 1; t0 <= D - DT; ++t0) {
+                ppre[q] = acc;
+                pinfo[q] = (unsigned short)((g << 8) | t0);
+                acc += btab[(D - 1 - t0) * (DM + 1) + DT - 1];
+                ++q;
+            }
+        ppre[q] = acc;
+        *s_np = q;
+    }
+    __syncthreads();
+    const int tx = *s_tx;
+    const int np = *s_np;
+    const double Cxx = (double)(float)a.diag[x];                  // A~_xx
+    const uint64_t ntask = ppre[np];
+    const uint64_t r0 = (uint64_t)(chunk - a.cpre[x]) * (uint64_t)bs * (uint64_t)a.spl;
+    const uint64_t r1 = min(ntask, r0 + (uint64_t)bs * (uint64_t)a.spl);
+    unsigned long long tests = 0, indep = 0;
+    unsigned tcount = 0;
+    const unsigned long long lanebit = 1ull << (tid & 63);
+    const float inv_sf = (float)a.inv_s;                          // rounding covered by the check's margins
+    const float lo2f = (float)(a.lo2 * (1.0 - 4.0 * F32_U));     // <= lo2
+
+    for (uint64_t task = r0 + tid; task < r1; task += bs) {
+        int lq = 0, hq = np;
+        while (hq - lq > 1) {
+            const int mid = (lq + hq) >> 1;
+            if (ppre[mid] <= task) lq = mid; else hq = mid;
+        }
+        const int info = pinfo[lq];
+        const int cbase = (info >> 8) * TG;
+        int T[DT];
+        T[0] = info & 255;
+        {
+            unsigned rr = (unsigned)(task - ppre[lq]);
+            int hi_ = D - T[0] - 1;
+#pragma unroll
+            for (int ii = DT - 2; ii >= 0; --ii) {
+                int lo_ = ii, up = hi_ - 1;
+                while (lo_ < up) {
+                    const int mid = (lo_ + up + 1) >> 1;
+                    if (btab[mid * (DM + 1) + ii + 1] <= rr) lo_ = mid; else up = mid - 1;
+                }
+                T[ii + 1] = lo_;
+                rr -= btab[lo_ * (DM + 1) + ii + 1];
+                hi_ = lo_;
+            }
+#pragma unroll
+            for (int ii = 1; ii < DT; ++ii) T[ii] += T[0] + 1;
+        }
+        const int nval = min(T[0] - cbase, TG);
+        int nmax_ = 1;
+#pragma unroll
+        for (int k = 2; k <= TG; ++k) nmax_ += (__ballot(nval >= k) != 0);
+        const int nmax = __builtin_amdgcn_readfirstlane(nmax_);
+        Mask Tmask = 0;
+#pragma unroll
+        for (int i = 0; i < DT; ++i) Tmask |= (Mask)1 << T[i];
+        // T setup in fp64 on A~
+        double L[DT][DT], Li[DT][DT], uT[DT];
+        bool okT = true;
+        double gT = 1.0;
+#pragma unroll
+        for (int j = 0; j < DT; ++j) {
+            double s = M[T[j] * DS + T[j]];
+#pragma unroll
+            for (int q = 0; q < j; ++q) s -= L[j][q] * L[j][q];
+            okT = okT && (s > 0.0);
+            gT = fmin(gT, s);
+            L[j][j] = sqrt(s);
+            const double r = 1.0 / L[j][j];
+#pragma unroll
+            for (int i = j + 1; i < DT; ++i) {
+                double t = M[T[i] * DS + T[j]];
+#pragma unroll
+                for (int q = 0; q < j; ++q) t -= L[i][q] * L[j][q];
+                L[i][j] = t * r;
+            }
+            Li[j][j] = r;
+        }
+#pragma unroll
+        for (int i = 1; i < DT; ++i)
+#pragma unroll
+            for (int j = 0; j < i; ++j) {
+                double t = 0.0;
+#pragma unroll
+                for (int q = j; q < i; ++q) t += L[i][q] * Li[q][j];
+                Li[i][j] = -t * Li[i][i];
+            }
+        double uuT = 0.0, liF = 0.0;
+#pragma unroll
+        for (int i = 0; i < DT; ++i) {
+            double t = 0.0;
+#pragma unroll
+            for (int j = 0; j <= i; ++j) {
+                t += Li[i][j] * (double)Mx[T[j]];
+                liF += Li[i][j] * Li[i][j];
+            }
+            uT[i] = t;
+            uuT += t * t;
+        }
+        float Lif[DT][DT], uTf[DT];
+#pragma unroll
+        for (int i = 0; i < DT; ++i) {
+            uTf[i] = (float)uT[i];
+#pragma unroll
+            for (int j = 0; j <= i; ++j) Lif[i][j] = (float)Li[i][j];
+        }
+        // candidate constants, two candidates per packed register
+        f2v lcp[NP][DT], rlp[NP], ucp[NP], mp[NP], hhp[NP], k1p[NP], k2p[NP];
+        bool okc[TG];
+#pragma unroll
+        for (int jj = 0; jj < TG; ++jj) {
+            const int q = jj >> 1, h = jj & 1;
+            float lcf[DT];
+#pragma unroll
+            for (int i = 0; i < DT; ++i) lcf[i] = 0.0f;
+            float rlf = 0.0f, ucf = 0.0f, mf = 0.0f, hhf = -1.0f, k1f = 0.0f, k2f = 1.0f;   // never "dependent"
+            bool ok = false;
+            if (jj < nmax) {                          // wave-uniform
+                const int c = cbase + jj;
+                const bool valid = c < T[0];
+                const int cc = valid ? c : 0;
+                double lc[DT], ll = 0.0;
+#pragma unroll
+                for (int i = 0; i < DT; ++i) {
+                    double t = 0.0;
+#pragma unroll
+                    for (int j = 0; j <= i; ++j) t += Li[i][j] * (double)M[T[j] * DS + cc];
+                    lc[i] = t;
+                    ll += t * t;
+                }
+                const double lam2 = (double)M[cc * DS + cc] - ll;
+                const double r = 1.0 / sqrt(lam2);
+                double lu = 0.0;
+#pragma unroll
+                for (int i = 0; i < DT; ++i) lu += lc[i] * uT[i];
+                const double u = ((double)Mx[cc] - lu) * r;
+                const double cxx = Cxx - uuT - u * u;
+                // nu^2 = ||L_S^-1||_F^2 = ||Li||_F^2 + (|l_c^T Li|^2 + 1) / lambda^2
+                double ww = 0.0;
+#pragma unroll
+                for (int j = 0; j < DT; ++j) {
+                    double w = 0.0;
+#pragma unroll
+                    for (int i = j; i < DT; ++i) w += lc[i] * Li[i][j];
+                    ww += w * w;
+                }
+                const double nu = sqrt(liF + (ww + 1.0) * r * r);
+                const double E = PCG_F32_KE * F32_U * (1.0 + nu) * (1.0 + nu);
+                const double te = E * a.inv_s;                       // E / s
+                const double g = fmin(gT, lam2) - E;                  // smallest pivot^2 of C_SS, lower bound
+                ok = valid && okT && (lam2 > 0.0) && (te <= 0.5) && (cxx - E > 0.0) && (g > 0.0);
+                if (ok) {
+                    const double s = a.s_amgm, u8 = 8.0 * F32_U;
+                    const double kg = a.tau / g;
+                    const double hx = a.hi2 * (cxx + E);
+                    const double al = hx * (1.0 + 2.0 * te) * (1.0 + u8);
+                    const double be = (hx * E + E * s) * (1.0 + 2.0 * te) * (1.0 + u8);
+                    const double ga = (cxx - E) * (1.0 - te) * (1.0 - u8);
+                    const double ka = ((cxx - E) * E + kg + E * s + E * E) * (1.0 + u8);
+                    ok = ga > al;
+                    mf = (float)(0.5 * (al + ga));
+                    hhf = (float)(0.5 * (ga - al) - 2.0 * u8 * ga);
+                    k1f = (float)(0.5 * (be - ka));
+                    k2f = (float)(0.5 * (be + ka) * (1.0 + u8));
+                    if (!ok) { mf = 0.0f; hhf = -1.0f; k1f = 0.0f; k2f = 1.0f; }
+                }
+#pragma unroll
+                for (int i = 0; i < DT; ++i) lcf[i] = (float)lc[i];
+                rlf = (float)r;
+                ucf = (float)u;
+            }
+#pragma unroll
+            for (int i = 0; i < DT; ++i) lcp[q][i][h] = lcf[i];
+            rlp[q][h] = rlf;
+            ucp[q][h] = ucf;
+            mp[q][h] = mf;
+            hhp[q][h] = hhf;
+            k1p[q][h] = k1f;
+            k2p[q][h] = k2f;
+            okc[jj] = ok;
+        }
+        const int cend = min(T[0], cbase + TG);
+        unsigned okm = 0;
+#pragma unroll
+        for (int jj = 0; jj < TG; ++jj) okm |= (unsigned)okc[jj] << jj;
+        const unsigned vmask = (1u << (cend - cbase)) - 1u;
+        unsigned long long okv[TG];
+        tcount += (unsigned)(nval * (D - DT - 1));
+#pragma unroll
+        for (int jj = 0; jj < TG; ++jj) okv[jj] = __builtin_amdgcn_ballot_w64(okc[jj]);
+        const unsigned long long notok = __builtin_amdgcn_ballot_w64((vmask & ~okm) != 0u);
+        const int cb0 = __builtin_amdgcn_readfirstlane(cbase);
+        const bool uni = __builtin_amdgcn_ballot_w64(cbase != cb0) == 0ull;
+
+        auto sweep = [&](auto nc_tag) {
+            constexpr int NC = decltype(nc_tag)::value;
+            constexpr int NQ = NC / 2;
+            auto ystep = [&](int t, auto ym_tag) {
+                constexpr int YM = decltype(ym_tag)::value;
+                const float *Mt = M + t * DS;
+                f2v sc[NQ];
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) sc[q] = *reinterpret_cast<const f2v *>(Mt + cbase + 2 * q);
+                float vT[DT], mT[DT];
+#pragma unroll
+                for (int j = 0; j < DT; ++j) mT[j] = Mt[T[j]];
+                float vv = 0.0f, uv = 0.0f;
+#pragma unroll
+                for (int i = 0; i < DT; ++i) {
+                    float v = 0.0f;
+#pragma unroll
+                    for (int j = 0; j <= i; ++j) v = fmaf(Lif[i][j], mT[j], v);
+                    vT[i] = v;
+                    vv = fmaf(v, v, vv);
+                    uv = fmaf(uTf[i], v, uv);
+                }
+                const float byy = Md[t] - vv;
+                const float bxy = Mx[t] - uv;
+#pragma unroll
+                for (int i = 0; i < DT; ++i) {
+                    const f2v vb = {vT[i], vT[i]};
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) sc[q] = __builtin_elementwise_fma(-lcp[q][i], vb, sc[q]);
+                }
+                const f2v byy2 = {byy, byy}, bxy2 = {bxy, bxy};
+                const int jdead = YM == 1 ? t - cb0 : -1;
+                unsigned long long bad = 0ull;
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const f2v vc = sc[q] * rlp[q];
+                    const f2v cyy = __builtin_elementwise_fma(-vc, vc, byy2);
+                    const f2v cxy = __builtin_elementwise_fma(-ucp[q], vc, bxy2);
+                    const f2v nm = __builtin_elementwise_fma(cxy, cxy, -k1p[q]);
+                    const f2v w = __builtin_elementwise_fma(-mp[q], cyy, nm);
+                    const f2v hh = __builtin_elementwise_fma(hhp[q], cyy, -k2p[q]);
+                    const unsigned long long keep0 = 2 * q == jdead ? 0ull : okv[2 * q];
+                    const unsigned long long keep1 = 2 * q + 1 == jdead ? 0ull : okv[2 * q + 1];
+                    bad |= keep0 & ~__builtin_amdgcn_ballot_w64(__builtin_fabsf(w[0]) < hh[0]);
+                    bad |= keep1 & ~__builtin_amdgcn_ballot_w64(__builtin_fabsf(w[1]) < hh[1]);
+                }
+                const Mask lm = lmask[t];
+                const unsigned long long inT = __builtin_amdgcn_ballot_w64((bool)((Tmask >> t) & 1u));
+                unsigned long long rarel = (bad | notok) & ~inT;
+                if (YM == 2) rarel |= __builtin_amdgcn_ballot_w64((unsigned)(t - cbase) < (unsigned)nval);
+                if (t < tx) rarel |= __builtin_amdgcn_ballot_w64((lm & Tmask) == Tmask) & ~inT;
+                if (!rarel) return;
+                if (!(rarel & lanebit)) return;
+                // rare path (this lane): live set and dedup skips as in k_level_lds_t; a live test
+                // the fp32 check does not make certain is evaluated in fp64 from HBM
+                const bool own = (t < tx) && ((lm & Tmask) == Tmask);
+                const unsigned tb = ((unsigned)(t - cbase) < (unsigned)TG) ? (1u << (t - cbase)) : 0u;
+                const unsigned skip = own ? (unsigned)(lm >> cbase) : 0u;
+                if ((Tmask >> t) & 1u) return;
+                const unsigned live = vmask & ~tb & ~skip;
+                tcount -= __popc(vmask & ~tb & skip);
+#pragma unroll
+                for (int jj = 0; jj < TG; ++jj) {
+                    if (!((live >> jj) & 1u)) continue;
+                    const int q = jj >> 1, h = jj & 1;
+                    const int c = cbase + jj;
+                    if (okc[jj]) {   // the sweep's check for this candidate, recomputed
+                        float s_ = Mt[c];
+#pragma unroll
+                        for (int i = 0; i < DT; ++i) s_ = fmaf(-lcp[q][i][h], vT[i], s_);
+                        const float vc = s_ * rlp[q][h];
+                        const float cyy = fmaf(-vc, vc, byy);
+                        const float cxy = fmaf(-ucp[q][h], vc, bxy);
+                        const float w = fmaf(-mp[q][h], cyy, fmaf(cxy, cxy, -k1p[q][h]));
+                        if (__builtin_fabsf(w) < fmaf(hhp[q][h], cyy, -k2p[q][h])) continue;
+                        // certain independence, with bounds recovered from the candidate's
+                        // constants: m + hh <= c_xx - E, (k1 + k2) / s >= E, k2 - k1 >= kappa >=
+                        // tau / g (see the setup); each fp32 rounding below is covered by a
+                        // (1 +- 8 u32) factor:
+                        //   (|c_xy^| + E)^2 < lo2 (c_xx^ - E)(c_yy^ - E)            (r^2 < lo2)
+                        //   (c_xx^ - E)(c_yy^ - E) - (|c_xy^| + E)^2 > tau / g       (the guard)
+                        constexpr float U8 = (float)(8.0 * F32_U);
+                        const float Alb = (mp[q][h] + hhp[q][h]) * (1.0f - U8);
+                        const float Eub = (k1p[q][h] + k2p[q][h]) * inv_sf * (1.0f + U8);
+                        const float kgub = (k2p[q][h] - k1p[q][h]) * (1.0f + U8);
+                        const float ay = (cyy - Eub) * (1.0f - U8);
+                        const float ax = (__builtin_fabsf(cxy) + Eub) * (1.0f + U8);
+                        if (ay > 0.0f && ax * ax * (1.0f + U8) < lo2f * Alb * ay &&
+                            fmaf(ax, ax, kgub) * (1.0f + U8) < Alb * ay) {
+                            const Mask Smask = Tmask | ((Mask)1 << c);
+                            ++indep;
+                            lmask_atomic_or<WIDE>(&uself[t], Smask);
+                            if (((lm & Smask) == Smask) && t >= tx) lmask_atomic_or<WIDE>(&uprop[t], Smask);
+                            continue;
+                        }
+                    }
+                    int sg[DM];
+                    sg[0] = nxs[c];
+#pragma unroll
+                    for (int i = 0; i < DT; ++i) sg[i + 1] = nxs[T[i]];
+                    push_screen(a, x, nxs[t], sg, DM);
+                }
+            };
+            using Y1 = std::integral_constant<int, 1>;
+            using Y2 = std::integral_constant<int, 2>;
+            if (uni) {
+                for (int t = 0; t < D; ++t) ystep(t, Y1{});
+            } else {
+                for (int t = 0; t < D; ++t) ystep(t, Y2{});
+            }
+        };
+        if constexpr (TG == 4) {
+            if (nmax > 2) sweep(std::integral_constant<int, 4>{});
+            else sweep(std::integral_constant<int, 2>{});
+        } else if constexpr (TG == 6) {
+            if (nmax > 4) sweep(std::integral_constant<int, 6>{});
+            else if (nmax > 2) sweep(std::integral_constant<int, 4>{});
+            else sweep(std::integral_constant<int, 2>{});
+        } else {
+            if (nmax > 6) sweep(std::integral_constant<int, 8>{});
+            else if (nmax > 4) sweep(std::integral_constant<int, 6>{});
+            else if (nmax > 2) sweep(std::integral_constant<int, 4>{});
+            else sweep(std::integral_constant<int, 2>{});
+        }
+        tests += tcount;
+        tcount = 0;
+    }
+    __syncthreads();
+    for (int t = tid; t < D; t += bs) {
+        const Mask us = uself[t], up = uprop[t];
+        if (!(us | up)) continue;
+        const int yg = nxs[t];
+        a.rm[(int64_t)x * a.n + yg] = 1;
+        a.rm[(int64_t)yg * a.n + x] = 1;
+        for (int side = 0; side < 2; ++side) {
+            const Mask bits = side ? up : us;
+            if (!bits) continue;
+            const int64_t slot = side ? (int64_t)a.off[yg] + find_in_sorted(a.nbr + a.off[yg], a.deg[yg], x)
+                                      : (int64_t)a.off[x] + t;
+            unsigned long long *row = reinterpret_cast<unsigned long long *>(a.ug + slot * a.W);
+            for (int half = 0; half < (WIDE ? 2 : 1); ++half) {
+                unsigned long long m = (unsigned long long)(bits >> (64 * half));
+                while (m) {
+                    const int b = 64 * half + __ffsll((long long)m) - 1;
+                    const int gid = nxs[b];
+                    atomicOr(&row[gid >> 6], 1ull << (gid & 63));
+                    m &= m - 1;
+                }
+            }
+        }
+    }
+    tests = wave_sum(tests);
+    indep = wave_sum(indep);
+    if ((tid & 63) == 0) {
+        if (tests) atomicAdd(&a.ctr->tests, tests);
+        if (indep) atomicAdd(&a.ctr->indep, indep);
+    }
+}
+
+// The fp64 screen of the tests the fp32 sweep handed over (one lane per test, after the level
+// kernels, before k_exact): decided like the fp64 kernels; independence writes the removal
+// flags and both sides' unions as k_exact does, the band goes on to the exact path.
+template <int DM>
+__global__ __launch_bounds__(256) void k_screen(LevelArgs a) {
+    const unsigned long long pushed = a.ctr->screened;
+    const int64_t count = (int64_t)min((unsigned long long)a.scr_cap, pushed);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (int64_t)pushed > a.scr_cap)
+        a.rm[(int64_t)a.n * a.n] = 1;      // overflow: every rank reruns (status byte 0)
+    unsigned long long nindep = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
+        const ScreenEntry e = a.screen[i];
+        const int x = e.x, y = e.y;
+        int sg[DM];
+#pragma unroll
+        for (int q = 0; q < DM; ++q) sg[q] = e.s[q];
+        const int dec = eval_test_global<DM>(a, x, y, sg);
+        if (dec == 2) {
+            push_deferred(a, x, y, sg, DM);
+        } else if (dec == 1) {
+            ++nindep;
+            a.rm[(int64_t)x * a.n + y] = 1;
+            a.rm[(int64_t)y * a.n + x] = 1;
+            bool in_y = true;
+#pragma unroll
+            for (int q = 0; q < DM; ++q)
+                in_y = in_y && ((a.adj[(int64_t)y * a.W + (sg[q] >> 6)] >> (sg[q] & 63)) & 1ull);
+            const int sx = a.off[x] + find_in_sorted(a.nbr + a.off[x], a.deg[x], y);
+#pragma unroll
+            for (int q = 0; q < DM; ++q)
+                atomicOr(reinterpret_cast<unsigned long long *>(&a.ug[(int64_t)sx * a.W + (sg[q] >> 6)]),
+                         1ull << (sg[q] & 63));
+            if (in_y && y > x) {
+                const int sy = a.off[y] + find_in_sorted(a.nbr + a.off[y], a.deg[y], x);
+#pragma unroll
+                for (int q = 0; q < DM; ++q)
+                    atomicOr(reinterpret_cast<unsigned long long *>(&a.ug[(int64_t)sy * a.W + (sg[q] >> 6)]),
+                             1ull << (sg[q] & 63));
+            }
+        }
+    }
+    nindep = wave_sum(nindep);
+    if ((threadIdx.x & 63) == 0 && nindep) atomicAdd(&a.ctr->indep, nindep);
+}
+
+// ---------------------------------------------------------------------------------------
 // depths > PCG_MAX_DEPTH (degenerate graphs, e.g. constant columns whose NaN correlations
 // never separate): one thread per (x, S rank), exact LU path per test with per-thread
 // scratch in global memory. Throughput is not the goal here; semantics are.
@@ -1979,6 +2544,8 @@ LevelArgs make_args(pcg_handle *h, int d, int mode_exact_all) {
     a.ctr = (DevCounters *)h->ctr.p;
     a.deferred = (DeferredEntry *)h->deferred.p;
     a.def_cap = h->def_cap;
+    a.screen = (ScreenEntry *)h->screenq.p;
+    a.scr_cap = h->scr_cap;
     a.records = (pcg_record *)h->records.p;
     a.rec_cap = h->rec_cap;
     a.nearl = (pcg_record *)h->nearbuf.p;
@@ -1991,6 +2558,8 @@ LevelArgs make_args(pcg_handle *h, int d, int mode_exact_all) {
         const double r2 = threshold_r2(h->alpha, (double)h->N, d);
         a.lo2 = r2 * (1.0 - 1e-6);
         a.hi2 = r2 * (1.0 + 1e-6);
+        a.s_amgm = 0.5 * std::sqrt(r2);
+        a.inv_s = 1.0 / a.s_amgm;
     } else {
         a.lo2 = -1.0;  // never decides: every test to the exact path
         a.hi2 = 1e300;
@@ -2042,6 +2611,16 @@ size_t lds_tgroup_bytes(int D, int DM, int mask_bytes = 8) {
     const size_t np = (size_t)tg_pairs(D, DM);
     return lds_small_core(D, mask_bytes) + (size_t)(D + 1) * (DM + 1) * 4 + (np + 1) * 4 + np * 2 + 16;
 }
+// k_level_lds_f (D padded to 4): three mask arrays, fp32 M, Mx, Md, nxs, two ints; then the
+// same binomial table and task prefix as k_level_lds_t
+size_t lds_f32_core(int D, int mask_bytes) {
+    return ((size_t)D * 3 * mask_bytes + (size_t)D * D * 4 + (size_t)D * 3 * 4 + 8 + 15) & ~(size_t)15;
+}
+size_t lds_tgroup_f_bytes(int D, int DM, int mask_bytes) {
+    const size_t np = (size_t)tg_pairs(D, DM);
+    return lds_f32_core(D, mask_bytes) + (size_t)(D + 1) * (DM + 1) * 4 + (np + 1) * 4 + np * 2 + 16;
+}
+bool use_screen32(const pcg_handle *h, int d) { return h->screen32 && ((PCG_TG_F32 >> d) & 1); }
 constexpr size_t LDS_MAX = 160 * 1024;   // gfx950 LDS per workgroup
 
 // lane tasks of k_level_lds_t for a node of degree D at depth d (see the kernel)
@@ -2205,6 +2784,7 @@ extern "C" int pcg_skeleton_init(pcg_handle *h, const double *C, int64_t n, int6
         !pcg_ensure(h, h->diag, sizeof(double) * n) || !pcg_ensure(h, h->rm, (size_t)n * n + PCG_RM_STATUS) ||
         !pcg_ensure(h, h->ctr, sizeof(DevCounters)) || !pcg_ensure(h, h->exp_ctr, sizeof(unsigned long long)) ||
         !pcg_ensure(h, h->deferred, sizeof(DeferredEntry) * h->def_cap) ||
+        !pcg_ensure(h, h->screenq, sizeof(ScreenEntry) * h->scr_cap) ||
         !pcg_ensure(h, h->nearbuf, sizeof(pcg_record) * h->near_cap) ||
         !pcg_ensure(h, h->records, sizeof(pcg_record) * std::max<int64_t>(h->rec_cap, 1)))
         return pcg_fail(h, PCG_ERR_OOM, "device allocation failed (n=%lld)", (long long)n);
@@ -2389,6 +2969,12 @@ extern "C" int pcg_set_narrow_degree(pcg_handle *h, int max_degree) {
     return PCG_OK;
 }
 
+extern "C" int pcg_set_screen_precision(pcg_handle *h, int fp32) {
+    if (!h) return PCG_ERR_INVALID;
+    h->screen32 = fp32 != 0;
+    return PCG_OK;
+}
+
 extern "C" int pcg_set_world_size(pcg_handle *h, int world) {
     if (!h || world < 1) return pcg_fail(h, PCG_ERR_INVALID, "pcg_set_world_size: world %d", world);
     h->world = world;
@@ -2508,7 +3094,14 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                     const int dl = h->tgroup ? (h->maxdeg_small + 3) & ~3 : h->maxdeg_small;
                     as.lds_btab_off = (int)lds_small_core(dl);
                     const size_t lds = h->tgroup ? lds_tgroup_bytes(dl, d) : lds_small_bytes(dl);
-                    if (h->tgroup) {
+                    if (h->tgroup && use_screen32(h, d)) {
+                        as.lds_btab_off = (int)lds_f32_core(dl, 8);
+                        const size_t ldsf = lds_tgroup_f_bytes(dl, d, 8);
+                        const dim3 grid((unsigned)(s_hi - s_lo)), block(256);
+                        if (d == 2) hipLaunchKernelGGL((k_level_lds_f<2, false>), grid, block, ldsf, h->stream, as);
+                        else if (d == 3) hipLaunchKernelGGL((k_level_lds_f<3, false>), grid, block, ldsf, h->stream, as);
+                        else hipLaunchKernelGGL((k_level_lds_f<4, false>), grid, block, ldsf, h->stream, as);
+                    } else if (h->tgroup) {
                         const dim3 grid((unsigned)(s_hi - s_lo)), block(256);
                         if (d == 2) hipLaunchKernelGGL((k_level_lds_t<2, false>), grid, block, lds, h->stream, as);
                         else if (d == 3) hipLaunchKernelGGL((k_level_lds_t<3, false>), grid, block, lds, h->stream, as);
@@ -2532,12 +3125,20 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                     aw.bs = 256;
                     aw.spl = h->spl_w;
                     const int dl = (h->maxdeg_wide + 3) & ~3;
-                    aw.lds_btab_off = (int)lds_small_core(dl, 16);
-                    const size_t lds = lds_tgroup_bytes(dl, d, 16);
                     const dim3 grid((unsigned)(w_hi - w_lo)), block(256);
-                    if (d == 2) hipLaunchKernelGGL((k_level_lds_t<2, true>), grid, block, lds, h->stream, aw);
-                    else if (d == 3) hipLaunchKernelGGL((k_level_lds_t<3, true>), grid, block, lds, h->stream, aw);
-                    else hipLaunchKernelGGL((k_level_lds_t<4, true>), grid, block, lds, h->stream, aw);
+                    if (use_screen32(h, d)) {
+                        aw.lds_btab_off = (int)lds_f32_core(dl, 16);
+                        const size_t lds = lds_tgroup_f_bytes(dl, d, 16);
+                        if (d == 2) hipLaunchKernelGGL((k_level_lds_f<2, true>), grid, block, lds, h->stream, aw);
+                        else if (d == 3) hipLaunchKernelGGL((k_level_lds_f<3, true>), grid, block, lds, h->stream, aw);
+                        else hipLaunchKernelGGL((k_level_lds_f<4, true>), grid, block, lds, h->stream, aw);
+                    } else {
+                        aw.lds_btab_off = (int)lds_small_core(dl, 16);
+                        const size_t lds = lds_tgroup_bytes(dl, d, 16);
+                        if (d == 2) hipLaunchKernelGGL((k_level_lds_t<2, true>), grid, block, lds, h->stream, aw);
+                        else if (d == 3) hipLaunchKernelGGL((k_level_lds_t<3, true>), grid, block, lds, h->stream, aw);
+                        else hipLaunchKernelGGL((k_level_lds_t<4, true>), grid, block, lds, h->stream, aw);
+                    }
                 }
                 if (l_hi > l_lo && d > PCG_MAX_DEPTH) {
                     LevelArgs al = a;
@@ -2579,6 +3180,11 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
         // exact path over the deferred list; the kernel reads the list length on the device
         // (no host round trip) and raises the overflow status byte if the list overflowed
         a = make_args(h, d, mode == MODE_EXACT);
+        if (h->tgroup && use_screen32(h, d)) {   // the fp32 sweep's undecided tests, in fp64
+            if (d == 2) hipLaunchKernelGGL(k_screen<2>, dim3(256), dim3(256), 0, h->stream, a);
+            else if (d == 3) hipLaunchKernelGGL(k_screen<3>, dim3(256), dim3(256), 0, h->stream, a);
+            else hipLaunchKernelGGL(k_screen<4>, dim3(256), dim3(256), 0, h->stream, a);
+        }
         const int m = d + 2;
         const int per = (m * m + 2 * m) * 8;      // one LDS slot per wave
         hipLaunchKernelGGL(k_exact, dim3(256), dim3(256), (size_t)per * 4, h->stream, a);
@@ -2651,6 +3257,7 @@ extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
     h->st.tests[d] = (int64_t)c.tests;
     h->st.indep[d] = (int64_t)c.indep;
     h->st.exact[d] = (int64_t)c.exact;
+    h->st.screened[d] = (int64_t)c.screened;
     h->st.near_alpha[d] = (int64_t)c.near_alpha;
     h->st.kernel_ms[d] = h->run_ms;
     if (status[3]) {   // checked first: the failed rank will not rerun, so nobody may
@@ -2661,6 +3268,7 @@ extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
         // some rank's exact-path (or record) list overflowed: the level is incomplete on every
         // rank. Enlarge and let the driver rerun the skeleton (pcg_skeleton does it itself).
         h->def_cap = std::max<int64_t>(h->def_cap * 4, (int64_t)c.deferred * 2);
+        if ((int64_t)c.screened > h->scr_cap) h->scr_cap = std::max<int64_t>(h->scr_cap * 4, (int64_t)c.screened * 2);
         if (h->flags & PCG_FLAG_RECORD) h->rec_cap = std::max<int64_t>(h->rec_cap * 4, (int64_t)c.records * 2);
         if (stats) *stats = h->st;
         return pcg_fail(h, PCG_ERR_OVERFLOW, "level %d: exact-path list overflowed; capacity raised to %lld, rerun",

@@ -198,7 +198,7 @@ def _allgather_rows(xy, bits, group=None):
 def _allreduce_stats(stats: dict, device, group=None) -> dict:
     import torch
     import torch.distributed as dist
-    keys = ("tests", "indep", "exact", "near_alpha")
+    keys = ("tests", "indep", "exact", "near_alpha", "screened")
     L = stats["levels"]
     t = torch.tensor([stats[k][i] for k in keys for i in range(L)], dtype=torch.int64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)

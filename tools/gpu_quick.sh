@@ -13,5 +13,6 @@ import json
 l = [x for x in open("gpurun_out/quick_bench.log") if x.startswith("{")]
 d = json.loads(l[-1])
 print("value %.3e  ms %.3f  kernel_ms %s  level_ms %s  corr %s" % (d["value"], d["ms_per_step"], d["kernel_ms_per_level"], d["level_ms"], d["corr_ms"][-1]))
+print("screened %s  exact %s  edges %s" % (d.get("screened"), d.get("exact_path"), d.get("edges_after")))
 PY
 exit $rc
