@@ -1773,7 +1773,10 @@ constexpr double F32_U = 5.9604644775390625e-08;   // 2^-24
 #define PCG_F32_KE 64.0
 #endif
 #ifndef PCG_TG_F32
-#define PCG_TG_F32 0x1c   // depths (bit 1 << d) whose T-group sweep is fp32-screened by default
+#define PCG_TG_F32 0x18   // depths (bit 1 << d) whose T-group sweep is fp32-screened by default
+#endif
+#ifndef PCG_TGF_SGPR
+#define PCG_TGF_SGPR 0x10 // k_level_lds_f depths (bit 1 << d) whose per-y bookkeeping is in wave lane masks
 #endif
 #ifndef PCG_MBF2
 #define PCG_MBF2 4
@@ -1785,6 +1788,18 @@ constexpr double F32_U = 5.9604644775390625e-08;   // 2^-24
 #define PCG_MBF4 4
 #endif
 __host__ __device__ constexpr int tgf_minblocks(int DM) { return DM == 2 ? PCG_MBF2 : (DM == 3 ? PCG_MBF3 : PCG_MBF4); }
+
+// 1/sqrt(x) and 1/x in fp64 from the fp32 hardware estimate plus one Newton step (relative
+// error ~1e-14 for normal fp32-range x; x <= 0 or out of fp32 range gives inf / NaN, which the
+// callers' checks reject)
+__device__ __forceinline__ double rsq_nr(double x) {
+    const double r0 = (double)__builtin_amdgcn_rsqf((float)x);
+    return r0 * fma(-0.5 * x * r0, r0, 1.5);
+}
+__device__ __forceinline__ double rcp_nr(double x) {
+    const double r0 = (double)__builtin_amdgcn_rcpf((float)x);
+    return r0 * fma(-x, r0, 2.0);
+}
 
 // (x, y | S) in fp64 from the C in HBM (Cholesky of C_SS, the fp64 kernels' guard and band):
 // 0 dependent, 1 independent, 2 exact path
@@ -1854,9 +1869,8 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
     Mask *uself = lmask + DS;                                     // DS
     Mask *uprop = uself + DS;                                     // DS
     float *M = reinterpret_cast<float *>(uprop + DS);             // D * DS (columns >= D zero)
-    float *Mx = M + D * DS;                                       // DS
-    float *Md = Mx + DS;                                          // DS
-    int32_t *nxs = reinterpret_cast<int32_t *>(Md + DS);         // DS
+    float *Mdx = M + D * DS;                                      // 2 DS: {A~_yy, A~_xy} per y
+    int32_t *nxs = reinterpret_cast<int32_t *>(Mdx + 2 * DS);    // DS
     int *s_tx = nxs + DS;                                         // 1
     int *s_np = s_tx + 1;                                         // 1
     unsigned *btab = reinterpret_cast<unsigned *>(smem + a.lds_btab_off);   // C(c, i), c <= D, i <= DM
@@ -1885,8 +1899,8 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
     }
     for (int t = tid; t < D; t += bs) {
         const int yg = nxs[t];
-        Mx[t] = (float)a.C[(int64_t)x * a.ldc + yg];
-        Md[t] = (float)a.diag[yg];
+        Mdx[2 * t] = (float)a.diag[yg];
+        Mdx[2 * t + 1] = (float)a.C[(int64_t)x * a.ldc + yg];
         uself[t] = 0;
         uprop[t] = 0;
     }
@@ -1955,7 +1969,8 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
         Mask Tmask = 0;
 #pragma unroll
         for (int i = 0; i < DT; ++i) Tmask |= (Mask)1 << T[i];
-        // T setup in fp64 on A~
+        // T setup in fp64 on A~ (reciprocal square roots: fp32 estimate + one Newton step,
+        // relative error ~1e-14, far inside the E bound)
         double L[DT][DT], Li[DT][DT], uT[DT];
         bool okT = true;
         double gT = 1.0;
@@ -1966,8 +1981,7 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
             for (int q = 0; q < j; ++q) s -= L[j][q] * L[j][q];
             okT = okT && (s > 0.0);
             gT = fmin(gT, s);
-            L[j][j] = sqrt(s);
-            const double r = 1.0 / L[j][j];
+            const double r = rsq_nr(s);
 #pragma unroll
             for (int i = j + 1; i < DT; ++i) {
                 double t = M[T[i] * DS + T[j]];
@@ -1992,12 +2006,13 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
             double t = 0.0;
 #pragma unroll
             for (int j = 0; j <= i; ++j) {
-                t += Li[i][j] * (double)Mx[T[j]];
+                t += Li[i][j] * (double)Mdx[2 * T[j] + 1];
                 liF += Li[i][j] * Li[i][j];
             }
             uT[i] = t;
             uuT += t * t;
         }
+        const double cx0 = Cxx - uuT;
         float Lif[DT][DT], uTf[DT];
 #pragma unroll
         for (int i = 0; i < DT; ++i) {
@@ -2020,7 +2035,7 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
                 const int c = cbase + jj;
                 const bool valid = c < T[0];
                 const int cc = valid ? c : 0;
-                double lc[DT], ll = 0.0;
+                double lc[DT], ll = 0.0, lu = 0.0;
 #pragma unroll
                 for (int i = 0; i < DT; ++i) {
                     double t = 0.0;
@@ -2028,39 +2043,33 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
                     for (int j = 0; j <= i; ++j) t += Li[i][j] * (double)M[T[j] * DS + cc];
                     lc[i] = t;
                     ll += t * t;
+                    lu += t * uT[i];
                 }
                 const double lam2 = (double)M[cc * DS + cc] - ll;
-                const double r = 1.0 / sqrt(lam2);
-                double lu = 0.0;
-#pragma unroll
-                for (int i = 0; i < DT; ++i) lu += lc[i] * uT[i];
-                const double u = ((double)Mx[cc] - lu) * r;
-                const double cxx = Cxx - uuT - u * u;
-                // nu^2 = ||L_S^-1||_F^2 = ||Li||_F^2 + (|l_c^T Li|^2 + 1) / lambda^2
-                double ww = 0.0;
-#pragma unroll
-                for (int j = 0; j < DT; ++j) {
-                    double w = 0.0;
-#pragma unroll
-                    for (int i = j; i < DT; ++i) w += lc[i] * Li[i][j];
-                    ww += w * w;
-                }
-                const double nu = sqrt(liF + (ww + 1.0) * r * r);
-                const double E = PCG_F32_KE * F32_U * (1.0 + nu) * (1.0 + nu);
-                const double te = E * a.inv_s;                       // E / s
+                const double r = rsq_nr(lam2);
+                const double u = ((double)Mdx[2 * cc + 1] - lu) * r;
+                const double cxx = cx0 - u * u;
+                // nu^2 = ||L_S^-1||_F^2 = ||Li||_F^2 + (|Li^T l_c|^2 + 1) / lambda^2
+                //     <= liF + (liF |l_c|^2 + 1) r^2;   E = KE u32 (1 + nu)^2 <= 2 KE u32 (1 + nu^2)
+                const double r2 = r * r;
+                const double E = (2.0 * PCG_F32_KE * F32_U) * (1.0 + fma(fma(liF, ll, 1.0), r2, liF));
+                const double te = E * a.inv_s;                        // E / s
                 const double g = fmin(gT, lam2) - E;                  // smallest pivot^2 of C_SS, lower bound
-                ok = valid && okT && (lam2 > 0.0) && (te <= 0.5) && (cxx - E > 0.0) && (g > 0.0);
+                const double cmE = cxx - E;
+                ok = valid && okT && (lam2 > 0.0) && (te <= 0.5) && (cmE > 0.0) && (g > 0.0);
                 if (ok) {
-                    const double s = a.s_amgm, u8 = 8.0 * F32_U;
-                    const double kg = a.tau / g;
+                    constexpr double u8 = 8.0 * F32_U;
+                    const double s = a.s_amgm;
+                    const double kg = a.tau * rcp_nr(g) * (1.0 + 1e-9);
                     const double hx = a.hi2 * (cxx + E);
-                    const double al = hx * (1.0 + 2.0 * te) * (1.0 + u8);
-                    const double be = (hx * E + E * s) * (1.0 + 2.0 * te) * (1.0 + u8);
-                    const double ga = (cxx - E) * (1.0 - te) * (1.0 - u8);
-                    const double ka = ((cxx - E) * E + kg + E * s + E * E) * (1.0 + u8);
+                    const double f1 = fma(2.0 * te, 1.0 + u8, 1.0 + u8);   // (1 + 2 te)(1 + u8)
+                    const double al = hx * f1;
+                    const double be = E * (hx + s) * f1;
+                    const double ga = cmE * (1.0 - te) * (1.0 - u8);
+                    const double ka = fma(E, cmE + s + E, kg) * (1.0 + u8);
                     ok = ga > al;
                     mf = (float)(0.5 * (al + ga));
-                    hhf = (float)(0.5 * (ga - al) - 2.0 * u8 * ga);
+                    hhf = (float)(fma(-2.0 * u8, ga, 0.5 * (ga - al)));
                     k1f = (float)(0.5 * (be - ka));
                     k2f = (float)(0.5 * (be + ka) * (1.0 + u8));
                     if (!ok) { mf = 0.0f; hhf = -1.0f; k1f = 0.0f; k2f = 1.0f; }
@@ -2085,17 +2094,67 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
 #pragma unroll
         for (int jj = 0; jj < TG; ++jj) okm |= (unsigned)okc[jj] << jj;
         const unsigned vmask = (1u << (cend - cbase)) - 1u;
+        // lane-mask sweep (closed-form test count) at the depths whose bit is set, else per-lane bits
+        constexpr bool SG = (PCG_TGF_SGPR >> DM) & 1;
         unsigned long long okv[TG];
-        tcount += (unsigned)(nval * (D - DT - 1));
+        if (SG) tcount += (unsigned)(nval * (D - DT - 1));
 #pragma unroll
         for (int jj = 0; jj < TG; ++jj) okv[jj] = __builtin_amdgcn_ballot_w64(okc[jj]);
         const unsigned long long notok = __builtin_amdgcn_ballot_w64((vmask & ~okm) != 0u);
         const int cb0 = __builtin_amdgcn_readfirstlane(cbase);
         const bool uni = __builtin_amdgcn_ballot_w64(cbase != cb0) == 0ull;
 
+        // a live test of candidate jj at y = t that the sweep's check did not make certain:
+        // certain independence in fp32 (recomputed) or the fp64 screen list
+        auto rare_cand = [&](int jj, int t, const float *Mt, const float *vT, float byy, float bxy, Mask lm) {
+            const int q = jj >> 1, h = jj & 1;
+            const int c = cbase + jj;
+            if (okc[jj]) {   // the sweep's check for this candidate, recomputed
+                float s_ = Mt[c];
+#pragma unroll
+                for (int i = 0; i < DT; ++i) s_ = fmaf(-lcp[q][i][h], vT[i], s_);
+                const float vc = s_ * rlp[q][h];
+                const float cyy = fmaf(-vc, vc, byy);
+                const float cxy = fmaf(-ucp[q][h], vc, bxy);
+                const float w = fmaf(-mp[q][h], cyy, fmaf(cxy, cxy, -k1p[q][h]));
+                if (__builtin_fabsf(w) < fmaf(hhp[q][h], cyy, -k2p[q][h])) return;
+                // certain independence, with bounds recovered from the candidate's constants:
+                // m + hh <= c_xx - E, (k1 + k2) / s >= E, k2 - k1 >= kappa >= tau / g (see the
+                // setup); each fp32 rounding below is covered by a (1 +- 8 u32) factor:
+                //   (|c_xy^| + E)^2 < lo2 (c_xx^ - E)(c_yy^ - E)            (r^2 < lo2)
+                //   (c_xx^ - E)(c_yy^ - E) - (|c_xy^| + E)^2 > tau / g       (the guard)
+                // (the opaque copies keep the compiler from hoisting these per-candidate values
+                // out of the y loop, where they would only be spilled)
+                constexpr float U8 = (float)(8.0 * F32_U);
+                float m_ = mp[q][h], hh_ = hhp[q][h], k1_ = k1p[q][h], k2_ = k2p[q][h];
+                asm volatile("" : "+v"(m_), "+v"(hh_), "+v"(k1_), "+v"(k2_));
+                const float Alb = (m_ + hh_) * (1.0f - U8);
+                const float Eub = (k1_ + k2_) * inv_sf * (1.0f + U8);
+                const float kgub = (k2_ - k1_) * (1.0f + U8);
+                const float ay = (cyy - Eub) * (1.0f - U8);
+                const float ax = (__builtin_fabsf(cxy) + Eub) * (1.0f + U8);
+                if (ay > 0.0f && ax * ax * (1.0f + U8) < lo2f * Alb * ay &&
+                    fmaf(ax, ax, kgub) * (1.0f + U8) < Alb * ay) {
+                    const Mask Smask = Tmask | ((Mask)1 << c);
+                    ++indep;
+                    lmask_atomic_or<WIDE>(&uself[t], Smask);
+                    if (((lm & Smask) == Smask) && t >= tx) lmask_atomic_or<WIDE>(&uprop[t], Smask);
+                    return;
+                }
+            }
+            int sg[DM];
+            sg[0] = nxs[c];
+#pragma unroll
+            for (int i = 0; i < DT; ++i) sg[i + 1] = nxs[T[i]];
+            push_screen(a, x, nxs[t], sg, DM);
+        };
         auto sweep = [&](auto nc_tag) {
             constexpr int NC = decltype(nc_tag)::value;
             constexpr int NQ = NC / 2;
+            // YM 1: one candidate window per wave (lane masks, y = candidate masked by index);
+            // 2: windows differ (lane masks, such lanes to the rare path); 3: per-lane live and
+            // dependence bits (the depths where dedup skips are common: a lane that owns y is
+            // not sent down the rare path just to count its skips)
             auto ystep = [&](int t, auto ym_tag) {
                 constexpr int YM = decltype(ym_tag)::value;
                 const float *Mt = M + t * DS;
@@ -2105,18 +2164,20 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
                 float vT[DT], mT[DT];
 #pragma unroll
                 for (int j = 0; j < DT; ++j) mT[j] = Mt[T[j]];
-                float vv = 0.0f, uv = 0.0f;
+                // (|v_T|^2, u_T.v_T) accumulated as one packed pair: vu[i] = {v_i, u_i}
+                f2v acc = {0.0f, 0.0f};
 #pragma unroll
                 for (int i = 0; i < DT; ++i) {
                     float v = 0.0f;
 #pragma unroll
                     for (int j = 0; j <= i; ++j) v = fmaf(Lif[i][j], mT[j], v);
                     vT[i] = v;
-                    vv = fmaf(v, v, vv);
-                    uv = fmaf(uTf[i], v, uv);
+                    const f2v vu = {v, uTf[i]}, vb = {v, v};
+                    acc = __builtin_elementwise_fma(vu, vb, acc);
                 }
-                const float byy = Md[t] - vv;
-                const float bxy = Mx[t] - uv;
+                const f2v b2 = *reinterpret_cast<const f2v *>(Mdx + 2 * t) - acc;   // {byy, bxy}
+                const float byy = b2[0];
+                const float bxy = b2[1];
 #pragma unroll
                 for (int i = 0; i < DT; ++i) {
                     const f2v vb = {vT[i], vT[i]};
@@ -2124,6 +2185,36 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
                     for (int q = 0; q < NQ; ++q) sc[q] = __builtin_elementwise_fma(-lcp[q][i], vb, sc[q]);
                 }
                 const f2v byy2 = {byy, byy}, bxy2 = {bxy, bxy};
+                const Mask lm = lmask[t];
+                if constexpr (YM == 3) {
+                    unsigned dp = 0;
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        const f2v vc = sc[q] * rlp[q];
+                        const f2v cyy = __builtin_elementwise_fma(-vc, vc, byy2);
+                        const f2v cxy = __builtin_elementwise_fma(-ucp[q], vc, bxy2);
+                        const f2v nm = __builtin_elementwise_fma(cxy, cxy, -k1p[q]);
+                        const f2v w = __builtin_elementwise_fma(-mp[q], cyy, nm);
+                        const f2v hh = __builtin_elementwise_fma(hhp[q], cyy, -k2p[q]);
+                        dp |= ((unsigned)(__builtin_fabsf(w[0]) < hh[0]) << (2 * q)) |
+                              ((unsigned)(__builtin_fabsf(w[1]) < hh[1]) << (2 * q + 1));
+                    }
+                    const bool inTset = (bool)((Tmask >> t) & 1u);
+                    const bool own = (t < tx) && ((lm & Tmask) == Tmask);
+                    const unsigned tb = ((unsigned)(t - cbase) < (unsigned)TG) ? (1u << (t - cbase)) : 0u;
+                    const unsigned skip = own ? (unsigned)(lm >> cbase) : 0u;
+                    const unsigned live = inTset ? 0u : (vmask & ~tb & ~skip);
+                    tcount += __popc(live);
+                    const unsigned rare = live & ~(dp & okm);
+                    if (__builtin_amdgcn_ballot_w64(rare != 0u)) {
+                        if (rare) {
+#pragma unroll
+                            for (int jj = 0; jj < TG; ++jj)
+                                if ((rare >> jj) & 1u) rare_cand(jj, t, Mt, vT, byy, bxy, lm);
+                        }
+                    }
+                    return;
+                } else {
                 const int jdead = YM == 1 ? t - cb0 : -1;
                 unsigned long long bad = 0ull;
 #pragma unroll
@@ -2139,15 +2230,13 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
                     bad |= keep0 & ~__builtin_amdgcn_ballot_w64(__builtin_fabsf(w[0]) < hh[0]);
                     bad |= keep1 & ~__builtin_amdgcn_ballot_w64(__builtin_fabsf(w[1]) < hh[1]);
                 }
-                const Mask lm = lmask[t];
                 const unsigned long long inT = __builtin_amdgcn_ballot_w64((bool)((Tmask >> t) & 1u));
                 unsigned long long rarel = (bad | notok) & ~inT;
                 if (YM == 2) rarel |= __builtin_amdgcn_ballot_w64((unsigned)(t - cbase) < (unsigned)nval);
                 if (t < tx) rarel |= __builtin_amdgcn_ballot_w64((lm & Tmask) == Tmask) & ~inT;
                 if (!rarel) return;
                 if (!(rarel & lanebit)) return;
-                // rare path (this lane): live set and dedup skips as in k_level_lds_t; a live test
-                // the fp32 check does not make certain is evaluated in fp64 from HBM
+                // rare path (this lane): live set and dedup skips as in k_level_lds_t
                 const bool own = (t < tx) && ((lm & Tmask) == Tmask);
                 const unsigned tb = ((unsigned)(t - cbase) < (unsigned)TG) ? (1u << (t - cbase)) : 0u;
                 const unsigned skip = own ? (unsigned)(lm >> cbase) : 0u;
@@ -2155,50 +2244,16 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
                 const unsigned live = vmask & ~tb & ~skip;
                 tcount -= __popc(vmask & ~tb & skip);
 #pragma unroll
-                for (int jj = 0; jj < TG; ++jj) {
-                    if (!((live >> jj) & 1u)) continue;
-                    const int q = jj >> 1, h = jj & 1;
-                    const int c = cbase + jj;
-                    if (okc[jj]) {   // the sweep's check for this candidate, recomputed
-                        float s_ = Mt[c];
-#pragma unroll
-                        for (int i = 0; i < DT; ++i) s_ = fmaf(-lcp[q][i][h], vT[i], s_);
-                        const float vc = s_ * rlp[q][h];
-                        const float cyy = fmaf(-vc, vc, byy);
-                        const float cxy = fmaf(-ucp[q][h], vc, bxy);
-                        const float w = fmaf(-mp[q][h], cyy, fmaf(cxy, cxy, -k1p[q][h]));
-                        if (__builtin_fabsf(w) < fmaf(hhp[q][h], cyy, -k2p[q][h])) continue;
-                        // certain independence, with bounds recovered from the candidate's
-                        // constants: m + hh <= c_xx - E, (k1 + k2) / s >= E, k2 - k1 >= kappa >=
-                        // tau / g (see the setup); each fp32 rounding below is covered by a
-                        // (1 +- 8 u32) factor:
-                        //   (|c_xy^| + E)^2 < lo2 (c_xx^ - E)(c_yy^ - E)            (r^2 < lo2)
-                        //   (c_xx^ - E)(c_yy^ - E) - (|c_xy^| + E)^2 > tau / g       (the guard)
-                        constexpr float U8 = (float)(8.0 * F32_U);
-                        const float Alb = (mp[q][h] + hhp[q][h]) * (1.0f - U8);
-                        const float Eub = (k1p[q][h] + k2p[q][h]) * inv_sf * (1.0f + U8);
-                        const float kgub = (k2p[q][h] - k1p[q][h]) * (1.0f + U8);
-                        const float ay = (cyy - Eub) * (1.0f - U8);
-                        const float ax = (__builtin_fabsf(cxy) + Eub) * (1.0f + U8);
-                        if (ay > 0.0f && ax * ax * (1.0f + U8) < lo2f * Alb * ay &&
-                            fmaf(ax, ax, kgub) * (1.0f + U8) < Alb * ay) {
-                            const Mask Smask = Tmask | ((Mask)1 << c);
-                            ++indep;
-                            lmask_atomic_or<WIDE>(&uself[t], Smask);
-                            if (((lm & Smask) == Smask) && t >= tx) lmask_atomic_or<WIDE>(&uprop[t], Smask);
-                            continue;
-                        }
-                    }
-                    int sg[DM];
-                    sg[0] = nxs[c];
-#pragma unroll
-                    for (int i = 0; i < DT; ++i) sg[i + 1] = nxs[T[i]];
-                    push_screen(a, x, nxs[t], sg, DM);
+                for (int jj = 0; jj < TG; ++jj)
+                    if ((live >> jj) & 1u) rare_cand(jj, t, Mt, vT, byy, bxy, lm);
                 }
             };
             using Y1 = std::integral_constant<int, 1>;
             using Y2 = std::integral_constant<int, 2>;
-            if (uni) {
+            using Y3 = std::integral_constant<int, 3>;
+            if (!SG) {
+                for (int t = 0; t < D; ++t) ystep(t, Y3{});
+            } else if (uni) {
                 for (int t = 0; t < D; ++t) ystep(t, Y1{});
             } else {
                 for (int t = 0; t < D; ++t) ystep(t, Y2{});
@@ -2620,7 +2675,7 @@ size_t lds_tgroup_f_bytes(int D, int DM, int mask_bytes) {
     const size_t np = (size_t)tg_pairs(D, DM);
     return lds_f32_core(D, mask_bytes) + (size_t)(D + 1) * (DM + 1) * 4 + (np + 1) * 4 + np * 2 + 16;
 }
-bool use_screen32(const pcg_handle *h, int d) { return h->screen32 && ((PCG_TG_F32 >> d) & 1); }
+bool use_screen32(const pcg_handle *h, int d) { return ((h->screen_mask < 0 ? PCG_TG_F32 : h->screen_mask) >> d) & 1; }
 constexpr size_t LDS_MAX = 160 * 1024;   // gfx950 LDS per workgroup
 
 // lane tasks of k_level_lds_t for a node of degree D at depth d (see the kernel)
@@ -2898,7 +2953,13 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
         }
         // ~4096 LDS-resident blocks per depth and rank; each lane walks spl units. The wide class
         // (a few nodes) aims at ~512 blocks so its nodes are spread over the chip
-        h->spl = (int)std::min(64.0, std::max(1.0, std::floor(sum_small / (256.0 * 4096.0 * h->world))));
+        double nb_target = getenv("PCG_NB") ? atof(getenv("PCG_NB")) : 4096.0;   // A/B knobs
+        {
+            char nm[16];
+            snprintf(nm, sizeof nm, "PCG_NB%d", depth);
+            if (getenv(nm)) nb_target = atof(getenv(nm));
+        }
+        h->spl = (int)std::min(64.0, std::max(1.0, std::floor(sum_small / (256.0 * nb_target * h->world))));
         h->spl_w = (int)std::min(64.0, std::max(1.0, std::floor(sum_wide / (256.0 * 512.0 * h->world))));
         const double mean_large = cnt_large ? sum_large / cnt_large : 0.0;
         h->chunk = (depth > PCG_MAX_DEPTH || mean_large <= 64) ? 64 : (mean_large <= 128 ? 128 : 256);
@@ -2971,7 +3032,7 @@ extern "C" int pcg_set_narrow_degree(pcg_handle *h, int max_degree) {
 
 extern "C" int pcg_set_screen_precision(pcg_handle *h, int fp32) {
     if (!h) return PCG_ERR_INVALID;
-    h->screen32 = fp32 != 0;
+    h->screen_mask = fp32 ? -1 : 0;
     return PCG_OK;
 }
 
@@ -3292,6 +3353,7 @@ extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
 static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N, double alpha,
                          int max_depth, int flags, int8_t *removed_level) {
     h->htrace_on = getenv("PCG_HOST_TRACE") != nullptr;
+    if (const char *e = getenv("PCG_SCREEN_MASK")) h->screen_mask = (int)strtol(e, nullptr, 0);   // A/B knob
     h->htrace.clear();
     PCG_HT(h, "init:start");
     // level d's wall time = between the depth-boundary events graph_launch records after init's
