@@ -1933,6 +1933,18 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
     const unsigned long long lanebit = 1ull << (tid & 63);
     const float inv_sf = (float)a.inv_s;                          // rounding covered by the check's margins
     const float lo2f = (float)(a.lo2 * (1.0 - 4.0 * F32_U));     // <= lo2
+    const float hi2f = (float)(a.hi2 * (1.0 + 4.0 * F32_U));     // >= hi2
+    const float tauf = (float)(a.tau * (1.0 + 4.0 * F32_U));     // >= tau
+    const f2v s2 = {(float)(a.s_amgm * (1.0 + 4.0 * F32_U)), (float)(a.s_amgm * (1.0 + 4.0 * F32_U))};   // >= s
+    // constant factors of the candidate setup's bounds (each rounded in its safe direction)
+    constexpr double RUd = 1.0 + 16.0 * F32_U;
+    const f2v ke2 = {(float)(2.0 * PCG_F32_KE * F32_U * RUd), (float)(2.0 * PCG_F32_KE * F32_U * RUd)};
+    const f2v ke2u = {(float)((2.0 * PCG_F32_KE + 1.0) * F32_U * RUd), (float)((2.0 * PCG_F32_KE + 1.0) * F32_U * RUd)};
+    const f2v inv_su = {(float)(a.inv_s * RUd), (float)(a.inv_s * RUd)};
+    const f2v tauu = {(float)(a.tau * RUd * RUd), (float)(a.tau * RUd * RUd)};
+    const f2v two_u = {(float)(2.0 * (1.0 + 8.0 * F32_U) * RUd), (float)(2.0 * (1.0 + 8.0 * F32_U) * RUd)};
+    const f2v one_u = {(float)((1.0 + 8.0 * F32_U) * RUd), (float)((1.0 + 8.0 * F32_U) * RUd)};
+    const f2v s2u = s2 + (float)F32_U;
 
     for (uint64_t task = r0 + tid; task < r1; task += bs) {
         int lq = 0, hq = np;
@@ -2020,74 +2032,87 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
 #pragma unroll
             for (int j = 0; j <= i; ++j) Lif[i][j] = (float)Li[i][j];
         }
-        // candidate constants, two candidates per packed register
+        // candidate constants, two candidates per packed register. The candidate's Cholesky row
+        // (l_c, 1/lambda, u_c, c_xx) is fp64; the decision constants are bounds built from it in
+        // packed fp32, every rounding covered by a (1 +- 16 u32) factor in the safe direction
         f2v lcp[NP][DT], rlp[NP], ucp[NP], mp[NP], hhp[NP], k1p[NP], k2p[NP];
         bool okc[TG];
+        const float liFf = (float)liF;
+        const float gTf = (float)gT * (1.0f - (float)(4.0 * F32_U));
 #pragma unroll
-        for (int jj = 0; jj < TG; ++jj) {
-            const int q = jj >> 1, h = jj & 1;
-            float lcf[DT];
+        for (int q = 0; q < NP; ++q) {
+            f2v cxf = {0.0f, 0.0f}, l2f = {0.0f, 0.0f}, r2f = {0.0f, 0.0f}, llf = {0.0f, 0.0f};
+            bool vld[2] = {false, false};
 #pragma unroll
-            for (int i = 0; i < DT; ++i) lcf[i] = 0.0f;
-            float rlf = 0.0f, ucf = 0.0f, mf = 0.0f, hhf = -1.0f, k1f = 0.0f, k2f = 1.0f;   // never "dependent"
-            bool ok = false;
-            if (jj < nmax) {                          // wave-uniform
-                const int c = cbase + jj;
-                const bool valid = c < T[0];
-                const int cc = valid ? c : 0;
-                double lc[DT], ll = 0.0, lu = 0.0;
+            for (int h = 0; h < 2; ++h) {
+                const int jj = 2 * q + h;
 #pragma unroll
-                for (int i = 0; i < DT; ++i) {
-                    double t = 0.0;
+                for (int i = 0; i < DT; ++i) lcp[q][i][h] = 0.0f;
+                rlp[q][h] = 0.0f;
+                ucp[q][h] = 0.0f;
+                if (jj < nmax) {                      // wave-uniform
+                    const int c = cbase + jj;
+                    const bool valid = c < T[0];
+                    const int cc = valid ? c : 0;
+                    double lc[DT], ll = 0.0, lu = 0.0;
 #pragma unroll
-                    for (int j = 0; j <= i; ++j) t += Li[i][j] * (double)M[T[j] * DS + cc];
-                    lc[i] = t;
-                    ll += t * t;
-                    lu += t * uT[i];
+                    for (int i = 0; i < DT; ++i) {
+                        double t = 0.0;
+#pragma unroll
+                        for (int j = 0; j <= i; ++j) t += Li[i][j] * (double)M[T[j] * DS + cc];
+                        lc[i] = t;
+                        ll += t * t;
+                        lu += t * uT[i];
+                    }
+                    const double lam2 = (double)M[cc * DS + cc] - ll;
+                    const double r = rsq_nr(lam2);
+                    const double u = ((double)Mdx[2 * cc + 1] - lu) * r;
+                    const double cxx = cx0 - u * u;
+#pragma unroll
+                    for (int i = 0; i < DT; ++i) lcp[q][i][h] = (float)lc[i];
+                    rlp[q][h] = (float)r;
+                    ucp[q][h] = (float)u;
+                    cxf[h] = (float)cxx;
+                    l2f[h] = (float)lam2;
+                    r2f[h] = (float)(r * r);
+                    llf[h] = (float)ll;
+                    vld[h] = valid && okT && (lam2 > 0.0);
                 }
-                const double lam2 = (double)M[cc * DS + cc] - ll;
-                const double r = rsq_nr(lam2);
-                const double u = ((double)Mdx[2 * cc + 1] - lu) * r;
-                const double cxx = cx0 - u * u;
-                // nu^2 = ||L_S^-1||_F^2 = ||Li||_F^2 + (|Li^T l_c|^2 + 1) / lambda^2
-                //     <= liF + (liF |l_c|^2 + 1) r^2;   E = KE u32 (1 + nu)^2 <= 2 KE u32 (1 + nu^2)
-                const double r2 = r * r;
-                const double E = (2.0 * PCG_F32_KE * F32_U) * (1.0 + fma(fma(liF, ll, 1.0), r2, liF));
-                const double te = E * a.inv_s;                        // E / s
-                const double g = fmin(gT, lam2) - E;                  // smallest pivot^2 of C_SS, lower bound
-                const double cmE = cxx - E;
-                ok = valid && okT && (lam2 > 0.0) && (te <= 0.5) && (cmE > 0.0) && (g > 0.0);
-                if (ok) {
-                    constexpr double u8 = 8.0 * F32_U;
-                    const double s = a.s_amgm;
-                    const double kg = a.tau * rcp_nr(g) * (1.0 + 1e-9);
-                    const double hx = a.hi2 * (cxx + E);
-                    const double f1 = fma(2.0 * te, 1.0 + u8, 1.0 + u8);   // (1 + 2 te)(1 + u8)
-                    const double al = hx * f1;
-                    const double be = E * (hx + s) * f1;
-                    const double ga = cmE * (1.0 - te) * (1.0 - u8);
-                    const double ka = fma(E, cmE + s + E, kg) * (1.0 + u8);
-                    ok = ga > al;
-                    mf = (float)(0.5 * (al + ga));
-                    hhf = (float)(fma(-2.0 * u8, ga, 0.5 * (ga - al)));
-                    k1f = (float)(0.5 * (be - ka));
-                    k2f = (float)(0.5 * (be + ka) * (1.0 + u8));
-                    if (!ok) { mf = 0.0f; hhf = -1.0f; k1f = 0.0f; k2f = 1.0f; }
-                }
-#pragma unroll
-                for (int i = 0; i < DT; ++i) lcf[i] = (float)lc[i];
-                rlf = (float)r;
-                ucf = (float)u;
             }
+            // E >= KE u32 (1 + nu)^2 + |fp32(c_xx) - c_xx|, nu^2 <= liF + (liF |l_c|^2 + 1) r^2.
+            // Each bound below has fewer than 16 roundings between its inputs (themselves bounds
+            // in the right direction) and its single RU / RD factor.
+            constexpr float U = (float)F32_U;
+            constexpr float RU = 1.0f + 16.0f * U, RD = 1.0f - 16.0f * U, U8 = 8.0f * U;
+            const f2v one = {1.0f, 1.0f};
+            const f2v liF2 = {liFf, liFf};
+            const f2v nu2 = __builtin_elementwise_fma(__builtin_elementwise_fma(liF2, llf, one), r2f, liF2);
+            const f2v E = __builtin_elementwise_fma(nu2, ke2, ke2u);  // (KE2 (1 + nu^2) + u) RU
+            const f2v te = E * inv_su;                                // >= E / s
+            const f2v gT2 = {gTf, gTf};
+            const f2v g = (__builtin_elementwise_min(gT2, l2f) - (E + 2.0f * U)) * RD;   // <= smallest pivot^2 of C_SS
+            const f2v cmE = (cxf - E) * RD;                           // <= c_xx - E
+            const f2v rg = {__builtin_amdgcn_rcpf(g[0]), __builtin_amdgcn_rcpf(g[1])};
+            const f2v kg = tauu * rg;                                 // >= tau / g
+            const f2v hx = hi2f * (cxf + E);                          // hi2 (c_xx + E), RU in f1
+            const f2v f1 = __builtin_elementwise_fma(te, two_u, one_u);   // (1 + 2 te)(1 + u8) RU
+            const f2v al = hx * f1;
+            const f2v be = E * (hx + s2) * f1;
+            const f2v ga = (cmE - cmE * te) * ((1.0f - U8) * RD);
+            const f2v ka = __builtin_elementwise_fma(E, cxf + s2u, kg) * ((1.0f + U8) * RU);  // E (c_xx + s) + kg
+            const f2v mm = 0.5f * (al + ga);
+            const f2v hw = __builtin_elementwise_fma(-2.0f * U8 * one, ga, 0.5f * (ga - al));
+            const f2v kk1 = 0.5f * (be - ka);
+            const f2v kk2 = (be + ka) * (0.5f * (1.0f + U8));
 #pragma unroll
-            for (int i = 0; i < DT; ++i) lcp[q][i][h] = lcf[i];
-            rlp[q][h] = rlf;
-            ucp[q][h] = ucf;
-            mp[q][h] = mf;
-            hhp[q][h] = hhf;
-            k1p[q][h] = k1f;
-            k2p[q][h] = k2f;
-            okc[jj] = ok;
+            for (int h = 0; h < 2; ++h) {
+                const bool ok = vld[h] && (te[h] <= 0.5f) && (cmE[h] > 0.0f) && (g[h] > 0.0f) && (ga[h] > al[h]);
+                okc[2 * q + h] = ok;
+                mp[q][h] = ok ? mm[h] : 0.0f;                          // unusable: never "dependent"
+                hhp[q][h] = ok ? hw[h] : -1.0f;
+                k1p[q][h] = ok ? kk1[h] : 0.0f;
+                k2p[q][h] = ok ? kk2[h] : 1.0f;
+            }
         }
         const int cend = min(T[0], cbase + TG);
         unsigned okm = 0;
