@@ -112,11 +112,13 @@ def k1_roofline(n: int, N: int, corr_ms: float) -> dict:
 def dominant_kernel(d: int, full_p: bool) -> str:
     """Name (as rocprofv3 prints it, template args kept) of the CI-test kernel that runs
     depth ``d`` for nodes of degree <= 64 — the host dispatch in skeleton.hip
-    (``use_tgroup``: threshold mode at depths 2..4 uses the T-group kernel)."""
+    (``use_tgroup``: threshold mode at depths 2..4 uses the T-group kernel; ``use_screen32``:
+    its fp32-screened form k_level_lds_f at the depths of PCG_TG_F32 / PCG_SCREEN_MASK)."""
     if d == 0:
         return f"k_level0<{1 if full_p else 0}>"
     if not full_p and 2 <= d <= 4:
-        return f"k_level_lds_t<{d}, false>"
+        mask = int(os.environ.get("PCG_SCREEN_MASK", "0x18"), 0)
+        return f"k_level_lds_{'f' if (mask >> d) & 1 else 't'}<{d}, false>"
     return f"k_level_lds<{d}, {1 if full_p else 0}>"
 
 

@@ -1789,16 +1789,12 @@ constexpr double F32_U = 5.9604644775390625e-08;   // 2^-24
 #endif
 __host__ __device__ constexpr int tgf_minblocks(int DM) { return DM == 2 ? PCG_MBF2 : (DM == 3 ? PCG_MBF3 : PCG_MBF4); }
 
-// 1/sqrt(x) and 1/x in fp64 from the fp32 hardware estimate plus one Newton step (relative
+// 1/sqrt(x) in fp64 from the fp32 hardware estimate plus one Newton step (relative
 // error ~1e-14 for normal fp32-range x; x <= 0 or out of fp32 range gives inf / NaN, which the
 // callers' checks reject)
 __device__ __forceinline__ double rsq_nr(double x) {
     const double r0 = (double)__builtin_amdgcn_rsqf((float)x);
     return r0 * fma(-0.5 * x * r0, r0, 1.5);
-}
-__device__ __forceinline__ double rcp_nr(double x) {
-    const double r0 = (double)__builtin_amdgcn_rcpf((float)x);
-    return r0 * fma(-x, r0, 2.0);
 }
 
 // (x, y | S) in fp64 from the C in HBM (Cholesky of C_SS, the fp64 kernels' guard and band):
@@ -1934,7 +1930,6 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
     const float inv_sf = (float)a.inv_s;                          // rounding covered by the check's margins
     const float lo2f = (float)(a.lo2 * (1.0 - 4.0 * F32_U));     // <= lo2
     const float hi2f = (float)(a.hi2 * (1.0 + 4.0 * F32_U));     // >= hi2
-    const float tauf = (float)(a.tau * (1.0 + 4.0 * F32_U));     // >= tau
     const f2v s2 = {(float)(a.s_amgm * (1.0 + 4.0 * F32_U)), (float)(a.s_amgm * (1.0 + 4.0 * F32_U))};   // >= s
     // constant factors of the candidate setup's bounds (each rounded in its safe direction)
     constexpr double RUd = 1.0 + 16.0 * F32_U;
@@ -2700,7 +2695,7 @@ size_t lds_tgroup_f_bytes(int D, int DM, int mask_bytes) {
     const size_t np = (size_t)tg_pairs(D, DM);
     return lds_f32_core(D, mask_bytes) + (size_t)(D + 1) * (DM + 1) * 4 + (np + 1) * 4 + np * 2 + 16;
 }
-bool use_screen32(const pcg_handle *h, int d) { return ((h->screen_mask < 0 ? PCG_TG_F32 : h->screen_mask) >> d) & 1; }
+bool use_screen32(const pcg_handle *h, int d) { return (h->screen_eff >> d) & 1; }
 constexpr size_t LDS_MAX = 160 * 1024;   // gfx950 LDS per workgroup
 
 // lane tasks of k_level_lds_t for a node of degree D at depth d (see the kernel)
@@ -2953,6 +2948,9 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
         // small class units: T-group lane tasks (threshold mode, depth 2..4) or S ranks
         const bool tg = use_tgroup(mode_of(h, depth), depth);
         h->tgroup = tg;
+        // fp32-screened depths: pcg_set_screen_precision, or the PCG_SCREEN_MASK A/B knob
+        const char *sm = getenv("PCG_SCREEN_MASK");
+        h->screen_eff = sm ? (int)strtol(sm, nullptr, 0) : (h->screen_mask < 0 ? PCG_TG_F32 : h->screen_mask);
         std::vector<uint64_t> ns_of(maxd + 1, 0), units_of(maxd + 1, 0);
         std::vector<int> cls_of(maxd + 1, 2);
         double sum_small = 0.0, sum_wide = 0.0, sum_large = 0.0;
@@ -3378,7 +3376,6 @@ extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
 static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N, double alpha,
                          int max_depth, int flags, int8_t *removed_level) {
     h->htrace_on = getenv("PCG_HOST_TRACE") != nullptr;
-    if (const char *e = getenv("PCG_SCREEN_MASK")) h->screen_mask = (int)strtol(e, nullptr, 0);   // A/B knob
     h->htrace.clear();
     PCG_HT(h, "init:start");
     // level d's wall time = between the depth-boundary events graph_launch records after init's

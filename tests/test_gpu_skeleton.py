@@ -86,6 +86,27 @@ def test_wide_and_large_classes_match_oracle(eng, n, N, seed, wl, wh, ep, narrow
     assert_skeleton_matches(out, ref, n)
 
 
+@pytest.mark.parametrize("mask", ["0", "0x1c"])
+@pytest.mark.parametrize("narrow", [64, 16])
+@pytest.mark.parametrize("n,N,seed,wl,wh,ep", CASES[2:])
+def test_screen_precision_masks_match_oracle(eng, n, N, seed, wl, wh, ep, narrow, mask, monkeypatch):
+    """The fp32-screened T-group sweep (k_level_lds_f) against the all-fp64 one (mask 0) and
+    with depth 2 screened too (0x1c), narrow and wide classes: identical skeletons, unions and
+    per-level counts (PCG_SCREEN_MASK is read per skeleton call)."""
+    X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
+    C = np.corrcoef(X.T)
+    ref = cpc.skeleton(C, N)
+    monkeypatch.setenv("PCG_SCREEN_MASK", mask)
+    _lib.check(eng.h, eng.lib.pcg_set_narrow_degree(eng.h, narrow), "pcg_set_narrow_degree")
+    try:
+        out = eng.skeleton(C, N)
+    finally:
+        eng.lib.pcg_set_narrow_degree(eng.h, 64)
+    assert_skeleton_matches(out, ref, n)
+    if mask == "0":
+        assert sum(out.stats["screened"]) == 0
+
+
 @pytest.mark.parametrize("noise", [1e-2, 1e-4, 1e-6, 1e-7])
 @pytest.mark.parametrize("flags", [0, _lib.PCG_FLAG_FULL_P | _lib.PCG_FLAG_RECORD])
 def test_near_collinear_columns_match_lu_oracle(eng, noise, flags):
@@ -152,6 +173,16 @@ def test_config5_full_depth4_matches_oracle(eng):
           f"near-alpha {len(ref.near_alpha)} / engine {len(a.near_alpha)}", file=sys.stderr, flush=True)
     flips = assert_skeleton_matches(a, ref, 2000)
     flips_b = assert_skeleton_matches(b, ref, 2000)
+    # the fp32-screened sweep (default at depths 3-4) left only a small share to its fp64
+    # screen; the all-fp64 T-group sweep gives the same skeleton
+    assert 0 < a.stats["screened"][4] < 1e-3 * a.stats["tests"][4], a.stats["screened"]
+    _lib.check(eng.h, eng.lib.pcg_set_screen_precision(eng.h, 0), "pcg_set_screen_precision")
+    try:
+        c = eng.skeleton(C, 10000, max_depth=4, flags=0)
+    finally:
+        eng.lib.pcg_set_screen_precision(eng.h, 1)
+    assert sum(c.stats["screened"]) == 0
+    assert_skeleton_matches(c, ref, 2000)
     print(f"near-alpha flips: threshold {flips}, full-p {flips_b}", file=sys.stderr, flush=True)
     rec = b.records
     per_depth = np.bincount(rec["d"], minlength=5)
