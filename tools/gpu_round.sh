@@ -28,7 +28,7 @@ step pmc_sq2 200 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_B
 step pmc_mfma 200 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_VALU GRBM_GUI_ACTIVE -d $OUT/pmc_mfma -o run --output-format csv -- $B
 python tools/pmc_summary.py profiles/${TAG}_pmc_summary.json $OUT > $OUT/pmc_summary.log 2>&1 && cp profiles/${TAG}_pmc_summary.json $OUT/
 python tools/timeline.py $OUT/prof/run_kernel_trace.csv > $OUT/${TAG}_timeline.txt 2>&1
-step valu_occ 120 ./tools/micro/valu_occ
+[ -x tools/micro/valu_occ ] && step valu_occ 120 ./tools/micro/valu_occ
 step bench 900 python bench.py --steps 20 --warmup 3
 cat $OUT/round_status.log
 tail -c 600 $OUT/bench.log
