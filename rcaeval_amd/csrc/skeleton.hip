@@ -132,6 +132,31 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
     return v;
 }
 
+// per-kernel test / independence counters: one atomic pair per BLOCK (wave sums staged in
+// LDS). Per-wave atomics on the two counter words queue at the L2 when many blocks end together
+// (measured: 40 us at depth 0, 0.35 ms for depth 1's 5 400 blocks). Every thread must call it.
+__device__ __forceinline__ void block_flush_counts(DevCounters *ctr, unsigned long long tests,
+                                                   unsigned long long indep) {
+    __shared__ unsigned long long s_cnt[2][16];
+    tests = wave_sum(tests);
+    indep = wave_sum(indep);
+    const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        s_cnt[0][w] = tests;
+        s_cnt[1][w] = indep;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0, i = 0;
+        for (int k = 0; k < nw; ++k) {
+            t += s_cnt[0][k];
+            i += s_cnt[1][k];
+        }
+        if (t) atomicAdd(&ctr->tests, t);
+        if (i) atomicAdd(&ctr->indep, i);
+    }
+}
+
 __device__ __forceinline__ int find_in_sorted(const int32_t *a, int len, int v) {
     int lo = 0, hi = len - 1;
     while (lo < hi) {
@@ -509,12 +534,7 @@ __global__ __launch_bounds__(256) void k_level0(LevelArgs a) {
         const int ym = y0 + r, xm = x0 + tx;
         if (ym < a.n && xm < a.n && ym > xm) a.rm[(int64_t)ym * a.n + xm] = flag[tx][r];
     }
-    tests = wave_sum(tests);
-    indep = wave_sum(indep);
-    if ((threadIdx.x & 63) == 0) {
-        if (tests) atomicAdd(&a.ctr->tests, tests);
-        if (indep) atomicAdd(&a.ctr->indep, indep);
-    }
+    block_flush_counts(a.ctr, tests, indep);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -745,12 +765,7 @@ __global__ __launch_bounds__(256) void k_level(LevelArgs a) {
         __syncthreads();
     }
 
-    tests = wave_sum(tests);
-    indep = wave_sum(indep);
-    if (lane == 0) {
-        if (tests) atomicAdd(&a.ctr->tests, tests);
-        if (indep) atomicAdd(&a.ctr->indep, indep);
-    }
+    block_flush_counts(a.ctr, tests, indep);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -763,11 +778,11 @@ __global__ __launch_bounds__(256) void k_level(LevelArgs a) {
 // for (x, y | z): v = C_yz / sqrt(C_zz), c_xy = C_xy - u_z v, c_yy = C_yy - v^2.
 // A chunk is (x, a contiguous share of the D(D-1)/2 pairs, row-major over y < z).
 constexpr int L1_MAXD = 1024;
+constexpr int L1_PB = 4;              // pairs in flight per lane (independent gathers)
+size_t l1_lds_bytes(int D) { return (size_t)D * (4 + 5 * 8) + 16; }
 __global__ __launch_bounds__(256) void k_level1_pairs(LevelArgs a) {
-    __shared__ int32_t s_nx[L1_MAXD];
-    __shared__ double s_cx[L1_MAXD], s_d[L1_MAXD], s_ri[L1_MAXD], s_u[L1_MAXD], s_cxx[L1_MAXD];
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x;
-    const int lane = tid & 63;
     const int64_t chunk = a.chunk_lo + blockIdx.x;
     int lo = 0, hi = a.n;
     while (hi - lo > 1) {
@@ -777,6 +792,10 @@ __global__ __launch_bounds__(256) void k_level1_pairs(LevelArgs a) {
     const int x = lo;
     const int D = a.deg[x];
     const int W = a.W;
+    // per-neighbour terms, sized by this node's degree (the launch reserves the largest)
+    double *s_cx = reinterpret_cast<double *>(smem);
+    double *s_d = s_cx + D, *s_ri = s_d + D, *s_u = s_ri + D, *s_cxx = s_u + D;
+    int32_t *s_nx = reinterpret_cast<int32_t *>(s_cxx + D);
     const int32_t *nx = a.nbr + a.off[x];
     const double *Cx = a.C + (int64_t)x * a.ldc;
     const double Cxx = a.diag[x];
@@ -800,60 +819,78 @@ __global__ __launch_bounds__(256) void k_level1_pairs(LevelArgs a) {
     const int64_t c = chunk - a.cpre[x];
     const int64_t p0 = npairs * c / nch, p1 = npairs * (c + 1) / nch;
     unsigned long long tests = 0, indep = 0;
-    const double twoD1 = 2.0 * D - 1.0;
+    const float twoD1 = 2.0f * D - 1.0f;
+    auto rowstart = [&](int r) -> int64_t { return (int64_t)r * (2 * D - 1 - r) / 2; };
 
-    for (int64_t p = p0 + tid; p < p1; p += blockDim.x) {
-        // pair p -> (y, z), y < z: row y starts at y(2D - 1 - y)/2
-        int y = (int)floor((twoD1 - sqrt(twoD1 * twoD1 - 8.0 * (double)p)) * 0.5);
-        auto rowstart = [&](int r) -> int64_t { return (int64_t)r * (2 * D - 1 - r) / 2; };
-        if (y < 0) y = 0;
-        while (y > 0 && rowstart(y) > p) --y;
-        while (rowstart(y + 1) <= p) ++y;
-        const int z = y + 1 + (int)(p - rowstart(y));
-        const int yg = s_nx[y], zg = s_nx[z];
-        const double cyz = a.C[(int64_t)yg * a.ldc + zg];
-        const bool adj_yz = (a.adj[(int64_t)yg * W + (zg >> 6)] >> (zg & 63)) & 1ull;
+    for (int64_t pb = p0 + tid; pb < p1; pb += (int64_t)L1_PB * blockDim.x) {
+        // L1_PB pairs per lane: indices first, then every gather, then the tests
+        int ys[L1_PB], zs[L1_PB];
+        double cyz[L1_PB];
+        uint64_t aw[L1_PB];
 #pragma unroll
-        for (int side = 0; side < 2; ++side) {
-            // side 0: test (x, y | z); side 1: test (x, z | y)
-            const int t = side ? z : y;        // the tested neighbour (local), S = {k}
-            const int k = side ? y : z;
-            const int tg = side ? zg : yg, kg = side ? yg : zg;
-            if (tg < x && adj_yz) continue;    // memo: node tg owns (tg, x, {kg})
-            ++tests;
-            const double cxx = s_cxx[k];
-            int dec = 2;
-            if (cxx == cxx) {
-                double pv = 0.0;
-                const double v = cyz * s_ri[k];
-                const double cxt = s_cx[t] - s_u[k] * v;
-                const double ctt = s_d[t] - v * v;
-                dec = decide<MODE_DECIDE>(a, cxt, cxx, ctt, a.tau * s_ri[k] * s_ri[k], &pv);
+        for (int q = 0; q < L1_PB; ++q) {
+            const int64_t p = pb + (int64_t)q * blockDim.x;
+            int y = 0, z = 1;
+            if (p < p1) {
+                // pair p -> (y, z), y < z: row y starts at y(2D - 1 - y)/2 (fp32 root, then exact fix-up)
+                y = (int)floorf((twoD1 - sqrtf(fmaxf(twoD1 * twoD1 - 8.0f * (float)p, 0.0f))) * 0.5f);
+                if (y < 0) y = 0;
+                while (y > 0 && rowstart(y) > p) --y;
+                while (rowstart(y + 1) <= p) ++y;
+                z = y + 1 + (int)(p - rowstart(y));
             }
-            if (dec == 2) {
-                const int sg[1] = {kg};
-                push_deferred(a, x, tg, sg, 1);
-            } else if (dec == 1) {
-                ++indep;
-                a.rm[(int64_t)x * a.n + tg] = 1;
-                a.rm[(int64_t)tg * a.n + x] = 1;
-                unsigned long long *row = reinterpret_cast<unsigned long long *>(
-                    a.ug + ((int64_t)a.off[x] + t) * W);
-                atomicOr(&row[kg >> 6], 1ull << (kg & 63));
-                if (adj_yz && tg > x) {        // S in adj(tg): also tg's side of the pair
-                    const int slot = a.off[tg] + find_in_sorted(a.nbr + a.off[tg], a.deg[tg], x);
-                    unsigned long long *rowt = reinterpret_cast<unsigned long long *>(a.ug + (int64_t)slot * W);
-                    atomicOr(&rowt[kg >> 6], 1ull << (kg & 63));
+            ys[q] = y;
+            zs[q] = z;
+        }
+#pragma unroll
+        for (int q = 0; q < L1_PB; ++q) {
+            const int yg = s_nx[ys[q]], zg = s_nx[zs[q]];
+            cyz[q] = a.C[(int64_t)yg * a.ldc + zg];
+            aw[q] = a.adj[(int64_t)yg * W + (zg >> 6)];
+        }
+#pragma unroll
+        for (int q = 0; q < L1_PB; ++q) {
+            if (pb + (int64_t)q * blockDim.x >= p1) continue;
+            const int y = ys[q], z = zs[q];
+            const int yg = s_nx[y], zg = s_nx[z];
+            const bool adj_yz = (aw[q] >> (zg & 63)) & 1ull;
+#pragma unroll
+            for (int side = 0; side < 2; ++side) {
+                // side 0: test (x, y | z); side 1: test (x, z | y)
+                const int t = side ? z : y;        // the tested neighbour (local), S = {k}
+                const int k = side ? y : z;
+                const int tg = side ? zg : yg, kg = side ? yg : zg;
+                if (tg < x && adj_yz) continue;    // memo: node tg owns (tg, x, {kg})
+                ++tests;
+                const double cxx = s_cxx[k];
+                int dec = 2;
+                if (cxx == cxx) {
+                    double pv = 0.0;
+                    const double v = cyz[q] * s_ri[k];
+                    const double cxt = s_cx[t] - s_u[k] * v;
+                    const double ctt = s_d[t] - v * v;
+                    dec = decide<MODE_DECIDE>(a, cxt, cxx, ctt, a.tau * s_ri[k] * s_ri[k], &pv);
+                }
+                if (dec == 2) {
+                    const int sg[1] = {kg};
+                    push_deferred(a, x, tg, sg, 1);
+                } else if (dec == 1) {
+                    ++indep;
+                    a.rm[(int64_t)x * a.n + tg] = 1;
+                    a.rm[(int64_t)tg * a.n + x] = 1;
+                    unsigned long long *row = reinterpret_cast<unsigned long long *>(
+                        a.ug + ((int64_t)a.off[x] + t) * W);
+                    atomicOr(&row[kg >> 6], 1ull << (kg & 63));
+                    if (adj_yz && tg > x) {        // S in adj(tg): also tg's side of the pair
+                        const int slot = a.off[tg] + find_in_sorted(a.nbr + a.off[tg], a.deg[tg], x);
+                        unsigned long long *rowt = reinterpret_cast<unsigned long long *>(a.ug + (int64_t)slot * W);
+                        atomicOr(&rowt[kg >> 6], 1ull << (kg & 63));
+                    }
                 }
             }
         }
     }
-    tests = wave_sum(tests);
-    indep = wave_sum(indep);
-    if (lane == 0) {
-        if (tests) atomicAdd(&a.ctr->tests, tests);
-        if (indep) atomicAdd(&a.ctr->indep, indep);
-    }
+    block_flush_counts(a.ctr, tests, indep);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1176,12 +1213,7 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
             }
         }
     }
-    tests = wave_sum(tests);
-    indep = wave_sum(indep);
-    if ((tid & 63) == 0) {
-        if (tests) atomicAdd(&a.ctr->tests, tests);
-        if (indep) atomicAdd(&a.ctr->indep, indep);
-    }
+    block_flush_counts(a.ctr, tests, indep);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1737,12 +1769,7 @@ __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_
             }
         }
     }
-    tests = wave_sum(tests);
-    indep = wave_sum(indep);
-    if ((tid & 63) == 0) {
-        if (tests) atomicAdd(&a.ctr->tests, tests);
-        if (indep) atomicAdd(&a.ctr->indep, indep);
-    }
+    block_flush_counts(a.ctr, tests, indep);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2319,12 +2346,7 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
             }
         }
     }
-    tests = wave_sum(tests);
-    indep = wave_sum(indep);
-    if ((tid & 63) == 0) {
-        if (tests) atomicAdd(&a.ctr->tests, tests);
-        if (indep) atomicAdd(&a.ctr->indep, indep);
-    }
+    block_flush_counts(a.ctr, tests, indep);
 }
 
 // The fp64 screen of the tests the fp32 sweep handed over (one lane per test, after the level
@@ -2710,6 +2732,13 @@ uint64_t tgroup_tasks(const pcg_handle *h, int D, int d) {
 }
 
 bool use_tgroup(int mode, int d) { return mode == MODE_DECIDE && d >= 2 && d <= 4; }
+// depth 1's large class runs k_level1_pairs (pcg_level_run); its chunks split a node's
+// D(D-1)/2 neighbour pairs evenly, ~L1_PAIRS_PER_CHUNK each, so a high-degree node is spread
+// over many blocks instead of a D/256-chunk tail
+constexpr int64_t L1_PAIRS_PER_CHUNK = 2048;
+int mode_of(const pcg_handle *h, int d);
+bool use_l1_pairs(const pcg_handle *h, int d) { return d == 1 && mode_of(h, d) == MODE_DECIDE && h->maxdeg <= L1_MAXD; }
+int64_t l1_pair_chunks(int D) { return std::max<int64_t>(1, ((int64_t)D * (D - 1) / 2 + L1_PAIRS_PER_CHUNK - 1) / L1_PAIRS_PER_CHUNK); }
 
 // node class of a degree-D node at depth d: 0 narrow, 1 wide (T-group depths only), 2 large
 int level_class(const pcg_handle *h, int D, int d, bool tg) {
@@ -2988,11 +3017,12 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
         h->chunk = (depth > PCG_MAX_DEPTH || mean_large <= 64) ? 64 : (mean_large <= 128 ? 128 : 256);
         const uint64_t csz = (uint64_t)256 * h->spl, cszw = (uint64_t)256 * h->spl_w;
         std::vector<int64_t> nch_of(maxd + 1, 0);
+        const bool l1p = use_l1_pairs(h, depth);
         for (int D = depth + 1; D <= maxd; ++D) {
             const int c = cls_of[D];
             nch_of[D] = c == 0 ? (int64_t)((units_of[D] + csz - 1) / csz)
                                : c == 1 ? (int64_t)((units_of[D] + cszw - 1) / cszw)
-                                        : (int64_t)((ns_of[D] + h->chunk - 1) / h->chunk);
+                                        : l1p ? l1_pair_chunks(D) : (int64_t)((ns_of[D] + h->chunk - 1) / h->chunk);
         }
         int64_t ss = 0, sw = 0, sl = 0;
         for (int x = 0; x < n; ++x) {
@@ -3098,6 +3128,14 @@ extern "C" int pcg_level_chunk_work(pcg_handle *h, int64_t *prefix_host, int64_t
                 continue;
             }
             const int D = h->deg_h[x];
+            if (cls == 2 && use_l1_pairs(h, h->depth)) {   // k_level1_pairs: an even share of the pairs, two tests each
+                const int64_t np = (int64_t)D * (D - 1) / 2, nch = c1 - c0;
+                for (int64_t c = c0; c < c1; ++c) {
+                    acc += 2 * (np * (c - c0 + 1) / nch - np * (c - c0) / nch) + 1;
+                    prefix_host[base + c + 1] = acc;
+                }
+                continue;
+            }
             const bool tg = (cls < 2) && h->tgroup;
             const uint64_t ns = tg ? tgroup_tasks(h, D, h->depth) : hbinom(h, D, h->depth);
             const int64_t per_unit = (int64_t)(D - h->depth) * (tg ? tg_of_depth(h->depth) : 1);
@@ -3244,7 +3282,8 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                     if (lds > LDS_MAX)
                         return pcg_fail(h, PCG_ERR_INVALID, "max degree %d too large for LDS staging", h->maxdeg);
                     if (mode == MODE_DECIDE && d == 1 && h->maxdeg <= L1_MAXD)
-                        hipLaunchKernelGGL(k_level1_pairs, dim3((unsigned)(l_hi - l_lo)), dim3(256), 0, h->stream, al);
+                        hipLaunchKernelGGL(k_level1_pairs, dim3((unsigned)(l_hi - l_lo)), dim3(256),
+                                           l1_lds_bytes(h->maxdeg), h->stream, al);
                     else if (mode == MODE_DECIDE) launch_level_mode<MODE_DECIDE>(h, al, l_hi - l_lo, lds);
                     else if (mode == MODE_FULLP) launch_level_mode<MODE_FULLP>(h, al, l_hi - l_lo, lds);
                     else launch_level_mode<MODE_EXACT>(h, al, l_hi - l_lo, lds);
