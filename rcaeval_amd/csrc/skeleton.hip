@@ -1906,19 +1906,58 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
         btab[e] = (unsigned)pcg_binom(a.binom, c, i);
     }
     __syncthreads();
-    for (int e = tid; e < D * DS; e += bs) {
-        const int t = e / DS, k = e - t * DS;
-        M[e] = k < D ? (float)a.C[(int64_t)nxs[t] * a.ldc + nxs[k]] : 0.0f;
-    }
-    for (int t = tid >> 6; t < D; t += bs >> 6) {
-        const uint64_t *ar = a.adj + (int64_t)nxs[t] * a.W;
-        Mask m = 0;
-        for (int k0 = 0; k0 < D; k0 += 64) {
-            const int k = k0 + (tid & 63);
-            const bool bit = k < D && ((ar[nxs[k] >> 6] >> (nxs[k] & 63)) & 1ull);
-            m |= (Mask)__ballot(bit) << k0;
+    if constexpr (WIDE) {   // (the row-batched form below measured slower for the 128-wide blocks)
+        for (int e = tid; e < D * DS; e += bs) {
+            const int t = e / DS, k = e - t * DS;
+            M[e] = k < D ? (float)a.C[(int64_t)nxs[t] * a.ldc + nxs[k]] : 0.0f;
         }
-        if ((tid & 63) == 0) lmask[t] = m;
+        for (int t = tid >> 6; t < D; t += bs >> 6) {
+            const uint64_t *ar = a.adj + (int64_t)nxs[t] * a.W;
+            Mask m = 0;
+            for (int k0 = 0; k0 < D; k0 += 64) {
+                const int k = k0 + (tid & 63);
+                const bool bit = k < D && ((ar[nxs[k] >> 6] >> (nxs[k] & 63)) & 1ull);
+                m |= (Mask)__ballot(bit) << k0;
+            }
+            if ((tid & 63) == 0) lmask[t] = m;
+        }
+    } else {   // rows of A~ and of the local adjacency masks: a wave takes SR rows at a time, lane k
+        // column k (its global id hoisted), so SR x (C entry, adjacency word) loads are in flight
+        // per lane before the first is used; no index division
+        constexpr int H = 1, SR = 4;
+        const int lane = tid & 63, wv = tid >> 6, nwv = bs >> 6;
+        int kg[H];
+#pragma unroll
+        for (int hh = 0; hh < H; ++hh) kg[hh] = lane + 64 * hh < D ? nxs[lane + 64 * hh] : -1;
+        for (int t0 = wv * SR; t0 < D; t0 += nwv * SR) {
+            float v[SR][H];
+            uint64_t w[SR][H];
+#pragma unroll
+            for (int r = 0; r < SR; ++r) {
+                const int t = min(t0 + r, D - 1);
+                const int rg = nxs[t];
+#pragma unroll
+                for (int hh = 0; hh < H; ++hh) {
+                    const int k = kg[hh] < 0 ? 0 : kg[hh];
+                    v[r][hh] = (float)a.C[(int64_t)rg * a.ldc + k];
+                    w[r][hh] = a.adj[(int64_t)rg * a.W + (k >> 6)];
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < SR; ++r) {
+                const int t = t0 + r;
+                if (t >= D) break;                   // wave-uniform
+                Mask m = 0;
+#pragma unroll
+                for (int hh = 0; hh < H; ++hh) {
+                    const int k = lane + 64 * hh;
+                    if (k < DS) M[t * DS + k] = kg[hh] >= 0 ? v[r][hh] : 0.0f;
+                    const bool bit = kg[hh] >= 0 && ((w[r][hh] >> (kg[hh] & 63)) & 1ull);
+                    m |= (Mask)__ballot(bit) << (64 * hh);
+                }
+                if (lane == 0) lmask[t] = m;
+            }
+        }
     }
     for (int t = tid; t < D; t += bs) {
         const int yg = nxs[t];
