@@ -364,8 +364,9 @@ def main():
 
     for _ in range(args.warmup):
         one_step()
-    times, outs = [], []
+    times, out = [], None
     for _ in range(args.steps):
+        out = None          # the previous step's result is released, as a caller consuming each result would
         barrier()
         t0 = time.perf_counter()
         out = one_step()
@@ -378,8 +379,6 @@ def main():
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
             dt = float(t.item())
         times.append(dt)
-        outs.append(out)
-    out = outs[-1]
     st = out.stats
     tests_total = int(sum(st["tests"]))
     ms = 1000.0 * float(np.mean(times))
