@@ -3051,7 +3051,8 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
             if (getenv(nm)) nb_target = atof(getenv(nm));
         }
         h->spl = (int)std::min(64.0, std::max(1.0, std::floor(sum_small / (256.0 * nb_target * h->world))));
-        h->spl_w = (int)std::min(64.0, std::max(1.0, std::floor(sum_wide / (256.0 * 512.0 * h->world))));
+        const double nbw_target = getenv("PCG_NBW") ? atof(getenv("PCG_NBW")) : 512.0;   // A/B knob
+        h->spl_w = (int)std::min(64.0, std::max(1.0, std::floor(sum_wide / (256.0 * nbw_target * h->world))));
         const double mean_large = cnt_large ? sum_large / cnt_large : 0.0;
         h->chunk = (depth > PCG_MAX_DEPTH || mean_large <= 64) ? 64 : (mean_large <= 128 ? 128 : 256);
         const uint64_t csz = (uint64_t)256 * h->spl, cszw = (uint64_t)256 * h->spl_w;
