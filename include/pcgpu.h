@@ -200,6 +200,10 @@ int pcg_set_narrow_degree(pcg_handle *h, int max_degree);
  * fp32 with an a-priori error bound (tests it cannot make certain are evaluated in fp64:
  * k_level_lds_f); 0 runs the all-fp64 sweep (k_level_lds_t). Results are identical.      */
 int pcg_set_screen_precision(pcg_handle *h, int fp32);
+/* Capacity (tests) of the fp32 sweep's fp64 screen list (default 2^20 per depth). An overflow
+ * makes the level report PCG_ERR_OVERFLOW with the capacity raised; pcg_skeleton /
+ * pcg_pc_skeleton rerun by themselves, level-step drivers rerun the skeleton.              */
+int pcg_set_screen_capacity(pcg_handle *h, int64_t entries);
 /* Number of ranks the level work lists are split over (default 1). The per-depth
  * decomposition sizes its chunks so that each rank's slice still fills its GPU.          */
 int pcg_set_world_size(pcg_handle *h, int world);

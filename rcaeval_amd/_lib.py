@@ -109,6 +109,7 @@ SIGNATURES = [
     ("pcg_set_world_size", I32, [P, ctypes.c_int]),
     ("pcg_set_narrow_degree", I32, [P, ctypes.c_int]),
     ("pcg_set_screen_precision", I32, [P, ctypes.c_int]),
+    ("pcg_set_screen_capacity", I32, [P, ctypes.c_int64]),
     ("pcg_comm_unique_id", I32, [P, I64]),
     ("pcg_comm_init", I32, [P, P, ctypes.c_int, ctypes.c_int]),
     ("pcg_comm_destroy", I32, [P]),

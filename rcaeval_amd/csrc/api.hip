@@ -128,6 +128,12 @@ extern "C" int pcg_set_capacity(pcg_handle *h, int64_t record_capacity, int64_t 
     return PCG_OK;
 }
 
+extern "C" int pcg_set_screen_capacity(pcg_handle *h, int64_t entries) {
+    if (!h || entries < 1) return pcg_fail(h, PCG_ERR_INVALID, "pcg_set_screen_capacity: %lld", (long long)entries);
+    h->scr_cap = entries;
+    return PCG_OK;
+}
+
 extern "C" int pcg_set_record_sample(pcg_handle *h, int64_t modulus, int64_t residue) {
     if (!h || modulus < 0 || (modulus > 1 && (residue < 0 || residue >= modulus)))
         return pcg_fail(h, PCG_ERR_INVALID, "pcg_set_record_sample: modulus %lld residue %lld", (long long)modulus,

@@ -3344,11 +3344,11 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
         // (no host round trip) and raises the overflow status byte if the list overflowed
         a = make_args(h, d, mode == MODE_EXACT);
         if (h->tgroup && use_screen32(h, d)) {   // the fp32 sweep's undecided tests, in fp64
-            // the list length is only known on the device: 1024 blocks cover ~2.6e5 tests at one per
-            // lane (a test is a latency-bound gather + factorisation), the rest stride
-            if (d == 2) hipLaunchKernelGGL(k_screen<2>, dim3(1024), dim3(256), 0, h->stream, a);
-            else if (d == 3) hipLaunchKernelGGL(k_screen<3>, dim3(1024), dim3(256), 0, h->stream, a);
-            else hipLaunchKernelGGL(k_screen<4>, dim3(1024), dim3(256), 0, h->stream, a);
+            // the list length is only known on the device; a grid-stride loop over it (1024 blocks
+            // measured no faster than 256: 40 vs 36 us for 1.3e5 tests)
+            if (d == 2) hipLaunchKernelGGL(k_screen<2>, dim3(256), dim3(256), 0, h->stream, a);
+            else if (d == 3) hipLaunchKernelGGL(k_screen<3>, dim3(256), dim3(256), 0, h->stream, a);
+            else hipLaunchKernelGGL(k_screen<4>, dim3(256), dim3(256), 0, h->stream, a);
         }
         const int m = d + 2;
         const int per = (m * m + 2 * m) * 8;      // one LDS slot per wave

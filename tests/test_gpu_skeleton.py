@@ -107,6 +107,21 @@ def test_screen_precision_masks_match_oracle(eng, n, N, seed, wl, wh, ep, narrow
         assert sum(out.stats["screened"]) == 0
 
 
+def test_screen_list_overflow_reruns(eng):
+    """A screen list too small for the fp32 sweep's undecided tests (config 5, depth <= 3:
+    ~9e4 of them at depth 3) overflows, the level reports it with the capacity raised, and
+    pcg_skeleton reruns: the result equals a run with room to spare."""
+    X = synth.gaussian_sem(2000, 10000, seed=0)
+    C = eng.corr(X)
+    a = eng.skeleton(C, 10000, max_depth=3)
+    assert a.stats["screened"][3] > 1000
+    _lib.check(eng.h, eng.lib.pcg_set_screen_capacity(eng.h, 1000), "pcg_set_screen_capacity")
+    b = eng.skeleton(C, 10000, max_depth=3)
+    assert b.stats["screened"] == a.stats["screened"]
+    assert b.stats["tests"] == a.stats["tests"] and b.stats["indep"] == a.stats["indep"]
+    assert np.array_equal(b.removed_level, a.removed_level)
+
+
 @pytest.mark.parametrize("noise", [1e-2, 1e-4, 1e-6, 1e-7])
 @pytest.mark.parametrize("flags", [0, _lib.PCG_FLAG_FULL_P | _lib.PCG_FLAG_RECORD])
 def test_near_collinear_columns_match_lu_oracle(eng, noise, flags):
