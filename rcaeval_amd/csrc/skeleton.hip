@@ -50,7 +50,7 @@ constexpr int MODE_DECIDE = 0;
 constexpr int MODE_FULLP = 1;
 constexpr int MODE_EXACT = 2;
 // candidates c per lane task in k_level_lds_t, per depth (measured, tools/variant_bench.sh):
-// depth 2 groups of 6 (round 2: 0.314 -> 0.282 ms vs 8, which had been -28 % vs 4); depth 3 groups of 4 (4 waves/SIMD, 8 was +15 %, 6 equal);
+// depth 2 groups of 6 (round 2: 0.314 -> 0.282 ms vs 8, which had been -28 % vs 4); depth 3 groups of 6 (fp32 sweep: 0.715 -> 0.688 ms vs 4; the fp64 form measured 4 ~ 6, 8 +15 %);
 // depth 4 groups of 6 at 3 waves/SIMD (168 VGPRs): fp64 VALU from one wave issues at most every
 // ~8 cycles with a ~50-cycle dependent latency (tools/micro/valu_occ.hip), so a third wave of 6
 // chains beats two waves of 8 (4.03 vs 4.29 ms; groups of 4 at 3 waves 4.46 ms)
@@ -74,7 +74,7 @@ constexpr int MODE_EXACT = 2;
 #define PCG_TG_SPLIT 0   // lane-mask sweep: split the y range around a shared candidate window (spills: slower)
 #endif
 #ifndef PCG_TG3
-#define PCG_TG3 4
+#define PCG_TG3 6
 #endif
 #ifndef PCG_TG4
 #define PCG_TG4 6
