@@ -1828,12 +1828,24 @@ __device__ __forceinline__ double rsq_nr(double x) {
 // 0 dependent, 1 independent, 2 exact path
 template <int DM>
 __device__ int eval_test_global(const LevelArgs &a, int x, int y, const int *Sg) {
+    // every entry is gathered before the factorisation uses any of them (one round of load
+    // latency per test instead of one per Cholesky step)
+    double Cs[DM][DM], Cx[DM], Cy[DM];
+#pragma unroll
+    for (int j = 0; j < DM; ++j) {
+        Cs[j][j] = a.diag[Sg[j]];
+#pragma unroll
+        for (int i = j + 1; i < DM; ++i) Cs[i][j] = a.C[(int64_t)Sg[i] * a.ldc + Sg[j]];
+        Cx[j] = a.C[(int64_t)Sg[j] * a.ldc + x];
+        Cy[j] = a.C[(int64_t)Sg[j] * a.ldc + y];
+    }
+    const double cxy0 = a.C[(int64_t)x * a.ldc + y], dx = a.diag[x], dy = a.diag[y];
     double L[DM][DM], rinv[DM], u[DM], v[DM];
     double gmin = 1.0;
     bool ok = true;
 #pragma unroll
     for (int j = 0; j < DM; ++j) {
-        double s = a.diag[Sg[j]];
+        double s = Cs[j][j];
 #pragma unroll
         for (int q = 0; q < j; ++q) s -= L[j][q] * L[j][q];
         ok = ok && (s > 0.0);
@@ -1842,7 +1854,7 @@ __device__ int eval_test_global(const LevelArgs &a, int x, int y, const int *Sg)
         rinv[j] = 1.0 / L[j][j];
 #pragma unroll
         for (int i = j + 1; i < DM; ++i) {
-            double t = a.C[(int64_t)Sg[i] * a.ldc + Sg[j]];
+            double t = Cs[i][j];
 #pragma unroll
             for (int q = 0; q < j; ++q) t -= L[i][q] * L[j][q];
             L[i][j] = t * rinv[j];
@@ -1851,7 +1863,7 @@ __device__ int eval_test_global(const LevelArgs &a, int x, int y, const int *Sg)
     double uu = 0.0, vv = 0.0, uv = 0.0;
 #pragma unroll
     for (int i = 0; i < DM; ++i) {
-        double tu = a.C[(int64_t)Sg[i] * a.ldc + x], tv = a.C[(int64_t)Sg[i] * a.ldc + y];
+        double tu = Cx[i], tv = Cy[i];
 #pragma unroll
         for (int q = 0; q < i; ++q) {
             tu -= L[i][q] * u[q];
@@ -1864,8 +1876,7 @@ __device__ int eval_test_global(const LevelArgs &a, int x, int y, const int *Sg)
         uv += u[i] * v[i];
     }
     if (!ok) return 2;
-    return decide<MODE_DECIDE>(a, a.C[(int64_t)x * a.ldc + y] - uv, a.diag[x] - uu, a.diag[y] - vv, a.tau / gmin,
-                               nullptr);
+    return decide<MODE_DECIDE>(a, cxy0 - uv, dx - uu, dy - vv, a.tau / gmin, nullptr);
 }
 
 template <int DM, bool WIDE>
