@@ -252,23 +252,40 @@ __device__ __forceinline__ int decide(const LevelArgs &a, double cxy, double cxx
 
 // ---------------------------------------------------------------------------------------
 // utility kernels
-__global__ void k_init_adj(uint64_t *adj, int n, int W) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)n * W) return;
-    const int x = (int)(i / W), w = (int)(i % W);
-    const int base = w * 64;
-    const int rem = n - base;
-    uint64_t m = rem >= 64 ? ~0ull : ((1ull << rem) - 1ull);
-    if (x >= base && x < base + 64) m &= ~(1ull << (x - base));
-    adj[i] = m;
+// byte fill by a grid-stride loop: unaligned head and tail bytewise, the body in 16-byte stores
+__device__ __forceinline__ void fill_bytes(uint8_t *p, int64_t bytes, uint8_t v, int64_t tid, int64_t nth) {
+    const int64_t head = std::min<int64_t>(bytes, (int64_t)((16 - ((uintptr_t)p & 15)) & 15));
+    const int64_t body = (bytes - head) / 16;
+    if (tid < head) p[tid] = v;
+    uint4 *q = reinterpret_cast<uint4 *>(p + head);
+    const unsigned w = 0x01010101u * v;
+    for (int64_t i = tid; i < body; i += nth) q[i] = make_uint4(w, w, w, w);
+    const int64_t t0 = head + body * 16;
+    if (tid < bytes - t0) p[t0 + tid] = v;
 }
 
-__global__ void k_diag(const double *C, int64_t ldc, int n, double *diag, int32_t *deg) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) {
-        diag[i] = C[(int64_t)i * ldc + i];
-        deg[i] = n - 1;                  // the complete graph k_init_adj builds
+// the skeleton's initial state in one launch: complete-graph adjacency bits, diag(C), degrees
+// n - 1, removed_level = -1, removal flags + status bytes = 0, export row counter = 0
+__global__ __launch_bounds__(256) void k_init(uint64_t *adj, int n, int W, const double *C, int64_t ldc, double *diag,
+                                              int32_t *deg, int8_t *rl, uint8_t *rm, int64_t rm_bytes,
+                                              unsigned long long *exp_ctr) {
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t nth = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = tid; i < (int64_t)n * W; i += nth) {
+        const int x = (int)(i / W), w = (int)(i % W);
+        const int base = w * 64;
+        const int rem = n - base;
+        uint64_t m = rem >= 64 ? ~0ull : ((1ull << rem) - 1ull);
+        if (x >= base && x < base + 64) m &= ~(1ull << (x - base));
+        adj[i] = m;
     }
+    for (int64_t i = tid; i < n; i += nth) {
+        diag[i] = C[i * ldc + i];
+        deg[i] = n - 1;
+    }
+    fill_bytes(reinterpret_cast<uint8_t *>(rl), (int64_t)n * n, 0xFF, tid, nth);
+    fill_bytes(rm, rm_bytes, 0, tid, nth);
+    if (tid == 0) *exp_ctr = 0;
 }
 
 constexpr int EXPORT_GROUP = 8;     // union rows in flight per wave in the sepset export
@@ -2949,15 +2966,11 @@ extern "C" int pcg_skeleton_init(pcg_handle *h, const double *C, int64_t n, int6
                                   hipMemcpyHostToDevice, h->stream));
         h->binom_n = (int)n;
     }
-    const int64_t nw = n * W;
-    hipLaunchKernelGGL(k_init_adj, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, h->stream,
-                       (uint64_t *)h->adj.p, (int)n, W);
-    hipLaunchKernelGGL(k_diag, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream, C, ldc, (int)n,
-                       (double *)h->diag.p, (int32_t *)h->deg.p);
-    PCG_HIP(h, hipMemsetAsync(removed_level, 0xFF, (size_t)n * n, h->stream));
+    hipLaunchKernelGGL(k_init, dim3(1024), dim3(256), 0, h->stream, (uint64_t *)h->adj.p, (int)n, W, C, ldc,
+                       (double *)h->diag.p, (int32_t *)h->deg.p, removed_level,
+                       h->rm_ext ? h->rm_ext : (uint8_t *)h->rm.p, (int64_t)n * n + PCG_RM_STATUS,
+                       (unsigned long long *)h->exp_ctr.p);
     PCG_HIP(h, hipGetLastError());
-    PCG_HIP(h, hipMemsetAsync(h->rm_ext ? (void *)h->rm_ext : h->rm.p, 0, (size_t)n * n + PCG_RM_STATUS, h->stream));
-    PCG_HIP(h, hipMemsetAsync(h->exp_ctr.p, 0, sizeof(unsigned long long), h->stream));
     int rc = graph_launch(h);            // also clears the counters
     if (!rc) rc = level_wait(h);
     if (rc) return rc;
