@@ -3068,7 +3068,10 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
         }
         // ~4096 LDS-resident blocks per depth and rank; each lane walks spl units. The wide class
         // (a few nodes) aims at ~512 blocks so its nodes are spread over the chip
-        double nb_target = getenv("PCG_NB") ? atof(getenv("PCG_NB")) : 4096.0;   // A/B knobs
+        // narrow-class block target: ~4096 blocks per depth and rank, 16384 at depth 4, whose long
+        // per-node task lists otherwise leave a tail (measured 2.53 -> 2.40 ms; depth 3 is best at
+        // 4096); PCG_NB / PCG_NB<d> override (A/B knobs)
+        double nb_target = getenv("PCG_NB") ? atof(getenv("PCG_NB")) : (depth == 4 ? 16384.0 : 4096.0);
         {
             char nm[16];
             snprintf(nm, sizeof nm, "PCG_NB%d", depth);
