@@ -84,6 +84,15 @@ typedef struct {                       /* one unique CI test (PCG_FLAG_RECORD / 
     double p;                          /* Fisher-z p-value                                  */
 } pcg_record;
 
+/* ---- ABI identity ------------------------------------------------------------------
+ * Bumped whenever a struct above changes layout or an entry point changes signature.
+ * Round 3: pcg_stats gained `screened` (v2 had no such field).                         */
+#define PCG_ABI_VERSION 3
+/* Sizes of the structs this library writes through caller pointers, and its ABI version;
+ * a binding checks them against its own declarations before the first call (host only, no
+ * GPU needed). Any out pointer may be NULL.                                             */
+int pcg_abi_info(int64_t *stats_bytes, int64_t *record_bytes, int32_t *version);
+
 /* ---- lifetime --------------------------------------------------------------------- */
 int pcg_create(int device, pcg_handle **out);
 int pcg_destroy(pcg_handle *h);

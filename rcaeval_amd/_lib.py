@@ -27,6 +27,7 @@ PCG_FLAG_RECORD = 0x2
 PCG_FLAG_EXACT_ALL = 0x4
 
 PCG_MAX_LEVELS = 32
+PCG_ABI_VERSION = 3         # include/pcgpu.h; checked against the library by load()
 PCG_RM_STATUS = 64          # status bytes after the n*n removal flags (pcgpu.h)
 PCG_MAX_DEPTH = 12
 PCG_MAX_LEVEL_DEPTH = 30
@@ -77,6 +78,7 @@ class PcgRecord(ctypes.Structure):
 
 # (name, restype, argtypes) — exactly the exports of include/pcgpu.h
 SIGNATURES = [
+    ("pcg_abi_info", I32, [ctypes.POINTER(I64), ctypes.POINTER(I64), ctypes.POINTER(I32)]),
     ("pcg_create", I32, [ctypes.c_int, ctypes.POINTER(P)]),
     ("pcg_destroy", I32, [P]),
     ("pcg_last_error", ctypes.c_char_p, [P]),
@@ -146,8 +148,30 @@ def load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    check_abi(lib)
     _lib = lib
     return lib
+
+
+def abi_info(lib) -> tuple:
+    """(sizeof(pcg_stats), sizeof(pcg_record), PCG_ABI_VERSION) as the library was built."""
+    sb, rb, ver = I64(), I64(), I32()
+    lib.pcg_abi_info(ctypes.byref(sb), ctypes.byref(rb), ctypes.byref(ver))
+    return sb.value, rb.value, ver.value
+
+
+def check_abi(lib, stats_cls=None, record_cls=None) -> None:
+    """Refuse a library whose struct layouts or ABI version differ from these bindings (a
+    stale .so, or a header change the ctypes structs did not follow)."""
+    stats_cls = stats_cls or PcgStats
+    record_cls = record_cls or PcgRecord
+    sb, rb, ver = abi_info(lib)
+    mine = (ctypes.sizeof(stats_cls), ctypes.sizeof(record_cls), PCG_ABI_VERSION)
+    if (sb, rb, ver) != mine:
+        raise EngineUnavailable(
+            f"{LIB_PATH}: ABI mismatch (library sizeof(pcg_stats)={sb}, sizeof(pcg_record)={rb}, "
+            f"version {ver}; bindings {mine[0]}, {mine[1]}, version {mine[2]}): rebuild the library "
+            "or update rcaeval_amd/_lib.py with include/pcgpu.h")
 
 
 class PcgError(RuntimeError):

@@ -52,6 +52,13 @@ bool pcg_ensure_pinned(pcg_handle *h, PinBuf &b, size_t bytes) {
     return true;
 }
 
+extern "C" int pcg_abi_info(int64_t *stats_bytes, int64_t *record_bytes, int32_t *version) {
+    if (stats_bytes) *stats_bytes = (int64_t)sizeof(pcg_stats);
+    if (record_bytes) *record_bytes = (int64_t)sizeof(pcg_record);
+    if (version) *version = PCG_ABI_VERSION;
+    return PCG_OK;
+}
+
 extern "C" int pcg_create(int device, pcg_handle **out) {
     if (!out) return PCG_ERR_INVALID;
     *out = nullptr;

@@ -72,6 +72,29 @@ int need_comm(pcg_handle *h) {
     return PCG_OK;
 }
 
+// Every rank reaches every collective: a rank that fails locally (an allocation, a launch)
+// still joins with a "failed" status, and all ranks leave with the same verdict — the failing
+// rank its own error, its peers PCG_ERR_PEER — so no rank waits in a collective for a peer that
+// returned early. Inside the level loop the status rides in the packed barrier word; outside it
+// agree() all-reduces one status int (MAX) first.
+//   returns 0 (every rank ok), 1 (some rank failed) or a negative RCCL / HIP error
+int agree(pcg_handle *h, int failed) {
+    int32_t v = failed ? 1 : 0;
+    int32_t *d = (int32_t *)h->comm_status.p;
+    PCG_HIP(h, hipMemcpyAsync(d, &v, sizeof(v), hipMemcpyHostToDevice, h->stream));
+    PCG_NCCL(h, rccl().all_reduce(d, d, 1, ncclInt32, ncclMax, (ncclComm_t)h->comm, h->stream));
+    PCG_HIP(h, hipMemcpyAsync(&v, d, sizeof(v), hipMemcpyDeviceToHost, h->stream));
+    PCG_HIP(h, hipStreamSynchronize(h->stream));
+    return v;
+}
+
+// the verdict of agree() as this rank's return code
+int agreed_failure(pcg_handle *h, int local, int g, const char *what) {
+    if (g < 0) return g;
+    if (local) return local;
+    return pcg_fail(h, PCG_ERR_PEER, "%s: another rank failed", what);
+}
+
 // [x | y << 32, W union words] per exported row, zero-padded to `rows_out` rows
 __global__ void k_pack_rows(const int32_t *xy, const uint64_t *bits, int64_t rows, int W, int64_t rows_out,
                             int64_t *out) {
@@ -105,15 +128,22 @@ __global__ void k_unpack_rows(const int64_t *in, int64_t rows, int W, int32_t *x
 int sharded_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N, double alpha,
                  int max_depth, int flags, int8_t *removed_level) {
     int64_t P = 0;
-    int rc = pcg_level_packed_words(n, &P);
-    if (rc) return pcg_fail(h, PCG_ERR_INVALID, "n = %lld", (long long)n);
+    if (pcg_level_packed_words(n, &P)) return pcg_fail(h, PCG_ERR_INVALID, "n = %lld", (long long)n);
     const int world = h->comm_world;
+    // set-up (buffers, skeleton init) agreed by every rank before the first level collective
+    int local = PCG_OK;
     if (!pcg_ensure(h, h->comm_packed, sizeof(uint64_t) * (size_t)P) ||
         !pcg_ensure(h, h->comm_gathered, sizeof(uint64_t) * (size_t)P * world))
-        return pcg_fail(h, PCG_ERR_OOM, "packed removal flags");
-    rc = pcg_set_removal_buffer(h, nullptr, 0);   // the handle's own flags
-    if (!rc) rc = pcg_set_world_size(h, world);
-    if (!rc) rc = pcg_skeleton_init(h, C, n, ldc, N, alpha, flags, removed_level);
+        local = pcg_fail(h, PCG_ERR_OOM, "packed removal flags");
+    if (!local) local = pcg_set_removal_buffer(h, nullptr, 0);   // the handle's own flags
+    if (!local) local = pcg_set_world_size(h, world);
+    if (!local) local = pcg_skeleton_init(h, C, n, ldc, N, alpha, flags, removed_level);
+    int g = agree(h, local != 0);
+    if (g) {
+        pcg_set_world_size(h, 1);
+        return agreed_failure(h, local, g, "skeleton set-up");
+    }
+    int rc = PCG_OK;
     ncclComm_t comm = (ncclComm_t)h->comm;
     uint64_t *packed = (uint64_t *)h->comm_packed.p, *gathered = (uint64_t *)h->comm_gathered.p;
     for (int depth = 0; !rc; ++depth) {
@@ -122,14 +152,22 @@ int sharded_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t
         // begin is deterministic over the replicated adjacency ("done" agrees on every rank);
         // a local failure of begin / split / run still joins the all-gather below, flagged in
         // the status word, so no peer waits in the collective for this rank
-        int local = pcg_level_begin(h, depth, &total, nullptr, nullptr);
+        local = pcg_level_begin(h, depth, &total, nullptr, nullptr);
         if (local == 1) break;
         if (!local) local = pcg_level_split(h, h->comm_rank, world, &lo, &hi);
         if (!local) local = pcg_level_run(h, lo, hi);
         const std::string local_err = local ? h->err : std::string();
         rc = pcg_level_pack(h, packed, local != 0);
-        if (rc) break;   // a launch failure here leaves nothing sane to send
+        if (rc) {
+            // the pack did not launch: send a bare "failed" status word (no flags) instead, so the
+            // peers still get this depth's collective and leave with PCG_ERR_PEER
+            static const uint64_t failed_word = 1ull << 24;
+            (void)hipMemsetAsync(packed, 0, sizeof(uint64_t) * (size_t)(P - 1), h->stream);
+            (void)hipMemcpyAsync(packed + (P - 1), &failed_word, sizeof(failed_word), hipMemcpyHostToDevice,
+                                 h->stream);
+        }
         const ncclResult_t r = rccl().all_gather(packed, gathered, (size_t)P, ncclUint64, comm, h->stream);
+        if (rc) break;
         if (r != ncclSuccess) {
             rc = pcg_fail(h, PCG_ERR_RCCL, "ncclAllGather(packed removal flags) failed: %s", rccl().error_string(r));
             break;
@@ -160,7 +198,7 @@ int reduce_stats(pcg_handle *h) {
         v[3 * L + d] = h->st.near_alpha[d];
         v[4 * L + d] = h->st.screened[d];
     }
-    if (!pcg_ensure(h, h->comm_small, sizeof(int64_t) * v.size())) return pcg_fail(h, PCG_ERR_OOM, "stats");
+    // comm_small holds 5 * PCG_MAX_LEVELS int64 since pcg_comm_init: no allocation between collectives
     PCG_HIP(h, hipMemcpyAsync(h->comm_small.p, v.data(), sizeof(int64_t) * v.size(), hipMemcpyHostToDevice,
                               h->stream));
     PCG_NCCL(h, rccl().all_reduce(h->comm_small.p, h->comm_small.p, v.size(), ncclInt64, ncclSum,
@@ -178,34 +216,44 @@ int reduce_stats(pcg_handle *h) {
     return PCG_OK;
 }
 
-// every rank's exported sepset rows -> the handle's export buffers on every rank
+// every rank's exported sepset rows -> the handle's export buffers on every rank. The row
+// counts travel with a failure marker (-1), and the row-buffer sizes are agreed before the rows
+// move, so a rank that fails here takes its peers out of the gather with it.
 int gather_sepsets(pcg_handle *h) {
     const int world = h->comm_world, W = h->W;
     ncclComm_t comm = (ncclComm_t)h->comm;
-    int rc0 = export_sync(h);
-    if (rc0) return rc0;
-    if (!pcg_ensure(h, h->comm_small, sizeof(int64_t) * (size_t)(world + 1)))
-        return pcg_fail(h, PCG_ERR_OOM, "row counts");
+    int local = export_sync(h);
+    const std::string sync_err = local ? h->err : std::string();
     int64_t *cnt_d = (int64_t *)h->comm_small.p;
-    const int64_t mine = h->export_rows;
+    const int64_t mine = local ? -1 : h->export_rows;
     PCG_HIP(h, hipMemcpyAsync(cnt_d + world, &mine, sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
     PCG_NCCL(h, rccl().all_gather(cnt_d + world, cnt_d, 1, ncclInt64, comm, h->stream));
     std::vector<int64_t> cnt(world);
     PCG_HIP(h, hipMemcpyAsync(cnt.data(), cnt_d, sizeof(int64_t) * world, hipMemcpyDeviceToHost, h->stream));
     PCG_HIP(h, hipStreamSynchronize(h->stream));
     int64_t mx = 1, total = 0;
+    bool peer_failed = false;
     for (int64_t c : cnt) {
+        peer_failed = peer_failed || c < 0;
         mx = std::max(mx, c);
-        total += c;
+        total += std::max<int64_t>(c, 0);
     }
+    if (local) {
+        h->err = sync_err;
+        return local;
+    }
+    if (peer_failed) return pcg_fail(h, PCG_ERR_PEER, "sepset gather: another rank failed");
     const int64_t per = mx * (W + 1);
     if (!pcg_ensure(h, h->comm_packed, sizeof(int64_t) * (size_t)per) ||
         !pcg_ensure(h, h->comm_gathered, sizeof(int64_t) * (size_t)per * world))
-        return pcg_fail(h, PCG_ERR_OOM, "sepset row gather (%lld rows x %d words)", (long long)mx, W + 1);
+        local = pcg_fail(h, PCG_ERR_OOM, "sepset row gather (%lld rows x %d words)", (long long)mx, W + 1);
+    const int g = agree(h, local != 0);
+    if (g) return agreed_failure(h, local, g, "sepset gather");
     hipLaunchKernelGGL(k_pack_rows, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, h->stream,
                        (const int32_t *)h->export_xy.p, (const uint64_t *)h->exportbuf.p, mine, W, mx,
                        (int64_t *)h->comm_packed.p);
     PCG_NCCL(h, rccl().all_gather(h->comm_packed.p, h->comm_gathered.p, (size_t)per, ncclInt64, comm, h->stream));
+    // the last collective of the call: the export buffers grow (their rows are packed already)
     const int64_t cap = std::max<int64_t>(total, 1);
     if (!pcg_ensure(h, h->exportbuf, sizeof(uint64_t) * (size_t)cap * W) ||
         !pcg_ensure(h, h->export_xy, sizeof(int32_t) * 2 * (size_t)cap))
@@ -232,7 +280,7 @@ void pcg_comm_release(pcg_handle *h) {
     if (!h) return;
     if (h->comm && rccl().ok) rccl().comm_destroy((ncclComm_t)h->comm);
     h->comm = nullptr;
-    for (DevBuf *b : {&h->comm_rm, &h->comm_packed, &h->comm_gathered, &h->comm_small})
+    for (DevBuf *b : {&h->comm_rm, &h->comm_packed, &h->comm_gathered, &h->comm_small, &h->comm_status})
         if (b->p) {
             (void)hipFree(b->p);
             b->p = nullptr;
@@ -257,8 +305,17 @@ extern "C" int pcg_comm_init(pcg_handle *h, const void *unique_id, int rank, int
     PCG_HIP(h, hipSetDevice(h->device));
     ncclUniqueId id;
     std::memcpy(&id, unique_id, sizeof(id));
+    // the status int of agree() and the small stats / row-count buffer exist before the first
+    // collective, so no allocation can fail between two collectives later. A failure here still
+    // joins the communicator's creation (its peers are blocked in it) and then leaves it.
+    const bool bufs = pcg_ensure(h, h->comm_status, 64) &&
+                      pcg_ensure(h, h->comm_small, sizeof(int64_t) * (size_t)std::max(5 * PCG_MAX_LEVELS, world + 1));
     ncclComm_t comm = nullptr;
     PCG_NCCL(h, rccl().comm_init_rank(&comm, world, id, rank));
+    if (!bufs) {
+        rccl().comm_destroy(comm);
+        return pcg_fail(h, PCG_ERR_OOM, "pcg_comm_init: status buffers");
+    }
     h->comm = comm;
     h->comm_rank = rank;
     h->comm_world = world;
@@ -279,15 +336,29 @@ extern "C" int pcg_corr_sharded(pcg_handle *h, const double *X, int64_t N, int64
     if (rc) return rc;
     int64_t rows = 0;
     rc = pcg_corr_shard_rows(n, h->comm_world, &rows);
-    if (rc) return pcg_fail(h, rc, "pcg_corr_shard_rows");
+    if (rc) return pcg_fail(h, rc, "pcg_corr_shard_rows");   // a function of (n, world): every rank agrees
     const size_t per = (size_t)rows * (size_t)n;
-    if (!pcg_ensure(h, h->comm_packed, sizeof(double) * std::max<size_t>(per, 1)) ||
-        !pcg_ensure(h, h->comm_gathered, sizeof(double) * std::max<size_t>(per * h->comm_world, 1)))
-        return pcg_fail(h, PCG_ERR_OOM, "sharded K1 buffers");
-    rc = pcg_corr_shard(h, X, N, n, ldx, h->comm_rank, h->comm_world, (double *)h->comm_packed.p);
-    if (rc) return rc;
+    // buffer growth is the same decision on every rank (same n, world, call history); when it
+    // happens, its outcome is agreed before the all-gather
+    const size_t b1 = sizeof(double) * std::max<size_t>(per, 1);
+    const size_t b2 = sizeof(double) * std::max<size_t>(per * h->comm_world, 1);
+    if (h->comm_packed.bytes < b1 || h->comm_gathered.bytes < b2) {
+        int local = PCG_OK;
+        if (!pcg_ensure(h, h->comm_packed, b1) || !pcg_ensure(h, h->comm_gathered, b2))
+            local = pcg_fail(h, PCG_ERR_OOM, "sharded K1 buffers");
+        const int g = agree(h, local != 0);
+        if (g) return agreed_failure(h, local, g, "sharded K1");
+    }
+    const int local = pcg_corr_shard(h, X, N, n, ldx, h->comm_rank, h->comm_world, (double *)h->comm_packed.p);
+    const std::string local_err = local ? h->err : std::string();
+    // joined even after a local launch failure (the peers' C is then garbage, and so is ours:
+    // the failing rank reports it; the argument checks of pcg_corr_shard agree on every rank)
     PCG_NCCL(h, rccl().all_gather(h->comm_packed.p, h->comm_gathered.p, per, ncclFloat64, (ncclComm_t)h->comm,
                                   h->stream));
+    if (local) {
+        h->err = local_err;
+        return local;
+    }
     return pcg_corr_shard_finish(h, (const double *)h->comm_gathered.p, N, n, h->comm_world, C, ldc);
 }
 

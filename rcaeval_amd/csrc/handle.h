@@ -137,6 +137,7 @@ struct pcg_handle {
     void *comm = nullptr;
     int comm_rank = 0, comm_world = 1;
     DevBuf comm_rm, comm_packed, comm_gathered, comm_small;
+    DevBuf comm_status;   // agree(): one int32 all-reduced with MAX, allocated before the communicator
 };
 
 void pcg_comm_release(pcg_handle *h);      // comm.hip: destroy the communicator, free its buffers

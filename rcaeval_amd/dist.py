@@ -26,6 +26,41 @@ from . import _lib
 from ._lib import PcgStats, check
 
 
+FAILED_WORD = 1 << 24    # barrier.hip k_pack_status: byte 3 of the status word = "this rank failed"
+
+
+def agree(failed: bool, device="cpu", group=None) -> bool:
+    """True when ANY rank of ``group`` reports failure (one all-reduce MAX of a status int).
+    Every rank calls it at the same point, so a rank that failed locally outside the level
+    loop (set-up, result collection) takes its peers out with it instead of leaving them
+    blocked in the next collective."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([1 if failed else 0], dtype=torch.int32, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return bool(t.item())
+
+
+def raise_agreed(local_err, what: str):
+    """Re-raise this rank's own error, or PCG_ERR_PEER for a peer's."""
+    if local_err is not None:
+        raise local_err
+    raise _lib.PcgError(_lib.PCG_ERR_PEER, f"{what}: another rank failed")
+
+
+def agreed_backend(factory, device="cpu", group=None):
+    """Build this rank's level backend, then agree on every rank's success before the first
+    level collective (a rank whose set-up fails, e.g. OOM, raises; its peers raise PEER)."""
+    backend, err = None, None
+    try:
+        backend = factory()
+    except Exception as e:   # noqa: BLE001 - must reach the agreement below
+        err = e
+    if agree(err is not None, device=device, group=group):
+        raise_agreed(err, "skeleton set-up")
+    return backend
+
+
 def split_by_work(prefix: np.ndarray, rank: int, world: int) -> tuple[int, int]:
     """Contiguous chunk range of ``rank`` so that every rank gets ~1/world of the work.
 
@@ -100,6 +135,12 @@ class GpuLevelBackend:
               "pcg_level_pack")
         return self.packed
 
+    def pack_failed(self):
+        """A bare "this rank failed" word (no flags), for when pack itself failed."""
+        self.packed.zero_()
+        self.packed[-1] = FAILED_WORD
+        return self.packed
+
     def merge(self, gathered, world: int):
         """OR of every rank's packed words (rank-major) back into the removal flags."""
         g = gathered.contiguous()
@@ -144,7 +185,12 @@ def run_sharded_levels(backend, rank: int, world: int, max_depth: int = -1, grou
         except Exception as e:   # noqa: BLE001 - any local failure must still reach the collective
             local_err = e
         t2 = clock()
-        gathered = _gather_tensor(backend.pack(local_err is not None), group=group)
+        try:
+            packed = backend.pack(local_err is not None)
+        except Exception as e:   # noqa: BLE001 - join the collective with a bare failed word
+            local_err = local_err or e
+            packed = backend.pack_failed()
+        gathered = _gather_tensor(packed, group=group)
         backend.merge(gathered, world)
         t3 = clock()
         if local_err is not None:
@@ -172,15 +218,20 @@ def _gather_tensor(t, group=None):
     return torch.cat(parts)
 
 
-def _allgather_rows(xy, bits, group=None):
+def _allgather_rows(xy, bits, group=None, failed=None, device=None):
     """All-gather variable-length (xy, bits) device tensors from every rank: one count
     exchange (one host sync), then ONE all-gather of rows packed as [x | y << 32, bits...]
-    (int64, padded to the longest rank)."""
+    (int64, padded to the longest rank). ``failed`` (this rank's exception, xy/bits unused)
+    travels as a count of -1: every rank then raises (its own error or PCG_ERR_PEER) before
+    the rows move."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    cnt = torch.tensor([xy.shape[0]], dtype=torch.int64, device=xy.device)
+    dev = device if failed is not None else xy.device
+    cnt = torch.tensor([-1 if failed is not None else xy.shape[0]], dtype=torch.int64, device=dev)
     counts = _gather_tensor(cnt, group=group).cpu().tolist()
+    if failed is not None or min(counts) < 0:
+        raise_agreed(failed, "sepset gather")
     mx = max(max(counts), 1)
     W = bits.shape[1]
     k = xy.shape[0]
@@ -236,9 +287,10 @@ def sharded_skeleton(eng, C, N: int, alpha: float = 0.05, max_depth: int = -1, f
 
     import torch.distributed as dist
     rank, world = dist.get_rank(group), dist.get_world_size(group)
+    cdev = eng.device if dist.get_backend(group) == "nccl" else "cpu"
     for attempt in range(6):
         t0 = time.perf_counter()
-        backend = GpuLevelBackend(eng, C, N, alpha, flags, world)
+        backend = agreed_backend(lambda: GpuLevelBackend(eng, C, N, alpha, flags, world), device=cdev, group=group)
         if trace is not None:
             trace.append(("init", -1, time.perf_counter() - t0))
         try:
@@ -251,8 +303,13 @@ def sharded_skeleton(eng, C, N: int, alpha: float = 0.05, max_depth: int = -1, f
                 raise
             eng.lib.pcg_set_world_size(eng.h, 1)
     t0 = time.perf_counter()
-    out = backend.finish()
-    xy, bits = _allgather_rows(out.sep_xy_dev, out.sep_bits_dev, group=group)
+    out, err = None, None
+    try:
+        out = backend.finish()
+    except Exception as e:   # noqa: BLE001 - carried through the row-count exchange
+        err = e
+    xy, bits = _allgather_rows(out.sep_xy_dev if out else None, out.sep_bits_dev if out else None, group=group,
+                               failed=err, device=cdev)
     out.sep_xy_dev, out.sep_bits_dev = xy, bits
     out._host.clear()
     out.stats = _allreduce_stats(out.stats, eng.device, group=group)
@@ -287,6 +344,6 @@ def native_sharded_skeleton(eng, C, N: int, alpha: float = 0.05, max_depth: int 
     return eng.skeleton_sharded(C, N, alpha=alpha, max_depth=max_depth, flags=flags)
 
 
-__all__ = ["split_by_work", "run_sharded_levels", "sharded_skeleton", "sharded_corr", "GpuLevelBackend",
+__all__ = ["agree", "agreed_backend", "split_by_work", "run_sharded_levels", "sharded_skeleton", "sharded_corr", "GpuLevelBackend",
            "native_comm", "native_sharded_corr", "native_sharded_skeleton"]
 _ = _lib

@@ -1,18 +1,21 @@
 """RCA method plug-ins on the MI355X engine (mirror of ``RCAEval/e2e``).
 
 ``rca`` mirrors the reference wrapper (``RCAEval/e2e/__init__.py:21-31``): an exception
-raised by the method returns the dummy ranking ``preprocess(data, dataset).columns`` — engine
-run-time errors (``PcgError``: an overflowed list, a HIP error) included, with a warning, so an
-RQ2 run records dummy ranks for that case like the reference would. Only ``EngineUnavailable``
-(no GPU, library missing) propagates: there is no CPU path to degrade to, and a run without the
-engine must fail loudly rather than score every case with dummy ranks.
+raised by the method returns the dummy ranking ``preprocess(data, dataset).columns``. That
+covers what the reference's methods raise on their data — ``ValueError`` from a singular
+sub-matrix or a math domain error (which the engine raises as ``ValueError`` too), pandas /
+numpy errors — and the one data-driven engine outcome, a list overflow that survived the
+engine's own reruns (``PcgError`` PCG_ERR_OVERFLOW, with a warning). Engine FAULTS propagate:
+``EngineUnavailable`` (no GPU, library missing) and ``PcgError`` with PCG_ERR_INVALID / OOM /
+HIP / RCCL / PEER. A sticky device fault or an OOM would otherwise score that case and every
+later case of an RQ2 run as dummy rankings, silently corrupting the benchmark.
 """
 from __future__ import annotations
 
 import functools
 import warnings
 
-from .._lib import EngineUnavailable, PcgError
+from .._lib import PCG_ERR_OVERFLOW, EngineUnavailable, PcgError
 from ..io.time_series import preprocess
 
 
@@ -24,13 +27,21 @@ def rca(func):
             return func(*args, **kwargs)
         except EngineUnavailable:
             raise
-        except Exception as e:
-            if isinstance(e, PcgError):
-                warnings.warn(f"{func.__name__}: engine error, dummy ranks returned: {e}")
-            data = preprocess(data=args[0], dataset=kwargs.get("dataset"), dk_select_useful=False)
-            names = data.columns.to_list()
-            return {"adj": [], "node_names": names, "ranks": names}
+        except PcgError as e:
+            if e.code != PCG_ERR_OVERFLOW:
+                raise                       # an engine fault, not an outcome of this case's data
+            warnings.warn(f"{func.__name__}: engine error, dummy ranks returned: {e}")
+            return _dummy(args, kwargs)
+        except Exception:
+            return _dummy(args, kwargs)
     return wrapper
+
+
+def _dummy(args, kwargs):
+    """The reference's fallback ranking: the preprocessed column names."""
+    data = preprocess(data=args[0], dataset=kwargs.get("dataset"), dk_select_useful=False)
+    names = data.columns.to_list()
+    return {"adj": [], "node_names": names, "ranks": names}
 
 
 from .circa import circa  # noqa: E402

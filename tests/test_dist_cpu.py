@@ -110,6 +110,11 @@ class OracleLevelBackend:
         rm |= rm.T
         self.rm.copy_(__import__("torch").from_numpy(rm.reshape(-1).astype(np.uint8)))
 
+    def pack_failed(self):
+        import torch
+        iu = np.triu_indices(self.n, 1)
+        return torch.from_numpy(np.concatenate([np.zeros((len(iu[0]) + 7) // 8, np.uint8), [8]]).astype(np.uint8))
+
     def end(self):
         from rcaeval_amd import _lib
         if self.status & 8:
@@ -131,6 +136,20 @@ class FailingBackend(OracleLevelBackend):
         if self.fail and self.depth == self.fail_depth:
             raise MemoryError("injected local failure")
         super().run(lo, hi)
+
+
+class FailingPackBackend(OracleLevelBackend):
+    """Raises inside pack() at one depth on one rank: the rank must still join the gather."""
+
+    def __init__(self, C, N, fail_rank, rank, fail_depth=1):
+        super().__init__(C, N)
+        self.fail = rank == fail_rank
+        self.fail_depth = fail_depth
+
+    def pack(self, local_error):
+        if self.fail and self.depth == self.fail_depth:
+            raise RuntimeError("injected pack failure")
+        return super().pack(local_error)
 
 
 def _worker(rank, world, port, C, N, q):
@@ -227,6 +246,64 @@ def test_local_failure_reaches_every_rank_without_hanging(world):
         kind, depth = res[r]
         assert kind == ("own" if r == 1 else "peer"), res
         assert depth == 1
+
+
+def _setup_fail_worker(rank, world, port, C, N, mode, q):
+    """mode 'init': rank 1's backend constructor fails (OOM-like); 'pack': rank 1's pack fails
+    at depth 1; 'finish': rank 1 fails collecting its result before the sepset-row gather."""
+    import torch.distributed as dist
+    from rcaeval_amd import _lib
+    from rcaeval_amd.dist import _allgather_rows, agreed_backend, run_sharded_levels
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = ("ok", -1)
+    try:
+        def factory():
+            if mode == "init" and rank == 1:
+                raise MemoryError("injected set-up failure")
+            if mode == "pack":
+                return FailingPackBackend(C, N, fail_rank=1, rank=rank)
+            return OracleLevelBackend(C, N)
+        be = agreed_backend(factory)
+        run_sharded_levels(be, rank, world)
+        if mode == "finish":
+            import torch
+            xy = torch.zeros((0, 2), dtype=torch.int32)
+            bits = torch.zeros((0, 1), dtype=torch.int64)
+            err = RuntimeError("injected finish failure") if rank == 1 else None
+            _allgather_rows(xy, bits, failed=err, device="cpu")
+        out = ("ok", be.depth)
+    except (MemoryError, RuntimeError) as e:
+        if isinstance(e, _lib.PcgError):
+            out = ("peer" if e.code == _lib.PCG_ERR_PEER else "other", -1)
+        else:
+            out = ("own", -1)
+    dist.destroy_process_group()
+    q.put((rank, out))
+
+
+@pytest.mark.parametrize("mode", ["init", "pack", "finish"])
+def test_failures_outside_run_reach_every_rank_without_hanging(mode):
+    """Set-up, pack and result-collection failures on one rank: that rank raises its own error,
+    every peer raises PCG_ERR_PEER, and no rank is left in a collective (world 3)."""
+    import multiprocessing as mp
+    from rcaeval_amd import synth
+    world = 3
+    n, N = 10, 400
+    X = synth.gaussian_sem(n, N, seed=5, w_low=0.3, w_high=0.9, edge_prob=0.3)
+    C = np.corrcoef(X.T)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_setup_fail_worker, args=(r, world, port, C, N, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert res[r][0] == ("own" if r == 1 else "peer"), (mode, res)
 
 
 def _gather_worker(rank, world, port, q):

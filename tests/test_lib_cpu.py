@@ -27,6 +27,36 @@ def test_library_exports_every_declared_symbol():
     assert bound == set(syms), (set(syms) - bound, bound - set(syms))
 
 
+def test_library_abi_matches_bindings():
+    """pcg_abi_info: struct sizes / version of the built library equal the ctypes structs."""
+    from rcaeval_amd import _lib
+    lib = _lib.load()
+    sb, rb, ver = _lib.abi_info(lib)
+    assert (sb, rb, ver) == (ctypes.sizeof(_lib.PcgStats), ctypes.sizeof(_lib.PcgRecord), _lib.PCG_ABI_VERSION)
+    hdr = open(os.path.join(ROOT, "include", "pcgpu.h")).read()
+    assert int(re.search(r"#define PCG_ABI_VERSION (\d+)", hdr).group(1)) == ver
+
+    class Short(ctypes.Structure):       # a binding that missed a field must be refused
+        _fields_ = [("tests", ctypes.c_int64 * 32)]
+    with pytest.raises(_lib.EngineUnavailable, match="ABI mismatch"):
+        _lib.check_abi(lib, stats_cls=Short)
+
+
+def test_integration_stub_matches_library_abi():
+    """INTEGRATION.md's ctypes stub: its Stats struct and its ABI assertion, executed against
+    the built library (the stub's own `lib` line is replaced by the in-tree library path)."""
+    from rcaeval_amd import _lib
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    block = re.search(r"```python\n(# RCAEval/graph_construction/pc_mi355x.py.*?)```", text, re.S).group(1)
+    head = block.split("lib.pcg_create.argtypes")[0]          # struct + ABI check, before any GPU call
+    head = head.replace("import ctypes, numpy as np, torch", "import ctypes")
+    head = re.sub(r'lib = ctypes.CDLL\("[^"]+"\)', "lib = ctypes.CDLL(LIB_PATH)", head)
+    ns = {"LIB_PATH": _lib.LIB_PATH}
+    exec(compile(head, "INTEGRATION.md", "exec"), ns)      # asserts inside the stub
+    assert ctypes.sizeof(ns["Stats"]) == ctypes.sizeof(_lib.PcgStats)
+    assert [f[0] for f in ns["Stats"]._fields_] == [f[0] for f in _lib.PcgStats._fields_]
+
+
 def test_create_fails_loudly_without_gpu():
     import torch
     if torch.cuda.is_available():
@@ -63,6 +93,46 @@ def test_rca_wrapper_dummy_ranks_on_method_error():
     from rcaeval_amd.io.time_series import preprocess
     cols = preprocess(df, dataset="online-boutique").columns.to_list()
     assert out == {"adj": [], "node_names": cols, "ranks": cols}
+
+
+@pytest.mark.parametrize("code", [-1, -2, -3, -6, -8])
+def test_rca_wrapper_propagates_engine_faults(code):
+    """Engine faults (INVALID, OOM, HIP, RCCL, PEER) must not become dummy rankings: a sticky
+    device fault would otherwise score every later RQ2 case as a dummy silently."""
+    from rcaeval_amd import _lib, synth
+    from rcaeval_amd.e2e import rca
+
+    @rca
+    def broken(data, inject_time=None, dataset=None, **kw):
+        raise _lib.PcgError(code, "fault")
+    df = synth.telemetry_frame(8, 60, seed=2)
+    with pytest.raises(_lib.PcgError):
+        broken(df, 0, dataset="online-boutique")
+
+
+def test_rca_wrapper_dummy_ranks_on_data_errors():
+    """Data-driven engine outcomes keep the reference's dummy-rank fallback: singular / domain
+    (ValueError, as causal-learn raises) and an overflow that survived its reruns."""
+    from rcaeval_amd import _lib, synth
+    from rcaeval_amd.e2e import rca
+    from rcaeval_amd.io.time_series import preprocess
+    df = synth.telemetry_frame(8, 60, seed=2)
+    cols = preprocess(df, dataset="online-boutique").columns.to_list()
+    for exc in (ValueError("singular"), _lib.PcgError(_lib.PCG_ERR_OVERFLOW, "list overflow")):
+        @rca
+        def broken(data, inject_time=None, dataset=None, **kw):
+            raise exc
+        with pytest.warns(UserWarning) if isinstance(exc, _lib.PcgError) else _nullctx():
+            out = broken(df, 0, dataset="online-boutique")
+        assert out == {"adj": [], "node_names": cols, "ranks": cols}
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
 
 
 def test_orient_cpp_matches_python_oracle_golden():
