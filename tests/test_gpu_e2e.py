@@ -8,6 +8,7 @@ restatement + Python orientation restatement + scipy PageRank + the reference gl
 import json
 import os
 import socket
+import sys
 
 import numpy as np
 import pytest
@@ -87,15 +88,16 @@ def test_random_walk_serial_path_matches_numpy():
 
 
 def _oracle_pipeline(df, dataset, head, alpha=0.05, sli=None):
-    """Reference-equivalent CPU pipeline built only from oracle restatements + reference glue:
-    C-restated skeleton (pc_oracle.c), Python-restated orientation, scipy PageRank."""
+    """Reference-equivalent CPU pipeline built only from oracle restatements: C-restated skeleton
+    (pc_oracle.c), Python-restated orientation, scipy PageRank, and the glue restated in the test
+    (networkx DiGraph as pc_pagerank.py:20-29, the loop form of random_walk.py's transition
+    matrix) — no product code besides the golden-pinned preprocess."""
     from oracle import cpc
     from oracle import orient as oor
     from oracle import pagerank as opr
     from oracle import random_walk as orw
-    from rcaeval_amd.e2e.pc_pagerank import digraph_matrix
-    from rcaeval_amd.graph_heads.random_walk import transition_matrix
-    from rcaeval_amd.io.time_series import preprocess
+    from rcaeval_amd.io.time_series import preprocess      # pinned by preprocess.npz (reference outputs)
+    from tests_support import loop_transition_matrix, networkx_digraph_matrix
     data = preprocess(df, dataset=dataset)
     names = data.columns.to_list()
     X = data.to_numpy().astype(float)
@@ -120,12 +122,12 @@ def _oracle_pipeline(df, dataset, head, alpha=0.05, sli=None):
                                 names.index(sli), beta=0.3, rho=0.2)
         return [names[k - 1] for k, _ in rank], g
     if head == "pagerank":
-        M, _ = digraph_matrix(g)
+        M, _ = networkx_digraph_matrix(g)
         scores = opr.pagerank(M.T)
         ranked = sorted(zip(names, scores), key=lambda t: t[1], reverse=True)
         return [n_ for n_, _ in ranked], g
     uniq = list(dict.fromkeys(names))
-    P = transition_matrix(g, names, uniq)
+    P = loop_transition_matrix(g, names, uniq)
     counts = orw.walk_counts(P, 0, len(names))
     ranked = sorted([(nm, counts[i] / len(names)) for i, nm in enumerate(uniq)], key=lambda t: t[1], reverse=True)
     return [n_ for n_, _ in ranked], g
@@ -150,6 +152,53 @@ def test_pc_randomwalk_matches_oracle_pipeline(m, rows, seed):
     assert out["ranks"] == ranks
     from rcaeval_amd.io.time_series import preprocess
     np.testing.assert_array_equal(pc_default(preprocess(df, dataset="online-boutique")), g)
+
+
+def _glue_frame(case, tmp_path):
+    """A glue.json case's input frame, as the generator built it (seeded synth -> CSV -> read)."""
+    import pandas as pd
+    sys.path.insert(0, GOLD)
+    from make_glue_golden import frame, frame_digest
+    m, rows, seed, nc, dataset, noise = case["case"]
+    p = os.path.join(str(tmp_path), "case.csv")
+    frame(m, rows, seed, nc, noise).to_csv(p, index=False)
+    df = pd.read_csv(p)
+    assert frame_digest(df) == case["input_digest"], "regenerated input frame differs from the golden's"
+    return df, dataset
+
+
+def _glue():
+    return json.load(open(os.path.join(GOLD, "glue.json")))
+
+
+@pytest.mark.parametrize("k", range(6))
+def test_pc_pagerank_matches_reference_glue_golden(k, tmp_path):
+    """pc_pagerank on the GPU == the REFERENCE pc_pagerank function executed under networkx 2.6.3
+    with pc -> the oracle graph and PageRank -> the sknetwork restatement (glue.json): node
+    names, the to_numpy_matrix matrix (isolated nodes dropped) and the misaligned rank list."""
+    from rcaeval_amd.e2e import pc_pagerank
+    from rcaeval_amd.graph_construction.pc import pc_default
+    from rcaeval_amd.io.time_series import preprocess
+    case = _glue()["pagerank"][k]
+    df, dataset = _glue_frame(case, tmp_path)
+    np.testing.assert_array_equal(pc_default(preprocess(df, dataset=dataset)), np.array(case["graph"]))
+    out = pc_pagerank(df, 0, dataset=dataset)
+    assert out["node_names"] == case["node_names"]
+    np.testing.assert_array_equal(out["adj"], np.array(case["adj"]))
+    assert out["ranks"] == case["ranks"]
+
+
+@pytest.mark.parametrize("k", range(3))
+def test_pc_randomwalk_matches_reference_glue_golden(k, tmp_path):
+    """pc_randomwalk on the GPU == the REFERENCE pc_randomwalk + random_walk executed with
+    pc_default -> the oracle graph (glue.json)."""
+    from rcaeval_amd.e2e import pc_randomwalk
+    case = _glue()["randomwalk"][k]
+    df, dataset = _glue_frame(case, tmp_path)
+    out = pc_randomwalk(df, 0, dataset=dataset)
+    np.testing.assert_array_equal(out["adj"], np.array(case["graph"]))
+    assert out["node_names"] == case["node_names"]
+    assert out["ranks"] == case["ranks"]
 
 
 def test_pc_pagerank_readme_path_dataset_none_keeps_time_and_constants():

@@ -259,44 +259,6 @@ def test_uc_candidates_match_priority2_order():
         np.testing.assert_array_equal(orient(g[f"adj{i}"], g[f"xy{i}"], g[f"bits{i}"]), g[f"graph{i}"])
 
 
-def _loop_transition_matrix(adj, node_names, names, score_values=None, rho=0.5):
-    """Statement-by-statement restatement of random_walk.py:267-296 + :156-178 (test only)."""
-    m = len(adj)
-    idx = {nm: i for i, nm in enumerate(names)}
-    size = len(names)
-    score = np.zeros(size) if score_values is None else np.asarray(score_values, float)
-    edges = []
-    for a in range(m):
-        for b in range(m):
-            ab, ba = int(adj[a, b]), int(adj[b, a])
-            if ab == ba == 0:
-                continue
-            if (ab, ba) in ((-1, -1), (1, -1), (1, 0)):
-                edges.append((b, a))
-            elif (ab, ba) in ((-1, 1), (0, 1)):
-                edges.append((a, b))
-            elif (ab, ba) == (1, 1):
-                edges += [(a, b), (b, a)]
-            else:
-                raise ValueError(f"Unexpected value: {adj[a, b]}, {adj[b, a]}")
-    children = [set() for _ in range(size)]
-    parents = [set() for _ in range(size)]
-    for u, v in edges:                       # reversed: v -> u
-        cu, cv = idx[node_names[u]], idx[node_names[v]]
-        children[cv].add(cu)
-        parents[cu].add(cv)
-    M = np.zeros((size, size))
-    for c in range(size):
-        for ch in children[c]:
-            M[ch, c] = rho * abs(score[ch])
-        for pa in parents[c]:
-            M[pa, c] = abs(score[pa])
-        M[c, c] = max(abs(score[c]) - M[:, c].max(), 0)
-        tot = M[:, c].sum()
-        M[:, c] = M[:, c] / tot if tot > 0 else 1 / size
-    return M
-
-
 @pytest.mark.parametrize("seed", range(6))
 def test_transition_matrix_array_form_equals_loop(seed):
     from rcaeval_amd.graph_heads.random_walk import transition_matrix
@@ -312,8 +274,9 @@ def test_transition_matrix_array_form_equals_loop(seed):
     names = [f"n{int(v)}" for v in rng.integers(0, max(2, m - seed), size=m)]   # duplicates merge by name
     uniq = list(dict.fromkeys(names))
     scores = None if seed < 2 else rng.normal(size=len(uniq))
+    from tests_support import loop_transition_matrix
     np.testing.assert_array_equal(transition_matrix(adj, names, uniq, scores),
-                                  _loop_transition_matrix(adj, names, uniq, scores))
+                                  loop_transition_matrix(adj, names, uniq, scores))
 
 
 def test_random_walk_codes_error_first_cell():

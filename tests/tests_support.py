@@ -1,4 +1,5 @@
 """Pure-Python replicas used by the CPU tests to pin the GPU kernels' arithmetic."""
+import numpy as np
 
 
 def pairwise_sum(a):
@@ -113,3 +114,57 @@ def assert_skeleton_matches(out, ref, n, tests=True, unions=True):
         badu = [k for k in keys if ug.get(k) != ur.get(k)]
         assert not badu, f"sepset unions differ at {len(badu)} pairs, e.g. {badu[:5]}"
     return len(diff)
+
+
+def loop_transition_matrix(adj, node_names, names, score_values=None, rho=0.5):
+    """Statement-by-statement restatement of random_walk.py:267-296 + :156-178 (test only)."""
+    m = len(adj)
+    idx = {nm: i for i, nm in enumerate(names)}
+    size = len(names)
+    score = np.zeros(size) if score_values is None else np.asarray(score_values, float)
+    edges = []
+    for a in range(m):
+        for b in range(m):
+            ab, ba = int(adj[a, b]), int(adj[b, a])
+            if ab == ba == 0:
+                continue
+            if (ab, ba) in ((-1, -1), (1, -1), (1, 0)):
+                edges.append((b, a))
+            elif (ab, ba) in ((-1, 1), (0, 1)):
+                edges.append((a, b))
+            elif (ab, ba) == (1, 1):
+                edges += [(a, b), (b, a)]
+            else:
+                raise ValueError(f"Unexpected value: {adj[a, b]}, {adj[b, a]}")
+    children = [set() for _ in range(size)]
+    parents = [set() for _ in range(size)]
+    for u, v in edges:                       # reversed: v -> u
+        cu, cv = idx[node_names[u]], idx[node_names[v]]
+        children[cv].add(cu)
+        parents[cu].add(cv)
+    M = np.zeros((size, size))
+    for c in range(size):
+        for ch in children[c]:
+            M[ch, c] = rho * abs(score[ch])
+        for pa in parents[c]:
+            M[pa, c] = abs(score[pa])
+        M[c, c] = max(abs(score[c]) - M[:, c].max(), 0)
+        tot = M[:, c].sum()
+        M[:, c] = M[:, c] / tot if tot > 0 else 1 / size
+    return M
+
+
+def networkx_digraph_matrix(adj):
+    """pc_pagerank.py:20-29 written with networkx as the reference does (``to_numpy_array``: the
+    values of networkx 2.5's ``to_numpy_matrix``, which 3.x removed; glue.json pins the 2.6.3
+    call itself). Returns (matrix, sorted non-isolated nodes)."""
+    import networkx as nx
+    G = nx.DiGraph()
+    for i in range(len(adj)):
+        for j in range(len(adj)):
+            if adj[i, j] == -1:
+                G.add_edge(i, j)
+            if adj[i, j] == 1:
+                G.add_edge(j, i)
+    nodes = sorted(G.nodes())
+    return np.asarray(nx.to_numpy_array(G, nodelist=nodes)), nodes

@@ -17,7 +17,17 @@ EXPECT = {
     12: {"v_cndmask_b32": 16}, 13: {"v_cmp_lt_f32": 16}, 14: {"v_cmp_lt_f64": 16}, 15: {"v_mad_u64_u32": 16},
     16: {"v_lshl_add_u64": 16}, 17: {"v_cvt_f32_f64": 16}, 18: {"v_rsq_f32": 16},
     19: {"v_fma_f64": 16, "v_pk_fma_f32": 32}, 20: {"v_pk_fma_f32": 16, "v_add_u32": 16},
+    21: {"s_add_u32": 16}, 22: {"v_pk_fma_f32": 16, "s_add_u32": 16}, 23: {"v_pk_fma_f32": 16, "s_add_u32": 8},
+    24: {"v_pk_fma_f32": 16, "ds_read_b64": 8}, 25: {"v_pk_fma_f32": 16, "v_cmp_lt_f32": 16},
 }
+for _k, _op in enumerate(["v_fmac_f32_e32", "v_add_f32_e32", "v_cmp_lt_f32_e32", "v_cndmask_b32_e32", "v_or3_b32",
+                          "v_pk_add_f32", "v_max_f32_e32", "v_readfirstlane_b32", "v_fmac_f64_e32",
+                          "v_mbcnt_lo_u32_b32", "v_lshlrev_b64", "v_bfe_u32", "v_cvt_f64_f32"], start=26):
+    EXPECT[_k] = {_op: 16}
+EXPECT.update({39: {"v_fma_f32": 16}, 40: {"v_fma_f32": 16}, 41: {"v_pk_fma_f32": 16}, 42: {"v_pk_fma_f32": 16},
+               43: {"v_fma_f64": 16}, 44: {"v_pk_fma_f32": 16, "s_cselect_b64": 16, "s_andn2_b64": 16, "s_cmp_lg_u32": 16}})
+# non-vector instructions counted for the kinds that promise them
+COUNTED = ("s_add_u32", "ds_read_b64", "s_cselect_b64", "s_andn2_b64", "s_cmp_lg_u32")
 
 
 def loop_body(asm: str, kind: int) -> list:
@@ -41,7 +51,7 @@ def main():
     bad = 0
     for kind, want in EXPECT.items():
         ops = loop_body(asm, kind)
-        vec = collections.Counter(o for o in ops if o.startswith("v_"))
+        vec = collections.Counter(o for o in ops if o.startswith("v_") or o.startswith(COUNTED))
         got = {k: sum(v for o, v in vec.items() if o.startswith(k)) for k in want}
         other = {o: v for o, v in vec.items() if not any(o.startswith(k) for k in want)}
         ok = got == want and not other
