@@ -109,6 +109,7 @@ struct pcg_handle {
     int spl_w = 1;                   // tasks per lane of the wide class
     int narrow_deg = 64;             // pcg_set_narrow_degree (testing: route more nodes to the wide class)
     bool tgroup = false;             // small class runs k_level_lds_t this depth
+    bool wavek = false;              // small class runs k_level_wave this depth (deep levels)
     int screen_eff = 0;              // the current depth's effective mask (set by pcg_level_begin)
     int screen_mask = -1;            // depths (bit 1 << d) with the fp32-screened T-group sweep (k_level_lds_f); -1 = default
     int32_t maxdeg = 0;

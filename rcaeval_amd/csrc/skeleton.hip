@@ -2550,6 +2550,272 @@ __global__ __launch_bounds__(64) void k_level_deep(LevelArgs a, double *scratch,
 }
 
 // ---------------------------------------------------------------------------------------
+// Deep levels (d >= PCG_WAVE_LO, default 13; the reference's unlimited-depth loop reaches them on
+// sparse graphs, SkeletonDiscovery.py:72), narrow nodes (D <= WAVE_MAXD), threshold / full-p
+// modes: ONE WAVE PER CONDITIONING SET S, lanes = the columns of the node block — lane t < D
+// the neighbour t, lane D the node x itself. Every lane forward-solves its own column,
+//   v_c = L^-1 C[S, c],   L = chol(C_SS),
+// and the Cholesky factor is never formed separately: for a lane c = S_j its solve IS row j of L
+// (L^-1 C_SS = L^T), so at step i the lanes read L[i][q] = v_{S_i}[q] from lane S_i (v_readlane,
+// S_i is wave-uniform) and the pivot lambda_i^2 from lane S_i's own residual:
+//   t_c = C[S_i][c] - sum_{q<i} L[i][q] v_c[q],   lambda_i^2 = t_{S_i},   v_c[i] = t_c / lambda_i.
+// After |S| steps every lane holds |v_c|^2 and u.v_c (u = v_x, broadcast from lane D as it is
+// formed), so ALL tests (x, y | S), y in adj(x) \ S, finish in parallel: c_yy = C_yy - |v_y|^2,
+// c_xy = C_xy - u.v_y, c_xx = C_xx - |u|^2, decided like the other kernels (threshold band,
+// conditioning guard; the rest on the exact LU path: the deferred list for |S| <= PCG_MAX_DEPTH,
+// in the wave's LDS slot beyond). Per S: |S|^2 readlanes + |S|^2 / 2 fp64 FMAs per lane, for
+// D - |S| tests — replaces the per-test global-scratch LU of k_level_deep (10 ms for 19 tests).
+// Consecutive sets of a wave follow colex order (Gosper's next-combination on the 64-bit mask).
+#ifndef PCG_WAVE_LO
+#define PCG_WAVE_LO 13
+#endif
+constexpr int WAVE_MAXD = 63;    // D + 1 lanes (the neighbours and x) per wave
+// the wave's LDS slot: the L rows of the current set (md x (md + 1)), reused by the exact path
+// (m x m matrix, two solution columns, m variable ids; m <= md + 2)
+constexpr int WAVE_SLOT_DOUBLES(int md) {
+    return (md + 2) * (md + 2) + 3 * (md + 2) > md * (md + 1) ? (md + 2) * (md + 2) + 3 * (md + 2) : md * (md + 1);
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// The exact path of one test (numpy.linalg.inv-order LU of the m x m matrix A in LDS, the
+// reference p expression): 0 ok, 1 singular, 2 math domain. Not inlined: its polynomial
+// constants would otherwise be hoisted into registers across the callers' hot loops.
+__device__ __attribute__((noinline)) int exact_lu_pvalue(double *A, int m, double *B0, double *B1, double sqrt_dof,
+                                                         double *pv) {
+    int piv[PCG_MAX_LEVEL_DEPTH + 2];
+    double i00, i01, i11;
+    if (pcg_lu_inv01(A, m, piv, B0, B1, &i00, &i01, &i11)) return 1;
+    const double prod = i00 * i11;
+    if (prod < 0.0) return 2;
+    int err = 0;
+    *pv = pcg_pvalue_from_r(-i01 / sqrt(prod), sqrt_dof, &err);
+    return err;
+}
+
+// global ids of the members of a local set mask (ascending), -1 padded to PCG_MAX_DEPTH
+__device__ __forceinline__ void set_members(unsigned long long mask, const int32_t *nxs, int (&sg)[PCG_MAX_DEPTH]) {
+#pragma unroll
+    for (int q = 0; q < PCG_MAX_DEPTH; ++q) {
+        sg[q] = mask ? nxs[__builtin_ctzll(mask)] : -1;
+        mask &= mask - 1;
+    }
+}
+
+template <int MD, int MODE>
+__global__ __launch_bounds__(256) void k_level_wave(LevelArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wv = tid >> 6;
+    const int64_t chunk = a.chunk_lo + blockIdx.x;
+    int lo = 0, hi = a.n;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (a.cpre[mid] <= chunk) lo = mid; else hi = mid;
+    }
+    const int x = lo;
+    const int D = a.deg[x];
+    const int d = a.d;
+    const int32_t *nxg = a.nbr + a.off[x];
+
+    double *M = reinterpret_cast<double *>(smem);                 // D * D
+    double *Mx = M + D * D;                                       // D
+    double *Md = Mx + D;                                          // D
+    unsigned long long *lmask = reinterpret_cast<unsigned long long *>(Md + D);   // D
+    unsigned long long *uself = lmask + D;                        // D
+    unsigned long long *uprop = uself + D;                        // D
+    int32_t *nxs = reinterpret_cast<int32_t *>(uprop + D);       // D
+    int *s_tx = nxs + D;                                          // 1
+    // the wave's LDS slot (L rows; the exact path's matrix beyond PCG_MAX_DEPTH)
+    double *slot = reinterpret_cast<double *>(smem + a.lds_btab_off) + (size_t)wv * WAVE_SLOT_DOUBLES(MD);
+
+    for (int i = tid; i < D; i += blockDim.x) nxs[i] = nxg[i];
+    __syncthreads();
+    for (int e = tid; e < D * D; e += blockDim.x) {
+        const int t = e / D, k = e - t * D;
+        M[e] = a.C[(int64_t)nxs[t] * a.ldc + nxs[k]];
+    }
+    for (int t = wv; t < D; t += blockDim.x >> 6) {
+        const bool bit = lane < D && ((a.adj[(int64_t)nxs[t] * a.W + (nxs[lane] >> 6)] >> (nxs[lane] & 63)) & 1ull);
+        const unsigned long long m = __ballot(bit);
+        if (lane == 0) lmask[t] = m;
+    }
+    for (int t = tid; t < D; t += blockDim.x) {
+        const int yg = nxs[t];
+        Mx[t] = a.C[(int64_t)x * a.ldc + yg];
+        Md[t] = a.diag[yg];
+        uself[t] = 0;
+        uprop[t] = 0;
+    }
+    if (tid == 0) {
+        int c = 0;
+        while (c < D && nxs[c] < x) ++c;
+        *s_tx = c;
+    }
+    __syncthreads();
+    const int tx = *s_tx;
+    const double Cxx = a.diag[x];
+    const uint64_t nS = pcg_binom(a.binom, D, d);
+    const uint64_t r0 = (uint64_t)(chunk - a.cpre[x]) * 4u * (uint64_t)a.spl + (uint64_t)wv * (uint64_t)a.spl;
+    const uint64_t r1 = min(nS, r0 + (uint64_t)a.spl);
+    unsigned long long tests = 0, indep = 0;
+    if (r0 < r1) {
+        unsigned long long mask = 0;      // colex unrank of r0 (wave-uniform)
+        {
+            uint64_t rr = r0;
+            int hi_ = D;
+            for (int ii = d - 1; ii >= 0; --ii) {
+                int lo_ = ii, up = hi_ - 1;
+                while (lo_ < up) {
+                    const int mid = (lo_ + up + 1) >> 1;
+                    if (pcg_binom(a.binom, mid, ii + 1) <= rr) lo_ = mid; else up = mid - 1;
+                }
+                mask |= 1ull << lo_;
+                rr -= pcg_binom(a.binom, lo_, ii + 1);
+                hi_ = lo_;
+            }
+        }
+        const int cl = lane < D ? lane : 0;            // lane D (x) and idle lanes: a safe column
+        double *Lm = slot;                             // L rows of the current set: Lm[i * LS + q]
+        constexpr int LS = MD + 1;
+        for (uint64_t rank = r0; rank < r1; ++rank) {
+            double v[MD];
+            double vv = 0.0, uv = 0.0, gmin = 1.0;
+            bool ok = true;
+            unsigned long long m = mask;
+            // S position of this lane's column when it is a member (row of L it produces)
+            const bool member = lane < D && ((mask >> lane) & 1ull);
+            const int mypos = member ? __popcll(mask & ((1ull << lane) - 1ull)) : -1;
+#pragma unroll
+            for (int i = 0; i < MD; ++i) {
+                if (i < d) {                           // wave-uniform (no break: the loop stays unrolled)
+                    const int si = __builtin_ctzll(m); // S_i, wave-uniform
+                    m &= m - 1;
+                    double t = lane < D ? M[si * D + cl] : Mx[si];
+                    const double *Li = Lm + i * LS;    // row i of L (written by lane S_i, steps q < i)
+#pragma unroll
+                    for (int q = 0; q < i; ++q) t -= Li[q] * v[q];
+                    const double piv = readlane_f64(t, si);
+                    ok = ok && (piv > 0.0);
+                    gmin = fmin(gmin, piv);
+                    v[i] = t * (1.0 / sqrt(piv));
+                    vv += v[i] * v[i];
+                    uv += readlane_f64(v[i], D) * v[i];
+                    if (mypos > i) Lm[mypos * LS + i] = v[i];   // L[mypos][i] for the later steps
+                    wave_sync();
+                }
+            }
+            const double cxx = Cxx - readlane_f64(vv, D);
+            const double kg = a.tau / gmin;
+            bool live = lane < D && !((mask >> lane) & 1ull);
+            const unsigned long long lm = live ? lmask[cl] : 0ull;
+            const bool in_y = (lm & mask) == mask;
+            live = live && !(lane < tx && in_y);
+            tests += live;
+            int dec = 2;
+            double p = 0.0;
+            if (live && ok) dec = decide<MODE>(a, Mx[cl] - uv, cxx, Md[cl] - vv, kg, &p);
+            if (live && dec == 1) {
+                ++indep;
+                atomicOr(&uself[cl], mask);
+                if (in_y && lane >= tx) atomicOr(&uprop[cl], mask);
+            }
+            if (MODE == MODE_FULLP && live && dec != 2) {
+                const int yg = nxs[cl];
+                const int lo_ = x < yg ? x : yg, hi_ = x < yg ? yg : x;
+                const bool near = fabs(p - a.alpha) < 1e-9;
+                if (d <= PCG_MAX_DEPTH && (near || rec_on(a, lo_, hi_))) {
+                    int sg[PCG_MAX_DEPTH];
+                    set_members(mask, nxs, sg);
+                    if (rec_on(a, lo_, hi_)) push_record(a.records, a.rec_cap, &a.ctr->records, lo_, hi_, d, sg, p);
+                    if (near) push_record(a.nearl, a.near_cap, &a.ctr->near_alpha, lo_, hi_, d, sg, p);
+                } else if (near) {
+                    atomicAdd(&a.ctr->near_alpha, 1ull);   // counts only beyond PCG_MAX_DEPTH
+                }
+            }
+            if (d <= PCG_MAX_DEPTH) {
+                if (live && dec == 2) {
+                    int sg[PCG_MAX_DEPTH];
+                    set_members(mask, nxs, sg);
+                    push_deferred(a, x, nxs[cl], sg, d);
+                }
+            } else {
+                // the exact LU of each remaining test, one at a time in the wave's LDS slot
+                unsigned long long need = __ballot(live && dec == 2);
+                const int mm = d + 2;
+                double *A = slot, *B0 = slot + mm * mm, *B1 = B0 + mm;
+                int *var = reinterpret_cast<int *>(B1 + mm);   // mm ints after the two columns
+                while (need) {
+                    const int L = __builtin_ctzll(need);
+                    need &= need - 1;
+                    const int yg = nxs[L];
+                    wave_sync();
+                    if (lane < D && ((mask >> lane) & 1ull))      // S members in ascending order
+                        var[2 + __popcll(mask & ((1ull << lane) - 1ull))] = nxs[lane];
+                    if (lane == 0) {
+                        var[0] = x < yg ? x : yg;
+                        var[1] = x < yg ? yg : x;
+                    }
+                    wave_sync();
+                    for (int k = lane; k < mm * mm; k += 64) {
+                        const int r = k / mm, c = k - r * mm;
+                        A[k] = a.C[(int64_t)var[r] * a.ldc + var[c]];
+                    }
+                    wave_sync();
+                    if (lane == 0) {
+                        double pv = __builtin_nan("");
+                        const int err = exact_lu_pvalue(A, mm, B0, B1, a.sqrt_dof, &pv);
+                        atomicAdd(&a.ctr->exact, 1ull);
+                        if (err) {
+                            flag_error(a, err);
+                        } else {
+                            if (fabs(pv - a.alpha) < 1e-9) atomicAdd(&a.ctr->near_alpha, 1ull);
+                            if (pv > a.alpha) {
+                                ++indep;
+                                atomicOr(&uself[L], mask);
+                                if (((lmask[L] & mask) == mask) && L >= tx) atomicOr(&uprop[L], mask);
+                            }
+                        }
+                    }
+                }
+            }
+            // next set in colex order (Gosper: the next larger 64-bit word with |S| bits)
+            const unsigned long long c0 = mask & (0ull - mask);
+            const unsigned long long rr = mask + c0;
+            mask = (((rr ^ mask) >> 2) >> __builtin_ctzll(mask)) | rr;
+        }
+    }
+    __syncthreads();
+    // flush unions (local bits -> global node bits) and removal flags
+    for (int t = tid; t < D; t += blockDim.x) {
+        const unsigned long long us = uself[t], up = uprop[t];
+        if (!(us | up)) continue;
+        const int yg = nxs[t];
+        a.rm[(int64_t)x * a.n + yg] = 1;
+        a.rm[(int64_t)yg * a.n + x] = 1;
+        for (int side = 0; side < 2; ++side) {
+            unsigned long long mb = side ? up : us;
+            if (!mb) continue;
+            const int64_t s = side ? (int64_t)a.off[yg] + find_in_sorted(a.nbr + a.off[yg], a.deg[yg], x)
+                                   : (int64_t)a.off[x] + t;
+            unsigned long long *row = reinterpret_cast<unsigned long long *>(a.ug + s * a.W);
+            while (mb) {
+                const int b = __ffsll((long long)mb) - 1;
+                const int g = nxs[b];
+                atomicOr(&row[g >> 6], 1ull << (g & 63));
+                mb &= mb - 1;
+            }
+        }
+    }
+    block_flush_counts(a.ctr, tests, indep);
+}
+
+// ---------------------------------------------------------------------------------------
 // exact path over the deferred list (LU like numpy.linalg.inv; the reference p expression)
 template <int M>
 __device__ __forceinline__ int lu_from_lds(const double *A, double *i00, double *i01, double *i11) {
@@ -2799,6 +3065,13 @@ uint64_t tgroup_tasks(const pcg_handle *h, int D, int d) {
 }
 
 bool use_tgroup(int mode, int d) { return mode == MODE_DECIDE && d >= 2 && d <= 4; }
+// depths whose narrow class runs k_level_wave (one wave per conditioning set); PCG_WAVE_LO
+// overrides the first such depth (A/B knob)
+bool use_wave(int mode, int d) {
+    const char *e = getenv("PCG_WAVE_LO");        // read per depth, like PCG_SCREEN_MASK
+    const int lo = e ? atoi(e) : PCG_WAVE_LO;
+    return (mode == MODE_DECIDE || mode == MODE_FULLP) && d >= std::max(lo, 5) && d <= PCG_MAX_LEVEL_DEPTH;
+}
 // depth 1's large class runs k_level1_pairs (pcg_level_run); its chunks split a node's
 // D(D-1)/2 neighbour pairs evenly, ~L1_PAIRS_PER_CHUNK each, so a high-degree node is spread
 // over many blocks instead of a D/256-chunk tail (measured: 1024 pairs 0.36 ms, 2048 0.243,
@@ -2813,6 +3086,7 @@ int64_t l1_pair_chunks(int D) { return std::max<int64_t>(1, ((int64_t)D * (D - 1
 
 // node class of a degree-D node at depth d: 0 narrow, 1 wide (T-group depths only), 2 large
 int level_class(const pcg_handle *h, int D, int d, bool tg) {
+    if (h->wavek) return D <= std::min(WAVE_MAXD, h->narrow_deg) ? 0 : 2;   // k_level_wave depths
     if (D <= std::min(SMALL_DEG, h->narrow_deg) && d <= PCG_MAX_DEPTH) return 0;
     if (tg && D <= WIDE_DEG && lds_tgroup_bytes((D + 3) & ~3, d, 16) <= LDS_MAX) return 1;
     return 2;
@@ -3044,6 +3318,7 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
         // small class units: T-group lane tasks (threshold mode, depth 2..4) or S ranks
         const bool tg = use_tgroup(mode_of(h, depth), depth);
         h->tgroup = tg;
+        h->wavek = use_wave(mode_of(h, depth), depth);
         // fp32-screened depths: pcg_set_screen_precision, or the PCG_SCREEN_MASK A/B knob
         const char *sm = getenv("PCG_SCREEN_MASK");
         h->screen_eff = sm ? (int)strtol(sm, nullptr, 0) : (h->screen_mask < 0 ? PCG_TG_F32 : h->screen_mask);
@@ -3081,12 +3356,14 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
             snprintf(nm, sizeof nm, "PCG_NB%d", depth);
             if (getenv(nm)) nb_target = atof(getenv(nm));
         }
-        h->spl = (int)std::min(64.0, std::max(1.0, std::floor(sum_small / (256.0 * nb_target * h->world))));
+        // lanes per block: 256 S ranks / T-group tasks, or 4 conditioning sets (k_level_wave: a wave each)
+        const double per_block = h->wavek ? 4.0 : 256.0;
+        h->spl = (int)std::min(64.0, std::max(1.0, std::floor(sum_small / (per_block * nb_target * h->world))));
         const double nbw_target = getenv("PCG_NBW") ? atof(getenv("PCG_NBW")) : 512.0;   // A/B knob
         h->spl_w = (int)std::min(64.0, std::max(1.0, std::floor(sum_wide / (256.0 * nbw_target * h->world))));
         const double mean_large = cnt_large ? sum_large / cnt_large : 0.0;
         h->chunk = (depth > PCG_MAX_DEPTH || mean_large <= 64) ? 64 : (mean_large <= 128 ? 128 : 256);
-        const uint64_t csz = (uint64_t)256 * h->spl, cszw = (uint64_t)256 * h->spl_w;
+        const uint64_t csz = (uint64_t)(h->wavek ? 4 : 256) * h->spl, cszw = (uint64_t)256 * h->spl_w;
         std::vector<int64_t> nch_of(maxd + 1, 0);
         const bool l1p = use_l1_pairs(h, depth);
         for (int D = depth + 1; D <= maxd; ++D) {
@@ -3287,7 +3564,20 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                     const int dl = h->tgroup ? (h->maxdeg_small + 3) & ~3 : h->maxdeg_small;
                     as.lds_btab_off = (int)lds_small_core(dl);
                     const size_t lds = h->tgroup ? lds_tgroup_bytes(dl, d) : lds_small_bytes(dl);
-                    if (h->tgroup && use_screen32(h, d)) {
+                    if (h->wavek) {
+                        const dim3 grid((unsigned)(s_hi - s_lo)), block(256);
+                        const size_t core = lds_small_core(h->maxdeg_small);
+                        as.lds_btab_off = (int)core;
+                        if (d <= 16) {
+                            const size_t ldsw = core + 4 * sizeof(double) * WAVE_SLOT_DOUBLES(16);
+                            if (mode == MODE_DECIDE) hipLaunchKernelGGL((k_level_wave<16, MODE_DECIDE>), grid, block, ldsw, h->stream, as);
+                            else hipLaunchKernelGGL((k_level_wave<16, MODE_FULLP>), grid, block, ldsw, h->stream, as);
+                        } else {
+                            const size_t ldsw = core + 4 * sizeof(double) * WAVE_SLOT_DOUBLES(32);
+                            if (mode == MODE_DECIDE) hipLaunchKernelGGL((k_level_wave<32, MODE_DECIDE>), grid, block, ldsw, h->stream, as);
+                            else hipLaunchKernelGGL((k_level_wave<32, MODE_FULLP>), grid, block, ldsw, h->stream, as);
+                        }
+                    } else if (h->tgroup && use_screen32(h, d)) {
                         as.lds_btab_off = (int)lds_f32_core(dl, 8);
                         const size_t ldsf = lds_tgroup_f_bytes(dl, d, 8);
                         const dim3 grid((unsigned)(s_hi - s_lo)), block(256);

@@ -342,3 +342,36 @@ def test_packed_barrier_or_merges_ranks(eng, n):
         assert lib.pcg_level_end(h, None) == _lib.PCG_ERR_PEER
     finally:
         lib.pcg_set_removal_buffer(h, None, 0)
+
+
+def test_full_depth_n500_matches_oracle(eng):
+    """The reference's default: no depth cap (SkeletonDiscovery.py:72). n = 500 of the config-5
+    SEM family runs 19 levels; depths >= 13 take the one-wave-per-set kernel (k_level_wave) —
+    removal depths, per-level test counts and sepset unions equal the C oracle's."""
+    X = synth.gaussian_sem(500, 10000, seed=0)
+    C = np.corrcoef(X.T)
+    ref = cpc.skeleton(C, 10000, max_depth=-1)
+    out = eng.skeleton(C, 10000)
+    assert out.levels == ref.levels == 19
+    assert_skeleton_matches(out, ref, 500)
+
+
+@pytest.mark.parametrize("n,N,seed,wl,wh,ep", CASES[:5])
+@pytest.mark.parametrize("flags", [0, _lib.PCG_FLAG_FULL_P | _lib.PCG_FLAG_RECORD])
+def test_wave_kernel_from_depth5_matches_oracle(eng, n, N, seed, wl, wh, ep, flags, monkeypatch):
+    """k_level_wave at every depth >= 5 (PCG_WAVE_LO=5): the deferred-list exact path and the
+    FULL_P records of |S| <= 12 go through it too; skeleton, unions, counts and records as the
+    oracle's."""
+    monkeypatch.setenv("PCG_WAVE_LO", "5")
+    X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
+    C = np.corrcoef(X.T)
+    ref = cpc.skeleton(C, N, record_cap=2_000_000)
+    out = eng.skeleton(C, N, flags=flags, record_capacity=2_000_000)
+    assert_skeleton_matches(out, ref, n)
+    if flags & _lib.PCG_FLAG_RECORD:
+        d = {_key(r): r["p"] for r in ref.records}
+        g = {_key(r): r["p"] for r in out.records}
+        assert set(g) == set(d)
+        keys = sorted(d)
+        assert fisherz.p_close([g[k] for k in keys], [d[k] for k in keys]).all()
+
