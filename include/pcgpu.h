@@ -54,9 +54,9 @@ extern "C" {
                                  exact path                                            */
 
 #define PCG_MAX_LEVELS 32
-#define PCG_MAX_DEPTH 12      /* deepest conditioning set with the fast kernels and per-test
-                                 records; depths 13..PCG_MAX_LEVEL_DEPTH run on the generic
-                                 exact-path kernel (counts only, no records)            */
+#define PCG_MAX_DEPTH 12      /* deepest conditioning set with per-test records and the
+                                 deferred exact-path list; depths 13..PCG_MAX_LEVEL_DEPTH run
+                                 on the one-wave-per-set kernel (counts only, no records) */
 #define PCG_MAX_LEVEL_DEPTH 30 /* deepest conditioning-set size supported at all          */
 
 typedef struct pcg_handle pcg_handle;
@@ -201,6 +201,27 @@ int pcg_level_split(pcg_handle *h, int rank, int world, int64_t *chunk_lo, int64
 int pcg_level_packed_words(int64_t n, int64_t *words);
 int pcg_level_pack(pcg_handle *h, uint64_t *packed_dev, int local_error);
 int pcg_level_merge(pcg_handle *h, const uint64_t *gathered_dev, int world);
+/* Background knowledge (causal-learn BackgroundKnowledge, RCAEval/graph_construction/pc.py:6-9,19):
+ * banned_dev (device n x n uint8, symmetric, or NULL to clear) marks the pairs whose edge is
+ * forbidden in BOTH directions; skeleton_discovery removes them at the end of depth 0 whatever
+ * their tests said, with an empty separating set (SkeletonDiscovery.py:86-101, stable=True).
+ * Applies to the following pcg_skeleton / pcg_pc_skeleton / level-step runs of this handle
+ * (in a sharded run the rank owning chunk 0 of depth 0 contributes them to the merge).        */
+int pcg_set_forbidden_pairs(pcg_handle *h, const uint8_t *banned_dev);
+/* Host orientation with background knowledge [U]: orient_by_background_knowledge, then
+ * uc_sepset's collider step skipping (x, y, z) when x->y or z->y is forbidden or y->x or y->z
+ * required, then Meek skipping any orientation i->j that is forbidden or whose reverse is
+ * required. R0 (the candidates) is enumerated on the graph AFTER the background orientation,
+ * as uc_sepset does on its copy of it. priority 2: R0 in that order (triples/scores unused);
+ * priority 3 / 4: scores[q] is the max p-value of candidate triples[q] (any order, every R0
+ * triple present: pcg_uc_candidates + pcg_fisherz_batch), R0 is stable-sorted by it ascending
+ * (3) or descending (4). forbidden / required: host n x n uint8 directed relations
+ * (forbidden[i*n + j]: i->j forbidden), either may be NULL. graph: host n x n int32 out.
+ * Replaces causal-learn pc_alg's orient_by_background_knowledge + uc_sepset + meek calls with
+ * background_knowledge (reached from RCAEval/graph_construction/pc.py:15-20).               */
+int pcg_orient_bk(int64_t n, const uint8_t *adj, const int32_t *sep_xy, const uint64_t *sep_bits,
+                  int64_t count, int priority, const int32_t *triples, const double *scores, int64_t tcount,
+                  const uint8_t *forbidden, const uint8_t *required, int32_t *graph);
 /* Testing knob: nodes with more than `max_degree` (default and cap 64) neighbours leave the
  * narrow LDS-resident class, so the wide T-group kernel (64-bit masks -> 128-bit) and the
  * staged kernels can be checked on small graphs. Results are identical for any value.      */

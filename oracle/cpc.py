@@ -41,6 +41,8 @@ def lib():
         _LIB.orc_skeleton.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int,
                                       P, P, P, P, ctypes.c_int64, P, P, ctypes.c_int64, P, P, ctypes.c_int]
         _LIB.orc_skeleton.restype = ctypes.c_int
+        _LIB.orc_skeleton_bk.argtypes = _LIB.orc_skeleton.argtypes + [P]
+        _LIB.orc_skeleton_bk.restype = ctypes.c_int
         _LIB.orc_fisherz_batch.argtypes = [P, ctypes.c_int, ctypes.c_int, P, P, ctypes.c_int,
                                            ctypes.c_int64, P, P]
         _LIB.orc_corrcoef.argtypes = [P, ctypes.c_int64, ctypes.c_int, P]
@@ -75,8 +77,10 @@ class CSkeleton:
 
 
 def skeleton(C: np.ndarray, N: int, alpha: float = 0.05, max_depth: int = -1,
-             want_union: bool = True, record_cap: int = 0, nthreads: int = 0) -> CSkeleton:
+             want_union: bool = True, record_cap: int = 0, nthreads: int = 0, banned=None) -> CSkeleton:
+    """``banned``: n x n pairs forbidden both ways by background knowledge (removed at depth 0)."""
     C = np.ascontiguousarray(C, dtype=np.float64)
+    bn = None if banned is None else np.ascontiguousarray(banned, dtype=np.uint8)
     n = C.shape[0]
     W = (n + 63) // 64
     rl = np.empty((n, n), np.int8)
@@ -88,9 +92,9 @@ def skeleton(C: np.ndarray, N: int, alpha: float = 0.05, max_depth: int = -1,
     near = np.empty(near_cap, REC_DTYPE)
     ncnt = np.zeros(1, np.int64)
     st = OrcStats()
-    lib().orc_skeleton(_p(C), n, int(N), float(alpha), int(max_depth), _p(rl), _p(deg), _p(su),
-                       _p(rec), int(record_cap), _p(cnt), _p(near), near_cap, _p(ncnt),
-                       ctypes.byref(st), int(nthreads))
+    lib().orc_skeleton_bk(_p(C), n, int(N), float(alpha), int(max_depth), _p(rl), _p(deg), _p(su),
+                          _p(rec), int(record_cap), _p(cnt), _p(near), near_cap, _p(ncnt),
+                          ctypes.byref(st), int(nthreads), _p(bn))
     L = st.levels
     if rec is not None:
         if cnt[0] > record_cap:

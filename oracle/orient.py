@@ -8,6 +8,12 @@ causal-learn 0.1.3.3 GeneralGraph edge semantics [U] (add_edge no-op on an exist
 dpath ancestry via adjust_dpath / reconstitute_dpath on removal of a directed edge).
 Quadratic in the number of edges: small graphs only. The C++ ``pcg_orient`` is checked
 against this.
+
+Background knowledge [U] (``knowledge=(forbidden, required)`` n x n masks, [i, j] = rule for
+i -> j): ``orient_by_background_knowledge`` over ``get_graph_edges`` before uc_sepset, the
+collider skip (x->y or z->y forbidden, y->x or y->z required) in every priority, and the
+per-rule skip in Meek (orienting a->b forbidden, or b->a required), as causal-learn 0.1.3.3
+publishes them (PC.py / BackGroundKnowledgeOrientUtils.py / UCSepset.py / Meek.py, not vendored).
 """
 from __future__ import annotations
 
@@ -100,10 +106,53 @@ class _G:
                 and self.graph[p[0][1], p[1][1]] == 0]
 
 
-def uc_sepset_priority2(G: _G, sepset_has) -> None:
+class _NoKnowledge:
+    def forbidden(self, i, j):
+        return False
+
+    def required(self, i, j):
+        return False
+
+
+class _Knowledge:
+    def __init__(self, forbidden, required):
+        self.F, self.R = np.asarray(forbidden, bool), np.asarray(required, bool)
+
+    def forbidden(self, i, j):
+        return bool(self.F[i, j])
+
+    def required(self, i, j):
+        return bool(self.R[i, j])
+
+
+def orient_by_background_knowledge(G: _G, bk) -> None:
+    for (a, b) in G.get_graph_edges():
+        if not G.is_undirected(a, b):
+            continue
+        if bk.forbidden(b, a):
+            G.remove_edge(a, b)
+            G.add_directed(a, b)
+        elif bk.forbidden(a, b):
+            G.remove_edge(a, b)
+            G.add_directed(b, a)
+        elif bk.required(b, a):
+            G.remove_edge(a, b)
+            G.add_directed(b, a)
+        elif bk.required(a, b):
+            G.remove_edge(a, b)
+            G.add_directed(a, b)
+
+
+def _collider_blocked(bk, x, y, z):
+    return bk.forbidden(x, y) or bk.forbidden(z, y) or bk.required(y, x) or bk.required(y, z)
+
+
+def uc_sepset_priority2(G: _G, sepset_has, bk=_NoKnowledge()) -> None:
     UT = [(i, j, k) for (i, j, k) in G.find_unshielded_triples() if i < k]
     for (x, y, z) in UT:
         if sepset_has(x, z, y):
+            continue
+        if _collider_blocked(bk, x, y, z):
             continue
         if (not G.is_fully_directed(y, x)) and (not G.is_fully_directed(y, z)):
             if G.graph[x, y] != 0:
@@ -132,7 +181,7 @@ def find_cond_sets(G: _G, i, j):
     return list_union(powerset(ni), powerset(nj))
 
 
-def uc_sepset_priority34(G: _G, sepset_has, ci_test, priority: int) -> None:
+def uc_sepset_priority34(G: _G, sepset_has, ci_test, priority: int, bk=_NoKnowledge()) -> None:
     """uc_sepset(priority=3 | 4) [U]: R0 = candidates in UT order; score each by the max
     p-value of ``ci_test(x, z, S)`` over ``find_cond_sets_without_mid`` (3) or
     ``_with_mid`` (4) (GraphClass.py:198-204); stable sort ascending (3) / descending (4);
@@ -145,6 +194,8 @@ def uc_sepset_priority34(G: _G, sepset_has, ci_test, priority: int) -> None:
         UC[(x, y, z)] = max([ci_test(x, z, S) for S in cond])
     UC = dict(sorted(UC.items(), key=lambda item: item[1], reverse=(priority == 4)))
     for (x, y, z) in UC.keys():
+        if _collider_blocked(bk, x, y, z):
+            continue
         if (not G.is_fully_directed(y, x)) and (not G.is_fully_directed(y, z)):
             if G.graph[x, y] != 0:
                 G.remove_edge(x, y)
@@ -154,13 +205,15 @@ def uc_sepset_priority34(G: _G, sepset_has, ci_test, priority: int) -> None:
             G.add_directed(z, y)
 
 
-def meek(G: _G) -> None:
+def meek(G: _G, bk=_NoKnowledge()) -> None:
     UT, Tri, Kite = G.find_unshielded_triples(), G.find_triangles(), G.find_kites()
     loop = True
     while loop:
         loop = False
         for (i, j, k) in UT:
             if G.is_fully_directed(i, j) and G.is_undirected(j, k):
+                if bk.forbidden(j, k) or bk.required(k, j):
+                    continue
                 if G.is_ancestor_of(k, j):
                     continue
                 G.remove_edge(j, k)
@@ -168,6 +221,8 @@ def meek(G: _G) -> None:
                 loop = True
         for (i, j, k) in Tri:
             if G.is_fully_directed(i, j) and G.is_fully_directed(j, k) and G.is_undirected(i, k):
+                if bk.forbidden(i, k) or bk.required(k, i):
+                    continue
                 if G.is_ancestor_of(k, i):
                     continue
                 G.remove_edge(i, k)
@@ -176,6 +231,8 @@ def meek(G: _G) -> None:
         for (i, j, k, l) in Kite:
             if (G.is_undirected(i, j) and G.is_undirected(i, k) and G.is_fully_directed(j, l)
                     and G.is_fully_directed(k, l) and G.is_undirected(i, l)):
+                if bk.forbidden(i, l) or bk.required(l, i):
+                    continue
                 if G.is_ancestor_of(l, i):
                     continue
                 G.remove_edge(i, l)
@@ -183,17 +240,22 @@ def meek(G: _G) -> None:
                 loop = True
 
 
-def orient(skeleton_adj: np.ndarray, sepset, priority: int = 2, ci_test=None) -> np.ndarray:
+def orient(skeleton_adj: np.ndarray, sepset, priority: int = 2, ci_test=None, knowledge=None) -> np.ndarray:
     """``sepset``: n x n object array of lists of tuples (reference layout);
-    ``ci_test(x, z, S) -> p`` is needed for priority 3 / 4."""
+    ``ci_test(x, z, S) -> p`` is needed for priority 3 / 4; ``knowledge=(forbidden, required)``."""
     G = _G(np.where(skeleton_adj, -1, 0))
+    bk = _NoKnowledge() if knowledge is None else _Knowledge(*knowledge)
 
     def has(x, z, y):
         return not all(y not in S for S in sepset[x, z])
 
+    # uc_sepset's candidate list comes from its deepcopy of the graph after the background
+    # orientation; the triples depend on adjacency only, which that orientation keeps
+    if knowledge is not None:
+        orient_by_background_knowledge(G, bk)
     if priority == 2:
-        uc_sepset_priority2(G, has)
+        uc_sepset_priority2(G, has, bk)
     else:
-        uc_sepset_priority34(G, has, ci_test, priority)
-    meek(G)
+        uc_sepset_priority34(G, has, ci_test, priority, bk)
+    meek(G, bk)
     return G.graph

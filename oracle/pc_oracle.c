@@ -256,11 +256,14 @@ static int build_lists(const uint64_t *adj, int n, int W, int32_t *deg, int32_t 
  *                        whose decision north_star allows to differ; enumerated like the engine)
  * max_depth < 0: unlimited. nthreads <= 0: all. st->secs: wall time per depth.
  */
-int orc_skeleton(const double *C, int n, int N, double alpha, int max_depth,
-                 int8_t *removed_level, int32_t *deg_at_level, uint64_t *side_union,
-                 orc_record *rec, int64_t rec_cap, int64_t *rec_count,
-                 orc_record *nearl, int64_t near_cap, int64_t *near_count,
-                 orc_stats *st, int nthreads) {
+/* banned (NULL ok): n x n pairs forbidden in both directions by background knowledge; queued
+ * for removal at the end of depth 0 beside the tests' own decisions (SkeletonDiscovery.py:86-106,
+ * stable branch: every visit at every depth queues them, so they are gone after depth 0). */
+int orc_skeleton_bk(const double *C, int n, int N, double alpha, int max_depth,
+                    int8_t *removed_level, int32_t *deg_at_level, uint64_t *side_union,
+                    orc_record *rec, int64_t rec_cap, int64_t *rec_count,
+                    orc_record *nearl, int64_t near_cap, int64_t *near_count,
+                    orc_stats *st, int nthreads, const uint8_t *banned) {
     const int W = (n + 63) / 64;
     uint64_t *adj = (uint64_t *)calloc((size_t)n * W, sizeof(uint64_t));
     int32_t *deg = (int32_t *)malloc(sizeof(int32_t) * n);
@@ -297,6 +300,10 @@ int orc_skeleton(const double *C, int n, int N, double alpha, int max_depth,
         st->calls[depth] = calls;
         st->indep[depth] = indep;
         st->levels = depth + 1;
+        if (banned && depth == 0)
+            for (int x = 0; x < n; ++x)
+                for (int y = 0; y < n; ++y)
+                    if (x != y && banned[(size_t)x * n + y]) rm[(size_t)x * n + y] = 1;
         for (int x = 0; x < n; ++x)
             for (int y = 0; y < n; ++y)
                 if (rm[(size_t)x * n + y]) {
@@ -308,6 +315,15 @@ int orc_skeleton(const double *C, int n, int N, double alpha, int max_depth,
     st->error = error;
     free(adj); free(deg); free(nbr); free(rm);
     return error ? 1 : 0;
+}
+
+int orc_skeleton(const double *C, int n, int N, double alpha, int max_depth,
+                 int8_t *removed_level, int32_t *deg_at_level, uint64_t *side_union,
+                 orc_record *rec, int64_t rec_cap, int64_t *rec_count,
+                 orc_record *nearl, int64_t near_cap, int64_t *near_count,
+                 orc_stats *st, int nthreads) {
+    return orc_skeleton_bk(C, n, N, alpha, max_depth, removed_level, deg_at_level, side_union, rec, rec_cap,
+                           rec_count, nearl, near_cap, near_count, st, nthreads, NULL);
 }
 
 /* CPU-baseline sample of one depth: the visits of nodes x0, x0+xstep, ... at depth d on the

@@ -48,9 +48,12 @@ class SkeletonResult:
 
 
 def skeleton_discovery(C: np.ndarray, N: int, alpha: float = 0.05, stable: bool = True,
-                       max_depth: int = -1, pvalue=None) -> SkeletonResult:
-    """Run the restated loop on a correlation matrix ``C`` (n x n) for ``N`` samples."""
+                       max_depth: int = -1, pvalue=None, forbidden=None) -> SkeletonResult:
+    """Run the restated loop on a correlation matrix ``C`` (n x n) for ``N`` samples.
+    ``forbidden``: n x n bool (background knowledge, x -> y forbidden); a pair forbidden both
+    ways is queued for removal at every visit while its tests still run (``:86-106``, stable)."""
     assert 0 < alpha < 1
+    assert forbidden is None or stable, "background knowledge is restated for the stable branch only"
     n = C.shape[0]
     pvalue = pvalue or (lambda x, y, S: fisherz.pvalue(C, N, x, y, S))
     g = np.ones((n, n), dtype=bool)
@@ -84,6 +87,9 @@ def skeleton_discovery(C: np.ndarray, N: int, alpha: float = 0.05, stable: bool 
                 continue
             for y in Neigh_x:
                 sepsets = set()
+                if forbidden is not None and forbidden[x, y] and forbidden[y, x]:
+                    edge_removal.append((x, y))
+                    edge_removal.append((y, x))
                 Neigh_x_noy = np.delete(Neigh_x, np.where(Neigh_x == y))
                 for S in combinations(Neigh_x_noy, depth):
                     p = ci_test(x, y, S)

@@ -124,6 +124,8 @@ SIGNATURES = [
     ("pcg_orient", I32, [I64, P, P, P, I64, ctypes.c_int, P]),
     ("pcg_uc_candidates", I32, [I64, P, P, P, I64, P, I64, ctypes.POINTER(I64)]),
     ("pcg_orient_triples", I32, [I64, P, P, I64, P]),
+    ("pcg_orient_bk", I32, [I64, P, P, P, I64, ctypes.c_int, P, P, I64, P, P, P]),
+    ("pcg_set_forbidden_pairs", I32, [P, P]),
     ("pcg_fisherz_batch", I32, [P, P, I64, I64, I64, P, I32, I64, P, P]),
     ("pcg_chisq_batch", I32, [P, P, I64, I64, P, P, I32, I64, ctypes.c_int, I64, P, P, P]),
 ]

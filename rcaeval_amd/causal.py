@@ -21,6 +21,7 @@ from itertools import combinations
 import numpy as np
 
 from . import _lib
+from .background import BackgroundKnowledge, banned_pairs
 from .citest import CITester, uc_orient
 from .engine import SkeletonOut, get_engine, orient
 from .skeleton_seq import skeleton_unstable
@@ -174,7 +175,8 @@ class SepsetArray:
 MAX_P_VALUE_CALLS = 20_000_000
 
 
-def p_values_from_run(out: SkeletonOut, C, N: int, alpha: float, device: int | None = None) -> np.ndarray:
+def p_values_from_run(out: SkeletonOut, C, N: int, alpha: float, device: int | None = None,
+                      banned=None) -> np.ndarray:
     """``cg.p_values`` of a stable run (``SkeletonDiscovery.py:131-132``): for every visit of
     x -> y at every depth, the p of each dependent S in ``combinations`` order.
 
@@ -193,7 +195,7 @@ def p_values_from_run(out: SkeletonOut, C, N: int, alpha: float, device: int | N
     L = out.levels
     rer = eng.skeleton(C, N, alpha=alpha, max_depth=L - 1,
                        flags=_lib.PCG_FLAG_FULL_P | _lib.PCG_FLAG_RECORD,
-                       record_capacity=max(int(sum(out.stats["tests"])), 1))
+                       record_capacity=max(int(sum(out.stats["tests"])), 1), banned=banned)
     cache: dict = {}
     for r in rer.records:
         d = int(r["d"])
@@ -242,10 +244,10 @@ class CausalGraph:
     ``p_values`` is built on first access (``p_values_from_run``) for stable runs."""
 
     def __init__(self, graph: np.ndarray, names, skeleton: SkeletonOut | None, C=None, N: int = 0,
-                 alpha: float = 0.05, device: int | None = None):
+                 alpha: float = 0.05, device: int | None = None, banned=None):
         self.G = GeneralGraph(graph, names)
         self.skeleton = skeleton
-        self._run = (C, int(N), float(alpha), device)
+        self._run = (C, int(N), float(alpha), device, banned)
         ci = CITester(C, N, device=device) if (skeleton is not None and C is not None) else None
         self.sepset = (SepsetArray(skeleton, ci, alpha) if skeleton is not None
                        else np.empty(graph.shape, object))
@@ -257,8 +259,8 @@ class CausalGraph:
     @property
     def p_values(self) -> np.ndarray:
         if self._p_values is None:
-            C, N, alpha, device = self._run
-            self._p_values = p_values_from_run(self.skeleton, C, N, alpha, device)
+            C, N, alpha, device, banned = self._run
+            self._p_values = p_values_from_run(self.skeleton, C, N, alpha, device, banned)
         return self._p_values
 
     @p_values.setter
@@ -276,16 +278,20 @@ def _check_supported(indep_test, stable, uc_rule, uc_priority, mvpc, background_
         raise NotImplementedError("uc_rule != 0 is not on the pc_pagerank / pc_randomwalk path")
     if uc_priority not in (-1, 2, 3, 4):
         raise NotImplementedError(f"uc_priority={uc_priority}: priorities 2, 3 (= -1, the default) and 4 are built")
-    if background_knowledge is not None:
-        raise NotImplementedError("background_knowledge is a later-round item")
+    if background_knowledge is not None and not isinstance(background_knowledge, BackgroundKnowledge):
+        raise TypeError("'background_knowledge' must be 'BackgroundKnowledge' type!")
+    if background_knowledge is not None and not stable:
+        raise NotImplementedError("background_knowledge with stable=False is not on the RCAEval path "
+                                  "(pc_default passes it to the stable run only)")
 
 
 def skeleton_from_data(data: np.ndarray, alpha: float = 0.05, max_depth: int = -1, flags: int = 0,
-                       device: int | None = None, record_capacity: int = 0):
+                       device: int | None = None, record_capacity: int = 0, banned=None):
     """Correlation + stable skeleton on the GPU; returns (SkeletonOut, C tensor)."""
     eng = get_engine(device)
     X = np.asarray(data, dtype=np.float64)
-    return eng.corr_skeleton(X, alpha=alpha, max_depth=max_depth, flags=flags, record_capacity=record_capacity)
+    return eng.corr_skeleton(X, alpha=alpha, max_depth=max_depth, flags=flags, record_capacity=record_capacity,
+                             banned=banned)
 
 
 def pc(data: np.ndarray, alpha: float = 0.05, indep_test=fisherz, stable: bool = True, uc_rule: int = 0,
@@ -327,12 +333,14 @@ def pc(data: np.ndarray, alpha: float = 0.05, indep_test=fisherz, stable: bool =
         cg.PC_elapsed = time.time() - start
         return cg
     flags = _lib.PCG_FLAG_FULL_P if full_p else 0
-    out, C = skeleton_from_data(X, alpha=alpha, max_depth=max_depth, flags=flags, device=device)
-    if priority == 2:
+    knowledge = background_knowledge.masks(names) if background_knowledge is not None else None
+    banned = None if knowledge is None else banned_pairs(knowledge[0])
+    out, C = skeleton_from_data(X, alpha=alpha, max_depth=max_depth, flags=flags, device=device, banned=banned)
+    if priority == 2 and knowledge is None:
         graph = orient(out.adj, out.sep_xy, out.sep_bits, priority=2).astype(int)
     else:
-        ci = CITester(C, X.shape[0], device=device)
-        graph = uc_orient(out.adj, out.sep_xy, out.sep_bits, priority, ci).astype(int)
-    cg = CausalGraph(graph, names, out, C=C, N=X.shape[0], alpha=alpha, device=device)
+        ci = CITester(C, X.shape[0], device=device) if priority != 2 else None
+        graph = uc_orient(out.adj, out.sep_xy, out.sep_bits, priority, ci, knowledge=knowledge).astype(int)
+    cg = CausalGraph(graph, names, out, C=C, N=X.shape[0], alpha=alpha, device=device, banned=banned)
     cg.PC_elapsed = time.time() - start
     return cg

@@ -21,7 +21,7 @@ from itertools import chain, combinations
 import numpy as np
 
 from . import _lib
-from .engine import get_engine, orient, orient_triples, uc_candidates
+from .engine import get_engine, orient, orient_bk, orient_triples, uc_candidates
 
 # upper bound on the tests one priority-3/4 orientation may issue (the power sets of two
 # neighbourhoods grow as 2^deg; the reference would not finish either)
@@ -102,9 +102,13 @@ class CITester:
 
 
 def uc_orient(adj: np.ndarray, sep_xy: np.ndarray, sep_bits: np.ndarray, priority: int,
-              ci: CITester | None = None) -> np.ndarray:
-    """``uc_sepset(cg, priority)`` then ``meek`` → endpoint-code matrix (int32)."""
+              ci: CITester | None = None, knowledge: tuple | None = None) -> np.ndarray:
+    """``uc_sepset(cg, priority)`` then ``meek`` → endpoint-code matrix (int32).
+    ``knowledge=(forbidden, required)`` masks (``BackgroundKnowledge.masks``): the run goes through
+    ``orient_by_background_knowledge`` first and both steps skip what the masks rule out."""
     if priority == 2:
+        if knowledge is not None:
+            return orient_bk(adj, sep_xy, sep_bits, *knowledge, priority=2)
         return orient(adj, sep_xy, sep_bits, priority=2)
     if priority not in (3, 4):
         raise NotImplementedError(f"uc_priority={priority}: priorities 2, 3 and 4 are built")
@@ -124,6 +128,8 @@ def uc_orient(adj: np.ndarray, sep_xy: np.ndarray, sep_bits: np.ndarray, priorit
     p = ci.pvalues(tests)
     score = [max(p[a:b]) for (a, b) in spans]
     order = sorted(range(len(score)), key=lambda q: score[q], reverse=with_mid)   # stable, like sorted(dict)
+    if knowledge is not None:
+        return orient_bk(adj, sep_xy, sep_bits, *knowledge, priority=priority, triples=R0, scores=score)
     return orient_triples(adj, R0[order] if len(order) else R0)
 
 

@@ -84,6 +84,7 @@ struct pcg_handle {
     PinBuf ctr_pin, deg_pin, off_pin, cpre_pin, status_pin;
     std::vector<uint64_t> binom_h;   // host copy of the binomial table
     uint8_t *rm_ext = nullptr;       // caller-owned removal-flag buffer (multi-GPU)
+    const uint8_t *banned = nullptr; // pcg_set_forbidden_pairs: n x n pairs removed at depth 0
     int64_t rm_ext_bytes = 0;
     int64_t rec_cap = 0, def_cap = 1 << 20, near_cap = 1 << 16, scr_cap = 1 << 20;
     int64_t rec_mod = 0, rec_res = 0;  // pcg_set_record_sample (0/1 = record every test)

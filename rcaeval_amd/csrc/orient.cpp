@@ -94,6 +94,15 @@ std::vector<std::pair<int32_t, int32_t>> find_adj(const Graph &G) {
     return adj;
 }
 
+// background knowledge [U] (causal-learn BackgroundKnowledge): directed relations i -> j
+struct BK {
+    int64_t n = 0;
+    const uint8_t *forb = nullptr, *req = nullptr;
+    bool forbidden(int64_t i, int64_t j) const { return forb && forb[i * n + j]; }
+    bool required(int64_t i, int64_t j) const { return req && req[i * n + j]; }
+    bool any() const { return forb || req; }
+};
+
 struct Triple { int32_t i, j, k; };
 struct Kite { int32_t i, j, k, l; };
 
@@ -157,10 +166,36 @@ std::vector<Triple> uc_candidates(const Graph &G, const Sepsets &sep) {
     return R0;
 }
 
+// orient_by_background_knowledge [U] (pc_alg, before uc_sepset): every undirected edge in
+// get_graph_edges order (node1 < node2): node1 -> node2 if node2 -> node1 is forbidden, else
+// node2 -> node1 if node1 -> node2 is forbidden, else the required direction
+void orient_by_bk(Graph &G, const BK &bk) {
+    for (int64_t i = 0; i < G.n; ++i)
+        for (int64_t j = i + 1; j < G.n; ++j) {
+            if (!G.is_undirected(i, j)) continue;
+            int64_t a = -1, b = -1;
+            if (bk.forbidden(j, i)) a = i, b = j;
+            else if (bk.forbidden(i, j)) a = j, b = i;
+            else if (bk.required(j, i)) a = j, b = i;
+            else if (bk.required(i, j)) a = i, b = j;
+            if (a < 0) continue;
+            G.remove_edge(i, j);
+            G.add_directed(a, b);
+        }
+}
+
+// uc_sepset's background-knowledge skip [U]: x->y or z->y forbidden, y->x or y->z required
+bool bk_blocks_collider(const BK &bk, int64_t x, int64_t y, int64_t z) {
+    return bk.forbidden(x, y) || bk.forbidden(z, y) || bk.required(y, x) || bk.required(y, z);
+}
+// Meek's skip [U]: orienting i->j is forbidden, or j->i is required
+bool bk_blocks(const BK &bk, int64_t i, int64_t j) { return bk.forbidden(i, j) || bk.required(j, i); }
+
 // the collider step shared by priorities 2, 3 and 4: x->y<-z unless y->x or y->z is fully directed
-void apply_colliders(Graph &G, const Triple *T, int64_t count) {
+void apply_colliders(Graph &G, const Triple *T, int64_t count, const BK &bk = BK()) {
     for (int64_t q = 0; q < count; ++q) {
         const int64_t x = T[q].i, y = T[q].j, z = T[q].k;
+        if (bk.any() && bk_blocks_collider(bk, x, y, z)) continue;
         if (!G.is_fully_directed(y, x) && !G.is_fully_directed(y, z)) {
             if (G.adjacent(x, y)) G.remove_edge(x, y);
             G.add_directed(x, y);
@@ -171,7 +206,7 @@ void apply_colliders(Graph &G, const Triple *T, int64_t count) {
 }
 
 // Meek.meek [U]: triple / triangle / kite lists computed once from cg_new = deepcopy(cg_2)
-void meek(Graph &G) {
+void meek(Graph &G, const BK &bk = BK()) {
     const int64_t n = G.n;
     const auto A = find_adj(G);
     const auto UT = enumerate_triples(G, A, [&](int32_t i, int32_t, int32_t k) { return G.at(i, k) == 0; });
@@ -203,6 +238,7 @@ void meek(Graph &G) {
             const int64_t i = t.i, j = t.j, k = t.k;
             if (G.is_fully_directed(i, j) && G.is_undirected(j, k)) {
                 if (!G.adjacent(j, k)) continue;
+                if (bk.any() && bk_blocks(bk, j, k)) continue;
                 if (G.is_ancestor_of(k, j)) continue;
                 G.remove_edge(j, k);
                 G.add_directed(j, k);
@@ -213,6 +249,7 @@ void meek(Graph &G) {
             const int64_t i = t.i, j = t.j, k = t.k;
             if (G.is_fully_directed(i, j) && G.is_fully_directed(j, k) && G.is_undirected(i, k)) {
                 if (!G.adjacent(i, k)) continue;
+                if (bk.any() && bk_blocks(bk, i, k)) continue;
                 if (G.is_ancestor_of(k, i)) continue;
                 G.remove_edge(i, k);
                 G.add_directed(i, k);
@@ -224,6 +261,7 @@ void meek(Graph &G) {
             if (G.is_undirected(i, j) && G.is_undirected(i, k) && G.is_fully_directed(j, l) &&
                 G.is_fully_directed(k, l) && G.is_undirected(i, l)) {
                 if (!G.adjacent(i, l)) continue;
+                if (bk.any() && bk_blocks(bk, i, l)) continue;
                 if (G.is_ancestor_of(l, i)) continue;
                 G.remove_edge(i, l);
                 G.add_directed(i, l);
@@ -279,6 +317,52 @@ extern "C" int pcg_orient_triples(int64_t n, const uint8_t *adj, const int32_t *
     init_graph(G, n, adj);
     apply_colliders(G, T.data(), tcount);
     meek(G);
+    for (int64_t i = 0; i < n * n; ++i) graph[i] = G.g[i];
+    return PCG_OK;
+}
+
+extern "C" int pcg_orient_bk(int64_t n, const uint8_t *adj, const int32_t *sep_xy, const uint64_t *sep_bits,
+                             int64_t count, int priority, const int32_t *triples, const double *scores,
+                             int64_t tcount, const uint8_t *forbidden, const uint8_t *required, int32_t *graph) {
+    if (n < 1 || !adj || !graph || (count > 0 && (!sep_xy || !sep_bits))) return PCG_ERR_INVALID;
+    if (priority != 2 && priority != 3 && priority != 4) return PCG_ERR_INVALID;
+    if (priority != 2 && (tcount < 0 || (tcount > 0 && (!triples || !scores)))) return PCG_ERR_INVALID;
+    BK bk;
+    bk.n = n;
+    bk.forb = forbidden;
+    bk.req = required;
+    Graph G;
+    init_graph(G, n, adj);
+    orient_by_bk(G, bk);
+    // uc_sepset works on its deepcopy of the oriented graph: R0 in that graph's
+    // find_unshielded_triples order (the set is the skeleton's, the order is not)
+    std::vector<Triple> R0 = uc_candidates(G, Sepsets(n, sep_xy, sep_bits, count));
+    if (priority != 2) {
+        // priorities 3 / 4: the caller scored the candidates (any order); stable sort by score,
+        // ascending (3) or descending (4), ties in R0 order (sort_dict_ascending)
+        std::unordered_map<uint64_t, double> score;
+        score.reserve((size_t)tcount * 2);
+        auto key = [n](int64_t i, int64_t j, int64_t k) { return ((uint64_t)i * n + j) * n + k; };
+        for (int64_t q = 0; q < tcount; ++q) {
+            const int64_t i = triples[3 * q], j = triples[3 * q + 1], k = triples[3 * q + 2];
+            if (i < 0 || j < 0 || k < 0 || i >= n || j >= n || k >= n) return PCG_ERR_INVALID;
+            score[key(i, j, k)] = scores[q];
+        }
+        std::vector<std::pair<double, Triple>> sc;
+        sc.reserve(R0.size());
+        for (const Triple &t : R0) {
+            auto it = score.find(key(t.i, t.j, t.k));
+            if (it == score.end()) return PCG_ERR_INVALID;
+            sc.push_back({it->second, t});
+        }
+        if (priority == 3)
+            std::stable_sort(sc.begin(), sc.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+        else
+            std::stable_sort(sc.begin(), sc.end(), [](const auto &a, const auto &b) { return a.first > b.first; });
+        for (size_t q = 0; q < sc.size(); ++q) R0[q] = sc[q].second;
+    }
+    apply_colliders(G, R0.data(), (int64_t)R0.size(), bk);
+    meek(G, bk);
     for (int64_t i = 0; i < n * n; ++i) graph[i] = G.g[i];
     return PCG_OK;
 }

@@ -186,10 +186,28 @@ class Engine:
         return self._collect(n, rl, st, 0.0)
 
     # ------------------------------------------------------------------ K2/K3
+    def _banned(self, banned, n: int):
+        """Device copy of the n x n uint8 banned-pair mask, registered with the handle (or None)."""
+        if banned is None:
+            return None
+        b = np.ascontiguousarray(banned, dtype=np.uint8)
+        if b.shape != (n, n):
+            raise ValueError(f"banned mask shape {b.shape} != ({n}, {n})")
+        bd = self.to_device(b)
+        check(self.h, self.lib.pcg_set_forbidden_pairs(self.h, ctypes.c_void_p(bd.data_ptr())),
+              "pcg_set_forbidden_pairs")
+        return bd
+
+    def _unban(self, bd) -> None:
+        if bd is not None:
+            self.lib.pcg_set_forbidden_pairs(self.h, None)
+
     def skeleton(self, C, N: int, alpha: float = 0.05, max_depth: int = -1, flags: int = 0,
-                 record_capacity: int = 0, record_sample: tuple = (0, 0)) -> SkeletonOut:
+                 record_capacity: int = 0, record_sample: tuple = (0, 0), banned=None) -> SkeletonOut:
         """``record_sample=(modulus, residue)``: with PCG_FLAG_RECORD keep only the tests of the
-        canonical pairs (a, b) with (a*n + b) % modulus == residue (full-size parity samples)."""
+        canonical pairs (a, b) with (a*n + b) % modulus == residue (full-size parity samples).
+        ``banned``: n x n mask of pairs removed at the end of depth 0 (background knowledge,
+        ``rcaeval_amd.background.banned_pairs``)."""
         torch = _torch()
         Cd = self.to_device(C)
         n = Cd.shape[0]
@@ -200,11 +218,15 @@ class Engine:
               "pcg_set_record_sample")
         st = PcgStats()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ev0.record()
-        rc = self.lib.pcg_skeleton(self.h, ctypes.c_void_p(Cd.data_ptr()), n, n, int(N), float(alpha),
-                                   int(max_depth), int(flags), ctypes.c_void_p(rl.data_ptr()),
-                                   ctypes.byref(st))
-        ev1.record()
+        bd = self._banned(banned, n)
+        try:
+            ev0.record()
+            rc = self.lib.pcg_skeleton(self.h, ctypes.c_void_p(Cd.data_ptr()), n, n, int(N), float(alpha),
+                                       int(max_depth), int(flags), ctypes.c_void_p(rl.data_ptr()),
+                                       ctypes.byref(st))
+            ev1.record()
+        finally:
+            self._unban(bd)
         check(self.h, rc, "pcg_skeleton")
         self.sync()
         t0 = time.perf_counter()
@@ -213,7 +235,8 @@ class Engine:
         out.extra["device_ms"] = out.device_ms
         return out
 
-    def corr_skeleton(self, X, alpha: float = 0.05, max_depth: int = -1, flags: int = 0, record_capacity: int = 0):
+    def corr_skeleton(self, X, alpha: float = 0.05, max_depth: int = -1, flags: int = 0, record_capacity: int = 0,
+                      banned=None):
         """K1 + stable skeleton in one C call (``pcg_pc_skeleton``); returns (SkeletonOut, C)."""
         torch = _torch()
         Xd = self.to_device(X)
@@ -225,11 +248,15 @@ class Engine:
         check(self.h, self.lib.pcg_set_record_sample(self.h, 0, 0), "pcg_set_record_sample")
         st = PcgStats()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ev0.record()
-        rc = self.lib.pcg_pc_skeleton(self.h, ctypes.c_void_p(Xd.data_ptr()), N, n, n, ctypes.c_void_p(C.data_ptr()),
-                                      n, float(alpha), int(max_depth), int(flags), ctypes.c_void_p(rl.data_ptr()),
-                                      ctypes.byref(st))
-        ev1.record()
+        bd = self._banned(banned, n)
+        try:
+            ev0.record()
+            rc = self.lib.pcg_pc_skeleton(self.h, ctypes.c_void_p(Xd.data_ptr()), N, n, n,
+                                          ctypes.c_void_p(C.data_ptr()), n, float(alpha), int(max_depth), int(flags),
+                                          ctypes.c_void_p(rl.data_ptr()), ctypes.byref(st))
+            ev1.record()
+        finally:
+            self._unban(bd)
         check(self.h, rc, "pcg_pc_skeleton")
         self.sync()
         t0 = time.perf_counter()
@@ -399,4 +426,34 @@ def orient(adj: np.ndarray, sep_xy: np.ndarray, sep_bits: np.ndarray, priority: 
                         g.ctypes.data_as(ctypes.c_void_p))
     if rc != 0:
         raise _lib.PcgError(rc, f"pcg_orient(priority={priority}) failed")
+    return g
+
+
+def orient_bk(adj: np.ndarray, sep_xy: np.ndarray, sep_bits: np.ndarray, forbidden: np.ndarray,
+              required: np.ndarray, priority: int = 2, triples: np.ndarray | None = None,
+              scores: np.ndarray | None = None) -> np.ndarray:
+    """Orientation with background knowledge (``pcg_orient_bk``): orient_by_background_knowledge,
+    then the collider step and Meek, both skipping what the knowledge rules out. Priorities 3/4
+    take the candidates' scores (``triples`` in any order); the ordering happens in C++ on the
+    candidate order of the oriented graph."""
+    lib = _lib.load()
+    n = adj.shape[0]
+    a = np.ascontiguousarray(adj, dtype=np.uint8)
+    xy = np.ascontiguousarray(sep_xy, dtype=np.int32)
+    bits = np.ascontiguousarray(sep_bits, dtype=np.uint64)
+    fb = np.ascontiguousarray(forbidden, dtype=np.uint8)
+    rq = np.ascontiguousarray(required, dtype=np.uint8)
+    if fb.shape != (n, n) or rq.shape != (n, n):
+        raise ValueError("forbidden / required masks must be n x n")
+    t = np.ascontiguousarray(np.asarray(triples if triples is not None else np.zeros((0, 3)), np.int32).reshape(-1, 3))
+    sc = np.ascontiguousarray(np.asarray(scores if scores is not None else np.zeros(0), np.float64).reshape(-1))
+    if len(sc) != len(t):
+        raise ValueError("one score per triple")
+    g = np.zeros((n, n), np.int32)
+    vp = ctypes.c_void_p
+    rc = lib.pcg_orient_bk(n, a.ctypes.data_as(vp), xy.ctypes.data_as(vp), bits.ctypes.data_as(vp), len(xy),
+                           int(priority), t.ctypes.data_as(vp), sc.ctypes.data_as(vp), len(t),
+                           fb.ctypes.data_as(vp), rq.ctypes.data_as(vp), g.ctypes.data_as(vp))
+    if rc != 0:
+        raise _lib.PcgError(rc, f"pcg_orient_bk(priority={priority}) failed")
     return g

@@ -2,20 +2,26 @@
 
 ``pc_default`` (``pc.py:12-21``) is the path used by ``pc_randomwalk`` and CIRCA:
 ``pc(data.to_numpy().astype(float), node_names=..., show_progress=False,
-background_knowledge=None)`` -> ``cg.G.graph``.
+background_knowledge=background_knowledge if with_bg else None)`` -> ``cg.G.graph``.
 """
 from __future__ import annotations
 
+from ..background import BackgroundKnowledge
 from ..causal import fisherz, pc
+
+# pc.py:6-9: memory / CPU metrics never cause a 50th-percentile latency, nothing causes a
+# frontend metric
+background_knowledge = BackgroundKnowledge()
+background_knowledge.add_forbidden_by_pattern(".*mem$", ".*lat50$")
+background_knowledge.add_forbidden_by_pattern(".*cpu$", ".*lat50$")
+background_knowledge.add_forbidden_by_pattern(".*", "frontend.*")
 
 
 def pc_default(data, show_progress=False, with_bg=False, **kwargs):
     """Endpoint-code adjacency (n x n int) of stable PC-fisherz (``pc.py:12-21``)."""
-    if with_bg:
-        raise NotImplementedError("with_bg=True (background-knowledge patterns, pc.py:6-9) is a later-round item")
     names = data.columns.to_list()
     cg = pc(data.to_numpy().astype(float), node_names=names, show_progress=show_progress,
-            background_knowledge=None)
+            background_knowledge=background_knowledge if with_bg else None)
     return cg.G.graph
 
 
@@ -36,4 +42,4 @@ def pc_fisherz(data):
               uc_priority=-1, background_knowledge=None, show_progress=False, node_names=node_names)
 
 
-__all__ = ["pc_default", "pc_fisherz_stable", "pc_fisherz", "fisherz"]
+__all__ = ["background_knowledge", "pc_default", "pc_fisherz_stable", "pc_fisherz", "fisherz"]

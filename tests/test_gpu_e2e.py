@@ -473,3 +473,50 @@ def test_rq2_run_other_pc_methods(tmp_path, method):
                                     n_iter=c["num_node"])["ranks"]
         got = rq2.load_json(os.path.join(out_dir, "results", c["result_name"]))["0"]
         assert got == want and len(got) > 0
+
+
+def _bg_frame(m, rows, seed):
+    """Telemetry frame whose names the reference's with_bg patterns hit: frontend services,
+    *_cpu / *_mem metrics and *_lat50 latencies."""
+    svcs = ["frontend", "cart", "checkout", "frontend-web", "ad", "shipping", "pay", "email",
+            "redis", "catalog", "currency", "reco", "user", "orders", "queue", "db", "cache"]
+    df = synth.telemetry_frame(m, rows, n_constant=0, seed=seed, services=svcs)
+    return df.rename(columns={c: c.replace("_latency", "_lat50") for c in df.columns})
+
+
+@pytest.mark.parametrize("m,rows,seed", [(12, 300, 60), (30, 600, 61), (49, 800, 62)])
+def test_pc_default_with_bg_matches_oracle(m, rows, seed):
+    """pc_default(with_bg=True) (graph_construction/pc.py:6-9,19): banned pairs leave the GPU
+    skeleton at depth 0, the knowledge-aware orientation runs in host C++; against the C-restated
+    skeleton with the same banned pairs + the Python-restated orientation with the same masks.
+    Parity unpinned [U] (no with_bg fixture in the reference, causal-learn not importable)."""
+    from oracle import cpc
+    from oracle import orient as oor
+    from rcaeval_amd.background import banned_pairs
+    from rcaeval_amd.causal import pc
+    from rcaeval_amd.graph_construction.pc import background_knowledge, pc_default
+    df = _bg_frame(m, rows, seed).drop(columns=["time"])
+    names = df.columns.to_list()
+    X = df.to_numpy().astype(float)
+    F, R = background_knowledge.masks(names)
+    B = banned_pairs(F)
+    assert B.any() and F.sum() > B.sum()
+    C = np.corrcoef(X.T)
+    r = cpc.skeleton(C, X.shape[0], banned=B)
+    n = len(names)
+    sep = np.empty((n, n), object)
+    for a in range(n):
+        for b in range(n):
+            u = set()
+            if a != b and r.removed_level[a, b] >= 1:
+                for (p_, q) in ((a, b), (b, a)):
+                    bits = r.side_union[p_, q]
+                    u |= {j for j in range(n) if (int(bits[j >> 6]) >> (j & 63)) & 1}
+            sep[a, b] = [tuple(u)]
+    want = oor.orient(r.adj, sep, knowledge=(F, R))
+    got = pc_default(df, with_bg=True)
+    np.testing.assert_array_equal(got, want)
+    cg = pc(X, node_names=names, background_knowledge=background_knowledge)
+    np.testing.assert_array_equal(cg.skeleton.removed_level, r.removed_level)
+    assert list(cg.stats["calls"])[: r.levels] == r.calls and list(cg.stats["tests"])[: r.levels] == r.tests
+    assert not np.array_equal(pc_default(df), got)          # the knowledge changed the graph

@@ -60,6 +60,14 @@ def _screen(C, x, y, T, c, N):
 def _screen_blocks(Cb, N):
     """Vectorised over (B, d+2, d+2) blocks ordered (x, y, c, T...): (dep32, ind32, dep64,
     ind64) as the kernel and decide() see them."""
+    v = _sweep(Cb, N)
+    return v["dep32"], v["ind32"], v["dep64"], v["ind64"]
+
+
+def _sweep(Cb, N):
+    """The kernel's arithmetic on (B, d+2, d+2) blocks ordered (x, y, c, T...) plus the fp64
+    truth on C: a dict of the fp32 values (cxx, cyy, cxy as the sweep forms them), nu, E,
+    the usability mask and both decisions."""
     B, m, _ = Cb.shape
     d = m - 2
     lo2, hi2, s = _thresholds(N, d)
@@ -136,7 +144,9 @@ def _screen_blocks(Cb, N):
     guard = (gmin > 0) & (den > 0) & (den - num > TAU / gmin)
     dep64 = guard & (num > hi2 * den)
     ind64 = guard & (num < lo2 * den)
-    return dep32, ind32, dep64, ind64
+    return {"dep32": dep32, "ind32": ind32, "dep64": dep64, "ind64": ind64, "ok": ok, "nu": nu,
+            "cxx32": cxx.astype(f).astype(np.float64), "cyy32": cyy.astype(np.float64), "cxy32": cxy.astype(np.float64),
+            "cxx64": cxx64, "cyy64": cyy64, "cxy64": cxy64}
 
 
 def _tests(C, rng, count, d=4):
@@ -210,3 +220,62 @@ def test_screen32_near_threshold():
     assert not np.any(ind32 & ~ind64)
     decided = dep32 | ind32
     assert decided[np.abs(delta) > 2e-2].mean() > 0.95
+
+
+def _err_ratio(Cb, N=10000):
+    """max over (c_xx, c_yy, c_xy) of |fp32 sweep value - fp64 value on C| / (K u (1 + nu)^2),
+    K = KE = 64 (the derived bound, DESIGN.md "fp32 screen: error bound"; the kernel's E is
+    2 KE u (1 + nu^2) >= this), per block; NaN where the candidate is unusable (ok false: the
+    test never reaches the fp32 decision)."""
+    with np.errstate(all="ignore"):
+        v = _sweep(Cb, N)
+        bound = KE * U32 * (1 + v["nu"]) ** 2
+        err = np.maximum.reduce([np.abs(v["cxx32"] - v["cxx64"]), np.abs(v["cyy32"] - v["cyy64"]),
+                                 np.abs(v["cxy32"] - v["cxy64"])])
+        r = err / bound
+    return np.where(v["ok"], r, np.nan)
+
+
+def _blocks_from(Z, eps):
+    """(B, 6, 6) correlation blocks Z Z^T + eps I (PSD), normalised to unit diagonal."""
+    G = Z @ np.swapaxes(Z, 1, 2) + eps[:, None, None] * np.eye(Z.shape[1])
+    s = 1.0 / np.sqrt(np.einsum("bii->bi", G))
+    return G * s[:, :, None] * s[:, None, :]
+
+
+def test_screen32_adversarial_error_ratio():
+    """Adversarial search for the worst fp32-sweep error relative to the bound the screen
+    relies on: blocks with near-collinear conditioning sets (nu up to the screen's cut-off,
+    te = E / s <= 1/2), x and y nearly determined by S (small c_xx, c_yy), entries placed a
+    half fp32 ulp from a rounding boundary; then a random hill-climb on the worst blocks. The
+    derived bound needs K ~ 18; KE = 64. The worst ratio found must stay < 1/2."""
+    rng = np.random.default_rng(2024)
+    B, r = 512, 6
+    worst = 0.0
+    # starting population: factor models with a nearly collinear T / c block
+    Z = rng.standard_normal((B, 6, r))
+    lam = 10.0 ** rng.uniform(-4, -0.5, (B, 1))
+    Z[:, 3, :] = Z[:, 2, :] + lam * rng.standard_normal((B, r))                  # T0 ~ c
+    Z[:, 4, :] = Z[:, 3, :] * 0.5 + Z[:, 2, :] * 0.5 + lam * rng.standard_normal((B, r))
+    Z[:, 0, :] = Z[:, 2, :] + 10.0 ** rng.uniform(-3, -1, (B, 1)) * rng.standard_normal((B, r))   # x ~ S
+    Z[:, 1, :] = Z[:, 4, :] + 10.0 ** rng.uniform(-3, -1, (B, 1)) * rng.standard_normal((B, r))   # y ~ S
+    eps = 10.0 ** rng.uniform(-6, -2, B)
+    score = np.nan_to_num(_err_ratio(_blocks_from(Z, eps)), nan=-1.0)
+    for it in range(300):
+        step = 10.0 ** rng.uniform(-4, -1, (B, 1, 1))
+        Zn = Z + step * rng.standard_normal(Z.shape)
+        en = eps * 10.0 ** rng.uniform(-0.3, 0.3, B)
+        Cn = _blocks_from(Zn, en)
+        if it % 3 == 2:        # push entries to just below / above an fp32 rounding boundary
+            f = Cn.astype(np.float32).astype(np.float64)
+            ulp = np.spacing(np.abs(f).astype(np.float32)).astype(np.float64)
+            Cn = f + np.sign(rng.standard_normal(Cn.shape)) * 0.4999 * ulp
+            Cn = 0.5 * (Cn + np.swapaxes(Cn, 1, 2))
+            np.einsum("bii->bi", Cn)[:] = 1.0
+        sn = np.nan_to_num(_err_ratio(Cn), nan=-1.0)
+        better = sn > score
+        Z[better], eps[better], score[better] = Zn[better], en[better], sn[better]
+        worst = max(worst, float(score.max()))
+    print(f"worst |err| / (KE u (1 + nu)^2) found: {worst:.4f} (usable blocks: {(score >= 0).mean():.2f})")
+    assert (score >= 0).mean() > 0.3, "search left the screen's usable region"
+    assert worst < 0.5, worst
