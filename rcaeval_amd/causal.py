@@ -78,7 +78,8 @@ class SepsetArray:
     LU path) — all of them at once, on first access of such an entry.
     """
 
-    def __init__(self, out: SkeletonOut, ci: "CITester | None" = None, alpha: float = 0.05):
+    def __init__(self, out: SkeletonOut, ci=None, alpha: float = 0.05):
+        """``ci``: a CITester, or a zero-argument callable that builds one on first need."""
         self.shape = (out.n, out.n)
         self._out = out
         self._levels = out.levels
@@ -115,7 +116,10 @@ class SepsetArray:
         if not todo:
             return order
         if self._ci is None:
-            raise RuntimeError("sepset insertion order needs the CI tester of the run")
+            raise RuntimeError("sepset insertion order needs the CI tester of the run "
+                               "(CausalGraph.release() dropped it)")
+        if not isinstance(self._ci, CITester):
+            self._ci = self._ci()
         tests, spans = [], []
         for (x, y, d, mem) in todo:
             subs = list(combinations(mem, d))
@@ -248,7 +252,10 @@ class CausalGraph:
         self.G = GeneralGraph(graph, names)
         self.skeleton = skeleton
         self._run = (C, int(N), float(alpha), device, banned)
-        ci = CITester(C, N, device=device) if (skeleton is not None and C is not None) else None
+        # the device correlation stays referenced only for what may still need it (the lazy
+        # p_values rerun and the sepset insertion order); the CI tester is built on first use
+        ci = (lambda: CITester(self._run[0], self._run[1], device=self._run[3])) \
+            if (skeleton is not None and C is not None) else None
         self.sepset = (SepsetArray(skeleton, ci, alpha) if skeleton is not None
                        else np.empty(graph.shape, object))
         self._p_values = None if (skeleton is not None and C is not None) else np.empty(graph.shape, object)
@@ -260,12 +267,22 @@ class CausalGraph:
     def p_values(self) -> np.ndarray:
         if self._p_values is None:
             C, N, alpha, device, banned = self._run
+            if C is None:
+                raise RuntimeError("p_values needs the run's correlation matrix (CausalGraph.release() dropped it)")
             self._p_values = p_values_from_run(self.skeleton, C, N, alpha, device, banned)
         return self._p_values
 
     @p_values.setter
     def p_values(self, value) -> None:
         self._p_values = value
+
+    def release(self) -> None:
+        """Drop the run's device correlation (n x n fp64) once ``G`` is all that is needed:
+        afterwards ``p_values`` (if not yet read) and large-union ``sepset`` orders raise."""
+        C, N, alpha, device, banned = self._run
+        self._run = (None, N, alpha, device, banned)
+        if isinstance(self.sepset, SepsetArray):
+            self.sepset._ci = None
 
 
 def _check_supported(indep_test, stable, uc_rule, uc_priority, mvpc, background_knowledge):

@@ -3865,6 +3865,7 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
         // fp32-screened depths: pcg_set_screen_precision, or the PCG_SCREEN_MASK A/B knob
         const char *sm = getenv("PCG_SCREEN_MASK");
         h->screen_eff = sm ? (int)strtol(sm, nullptr, 0) : (h->screen_mask < 0 ? PCG_TG_F32 : h->screen_mask);
+        h->screen_eff &= 0x1c;   // the error bound (KE = 64) is derived for d = 2..4 only
         std::vector<uint64_t> ns_of(maxd + 1, 0), units_of(maxd + 1, 0);
         std::vector<int> cls_of(maxd + 1, 2);
         double sum_small = 0.0, sum_wide = 0.0, sum_large = 0.0;

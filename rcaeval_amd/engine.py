@@ -193,7 +193,7 @@ class Engine:
         b = np.ascontiguousarray(banned, dtype=np.uint8)
         if b.shape != (n, n):
             raise ValueError(f"banned mask shape {b.shape} != ({n}, {n})")
-        bd = self.to_device(b)
+        bd = _torch().from_numpy(b).to(self.device)          # bytes, not to_device's float64
         check(self.h, self.lib.pcg_set_forbidden_pairs(self.h, ctypes.c_void_p(bd.data_ptr())),
               "pcg_set_forbidden_pairs")
         return bd

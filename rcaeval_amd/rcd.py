@@ -42,6 +42,8 @@ class ChiSqTester:
     """``cg.ci_test`` with chisq / gsq (``GraphClass.py:78-98`` cache key and call count) on the
     device; ``data`` are the integer codes of ``np.apply_along_axis(_unique, 0, data)``."""
 
+    MAX_CELLS = 1 << 26          # largest contingency table one device test builds
+
     def __init__(self, codes: np.ndarray, cardinalities: np.ndarray, g_sq: bool = False, device: int | None = None):
         import torch
         self.eng = get_engine(device)
@@ -68,27 +70,34 @@ class ChiSqTester:
             dmax = max(len(k[2]) for k in todo)
             if dmax > _lib.PCG_MAX_LEVEL_DEPTH:
                 raise NotImplementedError(f"conditioning set of size {dmax} > {_lib.PCG_MAX_LEVEL_DEPTH}")
-            rows = np.full((len(todo), 3 + max(dmax, 1)), -1, np.int32)
-            cells = 1
-            for r, (a, b, S) in enumerate(todo):
-                s = sorted(S)
-                rows[r, 0], rows[r, 1], rows[r, 2] = a, b, len(s)
-                rows[r, 3:3 + len(s)] = s
-                cells = max(cells, int(np.prod(self.card[s + [a, b]], dtype=np.float64)))
-            if cells > (1 << 26):
-                raise NotImplementedError(f"contingency table of {cells} cells")
-            stat, df, st = self.eng.chisq_batch(self.data, self.card_dev, self.N, self.n, rows, self.g_sq, cells)
-            with np.errstate(invalid="ignore"):
-                p = np.where(df > 0, chi2.sf(stat, np.maximum(df, 1)), 1.0)
-            for r, k in enumerate(todo):
-                self.cache[k] = (float(p[r]), int(st[r]))
+            # a table beyond MAX_CELLS is marked per test (status 4) instead of failing the batch:
+            # it raises only if the caller consumes that test (the reference may stop before it)
+            fits, cells = [], 1
+            for k in todo:
+                c = int(np.prod(self.card[sorted(k[2]) + [k[0], k[1]]], dtype=np.float64))
+                if c > self.MAX_CELLS:
+                    self.cache[k] = (float("nan"), 4)
+                else:
+                    fits.append(k)
+                    cells = max(cells, c)
+            if fits:
+                rows = np.full((len(fits), 3 + max(dmax, 1)), -1, np.int32)
+                for r, (a, b, S) in enumerate(fits):
+                    s = sorted(S)
+                    rows[r, 0], rows[r, 1], rows[r, 2] = a, b, len(s)
+                    rows[r, 3:3 + len(s)] = s
+                stat, df, st = self.eng.chisq_batch(self.data, self.card_dev, self.N, self.n, rows, self.g_sq, cells)
+                with np.errstate(invalid="ignore"):
+                    p = np.where(df > 0, chi2.sf(stat, np.maximum(df, 1)), 1.0)
+                for r, k in enumerate(fits):
+                    self.cache[k] = (float(p[r]), int(st[r]))
         got = [self.cache[k] for k in keys]
         return [g[0] for g in got], [g[1] for g in got]
 
     @staticmethod
     def raise_for(status: int) -> None:
         if status == 4:
-            raise NotImplementedError("contingency table too large for the device batch")
+            raise NotImplementedError(f"contingency table beyond {ChiSqTester.MAX_CELLS} cells")
         if status != 0:
             raise AssertionError("X, Y cannot be in condition_set.")
 
@@ -212,226 +221,222 @@ def skeleton_unstable_discrete(data: np.ndarray, alpha: float, labels=None, g_sq
     return cg
 
 
-# ---------------------------------------------------------------- rcd.py
+# ---------------------------------------------------------------- the RCD search (rcd.py)
+# Reference behaviour kept: every frame operation that decides values or column order, the two
+# numpy.random consumption points (create_chunks; local_skeleton_discovery per depth), the
+# in-place F-node column on the frames handed to run_psi_pc (``add_fnode_and_concat``), and the
+# quirks of the result (object-array argmax in the neighbour order, ``filter(None, mi)``).
+import re
+from typing import NamedTuple
+
+
+class PsiResult(NamedTuple):
+    """``run_psi_pc``'s 4-tuple (``rcd.py:121-208``): ranks, graph, mi labels, CI-test count."""
+    ranks: list
+    graph: object
+    mi: list
+    ci_tests: int
+
+
 def drop_constant(df):
-    """``rcd.py:31-32``."""
-    return df.loc[:, (df != df.iloc[0]).any()]
+    """Columns with some value different from the first row (``rcd.py:31-32``; NaN counts as
+    different)."""
+    return df.loc[:, df.ne(df.iloc[0]).any(axis=0)]
 
 
 def add_fnode_and_concat(normal_df, anomalous_df):
-    """``rcd.py:64-67`` (mutates both frames, like the reference)."""
+    """Label the windows ("0" normal, "1" anomalous) IN PLACE and stack them, normal first
+    (``rcd.py:64-67``)."""
     import pandas as pd
-    normal_df[F_NODE] = "0"
-    anomalous_df[F_NODE] = "1"
+    for frame, flag in ((normal_df, "0"), (anomalous_df, "1")):
+        frame[F_NODE] = flag
     return pd.concat([normal_df, anomalous_df])
 
 
-def run_pc(data, alpha, localized=False, labels=None, mi=(), verbose=False, device=None):
-    """``rcd.py:72-102``."""
-    if not labels:
-        labels = {i: name for i, name in enumerate(data.columns)}
-    np_data = data.to_numpy()
-    if localized:
-        return local_skeleton_discovery(np_data, np_data.shape[1] - 1, alpha, mi=mi, labels=labels, device=device)
-    return skeleton_unstable_discrete(np_data, alpha, labels=labels, device=device)
-
-
-def _order_neighbors(neigh, p_values):
-    """``rcd.py:211-222``."""
-    _neigh = neigh.copy()
-    _p_values = p_values.copy()
-    stack = []
-    while len(_neigh) != 0:
-        i = np.argmax(_p_values)
-        node = _neigh[i]
-        stack = [node] + stack
-        _neigh.remove(node)
-        _p_values = np.delete(_p_values, i)
-    return stack
-
-
 def _discretize(data, bins):
-    """``rcd.py:278-289`` (scikit-learn KBinsDiscretizer, k-means strategy, on the host)."""
+    """k-means binning of every column but the (last) F-node, all codes as int
+    (``rcd.py:278-289``, scikit-learn KBinsDiscretizer on the host)."""
     import warnings
 
     import pandas as pd
     from sklearn.preprocessing import KBinsDiscretizer
-    d = data.iloc[:, :-1]
-    discretizer = KBinsDiscretizer(n_bins=bins, encode="ordinal", strategy="kmeans")
+    values = data.iloc[:, :-1]
+    binner = KBinsDiscretizer(n_bins=bins, encode="ordinal", strategy="kmeans")
     with warnings.catch_warnings():
         warnings.simplefilter("ignore")
-        discretizer.fit(d)
-        disc_d = discretizer.transform(d)
-    disc_d = pd.DataFrame(disc_d, columns=d.columns.values.tolist())
-    disc_d[F_NODE] = data[F_NODE].tolist()
-    for c in disc_d:
-        disc_d[c] = disc_d[c].astype(int)
-    return disc_d
+        coded = binner.fit(values).transform(values)
+    out = pd.DataFrame(coded, columns=list(values.columns))
+    out[F_NODE] = list(data[F_NODE])
+    return out.astype({c: int for c in out.columns})
 
 
 def _preprocess_for_fnode(normal_df, anomalous_df, bins):
-    df = add_fnode_and_concat(normal_df, anomalous_df)
-    if df is None:
-        return None
-    return _discretize(df, bins) if bins is not None else df
+    joined = add_fnode_and_concat(normal_df, anomalous_df)
+    return joined if bins is None else _discretize(joined, bins)
+
+
+def run_pc(data, alpha, localized=False, labels=None, mi=(), verbose=False, device=None):
+    """Skeleton of the F-node frame (``rcd.py:72-102``): the localized search around the last
+    column (the F-node), or the full order-dependent skeleton."""
+    labels = labels or dict(enumerate(data.columns))
+    X = data.to_numpy()
+    if not localized:
+        return skeleton_unstable_discrete(X, alpha, labels=labels, device=device)
+    return local_skeleton_discovery(X, X.shape[1] - 1, alpha, mi=mi, labels=labels, device=device)
+
+
+def _order_neighbors(neigh, p_values):
+    """Repeatedly take the neighbour whose p-value list is largest (``np.argmax`` over the object
+    array of lists: lexicographic) and put it in front: the first taken ends last
+    (``rcd.py:211-222``)."""
+    pending, scores, taken = list(neigh), p_values.copy(), []
+    while pending:
+        k = int(np.argmax(scores))
+        taken.append(pending.pop(k))
+        scores = np.delete(scores, k)
+    return taken[::-1]
 
 
 def run_psi_pc(normal_df, anomalous_df, bins=None, mi=None, localized=False, start_alpha=None, min_nodes=-1,
-               verbose=False, device=None):
-    """``rcd.py:121-208``: the alpha sweep; returns (rc, graph, mi, no_ci)."""
-    if mi is None:
-        mi = []
-    if 0 in [len(normal_df.columns), len(anomalous_df.columns)]:
-        return ([], None, [], 0)
+               verbose=False, device=None) -> PsiResult:
+    """Psi-PC (``rcd.py:121-208``): raise alpha from ``start_alpha`` in steps of 0.1 below 1; each
+    run's new F-node children join the ranking, ordered by their p-values, until ``min_nodes``
+    (default: every variable) are ranked."""
+    if len(normal_df.columns) == 0 or len(anomalous_df.columns) == 0:
+        return PsiResult([], None, [], 0)
     data = _preprocess_for_fnode(normal_df, anomalous_df, bins)
-    if min_nodes == -1:
-        min_nodes = len(data.columns) - 1
-    assert min_nodes < len(data)
-    G = None
-    no_ci = 0
-    i_to_labels = {i: name for i, name in enumerate(data.columns)}
-    labels_to_i = {name: i for i, name in enumerate(data.columns)}
-    processed_mi = [labels_to_i.get(i) for i in mi]
-    rc = []
-    cg = None
-    _alpha = START_ALPHA if start_alpha is None else start_alpha
-    for i in np.arange(_alpha, ALPHA_LIMIT, ALPHA_STEP):
-        cg = run_pc(data, i, localized=localized, mi=processed_mi, labels=i_to_labels, verbose=verbose,
-                    device=device)
-        G = cg
-        no_ci += cg.no_ci_tests
-        f_neigh = cg.successors(data.shape[1] - 1)
-        new_neigh = [x for x in f_neigh if x not in rc]
-        if len(new_neigh) == 0:
+    names = list(data.columns)
+    fnode = len(names) - 1
+    target = fnode if min_nodes == -1 else min_nodes
+    assert target < len(data)
+    index_of = {nm: k for k, nm in enumerate(names)}
+    label_of = dict(enumerate(names))
+    mi_index = [index_of.get(v) for v in (mi or [])]
+    ranks, ci_total, cg = [], 0, None
+    first = START_ALPHA if start_alpha is None else start_alpha
+    for alpha in np.arange(first, ALPHA_LIMIT, ALPHA_STEP):
+        cg = run_pc(data, alpha, localized=localized, mi=mi_index, labels=label_of, device=device)
+        ci_total += cg.no_ci_tests
+        fresh = [v for v in cg.successors(fnode) if v not in ranks]
+        if not fresh:
             continue
-        f_p_values = cg.p_values[-1][[labels_to_i.get(key) for key in new_neigh]]
-        rc += _order_neighbors(new_neigh, f_p_values)
-        if len(rc) == min_nodes:
+        ranks += _order_neighbors(fresh, cg.p_values[-1][[index_of[v] for v in fresh]])
+        if len(ranks) == target:
             break
-    mi_out = [i_to_labels.get(i) for i in list(filter(None, cg.mi))] if cg is not None else []
-    return (rc, G, mi_out, no_ci)
+    # filter(None, ...) drops the unset slots and node index 0 alike (reference quirk)
+    mi_labels = [label_of.get(k) for k in filter(None, cg.mi)] if cg is not None else []
+    return PsiResult(ranks, cg, mi_labels, ci_total)
 
 
 def create_chunks(df, gamma):
-    """``rcd.py:307-315``."""
-    chunks = list()
-    names = np.random.permutation(df.columns)
-    for i in range(df.shape[1] // gamma + 1):
-        chunks.append(names[i * gamma:(i * gamma) + gamma])
+    """Random partition of the columns into runs of ``gamma`` (``rcd.py:307-315``); draws one
+    ``np.random.permutation``."""
+    order = np.random.permutation(df.columns)
+    chunks = [order[k:k + gamma] for k in range(0, (df.shape[1] // gamma + 1) * gamma, gamma)]
     if len(chunks[-1]) == 0:
         chunks.pop()
     return chunks
 
 
 def run_level(normal_df, anomalous_df, gamma, localized, bins, verbose, device=None):
-    """``rcd.py:318-375`` (phase 1: one Psi-PC per chunk of gamma variables)."""
-    ci_tests = 0
-    chunks = create_chunks(normal_df, gamma)
-    f_child_union = []
-    mi_union = []
-    for c in chunks:
-        rc, _, mi, ci = run_psi_pc(normal_df.loc[:, c], anomalous_df.loc[:, c], bins=bins, localized=localized,
-                                   start_alpha=LOCAL_ALPHA, min_nodes=1, verbose=verbose, device=device)
-        f_child_union += rc
-        mi_union += mi
-        ci_tests += ci
-    return f_child_union, mi_union, ci_tests
+    """Phase 1, one level (``rcd.py:318-375``): Psi-PC on each chunk from alpha 0.01 until one
+    F-node child is found; returns (children, mi labels, CI tests) over all chunks."""
+    children, mi_labels, ci_total = [], [], 0
+    for cols in create_chunks(normal_df, gamma):
+        res = run_psi_pc(normal_df.loc[:, cols], anomalous_df.loc[:, cols], bins=bins, localized=localized,
+                         start_alpha=LOCAL_ALPHA, min_nodes=1, verbose=verbose, device=device)
+        children.extend(res.ranks)
+        mi_labels.extend(res.mi)
+        ci_total += res.ci_tests
+    return children, mi_labels, ci_total
 
 
 def run_multi_phase(normal_df, anomalous_df, gamma, localized, bins, verbose, device=None):
-    """``rcd.py:378-446``."""
-    f_child_union = normal_df.columns
-    mi_union = []
-    prev = len(f_child_union)
+    """Phase 1 levels until at most ``gamma`` candidates remain or a level removes none, then
+    phase 2: a full Psi-PC ranking of the survivors (``rcd.py:378-446``; the mi collected in
+    phase 1 is discarded before phase 2, as there)."""
+    survivors = normal_df.columns
+    count = len(survivors)
     while True:
-        f_child_union, mi, ci_tests = run_level(normal_df.loc[:, f_child_union], anomalous_df.loc[:, f_child_union],
-                                                gamma, localized, bins, verbose, device=device)
-        mi_union += mi
-        len_child = len(f_child_union)
-        if len_child <= gamma or len_child == prev:
+        survivors, _, _ = run_level(normal_df.loc[:, survivors], anomalous_df.loc[:, survivors], gamma, localized,
+                                    bins, verbose, device=device)
+        if len(survivors) <= gamma or len(survivors) == count:
             break
-        prev = len(f_child_union)
-    mi_union = []
-    new_nodes = f_child_union
-    rc, _, mi, ci = run_psi_pc(normal_df.loc[:, new_nodes], anomalous_df.loc[:, new_nodes], bins=bins, mi=mi_union,
-                               localized=localized, verbose=verbose, device=device)
-    return rc
+        count = len(survivors)
+    return run_psi_pc(normal_df.loc[:, survivors], anomalous_df.loc[:, survivors], bins=bins, mi=[],
+                      localized=localized, verbose=verbose, device=device).ranks
 
 
-# sock-shop / real-outage preprocessing (rcd.py:36-55, 227-275)
-_rm_time = lambda df: df.loc[:, ~df.columns.isin(["time"])]   # noqa: E731
-
-
-def _list_intersection(l1, l2):
-    return [x for x in l1 if x in l2]
-
-
-def _match_columns(n_df, a_df):
-    cols = _list_intersection(n_df.columns, a_df.columns)
-    return (n_df[cols], a_df[cols])
-
-
-def _scale_down_mem(df):
-    def update_mem(x):
-        if not x.name.endswith("_mem"):
-            return x
-        x /= 1e6
-        x = x.astype(int)
-        return x
-    return df.apply(update_mem)
+# --- window cleaning before the search (rcd.py:36-55, 227-275, 466-483)
+_LAT_ANY = re.compile(r"lat_\d{2}$")
 
 
 def _select_lat(df, per):
-    return df.filter(regex=(r".*(?<!lat_\d{2})$|_lat_" + str(per) + "$"))
+    """Non-latency columns plus the ``_lat_<per>`` ones (``rcd.py:271-272``)."""
+    return df[[c for c in df.columns if _LAT_ANY.search(c) is None or c.endswith(f"_lat_{per}")]]
+
+
+def _scale_down_mem(df):
+    """``*_mem`` columns in MB, truncated to int (``rcd.py:259-268``)."""
+    out = df.copy()
+    for c in out.columns:
+        if c.endswith("_mem"):
+            out[c] = (out[c] / 1e6).astype(int)
+    return out
 
 
 def _select_useful_cols(df):
-    i = df.loc[:, df.columns != F_NODE].std() > 1
-    cols = i[i].index.tolist()
-    cols.append(F_NODE)
-    if len(cols) == 1:
+    """Columns whose std over both windows exceeds 1, F-node kept last; None when none is
+    (``rcd.py:240-251``)."""
+    wide = df.loc[:, df.columns != F_NODE].std() > 1
+    keep = [c for c, w in wide.items() if w] + [F_NODE]
+    if len(keep) == 1:
         return None
-    elif len(cols) == len(df.columns):
-        return df
-    return df[cols]
+    return df if len(keep) == len(df.columns) else df[keep]
+
+
+def _split_windows(normal_df, anomal_df, clean, select_useful):
+    """Clean each window, keep their common columns (normal's order), optionally the useful
+    ones, and split back on the F-node label."""
+    normal_df, anomal_df = clean(normal_df), clean(anomal_df)
+    common = [c for c in normal_df.columns if c in anomal_df.columns]
+    joined = add_fnode_and_concat(normal_df[common], anomal_df[common])
+    if select_useful is True:
+        joined = _select_useful_cols(joined)
+    flag = joined[F_NODE]
+    return joined[flag == "0"].drop(columns=[F_NODE]), joined[flag == "1"].drop(columns=[F_NODE])
 
 
 def preprocess_sock_shop(n_df, a_df, per, dk_select_useful=False):
-    _process = lambda df: _select_lat(_scale_down_mem(_rm_time(df)), per)   # noqa: E731
-    n_df = drop_constant(_process(n_df))
-    a_df = drop_constant(_process(a_df))
-    n_df, a_df = _match_columns(n_df, a_df)
-    df = add_fnode_and_concat(n_df, a_df)
-    if dk_select_useful is True:
-        df = _select_useful_cols(df)
-    n_df = df[df[F_NODE] == "0"].drop(columns=[F_NODE])
-    a_df = df[df[F_NODE] == "1"].drop(columns=[F_NODE])
-    return (n_df, a_df)
+    """Sock Shop / real-outage cleaning (``rcd.py:36-55``)."""
+    def clean(df):
+        return drop_constant(_select_lat(_scale_down_mem(df.loc[:, ~df.columns.isin(["time"])]), per))
+    return _split_windows(n_df, a_df, clean, dk_select_useful)
+
+
+def _preprocess_generic(n_df, a_df, dk_select_useful=False):
+    """Every other named dataset (``rcd.py:474-483``: time dropped, memory in MB, constants
+    dropped)."""
+    return _split_windows(n_df, a_df, lambda df: _drop_constant_ts(convert_mem_mb(drop_time(df))),
+                          dk_select_useful)
 
 
 def rcd(data, inject_time, dk_select_useful=False, gamma=5, localized=True, bins=5, verbose=False, dataset=None,
         seed=None, device=None, **kwargs):
-    """``rcd.py:449-493``: returns ``{"ranks": rc}``."""
+    """``rcd.py:449-493``: split at ``inject_time``, clean per dataset, seed the global stream,
+    run both phases; returns ``{"ranks": ...}``."""
     normal_df = data[data["time"] < inject_time]
     anomal_df = data[data["time"] >= inject_time]
     if dk_select_useful is True:
-        normal_df = drop_extra(normal_df)
-        anomal_df = drop_extra(anomal_df)
+        normal_df, anomal_df = drop_extra(normal_df), drop_extra(anomal_df)
     if dataset == "sock-shop":
         normal_df, anomal_df = preprocess_sock_shop(normal_df, anomal_df, 90, dk_select_useful)
     elif dataset is not None:
-        normal_df = _drop_constant_ts(convert_mem_mb(drop_time(normal_df)))
-        anomal_df = _drop_constant_ts(convert_mem_mb(drop_time(anomal_df)))
-        normal_df, anomal_df = _match_columns(normal_df, anomal_df)
-        df = add_fnode_and_concat(normal_df, anomal_df)
-        if dk_select_useful is True:
-            df = _select_useful_cols(df)
-        normal_df = df[df[F_NODE] == "0"].drop(columns=[F_NODE])
-        anomal_df = df[df[F_NODE] == "1"].drop(columns=[F_NODE])
+        normal_df, anomal_df = _preprocess_generic(normal_df, anomal_df, dk_select_useful)
     if seed is not None:
         np.random.seed(seed)
-    rc = run_multi_phase(normal_df, anomal_df, gamma, localized, bins, verbose, device=device)
-    return {"ranks": rc}
+    return {"ranks": run_multi_phase(normal_df, anomal_df, gamma, localized, bins, verbose, device=device)}
 
 
-__all__ = ["rcd", "ChiSqTester", "local_skeleton_discovery", "run_psi_pc", "run_multi_phase"]
+__all__ = ["rcd", "ChiSqTester", "local_skeleton_discovery", "run_psi_pc", "run_multi_phase", "run_level",
+           "create_chunks", "PsiResult"]

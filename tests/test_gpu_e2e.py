@@ -520,3 +520,17 @@ def test_pc_default_with_bg_matches_oracle(m, rows, seed):
     np.testing.assert_array_equal(cg.skeleton.removed_level, r.removed_level)
     assert list(cg.stats["calls"])[: r.levels] == r.calls and list(cg.stats["tests"])[: r.levels] == r.tests
     assert not np.array_equal(pc_default(df), got)          # the knowledge changed the graph
+
+
+def test_causal_graph_release_drops_the_correlation():
+    """pc() keeps the device C only for lazy p_values / sepset order; release() drops it."""
+    from rcaeval_amd.causal import pc
+    X = synth.gaussian_sem(10, 400, seed=3)
+    cg = pc(X)
+    g = cg.G.graph.copy()
+    assert cg._run[0] is not None and not hasattr(cg.sepset._ci, "pvalues_status")   # tester not built yet
+    cg.release()
+    assert cg._run[0] is None and cg.sepset._ci is None
+    np.testing.assert_array_equal(cg.G.graph, g)
+    with pytest.raises(RuntimeError):
+        cg.p_values
