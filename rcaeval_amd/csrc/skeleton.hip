@@ -119,7 +119,6 @@ struct LevelArgs {
     int64_t chunk_lo;            // first chunk of this launch (within its class)
     int spl;                     // S ranks per lane (LDS-resident kernel)
     int lds_btab_off;            // byte offset of the LDS binomial table (LDS-resident kernel)
-    int lds_batch_off;           // k_level_ty: byte offset of the per-wave task batches
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -2447,509 +2446,6 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
     block_flush_counts(a.ctr, tests, indep);
 }
 
-// ---------------------------------------------------------------------------------------
-// y-parallel form of the fp32-screened T-group sweep (threshold mode, depths 2..4, D <= 64;
-// the default for the narrow class since round 3). Same tests, same arithmetic and the same
-// task set as k_level_lds_f — a task is a (d-1)-subset T of adj(x) with a group of TG = 6
-// candidates c < min(T) — but the roles of lanes and loop are swapped:
-//   phase A (per wave, a batch of 32 tasks): two lanes per task build the task's constants
-//     (L_T^-1, u_T in fp64 on A~ -> fp32; each candidate's Cholesky row and decision bounds,
-//     three candidates per lane) and leave them in the wave's LDS batch area;
-//   phase B (per task, wave-uniform): LANES ARE THE y's (lane t = neighbour t), the task's
-//     constants are LDS broadcasts. v_T(y) = L_T^-1 A~[T][y], b_yy, b_xy are formed once per
-//     (T, y) and reused by every group of the same T (tasks of one T are consecutive), and
-//     each candidate pair costs the sweep's 11 packed instructions for every y at once.
-// The per-y work of k_level_lds_f (~22 instructions: the T projection, addressing, masks)
-// is paid once per T instead of once per (task, y); the candidate setup runs with every lane
-// busy (two lanes per task) and its registers die before phase B (no spills at 3 blocks per
-// CU); partial candidate groups cost only their pairs. The bookkeeping is wave-uniform:
-// per candidate the live lanes are (y < D) & ~T & ~{c} & ~(own_T & adj(c)) — own_T = lanes
-// y < x with T in adj(y), adj(c) = the local adjacency row of c read as a lane mask (the
-// reference's memo: (x, y, S) is y's test when y < x and S is in adj(y)) — and the test
-// count is its popcount. The dependence check, the rare path (certain independence in
-// fp32, else the fp64 screen list) and their fp32 values are k_level_lds_f's, operation for
-// operation, so the decisions are the same.
-#ifndef PCG_TY_MINB
-#define PCG_TY_MINB 3
-#endif
-constexpr int TY_BATCH = 32;                          // tasks per phase-A batch (two lanes each)
-constexpr int TY_DS = 64;                             // LDS row stride of A~ (floats): compile-time offsets
-// LDS bytes before the binomial table: 3 mask arrays, A~ rows, {A~_yy, A~_xy}, ids, tx
-__host__ __device__ constexpr int ty_core_bytes(int D) { return 3 * 64 * 8 + D * TY_DS * 4 + 2 * 64 * 4 + 64 * 4 + 16; }
-constexpr int TY_TF = 10;                             // words per task: L_T^-1 (lower, 6) + u_T (3) + pad
-constexpr int TY_PAIR = 18;                           // floats per candidate pair (9 f2v)
-// per task: 2 ints (T packed, cbase | nval << 8 | okm << 16), TY_TF floats, 3 pairs (8-byte aligned)
-constexpr int TY_TASK_WORDS = 2 + TY_TF + 3 * TY_PAIR;
-static_assert(TY_TASK_WORDS % 2 == 0 && (2 + TY_TF) % 2 == 0, "packed pairs must be 8-byte aligned");
-constexpr int TY_WAVE_BYTES = TY_BATCH * TY_TASK_WORDS * 4;
-
-// a wave-uniform 64-bit value held in VGPRs (an LDS broadcast) as a scalar
-__device__ __forceinline__ unsigned long long uniform_u64(unsigned long long v) {
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
-    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-    return ((unsigned long long)hi << 32) | lo;
-}
-
-template <int DM>
-__global__ __launch_bounds__(256, PCG_TY_MINB) void k_level_ty(LevelArgs a) {
-    constexpr int DT = DM - 1;
-    constexpr int TG = tg_of_depth(DM);
-    static_assert(TG == 6, "k_level_ty: candidate groups of 6");
-    static_assert(DT >= 1 && DT <= 3, "k_level_ty: depths 2..4");
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, wv = tid >> 6;
-    const int64_t chunk = a.chunk_lo + blockIdx.x;
-    int lo = 0, hi = a.n;
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (a.cpre[mid] <= chunk) lo = mid; else hi = mid;
-    }
-    const int x = lo;
-    const int D = a.deg[x];
-    const int32_t *nxg = a.nbr + a.off[x];
-
-    constexpr int DS = TY_DS;                                     // row stride: 64 floats (256 B)
-    using Mask = unsigned long long;
-    Mask *lmask = reinterpret_cast<Mask *>(smem);                 // 64
-    Mask *uself = lmask + DS;                                     // 64
-    Mask *uprop = uself + DS;                                     // 64
-    float *M = reinterpret_cast<float *>(uprop + DS);             // D * 64 (columns >= D zero)
-    float *Mdx = M + D * DS;                                      // 128: {A~_yy, A~_xy} per y
-    int32_t *nxs = reinterpret_cast<int32_t *>(Mdx + 2 * DS);    // 64
-    int *s_tx = nxs + DS;                                         // 1
-    unsigned *btab = reinterpret_cast<unsigned *>(smem + a.lds_btab_off);   // C(c, i), c <= D, i <= DM
-    unsigned *tpre = btab + (D + 1) * (DM + 1);                   // tasks before min(T) = t0, t0 <= D
-    int *batch = reinterpret_cast<int *>(smem + a.lds_batch_off) + (size_t)wv * (TY_WAVE_BYTES / 4);
-
-    for (int i = tid; i < D; i += blockDim.x) nxs[i] = nxg[i];
-    for (int e = tid; e < (D + 1) * (DM + 1); e += blockDim.x) {
-        const int c = e / (DM + 1), i = e - c * (DM + 1);
-        btab[e] = (unsigned)pcg_binom(a.binom, c, i);
-    }
-    __syncthreads();
-    {   // rows of A~ and the local adjacency masks (k_level_lds_f's row-batched staging)
-        constexpr int SR = 4;
-        const int nwv = blockDim.x >> 6;
-        const int kg = lane < D ? nxs[lane] : -1;
-        for (int t0 = wv * SR; t0 < D; t0 += nwv * SR) {
-            float v[SR];
-            uint64_t w[SR];
-#pragma unroll
-            for (int r = 0; r < SR; ++r) {
-                const int rg = nxs[min(t0 + r, D - 1)];
-                const int k = kg < 0 ? 0 : kg;
-                v[r] = (float)a.C[(int64_t)rg * a.ldc + k];
-                w[r] = a.adj[(int64_t)rg * a.W + (k >> 6)];
-            }
-#pragma unroll
-            for (int r = 0; r < SR; ++r) {
-                const int t = t0 + r;
-                if (t >= D) break;                   // wave-uniform
-                if (lane < DS) M[t * DS + lane] = kg >= 0 ? v[r] : 0.0f;
-                const Mask m = __ballot(kg >= 0 && ((w[r] >> (kg & 63)) & 1ull));
-                if (lane == 0) lmask[t] = m;
-            }
-        }
-    }
-    for (int t = tid; t < D; t += blockDim.x) {
-        const int yg = nxs[t];
-        Mdx[2 * t] = (float)a.diag[yg];
-        Mdx[2 * t + 1] = (float)a.C[(int64_t)x * a.ldc + yg];
-        uself[t] = 0;
-        uprop[t] = 0;
-    }
-    if (tid == 0) {
-        int c = 0;
-        while (c < D && nxs[c] < x) ++c;
-        *s_tx = c;
-        // task order: t0 = min(T) ascending, then T \ {t0} in colex order, then the candidate
-        // group g = 0 .. (t0 - 1) / TG (so the groups of one T are consecutive)
-        unsigned acc = 0;
-        for (int t0 = 0; t0 <= D; ++t0) {
-            tpre[t0] = acc;
-            if (t0 >= 1 && t0 <= D - DT) acc += (unsigned)((t0 - 1) / TG + 1) * btab[(D - 1 - t0) * (DM + 1) + DT - 1];
-        }
-    }
-    __syncthreads();
-    const int tx = *s_tx;
-    const double Cxx = (double)(float)a.diag[x];                  // A~_xx
-    const uint64_t ntask = tpre[D];
-    const uint64_t r0 = (uint64_t)(chunk - a.cpre[x]) * 256u * (uint64_t)a.spl + (uint64_t)wv * 64u * (uint64_t)a.spl;
-    const uint64_t r1 = min(ntask, r0 + 64u * (uint64_t)a.spl);
-    unsigned long long tests = 0, indep = 0;
-    const float inv_sf = (float)a.inv_s;
-    const float lo2f = (float)(a.lo2 * (1.0 - 4.0 * F32_U));     // <= lo2
-    const float hi2f = (float)(a.hi2 * (1.0 + 4.0 * F32_U));     // >= hi2
-    const f2v s2 = {(float)(a.s_amgm * (1.0 + 4.0 * F32_U)), (float)(a.s_amgm * (1.0 + 4.0 * F32_U))};
-    constexpr double RUd = 1.0 + 16.0 * F32_U;
-    const f2v ke2 = {(float)(2.0 * PCG_F32_KE * F32_U * RUd), (float)(2.0 * PCG_F32_KE * F32_U * RUd)};
-    const f2v ke2u = {(float)((2.0 * PCG_F32_KE + 1.0) * F32_U * RUd), (float)((2.0 * PCG_F32_KE + 1.0) * F32_U * RUd)};
-    const f2v inv_su = {(float)(a.inv_s * RUd), (float)(a.inv_s * RUd)};
-    const f2v tauu = {(float)(a.tau * RUd * RUd), (float)(a.tau * RUd * RUd)};
-    const f2v two_u = {(float)(2.0 * (1.0 + 8.0 * F32_U) * RUd), (float)(2.0 * (1.0 + 8.0 * F32_U) * RUd)};
-    const f2v one_u = {(float)((1.0 + 8.0 * F32_U) * RUd), (float)((1.0 + 8.0 * F32_U) * RUd)};
-    const f2v s2u = s2 + (float)F32_U;
-    // lane t = neighbour t: its adjacency row, its {A~_yy, A~_xy}, lanes past D idle
-    const int tl = lane < D ? lane : D - 1;
-    const Mask lm_t = lmask[tl];
-    const Mask ymask = D >= 64 ? ~0ull : ((1ull << D) - 1ull);
-    const f2v mdx_t = *reinterpret_cast<const f2v *>(Mdx + 2 * tl);
-    unsigned prevT = 0xffffffffu;
-    f2v vT2[DT];                                                  // {v_i, v_i}: the packed FMA operand
-    f2v byy2 = {0.0f, 0.0f}, bxy2 = {0.0f, 0.0f};
-    Mask ownT = 0ull;
-    unsigned ntests = 0;                                          // wave-uniform test count
-#pragma unroll
-    for (int i = 0; i < DT; ++i) vT2[i] = f2v{0.0f, 0.0f};
-
-    for (uint64_t b0 = r0; b0 < r1; b0 += TY_BATCH) {
-        const int nb = (int)min((uint64_t)TY_BATCH, r1 - b0);
-        // ---- phase A: lane (k, h) builds candidates 3h .. 3h + 2 of task b0 + k
-        {
-            const int k = lane & (TY_BATCH - 1), h = lane >> 5;
-            int *rec = batch + k * TY_TASK_WORDS;
-            float *tf = reinterpret_cast<float *>(rec + 2);
-            float *cp = tf + TY_TF;
-            if (k < nb) {
-                const unsigned task = (unsigned)(b0 + k);
-                int lq = 1, hq = D - DT + 1;                         // t0: last with tpre[t0] <= task
-                while (hq - lq > 1) {
-                    const int mid = (lq + hq) >> 1;
-                    if (tpre[mid] <= task) lq = mid; else hq = mid;
-                }
-                const int t0 = lq;
-                const unsigned rem = task - tpre[t0];
-                const unsigned ngr = (unsigned)((t0 - 1) / TG + 1);
-                const unsigned trank = rem / ngr;
-                const int cbase = (int)(rem - trank * ngr) * TG;
-                int T[DT];
-                T[0] = t0;
-                {
-                    unsigned rr = trank;
-                    int hi_ = D - t0 - 1;
-#pragma unroll
-                    for (int ii = DT - 2; ii >= 0; --ii) {
-                        int lo_ = ii, up = hi_ - 1;
-                        while (lo_ < up) {
-                            const int mid = (lo_ + up + 1) >> 1;
-                            if (btab[mid * (DM + 1) + ii + 1] <= rr) lo_ = mid; else up = mid - 1;
-                        }
-                        T[ii + 1] = lo_;
-                        rr -= btab[lo_ * (DM + 1) + ii + 1];
-                        hi_ = lo_;
-                    }
-#pragma unroll
-                    for (int ii = 1; ii < DT; ++ii) T[ii] += t0 + 1;
-                }
-                const int nval = min(t0 - cbase, TG);
-                // T setup in fp64 on A~ (k_level_lds_f's operations)
-                double L[DT][DT], Li[DT][DT], uT[DT];
-                bool okT = true;
-                double gT = 1.0;
-#pragma unroll
-                for (int j = 0; j < DT; ++j) {
-                    double s_ = M[T[j] * DS + T[j]];
-#pragma unroll
-                    for (int q = 0; q < j; ++q) s_ -= L[j][q] * L[j][q];
-                    okT = okT && (s_ > 0.0);
-                    gT = fmin(gT, s_);
-                    const double r = rsq_nr(s_);
-#pragma unroll
-                    for (int i = j + 1; i < DT; ++i) {
-                        double t = M[T[i] * DS + T[j]];
-#pragma unroll
-                        for (int q = 0; q < j; ++q) t -= L[i][q] * L[j][q];
-                        L[i][j] = t * r;
-                    }
-                    Li[j][j] = r;
-                }
-#pragma unroll
-                for (int i = 1; i < DT; ++i)
-#pragma unroll
-                    for (int j = 0; j < i; ++j) {
-                        double t = 0.0;
-#pragma unroll
-                        for (int q = j; q < i; ++q) t += L[i][q] * Li[q][j];
-                        Li[i][j] = -t * Li[i][i];
-                    }
-                double uuT = 0.0, liF = 0.0;
-#pragma unroll
-                for (int i = 0; i < DT; ++i) {
-                    double t = 0.0;
-#pragma unroll
-                    for (int j = 0; j <= i; ++j) {
-                        t += Li[i][j] * (double)Mdx[2 * T[j] + 1];
-                        liF += Li[i][j] * Li[i][j];
-                    }
-                    uT[i] = t;
-                    uuT += t * t;
-                }
-                const double cx0 = Cxx - uuT;
-                if (h == 0) {
-                    unsigned tpk = 0;
-#pragma unroll
-                    for (int i = 0; i < DT; ++i) tpk |= (unsigned)T[i] << (8 * i);
-                    rec[0] = (int)tpk;
-                    int e = 0;
-#pragma unroll
-                    for (int i = 0; i < DT; ++i)
-#pragma unroll
-                        for (int j = 0; j <= i; ++j) tf[e++] = (float)Li[i][j];
-#pragma unroll
-                    for (int i = 0; i < DT; ++i) tf[6 + i] = (float)uT[i];
-                }
-                // this lane's three candidates jj = 3h + p as two packed pairs (slot 3 unused)
-                const float liFf = (float)liF;
-                const float gTf = (float)gT * (1.0f - (float)(4.0 * F32_U));
-                f2v lcq[2][DT], rlq[2], ucq[2], cxq[2], l2q[2], r2q[2], llq[2];
-                bool vld[4];
-#pragma unroll
-                for (int pp = 0; pp < 2; ++pp)
-#pragma unroll
-                    for (int hh_ = 0; hh_ < 2; ++hh_) {
-                        const int p = 2 * pp + hh_;
-                        const int jj = 3 * h + p;
-#pragma unroll
-                        for (int i = 0; i < DT; ++i) lcq[pp][i][hh_] = 0.0f;
-                        rlq[pp][hh_] = ucq[pp][hh_] = cxq[pp][hh_] = l2q[pp][hh_] = r2q[pp][hh_] = llq[pp][hh_] = 0.0f;
-                        vld[p] = false;
-                        if (p < 3 && jj < nval) {
-                            const int cc = cbase + jj;
-                            double lc[DT], ll = 0.0, lu = 0.0;
-#pragma unroll
-                            for (int i = 0; i < DT; ++i) {
-                                double t = 0.0;
-#pragma unroll
-                                for (int j = 0; j <= i; ++j) t += Li[i][j] * (double)M[T[j] * DS + cc];
-                                lc[i] = t;
-                                ll += t * t;
-                                lu += t * uT[i];
-                            }
-                            const double lam2 = (double)M[cc * DS + cc] - ll;
-                            const double r = rsq_nr(lam2);
-                            const double u = ((double)Mdx[2 * cc + 1] - lu) * r;
-                            const double cxx = cx0 - u * u;
-#pragma unroll
-                            for (int i = 0; i < DT; ++i) lcq[pp][i][hh_] = (float)lc[i];
-                            rlq[pp][hh_] = (float)r;
-                            ucq[pp][hh_] = (float)u;
-                            cxq[pp][hh_] = (float)cxx;
-                            l2q[pp][hh_] = (float)lam2;
-                            r2q[pp][hh_] = (float)(r * r);
-                            llq[pp][hh_] = (float)ll;
-                            vld[p] = okT && (lam2 > 0.0);
-                        }
-                    }
-                unsigned okbits = 0;
-#pragma unroll
-                for (int pp = 0; pp < 2; ++pp) {
-                    // k_level_lds_f's decision bounds, verbatim (see there)
-                    constexpr float U = (float)F32_U;
-                    constexpr float RU = 1.0f + 16.0f * U, RD = 1.0f - 16.0f * U, U8 = 8.0f * U;
-                    const f2v one = {1.0f, 1.0f};
-                    const f2v liF2 = {liFf, liFf};
-                    const f2v cxf = cxq[pp], l2f = l2q[pp], r2f = r2q[pp], llf = llq[pp];
-                    const f2v nu2 = __builtin_elementwise_fma(__builtin_elementwise_fma(liF2, llf, one), r2f, liF2);
-                    const f2v E = __builtin_elementwise_fma(nu2, ke2, ke2u);
-                    const f2v te = E * inv_su;
-                    const f2v gT2 = {gTf, gTf};
-                    const f2v g = (__builtin_elementwise_min(gT2, l2f) - (E + 2.0f * U)) * RD;
-                    const f2v cmE = (cxf - E) * RD;
-                    const f2v rg = {__builtin_amdgcn_rcpf(g[0]), __builtin_amdgcn_rcpf(g[1])};
-                    const f2v kg = tauu * rg;
-                    const f2v hx = hi2f * (cxf + E);
-                    const f2v f1 = __builtin_elementwise_fma(te, two_u, one_u);
-                    const f2v al = hx * f1;
-                    const f2v be = E * (hx + s2) * f1;
-                    const f2v ga = (cmE - cmE * te) * ((1.0f - U8) * RD);
-                    const f2v ka = __builtin_elementwise_fma(E, cxf + s2u, kg) * ((1.0f + U8) * RU);
-                    const f2v mm = 0.5f * (al + ga);
-                    const f2v hw = __builtin_elementwise_fma(-2.0f * U8 * one, ga, 0.5f * (ga - al));
-                    const f2v kk1 = 0.5f * (be - ka);
-                    const f2v kk2 = (be + ka) * (0.5f * (1.0f + U8));
-#pragma unroll
-                    for (int hh_ = 0; hh_ < 2; ++hh_) {
-                        const int p = 2 * pp + hh_;
-                        if (p >= 3) continue;
-                        const int jj = 3 * h + p;
-                        const bool ok = vld[p] && (te[hh_] <= 0.5f) && (cmE[hh_] > 0.0f) && (g[hh_] > 0.0f) &&
-                                        (ga[hh_] > al[hh_]);
-                        okbits |= (unsigned)ok << jj;
-                        // the pair slots of candidate jj: pair jj / 2, component jj & 1
-                        float *pr = cp + (jj >> 1) * TY_PAIR + (jj & 1);
-#pragma unroll
-                        for (int i = 0; i < DT; ++i) pr[2 * i] = lcq[pp][i][hh_];
-                        pr[6] = rlq[pp][hh_];
-                        pr[8] = ucq[pp][hh_];
-                        pr[10] = ok ? mm[hh_] : 0.0f;                // unusable: never "dependent"
-                        pr[12] = ok ? hw[hh_] : -1.0f;
-                        pr[14] = ok ? kk1[hh_] : 0.0f;
-                        pr[16] = ok ? kk2[hh_] : 1.0f;
-                    }
-                }
-                // the usable-candidate bits of both halves (lanes k, k + 32) meet in one word
-                okbits |= __shfl_xor(okbits, 32);
-                if (h == 0) rec[1] = cbase | (nval << 8) | (int)(okbits << 16);
-            }
-        }
-        wave_sync();
-        // ---- phase B: per task, lanes = the y's
-        for (int k = 0; k < nb; ++k) {
-            const int *rec = batch + k * TY_TASK_WORDS;
-            const unsigned tpk = (unsigned)__builtin_amdgcn_readfirstlane(rec[0]);
-            const unsigned inf = (unsigned)__builtin_amdgcn_readfirstlane(rec[1]);
-            const int cbase = (int)(inf & 255u), nval = (int)((inf >> 8) & 255u);
-            const unsigned okm = inf >> 16;
-            int T[DT];
-            Mask Tmask = 0ull;
-#pragma unroll
-            for (int i = 0; i < DT; ++i) {
-                T[i] = (int)((tpk >> (8 * i)) & 255u);
-                Tmask |= 1ull << T[i];
-            }
-            if (tpk != prevT) {                                      // wave-uniform
-                prevT = tpk;
-                const float *tf = reinterpret_cast<const float *>(rec + 2);
-                float mT[DT];
-#pragma unroll
-                for (int j = 0; j < DT; ++j) mT[j] = M[T[j] * DS + tl];
-                f2v acc = {0.0f, 0.0f};
-                int e = 0;
-#pragma unroll
-                for (int i = 0; i < DT; ++i) {
-                    float v = 0.0f;
-#pragma unroll
-                    for (int j = 0; j <= i; ++j) v = fmaf(tf[e++], mT[j], v);
-                    const f2v vu = {v, tf[6 + i]}, vb = {v, v};
-                    vT2[i] = vb;
-                    acc = __builtin_elementwise_fma(vu, vb, acc);
-                }
-                const f2v b2 = mdx_t - acc;
-                byy2 = f2v{b2[0], b2[0]};
-                bxy2 = f2v{b2[1], b2[1]};
-                ownT = __builtin_amdgcn_ballot_w64(lane < tx && (lm_t & Tmask) == Tmask);
-            }
-            const Mask own = uniform_u64(ownT);                      // the compiler's phi is a VGPR
-            const Mask base = ymask & ~Tmask;
-            const float *pr0 = reinterpret_cast<const float *>(rec + 2 + TY_TF);
-            const float *Mc = M + cbase * DS + tl;                   // rows cbase .. cbase + 5, this lane's y
-            // the sweep: all candidates of the task at every y at once; the compare masks and the
-            // fp32 c_yy / c_xy stay for the bookkeeping and the rare path
-            Mask pass[TG];
-            f2v cyyq[TG / 2], cxyq[TG / 2];
-#pragma unroll
-            for (int q = 0; q < TG / 2; ++q) {
-                pass[2 * q] = pass[2 * q + 1] = 0ull;
-                if (2 * q < nval) {                                  // wave-uniform
-                    const float *pr = pr0 + q * TY_PAIR;
-                    f2v sc = {Mc[(2 * q) * DS], Mc[(2 * q + 1) * DS]};   // row cbase + 2q + 1 <= t0 < D
-#pragma unroll
-                    for (int i = 0; i < DT; ++i)
-                        sc = __builtin_elementwise_fma(-*reinterpret_cast<const f2v *>(pr + 2 * i), vT2[i], sc);
-                    const f2v vc = sc * *reinterpret_cast<const f2v *>(pr + 6);
-                    const f2v cyy = __builtin_elementwise_fma(-vc, vc, byy2);
-                    const f2v cxy = __builtin_elementwise_fma(-*reinterpret_cast<const f2v *>(pr + 8), vc, bxy2);
-                    const f2v nm = __builtin_elementwise_fma(cxy, cxy, -*reinterpret_cast<const f2v *>(pr + 14));
-                    const f2v w = __builtin_elementwise_fma(-*reinterpret_cast<const f2v *>(pr + 10), cyy, nm);
-                    const f2v hh = __builtin_elementwise_fma(*reinterpret_cast<const f2v *>(pr + 12), cyy,
-                                                             -*reinterpret_cast<const f2v *>(pr + 16));
-                    pass[2 * q] = __builtin_amdgcn_ballot_w64(__builtin_fabsf(w[0]) < hh[0]);
-                    pass[2 * q + 1] = __builtin_amdgcn_ballot_w64(__builtin_fabsf(w[1]) < hh[1]);
-                    cyyq[q] = cyy;
-                    cxyq[q] = cxy;
-                }
-            }
-            // bookkeeping (wave-uniform): the live lanes of candidate c are base & ~{c} minus, on
-            // the lanes x does not own (own: y < x and T in adj(y)), the y adjacent to c
-            const Mask cand = (((1ull << nval) - 1ull) << cbase);
-            Mask anybad = 0ull;
-            unsigned nt;
-            if (!own) {                                              // the common case: no dedup
-                nt = (unsigned)(nval * __popcll(base) - __popcll(base & cand));
-#pragma unroll
-                for (int jj = 0; jj < TG; ++jj) {
-                    const Mask okj = ((okm >> jj) & 1u) ? pass[jj] : 0ull;
-                    if (jj < nval) anybad |= base & ~(1ull << (cbase + jj)) & ~okj;
-                }
-            } else {
-                nt = 0;
-#pragma unroll
-                for (int jj = 0; jj < TG; ++jj) {
-                    if (jj < nval) {
-                        const Mask live = base & ~(1ull << (cbase + jj)) & ~(own & uniform_u64(lmask[cbase + jj]));
-                        nt += (unsigned)__popcll(live);
-                        const Mask okj = ((okm >> jj) & 1u) ? pass[jj] : 0ull;
-                        anybad |= live & ~okj;
-                    }
-                }
-            }
-            ntests += nt;
-            if (anybad) {                                            // wave-uniform, rare
-#pragma unroll
-                for (int jj = 0; jj < TG; ++jj) {
-                    if (jj >= nval) continue;
-                    const int c = cbase + jj;
-                    const Mask adjc = own ? uniform_u64(lmask[c]) : 0ull;
-                    const Mask live = base & ~(1ull << c) & ~(own & adjc);
-                    const bool okj = (okm >> jj) & 1u;
-                    const Mask badj = live & ~(okj ? pass[jj] : 0ull);
-                    if (!((badj >> lane) & 1ull)) continue;
-                    const Mask Smask = Tmask | (1ull << c);
-                    if (okj) {
-                        // certain independence, k_level_lds_f's rare-path bounds (see there)
-                        const float *pr = pr0 + (jj >> 1) * TY_PAIR + (jj & 1);
-                        constexpr float U8 = (float)(8.0 * F32_U);
-                        const float m_ = pr[10], hq_ = pr[12], k1_ = pr[14], k2_ = pr[16];
-                        const float cyy = cyyq[jj >> 1][jj & 1], cxy = cxyq[jj >> 1][jj & 1];
-                        const float Alb = (m_ + hq_) * (1.0f - U8);
-                        const float Eub = (k1_ + k2_) * inv_sf * (1.0f + U8);
-                        const float kgub = (k2_ - k1_) * (1.0f + U8);
-                        const float ay = (cyy - Eub) * (1.0f - U8);
-                        const float ax = (__builtin_fabsf(cxy) + Eub) * (1.0f + U8);
-                        if (ay > 0.0f && ax * ax * (1.0f + U8) < lo2f * Alb * ay &&
-                            fmaf(ax, ax, kgub) * (1.0f + U8) < Alb * ay) {
-                            ++indep;
-                            atomicOr(&uself[lane], Smask);
-                            if (((lm_t & Smask) == Smask) && lane >= tx) atomicOr(&uprop[lane], Smask);
-                            continue;
-                        }
-                    }
-                    int sg[DM];
-                    sg[0] = nxs[c];
-#pragma unroll
-                    for (int i = 0; i < DT; ++i) sg[i + 1] = nxs[T[i]];
-                    push_screen(a, x, nxs[lane], sg, DM);
-                }
-            }
-        }
-        wave_sync();                                                 // the batch area is rewritten next
-    }
-    if (lane == 0) tests = ntests;
-    __syncthreads();
-    for (int t = tid; t < D; t += blockDim.x) {
-        const Mask us = uself[t], up = uprop[t];
-        if (!(us | up)) continue;
-        const int yg = nxs[t];
-        a.rm[(int64_t)x * a.n + yg] = 1;
-        a.rm[(int64_t)yg * a.n + x] = 1;
-        for (int side = 0; side < 2; ++side) {
-            Mask m = side ? up : us;
-            if (!m) continue;
-            const int64_t slot = side ? (int64_t)a.off[yg] + find_in_sorted(a.nbr + a.off[yg], a.deg[yg], x)
-                                      : (int64_t)a.off[x] + t;
-            unsigned long long *row = reinterpret_cast<unsigned long long *>(a.ug + slot * a.W);
-            while (m) {
-                const int b = __ffsll((long long)m) - 1;
-                const int gid = nxs[b];
-                atomicOr(&row[gid >> 6], 1ull << (gid & 63));
-                m &= m - 1;
-            }
-        }
-    }
-    block_flush_counts(a.ctr, tests, indep);
-}
-
 // The fp64 screen of the tests the fp32 sweep handed over (one lane per test, after the level
 // kernels, before k_exact): decided like the fp64 kernels; independence writes the removal
 // flags and both sides' unions as k_exact does, the band goes on to the exact path.
@@ -3585,15 +3081,6 @@ size_t lds_tgroup_f_bytes(int D, int DM, int mask_bytes) {
     return lds_f32_core(D, mask_bytes) + (size_t)(D + 1) * (DM + 1) * 4 + (np + 1) * 4 + np * 2 + 16;
 }
 bool use_screen32(const pcg_handle *h, int d) { return (h->screen_eff >> d) & 1; }
-// k_level_ty (y-parallel T-sweep) for the fp32-screened narrow class: PCG_TY=0 selects
-// k_level_lds_f instead (A/B knob, read per depth)
-bool use_ty() {
-    const char *e = getenv("PCG_TY");
-    return !e || atoi(e) != 0;
-}
-size_t lds_ty_batch_off(int D, int DM) {
-    return ((size_t)ty_core_bytes(D) + (size_t)(D + 1) * (DM + 1) * 4 + (size_t)(D + 1) * 4 + 15) & ~(size_t)15;
-}
 constexpr size_t LDS_MAX = 160 * 1024;   // gfx950 LDS per workgroup
 
 // lane tasks of k_level_lds_t for a node of degree D at depth d (see the kernel)
@@ -3793,9 +3280,12 @@ extern "C" int pcg_skeleton_init(pcg_handle *h, const double *C, int64_t n, int6
                        (unsigned long long *)h->exp_ctr.p);
     PCG_HIP(h, hipGetLastError());
     int rc = graph_launch(h);            // also clears the counters
-    if (!rc) rc = level_wait(h);
     if (rc) return rc;
-    graph_finish(h);
+    // the complete graph's degrees are known (k_init writes n - 1 everywhere): depth 0 is
+    // decided and enqueued without waiting for this summary (the next level_wait covers it)
+    h->deg_h.assign((size_t)n, (int32_t)(n - 1));
+    h->sumdeg = (int64_t)n * (n - 1);
+    h->maxdeg = (int32_t)(n - 1);
     return PCG_OK;
 }
 
@@ -4136,14 +3626,6 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                             if (mode == MODE_DECIDE) hipLaunchKernelGGL((k_level_wave<32, MODE_DECIDE>), grid, block, ldsw, h->stream, as);
                             else hipLaunchKernelGGL((k_level_wave<32, MODE_FULLP>), grid, block, ldsw, h->stream, as);
                         }
-                    } else if (h->tgroup && use_screen32(h, d) && use_ty()) {
-                        as.lds_btab_off = (int)ty_core_bytes(h->maxdeg_small);
-                        as.lds_batch_off = (int)lds_ty_batch_off(h->maxdeg_small, d);
-                        const size_t ldsy = (size_t)as.lds_batch_off + 4 * (size_t)TY_WAVE_BYTES;
-                        const dim3 grid((unsigned)(s_hi - s_lo)), block(256);
-                        if (d == 2) hipLaunchKernelGGL((k_level_ty<2>), grid, block, ldsy, h->stream, as);
-                        else if (d == 3) hipLaunchKernelGGL((k_level_ty<3>), grid, block, ldsy, h->stream, as);
-                        else hipLaunchKernelGGL((k_level_ty<4>), grid, block, ldsy, h->stream, as);
                     } else if (h->tgroup && use_screen32(h, d)) {
                         as.lds_btab_off = (int)lds_f32_core(dl, 8);
                         const size_t ldsf = lds_tgroup_f_bytes(dl, d, 8);
