@@ -31,56 +31,69 @@ def bytes_per_test(d: int) -> int:
     return 8 * (d + 2) * (d + 3) // 2 + 4 * (d + 2) + 8
 
 
+def _latest(pattern: str):
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
+    return files[-1] if files else None
+
+
 def _pmc(kernel: str):
     """Per-dispatch PMC counters of ``kernel`` (rocprof name, template args kept) from the latest
-    committed rocprofv3 pass over this same bench command (profiles/r*_pmc_summary.json)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
-    if not files:
+    committed rocprofv3 passes over this same bench command (profiles/r*_pmc_summary.json)."""
+    f = _latest("r*_pmc_summary.json")
+    if not f:
         return {}, None
-    data = json.load(open(files[-1]))
-    ctr = data.get(kernel, {})
-    return {k: v["per_dispatch_mean"] for k, v in ctr.items()}, os.path.basename(files[-1])
+    ctr = json.load(open(f)).get(kernel, {})
+    return {k: v["per_dispatch_mean"] for k, v in ctr.items()}, os.path.basename(f)
+
+
+def _issue_model(kernel: str):
+    """The committed VALU issue-cost model of ``kernel`` (tools/roofline_model.py): the kernel's
+    per-dispatch VALU instructions by PMC class x the measured cycles of each class's opcodes
+    (profiles/r03_issue_cost.json, split in the proportions of the kernel's own ISA)."""
+    f = _latest("r*_roofline_model.json")
+    if not f:
+        return None, None
+    m = json.load(open(f))
+    return (m if m.get("kernel") == kernel else None), os.path.basename(f)
 
 
 def roofline_of(kernel: str, tests: int, d: int, k_ms: float) -> dict:
     """Roofline of the dominant CI-test kernel.
 
     Binding resource: VALU issue. The kernel stages each node's correlation block in LDS, so
-    its HBM traffic (PMC) is ~10^3 below SURVEY §8(d)'s per-test byte model and HBM is not what
-    binds. Measured from the committed PMC pass of the same kernel and workload:
-    ``SQ_ACTIVE_INST_VALU`` counts, per wave, the quad-cycles (4 shader cycles,
-    MI355X_MICROARCH.md constants table) in which the wave's VALU instructions occupy its SIMD;
-    summed over waves it is the SIMD-cycles the VALUs were busy. achieved = those cycles / the
-    live kernel time; peak = 1024 SIMDs x 2.4 GHz; frac = achieved / peak (the VALU-busy share
-    of the chip over the kernel). The issue-cost model it agrees with — every wave64 VALU
-    instruction, fp64 or not, 4 SIMD-cycles (tools/micro/valu_occ.hip, profiles/r02_valu_occ.log)
-    — and the HBM / fp64 figures are secondary keys."""
-    ctr, src = _pmc(kernel)
+    its HBM traffic (PMC) is far below SURVEY §8(d)'s per-test byte model and HBM is not what
+    binds. achieved = the SIMD-cycles its VALU instructions need to issue, per launch ÷ the
+    live kernel time; peak = 1024 SIMDs × 2.4 GHz; frac = achieved / peak.
+
+    The SIMD-cycles per launch come from the committed issue-cost model
+    (profiles/r*_roofline_model.json, tools/roofline_model.py): the PMC class counters of this
+    kernel on this bench command (SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_{F32,F64}, _INT32, _INT64,
+    _CVT, SQ_INSTS_VALU for the rest), each class split over its opcodes in the proportions of
+    the kernel's ISA, times the wall-clock cycles of those opcodes measured by
+    tools/micro/issue_cost.hip at the kernel's occupancy (profiles/r03_issue_cost.json). The
+    model's bounds (every class at its cheapest / dearest opcode) ride along as frac_bounds."""
     peak_gcyc = 1024 * 2.4   # G SIMD-cycles/s
-    line = {"bound": "valu", "unit": "G SIMD-cycles/s (VALU busy)", "peak": peak_gcyc, "achieved": None,
-            "frac": None, "traffic": None, "kernel": kernel, "kernel_ms": k_ms, "pmc_source": src}
+    line = {"bound": "valu", "unit": "G SIMD-cycles/s (VALU issue)", "peak": peak_gcyc, "achieved": None,
+            "frac": None, "traffic": None, "kernel": kernel, "kernel_ms": k_ms}
     alg = tests * bytes_per_test(d)
     sec = {"hbm_contract_bytes_per_test": bytes_per_test(d),
            "hbm_contract_gbs": alg / (k_ms / 1e3) / 1e9 if k_ms > 0 else None,
            "note": "SURVEY 8(d) per-test byte model; operands are LDS-resident, so it is not a traffic figure"}
-    if k_ms > 0 and "SQ_ACTIVE_INST_VALU" in ctr:
-        busy = 4.0 * ctr["SQ_ACTIVE_INST_VALU"]
-        line["achieved"] = busy / (k_ms / 1e3) / 1e9
+    model, msrc = _issue_model(kernel)
+    line["model_source"] = msrc
+    if k_ms > 0 and model:
+        cyc = float(model["valu_issue_cycles"])
+        lo, hi = (float(v) for v in model["valu_issue_cycles_bounds"])
+        line["achieved"] = cyc / (k_ms / 1e3) / 1e9
         line["frac"] = line["achieved"] / peak_gcyc
-        line["valu_busy_ms_per_simd"] = busy / 1024 / 2.4e9 * 1e3
-    need = ("SQ_INSTS_VALU", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64")
-    if k_ms > 0 and all(k in ctr for k in need):
-        valu = ctr["SQ_INSTS_VALU"]
-        f64 = sum(ctr[k] for k in need[1:])
-        sec["issue_model_4cyc_frac"] = 4.0 * valu / (peak_gcyc * 1e9) / (k_ms / 1e3)
-        sec["issue_model_4cyc_fp64_2cyc_other_frac"] = (4.0 * f64 + 2.0 * (valu - f64)) / (peak_gcyc * 1e9) / (k_ms / 1e3)
-        sec["valu_instr_per_64_tests"] = valu / (tests / 64.0) if tests else None
-        sec["fp64_instr_per_64_tests"] = f64 / (tests / 64.0) if tests else None
-        if "SQ_INSTS_VALU_FLOPS_FP64" in ctr:     # per wave-instruction flops -> x64 lanes
-            tf = 64.0 * ctr["SQ_INSTS_VALU_FLOPS_FP64"] / (k_ms / 1e3) / 1e12
-            sec["fp64_tflops_executed"] = tf
-            sec["fp64_frac"] = tf / FP64_PEAK_TFLOPS
+        line["frac_bounds"] = [lo / (k_ms / 1e3) / 1e9 / peak_gcyc, hi / (k_ms / 1e3) / 1e9 / peak_gcyc]
+        line["valu_issue_cycles_per_launch"] = cyc
+        line["valu_instructions_per_launch"] = model["valu_instructions"]
+        line["mean_cycles_per_valu"] = model["mean_cycles_per_valu"]
+        sec["valu_instr_per_64_tests"] = model["valu_instructions"] / (tests / 64.0) if tests else None
+    ctr, src = _pmc(kernel)
+    line["pmc_source"] = src
     if k_ms > 0 and "FETCH_SIZE" in ctr and "WRITE_SIZE" in ctr:
         # FETCH_SIZE counts KiB with gfx950's wide reads at half weight (MI355X_MICROARCH.md HBM
         # section): x2; WRITE_SIZE KiB as is
@@ -92,21 +105,36 @@ def roofline_of(kernel: str, tests: int, d: int, k_ms: float) -> dict:
     return line
 
 
-K1_TILE = 64                  # corr.hip PCG_K1_TILE
+K1_TILE = 64                  # corr.hip tile (both paths)
+K1_DIGITS = 9                 # corr.hip K1_DIG: int8 digits per value
+I8_PEAK_TOPS = 5000.0         # MI355X dense int8 MFMA (2x the dense BF16 rate; MI355X_MICROARCH.md)
 MFMA_F64_MEASURED_TFLOPS = 47.9   # v_mfma_f64_16x16x4_f64 at 4 waves/SIMD, tools/micro/mfma_f64.hip (profiles/r02_mfma_f64.log)
 
 
 def k1_roofline(n: int, N: int, corr_ms: float) -> dict:
-    """K1 (np.corrcoef) on fp64 MFMA: 2 N n^2 algorithmic flop; the kernel multiplies the
-    upper-triangle K1_TILE-square tiles only (T(T+1)/2 tiles, T = ceil(n/K1_TILE))."""
+    """K1 (np.corrcoef). Default path (PCG_K1_I8, corr.hip): the centred X split into 9 int8 digit
+    planes and the Gram as 45 exact int8 GEMMs of the upper-triangle 64-square tiles on
+    v_mfma_i32_32x32x32_i8; executed int8 ops = 45 x 2 x T(T+1)/2 x 64^2 x N_pad. The fp64 path
+    (PCG_K1_I8=0) runs v_mfma_f64_16x16x4_f64 on the same tiles. Either way the algorithmic
+    work is 2 N n^2 (reported as achieved_algorithmic, TFLOP/s)."""
     T = (n + K1_TILE - 1) // K1_TILE
-    mfma_flop = T * (T + 1) // 2 * K1_TILE * K1_TILE * 2.0 * N
-    ex = mfma_flop / (corr_ms / 1e3) / 1e12
-    return {"bound": "mfma", "unit": "TFLOP/s", "peak": FP64_PEAK_TFLOPS, "ms": corr_ms,
-            "achieved_algorithmic": 2.0 * N * n * n / (corr_ms / 1e3) / 1e12,
-            "achieved_executed": ex, "frac": ex / FP64_PEAK_TFLOPS,
-            "frac_of_measured_instruction_ceiling": ex / MFMA_F64_MEASURED_TFLOPS,
-            "what": "pcg_corr end to end (column means, split-K k_xtx, fused normalisation)"}
+    tiles = T * (T + 1) // 2
+    i8 = os.environ.get("PCG_K1_I8", "1") != "0"
+    line = {"bound": "mfma", "ms": corr_ms, "path": "int8 digits" if i8 else "fp64",
+            "achieved_algorithmic_tflops": 2.0 * N * n * n / (corr_ms / 1e3) / 1e12,
+            "what": "pcg_corr end to end (column stats, digit planes, split-K GEMM, fused normalisation)"}
+    if i8:
+        npad = (N + 63) // 64 * 64
+        ops = K1_DIGITS * (K1_DIGITS + 1) // 2 * 2.0 * tiles * K1_TILE * K1_TILE * npad
+        ex = ops / (corr_ms / 1e3) / 1e12
+        line.update({"unit": "TOP/s (int8)", "peak": I8_PEAK_TOPS, "achieved_executed": ex, "frac": ex / I8_PEAK_TOPS})
+    else:
+        mfma_flop = tiles * K1_TILE * K1_TILE * 2.0 * N
+        ex = mfma_flop / (corr_ms / 1e3) / 1e12
+        line.update({"unit": "TFLOP/s", "peak": FP64_PEAK_TFLOPS, "achieved_executed": ex,
+                     "frac": ex / FP64_PEAK_TFLOPS,
+                     "frac_of_measured_instruction_ceiling": ex / MFMA_F64_MEASURED_TFLOPS})
+    return line
 
 
 def dominant_kernel(d: int, full_p: bool) -> str:

@@ -59,23 +59,38 @@ constexpr int KT = PCG_K1_KT;
 constexpr int PAD = 1;  // LDS row padding (doubles) against bank conflicts
 constexpr int MEAN_ROWS = 64;   // rows per partial column sum (N = 10k: 157 chunks x 8 column blocks)
 
-// partial column sums over row chunks (deterministic two-pass mean)
-__global__ __launch_bounds__(256) void k_colsum_partial(const double *X, int64_t N, int n, int64_t ldx, double *part) {
+// partial column sums over row chunks (deterministic two-pass mean); with pmax / pmin also the
+// chunk's column maximum and minimum (the int8 digit path's exponents)
+__global__ __launch_bounds__(256) void k_colsum_partial(const double *X, int64_t N, int n, int64_t ldx, double *part,
+                                                       double *pmax, double *pmin) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t r0 = (int64_t)blockIdx.y * MEAN_ROWS;
     if (j >= n) return;
     const int64_t r1 = std::min<int64_t>(r0 + MEAN_ROWS, N);
-    double s = 0.0;
+    double s = 0.0, mx = -INFINITY, mn = INFINITY;
     int64_t t = r0;
     for (; t + 8 <= r1; t += 8) {           // 8 loads in flight, summed in row order
         double v[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = X[(t + k) * ldx + j];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) s += v[k];
+        for (int k = 0; k < 8; ++k) {
+            s += v[k];
+            mx = fmax(mx, v[k]);
+            mn = fmin(mn, v[k]);
+        }
     }
-    for (; t < r1; ++t) s += X[t * ldx + j];
+    for (; t < r1; ++t) {
+        const double v = X[t * ldx + j];
+        s += v;
+        mx = fmax(mx, v);
+        mn = fmin(mn, v);
+    }
     part[(int64_t)blockIdx.y * n + j] = s;
+    if (pmax) {
+        pmax[(int64_t)blockIdx.y * n + j] = mx;
+        pmin[(int64_t)blockIdx.y * n + j] = mn;
+    }
 }
 
 // mean_j = (sum of the chunk partials) / N: 64 columns per block, the 4 waves take contiguous
@@ -101,6 +116,39 @@ __global__ __launch_bounds__(256) void k_colmean(const double *part, int nchunks
     q4[w][c] = s;
     __syncthreads();
     if (w == 0 && j < n) mean[j] = (((q4[0][c] + q4[1][c]) + q4[2][c]) + q4[3][c]) / (double)N;
+}
+
+// digit exponent of column j: 2^e > max_t |fl(X_tj - mean_j)| = max(fl(max - mean), fl(mean - min))
+// (rounding is monotone, so the extremes of the centred column are the centred extremes);
+// K1_NONFINITE marks a column whose mean or range is not finite (numpy: that row and column of
+// C are NaN)
+constexpr int K1_NONFINITE = -100000;
+// (k_colmean's layout: 64 columns per block, the 4 waves take quarters of the chunk list)
+__global__ __launch_bounds__(256) void k_colexp(const double *pmax, const double *pmin, int nchunks, int n,
+                                               const double *mean, int *expo) {
+    __shared__ double q4[2][4][64];
+    const int c = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int j = blockIdx.x * 64 + c;
+    const int per = (nchunks + 3) / 4;
+    const int lo = std::min(nchunks, w * per), hi = std::min(nchunks, lo + per);
+    double mx = -INFINITY, mn = INFINITY;
+    if (j < n)
+        for (int k = lo; k < hi; ++k) {
+            mx = fmax(mx, pmax[(int64_t)k * n + j]);
+            mn = fmin(mn, pmin[(int64_t)k * n + j]);
+        }
+    q4[0][w][c] = mx;
+    q4[1][w][c] = mn;
+    __syncthreads();
+    if (w != 0 || j >= n) return;
+    mx = fmax(fmax(q4[0][0][c], q4[0][1][c]), fmax(q4[0][2][c], q4[0][3][c]));
+    mn = fmin(fmin(q4[1][0][c], q4[1][1][c]), fmin(q4[1][2][c], q4[1][3][c]));
+    const double m = mean[j];
+    const double amax = fmax(mx - m, m - mn);
+    int e = 0;
+    if (!isfinite(m) || !isfinite(amax)) e = K1_NONFINITE;
+    else if (amax > 0.0) frexp(amax, &e);     // amax = f 2^e, f in [0.5, 1): |centred| / 2^e < 1
+    expo[j] = e;
 }
 
 __device__ __forceinline__ void tile_of(int t, int T, int &bi, int &bj) {
@@ -217,6 +265,250 @@ __global__ __launch_bounds__(256) void k_xtx(const double *X, int64_t N, int n, 
                     }
                 }
             }
+}
+
+// ---------------------------------------------------------------------------------------
+// K1 on the int8 matrix cores ("digit GEMM", PCG_K1_I8; Ozaki-style splitting).
+//
+// Each centred value v = fl(X_tj - mean_j) (numpy's own subtraction) is written exactly as
+// v = 2^e_j * sum_{p=1..9} d_p 2^(-7p) + r, with signed digits d_p in [-127, 127] (truncation:
+// y = v 2^-e_j in (-1, 1); d_p = trunc(128 y_{p-1}), y_p = 128 y_{p-1} - d_p, every step exact in
+// fp64) and |r| < 2^(e_j - 63). The Gram entry is then
+//     G_ij = sum_t v_ti v_tj ~= sum_{p + q <= 10} 2^(e_i + e_j - 7(p + q)) * (D_p^T D_q)_ij
+// where every D_p^T D_q is an int8 GEMM accumulated EXACTLY in int32 (v_mfma_i32_32x32x32_i8):
+// the products of one level l = p + q share a scale, so they share one int32 accumulator
+// (at most 9 products x K x 127^2 < 2^31 for K <= K1_I8_MAXK rows per split-K slab). The dropped
+// levels p + q > 10 and the remainders r bound the error by ~50 * 2^-63 * 2^(e_i + e_j) per
+// row pair, i.e. relative to the fp64 Gram ~1e-17 x (max|v| / rms v)^2 -- far below fp64
+// dot-product rounding. The levels are combined in fp64 from the smallest (exact int32 ->
+// fp64, exact power-of-two scaling, 8 rounded adds), then the split-K slabs and the numpy-order
+// normalisation run as in the fp64 path (k_normalize_tiles / k_slab_sum / k_gather_finish).
+// Cost: 45 int8 GEMMs of the upper triangle = 45 x N n^2 int8 MACs at 2x the BF16 MFMA rate
+// (vs N n^2 fp64 MACs at 1/32 of it), plus one pass that writes 9 digit planes.
+constexpr int K1_DIG = 9;                    // digits per value (7 bits each)
+constexpr int K1_LEVELS = K1_DIG;            // p + q = 2 .. K1_DIG + 1
+constexpr int K1_TB = 32;                    // rows (t) per digit block = the MFMA K
+constexpr int K1_I8_MAXK = 14336;            // rows per slab: 9 * 14336 * 127^2 < 2^31
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+// t-th upper-triangle tile in supertile order: 8 x 8 groups of tiles (upper triangle of the
+// group grid, row-major; inside a group row-major, bi <= bj on the diagonal groups). An XCD runs
+// a contiguous run of blocks, so its ~64 resident blocks share 8 row panels and 8 column panels
+// per K block (k_xtx's row-major order shares one row panel and streams 64 column panels).
+#ifndef PCG_K1_SUPER
+#define PCG_K1_SUPER 8
+#endif
+__device__ __forceinline__ void tile_of_super(int t, int T, int &bi, int &bj) {
+    constexpr int S = PCG_K1_SUPER;
+    const int ST = (T + S - 1) / S;
+    for (int si = 0; si < ST; ++si)
+        for (int sj = si; sj < ST; ++sj) {
+            const int r0 = si * S, r1 = min(T, r0 + S), c0 = sj * S, c1 = min(T, c0 + S);
+            const int m = r1 - r0, w = c1 - c0;
+            const int cnt = si == sj ? m * (m + 1) / 2 : m * w;
+            if (t >= cnt) { t -= cnt; continue; }
+            if (si == sj) {
+                int row = 0;
+                while (t >= m - row) { t -= m - row; ++row; }
+                bi = r0 + row;
+                bj = r0 + row + t;
+            } else {
+                bi = r0 + t / w;
+                bj = c0 + t % w;
+            }
+            return;
+        }
+    bi = bj = 0;
+}
+
+// digit planes, blocked for the GEMM: Dg[((p * CB + cb) * TB + tb) * 2048 + c * 32 + tt] is digit
+// p of column 64 cb + c at row 32 tb + tt (64 x 32-byte blocks, each 2 KB contiguous); rows past
+// N and columns past n are zero. One block: 64 columns x 64 rows, transposed through LDS.
+__global__ __launch_bounds__(256) void k_digits(const double *X, int64_t N, int n, int64_t ldx, const double *mean,
+                                               const int *expo, int CB, int TB, int8_t *Dg) {
+    __shared__ __attribute__((aligned(16))) int8_t tile[K1_DIG][2][64][K1_TB];   // [p][t-half][col][t]
+    const int cb = blockIdx.x, t64 = blockIdx.y;
+    const int c = threadIdx.x & 63, r4 = threadIdx.x >> 6;
+    const int j = cb * 64 + c;
+    const bool vj = j < n;
+    const int e = vj ? expo[j] : 0;
+    const bool live = vj && e != K1_NONFINITE;
+    const double m = vj ? mean[j] : 0.0;
+    // this thread: rows 16 r4 .. 16 r4 + 15 of column c; the 16 digits of one plane pack into
+    // one 16-byte LDS store
+    double y[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int64_t t = (int64_t)t64 * 64 + r4 * 16 + i;
+        y[i] = (live && t < N) ? ldexp(X[t * ldx + j] - m, -e) : 0.0;
+    }
+#pragma unroll
+    for (int p = 0; p < K1_DIG; ++p) {
+        v4i pk = {0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            y[i] *= 128.0;
+            const double d = trunc(y[i]);
+            y[i] -= d;
+            pk[i >> 2] |= ((int)d & 255) << (8 * (i & 3));
+        }
+        *reinterpret_cast<v4i *>(&tile[p][r4 >> 1][c][16 * (r4 & 1)]) = pk;
+    }
+    __syncthreads();
+    // 9 x 2 blocks of 2 KB out: 16-byte stores, consecutive threads on consecutive addresses
+    const v4i *src = reinterpret_cast<const v4i *>(&tile[0][0][0][0]);
+    for (int q = threadIdx.x; q < K1_DIG * 2 * 128; q += 256) {
+        const int blk = q >> 7, w = q & 127;         // blk = p * 2 + half
+        const int p = blk >> 1, tb = t64 * 2 + (blk & 1);
+        if (tb >= TB) continue;
+        v4i *dst = reinterpret_cast<v4i *>(Dg + (((int64_t)p * CB + cb) * TB + tb) * 2048);
+        dst[w] = src[q];
+    }
+}
+
+// the digit GEMM of one 64 x 64 upper-triangle tile and one split-K slab (k_xtx's tiling, block
+// order and output conventions). 4 waves, each a 32 x 32 quarter: lane (r = l & 31, h = l >> 5)
+// feeds row / column r, rows t = 16h .. 16h + 15 of the block (A and B take the same k layout,
+// so the MFMA's k order inside a lane does not matter). LDS: two stages x 18 digit blocks.
+__global__ __launch_bounds__(256, 2) void k_xtx_i8(const int8_t *Dg, int CB, int TB, int n, const int *expo,
+                                                 int ntiles, int nslabs, int kb, double *G, int64_t ldg,
+                                                 int64_t slab_stride, const int32_t *tl, int super_order) {
+    __shared__ __attribute__((aligned(16))) int8_t st[2][2 * K1_DIG][2048];
+    const int T = (n + 63) / 64;
+    int bi, bj, pbi = -1;
+    int lin = blockIdx.x;
+    if (PCG_K1_XCD) {
+        const int per = gridDim.x / 8;
+        lin = (blockIdx.x % 8) * per + blockIdx.x / 8;
+        if (lin >= ntiles * nslabs) return;
+    }
+    if (tl) {
+        const int t = lin % ntiles;
+        bi = tl[3 * t];
+        bj = tl[3 * t + 1];
+        pbi = tl[3 * t + 2];
+    } else if (super_order) {
+        tile_of_super(lin % ntiles, T, bi, bj);
+    } else {
+        tile_of(lin % ntiles, T, bi, bj);
+    }
+    const int slab = lin / ntiles;
+    const int tb0 = slab * kb, tb1 = min(TB, tb0 + kb);
+    G += (int64_t)slab * slab_stride;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 31, hh = lane >> 5;
+    const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
+
+    v16i acc[K1_LEVELS];
+#pragma unroll
+    for (int l = 0; l < K1_LEVELS; ++l)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) acc[l][k] = 0;
+
+    // staging: 18 blocks of 2 KB = 2304 16-byte words, 9 per thread; thread tid moves words
+    // q * 256 + tid, i.e. block (q * 256 + tid) >> 7 (a digit of tile row bi for blocks < 9, of
+    // tile column bj after), word (q * 256 + tid) & 127
+    const v4i *srcq[K1_DIG];
+#pragma unroll
+    for (int q = 0; q < K1_DIG; ++q) {
+        const int o = q * 256 + tid;
+        const int blk = o >> 7, w = o & 127;
+        const int p = blk < K1_DIG ? blk : blk - K1_DIG;
+        const int cbk = blk < K1_DIG ? bi : bj;
+        srcq[q] = reinterpret_cast<const v4i *>(Dg + ((int64_t)p * CB + cbk) * TB * 2048) + w;
+    }
+    v4i pre[K1_DIG];
+#define K1_LOAD(tb_)                                                                   \
+    _Pragma("unroll") for (int q = 0; q < K1_DIG; ++q) pre[q] = srcq[q][(int64_t)(tb_) * 128];
+#define K1_STORE(buf_)                                                                 \
+    _Pragma("unroll") for (int q = 0; q < K1_DIG; ++q)                                 \
+        reinterpret_cast<v4i *>(&st[(buf_)][0][0])[q * 256 + tid] = pre[q];
+    if (tb0 < tb1) {
+        K1_LOAD(tb0);
+        K1_STORE(0);
+    }
+    __syncthreads();
+    for (int tb = tb0; tb < tb1; ++tb) {
+        const int buf = (tb - tb0) & 1;
+        if (tb + 1 < tb1) { K1_LOAD(tb + 1); }
+        v4i bq[K1_DIG];
+#pragma unroll
+        for (int q = 0; q < K1_DIG; ++q)
+            bq[q] = *reinterpret_cast<const v4i *>(&st[buf][K1_DIG + q][(wc + r) * 32 + 16 * hh]);
+#pragma unroll
+        for (int p = 0; p < K1_DIG; ++p) {
+            const v4i ap = *reinterpret_cast<const v4i *>(&st[buf][p][(wr + r) * 32 + 16 * hh]);
+#pragma unroll
+            for (int q = 0; q < K1_DIG - p; ++q)         // level p + q (0-based) <= K1_DIG - 1
+                acc[p + q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(ap, bq[q], acc[p + q], 0, 0, 0);
+        }
+        if (tb + 1 < tb1) { K1_STORE(buf ^ 1); }
+        __syncthreads();
+    }
+#undef K1_LOAD
+#undef K1_STORE
+    // epilogue: C/D map of the 32 x 32 forms: col = lane & 31, row = (k & 3) + 8 (k >> 2) + 4 h
+    const int j = bj * 64 + wc + r;
+    const int ej = j < n ? expo[j] : 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int i = bi * 64 + wr + (k & 3) + 8 * (k >> 2) + 4 * hh;
+        if (i >= n || j >= n) continue;
+        const int ei = expo[i];
+        double v = 0.0;
+        if (ei == K1_NONFINITE || ej == K1_NONFINITE) {
+            v = NAN;
+        } else {
+#pragma unroll
+            for (int l = K1_LEVELS - 1; l >= 0; --l)   // smallest level first; level l is p + q = l + 2
+                v += ldexp((double)acc[l][k], ei + ej - 7 * (l + 2));
+        }
+        if (pbi >= 0) {
+            G[((int64_t)pbi * 64 + (i - bi * 64)) * ldg + j] = v;
+        } else if (bi != bj || i <= j) {
+            G[(int64_t)i * ldg + j] = v;
+        }
+    }
+}
+
+// slab split of the digit GEMM: a function of (n, N) only (every world size sums the same slabs
+// in the same order), rows per slab a multiple of the 32-row digit block and <= K1_I8_MAXK
+int split_k_i8(int n, int64_t N, int *kb_out) {
+    const int T = (n + 63) / 64;
+    const int ntiles = T * (T + 1) / 2;
+    const int TB = (int)((N + 63) / 64 * 2);
+    int ks = (int)std::max<int64_t>(1, (PCG_K1_BLOCKS + ntiles / 2) / ntiles);
+    if (const char *e = getenv("PCG_K1_I8_KS")) ks = std::max(1, atoi(e));   // A/B knob
+    ks = std::min(ks, std::max(1, TB / 2));          // >= 64 rows per slab
+    ks = std::min(ks, 256);
+    int kb = (TB + ks - 1) / ks;
+    kb = std::min(kb, K1_I8_MAXK / K1_TB);
+    *kb_out = kb;
+    return (TB + kb - 1) / kb;
+}
+
+int k1_super() {                               // A/B knob: PCG_K1_SUPER_ORDER=0 -> row-major tiles
+    const char *e = getenv("PCG_K1_SUPER_ORDER");
+    return !e || atoi(e) != 0;
+}
+
+bool k1_i8() {
+    const char *e = getenv("PCG_K1_I8");
+    return !e || atoi(e) != 0;
+}
+
+// digits of X (all columns) into h->k1_digits; returns the plane geometry
+int k1_digits(pcg_handle *h, const double *X, int64_t N, int nn, int64_t ldx, const double *mean, const int *expo,
+              int *CB, int *TB, const int8_t **Dg) {
+    *CB = (nn + 63) / 64;
+    *TB = (int)((N + 63) / 64 * 2);
+    const size_t bytes = (size_t)K1_DIG * *CB * *TB * 2048;
+    if (!pcg_ensure(h, h->k1_digits, bytes)) return pcg_fail(h, PCG_ERR_OOM, "K1 digit planes (%zu bytes)", bytes);
+    hipLaunchKernelGGL(k_digits, dim3((unsigned)*CB, (unsigned)(*TB / 2)), dim3(256), 0, h->stream, X, N, nn, ldx,
+                       mean, expo, *CB, *TB, (int8_t *)h->k1_digits.p);
+    *Dg = (const int8_t *)h->k1_digits.p;
+    return PCG_OK;
 }
 
 // C_ij = clip(((sum_s G_s,ij) * 1/(N-1) / sd_i) / sd_j, -1, 1)   (numpy corrcoef order)
@@ -370,15 +662,26 @@ int split_k(int n, int64_t N, int64_t *kchunk_out) {
 
 unsigned xtx_grid(int blocks) { return PCG_K1_XCD ? (unsigned)((blocks + 7) / 8 * 8) : (unsigned)blocks; }
 
-int column_means(pcg_handle *h, const double *X, int64_t N, int nn, int64_t ldx, double **mean_out) {
+// column means (and, for the digit path, the per-column digit exponents)
+int column_means(pcg_handle *h, const double *X, int64_t N, int nn, int64_t ldx, double **mean_out,
+                 int **expo_out = nullptr) {
     const int nchunks = (int)((N + MEAN_ROWS - 1) / MEAN_ROWS);
-    if (!pcg_ensure(h, h->colmean, sizeof(double) * ((size_t)nn * (nchunks + 1))))
+    const size_t parts = (size_t)nn * nchunks * (expo_out ? 3 : 1);
+    if (!pcg_ensure(h, h->colmean, sizeof(double) * (parts + nn) + sizeof(int) * nn))
         return pcg_fail(h, PCG_ERR_OOM, "pcg_corr scratch");
     double *part = (double *)h->colmean.p;
-    double *mean = part + (size_t)nn * nchunks;
+    double *mean = part + parts;
+    double *pmax = expo_out ? part + (size_t)nn * nchunks : nullptr;
+    double *pmin = expo_out ? pmax + (size_t)nn * nchunks : nullptr;
     hipLaunchKernelGGL(k_colsum_partial, dim3((nn + 255) / 256, nchunks), dim3(256), 0, h->stream, X, N, nn, ldx,
-                       part);
+                       part, pmax, pmin);
     hipLaunchKernelGGL(k_colmean, dim3((nn + 63) / 64), dim3(256), 0, h->stream, part, nchunks, nn, N, mean);
+    if (expo_out) {
+        int *expo = reinterpret_cast<int *>(mean + nn);
+        hipLaunchKernelGGL(k_colexp, dim3((nn + 63) / 64), dim3(256), 0, h->stream, (const double *)pmax,
+                           (const double *)pmin, nchunks, nn, (const double *)mean, expo);
+        *expo_out = expo;
+    }
     *mean_out = mean;
     return PCG_OK;
 }
@@ -416,11 +719,14 @@ extern "C" int pcg_corr_shard(pcg_handle *h, const double *X, int64_t N, int64_t
     }
     const int ntiles = (int)(tl.size() / 3);
     if (ntiles == 0) return PCG_OK;
+    const bool i8 = k1_i8();
     double *mean;
-    int rc = column_means(h, X, N, nn, ldx, &mean);
+    int *expo = nullptr;
+    int rc = column_means(h, X, N, nn, ldx, &mean, i8 ? &expo : nullptr);
     if (rc) return rc;
     int64_t kchunk = 0;
-    const int ks = split_k(nn, N, &kchunk);
+    int kb = 0;
+    const int ks = i8 ? split_k_i8(nn, N, &kb) : split_k(nn, N, &kchunk);
     const int64_t stride = rows * nn;
     if (!pcg_ensure(h, h->pr_scratch, sizeof(double) * ((size_t)stride * (ks > 1 ? ks : 0) + tl.size())))
         return pcg_fail(h, PCG_ERR_OOM, "pcg_corr_shard slabs");
@@ -428,8 +734,17 @@ extern "C" int pcg_corr_shard(pcg_handle *h, const double *X, int64_t N, int64_t
     int32_t *tld = reinterpret_cast<int32_t *>((double *)h->pr_scratch.p + (ks > 1 ? (size_t)stride * ks : 0));
     PCG_HIP(h, hipMemcpyAsync(tld, tl.data(), sizeof(int32_t) * tl.size(), hipMemcpyHostToDevice, h->stream));
     if (ks > 1) PCG_HIP(h, hipMemsetAsync(G, 0, sizeof(double) * (size_t)stride * ks, h->stream));
-    hipLaunchKernelGGL(k_xtx, dim3(xtx_grid(ntiles * ks)), dim3(256), 0, h->stream, X, N, nn, ldx, mean, ntiles, ks,
-                       kchunk, G, (int64_t)nn, stride, (const int32_t *)tld);
+    if (i8) {
+        int CB = 0, TB = 0;
+        const int8_t *Dg = nullptr;
+        rc = k1_digits(h, X, N, nn, ldx, mean, expo, &CB, &TB, &Dg);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_xtx_i8, dim3(xtx_grid(ntiles * ks)), dim3(256), 0, h->stream, Dg, CB, TB, nn,
+                           (const int *)expo, ntiles, ks, kb, G, (int64_t)nn, stride, (const int32_t *)tld, 0);
+    } else {
+        hipLaunchKernelGGL(k_xtx, dim3(xtx_grid(ntiles * ks)), dim3(256), 0, h->stream, X, N, nn, ldx, mean, ntiles,
+                           ks, kchunk, G, (int64_t)nn, stride, (const int32_t *)tld);
+    }
     if (ks > 1)
         hipLaunchKernelGGL(k_slab_sum, dim3((unsigned)((stride + 255) / 256)), dim3(256), 0, h->stream, G, stride,
                            ks, stride, packed);
@@ -465,13 +780,16 @@ int pcg_corr_launch(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_
         return pcg_fail(h, PCG_ERR_INVALID, "pcg_corr: invalid arguments");
     PCG_HIP(h, hipSetDevice(h->device));
     const int nn = (int)n;
+    const bool i8 = k1_i8();
     double *mean;
-    int rc = column_means(h, X, N, nn, ldx, &mean);
+    int *expo = nullptr;
+    int rc = column_means(h, X, N, nn, ldx, &mean, i8 ? &expo : nullptr);
     if (rc) return rc;
     const int T = (nn + TILE - 1) / TILE;
     const int ntiles = T * (T + 1) / 2;
     int64_t kchunk = 0;
-    const int ks = split_k(nn, N, &kchunk);
+    int kb = 0;
+    const int ks = i8 ? split_k_i8(nn, N, &kb) : split_k(nn, N, &kchunk);
     double *G = C;
     int64_t ldg = ldc, stride = 0;
     if (ks > 1) {
@@ -482,8 +800,18 @@ int pcg_corr_launch(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_
         ldg = nn;
     }
     const double scale = 1.0 / (double)(N - 1);
-    hipLaunchKernelGGL(k_xtx, dim3(xtx_grid(ntiles * ks)), dim3(256), 0, h->stream, X, N, nn, ldx, mean, ntiles, ks,
-                       kchunk, G, ldg, stride, (const int32_t *)nullptr);
+    if (i8) {
+        int CB = 0, TB = 0;
+        const int8_t *Dg = nullptr;
+        rc = k1_digits(h, X, N, nn, ldx, mean, expo, &CB, &TB, &Dg);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_xtx_i8, dim3(xtx_grid(ntiles * ks)), dim3(256), 0, h->stream, Dg, CB, TB, nn,
+                           (const int *)expo, ntiles, ks, kb, G, ldg, stride, (const int32_t *)nullptr,
+                           k1_super());
+    } else {
+        hipLaunchKernelGGL(k_xtx, dim3(xtx_grid(ntiles * ks)), dim3(256), 0, h->stream, X, N, nn, ldx, mean, ntiles,
+                           ks, kchunk, G, ldg, stride, (const int32_t *)nullptr);
+    }
     const int T64 = (nn + NT - 1) / NT;
     hipLaunchKernelGGL(k_normalize_tiles, dim3(T64 * (T64 + 1) / 2), dim3(256), 0, h->stream, G, ldg, stride, ks, C,
                        ldc, nn, scale);

@@ -43,6 +43,34 @@ def test_corr_matches_numpy(eng, n, N, seed, wl, wh, ep):
     np.testing.assert_allclose(C, ref, rtol=0, atol=2e-14)
 
 
+@pytest.mark.parametrize("kind", ["spikes", "scales", "constant", "nonfinite"])
+def test_corr_hard_columns_match_numpy(eng, kind):
+    """K1 on columns that stress a per-column fixed-point split: heavy-tailed spikes (max/rms ~
+    100), scales from 1e-8 to 1e7 (memory bytes) plus a large offset, constant columns (numpy's
+    0/0 NaN), and NaN / inf columns (NaN row and column)."""
+    rng = np.random.default_rng({"spikes": 1, "scales": 2, "constant": 3, "nonfinite": 4}[kind])
+    N, n = 3000, 70
+    X = synth.gaussian_sem(n, N, seed=11, w_low=0.2, w_high=0.8)
+    if kind == "spikes":
+        for j in range(0, n, 3):
+            X[rng.integers(0, N, 3), j] += rng.choice([-1, 1], 3) * 100 * X[:, j].std()
+    elif kind == "scales":
+        X *= 10.0 ** rng.uniform(-8, 7, n)
+        X[:, 5] += 1e9
+    elif kind == "constant":           # exactly summable: mean exact, variance 0, numpy's 0/0
+        X[:, 3] = 0.0
+        X[:, 7] = 2.5
+    else:
+        X[17, 4] = np.nan
+        X[5, 8] = np.inf
+    with np.errstate(invalid="ignore", divide="ignore"):
+        ref = np.corrcoef(X.T)
+    C = eng.corr(X).cpu().numpy()
+    np.testing.assert_array_equal(np.isnan(C), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    np.testing.assert_allclose(C[ok], ref[ok], rtol=0, atol=2e-14)
+
+
 @pytest.mark.parametrize("n,N", [(44, 7000), (3, 40000), (130, 8193), (200, 33), (64, 32 * 256 + 5)])
 def test_corr_small_n_many_slabs(eng, n, N):
     """Small n splits K into up to 256 slabs of >= 32 rows (RQ2-shaped cases); ragged N and the
