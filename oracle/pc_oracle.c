@@ -148,13 +148,27 @@ static int level_pass(const orc_level *L, int64_t *tests_out, int64_t *calls_out
     const int n = L->n, W = L->W, d = L->d;
     int64_t tests = 0, calls = 0, indep = 0;
     volatile int error = 0;
+    /* work items = (x, y) visits, so that one high-degree node (work ~ D^(d+1)) is spread over
+       the threads instead of forming a tail */
+    int64_t nitem = 0;
+    for (int x = L->x0; x < n; x += L->xstep)
+        if (L->deg[x] >= d - 1) nitem += L->deg[x];
+    int32_t *item = (int32_t *)malloc(sizeof(int32_t) * 2 * (size_t)(nitem > 0 ? nitem : 1));
+    if (!item) return -1;
+    {
+        int64_t k = 0;
+        for (int x = L->x0; x < n; x += L->xstep)
+            if (L->deg[x] >= d - 1)
+                for (int yi = 0; yi < L->deg[x]; ++yi) { item[2 * k] = x; item[2 * k + 1] = yi; ++k; }
+    }
 #pragma omp parallel for schedule(dynamic, 1) reduction(+ : tests, calls, indep)
-    for (int x = L->x0; x < n; x += L->xstep) {
+    for (int64_t it = 0; it < nitem; ++it) {
+        const int x = item[2 * it];
         const int D = L->deg[x];
-        if (D < d - 1) continue;
         const int32_t *nx = L->nbr + (size_t)x * n;
         int idx[ORC_MAXD + 1], S[ORC_MAXD + 1];
-        for (int yi = 0; yi < D; ++yi) {
+        {
+            const int yi = item[2 * it + 1];
             const int y = nx[yi];
             const uint64_t *ady = L->adj + (size_t)y * W;
             /* combinations of nx \ {y} of size d, lexicographic */
@@ -217,6 +231,7 @@ static int level_pass(const orc_level *L, int64_t *tests_out, int64_t *calls_out
             }
         }
     }
+    free(item);
     *tests_out = tests;
     *calls_out = calls;
     *indep_out = indep;
