@@ -285,7 +285,10 @@ __global__ __launch_bounds__(256) void k_xtx(const double *X, int64_t N, int n, 
 // normalisation run as in the fp64 path (k_normalize_tiles / k_slab_sum / k_gather_finish).
 // Cost: 45 int8 GEMMs of the upper triangle = 45 x N n^2 int8 MACs at 2x the BF16 MFMA rate
 // (vs N n^2 fp64 MACs at 1/32 of it), plus one pass that writes 9 digit planes.
-constexpr int K1_DIG = 9;                    // digits per value (7 bits each)
+#ifndef PCG_K1_DIG
+#define PCG_K1_DIG 9          // digits per value (7 bits each); A/B knob
+#endif
+constexpr int K1_DIG = PCG_K1_DIG;
 constexpr int K1_LEVELS = K1_DIG;            // p + q = 2 .. K1_DIG + 1
 constexpr int K1_TB = 32;                    // rows (t) per digit block = the MFMA K
 constexpr int K1_I8_MAXK = 14336;            // rows per slab: 9 * 14336 * 127^2 < 2^31

@@ -112,6 +112,10 @@ struct pcg_handle {
     int narrow_deg = 64;             // pcg_set_narrow_degree (testing: route more nodes to the wide class)
     bool tgroup = false;             // small class runs k_level_lds_t this depth
     bool wavek = false;              // small class runs k_level_wave this depth (deep levels)
+    bool sp = false;                 // small class runs k_level_sp this depth (Schur-prefix sweep)
+    DevBuf cblk, lmk;                // k_level_sp: per-node compact correlation blocks, local masks
+    std::vector<int64_t> sp_ctab, sp_coff;   // k_level_sp chunk tables per degree (host copies)
+    int64_t sp_tab_off = 0;          // int64 offset of [coff, ctab, bo] in cpre / cpre_pin
     int screen_eff = 0;              // the current depth's effective mask (set by pcg_level_begin)
     int screen_mask = -1;            // depths (bit 1 << d) with the fp32-screened T-group sweep (k_level_lds_f); -1 = default
     int32_t maxdeg = 0;

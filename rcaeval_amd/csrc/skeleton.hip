@@ -119,6 +119,12 @@ struct LevelArgs {
     int64_t chunk_lo;            // first chunk of this launch (within its class)
     int spl;                     // S ranks per lane (LDS-resident kernel)
     int lds_btab_off;            // byte offset of the LDS binomial table (LDS-resident kernel)
+    // Schur-prefix sweep (k_level_sp): per-degree chunk tables and the per-node compact blocks
+    const int64_t *ctab;         // chunk (t0 << 40 | first task << 20 | tasks), per degree D from coff[D]
+    const int64_t *coff;         // SP_DMAX + 2 offsets into ctab
+    const int64_t *bo;           // n + 1 offsets of the compact blocks (doubles)
+    double *cblk;                // per node: C[adj(x) + x, adj(x) + x], stride D + 1, x last
+    uint64_t *lmk;               // per node: local adjacency masks of adj(x), at off[x]
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -2493,6 +2499,571 @@ __global__ __launch_bounds__(256) void k_screen(LevelArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Schur-prefix sweep (threshold mode, fp32 screen, narrow class, depths 3-4; PCG_SP).
+//
+// S = {c} + T with c < T[0] as in k_level_lds_f, T = {t0, (t1,) t}. A block owns a run of lane
+// tasks of one node x whose prefixes t0 take at most sp_pb(D) values; for each it stages
+//     P1 = C - w0 w0^T,  w0 = C[., t0] / sqrt(C[t0, t0])   (the Schur complement given t0)
+// over adj(x) + x, computed in fp64 from the compact block and rounded once to fp32. A lane task
+// = (t0, [t1,] t, candidate group): per y the sweep needs only the one or two Schur steps the
+// prefix does not cover (w_y = P1[y, t1] r1, q_y = (P1[y, t] - w_t w_y) rt) instead of the full
+// L_T^-1 projection of k_level_lds_f, and the task setup (r1, w, rt, q, lambda_c, u_c, c_xx)
+// runs in fp64 from the exact C entries (compact block, L2). The decision, its error bound
+// (|c^ - c| <= 18 u32 (1 + nu)^2, the same form as k_level_lds_f's), the rare path,
+// dedup and unions are k_level_lds_f's.
+#ifndef PCG_SP
+#define PCG_SP 0x10       // depths (bit 1 << d) whose narrow class runs k_level_sp: depth 4 (measured
+                          // 2.36 ms, = k_level_lds_f<4> at 6x less HBM fetch); depth 3 stays on
+                          // k_level_lds_f (0.69 vs 0.78-0.81 ms: ~6 tasks per prefix t0 do not pay for
+                          // staging up to 8 prefixes' P1 per block)
+#endif
+#ifndef PCG_SP_TG
+#define PCG_SP_TG 6       // candidates per lane task
+#endif
+#ifndef PCG_SP_PBUF
+#define PCG_SP_PBUF 32768 // LDS bytes for one block's fp32 P1 buffers
+#endif
+#ifndef PCG_SP_PBMAX
+#define PCG_SP_PBMAX 8    // prefixes t0 per block
+#endif
+#ifndef PCG_SP_MB
+#define PCG_SP_MB 4       // blocks per CU (launch bounds: 128 VGPRs)
+#endif
+#ifndef PCG_SP_XCD
+#define PCG_SP_XCD 1      // XCD-contiguous chunk order (each XCD's L2 sees few nodes at a time)
+#endif
+constexpr int SP_DMAX = 64;
+static_assert(PCG_SP_TG == 4 || PCG_SP_TG == 6 || PCG_SP_TG == 8, "k_level_sp candidate groups of 4, 6 or 8");
+__host__ __device__ constexpr int sp_stride(int D) { return (D + 3) & ~3; }
+__host__ __device__ constexpr int sp_pb(int D) {
+    return PCG_SP_PBUF / (D * sp_stride(D) * 4) < 1 ? 1
+         : (PCG_SP_PBUF / (D * sp_stride(D) * 4) > PCG_SP_PBMAX ? PCG_SP_PBMAX : PCG_SP_PBUF / (D * sp_stride(D) * 4));
+}
+// (t1, t) pairs (depth 4) or t choices (depth 3) after prefix t0, and lane tasks of prefix t0
+__host__ __device__ inline int64_t sp_npair(int D, int DM, int t0) {
+    const int64_t m = D - 1 - t0;
+    if (t0 < 1 || m < DM - 2) return 0;
+    return DM == 4 ? m * (m - 1) / 2 : m;
+}
+__host__ __device__ inline int64_t sp_tasks(int D, int DM, int t0) {
+    return (int64_t)((t0 + PCG_SP_TG - 1) / PCG_SP_TG) * sp_npair(D, DM, t0);
+}
+// LDS layout (bytes) of k_level_sp for a node of degree D (offsets of the doubles, float2 and
+// float arrays stay 8-byte aligned: DS is a multiple of 4)
+struct SpLds {
+    int DS, PB;
+    size_t w0, cdg, pdx, pf, nxs, cell, total;
+};
+// a block's lane tasks run candidate-group major over its prefixes (cells (g, prefix) in that
+// order), so the lanes of a wave share the candidate window: at most ceil(64 / TG) groups x
+// PBMAX prefixes
+constexpr int SP_CMAX = ((SP_DMAX + PCG_SP_TG - 1) / PCG_SP_TG) * PCG_SP_PBMAX;
+__host__ __device__ inline SpLds sp_lds(int D, int mask_bytes) {
+    SpLds s{};
+    s.DS = sp_stride(D);
+    s.PB = sp_pb(D);
+    s.w0 = (size_t)3 * s.DS * mask_bytes;                         // lmask, uself, uprop
+    s.cdg = s.w0 + (size_t)8 * s.PB * (s.DS + 4);                 // w0[PB][DS + 4] (index D = x)
+    s.pdx = s.cdg + (size_t)16 * (s.DS + 4);                      // cdg[DS + 4], cxr[DS + 4]
+    s.pf = s.pdx + (size_t)8 * s.PB * s.DS;                       // Pdx[PB][DS] {P1_yy, P1_xy}
+    s.nxs = s.pf + (size_t)4 * s.PB * D * s.DS;                   // Pf[PB][D][DS]
+    s.cell = s.nxs + (size_t)4 * s.DS;                            // nxs[DS]
+    s.total = s.cell + (size_t)4 * (2 * SP_CMAX + 2);             // cell prefix [CMAX + 1], info [CMAX], count
+    return s;
+}
+
+// the per-node compact blocks of the nodes with a chunk in [s_lo, s_hi): C[adj(x) + x, adj(x) + x]
+// (row-major, stride D + 1, x last; each C entry read once, in C's own orientation) and the
+// local adjacency masks (bit k of row t: nbr t and nbr k adjacent)
+__global__ __launch_bounds__(256) void k_node_blocks(LevelArgs a, int64_t s_lo, int64_t s_hi) {
+    const int x = blockIdx.x;
+    if (a.cpre[x + 1] <= s_lo || a.cpre[x] >= s_hi || a.cpre[x + 1] == a.cpre[x]) return;
+    const int D = a.deg[x];
+    const int L = D + 1;
+    __shared__ int ids[SP_DMAX + 1];
+    const int32_t *nx = a.nbr + a.off[x];
+    for (int i = threadIdx.x; i < D; i += blockDim.x) ids[i] = nx[i];
+    if (threadIdx.x == 0) ids[D] = x;
+    __syncthreads();
+    double *cb = a.cblk + a.bo[x];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    // rows: a wave per row, lane = column (D + 1 <= 65: lane 0 also takes column 64)
+    for (int r = wv; r < L; r += nwv) {
+        const double *row = a.C + (int64_t)ids[r] * a.ldc;
+        for (int k = lane; k < L; k += 64) cb[r * L + k] = row[ids[k]];
+        if (r < D) {
+            const uint64_t *ar = a.adj + (int64_t)ids[r] * a.W;
+            const bool bit = lane < D && ((ar[ids[lane] >> 6] >> (ids[lane] & 63)) & 1ull);
+            const unsigned long long m = __ballot(bit);
+            if (lane == 0) a.lmk[a.off[x] + r] = m;
+        }
+    }
+}
+
+template <int DM>
+__global__ __launch_bounds__(256, PCG_SP_MB) void k_level_sp(LevelArgs a) {
+    using Mask = unsigned long long;
+    constexpr int DT = DM - 1;                                    // |T|
+    constexpr int TG = PCG_SP_TG;
+    constexpr int NP = TG / 2;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x;
+    int64_t bid = blockIdx.x;
+    if (PCG_SP_XCD) {   // workgroups go to the 8 XCDs round-robin: give each XCD a contiguous chunk range
+        const int64_t nbk = gridDim.x, q = nbk >> 3, r = nbk & 7, xcd = bid & 7, i = bid >> 3;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + i;
+    }
+    const int64_t chunk = a.chunk_lo + bid;
+    int lo = 0, hi = a.n;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (a.cpre[mid] <= chunk) lo = mid; else hi = mid;
+    }
+    const int x = lo;
+    const int D = a.deg[x];
+    const int L = D + 1;
+    const SpLds ly = sp_lds(D, 8);
+    const int DS = ly.DS;
+    Mask *lmask = reinterpret_cast<Mask *>(smem);
+    Mask *uself = lmask + DS;
+    Mask *uprop = uself + DS;
+    double *w0s = reinterpret_cast<double *>(smem + ly.w0);      // [PB][DS + 4]
+    double *cdg = reinterpret_cast<double *>(smem + ly.cdg);     // C(r, r), r = D: C(x, x)
+    double *cxr = cdg + DS + 4;                                   // C(x, r)
+    f2v *Pdx = reinterpret_cast<f2v *>(smem + ly.pdx);           // [PB][DS]
+    float *Pf = reinterpret_cast<float *>(smem + ly.pf);         // [PB][D * DS]
+    int32_t *nxs = reinterpret_cast<int32_t *>(smem + ly.nxs);
+    int32_t *cpre_ = reinterpret_cast<int32_t *>(smem + ly.cell);  // [SP_CMAX + 1]
+    int32_t *cinfo = cpre_ + SP_CMAX + 1;                          // g | b << 8 | j0 << 12
+    int32_t *s_ncell = cinfo + SP_CMAX;
+
+    const int64_t e = a.ctab[a.coff[D] + (chunk - a.cpre[x])];
+    const int t0s = (int)(e >> 40);
+    const int ks = (int)((e >> 20) & 0xFFFFF);
+    const int nt = (int)(e & 0xFFFFF);
+    // buffers: prefixes t0s, t0s + 1, ... until the chunk's tasks are covered (<= sp_pb(D))
+    int nb = 0;
+    {
+        int acc = 0;
+        for (int b = 0; b < PCG_SP_PBMAX && acc < nt; ++b) {
+            acc += (int)sp_tasks(D, DM, t0s + b) - (b == 0 ? ks : 0);
+            nb = b + 1;
+        }
+    }
+    if (tid == 0) {   // cells (g, b): the tasks of prefix t0s + b in candidate group g, g-major
+        int nc = 0, acc = 0;
+        const int gmax = (t0s + nb - 1 + TG - 1) / TG;
+        auto upto = [&](int b) {           // the chunk's tasks in prefixes t0s .. t0s + b - 1
+            int s = 0;
+            for (int q = 0; q < b; ++q) s += (int)sp_tasks(D, DM, t0s + q) - (q == 0 ? ks : 0);
+            return min(s, nt);
+        };
+        for (int g = 0; g < gmax; ++g)
+            for (int b = 0; b < nb; ++b) {
+                const int np_ = (int)sp_npair(D, DM, t0s + b);
+                const int klo = b == 0 ? ks : 0, khi = klo + (upto(b + 1) - upto(b));
+                const int lo_ = max(klo, g * np_), hi_ = min(khi, (g + 1) * np_);
+                if (hi_ <= lo_) continue;
+                cpre_[nc] = acc;
+                cinfo[nc] = g | (b << 8) | ((lo_ - g * np_) << 12);
+                acc += hi_ - lo_;
+                ++nc;
+            }
+        cpre_[nc] = acc;
+        *s_ncell = nc;
+    }
+    const double *cb = a.cblk + a.bo[x];
+    for (int i = tid; i < D; i += 256) {
+        nxs[i] = a.nbr[a.off[x] + i];
+        lmask[i] = a.lmk[a.off[x] + i];
+        uself[i] = 0;
+        uprop[i] = 0;
+    }
+    for (int r = tid; r < L; r += 256) {
+        cdg[r] = cb[r * L + r];
+        cxr[r] = cb[D * L + r];
+    }
+    for (int i = tid; i < nb * L; i += 256) {
+        const int b = i / L, r = i - b * L, t0 = t0s + b;
+        w0s[b * (DS + 4) + r] = cb[r * L + t0] / sqrt(cb[t0 * L + t0]);
+    }
+    if (tid < nb) {   // per prefix, in w0's padding: 1 / C(t0, t0) (= ||L_t0^-1||_F^2) and C(t0, t0)
+        const double g0 = cb[(t0s + tid) * L + t0s + tid];
+        w0s[tid * (DS + 4) + DS + 1] = 1.0 / g0;
+        w0s[tid * (DS + 4) + DS + 2] = g0;
+    }
+    __syncthreads();
+    {   // P1 in fp32: a wave per row t, lane = column k (D <= 64)
+        const int lane = tid & 63, wv = tid >> 6;
+        for (int t = wv; t < D; t += 4) {
+            const double v = lane < D ? cb[t * L + lane] : 0.0;
+            for (int b = 0; b < nb; ++b) {
+                const double *w = w0s + b * (DS + 4);
+                if (lane < DS) Pf[(b * D + t) * DS + lane] = lane < D ? (float)(v - w[t] * w[lane]) : 0.0f;
+                if (lane == 0) {
+                    const f2v dxv = {(float)(cdg[t] - w[t] * w[t]), (float)(cxr[t] - w[D] * w[t])};
+                    Pdx[b * DS + t] = dxv;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    int tx = 0;
+    {
+        int lo2 = 0, hi2 = D;                 // first local index with global id > x
+        while (lo2 < hi2) {
+            const int mid = (lo2 + hi2) >> 1;
+            if (nxs[mid] < x) lo2 = mid + 1; else hi2 = mid;
+        }
+        tx = lo2;
+    }
+
+    unsigned long long tests = 0, indep = 0;
+    unsigned tcount = 0;
+    const unsigned long long lanebit = 1ull << (tid & 63);
+    const float inv_sf = (float)a.inv_s;
+    const float lo2f = (float)(a.lo2 * (1.0 - 4.0 * F32_U));
+    const float hi2f = (float)(a.hi2 * (1.0 + 4.0 * F32_U));
+    const f2v s2 = {(float)(a.s_amgm * (1.0 + 4.0 * F32_U)), (float)(a.s_amgm * (1.0 + 4.0 * F32_U))};
+    constexpr double RUd = 1.0 + 16.0 * F32_U;
+    const f2v ke2 = {(float)(2.0 * PCG_F32_KE * F32_U * RUd), (float)(2.0 * PCG_F32_KE * F32_U * RUd)};
+    const f2v ke2u = {(float)((2.0 * PCG_F32_KE + 1.0) * F32_U * RUd), (float)((2.0 * PCG_F32_KE + 1.0) * F32_U * RUd)};
+    const f2v inv_su = {(float)(a.inv_s * RUd), (float)(a.inv_s * RUd)};
+    const f2v tauu = {(float)(a.tau * RUd * RUd), (float)(a.tau * RUd * RUd)};
+    const f2v two_u = {(float)(2.0 * (1.0 + 8.0 * F32_U) * RUd), (float)(2.0 * (1.0 + 8.0 * F32_U) * RUd)};
+    const f2v one_u = {(float)((1.0 + 8.0 * F32_U) * RUd), (float)((1.0 + 8.0 * F32_U) * RUd)};
+    const f2v s2u = s2 + (float)F32_U;
+
+    const int ncell = *s_ncell;
+    for (int task = tid; task < nt; task += 256) {
+        int clo = 0, chi = ncell;
+        while (chi - clo > 1) {
+            const int mid = (clo + chi) >> 1;
+            if (cpre_[mid] <= task) clo = mid; else chi = mid;
+        }
+        const int info = cinfo[clo];
+        const int g = info & 255, b = (info >> 8) & 15;
+        const int j = (info >> 12) + (task - cpre_[clo]);
+        const int t0 = t0s + b;
+        int t1 = 0, t;
+        if constexpr (DM == 4) {   // colex pair (a_ < b_) of [0, D - 1 - t0): j = b_(b_-1)/2 + a_
+            int b_ = (int)((1.0f + __builtin_sqrtf(1.0f + 8.0f * (float)j)) * 0.5f);
+            while (b_ * (b_ - 1) / 2 > j) --b_;
+            while ((b_ + 1) * b_ / 2 <= j) ++b_;
+            t1 = t0 + 1 + (j - b_ * (b_ - 1) / 2);
+            t = t0 + 1 + b_;
+        } else {
+            t = t0 + 1 + j;
+        }
+        const int cbase = g * TG;
+        const int nval = min(t0 - cbase, TG);
+        int nmax_ = 1;
+#pragma unroll
+        for (int q = 2; q <= TG; ++q) nmax_ += (__ballot(nval >= q) != 0);
+        const int nmax = __builtin_amdgcn_readfirstlane(nmax_);
+        Mask Tmask = ((Mask)1 << t0) | ((Mask)1 << t);
+        if constexpr (DM == 4) Tmask |= (Mask)1 << t1;
+        const double *w0 = w0s + b * (DS + 4);
+        const float *Pb = Pf + (size_t)b * D * DS;
+        const f2v *Pdxb = Pdx + b * DS;
+
+        // task setup in fp64 from the exact C entries (P1(r, s) = C(r, s) - w0_r w0_s)
+        const double g0 = w0[DS + 2];
+        const double liF0 = w0[DS + 1];
+        double r1 = 0.0, wt = 0.0, wx = 0.0, liF1 = liF0, g1 = 1.0;
+        if constexpr (DM == 4) {
+            const double p11 = cdg[t1] - w0[t1] * w0[t1];
+            r1 = rsq_nr(p11);
+            wt = (cb[t * L + t1] - w0[t] * w0[t1]) * r1;
+            wx = (cxr[t1] - w0[D] * w0[t1]) * r1;
+            liF1 = liF0 + (liF0 * w0[t1] * w0[t1] + 1.0) * r1 * r1;
+            g1 = p11;
+        }
+        const double lt2 = cdg[t] - w0[t] * w0[t] - wt * wt;
+        const double rt = rsq_nr(lt2);
+        const double qx = (cxr[t] - w0[D] * w0[t] - wx * wt) * rt;
+        const double pxx = cdg[D] - w0[D] * w0[D] - wx * wx - qx * qx;
+        const double liF = liF1 + (liF1 * (w0[t] * w0[t] + wt * wt) + 1.0) * rt * rt;
+        const bool okT = g0 > 0.0 && g1 > 0.0 && lt2 > 0.0;
+        const double gT = fmin(fmin(g0, g1), lt2);
+        const float r1f = (float)r1, wtf = (float)wt, rtf = (float)rt, wxf = (float)wx, qxf = (float)qx;
+        f2v wcp[NP], qcp[NP], rlp[NP], ucp[NP], mp[NP], hhp[NP], k1p[NP], k2p[NP];
+        bool okc[TG];
+        f2v cxp[NP], l2p[NP], r2p[NP], llp[NP];
+        bool vldc[TG];
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int jj = 2 * q + h;
+                wcp[q][h] = qcp[q][h] = rlp[q][h] = ucp[q][h] = 0.0f;
+                cxp[q][h] = l2p[q][h] = r2p[q][h] = llp[q][h] = 0.0f;
+                vldc[jj] = false;
+                if (jj < nmax) {                      // wave-uniform
+                    const int c = cbase + jj;
+                    const bool valid = c < t0;
+                    const int cc = valid ? c : 0;
+                    double wc = 0.0;
+                    if constexpr (DM == 4) wc = (cb[cc * L + t1] - w0[cc] * w0[t1]) * r1;
+                    const double qc = (cb[cc * L + t] - w0[cc] * w0[t] - wc * wt) * rt;
+                    const double lam2 = cdg[cc] - w0[cc] * w0[cc] - wc * wc - qc * qc;
+                    const double r = rsq_nr(lam2);
+                    const double u = (cxr[cc] - w0[D] * w0[cc] - wx * wc - qx * qc) * r;
+                    wcp[q][h] = (float)wc;
+                    qcp[q][h] = (float)qc;
+                    rlp[q][h] = (float)r;
+                    ucp[q][h] = (float)u;
+                    cxp[q][h] = (float)(pxx - u * u);
+                    l2p[q][h] = (float)lam2;
+                    r2p[q][h] = (float)(r * r);
+                    llp[q][h] = (float)(cdg[cc] - lam2);  // |l_c|^2: explained by T
+                    vldc[jj] = valid && okT && (lam2 > 0.0);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const float liFf = (float)(liF * RUd);
+        const float gTf = (float)gT * (1.0f - (float)(4.0 * F32_U));
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {   // decision bounds: k_level_lds_f's, term for term
+            const f2v cxf = cxp[q], l2f = l2p[q], r2f = r2p[q], llf = llp[q];
+            constexpr float U = (float)F32_U;
+            constexpr float RD = 1.0f - 16.0f * U, U8 = 8.0f * U;
+            const f2v one = {1.0f, 1.0f};
+            const f2v liF2 = {liFf, liFf};
+            const f2v nu2 = __builtin_elementwise_fma(__builtin_elementwise_fma(liF2, llf, one), r2f, liF2);
+            const f2v E = __builtin_elementwise_fma(nu2, ke2, ke2u);
+            const f2v te = E * inv_su;
+            const f2v gT2 = {gTf, gTf};
+            const f2v gg = (__builtin_elementwise_min(gT2, l2f) - (E + 2.0f * U)) * RD;
+            const f2v cmE = (cxf - E) * RD;
+            const f2v rg = {__builtin_amdgcn_rcpf(gg[0]), __builtin_amdgcn_rcpf(gg[1])};
+            const f2v kg = tauu * rg;
+            const f2v hx = hi2f * (cxf + E);
+            const f2v f1 = __builtin_elementwise_fma(te, two_u, one_u);
+            const f2v al = hx * f1;
+            const f2v be = E * (hx + s2) * f1;
+            const f2v ga = (cmE - cmE * te) * ((1.0f - U8) * RD);
+            const f2v ka = __builtin_elementwise_fma(E, cxf + s2u, kg) * ((1.0f + U8) * (1.0f + 16.0f * U));
+            const f2v mm = 0.5f * (al + ga);
+            const f2v hw = __builtin_elementwise_fma(-2.0f * U8 * one, ga, 0.5f * (ga - al));
+            const f2v kk1 = 0.5f * (be - ka);
+            const f2v kk2 = (be + ka) * (0.5f * (1.0f + U8));
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const bool ok = vldc[2 * q + h] && (te[h] <= 0.5f) && (cmE[h] > 0.0f) && (gg[h] > 0.0f) && (ga[h] > al[h]);
+                okc[2 * q + h] = ok;
+                mp[q][h] = ok ? mm[h] : 0.0f;
+                hhp[q][h] = ok ? hw[h] : -1.0f;
+                k1p[q][h] = ok ? kk1[h] : 0.0f;
+                k2p[q][h] = ok ? kk2[h] : 1.0f;
+            }
+            // opaque: the rare path must read these registers, not keep (spill) the unselected values
+            asm volatile("" : "+v"(mp[q]), "+v"(hhp[q]), "+v"(k1p[q]), "+v"(k2p[q]));
+        }
+        const int cend = min(t0, cbase + TG);
+        unsigned okm = 0;
+#pragma unroll
+        for (int jj = 0; jj < TG; ++jj) okm |= (unsigned)okc[jj] << jj;
+        const unsigned vmask = (1u << (cend - cbase)) - 1u;
+        constexpr bool SG = (PCG_TGF_SGPR >> DM) & 1;
+        unsigned long long okv[TG];
+        if (SG) tcount += (unsigned)(nval * (D - DT - 1));
+#pragma unroll
+        for (int jj = 0; jj < TG; ++jj) okv[jj] = __builtin_amdgcn_ballot_w64(okc[jj]);
+        const unsigned long long notok = __builtin_amdgcn_ballot_w64((vmask & ~okm) != 0u);
+        const int cb0 = __builtin_amdgcn_readfirstlane(cbase);
+        const bool uni = __builtin_amdgcn_ballot_w64(cbase != cb0) == 0ull;
+
+        // a live test of candidate jj at y = ty that the sweep's check did not make certain
+        auto rare_cand = [&](int jj, int ty, const float *Pr, float wy, float qy, float byy, float bxy, Mask lm) {
+            const int q = jj >> 1, h = jj & 1;
+            int c = cbase + jj;
+            asm volatile("" : "+v"(c));      // no per-candidate masks / ids hoisted into the hot loop
+            if (okc[jj]) {
+                float s_ = Pr[c];
+                if constexpr (DM == 4) s_ = fmaf(-wcp[q][h], wy, s_);
+                s_ = fmaf(-qcp[q][h], qy, s_);
+                const float vc = s_ * rlp[q][h];
+                const float cyy = fmaf(-vc, vc, byy);
+                const float cxy = fmaf(-ucp[q][h], vc, bxy);
+                const float w = fmaf(-mp[q][h], cyy, fmaf(cxy, cxy, -k1p[q][h]));
+                if (__builtin_fabsf(w) < fmaf(hhp[q][h], cyy, -k2p[q][h])) return;
+                constexpr float U8 = (float)(8.0 * F32_U);
+                float m_ = mp[q][h], hh_ = hhp[q][h], k1_ = k1p[q][h], k2_ = k2p[q][h];
+                asm volatile("" : "+v"(m_), "+v"(hh_), "+v"(k1_), "+v"(k2_));
+                const float Alb = (m_ + hh_) * (1.0f - U8);
+                const float Eub = (k1_ + k2_) * inv_sf * (1.0f + U8);
+                const float kgub = (k2_ - k1_) * (1.0f + U8);
+                const float ay = (cyy - Eub) * (1.0f - U8);
+                const float ax = (__builtin_fabsf(cxy) + Eub) * (1.0f + U8);
+                if (ay > 0.0f && ax * ax * (1.0f + U8) < lo2f * Alb * ay &&
+                    fmaf(ax, ax, kgub) * (1.0f + U8) < Alb * ay) {
+                    const Mask Smask = Tmask | ((Mask)1 << c);
+                    ++indep;
+                    lmask_atomic_or<false>(&uself[ty], Smask);
+                    if (((lm & Smask) == Smask) && ty >= tx) lmask_atomic_or<false>(&uprop[ty], Smask);
+                    return;
+                }
+            }
+            int sg[DM];
+            sg[0] = nxs[c];
+            sg[1] = nxs[t0];
+            if constexpr (DM == 4) sg[2] = nxs[t1];
+            sg[DM - 1] = nxs[t];
+            push_screen(a, x, nxs[ty], sg, DM);
+        };
+        auto sweep = [&](auto nc_tag) {
+            constexpr int NC = decltype(nc_tag)::value;
+            constexpr int NQ = NC / 2;
+            auto ystep = [&](int ty, auto ym_tag) {
+                constexpr int YM = decltype(ym_tag)::value;
+                const float *Pr = Pb + ty * DS;
+                f2v sc[NQ];
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) sc[q] = *reinterpret_cast<const f2v *>(Pr + cbase + 2 * q);
+                float wy = 0.0f, qy;
+                f2v b2 = Pdxb[ty];                     // {P1_yy, P1_xy}
+                if constexpr (DM == 4) {
+                    wy = Pr[t1] * r1f;
+                    qy = fmaf(-wtf, wy, Pr[t]) * rtf;
+                    const f2v wv = {wy, wxf}, wb = {wy, wy};
+                    b2 = __builtin_elementwise_fma(-wv, wb, b2);
+                } else {
+                    qy = Pr[t] * rtf;
+                }
+                {
+                    const f2v qv = {qy, qxf}, qb = {qy, qy};
+                    b2 = __builtin_elementwise_fma(-qv, qb, b2);
+                }
+                const float byy = b2[0];
+                const float bxy = b2[1];
+                const f2v qb = {qy, qy};
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    if constexpr (DM == 4) {
+                        const f2v wb = {wy, wy};
+                        sc[q] = __builtin_elementwise_fma(-wcp[q], wb, sc[q]);
+                    }
+                    sc[q] = __builtin_elementwise_fma(-qcp[q], qb, sc[q]);
+                }
+                const f2v byy2 = {byy, byy}, bxy2 = {bxy, bxy};
+                const Mask lm = lmask[ty];
+                if constexpr (YM == 3) {
+                    unsigned dp = 0;
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        const f2v vc = sc[q] * rlp[q];
+                        const f2v cyy = __builtin_elementwise_fma(-vc, vc, byy2);
+                        const f2v cxy = __builtin_elementwise_fma(-ucp[q], vc, bxy2);
+                        const f2v nm = __builtin_elementwise_fma(cxy, cxy, -k1p[q]);
+                        const f2v w = __builtin_elementwise_fma(-mp[q], cyy, nm);
+                        const f2v hh = __builtin_elementwise_fma(hhp[q], cyy, -k2p[q]);
+                        dp |= ((unsigned)(__builtin_fabsf(w[0]) < hh[0]) << (2 * q)) |
+                              ((unsigned)(__builtin_fabsf(w[1]) < hh[1]) << (2 * q + 1));
+                    }
+                    const bool inTset = (bool)((Tmask >> ty) & 1u);
+                    const bool own = (ty < tx) && ((lm & Tmask) == Tmask);
+                    const unsigned tb = ((unsigned)(ty - cbase) < (unsigned)TG) ? (1u << (ty - cbase)) : 0u;
+                    const unsigned skip = own ? (unsigned)(lm >> cbase) : 0u;
+                    const unsigned live = inTset ? 0u : (vmask & ~tb & ~skip);
+                    tcount += __popc(live);
+                    const unsigned rare = live & ~(dp & okm);
+                    if (__builtin_amdgcn_ballot_w64(rare != 0u)) {
+                        if (rare) {
+#pragma unroll
+                            for (int jj = 0; jj < TG; ++jj)
+                                if ((rare >> jj) & 1u) rare_cand(jj, ty, Pr, wy, qy, byy, bxy, lm);
+                        }
+                    }
+                    return;
+                } else {
+                    const int jdead = YM == 1 ? ty - cb0 : -1;
+                    unsigned long long bad = 0ull;
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        const f2v vc = sc[q] * rlp[q];
+                        const f2v cyy = __builtin_elementwise_fma(-vc, vc, byy2);
+                        const f2v cxy = __builtin_elementwise_fma(-ucp[q], vc, bxy2);
+                        const f2v nm = __builtin_elementwise_fma(cxy, cxy, -k1p[q]);
+                        const f2v w = __builtin_elementwise_fma(-mp[q], cyy, nm);
+                        const f2v hh = __builtin_elementwise_fma(hhp[q], cyy, -k2p[q]);
+                        const unsigned long long keep0 = 2 * q == jdead ? 0ull : okv[2 * q];
+                        const unsigned long long keep1 = 2 * q + 1 == jdead ? 0ull : okv[2 * q + 1];
+                        bad |= keep0 & ~__builtin_amdgcn_ballot_w64(__builtin_fabsf(w[0]) < hh[0]);
+                        bad |= keep1 & ~__builtin_amdgcn_ballot_w64(__builtin_fabsf(w[1]) < hh[1]);
+                    }
+                    // lanes that need the per-lane path; y in T is masked only when some lane does
+                    unsigned long long rarel = bad | notok;
+                    if (YM == 2) rarel |= __builtin_amdgcn_ballot_w64((unsigned)(ty - cbase) < (unsigned)nval);
+                    if (ty < tx) rarel |= __builtin_amdgcn_ballot_w64((lmask[ty] & Tmask) == Tmask);
+                    if (!rarel) return;
+                    rarel &= ~__builtin_amdgcn_ballot_w64((bool)((Tmask >> ty) & 1u));
+                    if (!(rarel & lanebit)) return;
+                    const bool own = (ty < tx) && ((lm & Tmask) == Tmask);
+                    const unsigned tb = ((unsigned)(ty - cbase) < (unsigned)TG) ? (1u << (ty - cbase)) : 0u;
+                    const unsigned skip = own ? (unsigned)(lm >> cbase) : 0u;
+                    if ((Tmask >> ty) & 1u) return;
+                    const unsigned live = vmask & ~tb & ~skip;
+                    tcount -= __popc(vmask & ~tb & skip);
+#pragma unroll
+                    for (int jj = 0; jj < TG; ++jj)
+                        if ((live >> jj) & 1u) rare_cand(jj, ty, Pr, wy, qy, byy, bxy, lm);
+                }
+            };
+            using Y1 = std::integral_constant<int, 1>;
+            using Y2 = std::integral_constant<int, 2>;
+            using Y3 = std::integral_constant<int, 3>;
+            if (!SG) {
+                for (int ty = 0; ty < D; ++ty) ystep(ty, Y3{});
+            } else if (uni) {
+                for (int ty = 0; ty < D; ++ty) ystep(ty, Y1{});
+            } else {
+                for (int ty = 0; ty < D; ++ty) ystep(ty, Y2{});
+            }
+        };
+        if constexpr (TG == 4) {
+            if (nmax > 2) sweep(std::integral_constant<int, 4>{});
+            else sweep(std::integral_constant<int, 2>{});
+        } else if constexpr (TG == 6) {
+            if (nmax > 4) sweep(std::integral_constant<int, 6>{});
+            else if (nmax > 2) sweep(std::integral_constant<int, 4>{});
+            else sweep(std::integral_constant<int, 2>{});
+        } else {
+            if (nmax > 6) sweep(std::integral_constant<int, 8>{});
+            else if (nmax > 4) sweep(std::integral_constant<int, 6>{});
+            else if (nmax > 2) sweep(std::integral_constant<int, 4>{});
+            else sweep(std::integral_constant<int, 2>{});
+        }
+        tests += tcount;
+        tcount = 0;
+    }
+    __syncthreads();
+    for (int ty = tid; ty < D; ty += 256) {
+        const Mask us = uself[ty], up = uprop[ty];
+        if (!(us | up)) continue;
+        const int yg = nxs[ty];
+        a.rm[(int64_t)x * a.n + yg] = 1;
+        a.rm[(int64_t)yg * a.n + x] = 1;
+        for (int side = 0; side < 2; ++side) {
+            const Mask bits = side ? up : us;
+            if (!bits) continue;
+            const int64_t slot = side ? (int64_t)a.off[yg] + find_in_sorted(a.nbr + a.off[yg], a.deg[yg], x)
+                                      : (int64_t)a.off[x] + ty;
+            unsigned long long *row = reinterpret_cast<unsigned long long *>(a.ug + slot * a.W);
+            unsigned long long m = bits;
+            while (m) {
+                const int bb = __ffsll((long long)m) - 1;
+                const int gid = nxs[bb];
+                atomicOr(&row[gid >> 6], 1ull << (gid & 63));
+                m &= m - 1;
+            }
+        }
+    }
+    block_flush_counts(a.ctr, tests, indep);
+}
+
+// ---------------------------------------------------------------------------------------
 // depths > PCG_MAX_DEPTH (degenerate graphs, e.g. constant columns whose NaN correlations
 // never separate): one thread per (x, S rank), exact LU path per test with per-thread
 // scratch in global memory. Throughput is not the goal here; semantics are.
@@ -3029,6 +3600,14 @@ LevelArgs make_args(pcg_handle *h, int d, int mode_exact_all) {
     a.rec_mod = h->rec_mod;
     a.rec_res = h->rec_res;
     a.spl = h->spl;
+    if (h->sp) {
+        const int64_t *t = (const int64_t *)h->cpre.p + h->sp_tab_off;
+        a.coff = t;
+        a.ctab = t + SP_DMAX + 2;
+        a.bo = a.ctab + h->sp_ctab.size();
+        a.cblk = (double *)h->cblk.p;
+        a.lmk = (uint64_t *)h->lmk.p;
+    }
     (void)mode_exact_all;
     return a;
 }
@@ -3323,9 +3902,12 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
     // work decomposition: depth 0 = one chunk per row; depth >= 1 = three node classes:
     // narrow (D <= 64: LDS-resident kernels), wide (64 < D <= 128 at the T-group depths: the
     // T-group kernel with 128-bit masks), large (the rest: staged generic kernels)
-    if (!pcg_ensure_pinned(h, h->cpre_pin, sizeof(int64_t) * 3 * (n + 1)))
-        return pcg_fail(h, PCG_ERR_OOM, "pinned chunk prefix");
-    int64_t *cs = (int64_t *)h->cpre_pin.p, *cw = cs + (n + 1), *cl = cw + (n + 1);
+    h->cpre_h.assign(3 * (size_t)(n + 1), 0);
+    int64_t *cs = h->cpre_h.data(), *cw = cs + (n + 1), *cl = cw + (n + 1);
+    std::vector<int64_t> bo;           // k_level_sp compact-block offsets (doubles)
+    h->sp = false;
+    h->sp_ctab.clear();
+    h->sp_coff.assign(SP_DMAX + 2, 0);
     h->work_h.assign(n, 0);
     h->maxdeg_small = 0;
     h->maxdeg_wide = 0;
@@ -3356,6 +3938,11 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
         const char *sm = getenv("PCG_SCREEN_MASK");
         h->screen_eff = sm ? (int)strtol(sm, nullptr, 0) : (h->screen_mask < 0 ? PCG_TG_F32 : h->screen_mask);
         h->screen_eff &= 0x1c;   // the error bound (KE = 64) is derived for d = 2..4 only
+        {   // Schur-prefix sweep for the narrow class (PCG_SP A/B knob, read per depth)
+            const char *spe = getenv("PCG_SP");
+            const int spm = spe ? (int)strtol(spe, nullptr, 0) : PCG_SP;
+            h->sp = tg && use_screen32(h, depth) && (depth == 3 || depth == 4) && ((spm >> depth) & 1);
+        }
         std::vector<uint64_t> ns_of(maxd + 1, 0), units_of(maxd + 1, 0);
         std::vector<int> cls_of(maxd + 1, 2);
         double sum_small = 0.0, sum_wide = 0.0, sum_large = 0.0;
@@ -3367,6 +3954,11 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
             ns_of[D] = ns;
             cls_of[D] = level_class(h, D, depth, tg);
             units_of[D] = cls_of[D] < 2 ? (tg ? tgroup_tasks(h, D, depth) : ns) : ns;
+            if (h->sp && cls_of[D] == 0) {
+                uint64_t u = 0;
+                for (int t0 = 1; t0 <= D - depth + 1; ++t0) u += (uint64_t)sp_tasks(D, depth, t0);
+                units_of[D] = u;
+            }
             if (!hist[D]) continue;
             if (cls_of[D] == 0) {
                 sum_small += (double)units_of[D] * hist[D];
@@ -3405,18 +3997,49 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
             nch_of[D] = c == 0 ? (int64_t)((units_of[D] + csz - 1) / csz)
                                : c == 1 ? (int64_t)((units_of[D] + cszw - 1) / cszw)
                                         : l1p ? l1_pair_chunks(D) : (int64_t)((ns_of[D] + h->chunk - 1) / h->chunk);
+            if (h->sp && c == 0 && hist[D]) {
+                // k_level_sp chunks of a degree-D node: runs of <= csz consecutive lane tasks
+                // (prefix t0 major) spanning at most sp_pb(D) prefixes
+                h->sp_coff[D] = (int64_t)h->sp_ctab.size();
+                const int pb = sp_pb(D);
+                int64_t cur_t0 = -1, cur_k = 0, cur_n = 0;
+                int cur_b = 0;
+                auto emit = [&]() {
+                    if (cur_n > 0) h->sp_ctab.push_back((cur_t0 << 40) | (cur_k << 20) | cur_n);
+                    cur_n = 0;
+                    cur_b = 0;
+                };
+                for (int t0 = 1; t0 <= D - depth + 1; ++t0) {
+                    const int64_t T = sp_tasks(D, depth, t0);
+                    int64_t pos = 0;
+                    while (pos < T) {
+                        if (cur_n == 0) { cur_t0 = t0; cur_k = pos; }
+                        const int64_t take = std::min<int64_t>(T - pos, (int64_t)csz - cur_n);
+                        cur_n += take;
+                        pos += take;
+                        ++cur_b;
+                        if (cur_n >= (int64_t)csz || cur_b >= pb) emit();
+                    }
+                }
+                emit();
+                nch_of[D] = (int64_t)h->sp_ctab.size() - h->sp_coff[D];
+            }
         }
-        int64_t ss = 0, sw = 0, sl = 0;
+        int64_t ss = 0, sw = 0, sl = 0, sb = 0;
+        if (h->sp) bo.assign(n + 1, 0);
         for (int x = 0; x < n; ++x) {
             cs[x] = ss;
             cw[x] = sw;
             cl[x] = sl;
+            if (h->sp) bo[x] = sb;
             const int D = h->deg_h[x];
             if (D < depth + 1) continue;
             h->work_h[x] = (int64_t)ns_of[D] * (D - depth);
             const int c = cls_of[D];
             (c == 0 ? ss : c == 1 ? sw : sl) += nch_of[D];
+            if (h->sp && c == 0) sb += (int64_t)(D + 1) * (D + 1);
         }
+        if (h->sp) bo[n] = sb;
         cs[n] = ss;
         cw[n] = sw;
         cl[n] = sl;
@@ -3427,13 +4050,33 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
     h->total_chunks = h->total_small + h->total_wide + h->total_large;
     if (total_chunks) *total_chunks = h->total_chunks;
     PCG_HT(h, "begin:decomposed");
-    if (!pcg_ensure(h, h->cpre, sizeof(int64_t) * 3 * (n + 1))) return PCG_ERR_OOM;
+    // host-mapped upload: the three class prefixes, then (k_level_sp) the per-degree chunk table
+    // offsets, the chunk table and the compact-block offsets
+    h->sp_tab_off = 3 * (int64_t)(n + 1);
+    const int64_t cnt = h->sp_tab_off + (h->sp ? (int64_t)(SP_DMAX + 2) + (int64_t)h->sp_ctab.size() + (n + 1) : 0);
+    if (!pcg_ensure_pinned(h, h->cpre_pin, sizeof(int64_t) * cnt))
+        return pcg_fail(h, PCG_ERR_OOM, "pinned chunk prefix");
+    {
+        int64_t *pin = (int64_t *)h->cpre_pin.p;
+        memcpy(pin, h->cpre_h.data(), sizeof(int64_t) * 3 * (n + 1));
+        if (h->sp) {
+            int64_t *p = pin + h->sp_tab_off;
+            memcpy(p, h->sp_coff.data(), sizeof(int64_t) * (SP_DMAX + 2));
+            p += SP_DMAX + 2;
+            if (!h->sp_ctab.empty()) memcpy(p, h->sp_ctab.data(), sizeof(int64_t) * h->sp_ctab.size());
+            p += h->sp_ctab.size();
+            memcpy(p, bo.data(), sizeof(int64_t) * (n + 1));
+            if (!pcg_ensure(h, h->cblk, sizeof(double) * std::max<int64_t>(bo[n], 1)) ||
+                !pcg_ensure(h, h->lmk, sizeof(uint64_t) * std::max<int64_t>(h->sumdeg, 1)))
+                return pcg_fail(h, PCG_ERR_OOM, "Schur-prefix node blocks");
+        }
+    }
+    if (!pcg_ensure(h, h->cpre, sizeof(int64_t) * cnt)) return PCG_ERR_OOM;
     // rm, the counters and the status bytes were cleared by the previous depth's k_apply /
     // k_level_summary (or at init); the union rows by k_fill_nbr (or here, on first use)
     {
         void *src = nullptr;
         PCG_HIP(h, hipHostGetDevicePointer(&src, h->cpre_pin.p, 0));
-        const int64_t cnt = 3 * (int64_t)(n + 1);
         hipLaunchKernelGGL(k_copy_i64, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, h->stream,
                            (const int64_t *)src, cnt, (int64_t *)h->cpre.p);
         PCG_HIP(h, hipGetLastError());
@@ -3516,6 +4159,14 @@ extern "C" int pcg_level_chunk_work(pcg_handle *h, int64_t *prefix_host, int64_t
                 continue;
             }
             const int D = h->deg_h[x];
+            if (cls == 0 && h->sp) {   // k_level_sp: the chunk's lane tasks x candidates x y
+                const int64_t *tab = h->sp_ctab.data() + h->sp_coff[D];
+                for (int64_t c = c0; c < c1; ++c) {
+                    acc += (tab[c - c0] & 0xFFFFF) * PCG_SP_TG * (D - h->depth) + 1;
+                    prefix_host[base + c + 1] = acc;
+                }
+                continue;
+            }
             if (cls == 2 && use_l1_pairs(h, h->depth)) {   // k_level1_pairs: an even share of the pairs, two tests each
                 const int64_t np = (int64_t)D * (D - 1) / 2, nch = c1 - c0;
                 for (int64_t c = c0; c < c1; ++c) {
@@ -3626,6 +4277,14 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                             if (mode == MODE_DECIDE) hipLaunchKernelGGL((k_level_wave<32, MODE_DECIDE>), grid, block, ldsw, h->stream, as);
                             else hipLaunchKernelGGL((k_level_wave<32, MODE_FULLP>), grid, block, ldsw, h->stream, as);
                         }
+                    } else if (h->sp) {
+                        // per-node compact blocks of this range's nodes, then the Schur-prefix sweep
+                        hipLaunchKernelGGL(k_node_blocks, dim3((unsigned)h->n), dim3(256), 0, h->stream, as, s_lo, s_hi);
+                        size_t ldsp = 0;
+                        for (int D = d + 1; D <= h->maxdeg_small; ++D) ldsp = std::max(ldsp, sp_lds(D, 8).total);
+                        const dim3 grid((unsigned)(s_hi - s_lo)), block(256);
+                        if (d == 3) hipLaunchKernelGGL((k_level_sp<3>), grid, block, ldsp, h->stream, as);
+                        else hipLaunchKernelGGL((k_level_sp<4>), grid, block, ldsp, h->stream, as);
                     } else if (h->tgroup && use_screen32(h, d)) {
                         as.lds_btab_off = (int)lds_f32_core(dl, 8);
                         const size_t ldsf = lds_tgroup_f_bytes(dl, d, 8);

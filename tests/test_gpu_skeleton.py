@@ -135,6 +135,20 @@ def test_screen_precision_masks_match_oracle(eng, n, N, seed, wl, wh, ep, narrow
         assert sum(out.stats["screened"]) == 0
 
 
+@pytest.mark.parametrize("sp", ["0", "0x8", "0x10", "0x18"])
+@pytest.mark.parametrize("n,N,seed,wl,wh,ep", CASES[2:] + [(300, 1500, 7, 0.1, 0.6, 0.06)])
+def test_schur_prefix_sweep_matches_oracle(eng, n, N, seed, wl, wh, ep, sp, monkeypatch):
+    """The Schur-prefix sweep (k_level_sp: P1 = C - w0 w0^T staged per prefix t0, chunks of
+    several prefixes per block) on depth 3, depth 4, both, or neither (k_level_lds_f):
+    identical skeletons, unions and per-level counts (PCG_SP is read per depth)."""
+    X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
+    C = np.corrcoef(X.T)
+    ref = cpc.skeleton(C, N)
+    monkeypatch.setenv("PCG_SP", sp)
+    out = eng.skeleton(C, N)
+    assert_skeleton_matches(out, ref, n)
+
+
 def test_screen_list_overflow_reruns(eng):
     """A screen list too small for the fp32 sweep's undecided tests (config 5, depth <= 3:
     ~9e4 of them at depth 3) overflows, the level reports it with the capacity raised, and
