@@ -113,6 +113,7 @@ struct pcg_handle {
     bool tgroup = false;             // small class runs k_level_lds_t this depth
     bool wavek = false;              // small class runs k_level_wave this depth (deep levels)
     bool sp = false;                 // small class runs k_level_sp this depth (Schur-prefix sweep)
+    bool nblk = false;               // small class stages per-node compact blocks (k_node_blocks) this depth
     DevBuf cblk, lmk;                // k_level_sp: per-node compact correlation blocks, local masks
     std::vector<int64_t> sp_ctab, sp_coff;   // k_level_sp chunk tables per degree (host copies)
     int64_t sp_tab_off = 0;          // int64 offset of [coff, ctab, bo] in cpre / cpre_pin

@@ -1835,7 +1835,8 @@ constexpr double F32_U = 5.9604644775390625e-08;   // 2^-24
 #define PCG_TGF_SGPR 0x10 // k_level_lds_f depths (bit 1 << d) whose per-y bookkeeping is in wave lane masks
 #endif
 #ifndef PCG_TGF_SPLIT
-#define PCG_TGF_SPLIT 0   // k_level_lds_f, one candidate window per wave: y outside the window without the dead-candidate selects
+#define PCG_TGF_SPLIT 1   // k_level_lds_f, one candidate window per wave: y outside the window without the
+                          // dead-candidate selects (depth 4: 2.24 -> 2.09 ms once the rare-path values were opaque)
 #endif
 #ifndef PCG_MBF2
 #define PCG_MBF2 4
@@ -1949,7 +1950,15 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
         btab[e] = (unsigned)pcg_binom(a.binom, c, i);
     }
     __syncthreads();
-    if constexpr (WIDE) {   // (the row-batched form below measured slower for the 128-wide blocks)
+    if (!WIDE && a.cblk) {   // this depth's compact node block (k_node_blocks): coalesced rows
+        const double *cb = a.cblk + a.bo[x];
+        const int L = D + 1;
+        const int lane = tid & 63, wv = tid >> 6;
+        for (int t = wv; t < D; t += bs >> 6) {
+            if (lane < DS) M[t * DS + lane] = lane < D ? (float)cb[t * L + lane] : 0.0f;
+            if (lane == 0) lmask[t] = (Mask)a.lmk[a.off[x] + t];
+        }
+    } else if constexpr (WIDE) {   // (the row-batched form below measured slower for the 128-wide blocks)
         for (int e = tid; e < D * DS; e += bs) {
             const int t = e / DS, k = e - t * DS;
             M[e] = k < D ? (float)a.C[(int64_t)nxs[t] * a.ldc + nxs[k]] : 0.0f;
@@ -2225,11 +2234,15 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
             for (int h = 0; h < 2; ++h) {
                 const bool ok = vldc[2 * q + h] && (te[h] <= 0.5f) && (cmE[h] > 0.0f) && (g[h] > 0.0f) && (ga[h] > al[h]);
                 okc[2 * q + h] = ok;
-                mp[q][h] = ok ? mm[h] : 0.0f;                          // unusable: never "dependent"
-                hhp[q][h] = ok ? hw[h] : -1.0f;
+                // an unusable candidate always passes the sweep's compare (|c_xy^2| < 3e38): its
+                // lanes take the rare path through `notok`, whose per-candidate check reads okc
+                mp[q][h] = ok ? mm[h] : 0.0f;
+                hhp[q][h] = ok ? hw[h] : 0.0f;
                 k1p[q][h] = ok ? kk1[h] : 0.0f;
-                k2p[q][h] = ok ? kk2[h] : 1.0f;
+                k2p[q][h] = ok ? kk2[h] : -3.0e38f;
             }
+            // opaque: the rare path must read these registers, not keep (spill) the unselected values
+            asm volatile("" : "+v"(mp[q]), "+v"(hhp[q]), "+v"(k1p[q]), "+v"(k2p[q]));
         }
         const int cend = min(T[0], cbase + TG);
         unsigned okm = 0;
@@ -2250,7 +2263,8 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
         // certain independence in fp32 (recomputed) or the fp64 screen list
         auto rare_cand = [&](int jj, int t, const float *Mt, const float *vT, float byy, float bxy, Mask lm) {
             const int q = jj >> 1, h = jj & 1;
-            const int c = cbase + jj;
+            int c = cbase + jj;
+            asm volatile("" : "+v"(c));      // no per-candidate masks / ids hoisted into the hot loop
             if (okc[jj]) {   // the sweep's check for this candidate, recomputed
                 float s_ = Mt[c];
 #pragma unroll
@@ -2357,8 +2371,10 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
                     }
                     return;
                 } else {
+                // dall = lanes where every candidate is certainly dependent (unusable ones always
+                // pass, see the setup; YM 1 skips the candidate that is y)
                 const int jdead = YM == 1 ? t - cb0 : -1;
-                unsigned long long bad = 0ull;
+                unsigned long long dall = ~0ull;
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
                     const f2v vc = sc[q] * rlp[q];
@@ -2367,13 +2383,17 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
                     const f2v nm = __builtin_elementwise_fma(cxy, cxy, -k1p[q]);
                     const f2v w = __builtin_elementwise_fma(-mp[q], cyy, nm);
                     const f2v hh = __builtin_elementwise_fma(hhp[q], cyy, -k2p[q]);
-                    const unsigned long long keep0 = 2 * q == jdead ? 0ull : okv[2 * q];
-                    const unsigned long long keep1 = 2 * q + 1 == jdead ? 0ull : okv[2 * q + 1];
-                    bad |= keep0 & ~__builtin_amdgcn_ballot_w64(__builtin_fabsf(w[0]) < hh[0]);
-                    bad |= keep1 & ~__builtin_amdgcn_ballot_w64(__builtin_fabsf(w[1]) < hh[1]);
+                    const unsigned long long d0 = __builtin_amdgcn_ballot_w64(__builtin_fabsf(w[0]) < hh[0]);
+                    const unsigned long long d1 = __builtin_amdgcn_ballot_w64(__builtin_fabsf(w[1]) < hh[1]);
+                    if (YM == 1) {
+                        dall &= 2 * q == jdead ? ~0ull : d0;
+                        dall &= 2 * q + 1 == jdead ? ~0ull : d1;
+                    } else {
+                        dall &= d0 & d1;
+                    }
                 }
                 const unsigned long long inT = __builtin_amdgcn_ballot_w64((bool)((Tmask >> t) & 1u));
-                unsigned long long rarel = (bad | notok) & ~inT;
+                unsigned long long rarel = ((~dall & __builtin_amdgcn_read_exec()) | notok) & ~inT;
                 if (YM == 2) rarel |= __builtin_amdgcn_ballot_w64((unsigned)(t - cbase) < (unsigned)nval);
                 if (t < tx) rarel |= __builtin_amdgcn_ballot_w64((lm & Tmask) == Tmask) & ~inT;
                 if (!rarel) return;
@@ -2512,10 +2532,9 @@ __global__ __launch_bounds__(256) void k_screen(LevelArgs a) {
 // (|c^ - c| <= 18 u32 (1 + nu)^2, the same form as k_level_lds_f's), the rare path,
 // dedup and unions are k_level_lds_f's.
 #ifndef PCG_SP
-#define PCG_SP 0x10       // depths (bit 1 << d) whose narrow class runs k_level_sp: depth 4 (measured
-                          // 2.36 ms, = k_level_lds_f<4> at 6x less HBM fetch); depth 3 stays on
-                          // k_level_lds_f (0.69 vs 0.78-0.81 ms: ~6 tasks per prefix t0 do not pay for
-                          // staging up to 8 prefixes' P1 per block)
+#define PCG_SP 0          // depths (bit 1 << d) whose narrow class runs k_level_sp (A/B; off: at depth 4
+                          // it measured 2.23-2.27 ms vs k_level_lds_f<4>'s 2.09 once both lost their
+                          // spills, at depth 3 0.78-0.81 vs 0.69 ms)
 #endif
 #ifndef PCG_SP_TG
 #define PCG_SP_TG 6       // candidates per lane task
@@ -2528,6 +2547,13 @@ __global__ __launch_bounds__(256) void k_screen(LevelArgs a) {
 #endif
 #ifndef PCG_SP_MB
 #define PCG_SP_MB 4       // blocks per CU (launch bounds: 128 VGPRs)
+#endif
+#ifndef PCG_NODE_BLOCKS
+#define PCG_NODE_BLOCKS 0x10  // depths (bit 1 << d) whose fp32-screened narrow sweep stages compact node blocks
+                              // (depth 4: kernel 2.13-2.16 -> 2.08 ms, FETCH 1.8 -> 0.18 GB; depth 3 measured no gain)
+#endif
+#ifndef PCG_SP_FAKE_SETUP
+#define PCG_SP_FAKE_SETUP 0
 #endif
 #ifndef PCG_SP_XCD
 #define PCG_SP_XCD 1      // XCD-contiguous chunk order (each XCD's L2 sees few nodes at a time)
@@ -2768,13 +2794,18 @@ __global__ __launch_bounds__(256, PCG_SP_MB) void k_level_sp(LevelArgs a) {
         const f2v *Pdxb = Pdx + b * DS;
 
         // task setup in fp64 from the exact C entries (P1(r, s) = C(r, s) - w0_r w0_s)
+#if PCG_SP_FAKE_SETUP   // timing experiment only (wrong precision): C entries from the fp32 P1 buffer
+#define SPC(r_, s_) ((double)Pb[(r_) * DS + (s_)] + w0[r_] * w0[s_])
+#else
+#define SPC(r_, s_) cb[(r_) * L + (s_)]
+#endif
         const double g0 = w0[DS + 2];
         const double liF0 = w0[DS + 1];
         double r1 = 0.0, wt = 0.0, wx = 0.0, liF1 = liF0, g1 = 1.0;
         if constexpr (DM == 4) {
             const double p11 = cdg[t1] - w0[t1] * w0[t1];
             r1 = rsq_nr(p11);
-            wt = (cb[t * L + t1] - w0[t] * w0[t1]) * r1;
+            wt = (SPC(t, t1) - w0[t] * w0[t1]) * r1;
             wx = (cxr[t1] - w0[D] * w0[t1]) * r1;
             liF1 = liF0 + (liF0 * w0[t1] * w0[t1] + 1.0) * r1 * r1;
             g1 = p11;
@@ -2804,8 +2835,8 @@ __global__ __launch_bounds__(256, PCG_SP_MB) void k_level_sp(LevelArgs a) {
                     const bool valid = c < t0;
                     const int cc = valid ? c : 0;
                     double wc = 0.0;
-                    if constexpr (DM == 4) wc = (cb[cc * L + t1] - w0[cc] * w0[t1]) * r1;
-                    const double qc = (cb[cc * L + t] - w0[cc] * w0[t] - wc * wt) * rt;
+                    if constexpr (DM == 4) wc = (SPC(cc, t1) - w0[cc] * w0[t1]) * r1;
+                    const double qc = (SPC(cc, t) - w0[cc] * w0[t] - wc * wt) * rt;
                     const double lam2 = cdg[cc] - w0[cc] * w0[cc] - wc * wc - qc * qc;
                     const double r = rsq_nr(lam2);
                     const double u = (cxr[cc] - w0[D] * w0[cc] - wx * wc - qx * qc) * r;
@@ -2853,10 +2884,12 @@ __global__ __launch_bounds__(256, PCG_SP_MB) void k_level_sp(LevelArgs a) {
             for (int h = 0; h < 2; ++h) {
                 const bool ok = vldc[2 * q + h] && (te[h] <= 0.5f) && (cmE[h] > 0.0f) && (gg[h] > 0.0f) && (ga[h] > al[h]);
                 okc[2 * q + h] = ok;
+                // an unusable candidate always passes the sweep's compare (|c_xy^2| < 3e38): its
+                // lanes take the rare path through `notok`, whose per-candidate check reads okc
                 mp[q][h] = ok ? mm[h] : 0.0f;
-                hhp[q][h] = ok ? hw[h] : -1.0f;
+                hhp[q][h] = ok ? hw[h] : 0.0f;
                 k1p[q][h] = ok ? kk1[h] : 0.0f;
-                k2p[q][h] = ok ? kk2[h] : 1.0f;
+                k2p[q][h] = ok ? kk2[h] : -3.0e38f;
             }
             // opaque: the rare path must read these registers, not keep (spill) the unselected values
             asm volatile("" : "+v"(mp[q]), "+v"(hhp[q]), "+v"(k1p[q]), "+v"(k2p[q]));
@@ -2978,8 +3011,12 @@ __global__ __launch_bounds__(256, PCG_SP_MB) void k_level_sp(LevelArgs a) {
                     }
                     return;
                 } else {
+                    // YM 0: no candidate of the window is y; YM 1: candidate ty - cb0 (the same in
+                    // every lane) is y and is skipped; YM 2: windows differ, lanes whose window
+                    // holds y take the rare path. dall = lanes where every candidate is certainly
+                    // dependent (unusable ones always pass, see the setup)
                     const int jdead = YM == 1 ? ty - cb0 : -1;
-                    unsigned long long bad = 0ull;
+                    unsigned long long dall = ~0ull;
 #pragma unroll
                     for (int q = 0; q < NQ; ++q) {
                         const f2v vc = sc[q] * rlp[q];
@@ -2988,13 +3025,17 @@ __global__ __launch_bounds__(256, PCG_SP_MB) void k_level_sp(LevelArgs a) {
                         const f2v nm = __builtin_elementwise_fma(cxy, cxy, -k1p[q]);
                         const f2v w = __builtin_elementwise_fma(-mp[q], cyy, nm);
                         const f2v hh = __builtin_elementwise_fma(hhp[q], cyy, -k2p[q]);
-                        const unsigned long long keep0 = 2 * q == jdead ? 0ull : okv[2 * q];
-                        const unsigned long long keep1 = 2 * q + 1 == jdead ? 0ull : okv[2 * q + 1];
-                        bad |= keep0 & ~__builtin_amdgcn_ballot_w64(__builtin_fabsf(w[0]) < hh[0]);
-                        bad |= keep1 & ~__builtin_amdgcn_ballot_w64(__builtin_fabsf(w[1]) < hh[1]);
+                        const unsigned long long d0 = __builtin_amdgcn_ballot_w64(__builtin_fabsf(w[0]) < hh[0]);
+                        const unsigned long long d1 = __builtin_amdgcn_ballot_w64(__builtin_fabsf(w[1]) < hh[1]);
+                        if (YM == 1) {
+                            dall &= 2 * q == jdead ? ~0ull : d0;
+                            dall &= 2 * q + 1 == jdead ? ~0ull : d1;
+                        } else {
+                            dall &= d0 & d1;
+                        }
                     }
                     // lanes that need the per-lane path; y in T is masked only when some lane does
-                    unsigned long long rarel = bad | notok;
+                    unsigned long long rarel = (~dall & __builtin_amdgcn_read_exec()) | notok;
                     if (YM == 2) rarel |= __builtin_amdgcn_ballot_w64((unsigned)(ty - cbase) < (unsigned)nval);
                     if (ty < tx) rarel |= __builtin_amdgcn_ballot_w64((lmask[ty] & Tmask) == Tmask);
                     if (!rarel) return;
@@ -3011,13 +3052,17 @@ __global__ __launch_bounds__(256, PCG_SP_MB) void k_level_sp(LevelArgs a) {
                         if ((live >> jj) & 1u) rare_cand(jj, ty, Pr, wy, qy, byy, bxy, lm);
                 }
             };
+            using Y0 = std::integral_constant<int, 0>;
             using Y1 = std::integral_constant<int, 1>;
             using Y2 = std::integral_constant<int, 2>;
             using Y3 = std::integral_constant<int, 3>;
             if (!SG) {
                 for (int ty = 0; ty < D; ++ty) ystep(ty, Y3{});
-            } else if (uni) {
-                for (int ty = 0; ty < D; ++ty) ystep(ty, Y1{});
+            } else if (uni) {   // y outside the shared window [cb0, cb0 + NC) needs no dead candidate
+                const int w0_ = min(cb0, D), w1_ = min(cb0 + NC, D);
+                for (int ty = 0; ty < w0_; ++ty) ystep(ty, Y0{});
+                for (int ty = w0_; ty < w1_; ++ty) ystep(ty, Y1{});
+                for (int ty = w1_; ty < D; ++ty) ystep(ty, Y0{});
             } else {
                 for (int ty = 0; ty < D; ++ty) ystep(ty, Y2{});
             }
@@ -3600,7 +3645,7 @@ LevelArgs make_args(pcg_handle *h, int d, int mode_exact_all) {
     a.rec_mod = h->rec_mod;
     a.rec_res = h->rec_res;
     a.spl = h->spl;
-    if (h->sp) {
+    if (h->nblk) {
         const int64_t *t = (const int64_t *)h->cpre.p + h->sp_tab_off;
         a.coff = t;
         a.ctab = t + SP_DMAX + 2;
@@ -3906,6 +3951,7 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
     int64_t *cs = h->cpre_h.data(), *cw = cs + (n + 1), *cl = cw + (n + 1);
     std::vector<int64_t> bo;           // k_level_sp compact-block offsets (doubles)
     h->sp = false;
+    h->nblk = false;
     h->sp_ctab.clear();
     h->sp_coff.assign(SP_DMAX + 2, 0);
     h->work_h.assign(n, 0);
@@ -3942,6 +3988,10 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
             const char *spe = getenv("PCG_SP");
             const int spm = spe ? (int)strtol(spe, nullptr, 0) : PCG_SP;
             h->sp = tg && use_screen32(h, depth) && (depth == 3 || depth == 4) && ((spm >> depth) & 1);
+            // compact node blocks (k_node_blocks) for the narrow class of the fp32-screened sweeps
+            const char *nbe = getenv("PCG_NODE_BLOCKS");
+            const int nbm = nbe ? (int)strtol(nbe, nullptr, 0) : PCG_NODE_BLOCKS;
+            h->nblk = h->sp || (tg && use_screen32(h, depth) && ((nbm >> depth) & 1));
         }
         std::vector<uint64_t> ns_of(maxd + 1, 0), units_of(maxd + 1, 0);
         std::vector<int> cls_of(maxd + 1, 2);
@@ -4026,20 +4076,20 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
             }
         }
         int64_t ss = 0, sw = 0, sl = 0, sb = 0;
-        if (h->sp) bo.assign(n + 1, 0);
+        if (h->nblk) bo.assign(n + 1, 0);
         for (int x = 0; x < n; ++x) {
             cs[x] = ss;
             cw[x] = sw;
             cl[x] = sl;
-            if (h->sp) bo[x] = sb;
+            if (h->nblk) bo[x] = sb;
             const int D = h->deg_h[x];
             if (D < depth + 1) continue;
             h->work_h[x] = (int64_t)ns_of[D] * (D - depth);
             const int c = cls_of[D];
             (c == 0 ? ss : c == 1 ? sw : sl) += nch_of[D];
-            if (h->sp && c == 0) sb += (int64_t)(D + 1) * (D + 1);
+            if (h->nblk && c == 0) sb += (int64_t)(D + 1) * (D + 1);
         }
-        if (h->sp) bo[n] = sb;
+        if (h->nblk) bo[n] = sb;
         cs[n] = ss;
         cw[n] = sw;
         cl[n] = sl;
@@ -4053,13 +4103,13 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
     // host-mapped upload: the three class prefixes, then (k_level_sp) the per-degree chunk table
     // offsets, the chunk table and the compact-block offsets
     h->sp_tab_off = 3 * (int64_t)(n + 1);
-    const int64_t cnt = h->sp_tab_off + (h->sp ? (int64_t)(SP_DMAX + 2) + (int64_t)h->sp_ctab.size() + (n + 1) : 0);
+    const int64_t cnt = h->sp_tab_off + (h->nblk ? (int64_t)(SP_DMAX + 2) + (int64_t)h->sp_ctab.size() + (n + 1) : 0);
     if (!pcg_ensure_pinned(h, h->cpre_pin, sizeof(int64_t) * cnt))
         return pcg_fail(h, PCG_ERR_OOM, "pinned chunk prefix");
     {
         int64_t *pin = (int64_t *)h->cpre_pin.p;
         memcpy(pin, h->cpre_h.data(), sizeof(int64_t) * 3 * (n + 1));
-        if (h->sp) {
+        if (h->nblk) {
             int64_t *p = pin + h->sp_tab_off;
             memcpy(p, h->sp_coff.data(), sizeof(int64_t) * (SP_DMAX + 2));
             p += SP_DMAX + 2;
@@ -4286,6 +4336,8 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                         if (d == 3) hipLaunchKernelGGL((k_level_sp<3>), grid, block, ldsp, h->stream, as);
                         else hipLaunchKernelGGL((k_level_sp<4>), grid, block, ldsp, h->stream, as);
                     } else if (h->tgroup && use_screen32(h, d)) {
+                        if (h->nblk)   // compact node blocks: the sweep stages them instead of gathering C
+                            hipLaunchKernelGGL(k_node_blocks, dim3((unsigned)h->n), dim3(256), 0, h->stream, as, s_lo, s_hi);
                         as.lds_btab_off = (int)lds_f32_core(dl, 8);
                         const size_t ldsf = lds_tgroup_f_bytes(dl, d, 8);
                         const dim3 grid((unsigned)(s_hi - s_lo)), block(256);
