@@ -146,6 +146,9 @@ def dominant_kernel(d: int, full_p: bool) -> str:
         return f"k_level0<{1 if full_p else 0}>"
     if not full_p and 2 <= d <= 4:
         mask = int(os.environ.get("PCG_SCREEN_MASK", "0x18"), 0)
+        sp = int(os.environ.get("PCG_SP", "0"), 0)
+        if (mask >> d) & 1 and (sp >> d) & 1 and d in (3, 4):
+            return f"k_level_sp<{d}>"
         return f"k_level_lds_{'f' if (mask >> d) & 1 else 't'}<{d}, false>"
     return f"k_level_lds<{d}, {1 if full_p else 0}>"
 

@@ -91,10 +91,12 @@ extern "C" int pcg_destroy(pcg_handle *h) {
     DevBuf *bufs[] = {&h->adj, &h->deg, &h->off2[0], &h->off2[1], &h->nbr2[0], &h->nbr2[1], &h->rm, &h->ug2[0],
                       &h->ug2[1], &h->exp_ctr, &h->cpre, &h->binom, &h->ctr,
                       &h->deferred, &h->screenq, &h->records, &h->nearbuf, &h->exportbuf, &h->export_xy, &h->diag,
-                      &h->colmean, &h->pr_scratch, &h->batch_scratch, &h->chisq_scratch};
+                      &h->colmean, &h->pr_scratch, &h->batch_scratch, &h->chisq_scratch, &h->cblk, &h->lmk,
+                      &h->k1_digits};
     for (DevBuf *b : bufs)
         if (b->p) hipFree(b->p);
-    PinBuf *pins[] = {&h->ctr_pin, &h->deg_pin, &h->off_pin, &h->cpre_pin, &h->status_pin};
+    PinBuf *pins[] = {&h->ctr_pin, &h->deg_pin, &h->off_pin, &h->cpre_pin, &h->status_pin, &h->tab_pin[0],
+                      &h->tab_pin[1]};
     for (PinBuf *b : pins)
         if (b->p) hipHostFree(b->p);
     if (h->summary) hipHostFree(h->summary);
@@ -102,6 +104,9 @@ extern "C" int pcg_destroy(pcg_handle *h) {
         if (e) hipEventDestroy(e);
     for (auto &e : h->lev)
         if (e) hipEventDestroy(e);
+    for (auto &pr : h->rev)
+        for (auto &e : pr)
+            if (e) hipEventDestroy(e);
     if (h->ev_fork) hipEventDestroy(h->ev_fork);
     if (h->ev_join) hipEventDestroy(h->ev_join);
     if (h->aux) hipStreamDestroy(h->aux);

@@ -117,6 +117,18 @@ struct pcg_handle {
     DevBuf cblk, lmk;                // k_level_sp: per-node compact correlation blocks, local masks
     std::vector<int64_t> sp_ctab, sp_coff;   // k_level_sp chunk tables per degree (host copies)
     int64_t sp_tab_off = 0;          // int64 offset of [coff, ctab, bo] in cpre / cpre_pin
+    // pipelined level loop (skeleton_once, single GPU, threshold mode): depth d >= 2 is decomposed
+    // on upper-bound degrees (those at the start of d - 1) and enqueued before depth d - 1's
+    // summary is read; k_decompose computes the exact prefixes on the device
+    bool bound = false;              // the current depth was prepared in bound mode
+    int64_t dtab_off = 0;            // int64 offset of the per-degree class tables in cpre (bound mode)
+    int64_t bo_off = 0;              // int64 offset of the compact-block offsets in cpre
+    int dtab_maxd = 0;               // their largest degree
+    PinBuf tab_pin[2];               // bound-mode uploads, alternating by depth parity
+    hipEvent_t rev[PCG_MAX_LEVELS][2] = {};   // per-depth CI-test kernel brackets
+    int64_t near_seen = 0;           // near-alpha entries copied so far (the device list accumulates)
+    int64_t near_total_dev = 0;      // the device's cumulative near-alpha count at the last level end
+    size_t summary_slot = 0;         // bytes per slot of the two-slot host-mapped summary ring
     int screen_eff = 0;              // the current depth's effective mask (set by pcg_level_begin)
     int screen_mask = -1;            // depths (bit 1 << d) with the fp32-screened T-group sweep (k_level_lds_f); -1 = default
     int32_t maxdeg = 0;

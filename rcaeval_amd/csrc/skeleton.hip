@@ -376,7 +376,7 @@ __global__ __launch_bounds__(256) void k_export(const int32_t *off, const int32_
     const int64_t slot = wave_base + lane;
     int x = -1, y = -1;
     bool removed = false;
-    if (slot < sumdeg) {
+    if (slot < sumdeg && slot < off[n]) {   // (sumdeg may be an upper bound: pipelined level loop)
         int lo = 0, hi = n;  // off[lo] <= slot < off[hi]
         while (hi - lo > 1) {
             const int mid = (lo + hi) >> 1;
@@ -498,7 +498,9 @@ __global__ __launch_bounds__(256) void k_summary_fill(const int32_t *deg, int n,
     if (tid == 255) off[n] = part[255];
     if (tid == 0) {
         out->ctr = *ctr;
-        *ctr = DevCounters{};
+        DevCounters z{};
+        z.near_alpha = ctr->near_alpha;   // the near-alpha list accumulates over the run
+        *ctr = z;
         for (int k = 0; k < 8; ++k) out->status[k] = status ? status[k] : 0;
         if (status)
             for (int k = 0; k < PCG_RM_STATUS; ++k) status[k] = 0;
@@ -511,6 +513,67 @@ __global__ __launch_bounds__(256) void k_summary_fill(const int32_t *deg, int n,
     }
 }
 
+// The exact per-class chunk prefixes of the current graph from per-degree tables the host built
+// on upper-bound degrees (pipelined level loop, pcg_level_begin in bound mode): tab[c * (maxd + 1)
+// + D] = chunks of a degree-D node in class c (0 narrow, 1 wide, 2 large; 0 when D is not in c).
+// One block: each thread scans a contiguous node range; cpre gets 3 x (n + 1) prefixes, bo the
+// compact-block offsets of the narrow class (nblk). The reference loop condition (max degree - 1
+// > depth - 1) is evaluated here: when it fails every class total is 0 and the level's launches
+// exit at once.
+__global__ __launch_bounds__(256) void k_decompose(const int32_t *deg, int n, const int64_t *tab, int maxd, int depth,
+                                                   int nblk, int64_t *cpre, int64_t *bo) {
+    __shared__ int64_t part[4][256];
+    __shared__ int mx[256];
+    const int tid = threadIdx.x;
+    const int per = (n + 255) / 256;
+    const int lo = min(n, tid * per), hi = min(n, lo + per);
+    int64_t sum[4] = {0, 0, 0, 0};
+    int m = 0;
+    for (int i = lo; i < hi; ++i) {
+        const int D = min(deg[i], maxd);
+        m = max(m, deg[i]);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) sum[c] += tab[c * (maxd + 1) + D];
+        if (nblk && tab[D] > 0) sum[3] += (int64_t)(D + 1) * (D + 1);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) part[c][tid] = sum[c];
+    mx[tid] = m;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {        // inclusive scans of the four sums, max of the degrees
+        int64_t v[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] = tid >= o ? part[c][tid - o] : 0;
+        const int vm = tid >= o ? mx[tid - o] : 0;
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < 4; ++c) part[c][tid] += v[c];
+        mx[tid] = max(mx[tid], vm);
+        __syncthreads();
+    }
+    const bool run = mx[255] - 1 > depth - 1;
+    int64_t acc[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] = (run && tid) ? part[c][tid - 1] : 0;
+    for (int i = lo; i < hi; ++i) {
+        const int D = min(deg[i], maxd);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            cpre[c * (int64_t)(n + 1) + i] = acc[c];
+            if (run) acc[c] += tab[c * (maxd + 1) + D];
+        }
+        if (nblk) {
+            bo[i] = acc[3];
+            if (run && tab[D] > 0) acc[3] += (int64_t)(D + 1) * (D + 1);
+        }
+    }
+    if (tid == 255) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) cpre[c * (int64_t)(n + 1) + n] = run ? part[c][255] : 0;
+        if (nblk) bo[n] = run ? part[3][255] : 0;
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // depth 0: one chunk = one 64 x 64 tile (bi <= bj) of the pair triangle; node bi*64 owns the
 // chunks of tile row bi. Decisions are staged in LDS so both rm[x][y] and its mirror
@@ -520,6 +583,7 @@ template <int MODE>
 __global__ __launch_bounds__(256) void k_level0(LevelArgs a) {
     __shared__ uint8_t flag[64][68];
     const int64_t chunk = a.chunk_lo + blockIdx.x;
+    if (chunk >= a.cpre[a.n]) return;   // a launch sized by an upper bound (pipelined level loop)
     int lo = 0, hi = a.n;
     while (hi - lo > 1) {
         const int mid = (lo + hi) >> 1;
@@ -576,6 +640,7 @@ __global__ __launch_bounds__(256) void k_level(LevelArgs a) {
     const int wave = tid >> 6;
     const int bs = blockDim.x;
     const int64_t chunk = a.chunk_lo + blockIdx.x;
+    if (chunk >= a.cpre[a.n]) return;   // a launch sized by an upper bound (pipelined level loop)
 
     // node owning this chunk
     int lo = 0, hi = a.n;
@@ -813,6 +878,7 @@ __global__ __launch_bounds__(256) void k_level1_pairs(LevelArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x;
     const int64_t chunk = a.chunk_lo + blockIdx.x;
+    if (chunk >= a.cpre[a.n]) return;   // a launch sized by an upper bound (pipelined level loop)
     int lo = 0, hi = a.n;
     while (hi - lo > 1) {
         const int mid = (lo + hi) >> 1;
@@ -937,6 +1003,7 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
     const int tid = threadIdx.x;
     const int bs = blockDim.x;
     const int64_t chunk = a.chunk_lo + blockIdx.x;
+    if (chunk >= a.cpre[a.n]) return;   // a launch sized by an upper bound (pipelined level loop)
     int lo = 0, hi = a.n;
     while (hi - lo > 1) {
         const int mid = (lo + hi) >> 1;
@@ -1292,6 +1359,7 @@ __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_
     const int tid = threadIdx.x;
     const int bs = blockDim.x;
     const int64_t chunk = a.chunk_lo + blockIdx.x;
+    if (chunk >= a.cpre[a.n]) return;   // a launch sized by an upper bound (pipelined level loop)
     int lo = 0, hi = a.n;
     while (hi - lo > 1) {
         const int mid = (lo + hi) >> 1;
@@ -1922,6 +1990,7 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
     const int tid = threadIdx.x;
     const int bs = blockDim.x;
     const int64_t chunk = a.chunk_lo + blockIdx.x;
+    if (chunk >= a.cpre[a.n]) return;   // a launch sized by an upper bound (pipelined level loop)
     int lo = 0, hi = a.n;
     while (hi - lo > 1) {
         const int mid = (lo + hi) >> 1;
@@ -2640,6 +2709,7 @@ __global__ __launch_bounds__(256, PCG_SP_MB) void k_level_sp(LevelArgs a) {
         bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + i;
     }
     const int64_t chunk = a.chunk_lo + bid;
+    if (chunk >= a.cpre[a.n]) return;   // a launch sized by an upper bound (pipelined level loop)
     int lo = 0, hi = a.n;
     while (hi - lo > 1) {
         const int mid = (lo + hi) >> 1;
@@ -3125,6 +3195,7 @@ __global__ __launch_bounds__(64) void k_level_deep(LevelArgs a, double *scratch,
     unsigned long long tests = 0, nindep = 0;
     for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
         const int64_t chunk = a.chunk_lo + c;
+        if (chunk >= a.cpre[a.n]) break;    // (a bound-sized chunk range, pipelined level loop)
         int lo = 0, hi = a.n;
         while (hi - lo > 1) {
             const int mid = (lo + hi) >> 1;
@@ -3259,6 +3330,7 @@ __global__ __launch_bounds__(256) void k_level_wave(LevelArgs a) {
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6;
     const int64_t chunk = a.chunk_lo + blockIdx.x;
+    if (chunk >= a.cpre[a.n]) return;   // a launch sized by an upper bound (pipelined level loop)
     int lo = 0, hi = a.n;
     while (hi - lo > 1) {
         const int mid = (lo + hi) >> 1;
@@ -3649,7 +3721,7 @@ LevelArgs make_args(pcg_handle *h, int d, int mode_exact_all) {
         const int64_t *t = (const int64_t *)h->cpre.p + h->sp_tab_off;
         a.coff = t;
         a.ctab = t + SP_DMAX + 2;
-        a.bo = a.ctab + h->sp_ctab.size();
+        a.bo = (const int64_t *)h->cpre.p + h->bo_off;
         a.cblk = (double *)h->cblk.p;
         a.lmk = (uint64_t *)h->lmk.p;
     }
@@ -3752,28 +3824,36 @@ int mode_of(const pcg_handle *h, int d) {
     return MODE_DECIDE;
 }
 
+// the summary slot of sequence number seq (a ring of two: the pipelined loop reads depth d - 1's
+// summary while depth d's may already be written)
+LevelSummary *sum_slot(const pcg_handle *h, unsigned long long seq) {
+    return reinterpret_cast<LevelSummary *>(reinterpret_cast<char *>(h->summary) + (seq & 1) * h->summary_slot);
+}
+
 // the level summary (degrees, counters, status) of the current adjacency -> host-mapped memory;
 // level_wait() spins until the device has written it
 int graph_launch(pcg_handle *h) {
     const int n = (int)h->n, W = h->W;
-    const size_t bytes = sizeof(LevelSummary) + sizeof(int32_t) * (size_t)n;
-    if (!h->summary || h->summary_bytes < bytes) {
+    const size_t slot = (sizeof(LevelSummary) + sizeof(int32_t) * (size_t)n + 255) & ~(size_t)255;
+    if (!h->summary || h->summary_bytes < 2 * slot) {
         if (h->summary) { (void)hipStreamSynchronize(h->stream); (void)hipHostFree(h->summary); }
         h->summary = nullptr;
         h->summary_bytes = 0;
         void *p = nullptr;
-        if (hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+        if (hipHostMalloc(&p, 2 * slot, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
             return pcg_fail(h, PCG_ERR_OOM, "host-mapped level summary");
         h->summary = (LevelSummary *)p;
-        h->summary_bytes = bytes;
-        h->summary->seq = 0;
+        h->summary_bytes = 2 * slot;
+        h->summary_slot = slot;
+        sum_slot(h, 0)->seq = 0;
+        sum_slot(h, 1)->seq = 0;
         h->summary_seq = 0;
     }
+    const unsigned long long seq = ++h->summary_seq;
     void *dsum = nullptr;
-    PCG_HIP(h, hipHostGetDevicePointer(&dsum, h->summary, 0));
+    PCG_HIP(h, hipHostGetDevicePointer(&dsum, sum_slot(h, seq), 0));
     LevelSummary *ds = (LevelSummary *)dsum;
     uint8_t *status = h->depth >= 0 ? (h->rm_ext ? h->rm_ext : (uint8_t *)h->rm.p) + (int64_t)n * n : nullptr;
-    const unsigned long long seq = ++h->summary_seq;
     // the next depth's CSR is built from the device degrees while the host waits for the
     // summary; nbr is sized by the current graph (degrees only fall), and the union rows are
     // cleared along with it when the buffer already covers that bound
@@ -3816,16 +3896,16 @@ __global__ void k_copy_i64(const int64_t *src, int64_t count, int64_t *dst) {
     if (i < count) dst[i] = src[i];
 }
 
-// spin until the summary of the last graph_launch is visible (a stream error or a stream that
+// spin until the summary with sequence number `want` is visible (a stream error or a stream that
 // finished without it ends the wait with an error instead of hanging)
-int level_wait(pcg_handle *h) {
-    const unsigned long long want = h->summary_seq;
+int level_wait(pcg_handle *h, unsigned long long want) {
+    const LevelSummary *sm = sum_slot(h, want);
     unsigned spins = 0;
-    while (__atomic_load_n(&h->summary->seq, __ATOMIC_ACQUIRE) != want) {
+    while (__atomic_load_n(&sm->seq, __ATOMIC_ACQUIRE) != want) {
         if ((++spins & 1023) == 0) {
             const hipError_t e = hipStreamQuery(h->stream);
             if (e == hipSuccess) {
-                if (__atomic_load_n(&h->summary->seq, __ATOMIC_ACQUIRE) == want) break;
+                if (__atomic_load_n(&sm->seq, __ATOMIC_ACQUIRE) == want) break;
                 return pcg_fail(h, PCG_ERR_HIP, "level summary not written (seq %llu)", want);
             }
             if (e != hipErrorNotReady) return pcg_fail(h, PCG_ERR_HIP, "stream error: %s", hipGetErrorString(e));
@@ -3835,10 +3915,10 @@ int level_wait(pcg_handle *h) {
     return PCG_OK;
 }
 
-// after the wait: host degrees and their sum / maximum
-void graph_finish(pcg_handle *h) {
+// after the wait: host degrees (summary `seq`) and their sum / maximum
+void graph_finish(pcg_handle *h, unsigned long long seq) {
     const int n = (int)h->n;
-    const int32_t *dp = reinterpret_cast<const int32_t *>(h->summary + 1);
+    const int32_t *dp = reinterpret_cast<const int32_t *>(sum_slot(h, seq) + 1);
     h->deg_h.assign(dp, dp + n);
     int64_t s = 0;
     int32_t mx = 0;
@@ -3881,6 +3961,7 @@ extern "C" int pcg_skeleton_init(pcg_handle *h, const double *C, int64_t n, int6
     h->export_rows = 0;
     h->rec_h.clear(); h->near_h.clear();
     h->rec_total = h->near_total = 0;
+    h->near_seen = h->near_total_dev = 0;
     memset(&h->st, 0, sizeof(h->st));
     const int W = h->W;
     if (!pcg_ensure(h, h->adj, sizeof(uint64_t) * n * W) || !pcg_ensure(h, h->deg, sizeof(int32_t) * n) ||
@@ -3903,6 +3984,8 @@ extern "C" int pcg_skeleton_init(pcg_handle *h, const double *C, int64_t n, int6
                        h->rm_ext ? h->rm_ext : (uint8_t *)h->rm.p, (int64_t)n * n + PCG_RM_STATUS,
                        (unsigned long long *)h->exp_ctr.p);
     PCG_HIP(h, hipGetLastError());
+    // the level counters start at zero (k_summary_fill keeps the run's near-alpha count)
+    PCG_HIP(h, hipMemsetAsync(h->ctr.p, 0, sizeof(DevCounters), h->stream));
     int rc = graph_launch(h);            // also clears the counters
     if (rc) return rc;
     // the complete graph's degrees are known (k_init writes n - 1 everywhere): depth 0 is
@@ -3913,27 +3996,13 @@ extern "C" int pcg_skeleton_init(pcg_handle *h, const double *C, int64_t n, int6
     return PCG_OK;
 }
 
-extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, int32_t *max_degree,
-                               uint8_t **rm_dev) {
-    if (!h || depth != h->depth + 1) return pcg_fail(h, PCG_ERR_INVALID, "pcg_level_begin: depth order");
-    if (max_degree) *max_degree = h->maxdeg;
-    if (rm_dev) *rm_dev = h->rm_ext ? h->rm_ext : (uint8_t *)h->rm.p;
-    // reference loop condition: while max_degree() - 1 > depth_prev
-    if (!(h->maxdeg - 1 > depth - 1)) {
-        if (total_chunks) *total_chunks = 0;
-        return 1;  // done
-    }
-    if (depth >= PCG_MAX_LEVELS || depth > PCG_MAX_LEVEL_DEPTH)
-        return pcg_fail(h, PCG_ERR_INVALID, "conditioning depth %d exceeds PCG_MAX_LEVEL_DEPTH=%d", depth,
-                        PCG_MAX_LEVEL_DEPTH);
-    h->depth = depth;
-    const int n = (int)h->n;
+// the level's start-of-depth statistics from the exact degrees in h->deg_h (max degree, the
+// reference's ci_test call count, the degree snapshot, the level count)
+void level_start_stats(pcg_handle *h, int depth) {
+    const int n = (int)h->n, maxd = h->maxdeg;
     h->deg_levels.insert(h->deg_levels.end(), h->deg_h.begin(), h->deg_h.end());
     h->st.max_degree[depth] = h->maxdeg;
     h->st.levels = depth + 1;
-    // per-degree tables: the decomposition below is O(n) lookups (it sits between two
-    // device phases of the level loop, so it is on the critical path)
-    const int maxd = h->maxdeg;
     std::vector<int64_t> hist(maxd + 1, 0);
     for (int x = 0; x < n; ++x) ++hist[h->deg_h[x]];
     // calls-equivalent: sum_x D_x * C(D_x - 1, d) (ci_test invocations incl. cache hits)
@@ -3944,6 +4013,71 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
         calls += (int64_t)std::min<uint64_t>(c, (uint64_t)INT64_MAX / 4096) * D * hist[D];
     }
     h->st.calls[depth] = calls;
+}
+
+int level_begin_buffers(pcg_handle *h, int depth);
+
+// bound mode: the per-degree tables (and k_level_sp's chunk tables) go up through the depth
+// parity's pinned buffer; k_decompose then writes the exact class prefixes and compact-block
+// offsets of the device degrees into h->cpre: [3 x (n + 1) prefixes][coff][ctab][tab][bo]
+int level_begin_bound_upload(pcg_handle *h, int depth, int64_t blk_cap) {
+    const int n = (int)h->n, maxd = h->dtab_maxd;
+    const int64_t ntab = 3 * (int64_t)(maxd + 1);
+    const int64_t up = (int64_t)(SP_DMAX + 2) + (int64_t)h->sp_ctab.size() + ntab;
+    h->dtab_off = h->sp_tab_off + (int64_t)(SP_DMAX + 2) + (int64_t)h->sp_ctab.size();
+    h->bo_off = h->dtab_off + ntab;
+    const int64_t cnt = h->bo_off + (n + 1);
+    PinBuf &pb = h->tab_pin[depth & 1];
+    if (!pcg_ensure_pinned(h, pb, sizeof(int64_t) * up)) return pcg_fail(h, PCG_ERR_OOM, "pinned level tables");
+    int64_t *p = (int64_t *)pb.p;
+    memcpy(p, h->sp_coff.data(), sizeof(int64_t) * (SP_DMAX + 2));
+    p += SP_DMAX + 2;
+    if (!h->sp_ctab.empty()) memcpy(p, h->sp_ctab.data(), sizeof(int64_t) * h->sp_ctab.size());
+    p += h->sp_ctab.size();
+    memcpy(p, h->cpre_h.data(), sizeof(int64_t) * ntab);
+    if (!pcg_ensure(h, h->cpre, sizeof(int64_t) * cnt)) return PCG_ERR_OOM;
+    if (h->nblk && (!pcg_ensure(h, h->cblk, sizeof(double) * std::max<int64_t>(blk_cap, 1)) ||
+                    !pcg_ensure(h, h->lmk, sizeof(uint64_t) * std::max<int64_t>(h->sumdeg, 1))))
+        return pcg_fail(h, PCG_ERR_OOM, "compact node blocks");
+    void *src = nullptr;
+    PCG_HIP(h, hipHostGetDevicePointer(&src, pb.p, 0));
+    int64_t *dev = (int64_t *)h->cpre.p;
+    hipLaunchKernelGGL(k_copy_i64, dim3((unsigned)((up + 255) / 256)), dim3(256), 0, h->stream, (const int64_t *)src, up,
+                       dev + h->sp_tab_off);
+    hipLaunchKernelGGL(k_decompose, dim3(1), dim3(256), 0, h->stream, (const int32_t *)h->deg.p, n,
+                       (const int64_t *)(dev + h->dtab_off), maxd, depth, h->nblk ? 1 : 0, dev, dev + h->bo_off);
+    PCG_HIP(h, hipGetLastError());
+    PCG_HT(h, "begin:decompose-launched");
+    return level_begin_buffers(h, depth);
+}
+
+// bound: h->deg_h holds upper bounds of the degrees (those at the start of depth - 1; the
+// pipelined loop in skeleton_once). The class tables then cover every degree up to the bound, the
+// launch sizes are upper bounds, and k_decompose writes the exact prefixes on the device.
+int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks, bool bound) {
+    if (!h || depth != h->depth + 1) return pcg_fail(h, PCG_ERR_INVALID, "pcg_level_begin: depth order");
+    // reference loop condition: while max_degree() - 1 > depth_prev
+    if (!(h->maxdeg - 1 > depth - 1)) {
+        if (total_chunks) *total_chunks = 0;
+        return 1;  // done
+    }
+    if (depth >= PCG_MAX_LEVELS || depth > PCG_MAX_LEVEL_DEPTH)
+        return pcg_fail(h, PCG_ERR_INVALID, "conditioning depth %d exceeds PCG_MAX_LEVEL_DEPTH=%d", depth,
+                        PCG_MAX_LEVEL_DEPTH);
+    if (bound && depth < 1) return pcg_fail(h, PCG_ERR_INVALID, "bound-mode decomposition at depth 0");
+    h->depth = depth;
+    h->bound = bound;
+    const int n = (int)h->n;
+    if (!bound) level_start_stats(h, depth);
+    // per-degree tables: the decomposition below is O(n) lookups (it sits between two
+    // device phases of the level loop, so it is on the critical path)
+    const int maxd = h->maxdeg;
+    std::vector<int64_t> hist(maxd + 1, 0);
+    for (int x = 0; x < n; ++x) ++hist[h->deg_h[x]];
+    // bound mode: every degree up to the bound may occur
+    std::vector<int64_t> hist_t(hist);
+    if (bound)
+        for (int D = 0; D <= maxd; ++D) hist_t[D] = std::max<int64_t>(hist_t[D], 1);
     // work decomposition: depth 0 = one chunk per row; depth >= 1 = three node classes:
     // narrow (D <= 64: LDS-resident kernels), wide (64 < D <= 128 at the T-group depths: the
     // T-group kernel with 128-bit masks), large (the rest: staged generic kernels)
@@ -4009,13 +4143,13 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
                 for (int t0 = 1; t0 <= D - depth + 1; ++t0) u += (uint64_t)sp_tasks(D, depth, t0);
                 units_of[D] = u;
             }
+            if (hist_t[D] && cls_of[D] == 0) h->maxdeg_small = D;   // (bound mode: any degree up to the bound)
+            if (hist_t[D] && cls_of[D] == 1) h->maxdeg_wide = D;
             if (!hist[D]) continue;
             if (cls_of[D] == 0) {
                 sum_small += (double)units_of[D] * hist[D];
-                h->maxdeg_small = D;
             } else if (cls_of[D] == 1) {
                 sum_wide += (double)units_of[D] * hist[D];
-                h->maxdeg_wide = D;
             } else {
                 sum_large += (double)ns * hist[D];
                 cnt_large += (int)hist[D];
@@ -4047,7 +4181,7 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
             nch_of[D] = c == 0 ? (int64_t)((units_of[D] + csz - 1) / csz)
                                : c == 1 ? (int64_t)((units_of[D] + cszw - 1) / cszw)
                                         : l1p ? l1_pair_chunks(D) : (int64_t)((ns_of[D] + h->chunk - 1) / h->chunk);
-            if (h->sp && c == 0 && hist[D]) {
+            if (h->sp && c == 0 && hist_t[D]) {
                 // k_level_sp chunks of a degree-D node: runs of <= csz consecutive lane tasks
                 // (prefix t0 major) spanning at most sp_pb(D) prefixes
                 h->sp_coff[D] = (int64_t)h->sp_ctab.size();
@@ -4075,6 +4209,30 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
                 nch_of[D] = (int64_t)h->sp_ctab.size() - h->sp_coff[D];
             }
         }
+        if (bound) {
+            // launch sizes: a node whose degree is at most its bound D_b may fall into any class,
+            // with at most the largest chunk count of that class over degrees <= D_b
+            std::vector<int64_t> pm(3 * (size_t)(maxd + 1), 0);
+            for (int D = 0; D <= maxd; ++D)
+                for (int c = 0; c < 3; ++c)
+                    pm[c * (maxd + 1) + D] = std::max(D ? pm[c * (maxd + 1) + D - 1] : 0,
+                                                      (D >= depth + 1 && cls_of[D] == c) ? nch_of[D] : (int64_t)0);
+            int64_t tot[3] = {0, 0, 0}, sb = 0;
+            for (int x = 0; x < n; ++x) {
+                const int Db = h->deg_h[x];
+                for (int c = 0; c < 3; ++c) tot[c] += pm[c * (maxd + 1) + Db];
+                int Dn = std::min(Db, std::min(SMALL_DEG, h->narrow_deg));   // largest narrow block
+                sb += (int64_t)(Dn + 1) * (Dn + 1);
+            }
+            h->total_small = tot[0];
+            h->total_wide = tot[1];
+            h->total_large = tot[2];
+            // the per-degree class tables k_decompose reads: tab[c][D] = chunks of a degree-D node in class c
+            h->dtab_maxd = maxd;
+            h->cpre_h.assign(3 * (size_t)(maxd + 1), 0);
+            for (int D = depth + 1; D <= maxd; ++D) h->cpre_h[cls_of[D] * (maxd + 1) + D] = nch_of[D];
+            bo.assign(1, sb);                 // compact-block capacity (an upper bound)
+        } else {
         int64_t ss = 0, sw = 0, sl = 0, sb = 0;
         if (h->nblk) bo.assign(n + 1, 0);
         for (int x = 0; x < n; ++x) {
@@ -4096,14 +4254,17 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
         h->total_small = ss;
         h->total_wide = sw;
         h->total_large = sl;
+        }
     }
     h->total_chunks = h->total_small + h->total_wide + h->total_large;
     if (total_chunks) *total_chunks = h->total_chunks;
     PCG_HT(h, "begin:decomposed");
+    h->sp_tab_off = 3 * (int64_t)(n + 1);
+    if (bound) return level_begin_bound_upload(h, depth, bo.empty() ? 0 : bo[0]);
     // host-mapped upload: the three class prefixes, then (k_level_sp) the per-degree chunk table
     // offsets, the chunk table and the compact-block offsets
-    h->sp_tab_off = 3 * (int64_t)(n + 1);
     const int64_t cnt = h->sp_tab_off + (h->nblk ? (int64_t)(SP_DMAX + 2) + (int64_t)h->sp_ctab.size() + (n + 1) : 0);
+    h->bo_off = h->sp_tab_off + (int64_t)(SP_DMAX + 2) + (int64_t)h->sp_ctab.size();
     if (!pcg_ensure_pinned(h, h->cpre_pin, sizeof(int64_t) * cnt))
         return pcg_fail(h, PCG_ERR_OOM, "pinned chunk prefix");
     {
@@ -4132,6 +4293,12 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
         PCG_HIP(h, hipGetLastError());
     }
     PCG_HT(h, "begin:prefix-copy-launched");
+    return level_begin_buffers(h, depth);
+}
+
+// the depth's union rows (cleared unless k_summary_fill already did) and, once per run, the
+// sepset export buffer; sized by h->sumdeg (exact, or the bound in bound mode)
+int level_begin_buffers(pcg_handle *h, int depth) {
     if (depth >= 1) {
         const size_t ugb = sizeof(uint64_t) * (size_t)std::max<int64_t>(h->sumdeg, 1) * h->W;
         DevBuf &ugb_ = h->ug2[h->cb];
@@ -4150,6 +4317,13 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
         }
     }
     return PCG_OK;
+}
+
+extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, int32_t *max_degree,
+                               uint8_t **rm_dev) {
+    if (h && max_degree) *max_degree = h->maxdeg;
+    if (h && rm_dev) *rm_dev = h->rm_ext ? h->rm_ext : (uint8_t *)h->rm.p;
+    return level_begin_impl(h, depth, total_chunks, false);
 }
 
 extern "C" int pcg_set_forbidden_pairs(pcg_handle *h, const uint8_t *banned_dev) {
@@ -4274,7 +4448,10 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
         LevelArgs a = make_args(h, d, mode == MODE_EXACT);
         a.chunk_lo = chunk_lo;
         const int64_t nch = chunk_hi - chunk_lo;
-        PCG_HIP(h, hipEventRecord(h->ev[2], h->stream));
+        hipEvent_t *rv = h->rev[d];
+        for (int k = 0; k < 2; ++k)
+            if (!rv[k]) PCG_HIP(h, hipEventCreate(&rv[k]));
+        PCG_HIP(h, hipEventRecord(rv[0], h->stream));
         if (nch > 0) {
             if (d == 0) {
                 const dim3 grid((unsigned)nch), block(256);
@@ -4418,7 +4595,7 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
             }
         }
         PCG_HIP(h, hipGetLastError());
-        PCG_HIP(h, hipEventRecord(h->ev[3], h->stream));
+        PCG_HIP(h, hipEventRecord(rv[1], h->stream));
         h->run_timed = true;
         PCG_HT(h, "run:launched");
         // exact path over the deferred list; the kernel reads the list length on the device
@@ -4439,7 +4616,10 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
     }
 }
 
-extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
+// the level barrier of the current depth, enqueued: removals applied, the next graph's summary and
+// CSR (k_summary_fill), the depth's sepset export on the export stream. Returns the summary's
+// sequence number in *seq (level_end_finish waits for it).
+int level_end_enqueue(pcg_handle *h, unsigned long long *seq) {
     if (!h || h->depth < 0) return pcg_fail(h, PCG_ERR_INVALID, "pcg_level_end without begin");
     const int d = h->depth, n = (int)h->n, W = h->W;
     uint8_t *rmb = h->rm_ext ? h->rm_ext : (uint8_t *)h->rm.p;
@@ -4471,19 +4651,29 @@ extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
         h->xany = true;
     }
     PCG_HT(h, "end:summary-launched");
-    if (!rc) rc = level_wait(h);
+    if (seq) *seq = h->summary_seq;
+    return rc;
+}
+
+// wait for depth d's barrier summary (sequence number seq) and take the level's counters, status
+// and the degrees of the graph that follows it (into h->deg_h / sumdeg / maxdeg)
+int level_end_finish(pcg_handle *h, int d, unsigned long long seq, pcg_stats *stats) {
+    int rc = level_wait(h, seq);
     if (rc) return rc;
     PCG_HT(h, "end:summary-seen");
-    const DevCounters c = h->summary->ctr;
+    const LevelSummary *sm = sum_slot(h, seq);
+    const DevCounters c = sm->ctr;
     uint8_t status[8];
-    for (int k = 0; k < 8; ++k) status[k] = h->summary->status[k];
-    if (h->run_timed) {
-        hipError_t e = hipEventElapsedTime(&h->run_ms, h->ev[2], h->ev[3]);
+    for (int k = 0; k < 8; ++k) status[k] = sm->status[k];
+    if (h->rev[d][1]) {
+        float ms = 0.f;
+        hipError_t e = hipEventElapsedTime(&ms, h->rev[d][0], h->rev[d][1]);
         if (e == hipErrorNotReady) {        // the summary can land before the runtime marks the event
-            PCG_HIP(h, hipEventSynchronize(h->ev[3]));
-            e = hipEventElapsedTime(&h->run_ms, h->ev[2], h->ev[3]);
+            PCG_HIP(h, hipEventSynchronize(h->rev[d][1]));
+            e = hipEventElapsedTime(&ms, h->rev[d][0], h->rev[d][1]);
         }
         PCG_HIP(h, e);
+        h->run_ms = ms;
         h->run_timed = false;
     }
     PCG_HT(h, "end:kernel-ms-read");
@@ -4494,17 +4684,23 @@ extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
         PCG_HIP(h, hipMemcpy(h->rec_h.data() + old, h->records.p, sizeof(pcg_record) * c.records,
                              hipMemcpyDeviceToHost));
     }
-    if (c.near_alpha) {
-        const int64_t k = std::min<int64_t>((int64_t)c.near_alpha, h->near_cap);
+    // the device's near-alpha list accumulates over the run: this depth's entries follow the
+    // ones already copied
+    const int64_t near_cum = std::min<int64_t>((int64_t)c.near_alpha, h->near_cap);
+    if (near_cum > h->near_seen) {
         const size_t old = h->near_h.size();
-        h->near_h.resize(old + k);
-        PCG_HIP(h, hipMemcpy(h->near_h.data() + old, h->nearbuf.p, sizeof(pcg_record) * k, hipMemcpyDeviceToHost));
+        h->near_h.resize(old + (near_cum - h->near_seen));
+        PCG_HIP(h, hipMemcpy(h->near_h.data() + old, (pcg_record *)h->nearbuf.p + h->near_seen,
+                             sizeof(pcg_record) * (near_cum - h->near_seen), hipMemcpyDeviceToHost));
     }
+    const int64_t near_d = (int64_t)c.near_alpha - h->near_total_dev;
+    h->near_total_dev = (int64_t)c.near_alpha;
+    h->near_seen = std::max(h->near_seen, near_cum);
     h->st.tests[d] = (int64_t)c.tests;
     h->st.indep[d] = (int64_t)c.indep;
     h->st.exact[d] = (int64_t)c.exact;
     h->st.screened[d] = (int64_t)c.screened;
-    h->st.near_alpha[d] = (int64_t)c.near_alpha;
+    h->st.near_alpha[d] = near_d;
     h->st.kernel_ms[d] = h->run_ms;
     if (status[3]) {   // checked first: the failed rank will not rerun, so nobody may
         if (stats) *stats = h->st;
@@ -4528,11 +4724,39 @@ extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
                         singular ? "Data correlation matrix is singular. Cannot run fisherz test. Please check your data."
                                  : "math domain error");
     }
-    graph_finish(h);
+    graph_finish(h, seq);
     h->st.edges_after[d] = h->sumdeg / 2;
     PCG_HT(h, "end:done");
     if (stats) *stats = h->st;
     return PCG_OK;
+}
+
+extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
+    unsigned long long seq = 0;
+    int rc = level_end_enqueue(h, &seq);
+    if (rc) return rc;
+    return level_end_finish(h, h->depth, seq, stats);
+}
+
+// the pipelined level loop (PCG_PIPELINE=1; single GPU, the handle's own removal flags, threshold
+// mode) from depth PCG_PIPELINE_LO on. Off by default: it removes the host round trip per depth,
+// but that was not what the device waited for. Config 5 with depths 2-4 pipelined: 5.21-5.25 vs
+// 5.09 ms per step (bound-sized decomposition: too few, too large chunks where the degrees still
+// fall fast; k_decompose 21-42 us); n = 500 full depth (19 levels) from depth 2, 3 or 5: 2.49-2.51
+// vs 2.45-2.49 ms. The idle left between depths is the stream's dispatch gaps between its small
+// dependent kernels (profiles/r03_timeline.txt), not the host.
+#ifndef PCG_PIPELINE_LO
+#define PCG_PIPELINE_LO 5
+#endif
+static bool pipeline_ok(const pcg_handle *h) {
+    if (h->world != 1 || h->rm_ext) return false;
+    if (h->flags & (PCG_FLAG_FULL_P | PCG_FLAG_RECORD | PCG_FLAG_EXACT_ALL)) return false;
+    const char *e = getenv("PCG_PIPELINE");
+    return e && atoi(e) != 0;
+}
+static int pipeline_lo() {
+    const char *e = getenv("PCG_PIPELINE_LO");
+    return std::max(2, e ? atoi(e) : PCG_PIPELINE_LO);
 }
 
 static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N, double alpha,
@@ -4548,18 +4772,59 @@ static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc,
     if (rc) { h->lev_on = false; return rc; }
     PCG_HT(h, "init:done");
     int done = 0;
+    // Depth d >= 2 is decomposed on the degrees at the start of depth d - 1 (upper bounds) and
+    // enqueued before depth d - 1's summary is read, so the device runs from one depth into the
+    // next without waiting for the host; k_decompose computes the exact prefixes, the launches are
+    // sized by the bounds and their surplus blocks exit at once. `pending` is the depth whose
+    // summary has not been read yet.
+    int pending = -1;
+    unsigned long long pending_seq = 0;
+    auto finish_pending = [&]() -> int {
+        if (pending < 0) return PCG_OK;
+        const int r = level_end_finish(h, pending, pending_seq, nullptr);
+        pending = -1;
+        return r;
+    };
     for (int depth = 0;; ++depth) {
         if (max_depth >= 0 && depth > max_depth) break;
         if (depth >= PCG_MAX_LEVELS) break;   // pcg_level_begin refuses deeper levels itself
         int64_t total = 0;
         PCG_HT(h, "loop:begin");
-        rc = pcg_level_begin(h, depth, &total, nullptr, nullptr);
-        if (rc == 1) break;
+        const bool pipe = depth >= pipeline_lo() && pending == depth - 1 && pipeline_ok(h) &&
+                          mode_of(h, depth) == MODE_DECIDE;
+        if (!pipe) {
+            rc = finish_pending();
+            if (!rc) rc = level_begin_impl(h, depth, &total, false);
+            if (rc == 1) break;
+            if (!rc) rc = pcg_level_run(h, 0, total);
+            unsigned long long seq = 0;
+            if (!rc) rc = level_end_enqueue(h, &seq);
+            if (rc) { h->lev_on = false; return rc; }
+            done = depth + 1;
+            if (depth + 1 >= pipeline_lo() && pipeline_ok(h)) {   // the next depth is enqueued before this summary is read
+                pending = depth;
+                pending_seq = seq;
+            } else {
+                rc = level_end_finish(h, depth, seq, nullptr);
+                if (rc) { h->lev_on = false; return rc; }
+            }
+            continue;
+        }
+        rc = level_begin_impl(h, depth, &total, true);
+        if (rc == 1) break;                   // not even the bound degrees allow another depth
         if (!rc) rc = pcg_level_run(h, 0, total);
-        if (!rc) rc = pcg_level_end(h, nullptr);
+        unsigned long long seq = 0;
+        if (!rc) rc = level_end_enqueue(h, &seq);
+        if (!rc) rc = finish_pending();       // depth - 1's counters; h->deg_h: the start of depth
         if (rc) { h->lev_on = false; return rc; }
+        if (!(h->maxdeg - 1 > depth - 1)) break;   // the enqueued depth found no work on the device
+        level_start_stats(h, depth);
         done = depth + 1;
+        pending = depth;
+        pending_seq = seq;
     }
+    rc = finish_pending();
+    if (rc) { h->lev_on = false; return rc; }
     h->lev_on = false;
     rc = export_sync(h);                 // the last depth's export (the skeleton's sepset rows)
     if (rc) return rc;

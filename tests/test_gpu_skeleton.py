@@ -149,6 +149,23 @@ def test_schur_prefix_sweep_matches_oracle(eng, n, N, seed, wl, wh, ep, sp, monk
     assert_skeleton_matches(out, ref, n)
 
 
+@pytest.mark.parametrize("lo", ["2", "3", "5"])
+@pytest.mark.parametrize("n,N,seed,wl,wh,ep", [CASES[6], (300, 1500, 7, 0.1, 0.6, 0.06)])
+def test_pipelined_level_loop_matches_oracle(eng, n, N, seed, wl, wh, ep, lo, monkeypatch):
+    """The pipelined level loop (PCG_PIPELINE=1: depth d >= PCG_PIPELINE_LO decomposed on the
+    degrees at the start of d - 1 and enqueued before depth d - 1's summary is read, k_decompose
+    writing the exact prefixes on the device, bound-sized launches): the oracle's skeleton, unions,
+    per-level counts and level count, unlimited depth."""
+    X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
+    C = np.corrcoef(X.T)
+    ref = cpc.skeleton(C, N)
+    monkeypatch.setenv("PCG_PIPELINE", "1")
+    monkeypatch.setenv("PCG_PIPELINE_LO", lo)
+    out = eng.skeleton(C, N)
+    assert_skeleton_matches(out, ref, n)
+    assert out.levels == ref.levels
+
+
 def test_screen_list_overflow_reruns(eng):
     """A screen list too small for the fp32 sweep's undecided tests (config 5, depth <= 3:
     ~9e4 of them at depth 3) overflows, the level reports it with the capacity raised, and

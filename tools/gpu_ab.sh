@@ -1,22 +1,19 @@
 #!/bin/bash
-# A/B of the fp32 screen per depth: kernel stats under rocprofv3 for each PCG_SCREEN_MASK given
+# A/B bench lines: every in-tree env setting in $AB_ENVS (space-separated, "base" = none) on the
+# in-tree library, then every tools/micro/variants/libpcgpu_*.so (variant_bench.sh).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-for m in "$@"; do
-  export ${AB_VAR:-PCG_SCREEN_MASK}=$m
-  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/ab_$m -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/ab_$m.log 2>&1 || exit $?
-  echo "== mask $m"
-  python - "$m" <<'PY'
-import csv, glob, json, sys
-m = sys.argv[1]
-f = glob.glob(f"gpurun_out/ab_{m}/**/run_kernel_stats.csv", recursive=True)
-r = list(csv.DictReader(open(f[0])))
-for x in sorted(r, key=lambda x: -float(x["TotalDurationNs"]))[:14]:
-    if "1>" in x["Name"] and "k_level" in x["Name"]: continue
-    print(x["Name"][:58].ljust(58), x["Calls"], "%.3f" % (float(x["AverageNs"]) / 1e6))
-l = [x for x in open(f"gpurun_out/ab_{m}.log") if x.startswith("{")]
-d = json.loads(l[-1]); print("ms", round(d["ms_per_step"], 3), "level_ms", d["level_ms"])
+O=gpurun_out/ab
+mkdir -p $O
+for v in ${AB_ENVS:-base}; do
+  if [ "$v" = base ]; then e=""; else e="$v"; fi
+  env $e timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline > $O/bench.log 2>&1 || { tail -5 $O/bench.log; exit 1; }
+  python - $O/bench.log "$v" <<'PY'
+import json,sys
+d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print('%-28s'%sys.argv[2], round(d['ms_per_step'],3), d['kernel_ms_per_level'], d['level_ms'], 'corr', d['corr_ms'][-2:])
 PY
 done
+ls tools/micro/variants/libpcgpu_*.so > /dev/null 2>&1 && { timeout -k 10 900 bash tools/variant_bench.sh || exit 1; }
+echo done
