@@ -4869,9 +4869,11 @@ extern "C" int pcg_pc_skeleton(pcg_handle *h, const double *X, int64_t N, int64_
 // wait for the queued sepset exports and take their row count (the export stream's counter)
 int export_sync(pcg_handle *h) {
     if (!h->xany) return PCG_OK;
+    // the row counter comes back on the export stream itself: one stream sync, no device-wide copy
+    if (!pcg_ensure_pinned(h, h->ctr_pin, sizeof(unsigned long long))) return pcg_fail(h, PCG_ERR_OOM, "pinned counter");
+    PCG_HIP(h, hipMemcpyAsync(h->ctr_pin.p, h->exp_ctr.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, h->xs));
     PCG_HIP(h, hipStreamSynchronize(h->xs));
-    unsigned long long rows = 0;
-    PCG_HIP(h, hipMemcpy(&rows, h->exp_ctr.p, sizeof(rows), hipMemcpyDeviceToHost));
+    const unsigned long long rows = *(const unsigned long long *)h->ctr_pin.p;
     h->xany = false;
     h->xpending[0] = h->xpending[1] = false;
     if ((int64_t)rows > h->export_cap)

@@ -93,6 +93,7 @@ class Engine:
         self.h = h
         with torch.cuda.device(self.device):
             stream = torch.cuda.current_stream(self.device)
+        self.stream = stream
         check(self.h, self.lib.pcg_set_stream(self.h, ctypes.c_void_p(stream.cuda_stream)), "pcg_set_stream")
 
     def close(self):
@@ -228,7 +229,7 @@ class Engine:
         finally:
             self._unban(bd)
         check(self.h, rc, "pcg_skeleton")
-        self.sync()
+        ev1.synchronize()       # the call returned after its last device phase; the timing event follows it
         t0 = time.perf_counter()
         out = self._collect(n, rl, st, ev0.elapsed_time(ev1))
         out.extra["collect_ms"] = 1000.0 * (time.perf_counter() - t0)
@@ -258,7 +259,7 @@ class Engine:
         finally:
             self._unban(bd)
         check(self.h, rc, "pcg_pc_skeleton")
-        self.sync()
+        ev1.synchronize()
         t0 = time.perf_counter()
         out = self._collect(n, rl, st, ev0.elapsed_time(ev1))
         out.extra["collect_ms"] = 1000.0 * (time.perf_counter() - t0)
@@ -288,7 +289,10 @@ class Engine:
             check(self.h, self.lib.pcg_record_export(self.h, rec.ctypes.data_as(ctypes.c_void_p), rc_.value,
                                                      near.ctypes.data_as(ctypes.c_void_p), nc_.value),
                   "pcg_record_export")
-        self.sync()
+        # the sepset rows were copied on the handle's stream: a caller on that stream is ordered
+        # after them; any other current stream waits for them
+        if torch.cuda.current_stream(self.device) != self.stream:
+            torch.cuda.current_stream(self.device).wait_stream(self.stream)
         return SkeletonOut(n, rl, xy, bits, deg[:L].copy(), st.as_dict(), rec, near, device_ms)
 
     # ------------------------------------------------------------------ batched CI tests
