@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -111,20 +112,51 @@ I8_PEAK_TOPS = 5000.0         # MI355X dense int8 MFMA (2x the dense BF16 rate; 
 MFMA_F64_MEASURED_TFLOPS = 47.9   # v_mfma_f64_16x16x4_f64 at 4 waves/SIMD, tools/micro/mfma_f64.hip (profiles/r02_mfma_f64.log)
 
 
+CRT_MODULI = (256, 255, 253, 251, 247, 241, 239, 233, 229, 227, 223, 217, 211, 199, 197, 193, 191, 181, 179, 173,
+              167, 163, 157, 151)     # corr.hip kCrtModuli
+CRT_TILE = 256
+
+
+def k1_crt_moduli(n: int, N: int):
+    """(k, b) of corr.hip's crt_plan, or None when K1 takes the digit / fp64 path: the fewest
+    moduli whose product M leaves b >= PCG_K1_CRT_BITS bits per value with M > 2 N 4^b."""
+    if (os.environ.get("PCG_K1_I8", "1") == "0" or os.environ.get("PCG_K1_CRT", "1") == "0"
+            or n < int(os.environ.get("PCG_K1_CRT_MINN", "256"))):
+        return None
+    bmin = int(os.environ.get("PCG_K1_CRT_BITS", "56"))
+    lm = 0.0
+    for k, m in enumerate(CRT_MODULI, 1):
+        lm += math.log2(m)
+        b = math.floor((lm - math.log2(N) - 1.0 - 0.01) / 2.0)
+        if b >= bmin:
+            return k, min(b, 63)
+    return None
+
+
 def k1_roofline(n: int, N: int, corr_ms: float) -> dict:
-    """K1 (np.corrcoef). Default path (PCG_K1_I8, corr.hip): the centred X split into 9 int8 digit
-    planes and the Gram as 45 exact int8 GEMMs of the upper-triangle 64-square tiles on
-    v_mfma_i32_32x32x32_i8; executed int8 ops = 45 x 2 x T(T+1)/2 x 64^2 x N_pad. The fp64 path
-    (PCG_K1_I8=0) runs v_mfma_f64_16x16x4_f64 on the same tiles. Either way the algorithmic
-    work is 2 N n^2 (reported as achieved_algorithmic, TFLOP/s)."""
+    """K1 (np.corrcoef). Default path for n >= 256 (corr.hip, CRT): the centred X truncated to
+    b-bit integers, k residue planes, the Gram as k exact int8 GEMMs of the upper-triangle
+    256-square tiles on v_mfma_i32_32x32x32_i8, rebuilt by the Chinese remainder theorem;
+    executed int8 ops = k x 2 x T(T+1)/2 x 256^2 x N_pad. Below n = 256: 9 digit planes and 45
+    GEMMs of 64-square tiles. The fp64 path (PCG_K1_I8=0) runs v_mfma_f64_16x16x4_f64 on 64-square
+    tiles. Either way the algorithmic work is 2 N n^2 (reported as achieved_algorithmic, TFLOP/s)."""
+    i8 = os.environ.get("PCG_K1_I8", "1") != "0"
+    crt = k1_crt_moduli(n, N)
+    npad = (N + 63) // 64 * 64
+    line = {"bound": "mfma", "ms": corr_ms, "path": "int8 CRT" if crt else ("int8 digits" if i8 else "fp64"),
+            "achieved_algorithmic_tflops": 2.0 * N * n * n / (corr_ms / 1e3) / 1e12,
+            "what": "pcg_corr end to end (column stats, residue / digit planes, split-K GEMM, rebuild, normalisation)"}
+    if crt:
+        k, b = crt
+        T = (n + CRT_TILE - 1) // CRT_TILE
+        ops = k * 2.0 * (T * (T + 1) // 2) * CRT_TILE * CRT_TILE * npad
+        ex = ops / (corr_ms / 1e3) / 1e12
+        line.update({"moduli": k, "bits": b, "unit": "TOP/s (int8)", "peak": I8_PEAK_TOPS, "achieved_executed": ex,
+                     "frac": ex / I8_PEAK_TOPS})
+        return line
     T = (n + K1_TILE - 1) // K1_TILE
     tiles = T * (T + 1) // 2
-    i8 = os.environ.get("PCG_K1_I8", "1") != "0"
-    line = {"bound": "mfma", "ms": corr_ms, "path": "int8 digits" if i8 else "fp64",
-            "achieved_algorithmic_tflops": 2.0 * N * n * n / (corr_ms / 1e3) / 1e12,
-            "what": "pcg_corr end to end (column stats, digit planes, split-K GEMM, fused normalisation)"}
     if i8:
-        npad = (N + 63) // 64 * 64
         ops = K1_DIGITS * (K1_DIGITS + 1) // 2 * 2.0 * tiles * K1_TILE * K1_TILE * npad
         ex = ops / (corr_ms / 1e3) / 1e12
         line.update({"unit": "TOP/s (int8)", "peak": I8_PEAK_TOPS, "achieved_executed": ex, "frac": ex / I8_PEAK_TOPS})

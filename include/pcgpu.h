@@ -110,19 +110,23 @@ int pcg_set_record_sample(pcg_handle *h, int64_t modulus, int64_t residue);
 
 /* ---- K1: correlation -------------------------------------------------------------
  * Replaces FisherZ.__init__'s `np.corrcoef(data.T)` [U]: column means,
- * centred X^T X on fp64 MFMA (v_mfma_f64_16x16x4_f64, LDS-tiled, upper-triangle tiles),
- * *= 1/(N-1), /= s_i, /= s_j, clip to [-1, 1] (numpy's order).
+ * centred X^T X, *= 1/(N-1), /= s_i, /= s_j, clip to [-1, 1] (numpy's order). The Gram runs on
+ * the int8 matrix cores: for n >= 256 as k residue GEMMs combined by the Chinese remainder
+ * theorem (exact integer Gram of the values truncated to b >= 56 bits of their column scale,
+ * rounded to fp64 once), below that as 45 digit GEMMs; PCG_K1_I8=0 selects fp64 MFMA.
  * X: device, N x n (ldx >= n). C: device, n x n (ldc >= n).                            */
 int pcg_corr(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx,
              double *C, int64_t ldc);
 
 /* ---- K1 sharded over ranks (multi-GPU) --------------------------------------------
- * Rank `rank` of `world` computes the centred Gram sums of its share of the 64-row tile
- * rows (zig-zag assignment, upper-triangle tiles only) into `packed` (device,
- * rows_per_rank x n doubles, see pcg_corr_shard_rows). The caller all-gathers the packed
- * buffers rank-major (RCCL over xGMI) and calls pcg_corr_shard_finish, which unpacks,
- * mirrors and normalises: C is bitwise the single-GPU pcg_corr result (same split-K,
- * same summation order) for every world size.                                          */
+ * Rank `rank` of `world` computes its share of the Gram work into `packed` (device,
+ * pcg_corr_shard_bytes bytes): a contiguous run of (tile, modulus, slab) residue units on the
+ * CRT path, else the Gram sums of its zig-zag share of the 64-row tile rows. The caller
+ * all-gathers the packed buffers rank-major (RCCL over xGMI) and calls pcg_corr_shard_finish on
+ * the same handle (it reads the column exponents pcg_corr_shard left there), which rebuilds,
+ * mirrors and normalises: C is bitwise the single-GPU pcg_corr result for every world size.
+ * pcg_corr_shard_rows: the digit / fp64 path's rows_per_rank (packed = rows x n doubles).     */
+int pcg_corr_shard_bytes(int64_t n, int64_t N, int world, int64_t *bytes_per_rank);
 int pcg_corr_shard_rows(int64_t n, int world, int64_t *rows_per_rank);
 int pcg_corr_shard(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx, int rank,
                    int world, double *packed);

@@ -87,6 +87,7 @@ SIGNATURES = [
     ("pcg_set_record_sample", I32, [P, I64, I64]),
     ("pcg_corr", I32, [P, P, I64, I64, I64, P, I64]),
     ("pcg_corr_shard_rows", I32, [I64, ctypes.c_int, ctypes.POINTER(I64)]),
+    ("pcg_corr_shard_bytes", I32, [I64, I64, ctypes.c_int, ctypes.POINTER(I64)]),
     ("pcg_corr_shard", I32, [P, P, I64, I64, I64, ctypes.c_int, ctypes.c_int, P]),
     ("pcg_corr_shard_finish", I32, [P, P, I64, I64, ctypes.c_int, P, I64]),
     ("pcg_skeleton", I32, [P, P, I64, I64, I64, D, ctypes.c_int, ctypes.c_int, P, ctypes.POINTER(PcgStats)]),

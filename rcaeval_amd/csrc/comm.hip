@@ -334,10 +334,10 @@ extern "C" int pcg_corr_sharded(pcg_handle *h, const double *X, int64_t N, int64
                                 int64_t ldc) {
     int rc = need_comm(h);
     if (rc) return rc;
-    int64_t rows = 0;
-    rc = pcg_corr_shard_rows(n, h->comm_world, &rows);
-    if (rc) return pcg_fail(h, rc, "pcg_corr_shard_rows");   // a function of (n, world): every rank agrees
-    const size_t per = (size_t)rows * (size_t)n;
+    int64_t bytes = 0;
+    rc = pcg_corr_shard_bytes(n, N, h->comm_world, &bytes);
+    if (rc) return pcg_fail(h, rc, "pcg_corr_shard_bytes");   // a function of (n, N, world): every rank agrees
+    const size_t per = (size_t)bytes / sizeof(double);
     // buffer growth is the same decision on every rank (same n, world, call history); when it
     // happens, its outcome is agreed before the all-gather
     const size_t b1 = sizeof(double) * std::max<size_t>(per, 1);

@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
+#include <cstring>
 #include <vector>
 
 #include "handle.h"
@@ -294,6 +296,7 @@ constexpr int K1_TB = 32;                    // rows (t) per digit block = the M
 constexpr int K1_I8_MAXK = 14336;            // rows per slab: 9 * 14336 * 127^2 < 2^31
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 // t-th upper-triangle tile in supertile order: 8 x 8 groups of tiles (upper triangle of the
 // group grid, row-major; inside a group row-major, bi <= bj on the diagonal groups). An XCD runs
@@ -475,6 +478,364 @@ __global__ __launch_bounds__(256, 2) void k_xtx_i8(const int8_t *Dg, int CB, int
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// K1 on the int8 matrix cores, CRT form (PCG_K1_CRT, the default for n >= 256; the Ozaki
+// scheme II split: linear in the number of moduli instead of quadratic in the digits).
+//
+// Each centred value is truncated to a b-bit integer on its column's scale,
+//     a_tj = trunc(v_tj 2^(b - e_j)),  |a_tj| < 2^b,  v_tj = fl(X_tj - mean_j),
+// and the integer Gram A^T A is computed EXACTLY through the Chinese remainder theorem. For k
+// pairwise coprime moduli m_i <= 256 with M = prod m_i > 2 N 4^b, (A^T A) mod m_i is one int8
+// GEMM of the balanced residue planes (a mod m_i in [-128, 127]) accumulated exactly in int32
+// (|sum| <= rows x 128^2 < 2^31 per split-K slab), and the k residues determine every entry
+// (|G| < N 4^b < M / 2): x = sum_i z_i M_i - q M with M_i = M / m_i, z_i = r_i M_i^-1 mod m_i
+// and q = round(sum_i z_i / m_i), built in 32-bit limbs and rounded to fp64 once,
+// G_ij = x 2^(e_i + e_j - 2b). The only error is the truncation, 2^-b of the column scale
+// (b >= 56; b = 59 with k = 17 at N = 10^4); the digit path's 45 GEMMs become k.
+// Kernels: k_residues (the k residue planes, the digit path's blocked layout), k_xtx_crt
+// (one 256 x 256 upper tile x one modulus x one split-K slab per 512-thread block, operands
+// staged by LDS-DMA through a 4-stage ring; the residue
+// sums of the slab written mod m as bytes in the MFMA's own lane order), k_crt_finish (slab sums,
+// the CRT rebuild, the upper triangle of G), then k_normalize_tiles as for the other paths.
+// A result is the correctly rounded fp64 of the exact truncated Gram, so every tile split,
+// slab split and world size gives the same bits.
+constexpr int CRT_KMAX = 24;               // moduli (M < 2^192)
+constexpr int CRT_L = 6;                   // 32-bit limbs of M
+constexpr int CRT_T = 256;                 // output tile
+constexpr int CRT_KB = 2;                  // 32-row k-blocks per LDS stage
+constexpr int CRT_NS = 4;                  // LDS ring stages
+constexpr int CRT_STAGE = CRT_KB * 16384;  // bytes per stage: CRT_KB x (A, B) x 4 column blocks x 2 KB
+constexpr int CRT_MAXKB = 4095;            // k-blocks per slab: 4095 x 32 x 128^2 < 2^31
+constexpr int CRT_UNIT = CRT_T * CRT_T;    // residue bytes per (tile, modulus, slab)
+static const int kCrtModuli[CRT_KMAX] = {256, 255, 253, 251, 247, 241, 239, 233, 229, 227, 223, 217,
+                                         211, 199, 197, 193, 191, 181, 179, 173, 167, 163, 157, 151};
+
+struct CrtTab {
+    int k, b, L;                    // moduli, bits of |a|, limbs of M
+    int m[CRT_KMAX];
+    int y[CRT_KMAX];                // (M / m_i)^-1 mod m_i
+    float finv[CRT_KMAX];           // fl(1 / m_i)
+    double dinv[CRT_KMAX];
+    uint32_t wlo[CRT_KMAX], whi[CRT_KMAX];   // bytes 2^(8q) mod m_i, 2^(32 + 8q) mod m_i (q = 0..3)
+    uint32_t Mi[CRT_KMAX][CRT_L];   // M / m_i, little-endian limbs
+    uint32_t M[CRT_L];
+};
+
+// s mod m for 0 <= s < 2^20 (fp32 quotient, one correction each way)
+__device__ __forceinline__ uint32_t crt_mod(uint32_t s, int m, float finv) {
+    const float q = floorf((float)s * finv);
+    int r = (int)s - (int)q * m;
+    r += r < 0 ? m : 0;
+    r -= r >= m ? m : 0;
+    return (uint32_t)r;
+}
+
+// residue planes, blocked like the digit planes: R[((mi * CBp + cb) * TB + tb) * 2048 + c * 32 + tt]
+// = a mod m_i (balanced, int8) of column 64 cb + c at row 32 tb + tt; zero past n and N. One
+// thread = 16 rows of one column, a wave = 32 columns x 2 halves = one contiguous 1 KB store.
+__global__ __launch_bounds__(256) void k_residues(const double *X, int64_t N, int n, int64_t ldx, const double *mean,
+                                                 const int *expo, int CBp, int TB, CrtTab tab, int8_t *R) {
+    const int cb = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = 32 * (w & 1) + (lane >> 1), half = lane & 1;
+    const int tb = blockIdx.y * 2 + (w >> 1);
+    const int j = cb * 64 + c;
+    const bool vj = j < n;
+    const int e = vj ? expo[j] : 0;
+    const bool live = vj && e != K1_NONFINITE;
+    const double mu = live ? mean[j] : 0.0;
+    uint32_t lo[16], hi[16];
+    float sg[16];                                        // +-1 per value
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int64_t t = (int64_t)tb * 32 + 16 * half + i;
+        const double v = (live && t < N) ? X[t * ldx + j] - mu : 0.0;
+        const double y = ldexp(fabs(v), tab.b - e);      // < 2^b <= 2^63, exact scaling
+        hi[i] = (uint32_t)(y * 0x1p-32);                 // truncating conversions: |a| = trunc(y)
+        lo[i] = (uint32_t)(y - (double)hi[i] * 0x1p32);  // exact difference (multiples of ulp(y))
+        sg[i] = v < 0.0 ? -1.0f : 1.0f;
+    }
+    const int64_t plane = (int64_t)CBp * TB * 2048;
+    int8_t *dst = R + ((int64_t)cb * TB + tb) * 2048 + c * 32 + 16 * half;
+    // bytes: the low byte of each of 4 words packed into one word (v_perm_b32)
+    auto pack4 = [](uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) {
+        const uint32_t w01 = __builtin_amdgcn_perm(b1, b0, 0x0c0c0400u);
+        const uint32_t w23 = __builtin_amdgcn_perm(b3, b2, 0x0c0c0400u);
+        return __builtin_amdgcn_perm(w23, w01, 0x05040100u);
+    };
+    for (int mi = 0; mi < tab.k; ++mi) {
+        v4i pk;
+        const int m = tab.m[mi];
+        if (m == 256) {          // the low byte of the two's-complement a
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                uint32_t bb[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int i = 4 * q + u;
+                    bb[u] = sg[i] < 0.0f ? 0u - lo[i] : lo[i];
+                }
+                pk[q] = (int)pack4(bb[0], bb[1], bb[2], bb[3]);
+            }
+        } else {
+            // odd m: s = |a| mod-equivalent (< 8 x 255^2, exact in fp32), r = s - m rint(s / m) in
+            // [-(m-1)/2, (m-1)/2] (s / m is never a half-integer for odd m, and fl(1/m) moves it
+            // by < 1/(32 m)), then the sign; rint and the byte via the 1.5 x 2^23 magic constant
+            const f2 fi = {tab.finv[mi], tab.finv[mi]};
+            const f2 nm = {-(float)m, -(float)m};
+            const f2 mg = {12582912.0f, 12582912.0f};
+            const uint32_t wl = tab.wlo[mi], wh = tab.whi[mi];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                uint32_t bb[4];
+#pragma unroll
+                for (int u = 0; u < 4; u += 2) {
+                    const int i = 4 * q + u;
+                    const float x0 = (float)__builtin_amdgcn_udot4(lo[i], wl,
+                                                                   __builtin_amdgcn_udot4(hi[i], wh, 0u, false), false);
+                    const float x1 = (float)__builtin_amdgcn_udot4(lo[i + 1], wl,
+                                                                   __builtin_amdgcn_udot4(hi[i + 1], wh, 0u, false), false);
+                    const f2 x = {x0, x1};
+                    const f2 sv = {sg[i], sg[i + 1]};
+                    const f2 qv = __builtin_elementwise_fma(x, fi, mg) - mg;    // rint(s / m)
+                    const f2 rv = __builtin_elementwise_fma(qv, nm, x) * sv + mg;
+                    // (through named floats: this compiler's __builtin_bit_cast of a vector
+                    // component reads component 0)
+                    const float r0 = rv.x, r1 = rv.y;
+                    bb[u] = __float_as_uint(r0);
+                    bb[u + 1] = __float_as_uint(r1);
+                }
+                pk[q] = (int)pack4(bb[0], bb[1], bb[2], bb[3]);
+            }
+        }
+        *reinterpret_cast<v4i *>(dst + mi * plane) = pk;
+    }
+}
+
+// the residue GEMM of one 256 x 256 upper tile, one modulus and one split-K slab. 8 waves as 2 x 4,
+// each 128 x 64 (4 x 2 v_mfma_i32_32x32x32_i8 tiles, 128 accumulators); CRT_KB k-blocks per LDS
+// stage, two stages. Units u = (slab * k + mi) * ntiles + tile, this launch runs u0 .. u0 + nu - 1
+// (a rank's share) and writes unit u0 + l at out + l * CRT_UNIT, in lane order:
+// byte ((w * 4 + a) * 2 + b) * 1024 + lane * 16 + kk = accumulator kk of MFMA tile (a, b) of wave w.
+__global__ __launch_bounds__(512, 1) void k_xtx_crt(const int8_t *R, int TB, int64_t plane, int T, int ntiles, int k,
+                                                  int kb, CrtTab tab, int64_t u0, int64_t nu, uint8_t *out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    int64_t lin = blockIdx.x;
+    {   // XCD-contiguous runs: an XCD's resident blocks share the modulus and slab (all panels in its L2)
+        const int64_t per = gridDim.x / 8;
+        lin = (blockIdx.x % 8) * per + blockIdx.x / 8;
+        if (lin >= nu) return;
+    }
+    const int64_t u = u0 + lin;
+    const int t = (int)(u % ntiles);
+    const int64_t sm = u / ntiles;
+    const int mi = (int)(sm % k), slab = (int)(sm / k);
+    int bi, bj;
+    tile_of(t, T, bi, bj);
+    const int tb0 = slab * kb, tb1 = min(TB, tb0 + kb);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r = lane & 31, hh = lane >> 5;
+    const int wr = w >> 2, wc = w & 3;
+
+    v16i acc[4][2];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[a][b][q] = 0;
+
+    // staging by LDS-DMA (global_load_lds_dwordx4, no VGPR round trip): a stage is CRT_KB k-blocks,
+    // word o = q * 512 + tid of a stage is k-block q >> 1, side q & 1 (A = tile row bi, B = tile
+    // column bj), column block tid >> 7 of the side, 16-byte word tid & 127 -- lane-linear per wave,
+    // as the DMA writes. CRT_NS stages in a ring, CRT_NS - 1 in flight across the raw barriers
+    // (counted vmcnt, never a __syncthreads() that would drain them).
+    const int8_t *Rm = R + (int64_t)mi * plane;
+    const int8_t *srcA = Rm + (int64_t)(bi * 4 + (tid >> 7)) * TB * 2048 + (tid & 127) * 16;
+    const int8_t *srcB = Rm + (int64_t)(bj * 4 + (tid >> 7)) * TB * 2048 + (tid & 127) * 16;
+    const int ns = (tb1 - tb0) / CRT_KB;       // slabs hold whole stages (kb and TB even)
+    auto issue = [&](int sidx) {
+        if (sidx >= ns) return;
+        unsigned char *dst = smem + (sidx % CRT_NS) * CRT_STAGE + w * 1024;
+        const int64_t tb = (int64_t)(tb0 + sidx * CRT_KB);
+#pragma unroll
+        for (int q = 0; q < 2 * CRT_KB; ++q)
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(((q & 1) ? srcB : srcA) + (tb + (q >> 1)) * 2048),
+                (__attribute__((address_space(3))) void *)(dst + q * 8192), 16, 0, 0);
+    };
+#pragma unroll
+    for (int sidx = 0; sidx < CRT_NS - 1; ++sidx) issue(sidx);
+    const unsigned char *fa = smem + (2 * wr * 2048 + r * 32 + 16 * hh);
+    const unsigned char *fb = smem + (8192 + wc * 2048 + r * 32 + 16 * hh);
+    for (int sidx = 0; sidx < ns; ++sidx) {
+        // stage sidx landed (this thread's DMAs; the later stages stay in flight), then the
+        // barrier: every wave's DMAs of sidx are in LDS and every wave is done reading sidx - 1
+        const int ahead = min(CRT_NS - 2, ns - 1 - sidx);
+        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * 2 * CRT_KB) : "memory");
+        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * CRT_KB) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        issue(sidx + CRT_NS - 1);               // into the ring slot read in iteration sidx - 1
+        const int off = (sidx % CRT_NS) * CRT_STAGE;
+        v4i af[2][4], bf[2][2];
+        auto frag = [&](int kk, int sl) {
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+                af[sl][a] = *reinterpret_cast<const v4i *>(fa + off + kk * 16384 + (a >> 1) * 2048 + (a & 1) * 1024);
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+                bf[sl][b] = *reinterpret_cast<const v4i *>(fb + off + kk * 16384 + b * 1024);
+        };
+        frag(0, 0);
+#pragma unroll
+        for (int kk = 0; kk < CRT_KB; ++kk) {
+            if (kk + 1 < CRT_KB) frag(kk + 1, (kk + 1) & 1);
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[kk & 1][a], bf[kk & 1][b], acc[a][b], 0, 0, 0);
+        }
+    }
+    // epilogue: the slab's sums mod m as bytes, 16 per lane per MFMA tile (one 16-byte store)
+    const int m = tab.m[mi];
+    const double dm = (double)m, dinv = tab.dinv[mi];
+    uint8_t *o = out + lin * CRT_UNIT + (int64_t)w * 8192 + lane * 16;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            v4i pk = {0, 0, 0, 0};
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int v = acc[a][b][q];
+                uint32_t rr;
+                if (m == 256) {
+                    rr = (uint32_t)v & 255u;
+                } else {
+                    const double d = (double)v;
+                    int x = (int)fma(floor(d * dinv), -dm, d);
+                    x += x < 0 ? m : 0;
+                    x -= x >= m ? m : 0;
+                    rr = (uint32_t)x;
+                }
+                pk[q >> 2] |= (int)(rr << (8 * (q & 3)));
+            }
+            *reinterpret_cast<v4i *>(o + (a * 2 + b) * 1024) = pk;
+        }
+}
+
+// the CRT rebuild: one thread = 4 entries (one 32-bit word of a 16-byte lane word of the units:
+// the same column j, rows 8 apart... see the lane order above); residues summed over the ks slabs
+// in u16 lanes, G_ij (i <= j) written to the upper triangle of G
+__global__ __launch_bounds__(256) void k_crt_finish(const uint8_t *Rs, int T, int ntiles, int ks, CrtTab tab,
+                                                   const int *expo, int n, double *G, int64_t ldg) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int t = (int)(gid >> 14), rem = (int)((gid >> 2) & 4095), g = (int)(gid & 3);
+    if (t >= ntiles) return;
+    int bi, bj;
+    tile_of(t, T, bi, bj);
+    const int lane = rem & 63, wab = rem >> 6;
+    const int b = wab & 1, a = (wab >> 1) & 3, w = wab >> 3;
+    const int wr = w >> 2, wc = w & 3, r = lane & 31, hh = lane >> 5;
+    const int j = bj * CRT_T + wc * 64 + b * 32 + r;
+    // this word: accumulators q = 4 g .. 4 g + 3, rows ibase + (q & 3) + 8 (q >> 2) = ibase + q4 + 8 g
+    const int ibase = bi * CRT_T + wr * 128 + a * 32 + 4 * hh + 8 * g;
+    if (j >= n || ibase > j) return;
+    const int k = tab.k;
+    const int ej = expo[j];
+    const int64_t ustride = (int64_t)ntiles * CRT_UNIT;          // next modulus
+    const uint8_t *src = Rs + (int64_t)t * CRT_UNIT + rem * 16 + 4 * g;
+    // moduli outermost: each modulus' constants are read once for the 4 entries (4 independent
+    // accumulation chains); S = sum_i z_i M_i in 64-bit limb accumulators, fs = sum_i z_i / m_i
+    uint64_t acc[4][CRT_L] = {};
+    double fs[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int mi = 0; mi < CRT_KMAX; ++mi) {
+        if (mi >= k) continue;
+        uint32_t se = 0, so = 0;            // the ks slab bytes of the 4 entries, summed in u16 lanes
+        for (int s = 0; s < ks; ++s) {
+            const uint32_t wd = *reinterpret_cast<const uint32_t *>(src + ((int64_t)s * k + mi) * ustride);
+            se += wd & 0x00ff00ffu;
+            so += (wd >> 8) & 0x00ff00ffu;
+        }
+        const int m = tab.m[mi];
+        const float fi = tab.finv[mi];
+        const uint32_t y = (uint32_t)tab.y[mi];
+        const double dinv = tab.dinv[mi];
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+            const uint32_t sv = (((q4 & 1) ? so : se) >> (16 * (q4 >> 1))) & 0xffffu;   // < ks x 255
+            const uint32_t z = crt_mod(sv * y, m, fi);     // r M_i^-1 mod m, r = sv mod m: s y < 2^20
+            fs[q4] = fma((double)z, dinv, fs[q4]);
+#pragma unroll
+            for (int l = 0; l < CRT_L; ++l)
+                if (l < tab.L) acc[q4][l] += (uint64_t)z * tab.Mi[mi][l];
+        }
+    }
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+        const int i = ibase + q4;
+        if (i > j) break;
+        const int ei = expo[i];
+        double gv;
+        if (ei == K1_NONFINITE || ej == K1_NONFINITE) {
+            gv = NAN;
+        } else {
+            const int64_t qq = (int64_t)floor(fs[q4] + 0.5);     // x = S - q M in [-M/2, M/2)
+            uint32_t lim[CRT_L];
+            int64_t carry = 0;
+#pragma unroll
+            for (int l = 0; l < CRT_L; ++l) {
+                int64_t v = carry;
+                if (l < tab.L) v += (int64_t)acc[q4][l] - qq * (int64_t)tab.M[l];
+                lim[l] = (uint32_t)v;
+                carry = v >> 32;                              // arithmetic: the sign carries on
+            }
+            const bool negx = carry < 0;
+            if (negx) {                                       // magnitude: two's complement
+                uint64_t c = 1;
+#pragma unroll
+                for (int l = 0; l < CRT_L; ++l) {
+                    const uint64_t v = (uint64_t)(~lim[l]) + c;
+                    lim[l] = (uint32_t)v;
+                    c = v >> 32;
+                }
+            }
+            int top = -1;
+#pragma unroll
+            for (int l = 0; l < CRT_L; ++l)
+                if (lim[l]) top = l;
+            if (top < 0) {
+                gv = 0.0;
+            } else {
+                // the top 96 bits (limbs top, top-1, top-2), normalised; the rest as a sticky bit
+                uint32_t l2 = 0, l1 = 0, l0 = 0;
+                bool sticky = false;
+#pragma unroll
+                for (int l = 0; l < CRT_L; ++l) {
+                    if (l == top) l2 = lim[l];
+                    if (l == top - 1) l1 = lim[l];
+                    if (l == top - 2) l0 = lim[l];
+                    if (l < top - 2 && lim[l]) sticky = true;
+                }
+                const int sh = __builtin_clz(l2);
+                uint64_t h64 = ((uint64_t)l2 << 32) | l1;
+                uint32_t low = l0;
+                if (sh) {
+                    h64 = (h64 << sh) | (low >> (32 - sh));
+                    low <<= sh;
+                }
+                if (low || sticky) h64 |= 1;                  // below the 53-bit rounding point
+                const double mag = fma((double)(uint32_t)(h64 >> 32), 0x1p32, (double)(uint32_t)h64);
+                gv = ldexp(mag, 32 * (top - 1) - sh + ei + ej - 2 * tab.b);
+                if (negx) gv = -gv;
+            }
+        }
+        G[(int64_t)i * ldg + j] = gv;
+    }
+}
+
 // slab split of the digit GEMM: a function of (n, N) only (every world size sums the same slabs
 // in the same order), rows per slab a multiple of the 32-row digit block and <= K1_I8_MAXK
 int split_k_i8(int n, int64_t N, int *kb_out) {
@@ -499,6 +860,140 @@ int k1_super() {                               // A/B knob: PCG_K1_SUPER_ORDER=0
 bool k1_i8() {
     const char *e = getenv("PCG_K1_I8");
     return !e || atoi(e) != 0;
+}
+
+// the CRT path's plan: a function of (n, N) only, so every rank and world size agrees
+struct CrtPlan {
+    CrtTab tab;
+    int T = 0, ntiles = 0, ks = 0, kb = 0, TB = 0, CBp = 0;
+    int64_t units = 0;
+};
+
+static int env_int(const char *name, int dflt) {
+    const char *e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+
+// little-endian 32-bit limb helpers for the host tables
+static void big_mul_small(uint32_t *x, int L, uint32_t m) {
+    uint64_t c = 0;
+    for (int l = 0; l < L; ++l) {
+        const uint64_t v = (uint64_t)x[l] * m + c;
+        x[l] = (uint32_t)v;
+        c = v >> 32;
+    }
+}
+static uint32_t big_div_small(const uint32_t *x, int L, uint32_t m, uint32_t *q) {   // q = x / m, returns x % m
+    uint64_t r = 0;
+    for (int l = L - 1; l >= 0; --l) {
+        const uint64_t v = (r << 32) | x[l];
+        q[l] = (uint32_t)(v / m);
+        r = v % m;
+    }
+    return (uint32_t)r;
+}
+
+bool crt_plan(int n, int64_t N, CrtPlan &p) {
+    if (!k1_i8() || env_int("PCG_K1_CRT", 1) == 0 || n < env_int("PCG_K1_CRT_MINN", 256)) return false;
+    const int bmin = env_int("PCG_K1_CRT_BITS", 56);
+    // k: the fewest moduli whose product leaves b >= bmin bits per value, M > 2 N 4^b (0.01 bit margin)
+    double lm = 0.0;
+    int k = 0, b = 0;
+    for (; k < CRT_KMAX; ++k) {
+        lm += std::log2((double)kCrtModuli[k]);
+        b = (int)std::floor((lm - std::log2((double)N) - 1.0 - 0.01) / 2.0);
+        if (b >= bmin) { ++k; break; }
+    }
+    if (b < bmin) return false;
+    b = std::min(b, 63);
+    CrtTab &t = p.tab;
+    memset(&t, 0, sizeof(t));
+    t.k = k;
+    t.b = b;
+    uint32_t M[CRT_L] = {1, 0, 0, 0, 0, 0};
+    for (int i = 0; i < k; ++i) big_mul_small(M, CRT_L, (uint32_t)kCrtModuli[i]);
+    t.L = (int)std::floor(lm / 32.0) + 1;      // M < 2^(32 L - 1)... at least one spare bit
+    if (lm > 32.0 * t.L - 1.0) ++t.L;
+    if (t.L > CRT_L) return false;
+    memcpy(t.M, M, sizeof(M));
+    for (int i = 0; i < k; ++i) {
+        const uint32_t m = (uint32_t)kCrtModuli[i];
+        t.m[i] = (int)m;
+        t.finv[i] = 1.0f / (float)m;
+        t.dinv[i] = 1.0 / (double)m;
+        const uint32_t rem = big_div_small(M, CRT_L, m, t.Mi[i]);
+        (void)rem;                              // 0: m divides M
+        uint32_t mq[CRT_L];
+        const uint32_t mim = big_div_small(t.Mi[i], CRT_L, m, mq);   // (M / m) mod m
+        t.y[i] = 0;
+        for (uint32_t y = 1; y < m; ++y)
+            if ((mim * y) % m == 1) { t.y[i] = (int)y; break; }
+        uint32_t wl = 0, wh = 0;
+        for (int q = 0; q < 4; ++q) {
+            uint64_t p1 = 1, p2 = 1;
+            for (int s = 0; s < 8 * q; ++s) p1 = (p1 * 2) % m;
+            for (int s = 0; s < 32 + 8 * q; ++s) p2 = (p2 * 2) % m;
+            wl |= (uint32_t)p1 << (8 * q);
+            wh |= (uint32_t)p2 << (8 * q);
+        }
+        t.wlo[i] = wl;
+        t.whi[i] = wh;
+    }
+    p.T = (n + CRT_T - 1) / CRT_T;
+    p.ntiles = p.T * (p.T + 1) / 2;
+    p.CBp = p.T * 4;
+    p.TB = (int)((N + 63) / 64 * 2);
+    // split-K: rounds of 256 resident blocks x k-blocks per slab (~0.3 us each) + the residue bytes
+    // each unit writes and k_crt_finish reads (128 KB, ~0.026 us of chip bandwidth)
+    int best = 1;
+    double best_cost = 1e300;
+    const int force = env_int("PCG_K1_CRT_KS", 0);
+    for (int ks = 1; ks <= 16; ++ks) {
+        int kbk = (p.TB + ks - 1) / ks;
+        kbk = (kbk + CRT_KB - 1) / CRT_KB * CRT_KB;
+        const int kse = (p.TB + kbk - 1) / kbk;
+        if (kse != ks || kbk > CRT_MAXKB) continue;
+        const int64_t U = (int64_t)p.ntiles * k * ks;
+        const double cost = (double)((U + 255) / 256) * kbk * 0.3 + (double)U * 0.026;
+        if (force > 0 ? ks == force : cost < best_cost) {
+            best_cost = cost;
+            best = ks;
+        }
+    }
+    {
+        int kbk = (p.TB + best - 1) / best;
+        kbk = (kbk + CRT_KB - 1) / CRT_KB * CRT_KB;
+        if (kbk > CRT_MAXKB) return false;     // N beyond 16 slabs of 131k rows: the digit path
+        p.kb = kbk;
+        p.ks = (p.TB + kbk - 1) / kbk;
+    }
+    p.units = (int64_t)p.ntiles * k * p.ks;
+    return true;
+}
+
+// the residue planes of X into h->k1_digits
+int crt_residues(pcg_handle *h, const CrtPlan &p, const double *X, int64_t N, int nn, int64_t ldx, const double *mean,
+                 const int *expo, const int8_t **R) {
+    const size_t bytes = (size_t)p.tab.k * p.CBp * p.TB * 2048;
+    if (!pcg_ensure(h, h->k1_digits, bytes)) return pcg_fail(h, PCG_ERR_OOM, "K1 residue planes (%zu bytes)", bytes);
+    hipLaunchKernelGGL(k_residues, dim3((unsigned)p.CBp, (unsigned)(p.TB / 2)), dim3(256), 0, h->stream, X, N, nn,
+                       ldx, mean, expo, p.CBp, p.TB, p.tab, (int8_t *)h->k1_digits.p);
+    *R = (const int8_t *)h->k1_digits.p;
+    return PCG_OK;
+}
+
+// units u0 .. u0 + nu - 1 of the residue GEMM into out
+void crt_gemm(pcg_handle *h, const CrtPlan &p, const int8_t *R, int64_t u0, int64_t nu, uint8_t *out) {
+    if (nu <= 0) return;
+    const int64_t plane = (int64_t)p.CBp * p.TB * 2048;
+    hipLaunchKernelGGL(k_xtx_crt, dim3((unsigned)((nu + 7) / 8 * 8)), dim3(512), CRT_NS * CRT_STAGE, h->stream, R, p.TB,
+                       plane, p.T, p.ntiles, p.tab.k, p.kb, p.tab, u0, nu, out);
+}
+
+void crt_finish(pcg_handle *h, const CrtPlan &p, const uint8_t *Rs, const int *expo, int nn, double *G, int64_t ldg) {
+    const int64_t threads = (int64_t)p.ntiles * 16384;
+    hipLaunchKernelGGL(k_crt_finish, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, h->stream, Rs, p.T,
+                       p.ntiles, p.ks, p.tab, expo, nn, G, ldg);
 }
 
 // digits of X (all columns) into h->k1_digits; returns the plane geometry
@@ -698,6 +1193,27 @@ extern "C" int pcg_corr_shard_rows(int64_t n, int world, int64_t *rows_per_rank)
     return PCG_OK;
 }
 
+// bytes of one rank's share (the pcg_corr_shard buffer; the all-gather moves world x this): the
+// CRT path's residue units, else the digit / fp64 path's packed Gram rows
+extern "C" int pcg_corr_shard_bytes(int64_t n, int64_t N, int world, int64_t *bytes_per_rank) {
+    if (n < 1 || N < 2 || world < 1 || n > (1 << 24) || !bytes_per_rank) return PCG_ERR_INVALID;
+    CrtPlan cp;
+    if (crt_plan((int)n, N, cp)) {
+        *bytes_per_rank = (cp.units + world - 1) / world * (int64_t)CRT_UNIT;
+        return PCG_OK;
+    }
+    int64_t rows = 0;
+    pcg_corr_shard_rows(n, world, &rows);
+    *bytes_per_rank = rows * n * (int64_t)sizeof(double);
+    return PCG_OK;
+}
+
+// the per-column exponents column_means left in h->colmean (the CRT finish of a shard call)
+static int *colmean_expo(pcg_handle *h, int64_t N, int nn) {
+    const int nchunks = (int)((N + MEAN_ROWS - 1) / MEAN_ROWS);
+    return reinterpret_cast<int *>((double *)h->colmean.p + (size_t)nn * nchunks * 3 + nn);
+}
+
 extern "C" int pcg_corr_shard(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx, int rank,
                               int world, double *packed) {
     if (!h || !X || !packed || N < 2 || n < 1 || ldx < n || n > (1 << 24) || world < 1 || rank < 0 ||
@@ -705,6 +1221,21 @@ extern "C" int pcg_corr_shard(pcg_handle *h, const double *X, int64_t N, int64_t
         return pcg_fail(h, PCG_ERR_INVALID, "pcg_corr_shard: invalid arguments");
     PCG_HIP(h, hipSetDevice(h->device));
     const int nn = (int)n;
+    CrtPlan cp;
+    if (crt_plan(nn, N, cp)) {     // this rank's contiguous run of (tile, modulus, slab) units
+        double *mean;
+        int *expo = nullptr;
+        int rc = column_means(h, X, N, nn, ldx, &mean, &expo);
+        if (rc) return rc;
+        const int8_t *R = nullptr;
+        rc = crt_residues(h, cp, X, N, nn, ldx, mean, expo, &R);
+        if (rc) return rc;
+        const int64_t per = (cp.units + world - 1) / world, u0 = per * rank;
+        crt_gemm(h, cp, R, u0, std::min<int64_t>(per, cp.units - u0), (uint8_t *)packed);
+        PCG_HIP(h, hipGetLastError());
+        PCG_HIP(h, hipStreamSynchronize(h->stream));
+        return PCG_OK;
+    }
     int64_t rows = 0;
     pcg_corr_shard_rows(n, world, &rows);
     PCG_HIP(h, hipMemsetAsync(packed, 0, sizeof(double) * rows * nn, h->stream));
@@ -762,12 +1293,25 @@ extern "C" int pcg_corr_shard_finish(pcg_handle *h, const double *gathered, int6
         return pcg_fail(h, PCG_ERR_INVALID, "pcg_corr_shard_finish: invalid arguments");
     PCG_HIP(h, hipSetDevice(h->device));
     const int nn = (int)n;
+    const double scale = 1.0 / (double)(N - 1);
+    CrtPlan cp;
+    if (crt_plan(nn, N, cp)) {     // gathered = every unit in canonical order; exponents from pcg_corr_shard
+        if (!pcg_ensure(h, h->pr_scratch, sizeof(double) * (size_t)nn * nn))
+            return pcg_fail(h, PCG_ERR_OOM, "pcg_corr_shard_finish scratch");
+        double *G = (double *)h->pr_scratch.p;
+        crt_finish(h, cp, (const uint8_t *)gathered, colmean_expo(h, N, nn), nn, G, nn);
+        const int T64 = (nn + NT - 1) / NT;
+        hipLaunchKernelGGL(k_normalize_tiles, dim3(T64 * (T64 + 1) / 2), dim3(256), 0, h->stream, (const double *)G,
+                           (int64_t)nn, (int64_t)0, 1, C, ldc, nn, scale);
+        PCG_HIP(h, hipGetLastError());
+        PCG_HIP(h, hipStreamSynchronize(h->stream));
+        return PCG_OK;
+    }
     int64_t rows = 0;
     pcg_corr_shard_rows(n, world, &rows);
     if (!pcg_ensure(h, h->colmean, sizeof(double) * ((size_t)nn * 2)))
         return pcg_fail(h, PCG_ERR_OOM, "pcg_corr scratch");
     double *sd = (double *)h->colmean.p;
-    const double scale = 1.0 / (double)(N - 1);
     hipLaunchKernelGGL(k_gather_finish_sd, dim3((nn + 255) / 256), dim3(256), 0, h->stream, gathered, rows, nn,
                        world, scale, sd);
     hipLaunchKernelGGL(k_gather_finish, dim3((nn + 255) / 256, nn), dim3(256), 0, h->stream, gathered, rows, nn,
@@ -783,6 +1327,29 @@ int pcg_corr_launch(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_
         return pcg_fail(h, PCG_ERR_INVALID, "pcg_corr: invalid arguments");
     PCG_HIP(h, hipSetDevice(h->device));
     const int nn = (int)n;
+    const double scale = 1.0 / (double)(N - 1);
+    CrtPlan cp;
+    if (crt_plan(nn, N, cp)) {
+        double *mean;
+        int *expo = nullptr;
+        int rc = column_means(h, X, N, nn, ldx, &mean, &expo);
+        if (rc) return rc;
+        const int8_t *R = nullptr;
+        rc = crt_residues(h, cp, X, N, nn, ldx, mean, expo, &R);
+        if (rc) return rc;
+        const size_t gbytes = sizeof(double) * (size_t)nn * nn;
+        if (!pcg_ensure(h, h->pr_scratch, gbytes + (size_t)cp.units * CRT_UNIT))
+            return pcg_fail(h, PCG_ERR_OOM, "pcg_corr CRT scratch");
+        double *G = (double *)h->pr_scratch.p;
+        uint8_t *Rs = (uint8_t *)h->pr_scratch.p + gbytes;
+        crt_gemm(h, cp, R, 0, cp.units, Rs);
+        crt_finish(h, cp, Rs, expo, nn, G, nn);
+        const int T64 = (nn + NT - 1) / NT;
+        hipLaunchKernelGGL(k_normalize_tiles, dim3(T64 * (T64 + 1) / 2), dim3(256), 0, h->stream, (const double *)G,
+                           (int64_t)nn, (int64_t)0, 1, C, ldc, nn, scale);
+        PCG_HIP(h, hipGetLastError());
+        return PCG_OK;
+    }
     const bool i8 = k1_i8();
     double *mean;
     int *expo = nullptr;
@@ -802,7 +1369,6 @@ int pcg_corr_launch(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_
         G = (double *)h->pr_scratch.p;
         ldg = nn;
     }
-    const double scale = 1.0 / (double)(N - 1);
     if (i8) {
         int CB = 0, TB = 0;
         const int8_t *Dg = nullptr;

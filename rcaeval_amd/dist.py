@@ -261,9 +261,10 @@ def _allreduce_stats(stats: dict, device, group=None) -> dict:
 
 
 def sharded_corr(eng, X, group=None):
-    """K1 sharded over the ranks of ``group``: each rank computes its zig-zag share of the
-    upper-triangle Gram tiles, one all-gather (RCCL over xGMI) assembles them, and every
-    rank normalises locally. Bitwise equal to the single-GPU ``eng.corr(X)``."""
+    """K1 sharded over the ranks of ``group``: each rank computes its share of the Gram work
+    (residue units on the CRT path, zig-zag tile rows otherwise), one all-gather (RCCL over
+    xGMI) assembles them, and every rank rebuilds and normalises locally. Bitwise equal to the
+    single-GPU ``eng.corr(X)``."""
     import torch
     import torch.distributed as dist
     rank, world = dist.get_rank(group), dist.get_world_size(group)
@@ -271,7 +272,7 @@ def sharded_corr(eng, X, group=None):
     N, n = Xd.shape
     packed = eng.corr_shard(Xd, rank, world)
     if dist.get_backend(group) == "nccl":
-        gathered = torch.empty((world * packed.shape[0], n), dtype=torch.float64, device=eng.device)
+        gathered = torch.empty(world * packed.numel(), dtype=torch.float64, device=eng.device)
         dist.all_gather_into_tensor(gathered, packed, group=group)
     else:   # gloo rehearsal (several ranks on one GPU)
         parts = [torch.empty_like(packed) for _ in range(world)]

@@ -130,19 +130,19 @@ class Engine:
         return C
 
     def corr_shard(self, X, rank: int, world: int):
-        """This rank's packed Gram rows of the sharded K1 (see ``pcg_corr_shard``)."""
+        """This rank's share of the sharded K1 (see ``pcg_corr_shard``), a flat fp64 tensor."""
         torch = _torch()
         Xd = self.to_device(X)
         N, n = Xd.shape
-        rows = ctypes.c_int64()
-        check(self.h, self.lib.pcg_corr_shard_rows(n, int(world), ctypes.byref(rows)), "pcg_corr_shard_rows")
-        packed = torch.empty((rows.value, n), dtype=torch.float64, device=self.device)
+        nbytes = ctypes.c_int64()
+        check(self.h, self.lib.pcg_corr_shard_bytes(n, N, int(world), ctypes.byref(nbytes)), "pcg_corr_shard_bytes")
+        packed = torch.empty(nbytes.value // 8, dtype=torch.float64, device=self.device)
         check(self.h, self.lib.pcg_corr_shard(self.h, ctypes.c_void_p(Xd.data_ptr()), N, n, n, int(rank),
                                               int(world), ctypes.c_void_p(packed.data_ptr())), "pcg_corr_shard")
         return packed
 
     def corr_shard_finish(self, gathered, N: int, n: int, world: int):
-        """C from the rank-major concatenation of every rank's packed rows."""
+        """C from the rank-major concatenation of every rank's share (same handle as ``corr_shard``)."""
         torch = _torch()
         g = gathered.contiguous()
         C = torch.empty((n, n), dtype=torch.float64, device=self.device)

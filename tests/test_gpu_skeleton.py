@@ -43,13 +43,15 @@ def test_corr_matches_numpy(eng, n, N, seed, wl, wh, ep):
     np.testing.assert_allclose(C, ref, rtol=0, atol=2e-14)
 
 
+@pytest.mark.parametrize("n", [70, 300])
 @pytest.mark.parametrize("kind", ["spikes", "scales", "constant", "nonfinite"])
-def test_corr_hard_columns_match_numpy(eng, kind):
+def test_corr_hard_columns_match_numpy(eng, kind, n):
     """K1 on columns that stress a per-column fixed-point split: heavy-tailed spikes (max/rms ~
     100), scales from 1e-8 to 1e7 (memory bytes) plus a large offset, constant columns (numpy's
-    0/0 NaN), and NaN / inf columns (NaN row and column)."""
+    0/0 NaN), and NaN / inf columns (NaN row and column). n = 70 runs the digit GEMMs, n = 300
+    the CRT residue GEMMs."""
     rng = np.random.default_rng({"spikes": 1, "scales": 2, "constant": 3, "nonfinite": 4}[kind])
-    N, n = 3000, 70
+    N = 3000
     X = synth.gaussian_sem(n, N, seed=11, w_low=0.2, w_high=0.8)
     if kind == "spikes":
         for j in range(0, n, 3):
@@ -69,6 +71,32 @@ def test_corr_hard_columns_match_numpy(eng, kind):
     np.testing.assert_array_equal(np.isnan(C), np.isnan(ref))
     ok = ~np.isnan(ref)
     np.testing.assert_allclose(C[ok], ref[ok], rtol=0, atol=2e-14)
+
+
+@pytest.mark.parametrize("n,N", [(256, 1000), (300, 1200), (513, 4097), (700, 33), (260, 40000), (2000, 10000)])
+def test_corr_crt_matches_numpy(eng, n, N):
+    """The CRT K1 (n >= 256: residue GEMMs, exact integer Gram of the b-bit truncated values,
+    rounded once): ragged tiles (n = 300, 513, 700), a single k-block (N = 33), many slabs
+    (N = 40000), the headline shape. Same tolerance as the digit path."""
+    X = synth.gaussian_sem(n, N, seed=n + 7 * N, w_low=0.1, w_high=0.5)
+    C = eng.corr(X).cpu().numpy()
+    np.testing.assert_allclose(C, np.corrcoef(X.T), rtol=0, atol=2e-14)
+
+
+@pytest.mark.parametrize("n,N", [(300, 1200), (2000, 10000)])
+def test_corr_crt_split_invariant(eng, n, N, monkeypatch):
+    """The CRT result is the correctly rounded exact Gram, so every split-K choice gives the same
+    bits; the digit path (PCG_K1_CRT=0) agrees to within its own truncation."""
+    X = synth.gaussian_sem(n, N, seed=5, w_low=0.1, w_high=0.5)
+    Xd = eng.to_device(X)
+    C0 = eng.corr(Xd).cpu().numpy()
+    for ks in ("1", "3", "7"):
+        monkeypatch.setenv("PCG_K1_CRT_KS", ks)
+        np.testing.assert_array_equal(eng.corr(Xd).cpu().numpy(), C0)
+    monkeypatch.delenv("PCG_K1_CRT_KS")
+    monkeypatch.setenv("PCG_K1_CRT", "0")
+    Cd = eng.corr(Xd).cpu().numpy()
+    np.testing.assert_allclose(Cd, C0, rtol=0, atol=1e-15)
 
 
 @pytest.mark.parametrize("n,N", [(44, 7000), (3, 40000), (130, 8193), (200, 33), (64, 32 * 256 + 5)])
@@ -316,7 +344,8 @@ def test_max_depth_cap(eng):
         np.testing.assert_array_equal(out.removed_level, ref.removed_level)
 
 
-@pytest.mark.parametrize("n,N,world", [(50, 600, 2), (130, 3000, 3), (300, 1200, 8), (2000, 10000, 8)])
+@pytest.mark.parametrize("n,N,world", [(50, 600, 2), (130, 3000, 3), (300, 1200, 8), (700, 5000, 3),
+                                       (2000, 10000, 8)])
 def test_sharded_corr_bitwise_equals_single_gpu(eng, n, N, world):
     """K1 sharded over `world` ranks (each rank's packed share computed here in turn on one
     GPU, then concatenated rank-major as the all-gather would) is bitwise pcg_corr."""
