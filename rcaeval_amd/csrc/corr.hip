@@ -95,15 +95,23 @@ __global__ __launch_bounds__(256) void k_colsum_partial(const double *X, int64_t
     }
 }
 
-// mean_j = (sum of the chunk partials) / N: 64 columns per block, the 4 waves take contiguous
-// quarters of the chunk list (8 loads in flight each), quarters added in order through LDS
-__global__ __launch_bounds__(256) void k_colmean(const double *part, int nchunks, int n, int64_t N, double *mean) {
-    __shared__ double q4[4][64];
-    const int c = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int j = blockIdx.x * 64 + c;
-    const int per = (nchunks + 3) / 4;
-    const int lo = std::min(nchunks, w * per), hi = std::min(nchunks, lo + per);
-    double s = 0.0;
+// digit exponent of column j: 2^e > max_t |fl(X_tj - mean_j)| = max(fl(max - mean), fl(mean - min))
+// (rounding is monotone, so the extremes of the centred column are the centred extremes);
+// K1_NONFINITE marks a column whose mean or range is not finite (numpy: that row and column of
+// C are NaN)
+constexpr int K1_NONFINITE = -100000;
+
+// mean_j = (sum of the chunk partials) / N and, with pmax / pmin, the exponent e_j: 16 columns per
+// block, 16 contiguous partitions of the chunk list per column (8 loads in flight each), the
+// partition sums added in partition order through LDS
+__global__ __launch_bounds__(256) void k_colstats(const double *part, const double *pmax, const double *pmin,
+                                                 int nchunks, int n, int64_t N, double *mean, int *expo) {
+    __shared__ double sq[3][16][17];
+    const int c = threadIdx.x & 15, p = threadIdx.x >> 4;
+    const int j = blockIdx.x * 16 + c;
+    const int per = (nchunks + 15) / 16;
+    const int lo = min(nchunks, p * per), hi = min(nchunks, lo + per);
+    double s = 0.0, mx = -INFINITY, mn = INFINITY;
     if (j < n) {
         int k = lo;
         for (; k + 8 <= hi; k += 8) {
@@ -114,38 +122,29 @@ __global__ __launch_bounds__(256) void k_colmean(const double *part, int nchunks
             for (int u = 0; u < 8; ++u) s += v[u];
         }
         for (; k < hi; ++k) s += part[(int64_t)k * n + j];
+        if (expo)
+            for (k = lo; k < hi; ++k) {
+                mx = fmax(mx, pmax[(int64_t)k * n + j]);
+                mn = fmin(mn, pmin[(int64_t)k * n + j]);
+            }
     }
-    q4[w][c] = s;
+    sq[0][p][c] = s;
+    sq[1][p][c] = mx;
+    sq[2][p][c] = mn;
     __syncthreads();
-    if (w == 0 && j < n) mean[j] = (((q4[0][c] + q4[1][c]) + q4[2][c]) + q4[3][c]) / (double)N;
-}
-
-// digit exponent of column j: 2^e > max_t |fl(X_tj - mean_j)| = max(fl(max - mean), fl(mean - min))
-// (rounding is monotone, so the extremes of the centred column are the centred extremes);
-// K1_NONFINITE marks a column whose mean or range is not finite (numpy: that row and column of
-// C are NaN)
-constexpr int K1_NONFINITE = -100000;
-// (k_colmean's layout: 64 columns per block, the 4 waves take quarters of the chunk list)
-__global__ __launch_bounds__(256) void k_colexp(const double *pmax, const double *pmin, int nchunks, int n,
-                                               const double *mean, int *expo) {
-    __shared__ double q4[2][4][64];
-    const int c = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int j = blockIdx.x * 64 + c;
-    const int per = (nchunks + 3) / 4;
-    const int lo = std::min(nchunks, w * per), hi = std::min(nchunks, lo + per);
-    double mx = -INFINITY, mn = INFINITY;
-    if (j < n)
-        for (int k = lo; k < hi; ++k) {
-            mx = fmax(mx, pmax[(int64_t)k * n + j]);
-            mn = fmin(mn, pmin[(int64_t)k * n + j]);
-        }
-    q4[0][w][c] = mx;
-    q4[1][w][c] = mn;
-    __syncthreads();
-    if (w != 0 || j >= n) return;
-    mx = fmax(fmax(q4[0][0][c], q4[0][1][c]), fmax(q4[0][2][c], q4[0][3][c]));
-    mn = fmin(fmin(q4[1][0][c], q4[1][1][c]), fmin(q4[1][2][c], q4[1][3][c]));
-    const double m = mean[j];
+    if (p != 0 || j >= n) return;
+    double t = 0.0;
+    mx = -INFINITY;
+    mn = INFINITY;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        t += sq[0][q][c];
+        mx = fmax(mx, sq[1][q][c]);
+        mn = fmin(mn, sq[2][q][c]);
+    }
+    const double m = t / (double)N;
+    mean[j] = m;
+    if (!expo) return;
     const double amax = fmax(mx - m, m - mn);
     int e = 0;
     if (!isfinite(m) || !isfinite(amax)) e = K1_NONFINITE;
@@ -502,8 +501,18 @@ __global__ __launch_bounds__(256, 2) void k_xtx_i8(const int8_t *Dg, int CB, int
 constexpr int CRT_KMAX = 24;               // moduli (M < 2^192)
 constexpr int CRT_L = 6;                   // 32-bit limbs of M
 constexpr int CRT_T = 256;                 // output tile
-constexpr int CRT_KB = 2;                  // 32-row k-blocks per LDS stage
-constexpr int CRT_NS = 4;                  // LDS ring stages
+#ifndef PCG_CRT_KB
+#define PCG_CRT_KB 2
+#endif
+#ifndef PCG_CRT_NS
+#define PCG_CRT_NS 4
+#endif
+#ifndef PCG_CRT_PRIO
+#define PCG_CRT_PRIO 0          // s_setprio 1 around the MFMAs of a stage
+#endif
+constexpr int CRT_KB = PCG_CRT_KB;         // 32-row k-blocks per LDS stage
+constexpr int CRT_NS = PCG_CRT_NS;         // LDS ring stages (CRT_NS x CRT_KB x 16 KB <= 160 KB)
+static_assert(CRT_NS * CRT_KB * 16384 <= 160 * 1024 && CRT_NS >= 2 && CRT_NS <= 5, "CRT LDS ring");
 constexpr int CRT_STAGE = CRT_KB * 16384;  // bytes per stage: CRT_KB x (A, B) x 4 column blocks x 2 KB
 constexpr int CRT_MAXKB = 4095;            // k-blocks per slab: 4095 x 32 x 128^2 < 2^31
 constexpr int CRT_UNIT = CRT_T * CRT_T;    // residue bytes per (tile, modulus, slab)
@@ -517,16 +526,100 @@ struct CrtTab {
     float finv[CRT_KMAX];           // fl(1 / m_i)
     double dinv[CRT_KMAX];
     uint32_t wlo[CRT_KMAX], whi[CRT_KMAX];   // bytes 2^(8q) mod m_i, 2^(32 + 8q) mod m_i (q = 0..3)
-    uint32_t Mi[CRT_KMAX][CRT_L];   // M / m_i, little-endian limbs
-    uint32_t M[CRT_L];
+    uint32_t Mi[CRT_KMAX][2 * CRT_L];   // M / m_i, little-endian 16-bit limbs (one per word)
+    uint32_t M[2 * CRT_L];
 };
 
-// s mod m for 0 <= s < 2^20 (fp32 quotient, one correction each way)
+// the CRT sum of one entry: S = sum_i z_i M_i in 16-bit limb accumulators (z_i < 256, limbs
+// < 2^16: full-rate 24-bit multiply-adds, sums < 24 x 2^24), fs = sum_i z_i / m_i
+// (L = tab.L 32-bit limbs, a template parameter: no per-limb branches)
+template <int L>
+struct CrtAcc {
+    uint32_t l[2 * L];
+    float fs;      // |x| / M <= 0.4966 (the plan's 0.01-bit margin): fp32's ~1e-6 error picks q exactly
+};
+
+template <int L>
+__device__ __forceinline__ void crt_acc_init(CrtAcc<L> &a) {
+#pragma unroll
+    for (int l = 0; l < 2 * L; ++l) a.l[l] = 0;
+    a.fs = 0.0f;
+}
+
+template <int L>
+__device__ __forceinline__ void crt_acc_add(CrtAcc<L> &a, uint32_t z, int mi, const CrtTab &tab) {
+    a.fs = fmaf((float)z, tab.finv[mi], a.fs);
+#pragma unroll
+    for (int l = 0; l < 2 * L; ++l) a.l[l] = __umul24(z, tab.Mi[mi][l]) + a.l[l];
+}
+
+// G = x 2^(ei + ej - 2b) with x = S - q M, q = round(fs): |x| < M / 2, rounded to fp64 once
+template <int L>
+__device__ __forceinline__ double crt_value(const CrtAcc<L> &a, const CrtTab &tab, int ei, int ej) {
+    const int32_t qq = (int32_t)floorf(a.fs + 0.5f);
+    uint32_t lim[CRT_L];
+    int32_t carry = 0;
+#pragma unroll
+    for (int l = 0; l < CRT_L; ++l) {          // 16-bit carries (every term < 2^29), two limbs per word
+        int32_t v0 = carry, v1;
+        if (l < L) v0 += (int32_t)a.l[2 * l] - qq * (int32_t)tab.M[2 * l];
+        const uint32_t lo = (uint32_t)v0 & 0xffffu;
+        v1 = v0 >> 16;                          // arithmetic: the sign carries on
+        if (l < L) v1 += (int32_t)a.l[2 * l + 1] - qq * (int32_t)tab.M[2 * l + 1];
+        lim[l] = lo | ((uint32_t)v1 << 16);
+        carry = v1 >> 16;
+    }
+    const bool negx = carry < 0;
+    if (negx) {                                 // magnitude: two's complement
+        uint64_t c = 1;
+#pragma unroll
+        for (int l = 0; l < CRT_L; ++l) {
+            const uint64_t v = (uint64_t)(~lim[l]) + c;
+            lim[l] = (uint32_t)v;
+            c = v >> 32;
+        }
+    }
+    int top = -1;
+#pragma unroll
+    for (int l = 0; l < CRT_L; ++l)
+        if (lim[l]) top = l;
+    if (top < 0) return 0.0;
+    // the top 96 bits (limbs top, top-1, top-2), normalised; the rest as a sticky bit
+    uint32_t l2 = 0, l1 = 0, l0 = 0;
+    bool sticky = false;
+#pragma unroll
+    for (int l = 0; l < CRT_L; ++l) {
+        if (l == top) l2 = lim[l];
+        if (l == top - 1) l1 = lim[l];
+        if (l == top - 2) l0 = lim[l];
+        if (l < top - 2 && lim[l]) sticky = true;
+    }
+    const int sh = __builtin_clz(l2);
+    uint64_t h64 = ((uint64_t)l2 << 32) | l1;
+    uint32_t low = l0;
+    if (sh) {
+        h64 = (h64 << sh) | (low >> (32 - sh));
+        low <<= sh;
+    }
+    if (low || sticky) h64 |= 1;                // below the 53-bit rounding point
+    const double mag = fma((double)(uint32_t)(h64 >> 32), 0x1p32, (double)(uint32_t)h64);
+    const double gv = ldexp(mag, 32 * (top - 1) - sh + ei + ej - 2 * tab.b);
+    return negx ? -gv : gv;
+}
+
+// numpy.corrcoef's order: ((g * 1/(N-1)) / sd_row) / sd_col, clipped (NaN passes)
+__device__ __forceinline__ double corr_of(double g, double scale, double sr, double sc) {
+    double v = (g * scale) / sr;
+    v = v / sc;
+    return v > 1.0 ? 1.0 : (v < -1.0 ? -1.0 : v);
+}
+
+// s mod m for 0 <= s < 2^20, all in fp32 (exact integers; the quotient off by at most one each way)
 __device__ __forceinline__ uint32_t crt_mod(uint32_t s, int m, float finv) {
-    const float q = floorf((float)s * finv);
-    int r = (int)s - (int)q * m;
-    r += r < 0 ? m : 0;
-    r -= r >= m ? m : 0;
+    const float x = (float)s, fm = (float)m;
+    float r = fmaf(floorf(x * finv), -fm, x);
+    r = r < 0.0f ? r + fm : r;
+    r = r >= fm ? r - fm : r;
     return (uint32_t)r;
 }
 
@@ -652,16 +745,20 @@ __global__ __launch_bounds__(512, 1) void k_xtx_crt(const int8_t *R, int TB, int
     const int8_t *Rm = R + (int64_t)mi * plane;
     const int8_t *srcA = Rm + (int64_t)(bi * 4 + (tid >> 7)) * TB * 2048 + (tid & 127) * 16;
     const int8_t *srcB = Rm + (int64_t)(bj * 4 + (tid >> 7)) * TB * 2048 + (tid & 127) * 16;
-    const int ns = (tb1 - tb0) / CRT_KB;       // slabs hold whole stages (kb and TB even)
+    const int nkb = tb1 - tb0;
+    const int ns = (nkb + CRT_KB - 1) / CRT_KB;
     auto issue = [&](int sidx) {
         if (sidx >= ns) return;
         unsigned char *dst = smem + (sidx % CRT_NS) * CRT_STAGE + w * 1024;
-        const int64_t tb = (int64_t)(tb0 + sidx * CRT_KB);
 #pragma unroll
-        for (int q = 0; q < 2 * CRT_KB; ++q)
+        for (int q = 0; q < 2 * CRT_KB; ++q) {
+            // a partial last stage re-reads its last k-block (the DMA count per stage stays fixed
+            // for the counted waits; those k-blocks are not multiplied)
+            const int64_t tb = tb0 + min(sidx * CRT_KB + (q >> 1), nkb - 1);
             __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void *)(((q & 1) ? srcB : srcA) + (tb + (q >> 1)) * 2048),
+                (const __attribute__((address_space(1))) void *)(((q & 1) ? srcB : srcA) + tb * 2048),
                 (__attribute__((address_space(3))) void *)(dst + q * 8192), 16, 0, 0);
+        }
     };
 #pragma unroll
     for (int sidx = 0; sidx < CRT_NS - 1; ++sidx) issue(sidx);
@@ -671,7 +768,8 @@ __global__ __launch_bounds__(512, 1) void k_xtx_crt(const int8_t *R, int TB, int
         // stage sidx landed (this thread's DMAs; the later stages stay in flight), then the
         // barrier: every wave's DMAs of sidx are in LDS and every wave is done reading sidx - 1
         const int ahead = min(CRT_NS - 2, ns - 1 - sidx);
-        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * 2 * CRT_KB) : "memory");
+        if (ahead >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * 2 * CRT_KB) : "memory");
+        else if (ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * 2 * CRT_KB) : "memory");
         else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * CRT_KB) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -686,16 +784,22 @@ __global__ __launch_bounds__(512, 1) void k_xtx_crt(const int8_t *R, int TB, int
             for (int b = 0; b < 2; ++b)
                 bf[sl][b] = *reinterpret_cast<const v4i *>(fb + off + kk * 16384 + b * 1024);
         };
+        const int cnt = min(CRT_KB, nkb - sidx * CRT_KB);
         frag(0, 0);
+        if (PCG_CRT_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int kk = 0; kk < CRT_KB; ++kk) {
-            if (kk + 1 < CRT_KB) frag(kk + 1, (kk + 1) & 1);
+            if (kk < cnt) {
+                if (kk + 1 < CRT_KB && kk + 1 < cnt) frag(kk + 1, (kk + 1) & 1);
 #pragma unroll
-            for (int a = 0; a < 4; ++a)
+                for (int a = 0; a < 4; ++a)
 #pragma unroll
-                for (int b = 0; b < 2; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[kk & 1][a], bf[kk & 1][b], acc[a][b], 0, 0, 0);
+                    for (int b = 0; b < 2; ++b)
+                        acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[kk & 1][a], bf[kk & 1][b], acc[a][b], 0,
+                                                                          0, 0);
+            }
         }
+        if (PCG_CRT_PRIO) __builtin_amdgcn_s_setprio(0);
     }
     // epilogue: the slab's sums mod m as bytes, 16 per lane per MFMA tile (one 16-byte store)
     const int m = tab.m[mi];
@@ -725,11 +829,57 @@ __global__ __launch_bounds__(512, 1) void k_xtx_crt(const int8_t *R, int TB, int
         }
 }
 
-// the CRT rebuild: one thread = 4 entries (one 32-bit word of a 16-byte lane word of the units:
-// the same column j, rows 8 apart... see the lane order above); residues summed over the ks slabs
-// in u16 lanes, G_ij (i <= j) written to the upper triangle of G
+// byte offset of entry (li, lj) of a unit (the lane order of k_xtx_crt's epilogue)
+__device__ __forceinline__ int crt_unit_offset(int li, int lj) {
+    const int wr = li >> 7, a = (li >> 5) & 3, rr = li & 31;
+    const int hh = (rr >> 2) & 1, q = (rr & 3) | ((rr >> 3) << 2);
+    const int wc = lj >> 6, b = (lj >> 5) & 1, r = lj & 31;
+    return ((((wr * 4 + wc) * 4 + a) * 2 + b) * 64 + r + 32 * hh) * 16 + q;
+}
+
+// sd_i = sqrt(G_ii / (N - 1)) from the diagonal entries' residues (one thread per i; every
+// residue load issued before the first use)
+template <int L>
+__global__ __launch_bounds__(256) void k_crt_diag(const uint8_t *Rs, int T, int ntiles, int ks, CrtTab tab,
+                                                 const int *expo, int n, double scale, double *sd) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int bi = i / CRT_T;
+    const int t = bi * T - bi * (bi - 1) / 2;          // tile (bi, bi), row-major upper triangle
+    const int ei = expo[i];
+    if (ei == K1_NONFINITE) {
+        sd[i] = NAN;
+        return;
+    }
+    const int k = tab.k;
+    const int64_t ustride = (int64_t)ntiles * CRT_UNIT;
+    const uint8_t *src = Rs + (int64_t)t * CRT_UNIT + crt_unit_offset(i % CRT_T, i % CRT_T);
+    uint32_t sv[CRT_KMAX];
+#pragma unroll
+    for (int mi = 0; mi < CRT_KMAX; ++mi) sv[mi] = 0;
+    for (int s = 0; s < ks; ++s) {
+        uint32_t b[CRT_KMAX];             // unconditional loads (see k_crt_finish)
+#pragma unroll
+        for (int mi = 0; mi < CRT_KMAX; ++mi) b[mi] = src[((int64_t)s * k + min(mi, k - 1)) * ustride];
+#pragma unroll
+        for (int mi = 0; mi < CRT_KMAX; ++mi) sv[mi] += b[mi];
+    }
+    CrtAcc<L> acc;
+    crt_acc_init(acc);
+#pragma unroll
+    for (int mi = 0; mi < CRT_KMAX; ++mi)
+        if (mi < k) crt_acc_add(acc, crt_mod(__umul24(sv[mi], (uint32_t)tab.y[mi]), tab.m[mi], tab.finv[mi]), mi, tab);
+    sd[i] = sqrt(crt_value(acc, tab, ei, ei) * scale);
+}
+
+// the CRT rebuild fused with the normalisation: one thread = 4 entries (one 32-bit word of a
+// 16-byte lane word of the units: the same column j, 4 consecutive rows i); residues summed over
+// the ks slabs in u16 lanes, moduli outermost (each modulus' constants read once, 4 independent
+// chains); writes C_ij and its mirror C_ji, each in numpy's division order
+template <int L>
 __global__ __launch_bounds__(256) void k_crt_finish(const uint8_t *Rs, int T, int ntiles, int ks, CrtTab tab,
-                                                   const int *expo, int n, double *G, int64_t ldg) {
+                                                   const int *expo, int n, const double *sd, double scale, double *C,
+                                                   int64_t ldc) {
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int t = (int)(gid >> 14), rem = (int)((gid >> 2) & 4095), g = (int)(gid & 3);
     if (t >= ntiles) return;
@@ -746,93 +896,49 @@ __global__ __launch_bounds__(256) void k_crt_finish(const uint8_t *Rs, int T, in
     const int ej = expo[j];
     const int64_t ustride = (int64_t)ntiles * CRT_UNIT;          // next modulus
     const uint8_t *src = Rs + (int64_t)t * CRT_UNIT + rem * 16 + 4 * g;
-    // moduli outermost: each modulus' constants are read once for the 4 entries (4 independent
-    // accumulation chains); S = sum_i z_i M_i in 64-bit limb accumulators, fs = sum_i z_i / m_i
-    uint64_t acc[4][CRT_L] = {};
-    double fs[4] = {0.0, 0.0, 0.0, 0.0};
+    // the ks slab bytes of the 4 entries, summed in u16 lanes; every load issued before the first use
+    uint32_t se[CRT_KMAX], so[CRT_KMAX];
+#pragma unroll
+    for (int mi = 0; mi < CRT_KMAX; ++mi) se[mi] = so[mi] = 0;
+    for (int s = 0; s < ks; ++s) {
+        // unconditional loads (moduli past k re-read modulus k - 1 and are never used): a guarded
+        // load would be a branch with its own vmcnt(0)
+        uint32_t wd[CRT_KMAX];
+#pragma unroll
+        for (int mi = 0; mi < CRT_KMAX; ++mi)
+            wd[mi] = *reinterpret_cast<const uint32_t *>(src + ((int64_t)s * k + min(mi, k - 1)) * ustride);
+#pragma unroll
+        for (int mi = 0; mi < CRT_KMAX; ++mi) {
+            se[mi] += wd[mi] & 0x00ff00ffu;
+            so[mi] += (wd[mi] >> 8) & 0x00ff00ffu;
+        }
+    }
+    CrtAcc<L> acc[4];
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) crt_acc_init(acc[q4]);
 #pragma unroll
     for (int mi = 0; mi < CRT_KMAX; ++mi) {
         if (mi >= k) continue;
-        uint32_t se = 0, so = 0;            // the ks slab bytes of the 4 entries, summed in u16 lanes
-        for (int s = 0; s < ks; ++s) {
-            const uint32_t wd = *reinterpret_cast<const uint32_t *>(src + ((int64_t)s * k + mi) * ustride);
-            se += wd & 0x00ff00ffu;
-            so += (wd >> 8) & 0x00ff00ffu;
-        }
         const int m = tab.m[mi];
         const float fi = tab.finv[mi];
         const uint32_t y = (uint32_t)tab.y[mi];
-        const double dinv = tab.dinv[mi];
 #pragma unroll
         for (int q4 = 0; q4 < 4; ++q4) {
-            const uint32_t sv = (((q4 & 1) ? so : se) >> (16 * (q4 >> 1))) & 0xffffu;   // < ks x 255
-            const uint32_t z = crt_mod(sv * y, m, fi);     // r M_i^-1 mod m, r = sv mod m: s y < 2^20
-            fs[q4] = fma((double)z, dinv, fs[q4]);
-#pragma unroll
-            for (int l = 0; l < CRT_L; ++l)
-                if (l < tab.L) acc[q4][l] += (uint64_t)z * tab.Mi[mi][l];
+            const uint32_t sv = (((q4 & 1) ? so[mi] : se[mi]) >> (16 * (q4 >> 1))) & 0xffffu;   // < ks x 255
+            // z = r M_i^-1 mod m with r = sv mod m: one reduction of sv y < 2^20
+            crt_acc_add(acc[q4], crt_mod(__umul24(sv, y), m, fi), mi, tab);
         }
     }
+    const double sj = sd[j];
 #pragma unroll
     for (int q4 = 0; q4 < 4; ++q4) {
         const int i = ibase + q4;
         if (i > j) break;
         const int ei = expo[i];
-        double gv;
-        if (ei == K1_NONFINITE || ej == K1_NONFINITE) {
-            gv = NAN;
-        } else {
-            const int64_t qq = (int64_t)floor(fs[q4] + 0.5);     // x = S - q M in [-M/2, M/2)
-            uint32_t lim[CRT_L];
-            int64_t carry = 0;
-#pragma unroll
-            for (int l = 0; l < CRT_L; ++l) {
-                int64_t v = carry;
-                if (l < tab.L) v += (int64_t)acc[q4][l] - qq * (int64_t)tab.M[l];
-                lim[l] = (uint32_t)v;
-                carry = v >> 32;                              // arithmetic: the sign carries on
-            }
-            const bool negx = carry < 0;
-            if (negx) {                                       // magnitude: two's complement
-                uint64_t c = 1;
-#pragma unroll
-                for (int l = 0; l < CRT_L; ++l) {
-                    const uint64_t v = (uint64_t)(~lim[l]) + c;
-                    lim[l] = (uint32_t)v;
-                    c = v >> 32;
-                }
-            }
-            int top = -1;
-#pragma unroll
-            for (int l = 0; l < CRT_L; ++l)
-                if (lim[l]) top = l;
-            if (top < 0) {
-                gv = 0.0;
-            } else {
-                // the top 96 bits (limbs top, top-1, top-2), normalised; the rest as a sticky bit
-                uint32_t l2 = 0, l1 = 0, l0 = 0;
-                bool sticky = false;
-#pragma unroll
-                for (int l = 0; l < CRT_L; ++l) {
-                    if (l == top) l2 = lim[l];
-                    if (l == top - 1) l1 = lim[l];
-                    if (l == top - 2) l0 = lim[l];
-                    if (l < top - 2 && lim[l]) sticky = true;
-                }
-                const int sh = __builtin_clz(l2);
-                uint64_t h64 = ((uint64_t)l2 << 32) | l1;
-                uint32_t low = l0;
-                if (sh) {
-                    h64 = (h64 << sh) | (low >> (32 - sh));
-                    low <<= sh;
-                }
-                if (low || sticky) h64 |= 1;                  // below the 53-bit rounding point
-                const double mag = fma((double)(uint32_t)(h64 >> 32), 0x1p32, (double)(uint32_t)h64);
-                gv = ldexp(mag, 32 * (top - 1) - sh + ei + ej - 2 * tab.b);
-                if (negx) gv = -gv;
-            }
-        }
-        G[(int64_t)i * ldg + j] = gv;
+        const double gv = (ei == K1_NONFINITE || ej == K1_NONFINITE) ? NAN : crt_value(acc[q4], tab, ei, ej);
+        const double si = sd[i];
+        C[(int64_t)i * ldc + j] = corr_of(gv, scale, si, sj);
+        if (i != j) C[(int64_t)j * ldc + i] = corr_of(gv, scale, sj, si);
     }
 }
 
@@ -915,16 +1021,22 @@ bool crt_plan(int n, int64_t N, CrtPlan &p) {
     t.L = (int)std::floor(lm / 32.0) + 1;      // M < 2^(32 L - 1)... at least one spare bit
     if (lm > 32.0 * t.L - 1.0) ++t.L;
     if (t.L > CRT_L) return false;
-    memcpy(t.M, M, sizeof(M));
+    for (int l = 0; l < CRT_L; ++l) {
+        t.M[2 * l] = M[l] & 0xffffu;
+        t.M[2 * l + 1] = M[l] >> 16;
+    }
     for (int i = 0; i < k; ++i) {
         const uint32_t m = (uint32_t)kCrtModuli[i];
         t.m[i] = (int)m;
         t.finv[i] = 1.0f / (float)m;
         t.dinv[i] = 1.0 / (double)m;
-        const uint32_t rem = big_div_small(M, CRT_L, m, t.Mi[i]);
-        (void)rem;                              // 0: m divides M
-        uint32_t mq[CRT_L];
-        const uint32_t mim = big_div_small(t.Mi[i], CRT_L, m, mq);   // (M / m) mod m
+        uint32_t Mi32[CRT_L], mq[CRT_L];
+        big_div_small(M, CRT_L, m, Mi32);        // exact: m divides M
+        for (int l = 0; l < CRT_L; ++l) {
+            t.Mi[i][2 * l] = Mi32[l] & 0xffffu;
+            t.Mi[i][2 * l + 1] = Mi32[l] >> 16;
+        }
+        const uint32_t mim = big_div_small(Mi32, CRT_L, m, mq);      // (M / m) mod m
         t.y[i] = 0;
         for (uint32_t y = 1; y < m; ++y)
             if ((mim * y) % m == 1) { t.y[i] = (int)y; break; }
@@ -990,10 +1102,20 @@ void crt_gemm(pcg_handle *h, const CrtPlan &p, const int8_t *R, int64_t u0, int6
                        plane, p.T, p.ntiles, p.tab.k, p.kb, p.tab, u0, nu, out);
 }
 
-void crt_finish(pcg_handle *h, const CrtPlan &p, const uint8_t *Rs, const int *expo, int nn, double *G, int64_t ldg) {
+// C from the units' residues: the diagonal (sd) first, then every upper entry and its mirror
+void crt_finish(pcg_handle *h, const CrtPlan &p, const uint8_t *Rs, const int *expo, int nn, int64_t N, double *sd,
+                double *C, int64_t ldc) {
+    const double scale = 1.0 / (double)(N - 1);
     const int64_t threads = (int64_t)p.ntiles * 16384;
-    hipLaunchKernelGGL(k_crt_finish, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, h->stream, Rs, p.T,
-                       p.ntiles, p.ks, p.tab, expo, nn, G, ldg);
+#define CRT_LAUNCH(L_)                                                                                          \
+    hipLaunchKernelGGL(k_crt_diag<L_>, dim3((unsigned)((nn + 255) / 256)), dim3(256), 0, h->stream, Rs, p.T,     \
+                       p.ntiles, p.ks, p.tab, expo, nn, scale, sd);                                              \
+    hipLaunchKernelGGL(k_crt_finish<L_>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, h->stream, Rs, p.T, \
+                       p.ntiles, p.ks, p.tab, expo, nn, (const double *)sd, scale, C, ldc)
+    if (p.tab.L <= 4) { CRT_LAUNCH(4); }
+    else if (p.tab.L == 5) { CRT_LAUNCH(5); }
+    else { CRT_LAUNCH(6); }
+#undef CRT_LAUNCH
 }
 
 // digits of X (all columns) into h->k1_digits; returns the plane geometry
@@ -1173,13 +1295,10 @@ int column_means(pcg_handle *h, const double *X, int64_t N, int nn, int64_t ldx,
     double *pmin = expo_out ? pmax + (size_t)nn * nchunks : nullptr;
     hipLaunchKernelGGL(k_colsum_partial, dim3((nn + 255) / 256, nchunks), dim3(256), 0, h->stream, X, N, nn, ldx,
                        part, pmax, pmin);
-    hipLaunchKernelGGL(k_colmean, dim3((nn + 63) / 64), dim3(256), 0, h->stream, part, nchunks, nn, N, mean);
-    if (expo_out) {
-        int *expo = reinterpret_cast<int *>(mean + nn);
-        hipLaunchKernelGGL(k_colexp, dim3((nn + 63) / 64), dim3(256), 0, h->stream, (const double *)pmax,
-                           (const double *)pmin, nchunks, nn, (const double *)mean, expo);
-        *expo_out = expo;
-    }
+    int *expo = expo_out ? reinterpret_cast<int *>(mean + nn) : nullptr;
+    hipLaunchKernelGGL(k_colstats, dim3((nn + 15) / 16), dim3(256), 0, h->stream, (const double *)part,
+                       (const double *)pmax, (const double *)pmin, nchunks, nn, N, mean, expo);
+    if (expo_out) *expo_out = expo;
     *mean_out = mean;
     return PCG_OK;
 }
@@ -1296,13 +1415,10 @@ extern "C" int pcg_corr_shard_finish(pcg_handle *h, const double *gathered, int6
     const double scale = 1.0 / (double)(N - 1);
     CrtPlan cp;
     if (crt_plan(nn, N, cp)) {     // gathered = every unit in canonical order; exponents from pcg_corr_shard
-        if (!pcg_ensure(h, h->pr_scratch, sizeof(double) * (size_t)nn * nn))
+        if (!pcg_ensure(h, h->pr_scratch, sizeof(double) * (size_t)(nn + 32)))
             return pcg_fail(h, PCG_ERR_OOM, "pcg_corr_shard_finish scratch");
-        double *G = (double *)h->pr_scratch.p;
-        crt_finish(h, cp, (const uint8_t *)gathered, colmean_expo(h, N, nn), nn, G, nn);
-        const int T64 = (nn + NT - 1) / NT;
-        hipLaunchKernelGGL(k_normalize_tiles, dim3(T64 * (T64 + 1) / 2), dim3(256), 0, h->stream, (const double *)G,
-                           (int64_t)nn, (int64_t)0, 1, C, ldc, nn, scale);
+        crt_finish(h, cp, (const uint8_t *)gathered, colmean_expo(h, N, nn), nn, N, (double *)h->pr_scratch.p, C,
+                   ldc);
         PCG_HIP(h, hipGetLastError());
         PCG_HIP(h, hipStreamSynchronize(h->stream));
         return PCG_OK;
@@ -1337,16 +1453,13 @@ int pcg_corr_launch(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_
         const int8_t *R = nullptr;
         rc = crt_residues(h, cp, X, N, nn, ldx, mean, expo, &R);
         if (rc) return rc;
-        const size_t gbytes = sizeof(double) * (size_t)nn * nn;
-        if (!pcg_ensure(h, h->pr_scratch, gbytes + (size_t)cp.units * CRT_UNIT))
+        const size_t sbytes = sizeof(double) * (size_t)(nn + 32);
+        if (!pcg_ensure(h, h->pr_scratch, sbytes + (size_t)cp.units * CRT_UNIT))
             return pcg_fail(h, PCG_ERR_OOM, "pcg_corr CRT scratch");
-        double *G = (double *)h->pr_scratch.p;
-        uint8_t *Rs = (uint8_t *)h->pr_scratch.p + gbytes;
+        double *sd = (double *)h->pr_scratch.p;
+        uint8_t *Rs = (uint8_t *)h->pr_scratch.p + sbytes;
         crt_gemm(h, cp, R, 0, cp.units, Rs);
-        crt_finish(h, cp, Rs, expo, nn, G, nn);
-        const int T64 = (nn + NT - 1) / NT;
-        hipLaunchKernelGGL(k_normalize_tiles, dim3(T64 * (T64 + 1) / 2), dim3(256), 0, h->stream, (const double *)G,
-                           (int64_t)nn, (int64_t)0, 1, C, ldc, nn, scale);
+        crt_finish(h, cp, Rs, expo, nn, N, sd, C, ldc);
         PCG_HIP(h, hipGetLastError());
         return PCG_OK;
     }
