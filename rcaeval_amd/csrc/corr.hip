@@ -327,12 +327,13 @@ __device__ __forceinline__ void tile_of_super(int t, int T, int &bi, int &bj) {
     bi = bj = 0;
 }
 
-// digit planes, blocked for the GEMM: Dg[((p * CB + cb) * TB + tb) * 2048 + c * 32 + tt] is digit
-// p of column 64 cb + c at row 32 tb + tt (64 x 32-byte blocks, each 2 KB contiguous); rows past
-// N and columns past n are zero. One block: 64 columns x 64 rows, transposed through LDS.
+// digit planes, blocked for the GEMM: Dg[((p * CB + cb) * TB + tb) * 2048 + (tt >> 4) * 1024 + c * 16
+// + (tt & 15)] is digit p of column 64 cb + c at row 32 tb + tt (2 KB blocks, k-half major like the
+// CRT residue planes: conflict-free fragment reads); rows past N and columns past n are zero. One
+// block: 64 columns x 64 rows, transposed through LDS.
 __global__ __launch_bounds__(256) void k_digits(const double *X, int64_t N, int n, int64_t ldx, const double *mean,
                                                const int *expo, int CB, int TB, int8_t *Dg) {
-    __shared__ __attribute__((aligned(16))) int8_t tile[K1_DIG][2][64][K1_TB];   // [p][t-half][col][t]
+    __shared__ __attribute__((aligned(16))) int8_t tile[K1_DIG][2][2][64][16];   // [p][tb][k-half][col][t]
     const int cb = blockIdx.x, t64 = blockIdx.y;
     const int c = threadIdx.x & 63, r4 = threadIdx.x >> 6;
     const int j = cb * 64 + c;
@@ -358,7 +359,7 @@ __global__ __launch_bounds__(256) void k_digits(const double *X, int64_t N, int 
             y[i] -= d;
             pk[i >> 2] |= ((int)d & 255) << (8 * (i & 3));
         }
-        *reinterpret_cast<v4i *>(&tile[p][r4 >> 1][c][16 * (r4 & 1)]) = pk;
+        *reinterpret_cast<v4i *>(&tile[p][r4 >> 1][r4 & 1][c][0]) = pk;
     }
     __syncthreads();
     // 9 x 2 blocks of 2 KB out: 16-byte stores, consecutive threads on consecutive addresses
@@ -440,10 +441,10 @@ __global__ __launch_bounds__(256, 2) void k_xtx_i8(const int8_t *Dg, int CB, int
         v4i bq[K1_DIG];
 #pragma unroll
         for (int q = 0; q < K1_DIG; ++q)
-            bq[q] = *reinterpret_cast<const v4i *>(&st[buf][K1_DIG + q][(wc + r) * 32 + 16 * hh]);
+            bq[q] = *reinterpret_cast<const v4i *>(&st[buf][K1_DIG + q][hh * 1024 + (wc + r) * 16]);
 #pragma unroll
         for (int p = 0; p < K1_DIG; ++p) {
-            const v4i ap = *reinterpret_cast<const v4i *>(&st[buf][p][(wr + r) * 32 + 16 * hh]);
+            const v4i ap = *reinterpret_cast<const v4i *>(&st[buf][p][hh * 1024 + (wr + r) * 16]);
 #pragma unroll
             for (int q = 0; q < K1_DIG - p; ++q)         // level p + q (0-based) <= K1_DIG - 1
                 acc[p + q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(ap, bq[q], acc[p + q], 0, 0, 0);
@@ -623,9 +624,12 @@ __device__ __forceinline__ uint32_t crt_mod(uint32_t s, int m, float finv) {
     return (uint32_t)r;
 }
 
-// residue planes, blocked like the digit planes: R[((mi * CBp + cb) * TB + tb) * 2048 + c * 32 + tt]
-// = a mod m_i (balanced, int8) of column 64 cb + c at row 32 tb + tt; zero past n and N. One
-// thread = 16 rows of one column, a wave = 32 columns x 2 halves = one contiguous 1 KB store.
+// residue planes in 2 KB blocks of 64 columns x 32 rows, k-half major:
+// R[((mi * CBp + cb) * TB + tb) * 2048 + (tt >> 4) * 1024 + c * 16 + (tt & 15)] = a mod m_i
+// (balanced, int8) of column 64 cb + c at row 32 tb + tt; zero past n and N. A lane's MFMA
+// fragment (16 rows of one column) is 16 contiguous bytes and a half-wave's 32 columns are one
+// contiguous 512 B (no LDS bank conflicts; the column-major [c][32] form conflicts 2-way). One
+// thread = 16 rows of one column; a wave stores two contiguous 512 B runs.
 __global__ __launch_bounds__(256) void k_residues(const double *X, int64_t N, int n, int64_t ldx, const double *mean,
                                                  const int *expo, int CBp, int TB, CrtTab tab, int8_t *R) {
     const int cb = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -648,7 +652,7 @@ __global__ __launch_bounds__(256) void k_residues(const double *X, int64_t N, in
         sg[i] = v < 0.0 ? -1.0f : 1.0f;
     }
     const int64_t plane = (int64_t)CBp * TB * 2048;
-    int8_t *dst = R + ((int64_t)cb * TB + tb) * 2048 + c * 32 + 16 * half;
+    int8_t *dst = R + ((int64_t)cb * TB + tb) * 2048 + half * 1024 + c * 16;
     // bytes: the low byte of each of 4 words packed into one word (v_perm_b32)
     auto pack4 = [](uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) {
         const uint32_t w01 = __builtin_amdgcn_perm(b1, b0, 0x0c0c0400u);
@@ -739,8 +743,8 @@ __global__ __launch_bounds__(512, 1) void k_xtx_crt(const int8_t *R, int TB, int
 
     // staging by LDS-DMA (global_load_lds_dwordx4, no VGPR round trip): a stage is CRT_KB k-blocks,
     // word o = q * 512 + tid of a stage is k-block q >> 1, side q & 1 (A = tile row bi, B = tile
-    // column bj), column block tid >> 7 of the side, 16-byte word tid & 127 -- lane-linear per wave,
-    // as the DMA writes. CRT_NS stages in a ring, CRT_NS - 1 in flight across the raw barriers
+    // column bj), column block tid >> 7 of the side, 16-byte word tid & 127 of its 2 KB block --
+    // lane-linear per wave, as the DMA writes; the block keeps the planes' k-half-major order. CRT_NS stages in a ring, CRT_NS - 1 in flight across the raw barriers
     // (counted vmcnt, never a __syncthreads() that would drain them).
     const int8_t *Rm = R + (int64_t)mi * plane;
     const int8_t *srcA = Rm + (int64_t)(bi * 4 + (tid >> 7)) * TB * 2048 + (tid & 127) * 16;
@@ -762,8 +766,8 @@ __global__ __launch_bounds__(512, 1) void k_xtx_crt(const int8_t *R, int TB, int
     };
 #pragma unroll
     for (int sidx = 0; sidx < CRT_NS - 1; ++sidx) issue(sidx);
-    const unsigned char *fa = smem + (2 * wr * 2048 + r * 32 + 16 * hh);
-    const unsigned char *fb = smem + (8192 + wc * 2048 + r * 32 + 16 * hh);
+    const unsigned char *fa = smem + (2 * wr * 2048 + hh * 1024 + r * 16);
+    const unsigned char *fb = smem + (8192 + wc * 2048 + hh * 1024 + r * 16);
     for (int sidx = 0; sidx < ns; ++sidx) {
         // stage sidx landed (this thread's DMAs; the later stages stay in flight), then the
         // barrier: every wave's DMAs of sidx are in LDS and every wave is done reading sidx - 1
@@ -779,10 +783,10 @@ __global__ __launch_bounds__(512, 1) void k_xtx_crt(const int8_t *R, int TB, int
         auto frag = [&](int kk, int sl) {
 #pragma unroll
             for (int a = 0; a < 4; ++a)
-                af[sl][a] = *reinterpret_cast<const v4i *>(fa + off + kk * 16384 + (a >> 1) * 2048 + (a & 1) * 1024);
+                af[sl][a] = *reinterpret_cast<const v4i *>(fa + off + kk * 16384 + (a >> 1) * 2048 + (a & 1) * 512);
 #pragma unroll
             for (int b = 0; b < 2; ++b)
-                bf[sl][b] = *reinterpret_cast<const v4i *>(fb + off + kk * 16384 + b * 1024);
+                bf[sl][b] = *reinterpret_cast<const v4i *>(fb + off + kk * 16384 + b * 512);
         };
         const int cnt = min(CRT_KB, nkb - sidx * CRT_KB);
         frag(0, 0);
