@@ -503,10 +503,13 @@ constexpr int CRT_KMAX = 24;               // moduli (M < 2^192)
 constexpr int CRT_L = 6;                   // 32-bit limbs of M
 constexpr int CRT_T = 256;                 // output tile
 #ifndef PCG_CRT_KB
-#define PCG_CRT_KB 2
+#define PCG_CRT_KB 4
 #endif
 #ifndef PCG_CRT_NS
-#define PCG_CRT_NS 4
+#define PCG_CRT_NS 2
+#endif
+#ifndef PCG_CRT_SCHED
+#define PCG_CRT_SCHED 1         // interleave fragment reads with MFMAs (sched_group_barrier)
 #endif
 #ifndef PCG_CRT_PRIO
 #define PCG_CRT_PRIO 0          // s_setprio 1 around the MFMAs of a stage
@@ -794,13 +797,23 @@ __global__ __launch_bounds__(512, 1) void k_xtx_crt(const int8_t *R, int TB, int
 #pragma unroll
         for (int kk = 0; kk < CRT_KB; ++kk) {
             if (kk < cnt) {
-                if (kk + 1 < CRT_KB && kk + 1 < cnt) frag(kk + 1, (kk + 1) & 1);
+                const bool nxt = kk + 1 < CRT_KB && kk + 1 < cnt;
+                if (nxt) frag(kk + 1, (kk + 1) & 1);
 #pragma unroll
                 for (int a = 0; a < 4; ++a)
 #pragma unroll
                     for (int b = 0; b < 2; ++b)
                         acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[kk & 1][a], bf[kk & 1][b], acc[a][b], 0,
                                                                           0, 0);
+                if (PCG_CRT_SCHED && nxt) {
+                    // interleave the 6 fragment reads of k-block kk + 1 with the 8 MFMAs of kk
+#pragma unroll
+                    for (int u = 0; u < 6; ++u) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // 1 DS read
+                    }
+                    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                }
             }
         }
         if (PCG_CRT_PRIO) __builtin_amdgcn_s_setprio(0);

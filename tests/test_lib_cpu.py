@@ -311,3 +311,59 @@ def test_page_rank_preprocess_table_equals_visit_loop():
                 if rule[1] is not None:
                     ref[b, a] = rule[1]
         np.testing.assert_array_equal(page_rank_preprocess(adj), ref)
+
+
+def _crt_units_host(n, N):
+    """corr.hip crt_plan restated: (moduli k, split-K slabs ks) of the CRT K1, or None."""
+    import bench
+    km = bench.k1_crt_moduli(n, N)
+    if km is None:
+        return None
+    k = km[0]
+    T = (n + 255) // 256
+    ntiles = T * (T + 1) // 2
+    TB = (N + 63) // 64 * 2
+    best, cost_best = 1, None
+    for ks in range(1, 17):
+        kb = -(-TB // ks)
+        kb = -(-kb // 4) * 4
+        if -(-TB // kb) != ks or kb > 4095:
+            continue
+        U = ntiles * k * ks
+        cost = ((U + 255) // 256) * kb * 0.3 + U * 0.026
+        if cost_best is None or cost < cost_best:
+            best, cost_best = ks, cost
+    return k, best, ntiles
+
+
+@pytest.mark.parametrize("n,N,world", [(2000, 10000, 1), (2000, 10000, 8), (300, 1200, 3), (256, 40000, 2),
+                                       (100, 5000, 2), (255, 1000, 1)])
+def test_corr_shard_bytes_follow_the_k1_plan(n, N, world):
+    """pcg_corr_shard_bytes (host-only): the CRT path (n >= 256) shares (tile, modulus, slab)
+    residue units of 64 KiB; below it, the digit path's packed rows x n doubles."""
+    from rcaeval_amd import _lib
+    lib = _lib.load()
+    got = ctypes.c_int64()
+    assert lib.pcg_corr_shard_bytes(n, N, world, ctypes.byref(got)) == 0
+    plan = _crt_units_host(n, N)
+    if plan is None:
+        rows = ctypes.c_int64()
+        assert lib.pcg_corr_shard_rows(n, world, ctypes.byref(rows)) == 0
+        assert got.value == rows.value * n * 8
+    else:
+        k, ks, ntiles = plan
+        units = ntiles * k * ks
+        assert got.value == -(-units // world) * 65536
+    if (n, N) == (2000, 10000):
+        assert plan[:2] == (17, 2)          # the headline: 17 moduli (b = 59), 2 slabs
+
+
+def test_corr_crt_path_switch(monkeypatch):
+    """PCG_K1_CRT=0 routes n >= 256 back to the digit path's row share."""
+    from rcaeval_amd import _lib
+    lib = _lib.load()
+    got, rows = ctypes.c_int64(), ctypes.c_int64()
+    monkeypatch.setenv("PCG_K1_CRT", "0")
+    assert lib.pcg_corr_shard_bytes(2000, 10000, 4, ctypes.byref(got)) == 0
+    assert lib.pcg_corr_shard_rows(2000, 4, ctypes.byref(rows)) == 0
+    assert got.value == rows.value * 2000 * 8
