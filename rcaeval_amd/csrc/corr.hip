@@ -520,6 +520,7 @@ static_assert(CRT_NS * CRT_KB * 16384 <= 160 * 1024 && CRT_NS >= 2 && CRT_NS <= 
 constexpr int CRT_STAGE = CRT_KB * 16384;  // bytes per stage: CRT_KB x (A, B) x 4 column blocks x 2 KB
 constexpr int CRT_MAXKB = 4095;            // k-blocks per slab: 4095 x 32 x 128^2 < 2^31
 constexpr int CRT_UNIT = CRT_T * CRT_T;    // residue bytes per (tile, modulus, slab)
+constexpr int CRT_MAXG = 4;                // modulus groups overlapping residues and GEMM (handle events)
 static const int kCrtModuli[CRT_KMAX] = {256, 255, 253, 251, 247, 241, 239, 233, 229, 227, 223, 217,
                                          211, 199, 197, 193, 191, 181, 179, 173, 167, 163, 157, 151};
 
@@ -634,7 +635,8 @@ __device__ __forceinline__ uint32_t crt_mod(uint32_t s, int m, float finv) {
 // contiguous 512 B (no LDS bank conflicts; the column-major [c][32] form conflicts 2-way). One
 // thread = 16 rows of one column; a wave stores two contiguous 512 B runs.
 __global__ __launch_bounds__(256) void k_residues(const double *X, int64_t N, int n, int64_t ldx, const double *mean,
-                                                 const int *expo, int CBp, int TB, CrtTab tab, int8_t *R) {
+                                                 const int *expo, int CBp, int TB, CrtTab tab, int m0, int m1,
+                                                 int8_t *R) {
     const int cb = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = 32 * (w & 1) + (lane >> 1), half = lane & 1;
     const int tb = blockIdx.y * 2 + (w >> 1);
@@ -662,7 +664,7 @@ __global__ __launch_bounds__(256) void k_residues(const double *X, int64_t N, in
         const uint32_t w23 = __builtin_amdgcn_perm(b3, b2, 0x0c0c0400u);
         return __builtin_amdgcn_perm(w23, w01, 0x05040100u);
     };
-    for (int mi = 0; mi < tab.k; ++mi) {
+    for (int mi = m0; mi < m1; ++mi) {           // this launch's moduli
         v4i pk;
         const int m = tab.m[mi];
         if (m == 256) {          // the low byte of the two's-complement a
@@ -713,10 +715,11 @@ __global__ __launch_bounds__(256) void k_residues(const double *X, int64_t N, in
 
 // the residue GEMM of one 256 x 256 upper tile, one modulus and one split-K slab. 8 waves as 2 x 4,
 // each 128 x 64 (4 x 2 v_mfma_i32_32x32x32_i8 tiles, 128 accumulators); CRT_KB k-blocks per LDS
-// stage, two stages. Units u = (slab * k + mi) * ntiles + tile, this launch runs u0 .. u0 + nu - 1
+// stage, two stages. Units u = (mi * ks + slab) * ntiles + tile (modulus-major: a modulus group is
+// one contiguous run, launched as soon as its residue planes exist), this launch runs u0 .. u0 + nu - 1
 // (a rank's share) and writes unit u0 + l at out + l * CRT_UNIT, in lane order:
 // byte ((w * 4 + a) * 2 + b) * 1024 + lane * 16 + kk = accumulator kk of MFMA tile (a, b) of wave w.
-__global__ __launch_bounds__(512, 1) void k_xtx_crt(const int8_t *R, int TB, int64_t plane, int T, int ntiles, int k,
+__global__ __launch_bounds__(512, 1) void k_xtx_crt(const int8_t *R, int TB, int64_t plane, int T, int ntiles, int ks,
                                                   int kb, CrtTab tab, int64_t u0, int64_t nu, uint8_t *out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     int64_t lin = blockIdx.x;
@@ -728,7 +731,7 @@ __global__ __launch_bounds__(512, 1) void k_xtx_crt(const int8_t *R, int TB, int
     const int64_t u = u0 + lin;
     const int t = (int)(u % ntiles);
     const int64_t sm = u / ntiles;
-    const int mi = (int)(sm % k), slab = (int)(sm / k);
+    const int mi = (int)(sm / ks), slab = (int)(sm % ks);
     int bi, bj;
     tile_of(t, T, bi, bj);
     const int tb0 = slab * kb, tb1 = min(TB, tb0 + kb);
@@ -877,7 +880,7 @@ __global__ __launch_bounds__(256) void k_crt_diag(const uint8_t *Rs, int T, int 
     for (int s = 0; s < ks; ++s) {
         uint32_t b[CRT_KMAX];             // unconditional loads (see k_crt_finish)
 #pragma unroll
-        for (int mi = 0; mi < CRT_KMAX; ++mi) b[mi] = src[((int64_t)s * k + min(mi, k - 1)) * ustride];
+        for (int mi = 0; mi < CRT_KMAX; ++mi) b[mi] = src[((int64_t)min(mi, k - 1) * ks + s) * ustride];
 #pragma unroll
         for (int mi = 0; mi < CRT_KMAX; ++mi) sv[mi] += b[mi];
     }
@@ -911,7 +914,7 @@ __global__ __launch_bounds__(256) void k_crt_finish(const uint8_t *Rs, int T, in
     if (j >= n || ibase > j) return;
     const int k = tab.k;
     const int ej = expo[j];
-    const int64_t ustride = (int64_t)ntiles * CRT_UNIT;          // next modulus
+    const int64_t ustride = (int64_t)ntiles * CRT_UNIT;          // next (modulus, slab)
     const uint8_t *src = Rs + (int64_t)t * CRT_UNIT + rem * 16 + 4 * g;
     // the ks slab bytes of the 4 entries, summed in u16 lanes; every load issued before the first use
     uint32_t se[CRT_KMAX], so[CRT_KMAX];
@@ -923,7 +926,7 @@ __global__ __launch_bounds__(256) void k_crt_finish(const uint8_t *Rs, int T, in
         uint32_t wd[CRT_KMAX];
 #pragma unroll
         for (int mi = 0; mi < CRT_KMAX; ++mi)
-            wd[mi] = *reinterpret_cast<const uint32_t *>(src + ((int64_t)s * k + min(mi, k - 1)) * ustride);
+            wd[mi] = *reinterpret_cast<const uint32_t *>(src + ((int64_t)min(mi, k - 1) * ks + s) * ustride);
 #pragma unroll
         for (int mi = 0; mi < CRT_KMAX; ++mi) {
             se[mi] += wd[mi] & 0x00ff00ffu;
@@ -1101,12 +1104,13 @@ bool crt_plan(int n, int64_t N, CrtPlan &p) {
 }
 
 // the residue planes of X into h->k1_digits
+// the residue planes of moduli m0 .. m1 - 1 into h->k1_digits (allocated for all k)
 int crt_residues(pcg_handle *h, const CrtPlan &p, const double *X, int64_t N, int nn, int64_t ldx, const double *mean,
-                 const int *expo, const int8_t **R) {
+                 const int *expo, int m0, int m1, hipStream_t st, const int8_t **R) {
     const size_t bytes = (size_t)p.tab.k * p.CBp * p.TB * 2048;
     if (!pcg_ensure(h, h->k1_digits, bytes)) return pcg_fail(h, PCG_ERR_OOM, "K1 residue planes (%zu bytes)", bytes);
-    hipLaunchKernelGGL(k_residues, dim3((unsigned)p.CBp, (unsigned)(p.TB / 2)), dim3(256), 0, h->stream, X, N, nn,
-                       ldx, mean, expo, p.CBp, p.TB, p.tab, (int8_t *)h->k1_digits.p);
+    hipLaunchKernelGGL(k_residues, dim3((unsigned)p.CBp, (unsigned)(p.TB / 2)), dim3(256), 0, st, X, N, nn, ldx, mean,
+                       expo, p.CBp, p.TB, p.tab, m0, m1, (int8_t *)h->k1_digits.p);
     *R = (const int8_t *)h->k1_digits.p;
     return PCG_OK;
 }
@@ -1116,7 +1120,7 @@ void crt_gemm(pcg_handle *h, const CrtPlan &p, const int8_t *R, int64_t u0, int6
     if (nu <= 0) return;
     const int64_t plane = (int64_t)p.CBp * p.TB * 2048;
     hipLaunchKernelGGL(k_xtx_crt, dim3((unsigned)((nu + 7) / 8 * 8)), dim3(512), CRT_NS * CRT_STAGE, h->stream, R, p.TB,
-                       plane, p.T, p.ntiles, p.tab.k, p.kb, p.tab, u0, nu, out);
+                       plane, p.T, p.ntiles, p.ks, p.kb, p.tab, u0, nu, out);
 }
 
 // C from the units' residues: the diagonal (sd) first, then every upper entry and its mirror
@@ -1364,7 +1368,7 @@ extern "C" int pcg_corr_shard(pcg_handle *h, const double *X, int64_t N, int64_t
         int rc = column_means(h, X, N, nn, ldx, &mean, &expo);
         if (rc) return rc;
         const int8_t *R = nullptr;
-        rc = crt_residues(h, cp, X, N, nn, ldx, mean, expo, &R);
+        rc = crt_residues(h, cp, X, N, nn, ldx, mean, expo, 0, cp.tab.k, h->stream, &R);
         if (rc) return rc;
         const int64_t per = (cp.units + world - 1) / world, u0 = per * rank;
         crt_gemm(h, cp, R, u0, std::min<int64_t>(per, cp.units - u0), (uint8_t *)packed);
@@ -1467,15 +1471,41 @@ int pcg_corr_launch(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_
         int *expo = nullptr;
         int rc = column_means(h, X, N, nn, ldx, &mean, &expo);
         if (rc) return rc;
-        const int8_t *R = nullptr;
-        rc = crt_residues(h, cp, X, N, nn, ldx, mean, expo, &R);
-        if (rc) return rc;
         const size_t sbytes = sizeof(double) * (size_t)(nn + 32);
         if (!pcg_ensure(h, h->pr_scratch, sbytes + (size_t)cp.units * CRT_UNIT))
             return pcg_fail(h, PCG_ERR_OOM, "pcg_corr CRT scratch");
         double *sd = (double *)h->pr_scratch.p;
         uint8_t *Rs = (uint8_t *)h->pr_scratch.p + sbytes;
-        crt_gemm(h, cp, R, 0, cp.units, Rs);
+        // PCG_K1_CRT_GROUPS > 1: moduli in groups, the residue planes of group g + 1 computed on the
+        // aux stream while the GEMM of group g runs. Measured slower (pcg_corr 0.63 ms at 1 group,
+        // 0.76 / 0.80 / 0.95 ms at 2 / 3 / 4: the co-resident residue blocks delay the GEMM's
+        // one-block-per-CU waves more than they hide), so 1 is the default.
+        const int k = cp.tab.k;
+        const int groups = std::max(1, std::min(k, std::min(CRT_MAXG, env_int("PCG_K1_CRT_GROUPS", 1))));
+        const int8_t *R = nullptr;
+        if (groups == 1) {
+            rc = crt_residues(h, cp, X, N, nn, ldx, mean, expo, 0, k, h->stream, &R);
+            if (rc) return rc;
+            crt_gemm(h, cp, R, 0, cp.units, Rs);
+        } else {
+            if (!h->aux) PCG_HIP(h, hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking));
+            for (int g = 0; g <= groups; ++g)
+                if (!h->k1ev[g]) PCG_HIP(h, hipEventCreateWithFlags(&h->k1ev[g], hipEventDisableTiming));
+            PCG_HIP(h, hipEventRecord(h->k1ev[groups], h->stream));        // column statistics done
+            PCG_HIP(h, hipStreamWaitEvent(h->aux, h->k1ev[groups], 0));
+            const int64_t per_mod = (int64_t)cp.ks * cp.ntiles;
+            for (int g = 0; g < groups; ++g) {
+                const int m0 = k * g / groups, m1 = k * (g + 1) / groups;
+                rc = crt_residues(h, cp, X, N, nn, ldx, mean, expo, m0, m1, h->aux, &R);
+                if (rc) return rc;
+                PCG_HIP(h, hipEventRecord(h->k1ev[g], h->aux));
+            }
+            for (int g = 0; g < groups; ++g) {
+                const int m0 = k * g / groups, m1 = k * (g + 1) / groups;
+                PCG_HIP(h, hipStreamWaitEvent(h->stream, h->k1ev[g], 0));
+                crt_gemm(h, cp, R, m0 * per_mod, (m1 - m0) * per_mod, Rs + m0 * per_mod * CRT_UNIT);
+            }
+        }
         crt_finish(h, cp, Rs, expo, nn, N, sd, C, ldc);
         PCG_HIP(h, hipGetLastError());
         return PCG_OK;

@@ -71,7 +71,8 @@ struct pcg_handle {
     DevBuf screenq;                 // fp32 sweep -> fp64 screen list (k_level_lds_f -> k_screen)
     DevBuf adj, deg, rm, cpre, binom, ctr, deferred, records, nearbuf, exportbuf, export_xy, diag, colmean,
         pr_scratch, batch_scratch, chisq_scratch;
-    DevBuf k1_digits;               // K1 int8 digit planes of the centred X (corr.hip, PCG_K1_I8)
+    DevBuf k1_digits;               // K1 int8 digit / residue planes of the centred X (corr.hip)
+    hipEvent_t k1ev[5] = {};        // K1 CRT: residue groups done on aux (+ column statistics done)
     // CSR (offsets, neighbour lists) and sepset union rows, double-buffered: depth d's sepset
     // export reads buffer set cb on the export stream while depth d + 1 runs on set 1 - cb
     DevBuf off2[2], nbr2[2], ug2[2];
