@@ -531,6 +531,7 @@ struct CrtTab {
     float finv[CRT_KMAX];           // fl(1 / m_i)
     double dinv[CRT_KMAX];
     uint32_t wlo[CRT_KMAX], whi[CRT_KMAX];   // bytes 2^(8q) mod m_i, 2^(32 + 8q) mod m_i (q = 0..3)
+    uint32_t cneg[CRT_KMAX];        // -(2^b mod m_i) as u32: the offset's residue, subtracted in the dot
     uint32_t Mi[CRT_KMAX][2 * CRT_L];   // M / m_i, little-endian 16-bit limbs (one per word)
     uint32_t M[2 * CRT_L];
 };
@@ -645,16 +646,21 @@ __global__ __launch_bounds__(256) void k_residues(const double *X, int64_t N, in
     const int e = vj ? expo[j] : 0;
     const bool live = vj && e != K1_NONFINITE;
     const double mu = live ? mean[j] : 0.0;
+    // offset binary: (hi, lo) = a + 2^b in [1, 2^(b+1)), so every residue is of a nonnegative
+    // integer and the offset's residue 2^b mod m is subtracted inside the dot product (tab.cneg)
     uint32_t lo[16], hi[16];
-    float sg[16];                                        // +-1 per value
+    const uint32_t B = 1u << (tab.b - 32);
+    const int64_t t0 = (int64_t)tb * 32 + 16 * half;
+    const double *xp = X + t0 * ldx + j;                 // rows t0 + i at xp + i ldx (uniform stride)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-        const int64_t t = (int64_t)tb * 32 + 16 * half + i;
-        const double v = (live && t < N) ? X[t * ldx + j] - mu : 0.0;
+        const double v = (live && t0 + i < N) ? xp[(int64_t)i * ldx] - mu : 0.0;
         const double y = ldexp(fabs(v), tab.b - e);      // < 2^b <= 2^63, exact scaling
-        hi[i] = (uint32_t)(y * 0x1p-32);                 // truncating conversions: |a| = trunc(y)
-        lo[i] = (uint32_t)(y - (double)hi[i] * 0x1p32);  // exact difference (multiples of ulp(y))
-        sg[i] = v < 0.0 ? -1.0f : 1.0f;
+        const uint32_t h = (uint32_t)(y * 0x1p-32);      // truncating conversions: |a| = trunc(y)
+        const uint32_t l = (uint32_t)(y - (double)h * 0x1p32);   // exact difference (multiples of ulp(y))
+        const bool neg = v < 0.0;
+        lo[i] = neg ? 0u - l : l;
+        hi[i] = neg ? B - h - (l != 0u) : B + h;
     }
     const int64_t plane = (int64_t)CBp * TB * 2048;
     int8_t *dst = R + ((int64_t)cb * TB + tb) * 2048 + half * 1024 + c * 16;
@@ -667,39 +673,30 @@ __global__ __launch_bounds__(256) void k_residues(const double *X, int64_t N, in
     for (int mi = m0; mi < m1; ++mi) {           // this launch's moduli
         v4i pk;
         const int m = tab.m[mi];
-        if (m == 256) {          // the low byte of the two's-complement a
+        if (m == 256) {          // the low byte (2^b = 0 mod 256)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                uint32_t bb[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int i = 4 * q + u;
-                    bb[u] = sg[i] < 0.0f ? 0u - lo[i] : lo[i];
-                }
-                pk[q] = (int)pack4(bb[0], bb[1], bb[2], bb[3]);
-            }
+            for (int q = 0; q < 4; ++q) pk[q] = (int)pack4(lo[4 * q], lo[4 * q + 1], lo[4 * q + 2], lo[4 * q + 3]);
         } else {
-            // odd m: s = |a| mod-equivalent (< 8 x 255^2, exact in fp32), r = s - m rint(s / m) in
-            // [-(m-1)/2, (m-1)/2] (s / m is never a half-integer for odd m, and fl(1/m) moves it
-            // by < 1/(32 m)), then the sign; rint and the byte via the 1.5 x 2^23 magic constant
+            // odd m: s = a + 2^b - (2^b mod m) = a (mod m), |s| < 8 x 255^2 (exact in fp32), r = s - m
+            // rint(s / m) in [-(m-1)/2, (m-1)/2] (s / m is never a half-integer for odd m, and
+            // fl(1/m) moves it by < 1/(32 m)); rint and the byte via the 1.5 x 2^23 magic constant
             const f2 fi = {tab.finv[mi], tab.finv[mi]};
             const f2 nm = {-(float)m, -(float)m};
             const f2 mg = {12582912.0f, 12582912.0f};
-            const uint32_t wl = tab.wlo[mi], wh = tab.whi[mi];
+            const uint32_t wl = tab.wlo[mi], wh = tab.whi[mi], cn = tab.cneg[mi];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 uint32_t bb[4];
 #pragma unroll
                 for (int u = 0; u < 4; u += 2) {
                     const int i = 4 * q + u;
-                    const float x0 = (float)__builtin_amdgcn_udot4(lo[i], wl,
-                                                                   __builtin_amdgcn_udot4(hi[i], wh, 0u, false), false);
-                    const float x1 = (float)__builtin_amdgcn_udot4(lo[i + 1], wl,
-                                                                   __builtin_amdgcn_udot4(hi[i + 1], wh, 0u, false), false);
+                    const float x0 = (float)(int)__builtin_amdgcn_udot4(
+                        lo[i], wl, __builtin_amdgcn_udot4(hi[i], wh, cn, false), false);
+                    const float x1 = (float)(int)__builtin_amdgcn_udot4(
+                        lo[i + 1], wl, __builtin_amdgcn_udot4(hi[i + 1], wh, cn, false), false);
                     const f2 x = {x0, x1};
-                    const f2 sv = {sg[i], sg[i + 1]};
                     const f2 qv = __builtin_elementwise_fma(x, fi, mg) - mg;    // rint(s / m)
-                    const f2 rv = __builtin_elementwise_fma(qv, nm, x) * sv + mg;
+                    const f2 rv = __builtin_elementwise_fma(qv, nm, x) + mg;
                     // (through named floats: this compiler's __builtin_bit_cast of a vector
                     // component reads component 0)
                     const float r0 = rv.x, r1 = rv.y;
@@ -1070,6 +1067,9 @@ bool crt_plan(int n, int64_t N, CrtPlan &p) {
         }
         t.wlo[i] = wl;
         t.whi[i] = wh;
+        uint64_t pb = 1;
+        for (int s2 = 0; s2 < b; ++s2) pb = (pb * 2) % m;
+        t.cneg[i] = 0u - (uint32_t)pb;
     }
     p.T = (n + CRT_T - 1) / CRT_T;
     p.ntiles = p.T * (p.T + 1) / 2;
