@@ -83,6 +83,28 @@ def test_corr_crt_matches_numpy(eng, n, N):
     np.testing.assert_allclose(C, np.corrcoef(X.T), rtol=0, atol=2e-14)
 
 
+@pytest.mark.parametrize("N", [778, 40000])
+def test_corr_crt_extreme_magnitudes(eng, N):
+    """The CRT rebuild at the top of its range: every centred value of a column has the same
+    magnitude just below a power of two (balanced signs, so the mean is exactly 0 and |a| =
+    trunc((1 - 2^-40) 2^b): the Gram entries reach (1 - 2^-39) N 4^b, the bound M / 2 is built
+    for); three sign patterns shared by column groups: C is the +-1 pattern numpy gives (within its
+    rounding) inside a group."""
+    rng = np.random.default_rng(N)
+    n = 300
+    base = np.repeat([-1.0, 1.0], N // 2)
+    sgn = np.stack([rng.permutation(base) for _ in range(3)], axis=1)
+    grp = np.arange(n) % 3
+    mag = (1.0 - 2.0 ** -40) * 2.0 ** rng.integers(-20, 20, n).astype(np.float64)
+    X = np.ascontiguousarray(sgn[:, grp] * mag * np.where(np.arange(n) % 2, 1.0, -1.0))
+    assert np.all(X.mean(axis=0) == 0.0)
+    C = eng.corr(X).cpu().numpy()
+    ref = np.corrcoef(X.T)
+    np.testing.assert_allclose(C, ref, rtol=0, atol=2e-14)
+    same = grp[:, None] == grp[None, :]
+    assert np.all(np.abs(np.abs(C[same]) - 1.0) < 1e-14)
+
+
 @pytest.mark.parametrize("n,N", [(300, 1200), (2000, 10000)])
 def test_corr_crt_split_invariant(eng, n, N, monkeypatch):
     """The CRT result is the correctly rounded exact Gram, so every split-K choice gives the same
