@@ -59,7 +59,14 @@ constexpr int RS = 256 / TILE;         // staging row step
 #endif
 constexpr int KT = PCG_K1_KT;
 constexpr int PAD = 1;  // LDS row padding (doubles) against bank conflicts
-constexpr int MEAN_ROWS = 64;   // rows per partial column sum (N = 10k: 157 chunks x 8 column blocks)
+#ifndef PCG_MEAN_ROWS
+#define PCG_MEAN_ROWS 64
+#endif
+#ifndef PCG_COLSUM_UNROLL
+#define PCG_COLSUM_UNROLL 8
+#endif
+constexpr int MEAN_ROWS = PCG_MEAN_ROWS;   // rows per partial column sum (N = 10k: 157 chunks x 8 column blocks)
+constexpr int CS_U = PCG_COLSUM_UNROLL;    // loads in flight per thread (k_colsum_partial)
 
 // partial column sums over row chunks (deterministic two-pass mean); with pmax / pmin also the
 // chunk's column maximum and minimum (the int8 digit path's exponents)
@@ -71,12 +78,12 @@ __global__ __launch_bounds__(256) void k_colsum_partial(const double *X, int64_t
     const int64_t r1 = std::min<int64_t>(r0 + MEAN_ROWS, N);
     double s = 0.0, mx = -INFINITY, mn = INFINITY;
     int64_t t = r0;
-    for (; t + 8 <= r1; t += 8) {           // 8 loads in flight, summed in row order
-        double v[8];
+    for (; t + CS_U <= r1; t += CS_U) {     // CS_U loads in flight, summed in row order
+        double v[CS_U];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = X[(t + k) * ldx + j];
+        for (int k = 0; k < CS_U; ++k) v[k] = X[(t + k) * ldx + j];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < CS_U; ++k) {
             s += v[k];
             mx = fmax(mx, v[k]);
             mn = fmin(mn, v[k]);
