@@ -197,12 +197,15 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--full-p", action="store_true", help="compute every p-value (PCG_FLAG_FULL_P)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-full-p", action="store_true", help="skip the full-p comparison run after the timed steps")
     ap.add_argument("--cpu-depth", type=int, default=3, help="depths timed for the CPU port baseline")
     ap.add_argument("--json-extra", action="store_true", help="print per-level detail to stderr")
     ap.add_argument("--workload", choices=["skeleton", "rq2"], default="skeleton",
                     help="skeleton: the headline line (config 5); rq2: every case of an Online-Boutique-shaped "
                          "RQ2 tree through pc_pagerank, cases dealt one per GPU (config 2)")
     ap.add_argument("--rq2-cases", type=int, default=125, help="cases in the synthetic RQ2 tree")
+    ap.add_argument("--rq2-prefetch", type=int, default=2,
+                    help="loader threads reading / windowing the next cases while the GPU runs the current one")
     ap.add_argument("--rq2-dataset", choices=["online-boutique", "sock-shop"], default="online-boutique",
                     help="shape of the synthetic RQ2 tree (config 2 names both)")
     return ap.parse_args()
@@ -316,9 +319,12 @@ def rq2_main(args):
         rq2.process(p, "pc_pagerank", dataset, tempfile.mkdtemp(), length=None)
     if world > 1:
         torch.distributed.barrier()
+    from rcaeval_amd import phases
+    phases.enable()
     t0 = time.perf_counter()
-    res = rq2.run(root, "pc_pagerank", dataset, out_dir, rank=rank, world=world)
+    res = rq2.run(root, "pc_pagerank", dataset, out_dir, rank=rank, world=world, prefetch=args.rq2_prefetch)
     dt = time.perf_counter() - t0
+    phases.enable(False)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -337,6 +343,11 @@ def rq2_main(args):
                                    "read_csv + window + preprocess + PC + orientation + PageRank + JSON",
                        "parallelism": f"cases round-robin over {world} GPU(s)"},
             "seconds_per_case_per_gpu": s_per_case * world,
+            "prefetch_threads": args.rq2_prefetch,
+            # rank 0's cases: wall ms per case of each phase (read_csv / window run on the loader
+            # threads when prefetch > 0, overlapped with the GPU work of the previous case)
+            "phase_ms_per_case": {k: round(1000.0 * v[0] / max(res["my_cases"], 1), 4)
+                                  for k, v in sorted(res.get("phases", {}).items(), key=lambda kv: -kv[1][0])},
             "published_seconds_per_case_cpu": OB_PC_PAGERANK_S_PER_CASE,
             "summary": res["summary"]}), flush=True)
     if not os.environ.get("PCG_RQ2_DIR") and rank == 0:
@@ -425,8 +436,15 @@ def main():
             torch.distributed.barrier()
         torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
+    def progress(msg):
+        if rank == 0:
+            print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+    for w in range(args.warmup):
+        t0 = time.perf_counter()
         one_step()
+        torch.cuda.synchronize()
+        progress(f"warmup {w}: {1000 * (time.perf_counter() - t0):.2f} ms")
     times, out = [], None
     for _ in range(args.steps):
         out = None          # the previous step's result is released, as a caller consuming each result would
@@ -442,6 +460,7 @@ def main():
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
             dt = float(t.item())
         times.append(dt)
+        progress(f"step {len(times) - 1}: {1000 * dt:.3f} ms")
     st = out.stats
     tests_total = int(sum(st["tests"]))
     ms = 1000.0 * float(np.mean(times))
@@ -467,7 +486,8 @@ def main():
     # the same skeleton with every p-value computed (PCG_FLAG_FULL_P), once, after the timed
     # steps: the reference-arithmetic mode beside the threshold headline
     full_p = None
-    if not args.full_p and world == 1:
+    if not args.full_p and not args.no_full_p and world == 1:
+        progress("full-p comparison run")
         C = eng.corr(Xd)
         o = eng.skeleton(C, args.samples, alpha=args.alpha, max_depth=args.max_depth, flags=_lib.PCG_FLAG_FULL_P)
         fp_ms = float(sum(o.stats["level_ms"]))
@@ -500,6 +520,7 @@ def main():
             "full_p": full_p,
         }
         if not args.no_cpu_baseline and world == 1:
+            progress("CPU baseline")
             cb = cpu_baseline(X, args.alpha, args.cpu_depth, st["tests"], out.removed_level)
             ref = cb.pop("_ref")
             # parity of the timed GPU run on the CPU-sampled depths

@@ -24,6 +24,7 @@ from . import _lib
 from .background import BackgroundKnowledge, banned_pairs
 from .citest import CITester, uc_orient
 from .engine import SkeletonOut, get_engine, orient
+from .phases import phase
 from .skeleton_seq import skeleton_unstable
 
 fisherz = "fisherz"
@@ -352,12 +353,14 @@ def pc(data: np.ndarray, alpha: float = 0.05, indep_test=fisherz, stable: bool =
     flags = _lib.PCG_FLAG_FULL_P if full_p else 0
     knowledge = background_knowledge.masks(names) if background_knowledge is not None else None
     banned = None if knowledge is None else banned_pairs(knowledge[0])
-    out, C = skeleton_from_data(X, alpha=alpha, max_depth=max_depth, flags=flags, device=device, banned=banned)
-    if priority == 2 and knowledge is None:
-        graph = orient(out.adj, out.sep_xy, out.sep_bits, priority=2).astype(int)
-    else:
-        ci = CITester(C, X.shape[0], device=device) if priority != 2 else None
-        graph = uc_orient(out.adj, out.sep_xy, out.sep_bits, priority, ci, knowledge=knowledge).astype(int)
+    with phase("K1 + skeleton"):
+        out, C = skeleton_from_data(X, alpha=alpha, max_depth=max_depth, flags=flags, device=device, banned=banned)
+    with phase("orientation"):
+        if priority == 2 and knowledge is None:
+            graph = orient(out.adj, out.sep_xy, out.sep_bits, priority=2).astype(int)
+        else:
+            ci = CITester(C, X.shape[0], device=device) if priority != 2 else None
+            graph = uc_orient(out.adj, out.sep_xy, out.sep_bits, priority, ci, knowledge=knowledge).astype(int)
     cg = CausalGraph(graph, names, out, C=C, N=X.shape[0], alpha=alpha, device=device, banned=banned)
     cg.PC_elapsed = time.time() - start
     return cg

@@ -88,6 +88,19 @@ int agree(pcg_handle *h, int failed) {
     return v;
 }
 
+// agree() plus a value every rank must hold identically (a plan signature): one all-reduce (MAX)
+// of {failed, v, -v}; *same = every rank passed the same v
+int agree_value(pcg_handle *h, int failed, int64_t v, bool *same) {
+    int64_t a[3] = {failed ? 1 : 0, v, -v};
+    int64_t *d = (int64_t *)h->comm_small.p;     // >= 5 * PCG_MAX_LEVELS int64 since pcg_comm_init
+    PCG_HIP(h, hipMemcpyAsync(d, a, sizeof(a), hipMemcpyHostToDevice, h->stream));
+    PCG_NCCL(h, rccl().all_reduce(d, d, 3, ncclInt64, ncclMax, (ncclComm_t)h->comm, h->stream));
+    PCG_HIP(h, hipMemcpyAsync(a, d, sizeof(a), hipMemcpyDeviceToHost, h->stream));
+    PCG_HIP(h, hipStreamSynchronize(h->stream));
+    *same = a[1] == -a[2];
+    return (int)a[0];
+}
+
 // the verdict of agree() as this rank's return code
 int agreed_failure(pcg_handle *h, int local, int g, const char *what) {
     if (g < 0) return g;
@@ -138,6 +151,14 @@ int sharded_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t
     if (!local) local = pcg_set_removal_buffer(h, nullptr, 0);   // the handle's own flags
     if (!local) local = pcg_set_world_size(h, world);
     if (!local) local = pcg_skeleton_init(h, C, n, ldc, N, alpha, flags, removed_level);
+    // the per-depth barrier (merge, then pcg_level_end's CSR rebuild) must not be able to fail on
+    // one rank only: its only allocations, the two neighbour-list buffer sets, are sized here for
+    // the complete graph (degrees only fall), inside the agreed set-up. What is left to fail
+    // between two collectives is a launch / stream error, i.e. a device fault, not a local OOM.
+    for (int t = 0; t < 2 && !local; ++t)
+        if (!pcg_ensure(h, h->off2[t], sizeof(int32_t) * (size_t)(n + 1)) ||
+            !pcg_ensure(h, h->nbr2[t], sizeof(int32_t) * (size_t)std::max<int64_t>(n * (n - 1), 1)))
+            local = pcg_fail(h, PCG_ERR_OOM, "neighbour lists");
     int g = agree(h, local != 0);
     if (g) {
         pcg_set_world_size(h, 1);
@@ -186,7 +207,8 @@ int sharded_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t
 }
 
 // per-depth counters summed over ranks (replicated quantities — calls, degrees, edges — are
-// identical on every rank already)
+// identical on every rank already). Its only early returns are HIP copy / sync errors, i.e. a
+// faulted device, after which no collective on this communicator can complete anyway.
 int reduce_stats(pcg_handle *h) {
     const int L = h->st.levels;
     if (L <= 0) return PCG_OK;
@@ -349,16 +371,18 @@ extern "C" int pcg_corr_sharded(pcg_handle *h, const double *X, int64_t N, int64
         const int g = agree(h, local != 0);
         if (g) return agreed_failure(h, local, g, "sharded K1");
     }
+    // pcg_corr_shard can fail on one rank only (its column-statistics and residue-plane scratch
+    // grow on demand: ~350 MB at n = 2000, N = 1e4): the outcome is agreed before the all-gather,
+    // so no peer rebuilds C from a failed rank's unwritten units and every rank leaves together
+    // the plan (path, k, b, split-K) comes from (n, N) and the process's K1 knobs: ranks started
+    // with different knobs would gather mismatched units, so its signature is agreed with the outcome
     const int local = pcg_corr_shard(h, X, N, n, ldx, h->comm_rank, h->comm_world, (double *)h->comm_packed.p);
-    const std::string local_err = local ? h->err : std::string();
-    // joined even after a local launch failure (the peers' C is then garbage, and so is ours:
-    // the failing rank reports it; the argument checks of pcg_corr_shard agree on every rank)
+    bool same = true;
+    const int g = agree_value(h, local != 0, k1_plan_signature(n, N), &same);
+    if (g) return agreed_failure(h, local, g, "sharded K1");
+    if (!same) return pcg_fail(h, PCG_ERR_INVALID, "sharded K1: the ranks' K1 plans differ (PCG_K1_* environment)");
     PCG_NCCL(h, rccl().all_gather(h->comm_packed.p, h->comm_gathered.p, per, ncclFloat64, (ncclComm_t)h->comm,
                                   h->stream));
-    if (local) {
-        h->err = local_err;
-        return local;
-    }
     return pcg_corr_shard_finish(h, (const double *)h->comm_gathered.p, N, n, h->comm_world, C, ldc);
 }
 

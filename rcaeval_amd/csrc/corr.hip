@@ -1004,6 +1004,21 @@ static int env_int(const char *name, int dflt) {
     return e ? atoi(e) : dflt;
 }
 
+// the plan's A/B knobs (read at each call; pcg_corr_sharded agrees the resulting plan's signature
+// across ranks before its all-gather, so ranks started with different knobs fail together)
+struct CrtKnobs {
+    bool on;
+    int minn, bmin, ks;
+};
+static CrtKnobs crt_knobs() {
+    CrtKnobs v;
+    v.on = k1_i8() && env_int("PCG_K1_CRT", 1) != 0;
+    v.minn = env_int("PCG_K1_CRT_MINN", 256);
+    v.bmin = std::min(63, std::max(32, env_int("PCG_K1_CRT_BITS", 56)));   // k_residues needs b in [32, 63]
+    v.ks = env_int("PCG_K1_CRT_KS", 0);
+    return v;
+}
+
 // little-endian 32-bit limb helpers for the host tables
 static void big_mul_small(uint32_t *x, int L, uint32_t m) {
     uint64_t c = 0;
@@ -1024,8 +1039,9 @@ static uint32_t big_div_small(const uint32_t *x, int L, uint32_t m, uint32_t *q)
 }
 
 bool crt_plan(int n, int64_t N, CrtPlan &p) {
-    if (!k1_i8() || env_int("PCG_K1_CRT", 1) == 0 || n < env_int("PCG_K1_CRT_MINN", 256)) return false;
-    const int bmin = env_int("PCG_K1_CRT_BITS", 56);
+    const CrtKnobs kn = crt_knobs();
+    if (!kn.on || n < kn.minn) return false;
+    const int bmin = kn.bmin;
     // k: the fewest moduli whose product leaves b >= bmin bits per value, M > 2 N 4^b (0.01 bit margin)
     double lm = 0.0;
     int k = 0, b = 0;
@@ -1086,7 +1102,7 @@ bool crt_plan(int n, int64_t N, CrtPlan &p) {
     // each unit writes and k_crt_finish reads (128 KB, ~0.026 us of chip bandwidth)
     int best = 1;
     double best_cost = 1e300;
-    const int force = env_int("PCG_K1_CRT_KS", 0);
+    const int force = kn.ks;
     for (int ks = 1; ks <= 16; ++ks) {
         int kbk = (p.TB + ks - 1) / ks;
         kbk = (kbk + CRT_KB - 1) / CRT_KB * CRT_KB;
@@ -1315,6 +1331,7 @@ int column_means(pcg_handle *h, const double *X, int64_t N, int nn, int64_t ldx,
                  int **expo_out = nullptr) {
     const int nchunks = (int)((N + MEAN_ROWS - 1) / MEAN_ROWS);
     const size_t parts = (size_t)nn * nchunks * (expo_out ? 3 : 1);
+    h->k1_stamp_ok = false;          // h->colmean is rewritten: no shard's exponents survive
     if (!pcg_ensure(h, h->colmean, sizeof(double) * (parts + nn) + sizeof(int) * nn))
         return pcg_fail(h, PCG_ERR_OOM, "pcg_corr scratch");
     double *part = (double *)h->colmean.p;
@@ -1332,6 +1349,16 @@ int column_means(pcg_handle *h, const double *X, int64_t N, int nn, int64_t ldx,
 }
 
 }  // namespace
+
+// a signature of K1's plan for (n, N) (path, and the CRT path's k, b, split-K and unit count):
+// ranks whose environments select different plans would all-gather mismatched units
+int64_t k1_plan_signature(int64_t n, int64_t N) {
+    CrtPlan cp;
+    if (crt_plan((int)n, N, cp))
+        return ((int64_t)1 << 62) | ((int64_t)cp.tab.k << 48) | ((int64_t)cp.tab.b << 40) | ((int64_t)cp.ks << 32) |
+               (cp.units & 0xffffffffll);
+    return k1_i8() ? 1 : 2;
+}
 
 extern "C" int pcg_corr_shard_rows(int64_t n, int world, int64_t *rows_per_rank) {
     if (n < 1 || world < 1 || !rows_per_rank) return PCG_ERR_INVALID;
@@ -1374,6 +1401,11 @@ extern "C" int pcg_corr_shard(pcg_handle *h, const double *X, int64_t N, int64_t
         int *expo = nullptr;
         int rc = column_means(h, X, N, nn, ldx, &mean, &expo);
         if (rc) return rc;
+        h->k1_stamp[0] = N;
+        h->k1_stamp[1] = nn;
+        h->k1_stamp[2] = cp.tab.k;
+        h->k1_stamp[3] = cp.tab.b;
+        h->k1_stamp_ok = true;
         const int8_t *R = nullptr;
         rc = crt_residues(h, cp, X, N, nn, ldx, mean, expo, 0, cp.tab.k, h->stream, &R);
         if (rc) return rc;
@@ -1443,6 +1475,11 @@ extern "C" int pcg_corr_shard_finish(pcg_handle *h, const double *gathered, int6
     const double scale = 1.0 / (double)(N - 1);
     CrtPlan cp;
     if (crt_plan(nn, N, cp)) {     // gathered = every unit in canonical order; exponents from pcg_corr_shard
+        if (!h->k1_stamp_ok || h->k1_stamp[0] != N || h->k1_stamp[1] != nn || h->k1_stamp[2] != cp.tab.k ||
+            h->k1_stamp[3] != cp.tab.b)
+            return pcg_fail(h, PCG_ERR_INVALID,
+                            "pcg_corr_shard_finish: no CRT-mode pcg_corr_shard of (N %lld, n %lld) on this handle since "
+                            "the last K1 call", (long long)N, (long long)n);
         if (!pcg_ensure(h, h->pr_scratch, sizeof(double) * (size_t)(nn + 32)))
             return pcg_fail(h, PCG_ERR_OOM, "pcg_corr_shard_finish scratch");
         crt_finish(h, cp, (const uint8_t *)gathered, colmean_expo(h, N, nn), nn, N, (double *)h->pr_scratch.p, C,
@@ -1453,6 +1490,7 @@ extern "C" int pcg_corr_shard_finish(pcg_handle *h, const double *gathered, int6
     }
     int64_t rows = 0;
     pcg_corr_shard_rows(n, world, &rows);
+    h->k1_stamp_ok = false;          // sd overwrites h->colmean
     if (!pcg_ensure(h, h->colmean, sizeof(double) * ((size_t)nn * 2)))
         return pcg_fail(h, PCG_ERR_OOM, "pcg_corr scratch");
     double *sd = (double *)h->colmean.p;

@@ -72,6 +72,10 @@ struct pcg_handle {
     DevBuf adj, deg, rm, cpre, binom, ctr, deferred, records, nearbuf, exportbuf, export_xy, diag, colmean,
         pr_scratch, batch_scratch, chisq_scratch;
     DevBuf k1_digits;               // K1 int8 digit / residue planes of the centred X (corr.hip)
+    // the (N, n, k, b) a CRT-mode pcg_corr_shard computed h->colmean's column exponents for;
+    // pcg_corr_shard_finish refuses to rebuild C from exponents of any other call
+    int64_t k1_stamp[4] = {0, 0, 0, 0};
+    bool k1_stamp_ok = false;
     hipEvent_t k1ev[5] = {};        // K1 CRT: residue groups done on aux (+ column statistics done)
     // CSR (offsets, neighbour lists) and sepset union rows, double-buffered: depth d's sepset
     // export reads buffer set cb on the export stream while depth d + 1 runs on set 1 - cb
@@ -165,6 +169,7 @@ void pcg_comm_release(pcg_handle *h);      // comm.hip: destroy the communicator
 // corr.hip: K1 queued on h->stream without the host sync of pcg_corr (pcg_pc_skeleton)
 int export_sync(pcg_handle *h);   // skeleton.hip: wait for the sepset exports, take their row count
 int pcg_corr_launch(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx, double *C, int64_t ldc);
+int64_t k1_plan_signature(int64_t n, int64_t N);   // corr.hip: K1's plan for (n, N), for cross-rank agreement
 
 int pcg_fail(pcg_handle *h, int code, const char *fmt, ...);
 bool pcg_ensure(pcg_handle *h, DevBuf &b, size_t bytes);   // grow-only allocation

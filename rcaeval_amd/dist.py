@@ -41,6 +41,17 @@ def agree(failed: bool, device="cpu", group=None) -> bool:
     return bool(t.item())
 
 
+def agree_value(failed: bool, value: int, device="cpu", group=None) -> tuple[bool, bool]:
+    """``agree`` plus a value every rank must hold identically (one all-reduce MAX of
+    {failed, v, -v}): (any rank failed, every rank passed the same value)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([1 if failed else 0, int(value), -int(value)], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    v = t.cpu().tolist()
+    return bool(v[0]), v[1] == -v[2]
+
+
 def raise_agreed(local_err, what: str):
     """Re-raise this rank's own error, or PCG_ERR_PEER for a peer's."""
     if local_err is not None:
@@ -268,9 +279,22 @@ def sharded_corr(eng, X, group=None):
     import torch
     import torch.distributed as dist
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    Xd = eng.to_device(X)
-    N, n = Xd.shape
-    packed = eng.corr_shard(Xd, rank, world)
+    cdev = eng.device if dist.get_backend(group) == "nccl" else "cpu"
+    N, n = X.shape
+    # a local failure (e.g. OOM on the residue planes) and the share's size (a function of the
+    # K1 plan, which each process's PCG_K1_* knobs select) are agreed before the all-gather, so no
+    # rank waits in it for a peer that raised or gathers shares of another size
+    packed, err = None, None
+    try:
+        packed = eng.corr_shard(eng.to_device(X), rank, world)
+    except Exception as e:   # noqa: BLE001 - must reach the agreement below
+        err = e
+    failed, same = agree_value(err is not None, packed.numel() if packed is not None else 0, device=cdev,
+                               group=group)
+    if failed:
+        raise_agreed(err, "sharded K1")
+    if not same:
+        raise _lib.PcgError(_lib.PCG_ERR_INVALID, "sharded K1: the ranks' K1 plans differ (PCG_K1_* environment)")
     if dist.get_backend(group) == "nccl":
         gathered = torch.empty(world * packed.numel(), dtype=torch.float64, device=eng.device)
         dist.all_gather_into_tensor(gathered, packed, group=group)

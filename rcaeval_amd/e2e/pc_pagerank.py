@@ -14,6 +14,7 @@ import numpy as np
 from ..causal import pc
 from ..graph_heads.page_rank import PageRank
 from ..io.time_series import preprocess
+from ..phases import phase
 from . import rca
 
 
@@ -30,10 +31,15 @@ def digraph_matrix(adj: np.ndarray):
 @rca
 def pc_pagerank(data, inject_time=None, dataset=None, dk_select_useful=False, with_bg=False, n_iter=10,
                 **kwargs):
-    data = preprocess(data=data, dataset=dataset, dk_select_useful=dk_select_useful)
-    node_names = data.columns.to_list()
-    cg = pc(data.to_numpy())
-    M, _nodes = digraph_matrix(cg.G.graph)
-    scores = PageRank().fit_transform(M.T)
-    ranked = sorted(zip(node_names, scores), key=lambda t: t[1], reverse=True)
+    with phase("preprocess"):
+        data = preprocess(data=data, dataset=dataset, dk_select_useful=dk_select_useful)
+        node_names = data.columns.to_list()
+        X = data.to_numpy()
+    cg = pc(X)
+    with phase("digraph"):
+        M, _nodes = digraph_matrix(cg.G.graph)
+    with phase("pagerank"):
+        scores = PageRank().fit_transform(M.T)
+    with phase("rank sort"):
+        ranked = sorted(zip(node_names, scores), key=lambda t: t[1], reverse=True)
     return {"adj": M, "node_names": node_names, "ranks": [name for name, _ in ranked]}

@@ -26,6 +26,7 @@ from os.path import basename, dirname, exists, join
 import numpy as np
 import pandas as pd
 
+from . import phases
 from .benchmark.evaluation import Evaluator
 from .classes.graph import Node
 
@@ -97,7 +98,10 @@ def load_case(data_path: str, length=None, tdelta: int = 0, is_synthetic: bool =
         case = basename(dirname(data_path))
     rp_name = f"{service}_{metric}_{case}.json"                        # :208
 
+    t_read = time.perf_counter()
     data = pd.read_csv(data_path)                                      # :211-235
+    t_read = time.perf_counter() - t_read
+    t_win = time.perf_counter()
     if "time.1" in data:
         data = data.drop(columns=["time.1"])
     if "rca_" in data_path:
@@ -141,22 +145,34 @@ def load_case(data_path: str, length=None, tdelta: int = 0, is_synthetic: bool =
         sli = "frontend_latency-90"
         if f"{service}_latency" in data:
             sli = f"{service}_latency"
+    # load timings travel with the case: a prefetching loader thread does not share the
+    # caller's phase accounting (rcaeval_amd.phases is per thread)
     return {"data": data, "inject_time": inject_time, "service": service, "metric": metric, "case": case,
-            "sli": sli, "num_node": num_node, "result_name": rp_name}
+            "sli": sli, "num_node": num_node, "result_name": rp_name,
+            "load_s": {"read_csv": t_read, "window": time.perf_counter() - t_win}}
 
 
 def process(data_path: str, method: str, dataset: str, result_path: str, length=None, tdelta: int = 0,
             is_synthetic: bool = False) -> dict:
     """``rq2.py:173-296`` for one case: run the method, dump ``{0: ranks}``."""
     c = load_case(data_path, length=length, tdelta=tdelta, is_synthetic=is_synthetic)
+    return process_loaded(c, method, dataset, result_path)
+
+
+def process_loaded(c: dict, method: str, dataset: str, result_path: str) -> dict:
+    """The method and the JSON dump of a case ``load_case`` returned (``rq2.py:272-289``)."""
+    for k, v in c.get("load_s", {}).items():
+        phases.add(k, v)
     func = methods()[method]
     t0 = time.perf_counter()
     out = func(c["data"], c["inject_time"], dataset=dataset, anomalies=None, dk_select_useful=False,
                sli=c["sli"], verbose=False, n_iter=c["num_node"], args=None)
     seconds = time.perf_counter() - t0
+    phases.add("method (total)", seconds)
     ranks = out.get("ranks")
     rp = join(result_path, c["result_name"])
-    dump_json(filename=rp, data={0: ranks})
+    with phases.phase("json"):
+        dump_json(filename=rp, data={0: ranks})
     return {"path": rp, "ranks": ranks, "seconds": seconds}
 
 
@@ -234,7 +250,7 @@ def evaluate(result_path: str, is_synthetic: bool = False) -> dict:
 
 
 def run(dataset_dir: str, method: str, dataset: str, output: str = "output", length=None, tdelta: int = 0,
-        test: bool = False, rank: int = 0, world: int = 1) -> dict:
+        test: bool = False, rank: int = 0, world: int = 1, prefetch: int = 2) -> dict:
     """Every case of ``dataset_dir`` through ``method``; rank ``r`` of ``world`` takes cases
     ``r, r + world, ...`` of the sorted list. Returns this rank's timings and, on rank 0,
     the evaluation (after a barrier when ``world > 1``)."""
@@ -245,9 +261,30 @@ def run(dataset_dir: str, method: str, dataset: str, output: str = "output", len
     mine = paths[rank::world]
     t0 = time.perf_counter()
     per_case = []
-    for p in mine:
-        per_case.append(process(p, method, dataset, result_path, length=length, tdelta=tdelta,
-                                is_synthetic=is_synthetic))
+    if prefetch > 0 and len(mine) > 1:
+        # loader threads read and window the next cases (pandas' C parser, file IO) while this
+        # thread runs the current case on the GPU (ctypes calls release the GIL); cases are still
+        # processed, and their errors raised, in the sorted order of the sequential loop
+        from collections import deque
+        from concurrent.futures import ThreadPoolExecutor
+
+        def load(p):
+            return load_case(p, length=length, tdelta=tdelta, is_synthetic=is_synthetic)
+
+        with ThreadPoolExecutor(max_workers=prefetch) as ex:
+            queue = deque((p, ex.submit(load, p)) for p in mine[:prefetch])
+            nxt = len(queue)
+            while queue:
+                _, fut = queue.popleft()
+                c = fut.result()
+                if nxt < len(mine):
+                    queue.append((mine[nxt], ex.submit(load, mine[nxt])))
+                    nxt += 1
+                per_case.append(process_loaded(c, method, dataset, result_path))
+    else:
+        for p in mine:
+            per_case.append(process(p, method, dataset, result_path, length=length, tdelta=tdelta,
+                                    is_synthetic=is_synthetic))
     wall = time.perf_counter() - t0
     if world > 1:
         import torch.distributed as dist
@@ -255,6 +292,8 @@ def run(dataset_dir: str, method: str, dataset: str, output: str = "output", len
             dist.barrier()
     out = {"cases": len(paths), "my_cases": len(mine), "wall_s": wall,
            "method_s": [c["seconds"] for c in per_case]}
+    if phases.enabled():
+        out["phases"] = phases.take()
     if rank == 0:
         out.update(evaluate(result_path, is_synthetic=is_synthetic))
         out["avg_speed"] = round(wall / max(len(mine), 1), 4)                # rq2.py:303-306

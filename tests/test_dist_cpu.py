@@ -341,3 +341,70 @@ def test_allgather_rows_packs_ragged_ranks():
     for _, _, _, oxy, obits in res:
         np.testing.assert_array_equal(oxy, want_xy)
         np.testing.assert_array_equal(obits, want_bits)
+
+
+class _FakeK1Engine:
+    """Engine stand-in for dist.sharded_corr (test only): shares of 8 doubles per rank; rank 1
+    fails ('fail') or sizes its share from another plan ('plan')."""
+    device = "cpu"
+
+    def __init__(self, rank, mode):
+        self.rank, self.mode = rank, mode
+
+    def to_device(self, X):
+        import torch
+        return torch.as_tensor(X)
+
+    def corr_shard(self, Xd, rank, world):
+        import torch
+        if self.mode == "fail" and rank == 1:
+            raise MemoryError("injected residue-plane OOM")
+        k = 9 if (self.mode == "plan" and rank == 1) else 8
+        return torch.full((k,), float(rank), dtype=torch.float64)
+
+    def corr_shard_finish(self, gathered, N, n, world):
+        return gathered.clone()
+
+
+def _k1_worker(rank, world, port, mode, q):
+    import torch.distributed as dist
+    from rcaeval_amd import _lib
+    from rcaeval_amd.dist import sharded_corr
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = sharded_corr(_FakeK1Engine(rank, mode), np.zeros((6, 3)))
+        res = ("ok", out.tolist())
+    except MemoryError:
+        res = ("own", None)
+    except _lib.PcgError as e:
+        res = ({_lib.PCG_ERR_PEER: "peer", _lib.PCG_ERR_INVALID: "invalid"}.get(e.code, "other"), None)
+    dist.destroy_process_group()
+    q.put((rank, res))
+
+
+@pytest.mark.parametrize("mode", ["ok", "fail", "plan"])
+def test_sharded_corr_agrees_failures_and_plans(mode):
+    """dist.sharded_corr: shares gathered in rank order; a rank whose corr_shard raises re-raises
+    its own error and every peer raises PCG_ERR_PEER before the all-gather; ranks whose K1 plans
+    give shares of different sizes all raise PCG_ERR_INVALID (nobody waits in the gather)."""
+    import multiprocessing as mp
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_k1_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        kind, out = res[r]
+        if mode == "ok":
+            assert kind == "ok" and out == [float(v) for v in range(world) for _ in range(8)]
+        elif mode == "fail":
+            assert kind == ("own" if r == 1 else "peer"), res
+        else:
+            assert kind == "invalid", res

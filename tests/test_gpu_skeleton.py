@@ -387,6 +387,24 @@ def test_sharded_corr_bitwise_equals_single_gpu(eng, n, N, world):
         np.testing.assert_allclose(C1.cpu().numpy(), np.corrcoef(X.T), rtol=0, atol=2e-14)
 
 
+def test_corr_shard_finish_refuses_exponents_of_another_call(eng):
+    """The CRT finish reads the column exponents pcg_corr_shard left on the handle: a K1 call of
+    another shape in between (or none at all) makes pcg_corr_shard_finish fail with
+    PCG_ERR_INVALID instead of rebuilding C from foreign exponents."""
+    import torch
+    from rcaeval_amd import _lib
+    n, N, world = 300, 1200, 2
+    X = synth.gaussian_sem(n, N, seed=3, w_low=0.1, w_high=0.5)
+    Xd = eng.to_device(X)
+    parts = torch.cat([eng.corr_shard(Xd, r, world) for r in range(world)])
+    eng.corr(eng.to_device(synth.gaussian_sem(400, 1500, seed=4)))
+    with pytest.raises(_lib.PcgError) as e:
+        eng.corr_shard_finish(parts, N, n, world)
+    assert e.value.code == _lib.PCG_ERR_INVALID
+    parts = torch.cat([eng.corr_shard(Xd, r, world) for r in range(world)])
+    assert torch.equal(eng.corr_shard_finish(parts, N, n, world), eng.corr(Xd))
+
+
 @pytest.mark.parametrize("n,N,max_depth", [(300, 1200, -1), (2000, 10000, 2)])
 def test_native_sharded_single_rank_equals_single_gpu(eng, n, N, max_depth):
     """pcg_comm_init / pcg_corr_sharded / pcg_skeleton_sharded (the C-side RCCL driver) on a

@@ -105,3 +105,45 @@ def test_run_deals_cases_round_robin(tmp_path, monkeypatch):
     assert mine == [2, 1, 1] and len(seen) == 4
     res = rq2.evaluate(os.path.join(out_dir, "results"))
     assert sorted(res["eval_data"]["service-fault"])[:2] == ["adservice_cpu", "cartservice_cpu"]
+
+
+def test_run_prefetch_gives_the_sequential_results_in_order(tmp_path, monkeypatch):
+    """Loader threads (prefetch > 0) read and window later cases while the current one runs: the
+    cases reach the method in the sorted order, with the same frames, and the result files are
+    identical to the sequential loop's; a load error surfaces at its own case, after every earlier
+    case was processed (like the reference's loop)."""
+    import json
+    import pandas as pd
+    from rcaeval_amd import phases
+    root, paths = _tree(tmp_path, services=["adservice", "cartservice", "emailservice"], faults=("cpu", "mem"),
+                        cases=2, rows=200)
+    runs = {}
+    for pf in (0, 1, 3):
+        seen = []
+
+        def stub(data, inject_time, **kw):
+            seen.append((inject_time, data.shape, float(data.to_numpy().sum())))
+            return {"ranks": list(data.columns[1:][::-1])}
+        monkeypatch.setattr(rq2, "methods", lambda: {"stub": stub})
+        out_dir = os.path.join(str(tmp_path), f"out{pf}")
+        phases.enable()
+        res = rq2.run(root, "stub", "online-boutique", out_dir, prefetch=pf)
+        phases.enable(False)
+        assert {"read_csv", "window", "method (total)", "json"} <= set(res["phases"])
+        files = sorted(os.listdir(os.path.join(out_dir, "results")))
+        runs[pf] = (seen, files, [json.load(open(os.path.join(out_dir, "results", f))) for f in files])
+    assert runs[0] == runs[1] == runs[3]
+    assert len(runs[0][0]) == len(paths)
+    # a broken case in the middle: earlier cases done, the error raised at its turn
+    bad = sorted(paths)[3]
+    with open(bad, "w") as f:
+        f.write("")
+    seen = []
+
+    def stub2(data, inject_time, **kw):
+        seen.append(1)
+        return {"ranks": []}
+    monkeypatch.setattr(rq2, "methods", lambda: {"stub": stub2})
+    with pytest.raises(pd.errors.EmptyDataError):
+        rq2.run(root, "stub", "online-boutique", os.path.join(str(tmp_path), "outbad"), prefetch=2)
+    assert len(seen) == 3
