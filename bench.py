@@ -204,8 +204,9 @@ def parse():
                     help="skeleton: the headline line (config 5); rq2: every case of an Online-Boutique-shaped "
                          "RQ2 tree through pc_pagerank, cases dealt one per GPU (config 2)")
     ap.add_argument("--rq2-cases", type=int, default=125, help="cases in the synthetic RQ2 tree")
-    ap.add_argument("--rq2-prefetch", type=int, default=2,
-                    help="loader threads reading / windowing the next cases while the GPU runs the current one")
+    ap.add_argument("--rq2-prefetch", type=int, default=4,
+                    help="loader processes reading / windowing the next cases while the GPU runs the current one")
+    ap.add_argument("--rq2-loader", choices=["process", "thread"], default="process")
     ap.add_argument("--rq2-dataset", choices=["online-boutique", "sock-shop"], default="online-boutique",
                     help="shape of the synthetic RQ2 tree (config 2 names both)")
     return ap.parse_args()
@@ -299,7 +300,11 @@ def rq2_main(args):
         torch.cuda.set_device(local)
         dist.init_process_group("gloo")
     get_engine(local)
-    base = os.environ.get("PCG_RQ2_DIR") or tempfile.mkdtemp(prefix="rq2_")
+    base = os.environ.get("PCG_RQ2_DIR") or (tempfile.mkdtemp(prefix="rq2_") if rank == 0 else None)
+    if world > 1:      # every rank reads rank 0's tree
+        box = [base]
+        torch.distributed.broadcast_object_list(box, src=0)
+        base = box[0]
     dataset = args.rq2_dataset
     root = os.path.join(base, "data", dataset)
     ss = dataset == "sock-shop"
@@ -312,19 +317,23 @@ def rq2_main(args):
                                 flavor=dataset)
     if world > 1:
         torch.distributed.barrier()
-    out_dir = os.path.join(base, f"out_{rank}")
+    out_dir = os.path.join(base, "out")         # one results dir: rank 0 evaluates every rank's cases
     # warm-up on this rank's first case (engine, HIP module load), then the timed pass
     first = rq2.list_cases(root)[rank::world][:1]
     for p in first:
         rq2.process(p, "pc_pagerank", dataset, tempfile.mkdtemp(), length=None)
+    from rcaeval_amd import phases
+    if args.rq2_loader == "process":
+        rq2.start_loaders(args.rq2_prefetch)     # spawned before the timed pass, like the engine itself
     if world > 1:
         torch.distributed.barrier()
-    from rcaeval_amd import phases
     phases.enable()
     t0 = time.perf_counter()
-    res = rq2.run(root, "pc_pagerank", dataset, out_dir, rank=rank, world=world, prefetch=args.rq2_prefetch)
+    res = rq2.run(root, "pc_pagerank", dataset, out_dir, rank=rank, world=world, prefetch=args.rq2_prefetch,
+                  loader=args.rq2_loader)
     dt = time.perf_counter() - t0
     phases.enable(False)
+    rq2.stop_loaders()
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -343,7 +352,7 @@ def rq2_main(args):
                                    "read_csv + window + preprocess + PC + orientation + PageRank + JSON",
                        "parallelism": f"cases round-robin over {world} GPU(s)"},
             "seconds_per_case_per_gpu": s_per_case * world,
-            "prefetch_threads": args.rq2_prefetch,
+            "loaders": f"{args.rq2_prefetch} {args.rq2_loader}es" if args.rq2_prefetch else "none (sequential)",
             # rank 0's cases: wall ms per case of each phase (read_csv / window run on the loader
             # threads when prefetch > 0, overlapped with the GPU work of the previous case)
             "phase_ms_per_case": {k: round(1000.0 * v[0] / max(res["my_cases"], 1), 4)

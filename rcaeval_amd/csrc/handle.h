@@ -88,6 +88,8 @@ struct pcg_handle {
     bool xany = false;               // exports queued since the last export_sync
     DevBuf exp_ctr;                  // rows exported so far (device, persists across depths)
     PinBuf ctr_pin, deg_pin, off_pin, cpre_pin, status_pin;
+    DevBuf small_sum;                // single-workgroup small-graph skeleton: summary + counters
+    PinBuf small_pin;                // its host copy
     std::vector<uint64_t> binom_h;   // host copy of the binomial table
     uint8_t *rm_ext = nullptr;       // caller-owned removal-flag buffer (multi-GPU)
     const uint8_t *banned = nullptr; // pcg_set_forbidden_pairs: n x n pairs removed at depth 0

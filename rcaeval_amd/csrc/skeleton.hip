@@ -1902,6 +1902,10 @@ constexpr double F32_U = 5.9604644775390625e-08;   // 2^-24
 #ifndef PCG_TGF_SGPR
 #define PCG_TGF_SGPR 0x10 // k_level_lds_f depths (bit 1 << d) whose per-y bookkeeping is in wave lane masks
 #endif
+#ifndef PCG_TGF_PREFETCH
+#define PCG_TGF_PREFETCH 0   // k_level_lds_f depths (bit 1 << d) whose per-lane y loop prefetches row t + 1
+                             // (depth 3: 0.703 vs 0.698 ms without it; measured no gain, off)
+#endif
 #ifndef PCG_TGF_SPLIT
 #define PCG_TGF_SPLIT 1   // k_level_lds_f, one candidate window per wave: y outside the window without the
                           // dead-candidate selects (depth 4: 2.24 -> 2.09 ms once the rare-path values were opaque)
@@ -2380,15 +2384,35 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
             // 2: windows differ (lane masks, such lanes to the rare path); 3: per-lane live and
             // dependence bits (the depths where dedup skips are common: a lane that owns y is
             // not sent down the rare path just to count its skips)
-            auto ystep = [&](int t, auto ym_tag) {
+            // the LDS operands of one y (row t of A~): the candidates' entries, the T entries, the
+            // {A~_yy, A~_xy} pair and the local adjacency mask. Loaded apart from their use so the
+            // y loop can issue row t + 1's reads before row t's arithmetic (PCG_TGF_PREFETCH)
+            struct YPre {
+                f2v sc[NQ];
+                float mT[DT];
+                f2v md;
+                Mask lm;
+            };
+            auto yload = [&](int t) {
+                YPre p;
+                const float *Mt = M + t * DS;
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) p.sc[q] = *reinterpret_cast<const f2v *>(Mt + cbase + 2 * q);
+#pragma unroll
+                for (int j = 0; j < DT; ++j) p.mT[j] = Mt[T[j]];
+                p.md = *reinterpret_cast<const f2v *>(Mdx + 2 * t);
+                p.lm = lmask[t];
+                return p;
+            };
+            auto ystep = [&](int t, auto ym_tag, const YPre &pre) {
                 constexpr int YM = decltype(ym_tag)::value;
                 const float *Mt = M + t * DS;
                 f2v sc[NQ];
 #pragma unroll
-                for (int q = 0; q < NQ; ++q) sc[q] = *reinterpret_cast<const f2v *>(Mt + cbase + 2 * q);
+                for (int q = 0; q < NQ; ++q) sc[q] = pre.sc[q];
                 float vT[DT], mT[DT];
 #pragma unroll
-                for (int j = 0; j < DT; ++j) mT[j] = Mt[T[j]];
+                for (int j = 0; j < DT; ++j) mT[j] = pre.mT[j];
                 // (|v_T|^2, u_T.v_T) accumulated as one packed pair: vu[i] = {v_i, u_i}
                 f2v acc = {0.0f, 0.0f};
 #pragma unroll
@@ -2400,7 +2424,7 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
                     const f2v vu = {v, uTf[i]}, vb = {v, v};
                     acc = __builtin_elementwise_fma(vu, vb, acc);
                 }
-                const f2v b2 = *reinterpret_cast<const f2v *>(Mdx + 2 * t) - acc;   // {byy, bxy}
+                const f2v b2 = pre.md - acc;   // {byy, bxy}
                 const float byy = b2[0];
                 const float bxy = b2[1];
 #pragma unroll
@@ -2410,7 +2434,7 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
                     for (int q = 0; q < NQ; ++q) sc[q] = __builtin_elementwise_fma(-lcp[q][i], vb, sc[q]);
                 }
                 const f2v byy2 = {byy, byy}, bxy2 = {bxy, bxy};
-                const Mask lm = lmask[t];
+                const Mask lm = pre.lm;
                 if constexpr (YM == 3) {
                     unsigned dp = 0;
 #pragma unroll
@@ -2484,18 +2508,29 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
             using Y2 = std::integral_constant<int, 2>;
             using Y3 = std::integral_constant<int, 3>;
             if (!SG) {
-                for (int t = 0; t < D; ++t) ystep(t, Y3{});
+                if constexpr ((PCG_TGF_PREFETCH >> DM) & 1) {
+                    // software-pipelined: row t + 1's LDS reads are in flight during row t's
+                    // arithmetic (the loop was LDS-latency bound: s_waitcnt right after the reads)
+                    YPre cur = yload(0);
+                    for (int t = 0; t < D; ++t) {
+                        const YPre nxt = yload(t + 1 < D ? t + 1 : t);
+                        ystep(t, Y3{}, cur);
+                        cur = nxt;
+                    }
+                } else {
+                    for (int t = 0; t < D; ++t) ystep(t, Y3{}, yload(t));
+                }
             } else if (uni && PCG_TGF_SPLIT) {
                 // the window [cb0, cb0 + NC) is the only place a candidate can be y: outside it the
                 // check needs no per-candidate "c == y" selects (YM 0)
                 const int w0 = min(cb0, D), w1 = min(cb0 + NC, D);
-                for (int t = 0; t < w0; ++t) ystep(t, Y0{});
-                for (int t = w0; t < w1; ++t) ystep(t, Y1{});
-                for (int t = w1; t < D; ++t) ystep(t, Y0{});
+                for (int t = 0; t < w0; ++t) ystep(t, Y0{}, yload(t));
+                for (int t = w0; t < w1; ++t) ystep(t, Y1{}, yload(t));
+                for (int t = w1; t < D; ++t) ystep(t, Y0{}, yload(t));
             } else if (uni) {
-                for (int t = 0; t < D; ++t) ystep(t, Y1{});
+                for (int t = 0; t < D; ++t) ystep(t, Y1{}, yload(t));
             } else {
-                for (int t = 0; t < D; ++t) ystep(t, Y2{});
+                for (int t = 0; t < D; ++t) ystep(t, Y2{}, yload(t));
             }
         };
         if constexpr (TG == 4) {
@@ -3634,6 +3669,616 @@ __global__ __launch_bounds__(256) void k_exact(LevelArgs a) {
     }
     if (nexact) atomicAdd(&a.ctr->exact, nexact);
     if (nindep) atomicAdd(&a.ctr->indep, nindep);
+}
+
+// ---------------------------------------------------------------------------------------
+// Small graphs (n <= 64: the RQ2 cases, 30-49 metrics): the WHOLE stable skeleton in one
+// workgroup launch. The multi-kernel level loop costs ~90 us of launches and host round trips
+// per depth whatever the work; an RQ2 case has 6-8 depths of 10^2..10^4 tests. Here C, the
+// adjacency, the neighbour lists and the per-side unions live in LDS, a depth ends at a block
+// barrier, and the host waits once. Same semantics as the level loop: the reference's visit
+// order and memo (x evaluates (x, y, S) unless y < x and S within adj(y); an owner x < y with S
+// within adj(y) also serves y's visit), the fp64 threshold decision with its band and guard, the
+// exact LU path (numpy.linalg.inv order, the reference p expression) in the wave for the band,
+// deferred removal, per-side unions, near-alpha records, FULL_P / RECORD / EXACT_ALL.
+constexpr int SMALL_N = 64;           // nodes: one u64 adjacency word per node
+constexpr int SMALL_MAXD = 16;        // deepest conditioning set here (deeper: the level loop reruns)
+constexpr int SMALL_LANE_D = 6;       // depths 1..6: one lane per test (chunks of SMALL_K sets of one (x, y))
+constexpr int SMALL_K = 32;
+constexpr int SMALL_WAVES = 8;        // 512 threads: two waves per SIMD (256 VGPRs: the fused solves fit unspilled)
+constexpr int SMALL_SLOT = (SMALL_MAXD + 2) * (SMALL_MAXD + 2) + 3 * (SMALL_MAXD + 2);   // doubles per wave
+constexpr int SMALL_QCAP = 1024;      // band tests per depth waiting for the exact path (overflow: the level loop reruns)
+static_assert(SMALL_SLOT >= SMALL_MAXD * (SMALL_MAXD + 1), "the wave slot holds the L rows too");
+
+struct SmallArgs {
+    const double *C;
+    int64_t ldc;
+    int n;
+    int max_depth;
+    double alpha, tau;
+    const uint8_t *banned;            // n x n pairs forbidden both ways, or null
+    const uint64_t *binom;
+    int8_t *rl;                       // n x n removal depths (-1 = kept)
+    int32_t *xy;                      // exported (x, y) of removed pairs with a non-empty side union
+    uint64_t *bits;                   // their union words (W = 1)
+    pcg_record *nearl, *records;
+    int64_t near_cap, rec_cap, rec_mod, rec_res;
+    unsigned long long *ctr;          // [0] near-alpha, [1] records (cumulative over the run)
+    int fullp, record, exact_all;
+    // per depth d (device memory, 4 doubles each): the threshold band on r^2 (lo2, hi2),
+    // sqrt(N - d - 3), and 1.0 when N - d - 3 < 0 (a dynamically indexed kernel-argument array
+    // would be copied to scratch)
+    const double *depth_cst;
+    struct SmallSummary *sum;
+};
+
+struct SmallDepth {
+    double lo2, hi2, sqrt_dof;
+    bool dof_negative;
+};
+
+struct SmallSummary {
+    int32_t levels, status;           // status: 1 singular, 2 math domain, 4 deeper than SMALL_MAXD / queue full
+    int64_t xrows;                    // exported sepset rows
+    int64_t tests[PCG_MAX_LEVELS], calls[PCG_MAX_LEVELS], indep[PCG_MAX_LEVELS], exact[PCG_MAX_LEVELS];
+    int64_t near_alpha[PCG_MAX_LEVELS], edges_after[PCG_MAX_LEVELS];
+    int32_t max_degree[PCG_MAX_LEVELS];
+    uint64_t stamp[PCG_MAX_LEVELS + 1];  // wall-clock ticks (100 MHz) at the depth boundaries
+    int32_t deg[PCG_MAX_LEVELS][SMALL_N];
+};
+
+// the reference p expression out of line: inlined, its erfc polynomial constants are hoisted into
+// registers across the callers' loops (hundreds of VGPRs spilled)
+__device__ __attribute__((noinline)) double small_pvalue(double r, double sqrt_dof, int *err) {
+    return pcg_pvalue_from_r(r, sqrt_dof, err);
+}
+
+__device__ __forceinline__ int small_decide(const SmallArgs &a, const SmallDepth &k, double cxy, double cxx, double cyy,
+                                            double kg, double *p) {
+    if (a.exact_all) return 2;
+    const double den = cxx * cyy;
+    if (!(den > 0.0)) return 2;
+    const double num = cxy * cxy;
+    if (!(den - num > kg)) return 2;
+    if (!a.fullp) {
+        if (num < k.lo2 * den) return 1;
+        if (num > k.hi2 * den) return 0;
+        return 2;
+    }
+    const double r = cxy / sqrt(den);
+    int err = 0;
+    const double pv = small_pvalue(r, k.sqrt_dof, &err);
+    if (err) return 2;
+    *p = pv;
+    return pv > a.alpha ? 1 : 0;
+}
+
+__device__ __forceinline__ bool small_rec_on(const SmallArgs &a, int lo, int hi) {
+    return a.record && (a.rec_mod <= 1 || ((int64_t)lo * a.n + hi) % a.rec_mod == a.rec_res);
+}
+
+// the exact path of one test (lo < hi, S ascending global ids in sg) in the wave's slot: lanes
+// gather the m x m matrix, lane 0 factors; returns 0 dependent, 1 independent, -1 error (flagged)
+__device__ __attribute__((noinline)) int small_exact(const SmallArgs &a, const SmallDepth &kd, const double *Cf, int n,
+                                                     int d, int lo, int hi,
+                           unsigned long long Sg, double *slot, int *status, double *pout) {
+    const int lane = threadIdx.x & 63, m = d + 2;
+    double *A = slot, *B0 = slot + m * m, *B1 = B0 + m;
+    int *var = reinterpret_cast<int *>(B1 + m);
+    wave_sync();
+    if (lane == 0) {
+        var[0] = lo;
+        var[1] = hi;
+        unsigned long long s = Sg;
+        for (int q = 0; q < d; ++q) {
+            var[2 + q] = __builtin_ctzll(s);
+            s &= s - 1;
+        }
+    }
+    wave_sync();
+    for (int k = lane; k < m * m; k += 64) {
+        const int r = k / m, c = k - r * m;
+        A[k] = Cf[var[r] * n + var[c]];
+    }
+    wave_sync();
+    int res = 0;
+    if (lane == 0) {
+        // k_exact's order of checks: singular, then a negative determinant ratio or N - d - 3 < 0
+        double pv = __builtin_nan("");
+        int err = 0;
+        int piv[PCG_MAX_LEVEL_DEPTH + 2];
+        double i00, i01, i11;
+        if (pcg_lu_inv01(A, m, piv, B0, B1, &i00, &i01, &i11)) {
+            err = 1;
+        } else {
+            const double prod = i00 * i11;
+            if (prod < 0.0 || kd.dof_negative) err = 2;
+            else pv = small_pvalue(-i01 / sqrt(prod), kd.sqrt_dof, &err);
+        }
+        if (err) {
+            atomicOr(status, err);
+            res = -1;
+        } else {
+            *pout = pv;
+            res = pv > a.alpha ? 1 : 0;
+        }
+    }
+    wave_sync();
+    return __shfl(res, 0);
+}
+
+__device__ __forceinline__ void small_sorted_set(unsigned long long Sg, int d, int (&sg)[PCG_MAX_DEPTH]) {
+#pragma unroll
+    for (int q = 0; q < PCG_MAX_DEPTH; ++q) {
+        sg[q] = (q < d && Sg) ? __builtin_ctzll(Sg) : -1;
+        if (q < d && Sg) Sg &= Sg - 1;
+    }
+}
+
+// (x, y | S) from the correlation block in LDS, one lane: Cholesky of C_SS row by row with the
+// solves for x and y fused (only L, 1/diag and the two solution vectors live); the fp64 kernels'
+// guard and band. 0 dependent, 1 independent, 2 exact path
+template <int DM>
+__device__ __forceinline__ int small_lane_eval(const SmallArgs &a, const SmallDepth &kd, const double *Cf, int n, int d,
+                                               int x, int y, const int (&sg)[DM], double *p) {
+    double L[DM][DM], rinv[DM], u[DM], v[DM];
+    double uu = 0.0, vv = 0.0, uv = 0.0, gmin = 1.0;
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < DM; ++i) {
+        if (i < d) {
+            const double *Ci = Cf + sg[i] * n;
+            double s = Ci[sg[i]];
+#pragma unroll
+            for (int j = 0; j < i; ++j) {
+                double t = Ci[sg[j]];
+#pragma unroll
+                for (int q = 0; q < j; ++q) t -= L[i][q] * L[j][q];
+                L[i][j] = t * rinv[j];
+                s -= L[i][j] * L[i][j];
+            }
+            ok = ok && (s > 0.0);
+            gmin = fmin(gmin, s);
+            rinv[i] = 1.0 / sqrt(s);
+            double tu = Ci[x], tv = Ci[y];
+#pragma unroll
+            for (int q = 0; q < i; ++q) {
+                tu -= L[i][q] * u[q];
+                tv -= L[i][q] * v[q];
+            }
+            u[i] = tu * rinv[i];
+            v[i] = tv * rinv[i];
+            uu += u[i] * u[i];
+            vv += v[i] * v[i];
+            uv += u[i] * v[i];
+        }
+    }
+    if (!ok) return 2;
+    return small_decide(a, kd, Cf[x * n + y] - uv, Cf[x * n + x] - uu, Cf[y * n + y] - vv, a.tau / gmin, p);
+}
+
+// one conditioning set S (local positions `mask` within x's neighbour list, |S| = d) of node x,
+// lanes = the neighbour columns (lane D = x): the k_level_wave solve, then every live y at once
+template <int MD>
+__device__ void small_set(const SmallArgs &a, const SmallDepth &kd, const double *Cf, const uint64_t *adjm, const uint8_t *nbx, int x,
+                          int D, int d, int tx, unsigned long long mask, double *slot, uint64_t *uni, uint64_t *rmb,
+                          int *status, unsigned long long &tests, unsigned long long &indep,
+                          unsigned long long &exact, unsigned long long &nearc) {
+    const int lane = threadIdx.x & 63, n = a.n;
+    const int colg = lane < D ? nbx[lane] : x;
+    double v[MD];
+    double vv = 0.0, uv = 0.0, gmin = 1.0;
+    bool ok = true;
+    unsigned long long m = mask, Sg = 0;
+    const bool member = lane < D && ((mask >> lane) & 1ull);
+    const int mypos = member ? __popcll(mask & ((1ull << lane) - 1ull)) : -1;
+    double *Lm = slot;
+    constexpr int LS = MD + 1;
+#pragma unroll
+    for (int i = 0; i < MD; ++i) {
+        if (i < d) {
+            const int si = __builtin_ctzll(m);
+            m &= m - 1;
+            const int sg = nbx[si];
+            Sg |= 1ull << sg;
+            double t = Cf[sg * n + colg];
+            const double *Li = Lm + i * LS;
+#pragma unroll
+            for (int q = 0; q < i; ++q) t -= Li[q] * v[q];
+            const double piv = readlane_f64(t, si);
+            ok = ok && (piv > 0.0);
+            gmin = fmin(gmin, piv);
+            v[i] = t * (1.0 / sqrt(piv));
+            vv += v[i] * v[i];
+            uv += readlane_f64(v[i], D) * v[i];
+            if (mypos > i) Lm[mypos * LS + i] = v[i];
+            wave_sync();
+        }
+    }
+    const double cxx = Cf[x * n + x] - readlane_f64(vv, D);
+    const double kg = a.tau / gmin;
+    bool live = lane < D && !member;
+    const bool in_y = live && ((adjm[colg] & Sg) == Sg);
+    live = live && !(lane < tx && in_y);
+    tests += live;
+    int dec = 2;
+    double p = 0.0;
+    if (live && ok) dec = small_decide(a, kd, Cf[x * n + colg] - uv, cxx, Cf[colg * n + colg] - vv, kg, &p);
+    const int lo_ = x < colg ? x : colg, hi_ = x < colg ? colg : x;
+    if (live && dec != 2 && a.fullp) {
+        if (d <= PCG_MAX_DEPTH && (small_rec_on(a, lo_, hi_) || fabs(p - a.alpha) < 1e-9)) {
+            int sgl[PCG_MAX_DEPTH];
+            small_sorted_set(Sg, d, sgl);
+            if (small_rec_on(a, lo_, hi_)) push_record(a.records, a.rec_cap, &a.ctr[1], lo_, hi_, d, sgl, p);
+            if (fabs(p - a.alpha) < 1e-9) push_record(a.nearl, a.near_cap, &a.ctr[0], lo_, hi_, d, sgl, p);
+        }
+        if (fabs(p - a.alpha) < 1e-9) ++nearc;
+    }
+    if (live && dec == 1) {
+        ++indep;
+        atomicOr(&uni[x * SMALL_N + colg], Sg);
+        if (in_y && lane >= tx) atomicOr(&uni[colg * SMALL_N + x], Sg);
+        atomicOr(&rmb[x], 1ull << colg);
+        atomicOr(&rmb[colg], 1ull << x);
+    }
+    // the exact path of this set's remaining tests, one at a time in the wave's slot (the L rows
+    // are no longer needed)
+    unsigned long long need = __ballot(live && dec == 2);
+    while (need) {
+        const int L = __builtin_ctzll(need);
+        need &= need - 1;
+        const int yg = nbx[L];
+        const int lo = x < yg ? x : yg, hi = x < yg ? yg : x;
+        double pv = 0.0;
+        const int r = small_exact(a, kd, Cf, n, d, lo, hi, Sg, slot, status, &pv);
+        if (lane == 0) {
+            ++exact;
+            if (r >= 0) {
+                int sgl[PCG_MAX_DEPTH];
+                small_sorted_set(Sg, d, sgl);
+                if (d <= PCG_MAX_DEPTH && small_rec_on(a, lo, hi))
+                    push_record(a.records, a.rec_cap, &a.ctr[1], lo, hi, d, sgl, pv);
+                if (fabs(pv - a.alpha) < 1e-9) {
+                    ++nearc;
+                    if (d <= PCG_MAX_DEPTH) push_record(a.nearl, a.near_cap, &a.ctr[0], lo, hi, d, sgl, pv);
+                }
+                if (r == 1) {
+                    ++indep;
+                    atomicOr(&uni[x * SMALL_N + yg], Sg);
+                    if (((adjm[yg] & Sg) == Sg) && L >= tx) atomicOr(&uni[yg * SMALL_N + x], Sg);
+                    atomicOr(&rmb[x], 1ull << yg);
+                    atomicOr(&rmb[yg], 1ull << x);
+                }
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(SMALL_WAVES * 64, 1) void k_pc_small(SmallArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int n = a.n, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    double *Cf = reinterpret_cast<double *>(smem);                                  // n x n
+    uint64_t *uni = reinterpret_cast<uint64_t *>(Cf + n * n);                         // 64 x 64 side unions
+    uint64_t *adjm = uni + SMALL_N * SMALL_N;                                         // 64
+    uint64_t *rmb = adjm + SMALL_N;                                                   // 64: this depth's removals
+    uint64_t *wpre = rmb + SMALL_N;                                                   // 65: work prefix over x
+    uint64_t *bin = wpre + SMALL_N + 1;                                               // C(c, k), c < 64, k <= MAXD
+    uint64_t *qS = bin + SMALL_N * (SMALL_MAXD + 1);                                  // band queue: S masks
+    double *slots = reinterpret_cast<double *>(qS + SMALL_QCAP);                      // waves x SMALL_SLOT
+    int *deg = reinterpret_cast<int *>(slots + SMALL_WAVES * SMALL_SLOT);             // 64
+    int *misc = deg + SMALL_N;                                                        // 16 ints
+    uint16_t *qxy = reinterpret_cast<uint16_t *>(misc + 16);                          // band queue: x | y << 8
+    int8_t *rlv = reinterpret_cast<int8_t *>(qxy + SMALL_QCAP);                       // 64 x 64
+    uint8_t *nb = reinterpret_cast<uint8_t *>(rlv + SMALL_N * SMALL_N);               // 64 x 64
+    unsigned long long *cnt = reinterpret_cast<unsigned long long *>(
+        (reinterpret_cast<uintptr_t>(nb + SMALL_N * SMALL_N) + 7) & ~(uintptr_t)7);  // next unit, tests, indep, exact, near, xrows, queue
+    SmallSummary *sum = a.sum;
+    int &status = misc[0];
+
+    for (int e = tid; e < n * n; e += blockDim.x) Cf[e] = a.C[(int64_t)(e / n) * a.ldc + e % n];
+    for (int e = tid; e < SMALL_N * SMALL_N; e += blockDim.x) {
+        uni[e] = 0;
+        rlv[e] = -1;
+    }
+    for (int e = tid; e < SMALL_N * (SMALL_MAXD + 1); e += blockDim.x)
+        bin[e] = pcg_binom(a.binom, e / (SMALL_MAXD + 1), e % (SMALL_MAXD + 1));
+    const unsigned long long all = n == 64 ? ~0ull : ((1ull << n) - 1ull);
+    for (int x = tid; x < SMALL_N; x += blockDim.x) {
+        adjm[x] = x < n ? all & ~(1ull << x) : 0ull;
+        rmb[x] = 0;
+        deg[x] = x < n ? n - 1 : 0;
+        for (int k = 0, c = 0; k < n; ++k)
+            if (k != x && x < n) nb[x * SMALL_N + c++] = (uint8_t)k;
+    }
+    if (tid == 0) {
+        status = 0;
+        for (int k = 0; k < 8; ++k) cnt[k] = 0;
+        sum->xrows = 0;
+    }
+    __syncthreads();
+    auto B = [&](int c, int k) -> uint64_t { return (c < k || c < 0) ? 0ull : bin[c * (SMALL_MAXD + 1) + k]; };
+    // an independent (x, y | S): removal flags both ways, x's side union, and y's when x's visit
+    // also served y's (S within adj(y), y > x)
+    auto indep_effects = [&](int x, int y, unsigned long long Sg, bool in_y) {
+        atomicOr(&rmb[x], 1ull << y);
+        atomicOr(&rmb[y], 1ull << x);
+        if (Sg) {
+            atomicOr(&uni[x * SMALL_N + y], Sg);
+            if (in_y && y > x) atomicOr(&uni[y * SMALL_N + x], Sg);
+        }
+    };
+    int levels = 0;
+    for (int d = 0;; ++d) {
+        // the reference's loop condition (max_degree() - 1 > depth - 1), the depth cap
+        int maxdeg = 0;
+        for (int x = 0; x < n; ++x) maxdeg = max(maxdeg, deg[x]);
+        if (!(maxdeg - 1 > d - 1) || (a.max_depth >= 0 && d > a.max_depth) || d >= PCG_MAX_LEVELS) break;
+        if (d > SMALL_MAXD) {
+            if (tid == 0) status |= 4;
+            break;
+        }
+        levels = d + 1;
+        const bool lanewise = d >= 1 && d <= SMALL_LANE_D;
+        SmallDepth kd;
+        kd.lo2 = a.depth_cst[4 * d];
+        kd.hi2 = a.depth_cst[4 * d + 1];
+        kd.sqrt_dof = a.depth_cst[4 * d + 2];
+        kd.dof_negative = a.depth_cst[4 * d + 3] != 0.0;
+        if (wv == 0) {   // work prefix over x, calls, the degree snapshot
+            const int D = lane < n ? deg[lane] : 0;
+            const uint64_t cd = D >= 1 ? B(D - 1, d) : 0ull;
+            const uint64_t units = d == 0 ? 0ull : lanewise ? (uint64_t)D * ((cd + SMALL_K - 1) / SMALL_K) : B(D, d);
+            uint64_t incl = units, csum = cd * (uint64_t)D;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint64_t t = __shfl_up(incl, o);
+                if (lane >= o) incl += t;
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) csum += __shfl_xor(csum, o);
+            wpre[lane + 1] = incl;
+            if (lane == 0) wpre[0] = 0;
+            if (lane < n) sum->deg[d][lane] = D;
+            if (lane == 0) {
+                sum->calls[d] = (int64_t)csum;
+                sum->max_degree[d] = maxdeg;
+                sum->stamp[d] = wall_clock64();
+                cnt[0] = 0;
+                cnt[6] = 0;
+            }
+        }
+        __syncthreads();
+        unsigned long long tests = 0, indep = 0, exact = 0, nearc = 0;
+        if (d == 0 || lanewise) {
+            // one lane per test: the pairs at depth 0; chunks of SMALL_K consecutive sets (colex over
+            // the positions of adj(x) \ {y}) of one (x, y) at depths 1..SMALL_LANE_D. Band tests
+            // queue for the exact path below.
+            const uint64_t total = d == 0 ? (uint64_t)n * (n - 1) / 2 : wpre[n];
+            for (uint64_t u = tid; u < total; u += blockDim.x) {
+                int x = 0, y = 0;
+                unsigned long long mask = 0;
+                uint64_t r0 = 0, r1 = 1;
+                int D = 0, yi = 0;
+                if (d == 0) {
+                    int r = (int)u;
+                    while (r >= n - 1 - x) { r -= n - 1 - x; ++x; }
+                    y = x + 1 + r;
+                } else {
+                    int lo = 0, hi = n;
+                    while (hi - lo > 1) {
+                        const int mid = (lo + hi) >> 1;
+                        if (wpre[mid] <= u) lo = mid; else hi = mid;
+                    }
+                    x = lo;
+                    D = deg[x];
+                    const uint64_t cd = B(D - 1, d), cpy = (cd + SMALL_K - 1) / SMALL_K;
+                    const uint64_t local = u - wpre[x];
+                    yi = (int)(local / cpy);
+                    y = nb[x * SMALL_N + yi];
+                    r0 = (local % cpy) * SMALL_K;
+                    r1 = min(cd, r0 + SMALL_K);
+                    uint64_t rr = r0;                 // colex unrank over D - 1 positions
+                    int hi_ = D - 1;
+                    for (int ii = d - 1; ii >= 0; --ii) {
+                        int l2 = ii, up = hi_ - 1;
+                        while (l2 < up) {
+                            const int mid = (l2 + up + 1) >> 1;
+                            if (B(mid, ii + 1) <= rr) l2 = mid; else up = mid - 1;
+                        }
+                        mask |= 1ull << l2;
+                        rr -= B(l2, ii + 1);
+                        hi_ = l2;
+                    }
+                }
+                for (uint64_t r = r0; r < r1; ++r) {
+                    // S: positions q of adj(x) \ {y} -> neighbour index q (< yi) or q + 1
+                    int sg[SMALL_LANE_D];
+                    unsigned long long Sg = 0, m = mask;
+#pragma unroll
+                    for (int i = 0; i < SMALL_LANE_D; ++i) {
+                        sg[i] = x;
+                        if (i < d) {
+                            const int q = __builtin_ctzll(m);
+                            m &= m - 1;
+                            sg[i] = nb[x * SMALL_N + (q < yi ? q : q + 1)];
+                            Sg |= 1ull << sg[i];
+                        }
+                    }
+                    const bool in_y = d > 0 && (adjm[y] & Sg) == Sg;
+                    if (!(d > 0 && y < x && in_y)) {     // y's visit evaluates it otherwise
+                        ++tests;
+                        double p = 0.0;
+                        int dec;
+                        if (d <= 2) dec = small_lane_eval<2>(a, kd, Cf, n, d, x, y, reinterpret_cast<const int(&)[2]>(sg), &p);
+                        else if (d <= 4) dec = small_lane_eval<4>(a, kd, Cf, n, d, x, y, reinterpret_cast<const int(&)[4]>(sg), &p);
+                        else dec = small_lane_eval<SMALL_LANE_D>(a, kd, Cf, n, d, x, y, sg, &p);
+                        const int lo_ = x < y ? x : y, hi_ = x < y ? y : x;
+                        if (dec == 2) {
+                            const unsigned long long slot = atomicAdd(&cnt[6], 1ull);
+                            if (slot < SMALL_QCAP) {
+                                qxy[slot] = (uint16_t)(x | (y << 8));
+                                qS[slot] = Sg;
+                            } else {
+                                atomicOr(&status, 4);    // more band tests than the queue holds
+                            }
+                        } else {
+                            if (a.fullp) {
+                                const bool near = fabs(p - a.alpha) < 1e-9;
+                                if (small_rec_on(a, lo_, hi_) || near) {
+                                    int sgl[PCG_MAX_DEPTH];
+                                    small_sorted_set(Sg, d, sgl);
+                                    if (small_rec_on(a, lo_, hi_))
+                                        push_record(a.records, a.rec_cap, &a.ctr[1], lo_, hi_, d, sgl, p);
+                                    if (near) push_record(a.nearl, a.near_cap, &a.ctr[0], lo_, hi_, d, sgl, p);
+                                }
+                                nearc += near;
+                            }
+                            if (dec == 1) {
+                                ++indep;
+                                indep_effects(x, y, Sg, in_y);
+                            }
+                        }
+                    }
+                    if (d > 0) {                      // next set (Gosper)
+                        const unsigned long long c0 = mask & (0ull - mask);
+                        const unsigned long long rr2 = mask + c0;
+                        mask = (((rr2 ^ mask) >> 2) >> __builtin_ctzll(mask)) | rr2;
+                    }
+                }
+            }
+            __syncthreads();
+            // the exact path of the queued band tests: one wave per test
+            const int qn = (int)min(cnt[6], (unsigned long long)SMALL_QCAP);
+            for (int i = wv; i < qn; i += SMALL_WAVES) {
+                const int x = qxy[i] & 255, y = qxy[i] >> 8;
+                const unsigned long long Sg = qS[i];
+                const int lo = x < y ? x : y, hi = x < y ? y : x;
+                double pv = 0.0;
+                const int r = small_exact(a, kd, Cf, n, d, lo, hi, Sg, slots + wv * SMALL_SLOT, &status, &pv);
+                if (lane == 0) {
+                    ++exact;
+                    if (r >= 0) {
+                        int sgl[PCG_MAX_DEPTH];
+                        small_sorted_set(Sg, d, sgl);
+                        if (small_rec_on(a, lo, hi)) push_record(a.records, a.rec_cap, &a.ctr[1], lo, hi, d, sgl, pv);
+                        if (fabs(pv - a.alpha) < 1e-9) {
+                            ++nearc;
+                            push_record(a.nearl, a.near_cap, &a.ctr[0], lo, hi, d, sgl, pv);
+                        }
+                        if (r == 1) {
+                            ++indep;
+                            indep_effects(x, y, Sg, d > 0 && (adjm[y] & Sg) == Sg);
+                        }
+                    }
+                }
+            }
+        } else {
+            const uint64_t total = wpre[n];
+            double *slot = slots + wv * SMALL_SLOT;
+            for (;;) {
+                unsigned long long u = 0;
+                if (lane == 0) u = atomicAdd(&cnt[0], 1ull);
+                u = __shfl(u, 0);
+                if (u >= total) break;
+                int lo = 0, hi = n;           // wpre[lo] <= u < wpre[lo + 1]
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (wpre[mid] <= u) lo = mid; else hi = mid;
+                }
+                const int x = lo, D = deg[x];
+                uint64_t rr = u - wpre[x];
+                unsigned long long mask = 0;  // colex unrank (wave-uniform)
+                int hi_ = D;
+                for (int ii = d - 1; ii >= 0; --ii) {
+                    int lo2 = ii, up = hi_ - 1;
+                    while (lo2 < up) {
+                        const int mid = (lo2 + up + 1) >> 1;
+                        if (B(mid, ii + 1) <= rr) lo2 = mid; else up = mid - 1;
+                    }
+                    mask |= 1ull << lo2;
+                    rr -= B(lo2, ii + 1);
+                    hi_ = lo2;
+                }
+                const int tx = __popcll(adjm[x] & ((1ull << x) - 1ull));
+                const uint8_t *nbx = nb + x * SMALL_N;
+                if (d <= 8)
+                    small_set<8>(a, kd, Cf, adjm, nbx, x, D, d, tx, mask, slot, uni, rmb, &status, tests, indep, exact, nearc);
+                else
+                    small_set<SMALL_MAXD>(a, kd, Cf, adjm, nbx, x, D, d, tx, mask, slot, uni, rmb, &status, tests, indep,
+                                          exact, nearc);
+            }
+        }
+        // counters (lane 0 of each wave holds the exact-path counts; every lane its tests / indep)
+        tests = wave_sum(tests);
+        indep = wave_sum(indep);
+        exact = wave_sum(exact);
+        nearc = wave_sum(nearc);
+        if (lane == 0) {
+            atomicAdd(&cnt[1], tests);
+            atomicAdd(&cnt[2], indep);
+            atomicAdd(&cnt[3], exact);
+            atomicAdd(&cnt[4], nearc);
+        }
+        __syncthreads();
+        // the level barrier: forbidden pairs leave at the end of depth 0, removals applied
+        // (SkeletonDiscovery.py:141-144), removed pairs' non-empty side unions exported, the next
+        // depth's neighbour lists
+        if (d == 0 && a.banned)
+            for (int e = tid; e < n * n; e += blockDim.x) {
+                const int x = e / n, y = e - x * n;
+                if (x != y && a.banned[e]) atomicOr(&rmb[x], 1ull << y);
+            }
+        __syncthreads();
+        if (tid < n) {
+            const int x = tid;
+            const unsigned long long gone = rmb[x] & adjm[x];
+            for (unsigned long long g = gone; g; g &= g - 1) {
+                const int y = __builtin_ctzll(g);
+                rlv[x * SMALL_N + y] = (int8_t)d;
+                const uint64_t un = uni[x * SMALL_N + y];
+                if (d >= 1 && un) {
+                    const unsigned long long r = atomicAdd(&cnt[5], 1ull);
+                    a.xy[2 * r] = x;
+                    a.xy[2 * r + 1] = y;
+                    a.bits[r] = un;
+                }
+            }
+            adjm[x] &= ~gone;
+            rmb[x] = 0;
+            deg[x] = __popcll(adjm[x]);
+            int c = 0;
+            for (unsigned long long g = adjm[x]; g; g &= g - 1) nb[x * SMALL_N + c++] = (uint8_t)__builtin_ctzll(g);
+        }
+        __syncthreads();              // every export read its union word before the clear
+        for (int e = tid; e < SMALL_N * SMALL_N; e += blockDim.x) uni[e] = 0;
+        __syncthreads();
+        if (tid == 0) {
+            int64_t edges = 0;
+            for (int x = 0; x < n; ++x) edges += deg[x];
+            sum->tests[d] = (int64_t)cnt[1];
+            sum->indep[d] = (int64_t)cnt[2];
+            sum->exact[d] = (int64_t)cnt[3];
+            sum->near_alpha[d] = (int64_t)cnt[4];
+            sum->edges_after[d] = edges / 2;
+            sum->stamp[d + 1] = wall_clock64();
+            for (int k = 1; k < 5; ++k) cnt[k] = 0;
+        }
+        __syncthreads();
+        if (status & 3) break;        // a singular / domain error ends the run after its depth
+    }
+    for (int e = tid; e < n * n; e += blockDim.x) a.rl[e] = rlv[(e / n) * SMALL_N + e % n];
+    if (tid == 0) {
+        sum->levels = levels;
+        sum->status = status;
+        sum->xrows = (int64_t)cnt[5];
+    }
+}
+
+size_t small_lds_bytes(int n) {
+    return sizeof(double) * (size_t)n * n +
+           sizeof(uint64_t) * (SMALL_N * SMALL_N + 3 * SMALL_N + 1 + SMALL_N * (SMALL_MAXD + 1) + SMALL_QCAP) +
+           sizeof(double) * SMALL_WAVES * SMALL_SLOT + sizeof(int) * (SMALL_N + 16) + sizeof(uint16_t) * SMALL_QCAP +
+           2 * SMALL_N * SMALL_N + 8 + sizeof(unsigned long long) * 8;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -4847,9 +5492,151 @@ static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc,
     return PCG_OK;
 }
 
+namespace {
+// the small-graph path is taken for n <= SMALL_N on one rank with the handle's own removal flags
+// (PCG_SMALL=0: the level loop for every size, an A/B knob)
+bool small_ok(const pcg_handle *h, int64_t n) {
+    if (n < 2 || n > SMALL_N || h->world != 1 || h->rm_ext) return false;
+    const char *e = getenv("PCG_SMALL");
+    return !e || atoi(e) != 0;
+}
+
+// returns PCG_OK, an error, or 1: deeper than SMALL_MAXD (the caller reruns on the level loop)
+int skeleton_small(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N, double alpha, int max_depth,
+                   int flags, int8_t *removed_level) {
+    if (!h || !C || !removed_level || n < 2 || ldc < n || !(alpha > 0 && alpha < 1))
+        return pcg_fail(h, PCG_ERR_INVALID, "pcg_skeleton: invalid arguments (n=%lld)", (long long)n);
+    PCG_HIP(h, hipSetDevice(h->device));
+    h->C = C; h->n = n; h->ldc = ldc; h->N = N; h->alpha = alpha; h->flags = flags;
+    h->rl = removed_level;
+    h->W = 1;
+    h->depth = -1;
+    h->deg_levels.clear();
+    if (h->xs) PCG_HIP(h, hipStreamSynchronize(h->xs));
+    h->xpending[0] = h->xpending[1] = false;
+    h->xany = false;
+    h->export_rows = 0;
+    h->rec_h.clear(); h->near_h.clear();
+    h->rec_total = h->near_total = 0;
+    h->near_seen = h->near_total_dev = 0;
+    memset(&h->st, 0, sizeof(h->st));
+    const int64_t rows = n * (n - 1);
+    if (!pcg_ensure(h, h->export_xy, sizeof(int32_t) * 2 * (size_t)rows) ||
+        !pcg_ensure(h, h->exportbuf, sizeof(uint64_t) * (size_t)rows) ||
+        !pcg_ensure(h, h->nearbuf, sizeof(pcg_record) * h->near_cap) ||
+        !pcg_ensure(h, h->records, sizeof(pcg_record) * std::max<int64_t>(h->rec_cap, 1)) ||
+        !pcg_ensure(h, h->small_sum, sizeof(SmallSummary) + 128 + 32 * (SMALL_MAXD + 1)) ||
+        !pcg_ensure_pinned(h, h->small_pin, sizeof(SmallSummary) + 64))
+        return pcg_fail(h, PCG_ERR_OOM, "small-graph skeleton buffers (n=%lld)", (long long)n);
+    h->export_cap = std::max(h->export_cap, rows);
+    if (h->binom_n != (int)n) {
+        build_binom(h, (int)n);
+        if (!pcg_ensure(h, h->binom, sizeof(uint64_t) * h->binom_h.size())) return PCG_ERR_OOM;
+        PCG_HIP(h, hipMemcpyAsync(h->binom.p, h->binom_h.data(), sizeof(uint64_t) * h->binom_h.size(),
+                                  hipMemcpyHostToDevice, h->stream));
+        h->binom_n = (int)n;
+    }
+    SmallArgs a{};
+    a.C = C; a.ldc = ldc; a.n = (int)n; a.max_depth = max_depth; a.alpha = alpha; a.tau = PCG_COND_TAU;
+    a.banned = h->banned;
+    a.binom = (const uint64_t *)h->binom.p;
+    a.rl = removed_level;
+    a.xy = (int32_t *)h->export_xy.p;
+    a.bits = (uint64_t *)h->exportbuf.p;
+    a.nearl = (pcg_record *)h->nearbuf.p;
+    a.records = (pcg_record *)h->records.p;
+    a.near_cap = h->near_cap;
+    a.rec_cap = h->rec_cap;
+    a.rec_mod = h->rec_mod;
+    a.rec_res = h->rec_res;
+    a.fullp = (flags & PCG_FLAG_FULL_P) ? 1 : 0;
+    a.record = (flags & PCG_FLAG_RECORD) ? 1 : 0;
+    a.exact_all = (flags & PCG_FLAG_EXACT_ALL) ? 1 : 0;
+    a.sum = (SmallSummary *)h->small_sum.p;
+    a.ctr = reinterpret_cast<unsigned long long *>((char *)h->small_sum.p + sizeof(SmallSummary) + 8 -
+                                                   (sizeof(SmallSummary) % 8));
+    double cst[4 * (SMALL_MAXD + 1)];
+    for (int d = 0; d <= SMALL_MAXD; ++d) {     // make_args' per-depth constants
+        const double dof = (double)N - d - 3;
+        cst[4 * d + 3] = dof < 0 ? 1.0 : 0.0;
+        cst[4 * d + 2] = dof >= 0 ? std::sqrt(dof) : 0.0;
+        if (dof > 0) {
+            const double r2 = threshold_r2(alpha, (double)N, d);
+            cst[4 * d] = r2 * (1.0 - 1e-6);
+            cst[4 * d + 1] = r2 * (1.0 + 1e-6);
+        } else {
+            cst[4 * d] = -1.0;
+            cst[4 * d + 1] = 1e300;
+        }
+    }
+    double *cst_dev = reinterpret_cast<double *>((char *)a.ctr + 64);
+    a.depth_cst = cst_dev;
+    PCG_HIP(h, hipMemcpyAsync(cst_dev, cst, sizeof(cst), hipMemcpyHostToDevice, h->stream));
+    PCG_HIP(h, hipMemsetAsync(a.ctr, 0, 2 * sizeof(unsigned long long), h->stream));
+    hipEvent_t *ev = h->lev;
+    for (int k = 0; k < 2; ++k)
+        if (!ev[k]) PCG_HIP(h, hipEventCreate(&ev[k]));
+    PCG_HIP(h, hipEventRecord(ev[0], h->stream));
+    hipLaunchKernelGGL(k_pc_small, dim3(1), dim3(SMALL_WAVES * 64), small_lds_bytes((int)n), h->stream, a);
+    PCG_HIP(h, hipGetLastError());
+    PCG_HIP(h, hipEventRecord(ev[1], h->stream));
+    const size_t sb = sizeof(SmallSummary) + 64;
+    PCG_HIP(h, hipMemcpyAsync(h->small_pin.p, h->small_sum.p, sb, hipMemcpyDeviceToHost, h->stream));
+    PCG_HIP(h, hipStreamSynchronize(h->stream));
+    const SmallSummary *sm = (const SmallSummary *)h->small_pin.p;
+    const unsigned long long *c2 = reinterpret_cast<const unsigned long long *>(
+        (const char *)h->small_pin.p + ((const char *)a.ctr - (const char *)h->small_sum.p));
+    if (sm->status & 4) return 1;
+    int wall_khz = 100000;            // wall_clock64's rate (kHz)
+    (void)hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, h->device);
+    if (wall_khz <= 0) wall_khz = 100000;
+    const int L = sm->levels;
+    h->st.levels = L;
+    for (int d = 0; d < L; ++d) {
+        h->st.tests[d] = sm->tests[d];
+        h->st.calls[d] = sm->calls[d];
+        h->st.indep[d] = sm->indep[d];
+        h->st.exact[d] = sm->exact[d];
+        h->st.near_alpha[d] = sm->near_alpha[d];
+        h->st.edges_after[d] = sm->edges_after[d];
+        h->st.max_degree[d] = sm->max_degree[d];
+        h->st.level_ms[d] = h->st.kernel_ms[d] = (double)(sm->stamp[d + 1] - sm->stamp[d]) / wall_khz;
+        h->deg_levels.insert(h->deg_levels.end(), sm->deg[d], sm->deg[d] + n);
+    }
+    h->export_rows = sm->xrows;
+    const int64_t nn = std::min<int64_t>((int64_t)c2[0], h->near_cap);
+    if (nn > 0) {
+        h->near_h.resize((size_t)nn);
+        PCG_HIP(h, hipMemcpy(h->near_h.data(), h->nearbuf.p, sizeof(pcg_record) * nn, hipMemcpyDeviceToHost));
+    }
+    if (flags & PCG_FLAG_RECORD) {
+        if ((int64_t)c2[1] > h->rec_cap)
+            return pcg_fail(h, PCG_ERR_OVERFLOW, "record buffer overflow (%llu > %lld)", c2[1], (long long)h->rec_cap);
+        h->rec_h.resize((size_t)c2[1]);
+        if (c2[1])
+            PCG_HIP(h, hipMemcpy(h->rec_h.data(), h->records.p, sizeof(pcg_record) * c2[1], hipMemcpyDeviceToHost));
+    }
+    if (sm->status & 3) {
+        const bool singular = sm->status & 1;
+        h->st.error = singular ? PCG_ERR_SINGULAR : PCG_ERR_DOMAIN;
+        return pcg_fail(h, h->st.error,
+                        singular ? "Data correlation matrix is singular. Cannot run fisherz test. Please check your data."
+                                 : "math domain error");
+    }
+    return PCG_OK;
+}
+}  // namespace
+
 extern "C" int pcg_skeleton(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N, double alpha,
                             int max_depth, int flags, int8_t *removed_level, pcg_stats *stats) {
     int rc = PCG_OK;
+    if (h && small_ok(h, n)) {
+        rc = skeleton_small(h, C, n, ldc, N, alpha, max_depth, flags, removed_level);
+        if (rc != 1) {
+            if (stats) *stats = h->st;
+            return rc;
+        }
+    }
     for (int attempt = 0; attempt < 6; ++attempt) {
         rc = skeleton_once(h, C, n, ldc, N, alpha, max_depth, flags, removed_level);
         if (rc != PCG_ERR_OVERFLOW) break;

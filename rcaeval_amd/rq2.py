@@ -249,8 +249,41 @@ def evaluate(result_path: str, is_synthetic: bool = False) -> dict:
     return {"eval_data": eval_data, "summary": summary}
 
 
+_LOADERS = None
+
+
+def _loader_ready(_):
+    return os.getpid()
+
+
+def start_loaders(n: int):
+    """A pool of ``n`` loader PROCESSES (spawned: fresh interpreters that import pandas and this
+    module, never the GPU) reading and windowing cases for ``run``; kept for later runs. pandas'
+    CSV parser holds the GIL, so loader threads contend with the GPU thread (measured: 3.5 ms of
+    read_csv per case alone, ~10 ms per case on two threads); processes do not."""
+    global _LOADERS
+    if n <= 0:
+        return None
+    if _LOADERS is not None and _LOADERS[1] == n:
+        return _LOADERS[0]
+    import multiprocessing
+    from concurrent.futures import ProcessPoolExecutor
+    stop_loaders()
+    pool = ProcessPoolExecutor(max_workers=n, mp_context=multiprocessing.get_context("spawn"))
+    list(pool.map(_loader_ready, range(n)))          # every worker up (imports done)
+    _LOADERS = (pool, n)
+    return pool
+
+
+def stop_loaders() -> None:
+    global _LOADERS
+    if _LOADERS is not None:
+        _LOADERS[0].shutdown(wait=True)
+        _LOADERS = None
+
+
 def run(dataset_dir: str, method: str, dataset: str, output: str = "output", length=None, tdelta: int = 0,
-        test: bool = False, rank: int = 0, world: int = 1, prefetch: int = 2) -> dict:
+        test: bool = False, rank: int = 0, world: int = 1, prefetch: int = 2, loader: str = "process") -> dict:
     """Every case of ``dataset_dir`` through ``method``; rank ``r`` of ``world`` takes cases
     ``r, r + world, ...`` of the sorted list. Returns this rank's timings and, on rank 0,
     the evaluation (after a barrier when ``world > 1``)."""
@@ -262,25 +295,33 @@ def run(dataset_dir: str, method: str, dataset: str, output: str = "output", len
     t0 = time.perf_counter()
     per_case = []
     if prefetch > 0 and len(mine) > 1:
-        # loader threads read and window the next cases (pandas' C parser, file IO) while this
-        # thread runs the current case on the GPU (ctypes calls release the GIL); cases are still
-        # processed, and their errors raised, in the sorted order of the sequential loop
+        # loaders (processes by default, or threads) read and window the next cases while this
+        # thread runs the current case on the GPU; cases are still processed, and their errors
+        # raised, in the sorted order of the sequential loop
         from collections import deque
         from concurrent.futures import ThreadPoolExecutor
-
-        def load(p):
-            return load_case(p, length=length, tdelta=tdelta, is_synthetic=is_synthetic)
-
-        with ThreadPoolExecutor(max_workers=prefetch) as ex:
-            queue = deque((p, ex.submit(load, p)) for p in mine[:prefetch])
+        kw = dict(length=length, tdelta=tdelta, is_synthetic=is_synthetic)
+        own = None
+        if loader == "process":
+            ex = start_loaders(prefetch)
+        else:
+            ex = own = ThreadPoolExecutor(max_workers=prefetch)
+        depth = 2 * prefetch                       # cases in flight ahead of the GPU thread
+        try:
+            queue = deque((p, ex.submit(load_case, p, **kw)) for p in mine[:depth])
             nxt = len(queue)
             while queue:
                 _, fut = queue.popleft()
                 c = fut.result()
                 if nxt < len(mine):
-                    queue.append((mine[nxt], ex.submit(load, mine[nxt])))
+                    queue.append((mine[nxt], ex.submit(load_case, mine[nxt], **kw)))
                     nxt += 1
                 per_case.append(process_loaded(c, method, dataset, result_path))
+        finally:
+            for _, f in (queue if "queue" in locals() else ()):
+                f.cancel()
+            if own is not None:
+                own.shutdown(wait=True)
     else:
         for p in mine:
             per_case.append(process(p, method, dataset, result_path, length=length, tdelta=tdelta,

@@ -137,7 +137,11 @@ def test_corr_small_n_many_slabs(eng, n, N):
 
 @pytest.mark.parametrize("n,N,seed,wl,wh,ep", CASES)
 @pytest.mark.parametrize("flags", [0, _lib.PCG_FLAG_FULL_P | _lib.PCG_FLAG_RECORD])
-def test_skeleton_matches_oracle(eng, n, N, seed, wl, wh, ep, flags):
+@pytest.mark.parametrize("small", ["1", "0"])
+def test_skeleton_matches_oracle(eng, n, N, seed, wl, wh, ep, flags, small, monkeypatch):
+    """Both drivers: n <= 64 runs the single-workgroup small-graph kernel (k_pc_small) unless
+    PCG_SMALL=0 sends it through the level loop; larger n always take the level loop."""
+    monkeypatch.setenv("PCG_SMALL", small)
     X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
     C = np.corrcoef(X.T)
     ref = cpc.skeleton(C, N, record_cap=2_000_000)
@@ -154,10 +158,11 @@ def test_skeleton_matches_oracle(eng, n, N, seed, wl, wh, ep, flags):
 
 @pytest.mark.parametrize("narrow", [4, 16])
 @pytest.mark.parametrize("n,N,seed,wl,wh,ep", CASES)
-def test_wide_and_large_classes_match_oracle(eng, n, N, seed, wl, wh, ep, narrow):
+def test_wide_and_large_classes_match_oracle(eng, n, N, seed, wl, wh, ep, narrow, monkeypatch):
     """Nodes above `narrow` neighbours leave the LDS-resident class: at the T-group depths they
     run the WIDE (128-bit mask) T-group kernel, elsewhere the staged kernels — the skeleton,
     the unions and the per-level test counts stay the oracle's."""
+    monkeypatch.setenv("PCG_SMALL", "0")   # the level-loop kernels under test, also at n <= 64
     X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
     C = np.corrcoef(X.T)
     ref = cpc.skeleton(C, N)
@@ -176,6 +181,7 @@ def test_screen_precision_masks_match_oracle(eng, n, N, seed, wl, wh, ep, narrow
     """The fp32-screened T-group sweep (k_level_lds_f) against the all-fp64 one (mask 0) and
     with depth 2 screened too (0x1c), narrow and wide classes: identical skeletons, unions and
     per-level counts (PCG_SCREEN_MASK is read per skeleton call)."""
+    monkeypatch.setenv("PCG_SMALL", "0")   # the level-loop kernels under test, also at n <= 64
     X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
     C = np.corrcoef(X.T)
     ref = cpc.skeleton(C, N)
@@ -196,6 +202,7 @@ def test_schur_prefix_sweep_matches_oracle(eng, n, N, seed, wl, wh, ep, sp, monk
     """The Schur-prefix sweep (k_level_sp: P1 = C - w0 w0^T staged per prefix t0, chunks of
     several prefixes per block) on depth 3, depth 4, both, or neither (k_level_lds_f):
     identical skeletons, unions and per-level counts (PCG_SP is read per depth)."""
+    monkeypatch.setenv("PCG_SMALL", "0")   # the level-loop kernels under test, also at n <= 64
     X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
     C = np.corrcoef(X.T)
     ref = cpc.skeleton(C, N)
@@ -211,6 +218,7 @@ def test_pipelined_level_loop_matches_oracle(eng, n, N, seed, wl, wh, ep, lo, mo
     degrees at the start of d - 1 and enqueued before depth d - 1's summary is read, k_decompose
     writing the exact prefixes on the device, bound-sized launches): the oracle's skeleton, unions,
     per-level counts and level count, unlimited depth."""
+    monkeypatch.setenv("PCG_SMALL", "0")   # the level-loop kernels under test, also at n <= 64
     X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
     C = np.corrcoef(X.T)
     ref = cpc.skeleton(C, N)
@@ -495,6 +503,7 @@ def test_wave_kernel_from_depth5_matches_oracle(eng, n, N, seed, wl, wh, ep, fla
     """k_level_wave at every depth >= 5 (PCG_WAVE_LO=5): the deferred-list exact path and the
     FULL_P records of |S| <= 12 go through it too; skeleton, unions, counts and records as the
     oracle's."""
+    monkeypatch.setenv("PCG_SMALL", "0")   # the level-loop kernels under test, also at n <= 64
     monkeypatch.setenv("PCG_WAVE_LO", "5")
     X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
     C = np.corrcoef(X.T)
