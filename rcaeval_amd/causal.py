@@ -89,21 +89,29 @@ class SepsetArray:
         self._deg = out.deg_levels
         self._ci = ci
         self._alpha = float(alpha)
-        self._rows: dict = {}
+        self._rows_built: dict | None = None       # decoded on first access (pc_pagerank never reads them)
         self._order: dict | None = None
-        W = out.sep_bits.shape[1] if out.sep_bits.size else (n + 63) // 64
-        for r in range(len(out.sep_xy)):
-            x, y = int(out.sep_xy[r, 0]), int(out.sep_xy[r, 1])
-            bits = out.sep_bits[r]
-            members = []
-            for w in range(W):
-                v = int(bits[w])
-                while v:
-                    b = (v & -v).bit_length() - 1
-                    members.append(w * 64 + b)
-                    v &= v - 1
-            prev = self._rows.get((x, y))          # several rows per pair when edge-sharded: OR
-            self._rows[(x, y)] = sorted(set(prev) | set(members)) if prev else members
+
+    @property
+    def _rows(self) -> dict:
+        """(x, y) -> ascending members of x's side union at the removal depth (export rows)."""
+        if self._rows_built is None:
+            out = self._out
+            rows: dict = {}
+            xy = np.asarray(out.sep_xy)
+            if len(xy):
+                bits = np.ascontiguousarray(out.sep_bits).view(np.uint64)
+                # little-endian bit order: member w * 64 + b <-> bit b of word w
+                flags = np.unpackbits(bits.view(np.uint8).reshape(len(xy), -1), axis=1, bitorder="little")
+                rr, cc = np.nonzero(flags)
+                starts = np.searchsorted(rr, np.arange(len(xy) + 1))
+                for r in range(len(xy)):
+                    x, y = int(xy[r, 0]), int(xy[r, 1])
+                    members = cc[starts[r]:starts[r + 1]].tolist()
+                    prev = rows.get((x, y))          # several rows per pair when edge-sharded: OR
+                    rows[(x, y)] = sorted(set(prev) | set(members)) if prev else members
+            self._rows_built = rows
+        return self._rows_built
 
     def _resolve_order(self) -> dict:
         """First-insertion order of every union with more members than its depth."""

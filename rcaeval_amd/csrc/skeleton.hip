@@ -3568,6 +3568,230 @@ __global__ __launch_bounds__(256) void k_level_wave(LevelArgs a) {
     block_flush_counts(a.ctr, tests, indep);
 }
 
+// k_level_wave with the factorisation shared between consecutive sets. A wave walks its run of
+// colex ranks; the colex successor (Gosper) changes only the LOWEST elements of S, so the steps
+// run in DESCENDING element order: steps 0..k-1 (the elements above the highest changed bit) and
+// every lane's solve values, pivot, |v|^2 and u.v prefixes up to them stay valid, and only the
+// steps of the changed low elements are redone — ~1-2 steps per set instead of |S|. Same tests,
+// same memo and union bookkeeping, same decision (threshold band, guard on the smallest pivot^2
+// of this factorisation order) and exact path as k_level_wave.
+template <int MD, int MODE>
+__global__ __launch_bounds__(256) void k_level_wave_pr(LevelArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wv = tid >> 6;
+    const int64_t chunk = a.chunk_lo + blockIdx.x;
+    if (chunk >= a.cpre[a.n]) return;
+    int lo = 0, hi = a.n;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (a.cpre[mid] <= chunk) lo = mid; else hi = mid;
+    }
+    const int x = lo;
+    const int D = a.deg[x];
+    const int d = a.d;
+    const int32_t *nxg = a.nbr + a.off[x];
+
+    double *M = reinterpret_cast<double *>(smem);                 // D * D
+    double *Mx = M + D * D;                                       // D
+    double *Md = Mx + D;                                          // D
+    unsigned long long *lmask = reinterpret_cast<unsigned long long *>(Md + D);   // D
+    unsigned long long *uself = lmask + D;                        // D
+    unsigned long long *uprop = uself + D;                        // D
+    int32_t *nxs = reinterpret_cast<int32_t *>(uprop + D);       // D
+    int *s_tx = nxs + D;                                          // 1
+    double *slot = reinterpret_cast<double *>(smem + a.lds_btab_off) + (size_t)wv * WAVE_SLOT_DOUBLES(MD);
+    // the pivots of the factorisation in registers (per wave, after the four slots)
+    double *pivs = reinterpret_cast<double *>(smem + a.lds_btab_off) + 4 * (size_t)WAVE_SLOT_DOUBLES(MD) + wv * MD;
+
+    for (int i = tid; i < D; i += blockDim.x) nxs[i] = nxg[i];
+    __syncthreads();
+    for (int e = tid; e < D * D; e += blockDim.x) {
+        const int t = e / D, k = e - t * D;
+        M[e] = a.C[(int64_t)nxs[t] * a.ldc + nxs[k]];
+    }
+    for (int t = wv; t < D; t += blockDim.x >> 6) {
+        const bool bit = lane < D && ((a.adj[(int64_t)nxs[t] * a.W + (nxs[lane] >> 6)] >> (nxs[lane] & 63)) & 1ull);
+        const unsigned long long m = __ballot(bit);
+        if (lane == 0) lmask[t] = m;
+    }
+    for (int t = tid; t < D; t += blockDim.x) {
+        const int yg = nxs[t];
+        Mx[t] = a.C[(int64_t)x * a.ldc + yg];
+        Md[t] = a.diag[yg];
+        uself[t] = 0;
+        uprop[t] = 0;
+    }
+    if (tid == 0) {
+        int c = 0;
+        while (c < D && nxs[c] < x) ++c;
+        *s_tx = c;
+    }
+    __syncthreads();
+    const int tx = *s_tx;
+    const double Cxx = a.diag[x];
+    const uint64_t nS = pcg_binom(a.binom, D, d);
+    const uint64_t r0 = (uint64_t)(chunk - a.cpre[x]) * 4u * (uint64_t)a.spl + (uint64_t)wv * (uint64_t)a.spl;
+    const uint64_t r1 = min(nS, r0 + (uint64_t)a.spl);
+    unsigned long long tests = 0, indep = 0;
+    if (r0 < r1) {
+        unsigned long long mask = 0;      // colex unrank of r0 (wave-uniform)
+        {
+            uint64_t rr = r0;
+            int hi_ = D;
+            for (int ii = d - 1; ii >= 0; --ii) {
+                int lo_ = ii, up = hi_ - 1;
+                while (lo_ < up) {
+                    const int mid = (lo_ + up + 1) >> 1;
+                    if (pcg_binom(a.binom, mid, ii + 1) <= rr) lo_ = mid; else up = mid - 1;
+                }
+                mask |= 1ull << lo_;
+                rr -= pcg_binom(a.binom, lo_, ii + 1);
+                hi_ = lo_;
+            }
+        }
+        const int cl = lane < D ? lane : 0;            // lane D (x) and idle lanes: a safe column
+        double v[MD];                                   // this lane's solve values, step order
+        unsigned long long prev = 0;                   // the mask whose steps are in registers
+        for (uint64_t rank = r0; rank < r1; ++rank) {
+            // steps 0..k-1 (elements above the highest bit that changed) are still valid
+            int k = 0;
+            if (prev) {
+                const unsigned long long ch = prev ^ mask;
+                const int hb = 63 - __builtin_clzll(ch);
+                k = __popcll(hb == 63 ? 0ull : (mask >> (hb + 1)));
+            }
+            unsigned long long m = mask;              // drop the top k elements
+            for (int q = 0; q < k; ++q) m &= ~(1ull << (63 - __builtin_clzll(m)));
+#pragma unroll
+            for (int i = 0; i < MD; ++i) {
+                if (i >= k && i < d) {                 // wave-uniform
+                    const int si = 63 - __builtin_clzll(m);   // the i-th largest element of S
+                    m &= ~(1ull << si);
+                    double t = lane < D ? M[si * D + cl] : Mx[si];
+#pragma unroll
+                    for (int q = 0; q < i; ++q) t -= readlane_f64(v[q], si) * v[q];   // L[i][q] = lane si's v[q]
+                    const double piv = readlane_f64(t, si);
+                    if (lane == 0) pivs[i] = piv;
+                    v[i] = t * (1.0 / sqrt(piv));
+                }
+            }
+            prev = mask;
+            wave_sync();
+            double vv = 0.0, uv = 0.0, gmin = 1.0;
+            bool ok = true;
+#pragma unroll
+            for (int i = 0; i < MD; ++i) {
+                if (i < d) {
+                    const double piv = pivs[i];
+                    ok = ok && (piv > 0.0);
+                    gmin = fmin(gmin, piv);
+                    vv += v[i] * v[i];
+                    uv += readlane_f64(v[i], D) * v[i];
+                }
+            }
+            const double cxx = Cxx - readlane_f64(vv, D);
+            const double kg = a.tau / gmin;
+            bool live = lane < D && !((mask >> lane) & 1ull);
+            const unsigned long long lm = live ? lmask[cl] : 0ull;
+            const bool in_y = (lm & mask) == mask;
+            live = live && !(lane < tx && in_y);
+            tests += live;
+            int dec = 2;
+            double p = 0.0;
+            if (live && ok) dec = decide<MODE>(a, Mx[cl] - uv, cxx, Md[cl] - vv, kg, &p);
+            if (live && dec == 1) {
+                ++indep;
+                atomicOr(&uself[cl], mask);
+                if (in_y && lane >= tx) atomicOr(&uprop[cl], mask);
+            }
+            if (MODE == MODE_FULLP && live && dec != 2) {
+                const int yg = nxs[cl];
+                const int lo_ = x < yg ? x : yg, hi_ = x < yg ? yg : x;
+                const bool near = fabs(p - a.alpha) < 1e-9;
+                if (d <= PCG_MAX_DEPTH && (near || rec_on(a, lo_, hi_))) {
+                    int sg[PCG_MAX_DEPTH];
+                    set_members(mask, nxs, sg);
+                    if (rec_on(a, lo_, hi_)) push_record(a.records, a.rec_cap, &a.ctr->records, lo_, hi_, d, sg, p);
+                    if (near) push_record(a.nearl, a.near_cap, &a.ctr->near_alpha, lo_, hi_, d, sg, p);
+                } else if (near) {
+                    atomicAdd(&a.ctr->near_alpha, 1ull);
+                }
+            }
+            if (d <= PCG_MAX_DEPTH) {
+                if (live && dec == 2) {
+                    int sg[PCG_MAX_DEPTH];
+                    set_members(mask, nxs, sg);
+                    push_deferred(a, x, nxs[cl], sg, d);
+                }
+            } else {
+                unsigned long long need = __ballot(live && dec == 2);
+                const int mm = d + 2;
+                double *A = slot, *B0 = slot + mm * mm, *B1 = B0 + mm;
+                int *var = reinterpret_cast<int *>(B1 + mm);
+                while (need) {
+                    const int L = __builtin_ctzll(need);
+                    need &= need - 1;
+                    const int yg = nxs[L];
+                    wave_sync();
+                    if (lane < D && ((mask >> lane) & 1ull))
+                        var[2 + __popcll(mask & ((1ull << lane) - 1ull))] = nxs[lane];
+                    if (lane == 0) {
+                        var[0] = x < yg ? x : yg;
+                        var[1] = x < yg ? yg : x;
+                    }
+                    wave_sync();
+                    for (int kk = lane; kk < mm * mm; kk += 64) {
+                        const int r = kk / mm, c = kk - r * mm;
+                        A[kk] = a.C[(int64_t)var[r] * a.ldc + var[c]];
+                    }
+                    wave_sync();
+                    if (lane == 0) {
+                        double pv = __builtin_nan("");
+                        const int err = exact_lu_pvalue(A, mm, B0, B1, a.sqrt_dof, &pv);
+                        atomicAdd(&a.ctr->exact, 1ull);
+                        if (err) {
+                            flag_error(a, err);
+                        } else {
+                            if (fabs(pv - a.alpha) < 1e-9) atomicAdd(&a.ctr->near_alpha, 1ull);
+                            if (pv > a.alpha) {
+                                ++indep;
+                                atomicOr(&uself[L], mask);
+                                if (((lmask[L] & mask) == mask) && L >= tx) atomicOr(&uprop[L], mask);
+                            }
+                        }
+                    }
+                }
+            }
+            const unsigned long long c0 = mask & (0ull - mask);
+            const unsigned long long rr = mask + c0;
+            mask = (((rr ^ mask) >> 2) >> __builtin_ctzll(mask)) | rr;
+        }
+    }
+    __syncthreads();
+    for (int t = tid; t < D; t += blockDim.x) {
+        const unsigned long long us = uself[t], up = uprop[t];
+        if (!(us | up)) continue;
+        const int yg = nxs[t];
+        a.rm[(int64_t)x * a.n + yg] = 1;
+        a.rm[(int64_t)yg * a.n + x] = 1;
+        for (int side = 0; side < 2; ++side) {
+            unsigned long long mb = side ? up : us;
+            if (!mb) continue;
+            const int64_t s = side ? (int64_t)a.off[yg] + find_in_sorted(a.nbr + a.off[yg], a.deg[yg], x)
+                                   : (int64_t)a.off[x] + t;
+            unsigned long long *row = reinterpret_cast<unsigned long long *>(a.ug + s * a.W);
+            while (mb) {
+                const int b = __ffsll((long long)mb) - 1;
+                const int g = nxs[b];
+                atomicOr(&row[g >> 6], 1ull << (g & 63));
+                mb &= mb - 1;
+            }
+        }
+    }
+    block_flush_counts(a.ctr, tests, indep);
+}
+
 // ---------------------------------------------------------------------------------------
 // exact path over the deferred list (LU like numpy.linalg.inv; the reference p expression)
 template <int M>
@@ -4264,7 +4488,9 @@ __global__ __launch_bounds__(SMALL_WAVES * 64, 1) void k_pc_small(SmallArgs a) {
             for (int k = 1; k < 5; ++k) cnt[k] = 0;
         }
         __syncthreads();
-        if (status & 3) break;        // a singular / domain error ends the run after its depth
+        // a singular / domain error ends the run after its depth; a full band queue (status 4:
+        // this depth's decisions are incomplete) ends it at once, the host reruns on the level loop
+        if (status & 7) break;
     }
     for (int e = tid; e < n * n; e += blockDim.x) a.rl[e] = rlv[(e / n) * SMALL_N + e % n];
     if (tid == 0) {
@@ -4438,6 +4664,13 @@ uint64_t tgroup_tasks(const pcg_handle *h, int D, int d) {
 bool use_tgroup(int mode, int d) { return mode == MODE_DECIDE && d >= 2 && d <= 4; }
 // depths whose narrow class runs k_level_wave (one wave per conditioning set); PCG_WAVE_LO
 // overrides the first such depth (A/B knob)
+// k_level_wave_pr (the factorisation shared between consecutive sets) instead of k_level_wave;
+// PCG_WAVE_PR=0: the per-set factorisation (A/B knob, read per launch)
+bool wave_pr() {
+    const char *e = getenv("PCG_WAVE_PR");
+    return !e || atoi(e) != 0;
+}
+
 bool use_wave(int mode, int d) {
     const char *e = getenv("PCG_WAVE_LO");        // read per depth, like PCG_SCREEN_MASK
     const int lo = e ? atoi(e) : PCG_WAVE_LO;
@@ -4813,7 +5046,9 @@ int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks, bool bound
         }
         // lanes per block: 256 S ranks / T-group tasks, or 4 conditioning sets (k_level_wave: a wave each)
         const double per_block = h->wavek ? 4.0 : 256.0;
-        h->spl = (int)std::min(64.0, std::max(1.0, std::floor(sum_small / (per_block * nb_target * h->world))));
+        // (k_level_wave_pr shares the factorisation along a wave's run of sets: longer runs there)
+        const double spl_cap = (h->wavek && wave_pr()) ? 512.0 : 64.0;
+        h->spl = (int)std::min(spl_cap, std::max(1.0, std::floor(sum_small / (per_block * nb_target * h->world))));
         const double nbw_target = getenv("PCG_NBW") ? atof(getenv("PCG_NBW")) : 512.0;   // A/B knob
         h->spl_w = (int)std::min(64.0, std::max(1.0, std::floor(sum_wide / (256.0 * nbw_target * h->world))));
         const double mean_large = cnt_large ? sum_large / cnt_large : 0.0;
@@ -5140,13 +5375,18 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                         const dim3 grid((unsigned)(s_hi - s_lo)), block(256);
                         const size_t core = lds_small_core(h->maxdeg_small);
                         as.lds_btab_off = (int)core;
+                        const bool pr = wave_pr();
                         if (d <= 16) {
-                            const size_t ldsw = core + 4 * sizeof(double) * WAVE_SLOT_DOUBLES(16);
-                            if (mode == MODE_DECIDE) hipLaunchKernelGGL((k_level_wave<16, MODE_DECIDE>), grid, block, ldsw, h->stream, as);
+                            const size_t ldsw = core + 4 * sizeof(double) * (WAVE_SLOT_DOUBLES(16) + 16);
+                            if (pr && mode == MODE_DECIDE) hipLaunchKernelGGL((k_level_wave_pr<16, MODE_DECIDE>), grid, block, ldsw, h->stream, as);
+                            else if (pr) hipLaunchKernelGGL((k_level_wave_pr<16, MODE_FULLP>), grid, block, ldsw, h->stream, as);
+                            else if (mode == MODE_DECIDE) hipLaunchKernelGGL((k_level_wave<16, MODE_DECIDE>), grid, block, ldsw, h->stream, as);
                             else hipLaunchKernelGGL((k_level_wave<16, MODE_FULLP>), grid, block, ldsw, h->stream, as);
                         } else {
-                            const size_t ldsw = core + 4 * sizeof(double) * WAVE_SLOT_DOUBLES(32);
-                            if (mode == MODE_DECIDE) hipLaunchKernelGGL((k_level_wave<32, MODE_DECIDE>), grid, block, ldsw, h->stream, as);
+                            const size_t ldsw = core + 4 * sizeof(double) * (WAVE_SLOT_DOUBLES(32) + 32);
+                            if (pr && mode == MODE_DECIDE) hipLaunchKernelGGL((k_level_wave_pr<32, MODE_DECIDE>), grid, block, ldsw, h->stream, as);
+                            else if (pr) hipLaunchKernelGGL((k_level_wave_pr<32, MODE_FULLP>), grid, block, ldsw, h->stream, as);
+                            else if (mode == MODE_DECIDE) hipLaunchKernelGGL((k_level_wave<32, MODE_DECIDE>), grid, block, ldsw, h->stream, as);
                             else hipLaunchKernelGGL((k_level_wave<32, MODE_FULLP>), grid, block, ldsw, h->stream, as);
                         }
                     } else if (h->sp) {

@@ -47,5 +47,27 @@ def main():
     print(res, flush=True)
 
 
+
+
+def profile_pc(n=44, N=600, reps=300):
+    """cProfile of pc() on one RQ2-shaped case (where the host time of a small case goes)."""
+    import cProfile
+    import pstats
+    from rcaeval_amd import synth
+    from rcaeval_amd.causal import pc
+    X = synth.gaussian_sem(n, N, seed=1, w_low=0.2, w_high=0.8, edge_prob=0.1)
+    for _ in range(10):
+        pc(X)
+    pr = cProfile.Profile()
+    pr.enable()
+    for _ in range(reps):
+        pc(X)
+    pr.disable()
+    pstats.Stats(pr).sort_stats("tottime").print_stats(25)
+
+
 if __name__ == "__main__":
-    main()
+    if "--profile" in sys.argv:
+        profile_pc()
+    else:
+        main()
