@@ -92,7 +92,7 @@ extern "C" int pcg_destroy(pcg_handle *h) {
                       &h->ug2[1], &h->exp_ctr, &h->cpre, &h->binom, &h->ctr,
                       &h->deferred, &h->screenq, &h->records, &h->nearbuf, &h->exportbuf, &h->export_xy, &h->diag,
                       &h->colmean, &h->pr_scratch, &h->batch_scratch, &h->chisq_scratch, &h->cblk, &h->lmk,
-                      &h->k1_digits, &h->small_sum};
+                      &h->k1_digits, &h->small_sum, &h->gbar, &h->spl_buf};
     for (DevBuf *b : bufs)
         if (b->p) hipFree(b->p);
     PinBuf *pins[] = {&h->ctr_pin, &h->deg_pin, &h->off_pin, &h->cpre_pin, &h->status_pin, &h->tab_pin[0],

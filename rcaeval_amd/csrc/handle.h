@@ -38,6 +38,7 @@ struct DevCounters {
 struct LevelSummary {
     DevCounters ctr;
     uint8_t status[8];
+    int32_t ug_clean;              // k_summary_fill cleared every union row of the new graph
     unsigned long long seq;        // written last, after a system-scope fence
 };
 
@@ -82,12 +83,16 @@ struct pcg_handle {
     DevBuf off2[2], nbr2[2], ug2[2];
     int cb = 0;                      // buffer set of the current graph
     bool ug_clean2[2] = {false, false};   // the union rows of set i's CSR are all zero
+    unsigned long long ug_pend_seq = 0;   // summary whose ug_clean still applies to set ug_pend_set
+    int ug_pend_set = 0;
     hipStream_t xs = nullptr;        // sepset export stream
     hipEvent_t ev_xready = nullptr, ev_xdone[2] = {nullptr, nullptr};
     bool xpending[2] = {false, false};    // an export reading set i is queued on xs
     bool xany = false;               // exports queued since the last export_sync
     DevBuf exp_ctr;                  // rows exported so far (device, persists across depths)
     PinBuf ctr_pin, deg_pin, off_pin, cpre_pin, status_pin;
+    DevBuf gbar;                     // the fused level barrier's grid-barrier words (k_level_end)
+    bool fuse_end = false;           // this depth's screen / exact path / removals run fused in k_level_end
     DevBuf small_sum;                // single-workgroup small-graph skeleton: summary + counters
     PinBuf small_pin;                // its host copy
     std::vector<uint64_t> binom_h;   // host copy of the binomial table
@@ -128,6 +133,11 @@ struct pcg_handle {
     // on upper-bound degrees (those at the start of d - 1) and enqueued before depth d - 1's
     // summary is read; k_decompose computes the exact prefixes on the device
     bool bound = false;              // the current depth was prepared in bound mode
+    bool dspl = false;               // bound mode: k_decompose_dev picks spl / spl_w on the device (spl_buf)
+    int dspl_lanes = 256;            // lanes per narrow-class chunk unit (4: a wave per set)
+    double dspl_tgt[2] = {0, 0};     // narrow / wide block targets
+    int dspl_cap[2] = {64, 64};      // narrow / wide spl caps
+    DevBuf spl_buf;                  // int32[2]: the device's narrow / wide spl
     int64_t dtab_off = 0;            // int64 offset of the per-degree class tables in cpre (bound mode)
     int64_t bo_off = 0;              // int64 offset of the compact-block offsets in cpre
     int dtab_maxd = 0;               // their largest degree

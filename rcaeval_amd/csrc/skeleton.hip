@@ -29,6 +29,7 @@
 // PCG_FLAG_FULL_P computes the p-value of every test inline instead.
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 
@@ -118,6 +119,7 @@ struct LevelArgs {
     int64_t rec_mod, rec_res;    // record sample: canonical pair (a, b) with (a*n + b) % rec_mod == rec_res
     int64_t chunk_lo;            // first chunk of this launch (within its class)
     int spl;                     // S ranks per lane (LDS-resident kernel)
+    const int32_t *spl_dev;      // pipelined loop: the spl k_decompose chose on the device (else null)
     int lds_btab_off;            // byte offset of the LDS binomial table (LDS-resident kernel)
     // Schur-prefix sweep (k_level_sp): per-degree chunk tables and the per-node compact blocks
     const int64_t *ctab;         // chunk (t0 << 40 | first task << 20 | tasks), per degree D from coff[D]
@@ -398,61 +400,68 @@ __global__ __launch_bounds__(256) void k_export(const int32_t *off, const int32_
 // adjacency words (a wave's ballot is the mask cleared from word (x, w)) + removed_level, deg[x]
 // lowered by the row's removed count; rm is the last read here, so set bytes are cleared for the
 // next depth.
+__device__ __forceinline__ void close_rows(uint8_t *rm, uint64_t *adj, int32_t *deg, int8_t *rl, int n, int W, int d,
+                                           int blk, int nblk, int *cleared) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int x = blk; x < n; x += nblk) {
+        int mine = 0;
+        for (int w = wave; w < W; w += 4) {
+            const int y = w * 64 + lane;
+            bool removed = false;
+            if (y < n) {
+                removed = rm[(int64_t)x * n + y] != 0;
+                if (removed) {
+                    rl[(int64_t)x * n + y] = (int8_t)d;
+                    rm[(int64_t)x * n + y] = 0;
+                }
+            }
+            const unsigned long long m = __ballot(removed);
+            if (lane == 0 && m) {
+                const uint64_t old = adj[(int64_t)x * W + w];
+                adj[(int64_t)x * W + w] = old & ~m;
+                mine += __popcll(old & m);
+            }
+        }
+        if (lane == 0) cleared[wave] = mine;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int c = cleared[0] + cleared[1] + cleared[2] + cleared[3];
+            if (c) deg[x] -= c;
+        }
+        __syncthreads();
+    }
+}
+
 __global__ __launch_bounds__(256) void k_level_close(uint8_t *rm, uint64_t *adj, int32_t *deg, int8_t *rl, int n,
                                                      int W, int d) {
     __shared__ int cleared[4];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int x = blockIdx.x;
-    int mine = 0;
-    for (int w = wave; w < W; w += 4) {
-        const int y = w * 64 + lane;
-        bool removed = false;
-        if (y < n) {
-            removed = rm[(int64_t)x * n + y] != 0;
-            if (removed) {
-                rl[(int64_t)x * n + y] = (int8_t)d;
-                rm[(int64_t)x * n + y] = 0;
-            }
-        }
-        const unsigned long long m = __ballot(removed);
-        if (lane == 0 && m) {
-            const uint64_t old = adj[(int64_t)x * W + w];
-            adj[(int64_t)x * W + w] = old & ~m;
-            mine += __popcll(old & m);
-        }
-    }
-    if (lane == 0) cleared[wave] = mine;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const int c = cleared[0] + cleared[1] + cleared[2] + cleared[3];
-        if (c) deg[x] -= c;
-    }
+    close_rows(rm, adj, deg, rl, n, W, d, blockIdx.x, gridDim.x, cleared);
 }
 
 // The level barrier's summary and the next depth's CSR in one launch. Blocks 0 .. nfill-1
 // (nfill = ceil(n/4); 0 at init: depth 0 reads no CSR):
 // one wave per node x builds its ascending neighbour list from the adjacency row at offset
 // sum(deg[0..x)) (each wave sums the prefix itself, so no grid-wide scan is waited for) and, with
-// ug, clears the node's union rows. The last block: the CSR offsets (exclusive scan of deg), the
+// ug, clears the node's union rows when they lie inside the buffer's ug_rows rows (the last block
+// reports whether all of them did, so the next depth skips its memset). The last block: the CSR offsets (exclusive scan of deg), the
 // degrees, level counters and merged status bytes written into host-mapped memory, then — after
 // a system-scope fence — the sequence number the host spins on (the host then enqueues work that
 // the stream orders after the whole grid). Counters and status bytes are cleared once copied.
-__global__ __launch_bounds__(256) void k_summary_fill(const int32_t *deg, int n, int W, const uint64_t *adj,
-                                                      int32_t *off, int32_t *nbr, uint64_t *ug, DevCounters *ctr,
-                                                      uint8_t *status, LevelSummary *out, int32_t *out_deg,
-                                                      unsigned long long seq, int nfill) {
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    if ((int)blockIdx.x < nfill) {
-        const int x = blockIdx.x * 4 + (tid >> 6);
-        if (x >= n) return;
+// the CSR part: node groups g = blk, blk + nblk, ... of 4 nodes (a wave per node)
+__device__ __forceinline__ void summary_nodes(const int32_t *deg, int n, int W, const uint64_t *adj, int32_t *nbr,
+                                              uint64_t *ug, int64_t ug_rows, int nfill, int blk, int nblk) {
+    const int lane = threadIdx.x & 63;
+    for (int g = blk; g < nfill; g += nblk) {
+        const int x = g * 4 + (threadIdx.x >> 6);
+        if (x >= n) continue;
         int ps = 0;
         for (int i = lane; i < x; i += 64) ps += deg[i];
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) ps += __shfl_xor(ps, o);
         int base = ps;
-        if (ug) {
-            const int64_t lo = (int64_t)base * W, hi = (int64_t)(base + deg[x]) * W;
+        const int dx = *(const volatile int32_t *)&deg[x];   // (written by other blocks in the fused barrier)
+        if (ug && (int64_t)base + dx <= ug_rows) {
+            const int64_t lo = (int64_t)base * W, hi = (int64_t)(base + dx) * W;
             for (int64_t e = lo + lane; e < hi; e += 64) ug[e] = 0ull;
         }
         for (int w0 = 0; w0 < W; w0 += 64) {
@@ -474,9 +483,16 @@ __global__ __launch_bounds__(256) void k_summary_fill(const int32_t *deg, int n,
             }
             base += tot;
         }
-        return;
     }
-    __shared__ int32_t part[256];
+}
+
+// the summary part (one block): CSR offsets, degrees, counters, status bytes (plus `extra` ORed
+// into status byte 4: a fused barrier's failure) -> host-mapped memory, then the sequence number
+__device__ __forceinline__ void summary_block(const int32_t *deg, int n, int32_t *off, const uint64_t *ug,
+                                              int64_t ug_rows, DevCounters *ctr, uint8_t *status, LevelSummary *out,
+                                              int32_t *out_deg, unsigned long long seq, int nfill, int32_t *part,
+                                              uint8_t extra) {
+    const int tid = threadIdx.x;
     const int per = (n + 255) / 256;
     const int lo = min(n, tid * per), hi = min(n, lo + per);
     int32_t sum = 0;
@@ -497,11 +513,19 @@ __global__ __launch_bounds__(256) void k_summary_fill(const int32_t *deg, int n,
     for (int i = lo; i < hi; ++i) { off[i] = acc; acc += deg[i]; }
     if (tid == 255) off[n] = part[255];
     if (tid == 0) {
-        out->ctr = *ctr;
-        DevCounters z{};
-        z.near_alpha = ctr->near_alpha;   // the near-alpha list accumulates over the run
-        *ctr = z;
-        for (int k = 0; k < 8; ++k) out->status[k] = status ? status[k] : 0;
+        // (volatile reads: in the fused barrier other blocks of this launch wrote them)
+        volatile unsigned long long *cw = reinterpret_cast<volatile unsigned long long *>(ctr);
+        unsigned long long *ow = reinterpret_cast<unsigned long long *>(&out->ctr);
+        constexpr int NW = (int)(sizeof(DevCounters) / sizeof(unsigned long long));
+        const int near_w = (int)(offsetof(DevCounters, near_alpha) / sizeof(unsigned long long));
+        for (int k = 0; k < NW; ++k) {
+            ow[k] = cw[k];
+            if (k != near_w) cw[k] = 0ull;    // the near-alpha list accumulates over the run
+        }
+        const volatile uint8_t *sv = status;
+        for (int k = 0; k < 8; ++k) out->status[k] = status ? sv[k] : 0;
+        out->status[4] |= extra;
+        out->ug_clean = ug != nullptr && nfill > 0 && (int64_t)part[255] <= ug_rows;
         if (status)
             for (int k = 0; k < PCG_RM_STATUS; ++k) status[k] = 0;
     }
@@ -511,6 +535,18 @@ __global__ __launch_bounds__(256) void k_summary_fill(const int32_t *deg, int n,
         __threadfence_system();
         __atomic_store_n(&out->seq, seq, __ATOMIC_RELEASE);
     }
+}
+
+__global__ __launch_bounds__(256) void k_summary_fill(const int32_t *deg, int n, int W, const uint64_t *adj,
+                                                      int32_t *off, int32_t *nbr, uint64_t *ug, int64_t ug_rows,
+                                                      DevCounters *ctr, uint8_t *status, LevelSummary *out,
+                                                      int32_t *out_deg, unsigned long long seq, int nfill) {
+    if ((int)blockIdx.x < nfill) {
+        summary_nodes(deg, n, W, adj, nbr, ug, ug_rows, nfill, blockIdx.x, nfill);
+        return;
+    }
+    __shared__ int32_t part[256];
+    summary_block(deg, n, off, ug, ug_rows, ctr, status, out, out_deg, seq, nfill, part, 0);
 }
 
 // The exact per-class chunk prefixes of the current graph from per-degree tables the host built
@@ -571,6 +607,138 @@ __global__ __launch_bounds__(256) void k_decompose(const int32_t *deg, int n, co
 #pragma unroll
         for (int c = 0; c < 3; ++c) cpre[c * (int64_t)(n + 1) + n] = run ? part[c][255] : 0;
         if (nblk) bo[n] = run ? part[3][255] : 0;
+    }
+}
+
+// The pipelined loop's decomposition with the chunk size chosen on the device. tab[0][D] /
+// tab[1][D] = units (T-group lane tasks or S ranks) of a degree-D node in the narrow / wide class
+// (0 if D is in another class), tab[2][D] = its large-class chunks. From the exact degrees: the
+// class sums, spl = clamp(floor(sum / (lanes * target)), 1, cap) per class (the host rule of
+// pcg_level_begin, now on the degrees the depth really starts from), chunks = ceil(units / (lanes
+// * spl)), the class prefixes, the compact-block offsets and spl_out[2] (which the level kernels
+// read through LevelArgs::spl_dev). One 1024-thread block; a thread's nodes are contiguous and
+// every load of a pass is issued before the first is used (the single-block form with one
+// dependent load chain per node took 21-42 us at n = 2000). The launch sizes of the depth are
+// host bounds on these counts (pcg_level_begin, bound mode); the reference loop condition is
+// evaluated here: when it fails every class total is 0.
+constexpr int DEC_THREADS = 1024, DEC_PER = 8;
+__global__ __launch_bounds__(DEC_THREADS) void k_decompose_dev(const int32_t *deg, int n, const int64_t *tab, int maxd,
+                                                               int depth, int nblk, int lanes0, double tgt0, int cap0,
+                                                               double tgt1, int cap1, int64_t *cpre, int64_t *bo,
+                                                               int32_t *spl_out) {
+    __shared__ int64_t part[4][DEC_THREADS / 64];
+    __shared__ int64_t wsum[4][DEC_THREADS / 64];
+    __shared__ int mxw[DEC_THREADS / 64];
+    __shared__ int s_spl[2];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int per = (n + DEC_THREADS - 1) / DEC_THREADS;
+    const int lo = min(n, tid * per), hi = min(n, lo + per);
+    // pass 1: the class unit sums and the largest degree
+    int64_t u0 = 0, u1 = 0;
+    int m = 0;
+    for (int b = lo; b < hi; b += DEC_PER) {
+        int Dk[DEC_PER];
+#pragma unroll
+        for (int k = 0; k < DEC_PER; ++k) Dk[k] = b + k < hi ? deg[b + k] : 0;
+        int64_t t0[DEC_PER], t1[DEC_PER];
+#pragma unroll
+        for (int k = 0; k < DEC_PER; ++k) {
+            const int D = min(Dk[k], maxd);
+            m = max(m, Dk[k]);
+            t0[k] = b + k < hi ? tab[D] : 0;
+            t1[k] = b + k < hi ? tab[(maxd + 1) + D] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < DEC_PER; ++k) { u0 += t0[k]; u1 += t1[k]; }
+    }
+    auto wred = [&](int64_t v) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        return v;
+    };
+    u0 = wred(u0);
+    u1 = wred(u1);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o));
+    if (lane == 0) { wsum[0][wv] = u0; wsum[1][wv] = u1; mxw[wv] = m; }
+    __syncthreads();
+    if (tid == 0) {
+        int64_t s0 = 0, s1 = 0;
+        int mm = 0;
+        for (int w = 0; w < DEC_THREADS / 64; ++w) { s0 += wsum[0][w]; s1 += wsum[1][w]; mm = max(mm, mxw[w]); }
+        const bool run = mm - 1 > depth - 1;
+        const double f0 = floor((double)s0 / ((double)lanes0 * tgt0)), f1 = floor((double)s1 / (256.0 * tgt1));
+        s_spl[0] = run ? (int)fmin((double)cap0, fmax(1.0, f0)) : 0;   // 0: the depth does not run
+        s_spl[1] = (int)fmin((double)cap1, fmax(1.0, f1));
+        spl_out[0] = max(s_spl[0], 1);
+        spl_out[1] = s_spl[1];
+    }
+    __syncthreads();
+    const bool run = s_spl[0] > 0;
+    const int64_t csz0 = (int64_t)lanes0 * max(s_spl[0], 1), csz1 = (int64_t)256 * s_spl[1];
+    // pass 2: per-node chunks (re-read: the loads stay batched), the thread's sums, the scan
+    auto chunks = [&](int i, int c, int64_t *v) {
+        const int D = min(deg[i], maxd);
+        v[0] = tab[D];
+        v[1] = tab[(maxd + 1) + D];
+        v[2] = tab[2 * (maxd + 1) + D];
+        v[3] = D;
+        (void)c;
+    };
+    int64_t sum[4] = {0, 0, 0, 0};
+    for (int i = lo; i < hi; ++i) {
+        int64_t v[4];
+        chunks(i, 0, v);
+        if (!run) continue;
+        sum[0] += (v[0] + csz0 - 1) / csz0;
+        sum[1] += (v[1] + csz1 - 1) / csz1;
+        sum[2] += v[2];
+        if (nblk && v[0] > 0) sum[3] += (v[3] + 1) * (v[3] + 1);
+    }
+    // exclusive scan over threads: wave inclusive scans, then the wave totals
+    int64_t inc[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        int64_t v = sum[c];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int64_t t = __shfl_up(v, o);
+            if (lane >= o) v += t;
+        }
+        inc[c] = v;
+        if (lane == 63) part[c][wv] = v;
+    }
+    __syncthreads();
+    if (tid < 4) {
+        int64_t acc = 0;
+        for (int w = 0; w < DEC_THREADS / 64; ++w) {
+            const int64_t v = part[tid][w];
+            part[tid][w] = acc;
+            acc += v;
+        }
+        wsum[tid][0] = acc;       // the class totals
+    }
+    __syncthreads();
+    int64_t acc[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] = part[c][wv] + inc[c] - sum[c];
+    for (int i = lo; i < hi; ++i) {
+        int64_t v[4];
+        chunks(i, 0, v);
+        cpre[i] = acc[0];
+        cpre[(int64_t)(n + 1) + i] = acc[1];
+        cpre[2 * (int64_t)(n + 1) + i] = acc[2];
+        if (nblk) bo[i] = acc[3];
+        if (!run) continue;
+        acc[0] += (v[0] + csz0 - 1) / csz0;
+        acc[1] += (v[1] + csz1 - 1) / csz1;
+        acc[2] += v[2];
+        if (nblk && v[0] > 0) acc[3] += (v[3] + 1) * (v[3] + 1);
+    }
+    if (tid == 0) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) cpre[c * (int64_t)(n + 1) + n] = wsum[c][0];
+        if (nblk) bo[n] = wsum[3][0];
     }
 }
 
@@ -1053,8 +1221,9 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
     const int tx = *s_tx;
     const double Cxx = a.diag[x];
     const uint64_t nS = pcg_binom(a.binom, D, d);
-    const uint64_t r0 = (uint64_t)(chunk - a.cpre[x]) * (uint64_t)bs * (uint64_t)a.spl;
-    const uint64_t r1 = min(nS, r0 + (uint64_t)bs * (uint64_t)a.spl);
+    const uint64_t spl = a.spl_dev ? (uint64_t)*a.spl_dev : (uint64_t)a.spl;
+    const uint64_t r0 = (uint64_t)(chunk - a.cpre[x]) * (uint64_t)bs * spl;
+    const uint64_t r1 = min(nS, r0 + (uint64_t)bs * spl);
     unsigned long long tests = 0, indep = 0;
 
     if constexpr (MODE == MODE_DECIDE && DM <= 4) {
@@ -1435,8 +1604,9 @@ __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_
     const int np = *s_np;
     const double Cxx = a.diag[x];
     const uint64_t ntask = ppre[np];
-    const uint64_t r0 = (uint64_t)(chunk - a.cpre[x]) * (uint64_t)bs * (uint64_t)a.spl;
-    const uint64_t r1 = min(ntask, r0 + (uint64_t)bs * (uint64_t)a.spl);
+    const uint64_t spl = a.spl_dev ? (uint64_t)*a.spl_dev : (uint64_t)a.spl;
+    const uint64_t r0 = (uint64_t)(chunk - a.cpre[x]) * (uint64_t)bs * spl;
+    const uint64_t r1 = min(ntask, r0 + (uint64_t)bs * spl);
     unsigned long long tests = 0, indep = 0;
     unsigned tcount = 0;
 
@@ -2113,8 +2283,9 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
     const int np = *s_np;
     const double Cxx = (double)(float)a.diag[x];                  // A~_xx
     const uint64_t ntask = ppre[np];
-    const uint64_t r0 = (uint64_t)(chunk - a.cpre[x]) * (uint64_t)bs * (uint64_t)a.spl;
-    const uint64_t r1 = min(ntask, r0 + (uint64_t)bs * (uint64_t)a.spl);
+    const uint64_t spl = a.spl_dev ? (uint64_t)*a.spl_dev : (uint64_t)a.spl;
+    const uint64_t r0 = (uint64_t)(chunk - a.cpre[x]) * (uint64_t)bs * spl;
+    const uint64_t r1 = min(ntask, r0 + (uint64_t)bs * spl);
     unsigned long long tests = 0, indep = 0;
     unsigned tcount = 0;
     const unsigned long long lanebit = 1ull << (tid & 63);
@@ -2580,14 +2751,15 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
 // kernels, before k_exact): decided like the fp64 kernels; independence writes the removal
 // flags and both sides' unions as k_exact does, the band goes on to the exact path.
 template <int DM>
-__global__ __launch_bounds__(256) void k_screen(LevelArgs a) {
-    const unsigned long long pushed = a.ctr->screened;
+__device__ __forceinline__ void screen_lanes(const LevelArgs &a, int blk, int nblk) {
+    // (volatile: in the fused barrier these counters were written by other blocks of this launch)
+    const unsigned long long pushed = *(volatile const unsigned long long *)&a.ctr->screened;
     const int64_t count = (int64_t)min((unsigned long long)a.scr_cap, pushed);
-    if (blockIdx.x == 0 && threadIdx.x == 0 && (int64_t)pushed > a.scr_cap)
+    if (blk == 0 && threadIdx.x == 0 && (int64_t)pushed > a.scr_cap)
         a.rm[(int64_t)a.n * a.n] = 1;      // overflow: every rank reruns (status byte 0)
     unsigned long long nindep = 0;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
+    const int64_t stride = (int64_t)nblk * blockDim.x;
+    for (int64_t i = (int64_t)blk * blockDim.x + threadIdx.x; i < count; i += stride) {
         const ScreenEntry e = a.screen[i];
         const int x = e.x, y = e.y;
         int sg[DM];
@@ -2620,6 +2792,11 @@ __global__ __launch_bounds__(256) void k_screen(LevelArgs a) {
     }
     nindep = wave_sum(nindep);
     if ((threadIdx.x & 63) == 0 && nindep) atomicAdd(&a.ctr->indep, nindep);
+}
+
+template <int DM>
+__global__ __launch_bounds__(256) void k_screen(LevelArgs a) {
+    screen_lanes<DM>(a, blockIdx.x, gridDim.x);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -3414,8 +3591,9 @@ __global__ __launch_bounds__(256) void k_level_wave(LevelArgs a) {
     const int tx = *s_tx;
     const double Cxx = a.diag[x];
     const uint64_t nS = pcg_binom(a.binom, D, d);
-    const uint64_t r0 = (uint64_t)(chunk - a.cpre[x]) * 4u * (uint64_t)a.spl + (uint64_t)wv * (uint64_t)a.spl;
-    const uint64_t r1 = min(nS, r0 + (uint64_t)a.spl);
+    const uint64_t spl = a.spl_dev ? (uint64_t)*a.spl_dev : (uint64_t)a.spl;
+    const uint64_t r0 = (uint64_t)(chunk - a.cpre[x]) * 4u * spl + (uint64_t)wv * spl;
+    const uint64_t r1 = min(nS, r0 + spl);
     unsigned long long tests = 0, indep = 0;
     if (r0 < r1) {
         unsigned long long mask = 0;      // colex unrank of r0 (wave-uniform)
@@ -3631,8 +3809,9 @@ __global__ __launch_bounds__(256) void k_level_wave_pr(LevelArgs a) {
     const int tx = *s_tx;
     const double Cxx = a.diag[x];
     const uint64_t nS = pcg_binom(a.binom, D, d);
-    const uint64_t r0 = (uint64_t)(chunk - a.cpre[x]) * 4u * (uint64_t)a.spl + (uint64_t)wv * (uint64_t)a.spl;
-    const uint64_t r1 = min(nS, r0 + (uint64_t)a.spl);
+    const uint64_t spl = a.spl_dev ? (uint64_t)*a.spl_dev : (uint64_t)a.spl;
+    const uint64_t r0 = (uint64_t)(chunk - a.cpre[x]) * 4u * spl + (uint64_t)wv * spl;
+    const uint64_t r1 = min(nS, r0 + spl);
     unsigned long long tests = 0, indep = 0;
     if (r0 < r1) {
         unsigned long long mask = 0;      // colex unrank of r0 (wave-uniform)
@@ -3807,8 +3986,7 @@ __device__ __forceinline__ int lu_from_lds(const double *A, double *i00, double 
 // One wave per deferred test: the lanes gather the (d+2)^2 correlation entries in parallel
 // into the wave's LDS slot (a single lane's rolled gather would wait out one HBM latency per
 // entry), then lane 0 factors and decides.
-__global__ __launch_bounds__(256) void k_exact(LevelArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+__device__ __forceinline__ void exact_waves(const LevelArgs &a, unsigned char *smem, int blk, int nblk) {
     const int d = a.d;
     const int m = d + 2;
     const int per = m * m + 2 * m;
@@ -3817,14 +3995,15 @@ __global__ __launch_bounds__(256) void k_exact(LevelArgs a) {
     double *B0 = A + m * m;
     double *B1 = B0 + m;
     int piv[PCG_MAX_DEPTH + 2];
-    const unsigned long long pushed = a.ctr->deferred;
+    const unsigned long long pushed = *(volatile const unsigned long long *)&a.ctr->deferred;
     const int64_t count = (int64_t)min((unsigned long long)a.def_cap, pushed);
-    if (blockIdx.x == 0 && threadIdx.x == 0 &&
-        ((int64_t)pushed > a.def_cap || (a.record && (int64_t)a.ctr->records > a.rec_cap)))
+    if (blk == 0 && threadIdx.x == 0 &&
+        ((int64_t)pushed > a.def_cap ||
+         (a.record && (int64_t)*(volatile const unsigned long long *)&a.ctr->records > a.rec_cap)))
         a.rm[(int64_t)a.n * a.n] = 1;      // overflow: every rank reruns (status byte 0)
     unsigned long long nexact = 0, nindep = 0;
-    const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
-    for (int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < count; i += waves) {
+    const int64_t waves = (int64_t)nblk * (blockDim.x >> 6);
+    for (int64_t i = (int64_t)blk * (blockDim.x >> 6) + (threadIdx.x >> 6); i < count; i += waves) {
         const DeferredEntry e = a.deferred[i];
         const int x = e.x, y = e.y;
         const int lo_ = x < y ? x : y, hi_ = x < y ? y : x;
@@ -3893,6 +4072,106 @@ __global__ __launch_bounds__(256) void k_exact(LevelArgs a) {
     }
     if (nexact) atomicAdd(&a.ctr->exact, nexact);
     if (nindep) atomicAdd(&a.ctr->indep, nindep);
+}
+
+__global__ __launch_bounds__(256) void k_exact(LevelArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    exact_waves(a, smem, blockIdx.x, gridDim.x);
+}
+
+// ---------------------------------------------------------------------------------------
+// The fused level barrier (single GPU): the fp32 sweep's fp64 screen, the exact path, the
+// removals (SkeletonDiscovery.py:141-144) and the next graph's summary + CSR in ONE launch of
+// FUSE_BLOCKS persistent blocks, its phases separated by grid barriers instead of four dependent
+// kernel launches (each a dispatch gap plus a ramp on an almost empty grid).
+//
+// Grid barrier: a self-resetting arrival count and a generation word in device memory. Block
+// leader: read gen, fence, add 1 to count; the last arrival zeroes count and bumps gen, the
+// others spin on gen. Every block of the grid is co-resident (FUSE_BLOCKS = one per CU, 256
+// threads, <= 64 KB LDS), so the spin always ends; it is bounded anyway: a leader that waits
+// ~1 s raises `abort`, every waiter leaves, the summary carries status byte 4 and the host
+// fails the level with PCG_ERR_HIP and clears the barrier words.
+constexpr int FUSE_BLOCKS = 256;
+struct GridBar {
+    unsigned count, gen, abort, pad;
+};
+
+__device__ bool grid_sync(GridBar *g, unsigned nblk) {
+    // every wave's stores have reached its XCD's L2 (gfx9 counts stores in vmcnt) before the
+    // leader's single agent-scope release writes the L2 back; the leader then polls with relaxed
+    // loads (an acquire per poll would invalidate the XCD's L2 on every iteration) and acquires
+    // once. (Measured first form: every thread fenced and every poll acquired, ~25-50 us per
+    // barrier.)
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    __shared__ int ok_s;
+    if (threadIdx.x == 0) {
+        int ok = 1;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const unsigned gen = __hip_atomic_load(&g->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned arrived = __hip_atomic_fetch_add(&g->count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (arrived == nblk - 1) {
+            (void)__hip_atomic_exchange(&g->count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&g->gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            unsigned spins = 0;
+            while (__hip_atomic_load(&g->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+                __builtin_amdgcn_s_sleep(2);
+                if (__hip_atomic_load(&g->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { ok = 0; break; }
+                if (++spins > (1u << 22)) {
+                    __hip_atomic_store(&g->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok = 0;
+                    break;
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        ok_s = ok;
+    }
+    __syncthreads();
+    return ok_s != 0;
+}
+
+struct LevelEndArgs {
+    GridBar *bar;
+    uint8_t *rm;
+    uint64_t *adj;
+    int32_t *deg;
+    int8_t *rl;
+    int n, W, d, nfill;
+    int32_t *off_new, *nbr_new;      // the next graph's CSR (the other buffer set)
+    uint64_t *ug_new;
+    int64_t ug_rows;
+    DevCounters *ctr;
+    uint8_t *status;
+    LevelSummary *out;
+    int32_t *out_deg;
+    unsigned long long seq;
+};
+
+template <int SDM>
+__global__ __launch_bounds__(256) void k_level_end(LevelArgs a, LevelEndArgs f) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ int cleared[4];
+    __shared__ int32_t part[256];
+    const int blk = blockIdx.x, nblk = gridDim.x;
+    bool ok = true;
+    if constexpr (SDM > 0) {
+        screen_lanes<SDM>(a, blk, nblk);
+        ok = grid_sync(f.bar, nblk);
+    }
+    if (ok) {
+        exact_waves(a, smem, blk, nblk);
+        ok = grid_sync(f.bar, nblk);
+    }
+    if (ok) {
+        close_rows(f.rm, f.adj, f.deg, f.rl, f.n, f.W, f.d, blk, nblk, cleared);
+        ok = grid_sync(f.bar, nblk);
+    }
+    if (blk == nblk - 1)   // the summary first: the host waits on it
+        summary_block(f.deg, f.n, f.off_new, f.ug_new, f.ug_rows, f.ctr, f.status, f.out, f.out_deg, f.seq, f.nfill,
+                      part, ok ? 0 : 1);
+    if (ok) summary_nodes(f.deg, f.n, f.W, f.adj, f.nbr_new, f.ug_new, f.ug_rows, f.nfill, blk, nblk);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -4588,6 +4867,7 @@ LevelArgs make_args(pcg_handle *h, int d, int mode_exact_all) {
     a.rec_mod = h->rec_mod;
     a.rec_res = h->rec_res;
     a.spl = h->spl;
+    a.spl_dev = (h->bound && h->dspl) ? (const int32_t *)h->spl_buf.p : nullptr;
     if (h->nblk) {
         const int64_t *t = (const int64_t *)h->cpre.p + h->sp_tab_off;
         a.coff = t;
@@ -4709,8 +4989,9 @@ LevelSummary *sum_slot(const pcg_handle *h, unsigned long long seq) {
 }
 
 // the level summary (degrees, counters, status) of the current adjacency -> host-mapped memory;
-// level_wait() spins until the device has written it
-int graph_launch(pcg_handle *h) {
+// level_wait() spins until the device has written it. With `fa` (the fused barrier, single GPU)
+// the depth's screen, exact path and removals run in the same launch (k_level_end) first.
+int graph_launch(pcg_handle *h, const LevelArgs *fa) {
     const int n = (int)h->n, W = h->W;
     const size_t slot = (sizeof(LevelSummary) + sizeof(int32_t) * (size_t)n + 255) & ~(size_t)255;
     if (!h->summary || h->summary_bytes < 2 * slot) {
@@ -4734,7 +5015,8 @@ int graph_launch(pcg_handle *h) {
     uint8_t *status = h->depth >= 0 ? (h->rm_ext ? h->rm_ext : (uint8_t *)h->rm.p) + (int64_t)n * n : nullptr;
     // the next depth's CSR is built from the device degrees while the host waits for the
     // summary; nbr is sized by the current graph (degrees only fall), and the union rows are
-    // cleared along with it when the buffer already covers that bound
+    // cleared along with it when the buffer already holds the new graph's rows (the device
+    // checks that against the new degree sum; at depth 0 the bound n(n - 1) would never fit)
     const int64_t bound = h->depth < 0 ? (int64_t)n * (n - 1) : h->sumdeg;
     // the new graph's CSR goes to the other buffer set; an export still reading that set (depth
     // d - 1's) is waited for on the device first
@@ -4749,14 +5031,55 @@ int graph_launch(pcg_handle *h) {
         (nfill && !pcg_ensure(h, h->nbr2[t], sizeof(int32_t) * std::max<int64_t>(bound, 1))))
         return pcg_fail(h, PCG_ERR_OOM, "neighbour lists");
     uint64_t *ug = nullptr;
-    if (h->depth >= 0 && h->ug2[t].p &&
-        h->ug2[t].bytes >= sizeof(uint64_t) * (size_t)std::max<int64_t>(bound, 1) * W)
+    int64_t ug_rows = 0;
+    if (h->depth >= 0 && h->ug2[t].p) {
         ug = (uint64_t *)h->ug2[t].p;
-    h->ug_clean2[t] = ug != nullptr;
-    hipLaunchKernelGGL(k_summary_fill, dim3((unsigned)(nfill + 1)), dim3(256), 0, h->stream,
-                       (const int32_t *)h->deg.p, n, W, (const uint64_t *)h->adj.p, (int32_t *)h->off2[t].p,
-                       (int32_t *)h->nbr2[t].p, ug, (DevCounters *)h->ctr.p, status, ds,
-                       reinterpret_cast<int32_t *>(ds + 1), seq, nfill);
+        ug_rows = (int64_t)(h->ug2[t].bytes / (sizeof(uint64_t) * (size_t)W));
+    }
+    // the new graph's degree sum is at most the current one (exact, or its bound): a buffer that
+    // holds that many rows is certainly cleared by the launch below; otherwise graph_finish takes
+    // the device's verdict from the summary
+    h->ug_clean2[t] = ug != nullptr && nfill > 0 && ug_rows >= h->sumdeg;
+    h->ug_pend_seq = (ug && !h->ug_clean2[t]) ? seq : 0;
+    h->ug_pend_set = t;
+    if (fa) {
+        if (!h->gbar.p) {
+            if (!pcg_ensure(h, h->gbar, sizeof(GridBar))) return pcg_fail(h, PCG_ERR_OOM, "grid barrier");
+            PCG_HIP(h, hipMemsetAsync(h->gbar.p, 0, sizeof(GridBar), h->stream));
+        }
+        LevelEndArgs f{};
+        f.bar = (GridBar *)h->gbar.p;
+        f.rm = h->rm_ext ? h->rm_ext : (uint8_t *)h->rm.p;
+        f.adj = (uint64_t *)h->adj.p;
+        f.deg = (int32_t *)h->deg.p;
+        f.rl = h->rl;
+        f.n = n;
+        f.W = W;
+        f.d = h->depth;
+        f.nfill = nfill;
+        f.off_new = (int32_t *)h->off2[t].p;
+        f.nbr_new = (int32_t *)h->nbr2[t].p;
+        f.ug_new = ug;
+        f.ug_rows = ug_rows;
+        f.ctr = (DevCounters *)h->ctr.p;
+        f.status = status;
+        f.out = ds;
+        f.out_deg = reinterpret_cast<int32_t *>(ds + 1);
+        f.seq = seq;
+        const int m = h->depth + 2;
+        const size_t lds = sizeof(double) * (size_t)(m * m + 2 * m) * 4;   // k_exact's slot per wave
+        const int sdm = fa->d >= 2 && fa->d <= 4 && h->tgroup && use_screen32(h, fa->d) ? fa->d : 0;
+        const dim3 grid(FUSE_BLOCKS), block(256);
+        if (sdm == 2) hipLaunchKernelGGL(k_level_end<2>, grid, block, lds, h->stream, *fa, f);
+        else if (sdm == 3) hipLaunchKernelGGL(k_level_end<3>, grid, block, lds, h->stream, *fa, f);
+        else if (sdm == 4) hipLaunchKernelGGL(k_level_end<4>, grid, block, lds, h->stream, *fa, f);
+        else hipLaunchKernelGGL(k_level_end<0>, grid, block, lds, h->stream, *fa, f);
+    } else {
+        hipLaunchKernelGGL(k_summary_fill, dim3((unsigned)(nfill + 1)), dim3(256), 0, h->stream,
+                           (const int32_t *)h->deg.p, n, W, (const uint64_t *)h->adj.p, (int32_t *)h->off2[t].p,
+                           (int32_t *)h->nbr2[t].p, ug, ug_rows, (DevCounters *)h->ctr.p, status, ds,
+                           reinterpret_cast<int32_t *>(ds + 1), seq, nfill);
+    }
     h->cb = t;
     PCG_HIP(h, hipGetLastError());
     if (h->lev_on && h->lev_n < 2 * PCG_MAX_LEVELS) {   // depth boundary (skeleton_once), off the host's critical path
@@ -4797,6 +5120,9 @@ int level_wait(pcg_handle *h, unsigned long long want) {
 void graph_finish(pcg_handle *h, unsigned long long seq) {
     const int n = (int)h->n;
     const int32_t *dp = reinterpret_cast<const int32_t *>(sum_slot(h, seq) + 1);
+    // the union rows' state counts only while no depth has used the set since (pipelined
+    // loops read the summary after level_begin_buffers has taken the set)
+    if (h->ug_pend_seq == seq && seq) h->ug_clean2[h->ug_pend_set] = sum_slot(h, seq)->ug_clean != 0;
     h->deg_h.assign(dp, dp + n);
     int64_t s = 0;
     int32_t mx = 0;
@@ -4864,7 +5190,7 @@ extern "C" int pcg_skeleton_init(pcg_handle *h, const double *C, int64_t n, int6
     PCG_HIP(h, hipGetLastError());
     // the level counters start at zero (k_summary_fill keeps the run's near-alpha count)
     PCG_HIP(h, hipMemsetAsync(h->ctr.p, 0, sizeof(DevCounters), h->stream));
-    int rc = graph_launch(h);            // also clears the counters
+    int rc = graph_launch(h, nullptr);   // also clears the counters
     if (rc) return rc;
     // the complete graph's degrees are known (k_init writes n - 1 everywhere): depth 0 is
     // decided and enqueued without waiting for this summary (the next level_wait covers it)
@@ -4922,8 +5248,16 @@ int level_begin_bound_upload(pcg_handle *h, int depth, int64_t blk_cap) {
     int64_t *dev = (int64_t *)h->cpre.p;
     hipLaunchKernelGGL(k_copy_i64, dim3((unsigned)((up + 255) / 256)), dim3(256), 0, h->stream, (const int64_t *)src, up,
                        dev + h->sp_tab_off);
-    hipLaunchKernelGGL(k_decompose, dim3(1), dim3(256), 0, h->stream, (const int32_t *)h->deg.p, n,
-                       (const int64_t *)(dev + h->dtab_off), maxd, depth, h->nblk ? 1 : 0, dev, dev + h->bo_off);
+    if (h->dspl) {
+        if (!pcg_ensure(h, h->spl_buf, 2 * sizeof(int32_t))) return pcg_fail(h, PCG_ERR_OOM, "device spl");
+        hipLaunchKernelGGL(k_decompose_dev, dim3(1), dim3(DEC_THREADS), 0, h->stream, (const int32_t *)h->deg.p, n,
+                           (const int64_t *)(dev + h->dtab_off), maxd, depth, h->nblk ? 1 : 0, h->dspl_lanes,
+                           h->dspl_tgt[0], h->dspl_cap[0], h->dspl_tgt[1], h->dspl_cap[1], dev, dev + h->bo_off,
+                           (int32_t *)h->spl_buf.p);
+    } else {
+        hipLaunchKernelGGL(k_decompose, dim3(1), dim3(256), 0, h->stream, (const int32_t *)h->deg.p, n,
+                           (const int64_t *)(dev + h->dtab_off), maxd, depth, h->nblk ? 1 : 0, dev, dev + h->bo_off);
+    }
     PCG_HIP(h, hipGetLastError());
     PCG_HT(h, "begin:decompose-launched");
     return level_begin_buffers(h, depth);
@@ -4932,6 +5266,27 @@ int level_begin_bound_upload(pcg_handle *h, int depth, int64_t blk_cap) {
 // bound: h->deg_h holds upper bounds of the degrees (those at the start of depth - 1; the
 // pipelined loop in skeleton_once). The class tables then cover every degree up to the bound, the
 // launch sizes are upper bounds, and k_decompose writes the exact prefixes on the device.
+// the pipelined loop's chunk size chosen on the device (k_decompose_dev); PCG_DEV_SPL=0: the
+// host's, from the bound degrees (A/B knob)
+static bool dev_spl_ok() {
+    const char *e = getenv("PCG_DEV_SPL");
+    return !e || atoi(e) != 0;
+}
+
+// the fused level barrier (k_level_end, PCG_FUSE_END=1) on one GPU with the handle's own removal
+// flags (a sharded run merges the ranks' flags between the exact path and the removals). Off by
+// default: measured slower than the separate k_screen / k_exact / k_level_close / k_summary_fill
+// launches (config 5: 4.77 vs 4.43 ms per step, n = 500 unlimited depth: 3.14 vs 2.50 ms; the
+// launch ran 87-143 us per depth against ~35 us for the four kernels and their gaps): its 256
+// persistent blocks process rows and nodes one after another where the separate launches put
+// one block per row / four nodes in flight at once, and each grid barrier costs an L2
+// write-back per block (profiles/r04_fused_barrier.txt)
+static bool fuse_end_ok(const pcg_handle *h) {
+    if (h->world != 1 || h->rm_ext) return false;
+    const char *e = getenv("PCG_FUSE_END");
+    return e && atoi(e) != 0;
+}
+
 int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks, bool bound) {
     if (!h || depth != h->depth + 1) return pcg_fail(h, PCG_ERR_INVALID, "pcg_level_begin: depth order");
     // reference loop condition: while max_degree() - 1 > depth_prev
@@ -4945,6 +5300,7 @@ int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks, bool bound
     if (bound && depth < 1) return pcg_fail(h, PCG_ERR_INVALID, "bound-mode decomposition at depth 0");
     h->depth = depth;
     h->bound = bound;
+    h->fuse_end = fuse_end_ok(h);
     const int n = (int)h->n;
     if (!bound) level_start_stats(h, depth);
     // per-degree tables: the decomposition below is O(n) lookups (it sits between two
@@ -5092,25 +5448,59 @@ int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks, bool bound
         if (bound) {
             // launch sizes: a node whose degree is at most its bound D_b may fall into any class,
             // with at most the largest chunk count of that class over degrees <= D_b
-            std::vector<int64_t> pm(3 * (size_t)(maxd + 1), 0);
-            for (int D = 0; D <= maxd; ++D)
+            std::vector<int64_t> pm(3 * (size_t)(maxd + 1), 0), pu(2 * (size_t)(maxd + 1), 0);
+            for (int D = 0; D <= maxd; ++D) {
                 for (int c = 0; c < 3; ++c)
                     pm[c * (maxd + 1) + D] = std::max(D ? pm[c * (maxd + 1) + D - 1] : 0,
                                                       (D >= depth + 1 && cls_of[D] == c) ? nch_of[D] : (int64_t)0);
-            int64_t tot[3] = {0, 0, 0}, sb = 0;
+                for (int c = 0; c < 2; ++c)
+                    pu[c * (maxd + 1) + D] = std::max(D ? pu[c * (maxd + 1) + D - 1] : 0,
+                                                      (D >= depth + 1 && cls_of[D] == c) ? (int64_t)units_of[D] : (int64_t)0);
+            }
+            int64_t tot[3] = {0, 0, 0}, sb = 0, ub[2] = {0, 0}, nb_[2] = {0, 0};
             for (int x = 0; x < n; ++x) {
                 const int Db = h->deg_h[x];
                 for (int c = 0; c < 3; ++c) tot[c] += pm[c * (maxd + 1) + Db];
+                for (int c = 0; c < 2; ++c) {
+                    ub[c] += pu[c * (maxd + 1) + Db];
+                    nb_[c] += pu[c * (maxd + 1) + Db] > 0;
+                }
                 int Dn = std::min(Db, std::min(SMALL_DEG, h->narrow_deg));   // largest narrow block
                 sb += (int64_t)(Dn + 1) * (Dn + 1);
+            }
+            // the chunk size chosen on the device (k_decompose_dev) from the exact degrees, unless
+            // the Schur-prefix sweep's per-degree chunk tables need the host's
+            h->dspl = !h->sp && dev_spl_ok();
+            h->dspl_lanes = h->wavek ? 4 : 256;
+            h->dspl_tgt[0] = nb_target * h->world;
+            h->dspl_tgt[1] = nbw_target * h->world;
+            h->dspl_cap[0] = (int)spl_cap;
+            h->dspl_cap[1] = 64;
+            if (h->dspl) {
+                // chunks <= nodes + sum / (lanes * spl): with spl = floor(sum / (lanes * target))
+                // >= 1 the second term is < 2 * target, with spl = 1 it is < target, and with spl at
+                // its cap it is at most the bound sum / (lanes * cap); never more than spl = 1 gives
+                const double L[2] = {(double)h->dspl_lanes, 256.0};
+                for (int c = 0; c < 2; ++c) {
+                    const double caps = std::ceil((double)ub[c] / (L[c] * h->dspl_cap[c]));
+                    const int64_t lim = nb_[c] + (int64_t)std::max(2.0 * h->dspl_tgt[c], caps) + 1;
+                    int64_t one = 0;          // the count at spl = 1
+                    for (int x = 0; x < n; ++x) {
+                        const int64_t u = pu[c * (maxd + 1) + h->deg_h[x]];
+                        one += (u + (int64_t)L[c] - 1) / (int64_t)L[c];
+                    }
+                    tot[c] = std::min(lim, one);
+                }
             }
             h->total_small = tot[0];
             h->total_wide = tot[1];
             h->total_large = tot[2];
-            // the per-degree class tables k_decompose reads: tab[c][D] = chunks of a degree-D node in class c
+            // the per-degree class tables k_decompose reads: tab[c][D] = chunks of a degree-D node in
+            // class c (k_decompose_dev: units for the narrow and wide classes, chunks for the large)
             h->dtab_maxd = maxd;
             h->cpre_h.assign(3 * (size_t)(maxd + 1), 0);
-            for (int D = depth + 1; D <= maxd; ++D) h->cpre_h[cls_of[D] * (maxd + 1) + D] = nch_of[D];
+            for (int D = depth + 1; D <= maxd; ++D)
+                h->cpre_h[cls_of[D] * (maxd + 1) + D] = (h->dspl && cls_of[D] < 2) ? (int64_t)units_of[D] : nch_of[D];
             bo.assign(1, sb);                 // compact-block capacity (an upper bound)
         } else {
         int64_t ss = 0, sw = 0, sl = 0, sb = 0;
@@ -5186,6 +5576,7 @@ int level_begin_buffers(pcg_handle *h, int depth) {
         if (!pcg_ensure(h, ugb_, ugb)) return pcg_fail(h, PCG_ERR_OOM, "sepset union rows (%zu B)", ugb);
         if (ugb_.p != before || !h->ug_clean2[h->cb]) PCG_HIP(h, hipMemsetAsync(ugb_.p, 0, ugb, h->stream));
         h->ug_clean2[h->cb] = false;
+        h->ug_pend_seq = 0;
         if (depth == 1 || h->export_cap == 0) {
             // every ordered pair adjacent at depth 1 is exported at most once over all depths
             // (depth-0 removals carry empty sepsets), so one allocation covers the run
@@ -5429,6 +5820,7 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                     aw.chunk_lo = w_lo;
                     aw.bs = 256;
                     aw.spl = h->spl_w;
+                    aw.spl_dev = a.spl_dev ? a.spl_dev + 1 : nullptr;
                     const int dl = (h->maxdeg_wide + 3) & ~3;
                     const dim3 grid((unsigned)(w_hi - w_lo)), block(256);
                     if (use_screen32(h, d)) {
@@ -5485,6 +5877,7 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
         PCG_HT(h, "run:launched");
         // exact path over the deferred list; the kernel reads the list length on the device
         // (no host round trip) and raises the overflow status byte if the list overflowed
+        if (h->fuse_end) return PCG_OK;   // the screen and exact path run in k_level_end
         a = make_args(h, d, mode == MODE_EXACT);
         if (h->tgroup && use_screen32(h, d)) {   // the fp32 sweep's undecided tests, in fp64
             // the list length is only known on the device; a grid-stride loop over it (1024 blocks
@@ -5511,13 +5904,20 @@ int level_end_enqueue(pcg_handle *h, unsigned long long *seq) {
     // everything below is stream-ordered; the level costs ONE host sync: export the unions of
     // removed pairs (device-side append), apply the removals (SkeletonDiscovery.py:141-144),
     // recount degrees, and fetch counters + status + degrees in one batch
-    hipLaunchKernelGGL(k_level_close, dim3((unsigned)n), dim3(256), 0, h->stream, rmb, (uint64_t *)h->adj.p,
-                       (int32_t *)h->deg.p, h->rl, n, W, d);
-    PCG_HIP(h, hipGetLastError());
+    LevelArgs fa{};
+    if (h->fuse_end) {
+        fa = make_args(h, d, mode_of(h, d) == MODE_EXACT);
+    } else {
+        hipLaunchKernelGGL(k_level_close, dim3((unsigned)n), dim3(256), 0, h->stream, rmb, (uint64_t *)h->adj.p,
+                           (int32_t *)h->deg.p, h->rl, n, W, d);
+        PCG_HIP(h, hipGetLastError());
+    }
     PCG_HT(h, "end:tail-launched");
     const int xcb = h->cb;               // depth d's CSR / union buffer set (graph_launch flips cb)
     const int64_t xsum = h->sumdeg;
-    int rc = graph_launch(h);            // degrees + counters + status -> host-mapped summary
+    // degrees + counters + status -> host-mapped summary (fused: after the screen, exact path
+    // and removals of the same launch)
+    int rc = graph_launch(h, h->fuse_end ? &fa : nullptr);
     if (!rc && d >= 1 && xsum > 0) {
         // depth d's sepset export on the export stream, queued behind the barrier (removed_level
         // written); it reads buffer set xcb while the next depth runs on the other set
@@ -5587,6 +5987,11 @@ int level_end_finish(pcg_handle *h, int d, unsigned long long seq, pcg_stats *st
     h->st.screened[d] = (int64_t)c.screened;
     h->st.near_alpha[d] = near_d;
     h->st.kernel_ms[d] = h->run_ms;
+    if (status[4]) {   // the fused barrier's grid barrier timed out: clear its words, fail the level
+        if (h->gbar.p) PCG_HIP(h, hipMemsetAsync(h->gbar.p, 0, sizeof(GridBar), h->stream));
+        if (stats) *stats = h->st;
+        return pcg_fail(h, PCG_ERR_HIP, "level %d: fused level barrier timed out", d);
+    }
     if (status[3]) {   // checked first: the failed rank will not rerun, so nobody may
         if (stats) *stats = h->st;
         return pcg_fail(h, PCG_ERR_PEER, "level %d: another rank failed at this depth", d);
@@ -5625,11 +6030,13 @@ extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
 
 // the pipelined level loop (PCG_PIPELINE=1; single GPU, the handle's own removal flags, threshold
 // mode) from depth PCG_PIPELINE_LO on. Off by default: it removes the host round trip per depth,
-// but that was not what the device waited for. Config 5 with depths 2-4 pipelined: 5.21-5.25 vs
-// 5.09 ms per step (bound-sized decomposition: too few, too large chunks where the degrees still
-// fall fast; k_decompose 21-42 us); n = 500 full depth (19 levels) from depth 2, 3 or 5: 2.49-2.51
-// vs 2.45-2.49 ms. The idle left between depths is the stream's dispatch gaps between its small
-// dependent kernels (profiles/r03_timeline.txt), not the host.
+// but that was not what the device waited for. Round 3, config 5 with depths 2-4 pipelined:
+// 5.21-5.25 vs 5.09 ms per step (bound-sized decomposition: too few, too large chunks where the
+// degrees still fall fast; k_decompose 21-42 us); n = 500 full depth (19 levels) from depth 2, 3
+// or 5: 2.49-2.51 vs 2.45-2.49 ms. Round 4, with the chunk size chosen on the device from the exact
+// degrees (k_decompose_dev, batched loads): config 5 4.53 vs 4.43 ms, n = 500 2.68 vs 2.50 ms
+// (host-chosen chunk size: 4.62 / 2.57) — the per-depth table upload and decomposition launches
+// and the bound-sized grids cost what the host round trip saved.
 #ifndef PCG_PIPELINE_LO
 #define PCG_PIPELINE_LO 5
 #endif

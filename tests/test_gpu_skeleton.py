@@ -211,22 +211,51 @@ def test_schur_prefix_sweep_matches_oracle(eng, n, N, seed, wl, wh, ep, sp, monk
     assert_skeleton_matches(out, ref, n)
 
 
-@pytest.mark.parametrize("lo", ["2", "3", "5"])
+@pytest.mark.parametrize("lo,dspl", [("2", "1"), ("3", "1"), ("5", "1"), ("2", "0")])
 @pytest.mark.parametrize("n,N,seed,wl,wh,ep", [CASES[6], (300, 1500, 7, 0.1, 0.6, 0.06)])
-def test_pipelined_level_loop_matches_oracle(eng, n, N, seed, wl, wh, ep, lo, monkeypatch):
+def test_pipelined_level_loop_matches_oracle(eng, n, N, seed, wl, wh, ep, lo, dspl, monkeypatch):
     """The pipelined level loop (PCG_PIPELINE=1: depth d >= PCG_PIPELINE_LO decomposed on the
-    degrees at the start of d - 1 and enqueued before depth d - 1's summary is read, k_decompose
-    writing the exact prefixes on the device, bound-sized launches): the oracle's skeleton, unions,
-    per-level counts and level count, unlimited depth."""
+    degrees at the start of d - 1 and enqueued before depth d - 1's summary is read, the exact
+    prefixes written on the device — with the chunk size chosen there from the exact degrees
+    (k_decompose_dev) or the host's from the bounds (PCG_DEV_SPL=0, k_decompose) — bound-sized
+    launches): the oracle's skeleton, unions, per-level counts and level count, unlimited depth."""
     monkeypatch.setenv("PCG_SMALL", "0")   # the level-loop kernels under test, also at n <= 64
     X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
     C = np.corrcoef(X.T)
     ref = cpc.skeleton(C, N)
     monkeypatch.setenv("PCG_PIPELINE", "1")
     monkeypatch.setenv("PCG_PIPELINE_LO", lo)
+    monkeypatch.setenv("PCG_DEV_SPL", dspl)
     out = eng.skeleton(C, N)
     assert_skeleton_matches(out, ref, n)
     assert out.levels == ref.levels
+
+
+@pytest.mark.parametrize("flags", [0, _lib.PCG_FLAG_FULL_P | _lib.PCG_FLAG_RECORD, _lib.PCG_FLAG_EXACT_ALL])
+@pytest.mark.parametrize("n,N,seed,wl,wh,ep", [CASES[6], (300, 1500, 7, 0.1, 0.6, 0.06)])
+def test_fused_level_barrier_equals_separate_launches(eng, n, N, seed, wl, wh, ep, flags, monkeypatch):
+    """The fused level barrier (k_level_end: screen, exact path, removals, summary + CSR in one
+    launch with grid barriers) against the separate launches (PCG_FUSE_END=0): identical removal
+    depths, per-level counters, degree snapshots and sepset rows; both equal the oracle."""
+    monkeypatch.setenv("PCG_SMALL", "0")   # the level-loop kernels under test, also at n <= 64
+    X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
+    C = np.corrcoef(X.T)
+    outs = []
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("PCG_FUSE_END", fuse)
+        outs.append(eng.skeleton(C, N, flags=flags, record_capacity=2_000_000))
+    a, b = outs
+    np.testing.assert_array_equal(a.removed_level, b.removed_level)
+    for k in ("levels", "tests", "calls", "indep", "exact", "screened", "edges_after", "max_degree", "error"):
+        assert a.stats[k] == b.stats[k], k
+    np.testing.assert_array_equal(a.deg_levels, b.deg_levels)
+    rows = [sorted((int(x), int(y), tuple(int(v) for v in r)) for (x, y), r in
+                   zip(np.asarray(o.sep_xy.cpu() if hasattr(o.sep_xy, "cpu") else o.sep_xy),
+                       np.asarray(o.sep_bits.cpu() if hasattr(o.sep_bits, "cpu") else o.sep_bits))) for o in outs]
+    assert rows[0] == rows[1]
+    if flags & _lib.PCG_FLAG_RECORD:
+        assert len(a.records) == len(b.records)
+    assert_skeleton_matches(a, cpc.skeleton(C, N), n)
 
 
 def test_screen_list_overflow_reruns(eng):
@@ -289,17 +318,19 @@ def test_decide_and_fullp_agree_2000_depth2(eng):
 def test_config5_full_depth4_matches_oracle(eng):
     """BASELINE config 5 at full size and full depth: 2000 vars x 10 000 samples, seed 0,
     max_depth 4 — the benchmarked workload, whose depth 4 (83 % of the 4.9e9 unique tests) runs
-    on the dominant k_level_lds_t<4> kernel. Threshold-mode removal depth of every pair,
-    per-level unique-test counts and sepset unions against the C oracle on the same C
-    (only pairs touched by an enumerated |p - alpha| < 1e-9 test are exempt); then the
+    on the dominant k_level_lds_t<4> kernel. Threshold-mode removal depth of every pair from
+    pcg_pc_skeleton (K1 + skeleton in one call), per-level unique-test counts and sepset unions
+    against the C oracle on np.corrcoef(X.T) (only pairs touched by an enumerated |p - alpha| < 1e-9 test are exempt); then the
     full-p kernels on the same graph, with recorded p of a fixed pair sample (1 in 4099 pairs,
     every depth) within 1e-9 relative (+2^-51) of the oracle's FisherZ."""
     import sys
     import time
     X = synth.gaussian_sem(2000, 10000, seed=0)
-    C = eng.corr(X)
-    Ch = C.cpu().numpy()
-    a = eng.skeleton(C, 10000, max_depth=4, flags=0)
+    # K1 + skeleton through the one C call (pcg_pc_skeleton); the oracle runs on numpy's
+    # corrcoef, so the correlation kernel is inside the end-to-end comparison
+    a, C = eng.corr_skeleton(X, max_depth=4, flags=0)
+    Ch = np.corrcoef(X.T)
+    assert np.abs(C.cpu().numpy() - Ch).max() <= 2e-14
     assert a.levels == 5 and sum(a.stats["tests"]) > 4.5e9
     b = eng.skeleton(C, 10000, max_depth=4, flags=_lib.PCG_FLAG_FULL_P | _lib.PCG_FLAG_RECORD,
                      record_capacity=4_000_000, record_sample=(4099, 17))

@@ -17,6 +17,10 @@ step() {
 }
 step small 300 python -u -m pytest tests/test_gpu_small.py tests/test_gpu_skeleton_ref.py -q --timeout 100 --timeout-method thread
 tail -2 $O/small.log
+step skel 500 python -u -m pytest tests/test_gpu_skeleton.py -q -x --timeout 150 --timeout-method thread
+tail -2 $O/skel.log
+step bench 300 python -u bench.py --steps 20 --warmup 5
+tail -1 $O/bench.log
 step e2e 600 python -u -m pytest tests/test_gpu_e2e.py tests/test_gpu_fci.py tests/test_gpu_rq1.py -q --timeout 200 --timeout-method thread
 tail -2 $O/e2e.log
 step small_bench 200 python -u tools/small_bench.py 44 600 200
