@@ -853,17 +853,154 @@ __global__ __launch_bounds__(512, 1) void k_xtx_crt(const int8_t *R, int TB, int
         }
 }
 
-// byte offset of entry (li, lj) of a unit (the lane order of k_xtx_crt's epilogue)
+// The same unit with 4 waves as 2 x 2, each 128 x 128 (4 x 4 MFMA tiles, 256 int32 accumulators
+// in AGPRs, one wave per SIMD). Per k-block a wave reads 8 fragments (8 KB for the CU's four waves
+// x 4 = 32 KB) for 16 MFMAs, where the 2 x 4 form reads 48 KB for the same 64 MFMAs per CU: with
+// the 16 KB the DMA writes, 48 instead of 64 KB of LDS traffic per 512 MFMA cycles of each SIMD
+// (LDS peak 128 B per CU cycle: 73 % instead of 98 % of it). Measured slower, so off by default
+// (PCG_K1_CRT_W4=1): 0.49 vs 0.40 ms per launch at config 5, MFMA busy 37 vs 44 % — with one wave
+// per SIMD the stage barriers and DMA waits are no longer covered by the other wave
+// (SQ_WAIT_INST_ANY 48 % of wave cycles); the LDS traffic was not what bound the 8-wave form.
+// Bitwise equal results (test_corr_crt_split_invariant). Staging: one DMA instruction moves
+// 4 KB (256 threads x 16 B); q = 0 .. 4 CRT_KB - 1 of a stage is k-block q >> 2, side (q >> 1) & 1,
+// column blocks 2 (q & 1) + (tid >> 7), word tid & 127 -- the same LDS image as k_xtx_crt's.
+// Unit byte order: ((w * 4 + a) * 4 + b) * 1024 + lane * 16 + kk (crt_unit_offset<true>).
+__global__ __launch_bounds__(256, 1) void k_xtx_crt4(const int8_t *R, int TB, int64_t plane, int T, int ntiles, int ks,
+                                                   int kb, CrtTab tab, int64_t u0, int64_t nu, uint8_t *out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    int64_t lin = blockIdx.x;
+    {   // XCD-contiguous runs: an XCD's resident blocks share the modulus and slab (all panels in its L2)
+        const int64_t per = gridDim.x / 8;
+        lin = (blockIdx.x % 8) * per + blockIdx.x / 8;
+        if (lin >= nu) return;
+    }
+    const int64_t u = u0 + lin;
+    const int t = (int)(u % ntiles);
+    const int64_t sm = u / ntiles;
+    const int mi = (int)(sm / ks), slab = (int)(sm % ks);
+    int bi, bj;
+    tile_of(t, T, bi, bj);
+    const int tb0 = slab * kb, tb1 = min(TB, tb0 + kb);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r = lane & 31, hh = lane >> 5;
+    const int wr = w >> 1, wc = w & 1;
+
+    v16i acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[a][b][q] = 0;
+
+    const int8_t *Rm = R + (int64_t)mi * plane;
+    const int8_t *srcA = Rm + (int64_t)(bi * 4 + (tid >> 7)) * TB * 2048 + (tid & 127) * 16;
+    const int8_t *srcB = Rm + (int64_t)(bj * 4 + (tid >> 7)) * TB * 2048 + (tid & 127) * 16;
+    const int64_t cb2 = (int64_t)2 * TB * 2048;    // two column blocks on
+    const int nkb = tb1 - tb0;
+    const int ns = (nkb + CRT_KB - 1) / CRT_KB;
+    auto issue = [&](int sidx) {
+        if (sidx >= ns) return;
+        unsigned char *dst = smem + (sidx % CRT_NS) * CRT_STAGE + w * 1024;
+#pragma unroll
+        for (int q = 0; q < 4 * CRT_KB; ++q) {
+            // a partial last stage re-reads its last k-block (fixed DMA count per stage)
+            const int64_t tb = tb0 + min(sidx * CRT_KB + (q >> 2), nkb - 1);
+            const int8_t *src = (((q >> 1) & 1) ? srcB : srcA) + ((q & 1) ? cb2 : 0) + tb * 2048;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                             (__attribute__((address_space(3))) void *)(dst + q * 4096), 16, 0, 0);
+        }
+    };
+#pragma unroll
+    for (int sidx = 0; sidx < CRT_NS - 1; ++sidx) issue(sidx);
+    const unsigned char *fa = smem + (2 * wr * 2048 + hh * 1024 + r * 16);
+    const unsigned char *fb = smem + (8192 + 2 * wc * 2048 + hh * 1024 + r * 16);
+    for (int sidx = 0; sidx < ns; ++sidx) {
+        const int ahead = min(CRT_NS - 2, ns - 1 - sidx);
+        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * 4 * CRT_KB) : "memory");
+        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * CRT_KB) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        issue(sidx + CRT_NS - 1);
+        const int off = (sidx % CRT_NS) * CRT_STAGE;
+        v4i af[2][4], bf[2][4];
+        auto frag = [&](int kk, int sl) {
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+                af[sl][a] = *reinterpret_cast<const v4i *>(fa + off + kk * 16384 + (a >> 1) * 2048 + (a & 1) * 512);
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                bf[sl][b] = *reinterpret_cast<const v4i *>(fb + off + kk * 16384 + (b >> 1) * 2048 + (b & 1) * 512);
+        };
+        const int cnt = min(CRT_KB, nkb - sidx * CRT_KB);
+        frag(0, 0);
+#pragma unroll
+        for (int kk = 0; kk < CRT_KB; ++kk) {
+            if (kk < cnt) {
+                const bool nxt = kk + 1 < CRT_KB && kk + 1 < cnt;
+                if (nxt) frag(kk + 1, (kk + 1) & 1);
+#pragma unroll
+                for (int a = 0; a < 4; ++a)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+                        acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[kk & 1][a], bf[kk & 1][b], acc[a][b], 0,
+                                                                          0, 0);
+                if (PCG_CRT_SCHED && nxt) {
+                    // the 8 fragment reads of k-block kk + 1 between the first 8 of kk's 16 MFMAs
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // 1 DS read
+                    }
+                    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+                }
+            }
+        }
+    }
+    const int m = tab.m[mi];
+    const double dm = (double)m, dinv = tab.dinv[mi];
+    uint8_t *o = out + lin * CRT_UNIT + (int64_t)w * 16384 + lane * 16;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            v4i pk = {0, 0, 0, 0};
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int v = acc[a][b][q];
+                uint32_t rr;
+                if (m == 256) {
+                    rr = (uint32_t)v & 255u;
+                } else {
+                    const double d = (double)v;
+                    int x = (int)fma(floor(d * dinv), -dm, d);
+                    x += x < 0 ? m : 0;
+                    x -= x >= m ? m : 0;
+                    rr = (uint32_t)x;
+                }
+                pk[q >> 2] |= (int)(rr << (8 * (q & 3)));
+            }
+            *reinterpret_cast<v4i *>(o + (a * 4 + b) * 1024) = pk;
+        }
+}
+
+// byte offset of entry (li, lj) of a unit (the lane order of k_xtx_crt's epilogue; W4:
+// k_xtx_crt4's)
+template <bool W4>
 __device__ __forceinline__ int crt_unit_offset(int li, int lj) {
     const int wr = li >> 7, a = (li >> 5) & 3, rr = li & 31;
     const int hh = (rr >> 2) & 1, q = (rr & 3) | ((rr >> 3) << 2);
+    if (W4) {
+        const int wc = lj >> 7, b = (lj >> 5) & 3, r = lj & 31;
+        return ((((wr * 2 + wc) * 4 + a) * 4 + b) * 64 + r + 32 * hh) * 16 + q;
+    }
     const int wc = lj >> 6, b = (lj >> 5) & 1, r = lj & 31;
     return ((((wr * 4 + wc) * 4 + a) * 2 + b) * 64 + r + 32 * hh) * 16 + q;
 }
 
 // sd_i = sqrt(G_ii / (N - 1)) from the diagonal entries' residues (one thread per i; every
 // residue load issued before the first use)
-template <int L>
+template <int L, bool W4>
 __global__ __launch_bounds__(256) void k_crt_diag(const uint8_t *Rs, int T, int ntiles, int ks, CrtTab tab,
                                                  const int *expo, int n, double scale, double *sd) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -877,7 +1014,7 @@ __global__ __launch_bounds__(256) void k_crt_diag(const uint8_t *Rs, int T, int 
     }
     const int k = tab.k;
     const int64_t ustride = (int64_t)ntiles * CRT_UNIT;
-    const uint8_t *src = Rs + (int64_t)t * CRT_UNIT + crt_unit_offset(i % CRT_T, i % CRT_T);
+    const uint8_t *src = Rs + (int64_t)t * CRT_UNIT + crt_unit_offset<W4>(i % CRT_T, i % CRT_T);
     uint32_t sv[CRT_KMAX];
 #pragma unroll
     for (int mi = 0; mi < CRT_KMAX; ++mi) sv[mi] = 0;
@@ -900,7 +1037,7 @@ __global__ __launch_bounds__(256) void k_crt_diag(const uint8_t *Rs, int T, int 
 // 16-byte lane word of the units: the same column j, 4 consecutive rows i); residues summed over
 // the ks slabs in u16 lanes, moduli outermost (each modulus' constants read once, 4 independent
 // chains); writes C_ij and its mirror C_ji, each in numpy's division order
-template <int L>
+template <int L, bool W4>
 __global__ __launch_bounds__(256) void k_crt_finish(const uint8_t *Rs, int T, int ntiles, int ks, CrtTab tab,
                                                    const int *expo, int n, const double *sd, double scale, double *C,
                                                    int64_t ldc) {
@@ -910,9 +1047,21 @@ __global__ __launch_bounds__(256) void k_crt_finish(const uint8_t *Rs, int T, in
     int bi, bj;
     tile_of(t, T, bi, bj);
     const int lane = rem & 63, wab = rem >> 6;
-    const int b = wab & 1, a = (wab >> 1) & 3, w = wab >> 3;
-    const int wr = w >> 2, wc = w & 3, r = lane & 31, hh = lane >> 5;
-    const int j = bj * CRT_T + wc * 64 + b * 32 + r;
+    const int r = lane & 31, hh = lane >> 5;
+    int a, b, wr, wc, j;
+    if (W4) {                               // ((w * 4 + a) * 4 + b), w = 2 wr + wc (k_xtx_crt4)
+        b = wab & 3;
+        a = (wab >> 2) & 3;
+        wr = wab >> 5;
+        wc = (wab >> 4) & 1;
+        j = bj * CRT_T + wc * 128 + b * 32 + r;
+    } else {                                // ((w * 4 + a) * 2 + b), w = 4 wr + wc (k_xtx_crt)
+        b = wab & 1;
+        a = (wab >> 1) & 3;
+        wr = wab >> 5;
+        wc = (wab >> 3) & 3;
+        j = bj * CRT_T + wc * 64 + b * 32 + r;
+    }
     // this word: accumulators q = 4 g .. 4 g + 3, rows ibase + (q & 3) + 8 (q >> 2) = ibase + q4 + 8 g
     const int ibase = bi * CRT_T + wr * 128 + a * 32 + 4 * hh + 8 * g;
     if (j >= n || ibase > j) return;
@@ -997,6 +1146,7 @@ struct CrtPlan {
     CrtTab tab;
     int T = 0, ntiles = 0, ks = 0, kb = 0, TB = 0, CBp = 0;
     int64_t units = 0;
+    bool w4 = false;    // k_xtx_crt4 (4 waves of 128 x 128) and its unit byte order (PCG_K1_CRT_W4=1); else k_xtx_crt
 };
 
 static int env_int(const char *name, int dflt) {
@@ -1007,7 +1157,7 @@ static int env_int(const char *name, int dflt) {
 // the plan's A/B knobs (read at each call; pcg_corr_sharded agrees the resulting plan's signature
 // across ranks before its all-gather, so ranks started with different knobs fail together)
 struct CrtKnobs {
-    bool on;
+    bool on, w4;
     int minn, bmin, ks;
 };
 static CrtKnobs crt_knobs() {
@@ -1016,6 +1166,7 @@ static CrtKnobs crt_knobs() {
     v.minn = env_int("PCG_K1_CRT_MINN", 256);
     v.bmin = std::min(63, std::max(32, env_int("PCG_K1_CRT_BITS", 56)));   // k_residues needs b in [32, 63]
     v.ks = env_int("PCG_K1_CRT_KS", 0);
+    v.w4 = env_int("PCG_K1_CRT_W4", 0) != 0;   // off: 0.49 vs 0.40 ms (one wave per SIMD waits out its latencies)
     return v;
 }
 
@@ -1052,6 +1203,7 @@ bool crt_plan(int n, int64_t N, CrtPlan &p) {
     }
     if (b < bmin) return false;
     b = std::min(b, 63);
+    p.w4 = kn.w4;
     CrtTab &t = p.tab;
     memset(&t, 0, sizeof(t));
     t.k = k;
@@ -1142,8 +1294,12 @@ int crt_residues(pcg_handle *h, const CrtPlan &p, const double *X, int64_t N, in
 void crt_gemm(pcg_handle *h, const CrtPlan &p, const int8_t *R, int64_t u0, int64_t nu, uint8_t *out) {
     if (nu <= 0) return;
     const int64_t plane = (int64_t)p.CBp * p.TB * 2048;
-    hipLaunchKernelGGL(k_xtx_crt, dim3((unsigned)((nu + 7) / 8 * 8)), dim3(512), CRT_NS * CRT_STAGE, h->stream, R, p.TB,
-                       plane, p.T, p.ntiles, p.ks, p.kb, p.tab, u0, nu, out);
+    if (p.w4)
+        hipLaunchKernelGGL(k_xtx_crt4, dim3((unsigned)((nu + 7) / 8 * 8)), dim3(256), CRT_NS * CRT_STAGE, h->stream, R,
+                           p.TB, plane, p.T, p.ntiles, p.ks, p.kb, p.tab, u0, nu, out);
+    else
+        hipLaunchKernelGGL(k_xtx_crt, dim3((unsigned)((nu + 7) / 8 * 8)), dim3(512), CRT_NS * CRT_STAGE, h->stream, R,
+                           p.TB, plane, p.T, p.ntiles, p.ks, p.kb, p.tab, u0, nu, out);
 }
 
 // C from the units' residues: the diagonal (sd) first, then every upper entry and its mirror
@@ -1151,11 +1307,19 @@ void crt_finish(pcg_handle *h, const CrtPlan &p, const uint8_t *Rs, const int *e
                 double *C, int64_t ldc) {
     const double scale = 1.0 / (double)(N - 1);
     const int64_t threads = (int64_t)p.ntiles * 16384;
-#define CRT_LAUNCH(L_)                                                                                          \
-    hipLaunchKernelGGL(k_crt_diag<L_>, dim3((unsigned)((nn + 255) / 256)), dim3(256), 0, h->stream, Rs, p.T,     \
+#define CRT_LAUNCH_W(L_, W_)                                                                                    \
+    hipLaunchKernelGGL((k_crt_diag<L_, W_>), dim3((unsigned)((nn + 255) / 256)), dim3(256), 0, h->stream, Rs, p.T, \
                        p.ntiles, p.ks, p.tab, expo, nn, scale, sd);                                              \
-    hipLaunchKernelGGL(k_crt_finish<L_>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, h->stream, Rs, p.T, \
-                       p.ntiles, p.ks, p.tab, expo, nn, (const double *)sd, scale, C, ldc)
+    hipLaunchKernelGGL((k_crt_finish<L_, W_>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, h->stream, Rs, \
+                       p.T, p.ntiles, p.ks, p.tab, expo, nn, (const double *)sd, scale, C, ldc)
+#define CRT_LAUNCH(L_)                  \
+    do {                                \
+        if (p.w4) {                     \
+            CRT_LAUNCH_W(L_, true);     \
+        } else {                        \
+            CRT_LAUNCH_W(L_, false);    \
+        }                               \
+    } while (0)
     if (p.tab.L <= 4) { CRT_LAUNCH(4); }
     else if (p.tab.L == 5) { CRT_LAUNCH(5); }
     else { CRT_LAUNCH(6); }
@@ -1355,8 +1519,8 @@ int column_means(pcg_handle *h, const double *X, int64_t N, int nn, int64_t ldx,
 int64_t k1_plan_signature(int64_t n, int64_t N) {
     CrtPlan cp;
     if (crt_plan((int)n, N, cp))
-        return ((int64_t)1 << 62) | ((int64_t)cp.tab.k << 48) | ((int64_t)cp.tab.b << 40) | ((int64_t)cp.ks << 32) |
-               (cp.units & 0xffffffffll);
+        return ((int64_t)1 << 62) | ((int64_t)cp.w4 << 56) | ((int64_t)cp.tab.k << 48) | ((int64_t)cp.tab.b << 40) |
+               ((int64_t)cp.ks << 32) | (cp.units & 0xffffffffll);
     return k1_i8() ? 1 : 2;
 }
 

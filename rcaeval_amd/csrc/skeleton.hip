@@ -2076,6 +2076,13 @@ constexpr double F32_U = 5.9604644775390625e-08;   // 2^-24
 #define PCG_TGF_PREFETCH 0   // k_level_lds_f depths (bit 1 << d) whose per-lane y loop prefetches row t + 1
                              // (depth 3: 0.703 vs 0.698 ms without it; measured no gain, off)
 #endif
+#ifndef PCG_TGF_ABL
+#define PCG_TGF_ABL 0     // k_level_lds_f ablation builds for timing (tools/build_variant.sh): 1 = tasks without their
+                          // sweeps, 2 = no tasks (staging and block overhead only); results are wrong
+#endif
+#ifndef PCG_TGF_ABL_D
+#define PCG_TGF_ABL_D 4   // the depth the ablation applies to (the narrow class only)
+#endif
 #ifndef PCG_TGF_SPLIT
 #define PCG_TGF_SPLIT 1   // k_level_lds_f, one candidate window per wave: y outside the window without the
                           // dead-candidate selects (depth 4: 2.24 -> 2.09 ms once the rare-path values were opaque)
@@ -2285,7 +2292,8 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
     const uint64_t ntask = ppre[np];
     const uint64_t spl = a.spl_dev ? (uint64_t)*a.spl_dev : (uint64_t)a.spl;
     const uint64_t r0 = (uint64_t)(chunk - a.cpre[x]) * (uint64_t)bs * spl;
-    const uint64_t r1 = min(ntask, r0 + (uint64_t)bs * spl);
+    constexpr int ABL = (DM == PCG_TGF_ABL_D && !WIDE) ? PCG_TGF_ABL : 0;
+    const uint64_t r1 = (ABL & 2) ? r0 : min(ntask, r0 + (uint64_t)bs * spl);   // (ablation: no tasks)
     unsigned long long tests = 0, indep = 0;
     unsigned tcount = 0;
     const unsigned long long lanebit = 1ull << (tid & 63);
@@ -2704,6 +2712,19 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
                 for (int t = 0; t < D; ++t) ystep(t, Y2{}, yload(t));
             }
         };
+        if constexpr (ABL & 1) {
+            // ablation timing only (wrong results): the task's decode + setup without its sweep;
+            // every setup output feeds one dummy so none of it is dead code
+            float z = (float)okm + (float)tx + uTf[0] + Lif[DT - 1][0];
+#pragma unroll
+            for (int q = 0; q < NP; ++q) {
+                z += mp[q][0] + hhp[q][1] + k1p[q][0] + k2p[q][1] + rlp[q][0] + ucp[q][1];
+#pragma unroll
+                for (int i = 0; i < DT; ++i) z += lcp[q][i][0] + lcp[q][i][1];
+            }
+            tests += (z == 1234.5f) ? 1u : 0u;
+            continue;
+        }
         if constexpr (TG == 4) {
             if (nmax > 2) sweep(std::integral_constant<int, 4>{});
             else sweep(std::integral_constant<int, 2>{});
@@ -5279,8 +5300,9 @@ static bool dev_spl_ok() {
 // launches (config 5: 4.77 vs 4.43 ms per step, n = 500 unlimited depth: 3.14 vs 2.50 ms; the
 // launch ran 87-143 us per depth against ~35 us for the four kernels and their gaps): its 256
 // persistent blocks process rows and nodes one after another where the separate launches put
-// one block per row / four nodes in flight at once, and each grid barrier costs an L2
-// write-back per block (profiles/r04_fused_barrier.txt)
+// one block per row / four nodes in flight at once, and a software grid barrier costs ~20 us
+// on this part against ~2.5 us for a dependent kernel boundary (tools/micro/grid_barrier.hip,
+// profiles/r04_grid_barrier.txt; timeline: profiles/r04_timeline_fused_barrier.txt)
 static bool fuse_end_ok(const pcg_handle *h) {
     if (h->world != 1 || h->rm_ext) return false;
     const char *e = getenv("PCG_FUSE_END");

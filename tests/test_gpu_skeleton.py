@@ -107,9 +107,9 @@ def test_corr_crt_extreme_magnitudes(eng, N):
 
 @pytest.mark.parametrize("n,N", [(300, 1200), (2000, 10000)])
 def test_corr_crt_split_invariant(eng, n, N, monkeypatch):
-    """The CRT result is the correctly rounded exact Gram, so every split-K choice and the grouped
-    residue / GEMM overlap give the same bits; the digit path (PCG_K1_CRT=0) agrees to within its
-    own truncation."""
+    """The CRT result is the correctly rounded exact Gram, so every split-K choice, the grouped
+    residue / GEMM overlap and both GEMM wave layouts (k_xtx_crt4 / k_xtx_crt) give the same bits;
+    the digit path (PCG_K1_CRT=0) agrees to within its own truncation."""
     X = synth.gaussian_sem(n, N, seed=5, w_low=0.1, w_high=0.5)
     Xd = eng.to_device(X)
     C0 = eng.corr(Xd).cpu().numpy()
@@ -121,6 +121,9 @@ def test_corr_crt_split_invariant(eng, n, N, monkeypatch):
         monkeypatch.setenv("PCG_K1_CRT_GROUPS", groups)
         np.testing.assert_array_equal(eng.corr(Xd).cpu().numpy(), C0)
     monkeypatch.delenv("PCG_K1_CRT_GROUPS")
+    monkeypatch.setenv("PCG_K1_CRT_W4", "1")   # the 4-wave 128 x 128 GEMM and its unit byte order
+    np.testing.assert_array_equal(eng.corr(Xd).cpu().numpy(), C0)
+    monkeypatch.delenv("PCG_K1_CRT_W4")
     monkeypatch.setenv("PCG_K1_CRT", "0")
     Cd = eng.corr(Xd).cpu().numpy()
     np.testing.assert_allclose(Cd, C0, rtol=0, atol=1e-15)
