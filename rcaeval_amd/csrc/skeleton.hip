@@ -742,6 +742,48 @@ __global__ __launch_bounds__(DEC_THREADS) void k_decompose_dev(const int32_t *de
     }
 }
 
+// The node owning a chunk: the last x < n with cpre[x] <= chunk (the caller checked chunk <
+// cpre[n]). A wave samples 64 prefix entries per round and narrows to the ballot's last hit, so
+// n = 2000 takes two dependent loads instead of a binary search's eleven (each an L2 round trip at
+// the start of every block). Every lane of the wave must be active; the result is wave-uniform.
+__device__ __forceinline__ int chunk_node(const int64_t *cpre, int n, int64_t chunk) {
+    const int lane = threadIdx.x & 63;
+    int lo = 0, hi = n;                                   // cpre[lo] <= chunk < cpre[hi]
+    while (hi - lo > 1) {
+        const int step = (hi - lo + 63) >> 6;
+        const int idx = lo + lane * step;
+        const bool le = idx < hi && cpre[idx] <= chunk;   // a prefix of the lanes (cpre ascends)
+        const unsigned long long b = __ballot(le);        // lane 0 always set
+        const int j = 63 - __builtin_clzll(b);
+        lo += j * step;
+        hi = min(hi, lo + step);
+    }
+    return lo;
+}
+
+// Local adjacency masks of a narrow node (D <= 64): row t's bit k = adj(nxs[t], nxs[k]); a wave
+// takes four rows at a time with their four loads in flight before the ballots (the one-row loop
+// waited out one L2 round trip per row)
+__device__ __forceinline__ void stage_lmask(const LevelArgs &a, const int32_t *nxs, int D, unsigned long long *lmask) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    const int kg = lane < D ? nxs[lane] : 0;
+    for (int t0 = wv; t0 < D; t0 += 4 * nwv) {
+        uint64_t w[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int t = t0 + r * nwv;
+            w[r] = (t < D && lane < D) ? a.adj[(int64_t)nxs[t] * a.W + (kg >> 6)] : 0ull;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int t = t0 + r * nwv;
+            if (t >= D) break;                // wave-uniform
+            const unsigned long long m = __ballot(lane < D && ((w[r] >> (kg & 63)) & 1ull));
+            if (lane == 0) lmask[t] = m;
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // depth 0: one chunk = one 64 x 64 tile (bi <= bj) of the pair triangle; node bi*64 owns the
 // chunks of tile row bi. Decisions are staged in LDS so both rm[x][y] and its mirror
@@ -752,11 +794,7 @@ __global__ __launch_bounds__(256) void k_level0(LevelArgs a) {
     __shared__ uint8_t flag[64][68];
     const int64_t chunk = a.chunk_lo + blockIdx.x;
     if (chunk >= a.cpre[a.n]) return;   // a launch sized by an upper bound (pipelined level loop)
-    int lo = 0, hi = a.n;
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (a.cpre[mid] <= chunk) lo = mid; else hi = mid;
-    }
+    int lo = chunk_node(a.cpre, a.n, chunk);
     const int bi = lo >> 6;
     const int bj = bi + (int)(chunk - a.cpre[lo]);
     const int x0 = bi * 64, y0 = bj * 64;
@@ -811,11 +849,7 @@ __global__ __launch_bounds__(256) void k_level(LevelArgs a) {
     if (chunk >= a.cpre[a.n]) return;   // a launch sized by an upper bound (pipelined level loop)
 
     // node owning this chunk
-    int lo = 0, hi = a.n;
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (a.cpre[mid] <= chunk) lo = mid; else hi = mid;
-    }
+    int lo = chunk_node(a.cpre, a.n, chunk);
     const int x = lo;
     const int D = a.deg[x];
     const int d = DM <= 4 ? DM : a.d;
@@ -1047,11 +1081,7 @@ __global__ __launch_bounds__(256) void k_level1_pairs(LevelArgs a) {
     const int tid = threadIdx.x;
     const int64_t chunk = a.chunk_lo + blockIdx.x;
     if (chunk >= a.cpre[a.n]) return;   // a launch sized by an upper bound (pipelined level loop)
-    int lo = 0, hi = a.n;
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (a.cpre[mid] <= chunk) lo = mid; else hi = mid;
-    }
+    int lo = chunk_node(a.cpre, a.n, chunk);
     const int x = lo;
     const int D = a.deg[x];
     const int W = a.W;
@@ -1172,11 +1202,7 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
     const int bs = blockDim.x;
     const int64_t chunk = a.chunk_lo + blockIdx.x;
     if (chunk >= a.cpre[a.n]) return;   // a launch sized by an upper bound (pipelined level loop)
-    int lo = 0, hi = a.n;
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (a.cpre[mid] <= chunk) lo = mid; else hi = mid;
-    }
+    int lo = chunk_node(a.cpre, a.n, chunk);
     const int x = lo;
     const int D = a.deg[x];
     const int d = DM <= 4 ? DM : a.d;
@@ -1212,10 +1238,9 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
         uself[t] = 0;
         uprop[t] = 0;
     }
-    if (tid == 0) {
-        int c = 0;
-        while (c < D && nxs[c] < x) ++c;
-        *s_tx = c;
+    if (tid < 64) {                   // #neighbours below x (nxs ascends; D <= 64 here)
+        const int c = __popcll(__ballot(tid < D && nxs[tid] < x));
+        if (tid == 0) *s_tx = c;
     }
     __syncthreads();
     const int tx = *s_tx;
@@ -1519,6 +1544,51 @@ __device__ __forceinline__ void lmask_atomic_or(LMask<WIDE> *p, LMask<WIDE> v) {
     }
 }
 
+// The T-group lane tasks' (g, t0) pair table of a node of degree D, built by the whole block:
+// pairs g-major, t0 = g TG + 1 .. D - DT ascending; a pair holds C(D - 1 - t0, DT - 1) tasks, so
+// (hockey stick) a group's tasks from t0 on number C(D - t0, DT) and
+//   ppre(g, t0) = sum_{g' < g} C(D - g' TG - 1, DT) + C(D - g TG - 1, DT) - C(D - t0, DT).
+// Every entry is independent (the serial thread-0 loop it replaces took ~D^2 / TG dependent LDS
+// round trips, 9-12 us per block at depths 3-4). s_tx = #neighbours below x (ballots).
+template <int DM, int TG>
+__device__ __forceinline__ void tgroup_pairs(int D, int x, const int32_t *nxs, const unsigned *btab, unsigned *ppre,
+                                             unsigned short *pinfo, int *s_tx, int *s_np) {
+    constexpr int DT = DM - 1;
+    const int tid = threadIdx.x, bs = blockDim.x;
+    const int ng = (D - DM) / TG + 1;
+    int np = 0;
+    for (int g = 0; g < ng; ++g) np += D - DT - g * TG;
+    for (int q = tid; q < np; q += bs) {
+        int g = 0, base = 0;
+        while (base + (D - DT - g * TG) <= q) {
+            base += D - DT - g * TG;
+            ++g;
+        }
+        const int t0 = g * TG + 1 + (q - base);
+        unsigned pre = btab[(D - g * TG - 1) * (DM + 1) + DT] - btab[(D - t0) * (DM + 1) + DT];
+        for (int h = 0; h < g; ++h) pre += btab[(D - h * TG - 1) * (DM + 1) + DT];
+        ppre[q] = pre;
+        pinfo[q] = (unsigned short)((g << 8) | t0);
+    }
+    if (tid < 64) {
+        int c = 0;
+        for (int k0 = 0; k0 < D; k0 += 64) {
+            const int k = k0 + tid;
+            c += __popcll(__ballot(k < D && nxs[k] < x));
+        }
+        if (tid == 0) {
+            unsigned tot = 0;
+            for (int g = 0; g < ng; ++g) tot += btab[(D - g * TG - 1) * (DM + 1) + DT];
+            ppre[np] = tot;
+            *s_np = np;
+            *s_tx = c;
+        }
+    }
+}
+
+#ifndef PCG_TGT_BATCH
+#define PCG_TGT_BATCH 1   // k_level_lds_t stages M and the local masks row-batched (0: per element, A/B)
+#endif
 template <int DM, bool WIDE>
 __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_t(LevelArgs a) {
     using Mask = LMask<WIDE>;
@@ -1529,11 +1599,7 @@ __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_
     const int bs = blockDim.x;
     const int64_t chunk = a.chunk_lo + blockIdx.x;
     if (chunk >= a.cpre[a.n]) return;   // a launch sized by an upper bound (pipelined level loop)
-    int lo = 0, hi = a.n;
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (a.cpre[mid] <= chunk) lo = mid; else hi = mid;
-    }
+    int lo = chunk_node(a.cpre, a.n, chunk);
     const int x = lo;
     const int D = a.deg[x];
     const int32_t *nxg = a.nbr + a.off[x];
@@ -1558,21 +1624,61 @@ __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_
         btab[e] = (unsigned)pcg_binom(a.binom, c, i);             // <= C(64, 4): fits 32 bits
     }
     __syncthreads();
-    for (int e = tid; e < D * DS; e += bs) {
-        const int t = e / DS, k = e - t * DS;
-        M[e] = k < D ? a.C[(int64_t)nxs[t] * a.ldc + nxs[k]] : 0.0;
-    }
-    // local adjacency masks: one wave per row t, lane k reads the bit adj(nxs[t], nxs[k]) and the
-    // wave's ballot is the row's 64-bit word (64 independent loads in flight per row)
-    for (int t = tid >> 6; t < D; t += bs >> 6) {
-        const uint64_t *ar = a.adj + (int64_t)nxs[t] * a.W;
-        Mask m = 0;
-        for (int k0 = 0; k0 < D; k0 += 64) {
-            const int k = k0 + (tid & 63);
-            const bool bit = k < D && ((ar[nxs[k] >> 6] >> (nxs[k] & 63)) & 1ull);
-            m |= (Mask)__ballot(bit) << k0;
+    if (PCG_TGT_BATCH) {
+        // rows of M and of the local adjacency masks: a wave takes SR rows at a time, lane k column
+        // k (+ 64: WIDE), so SR x H x (C entry, adjacency word) loads are in flight per lane before
+        // the first is used (the per-element loop below waits out one gather round trip per ~8
+        // entries of a thread: ~20 dependent round trips per block at D = 45, ~64 at D = 128)
+        constexpr int H = WIDE ? 2 : 1, SR = WIDE ? 2 : 4;
+        const int lane = tid & 63, wv = tid >> 6, nwv = bs >> 6;
+        int kg[H];
+#pragma unroll
+        for (int hh = 0; hh < H; ++hh) kg[hh] = lane + 64 * hh < D ? nxs[lane + 64 * hh] : -1;
+        for (int t0 = wv * SR; t0 < D; t0 += nwv * SR) {
+            double v[SR][H];
+            uint64_t w[SR][H];
+#pragma unroll
+            for (int r = 0; r < SR; ++r) {
+                const int rg = nxs[min(t0 + r, D - 1)];
+#pragma unroll
+                for (int hh = 0; hh < H; ++hh) {
+                    const int k = kg[hh] < 0 ? 0 : kg[hh];
+                    v[r][hh] = a.C[(int64_t)rg * a.ldc + k];
+                    w[r][hh] = a.adj[(int64_t)rg * a.W + (k >> 6)];
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < SR; ++r) {
+                const int t = t0 + r;
+                if (t >= D) break;                   // wave-uniform
+                Mask m = 0;
+#pragma unroll
+                for (int hh = 0; hh < H; ++hh) {
+                    const int k = lane + 64 * hh;
+                    if (k < DS) M[t * DS + k] = kg[hh] >= 0 ? v[r][hh] : 0.0;
+                    const bool bit = kg[hh] >= 0 && ((w[r][hh] >> (kg[hh] & 63)) & 1ull);
+                    m |= (Mask)__ballot(bit) << (64 * hh);
+                }
+                if (lane == 0) lmask[t] = m;
+            }
         }
-        if ((tid & 63) == 0) lmask[t] = m;
+    } else {
+        for (int e = tid; e < D * DS; e += bs) {
+            const int t = e / DS, k = e - t * DS;
+            M[e] = k < D ? a.C[(int64_t)nxs[t] * a.ldc + nxs[k]] : 0.0;
+        }
+        // local adjacency masks: one wave per row t, lane k reads the bit adj(nxs[t], nxs[k]) and the
+        // wave's ballot is the row's 64-bit word (64 independent loads in flight per row)
+        for (int t = tid >> 6; t < D; t += bs >> 6) {
+            const uint64_t *ar = a.adj + (int64_t)nxs[t] * a.W;
+            Mask m = 0;
+            for (int k0 = 0; k0 < D; k0 += 64) {
+                const int k = k0 + (tid & 63);
+                const bool bit = k < D && ((ar[nxs[k] >> 6] >> (nxs[k] & 63)) & 1ull);
+                m |= (Mask)__ballot(bit) << k0;
+            }
+            if ((tid & 63) == 0) lmask[t] = m;
+        }
     }
     for (int t = tid; t < D; t += bs) {
         const int yg = nxs[t];
@@ -1582,23 +1688,7 @@ __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_
         uprop[t] = 0;
     }
     const int ng = (D - DM) / TG + 1;     // groups with g*TG <= D - d
-    if (tid == 0) {
-        int c = 0;
-        while (c < D && nxs[c] < x) ++c;
-        *s_tx = c;
-        // tasks: group g, then t0 = min(T) ascending, then colex rank of T \ {t0} over (t0, D)
-        unsigned acc = 0;
-        int q = 0;
-        for (int g = 0; g < ng; ++g)
-            for (int t0 = g * TG + 1; t0 <= D - DT; ++t0) {
-                ppre[q] = acc;
-                pinfo[q] = (unsigned short)((g << 8) | t0);
-                acc += btab[(D - 1 - t0) * (DM + 1) + DT - 1];
-                ++q;
-            }
-        ppre[q] = acc;
-        *s_np = q;
-    }
+    tgroup_pairs<DM, TG>(D, x, nxs, btab, ppre, pinfo, s_tx, s_np);
     __syncthreads();
     const int tx = *s_tx;
     const int np = *s_np;
@@ -2172,11 +2262,7 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
     const int bs = blockDim.x;
     const int64_t chunk = a.chunk_lo + blockIdx.x;
     if (chunk >= a.cpre[a.n]) return;   // a launch sized by an upper bound (pipelined level loop)
-    int lo = 0, hi = a.n;
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (a.cpre[mid] <= chunk) lo = mid; else hi = mid;
-    }
+    int lo = chunk_node(a.cpre, a.n, chunk);
     const int x = lo;
     const int D = a.deg[x];
     const int32_t *nxg = a.nbr + a.off[x];
@@ -2269,22 +2355,7 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
         uprop[t] = 0;
     }
     const int ng = (D - DM) / TG + 1;
-    if (tid == 0) {
-        int c = 0;
-        while (c < D && nxs[c] < x) ++c;
-        *s_tx = c;
-        unsigned acc = 0;
-        int q = 0;
-        for (int g = 0; g < ng; ++g)
-            for (int t0 = g * TG + 1; t0 <= D - DT; ++t0) {
-                ppre[q] = acc;
-                pinfo[q] = (unsigned short)((g << 8) | t0);
-                acc += btab[(D - 1 - t0) * (DM + 1) + DT - 1];
-                ++q;
-            }
-        ppre[q] = acc;
-        *s_np = q;
-    }
+    tgroup_pairs<DM, TG>(D, x, nxs, btab, ppre, pinfo, s_tx, s_np);
     __syncthreads();
     const int tx = *s_tx;
     const int np = *s_np;
@@ -2943,11 +3014,7 @@ __global__ __launch_bounds__(256, PCG_SP_MB) void k_level_sp(LevelArgs a) {
     }
     const int64_t chunk = a.chunk_lo + bid;
     if (chunk >= a.cpre[a.n]) return;   // a launch sized by an upper bound (pipelined level loop)
-    int lo = 0, hi = a.n;
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (a.cpre[mid] <= chunk) lo = mid; else hi = mid;
-    }
+    int lo = chunk_node(a.cpre, a.n, chunk);
     const int x = lo;
     const int D = a.deg[x];
     const int L = D + 1;
@@ -3429,11 +3496,7 @@ __global__ __launch_bounds__(64) void k_level_deep(LevelArgs a, double *scratch,
     for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
         const int64_t chunk = a.chunk_lo + c;
         if (chunk >= a.cpre[a.n]) break;    // (a bound-sized chunk range, pipelined level loop)
-        int lo = 0, hi = a.n;
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (a.cpre[mid] <= chunk) lo = mid; else hi = mid;
-        }
+        int lo = chunk_node(a.cpre, a.n, chunk);
         const int x = lo;
         const int D = a.deg[x];
         const int32_t *nx = a.nbr + a.off[x];
@@ -3564,11 +3627,7 @@ __global__ __launch_bounds__(256) void k_level_wave(LevelArgs a) {
     const int lane = tid & 63, wv = tid >> 6;
     const int64_t chunk = a.chunk_lo + blockIdx.x;
     if (chunk >= a.cpre[a.n]) return;   // a launch sized by an upper bound (pipelined level loop)
-    int lo = 0, hi = a.n;
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (a.cpre[mid] <= chunk) lo = mid; else hi = mid;
-    }
+    int lo = chunk_node(a.cpre, a.n, chunk);
     const int x = lo;
     const int D = a.deg[x];
     const int d = a.d;
@@ -3591,11 +3650,7 @@ __global__ __launch_bounds__(256) void k_level_wave(LevelArgs a) {
         const int t = e / D, k = e - t * D;
         M[e] = a.C[(int64_t)nxs[t] * a.ldc + nxs[k]];
     }
-    for (int t = wv; t < D; t += blockDim.x >> 6) {
-        const bool bit = lane < D && ((a.adj[(int64_t)nxs[t] * a.W + (nxs[lane] >> 6)] >> (nxs[lane] & 63)) & 1ull);
-        const unsigned long long m = __ballot(bit);
-        if (lane == 0) lmask[t] = m;
-    }
+    stage_lmask(a, nxs, D, lmask);
     for (int t = tid; t < D; t += blockDim.x) {
         const int yg = nxs[t];
         Mx[t] = a.C[(int64_t)x * a.ldc + yg];
@@ -3603,10 +3658,9 @@ __global__ __launch_bounds__(256) void k_level_wave(LevelArgs a) {
         uself[t] = 0;
         uprop[t] = 0;
     }
-    if (tid == 0) {
-        int c = 0;
-        while (c < D && nxs[c] < x) ++c;
-        *s_tx = c;
+    if (tid < 64) {                   // #neighbours below x (nxs ascends; D <= 64 here)
+        const int c = __popcll(__ballot(tid < D && nxs[tid] < x));
+        if (tid == 0) *s_tx = c;
     }
     __syncthreads();
     const int tx = *s_tx;
@@ -3781,11 +3835,7 @@ __global__ __launch_bounds__(256) void k_level_wave_pr(LevelArgs a) {
     const int lane = tid & 63, wv = tid >> 6;
     const int64_t chunk = a.chunk_lo + blockIdx.x;
     if (chunk >= a.cpre[a.n]) return;
-    int lo = 0, hi = a.n;
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (a.cpre[mid] <= chunk) lo = mid; else hi = mid;
-    }
+    int lo = chunk_node(a.cpre, a.n, chunk);
     const int x = lo;
     const int D = a.deg[x];
     const int d = a.d;
@@ -3809,11 +3859,7 @@ __global__ __launch_bounds__(256) void k_level_wave_pr(LevelArgs a) {
         const int t = e / D, k = e - t * D;
         M[e] = a.C[(int64_t)nxs[t] * a.ldc + nxs[k]];
     }
-    for (int t = wv; t < D; t += blockDim.x >> 6) {
-        const bool bit = lane < D && ((a.adj[(int64_t)nxs[t] * a.W + (nxs[lane] >> 6)] >> (nxs[lane] & 63)) & 1ull);
-        const unsigned long long m = __ballot(bit);
-        if (lane == 0) lmask[t] = m;
-    }
+    stage_lmask(a, nxs, D, lmask);
     for (int t = tid; t < D; t += blockDim.x) {
         const int yg = nxs[t];
         Mx[t] = a.C[(int64_t)x * a.ldc + yg];
@@ -3821,10 +3867,9 @@ __global__ __launch_bounds__(256) void k_level_wave_pr(LevelArgs a) {
         uself[t] = 0;
         uprop[t] = 0;
     }
-    if (tid == 0) {
-        int c = 0;
-        while (c < D && nxs[c] < x) ++c;
-        *s_tx = c;
+    if (tid < 64) {                   // #neighbours below x (nxs ascends; D <= 64 here)
+        const int c = __popcll(__ballot(tid < D && nxs[tid] < x));
+        if (tid == 0) *s_tx = c;
     }
     __syncthreads();
     const int tx = *s_tx;

@@ -6,6 +6,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/r4/n
 mkdir -p $O
+timeout -k 10 700 python -u -m pytest tests/test_gpu_skeleton.py -q -x -k "skeleton_matches_oracle or wide_and_large or screen_precision or depth2 or n500 or schur or pipelined or fused or wave_kernel or config5" --timeout 150 --timeout-method thread > $O/tests.log 2>&1
+rc=$?; tail -3 $O/tests.log; [ $rc -eq 0 ] || exit $rc
 cp rcaeval_amd/libpcgpu.so /tmp/libpcgpu_base.so
 for v in /tmp/libpcgpu_base.so tools/variants_r4/libpcgpu_*.so; do
   name=$(basename "$v" .so)
