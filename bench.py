@@ -492,18 +492,25 @@ def main():
         corr_med = float(np.median([1000 * t for n_, t in phases if n_ == "corr"][args.warmup:] or [0.0]))
     roof["k1"] = k1_roofline(args.n, args.samples, corr_med) if corr_med > 0 else None
 
-    # the same skeleton with every p-value computed (PCG_FLAG_FULL_P), once, after the timed
-    # steps: the reference-arithmetic mode beside the threshold headline
+    # the full-p mode (PCG_FLAG_FULL_P | PCG_FLAG_RECORD) after the timed steps: the same skeleton
+    # with the reference-arithmetic p of every test of a 1-in-4099 pair sample recorded (the
+    # parity test's sample; the exact path computes those p with numpy.linalg.inv's LU), the
+    # threshold decisions elsewhere. Twice: the first call sizes the exact-path list
     full_p = None
     if not args.full_p and not args.no_full_p and world == 1:
         progress("full-p comparison run")
         C = eng.corr(Xd)
-        o = eng.skeleton(C, args.samples, alpha=args.alpha, max_depth=args.max_depth, flags=_lib.PCG_FLAG_FULL_P)
+        fl = _lib.PCG_FLAG_FULL_P | _lib.PCG_FLAG_RECORD
+        for _ in range(2):
+            o = eng.skeleton(C, args.samples, alpha=args.alpha, max_depth=args.max_depth, flags=fl,
+                             record_capacity=4_000_000, record_sample=(4099, 17))
         fp_ms = float(sum(o.stats["level_ms"]))
         same = bool(np.array_equal(o.removed_level, out.removed_level)) and o.stats["tests"] == st["tests"]
         full_p = {"skeleton_device_ms": fp_ms, "tests_per_s": sum(o.stats["tests"]) / (fp_ms / 1e3),
+                  "flags": "FULL_P|RECORD, record_sample=(4099, 17)", "records": int(len(o.records)),
                   "kernel_ms_per_level": [round(v, 3) for v in o.stats["kernel_ms"]],
-                  "same_skeleton_as_threshold": same}
+                  "level_ms": [round(v, 3) for v in o.stats["level_ms"]],
+                  "exact_path": o.stats["exact"], "same_skeleton_as_threshold": same}
 
     if rank == 0:
         line = {

@@ -1689,9 +1689,24 @@ __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_
     }
     const int ng = (D - DM) / TG + 1;     // groups with g*TG <= D - d
     tgroup_pairs<DM, TG>(D, x, nxs, btab, ppre, pinfo, s_tx, s_np);
+    // full-p mode with records (PCG_FLAG_RECORD): the recorded pairs (x, y) of this node, bit t.
+    // Every live test of such a y goes to the exact path, which decides it with the reference's
+    // own arithmetic and records its p (k_exact); the others are decided as in threshold mode
+    __shared__ Mask s_recm;
+    if (tid < 64) {
+        Mask rm_ = 0;
+        if (a.record)
+            for (int k0 = 0; k0 < D; k0 += 64) {
+                const int t = k0 + tid;
+                const int yg = t < D ? nxs[t] : 0;
+                rm_ |= (Mask)__ballot(t < D && rec_on(a, min(x, yg), max(x, yg))) << k0;
+            }
+        if (tid == 0) s_recm = rm_;
+    }
     __syncthreads();
     const int tx = *s_tx;
     const int np = *s_np;
+    const Mask recm = s_recm;
     const double Cxx = a.diag[x];
     const uint64_t ntask = ppre[np];
     const uint64_t spl = a.spl_dev ? (uint64_t)*a.spl_dev : (uint64_t)a.spl;
@@ -1916,9 +1931,11 @@ __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_
                                     __builtin_amdgcn_ballot_w64(fma(th, inv_hi2, -kg) > num));
                 }
                 const unsigned long long inT = __builtin_amdgcn_ballot_w64((bool)((Tmask >> t) & 1u));
+                const bool recy = (bool)((recm >> t) & 1u);     // wave-uniform
                 unsigned long long rarel = (bad | notok) & ~inT;
                 if (YM == 2) rarel |= __builtin_amdgcn_ballot_w64((unsigned)(t - cbase) < (unsigned)nval);
                 if (t < tx) rarel |= __builtin_amdgcn_ballot_w64((lm & Tmask) == Tmask) & ~inT;
+                if (recy) rarel = __builtin_amdgcn_read_exec() & ~inT;
                 if (!rarel) return;
                 if (!(rarel & lanebit)) return;
                 // rare path (this lane): the exact live set, the dedup skips, then the per-lane
@@ -1929,6 +1946,18 @@ __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_
                 if ((Tmask >> t) & 1u) return;
                 const unsigned live = vmask & ~tb & ~skip;
                 tcount -= __popc(vmask & ~tb & skip);
+                if (recy) {                                   // recorded pair: every live test to the exact path
+#pragma unroll
+                    for (int jj = 0; jj < TG; ++jj) {
+                        if (!((live >> jj) & 1u)) continue;
+                        int sg[DM];
+                        sg[0] = nxs[cbase + jj];
+#pragma unroll
+                        for (int i = 0; i < DT; ++i) sg[i + 1] = nxs[T[i]];
+                        push_deferred(a, x, nxs[t], sg, DM);
+                    }
+                    return;
+                }
 #pragma unroll
                 for (int jj = 0; jj < TG; ++jj) {
                     if (!((live >> jj) & 1u)) continue;
@@ -2046,7 +2075,8 @@ __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_
                 for (int k = 0; k < YU; ++k) {
                     const int t = tt[k];
                     tcount += __popc(live[k]);
-                    const unsigned rare = live[k] & ~(dep[k] & okm);
+                    const bool recy = (bool)((recm >> t) & 1u);   // recorded pair: every live test to the exact path
+                    const unsigned rare = recy ? live[k] : (live[k] & ~(dep[k] & okm));
                     if (__ballot(rare != 0u)) {
                         if (rare) {
                             const double *Mt = M + t * DS;
@@ -2055,6 +2085,14 @@ __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_
                             for (int jj = 0; jj < TG; ++jj) {
                                 if (!((rare >> jj) & 1u)) continue;
                                 const int c = cbase + jj;
+                                if (recy) {
+                                    int sg[DM];
+                                    sg[0] = nxs[c];
+#pragma unroll
+                                    for (int i = 0; i < DT; ++i) sg[i + 1] = nxs[T[i]];
+                                    push_deferred(a, x, nxs[t], sg, DM);
+                                    continue;
+                                }
                                 // recompute the decision pieces for this c (rare path)
                                 double s = Mt[c];
 #pragma unroll
@@ -2172,6 +2210,9 @@ constexpr double F32_U = 5.9604644775390625e-08;   // 2^-24
 #endif
 #ifndef PCG_TGF_ABL_D
 #define PCG_TGF_ABL_D 4   // the depth the ablation applies to (the narrow class only)
+#endif
+#ifndef PCG_TGF_PKV
+#define PCG_TGF_PKV 1     // k_level_lds_f: v_T = L_T^-1 m_T with two of its rows as one packed chain (A/B: 0)
 #endif
 #ifndef PCG_TGF_SPLIT
 #define PCG_TGF_SPLIT 1   // k_level_lds_f, one candidate window per wave: y outside the window without the
@@ -2665,13 +2706,32 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
                 for (int j = 0; j < DT; ++j) mT[j] = pre.mT[j];
                 // (|v_T|^2, u_T.v_T) accumulated as one packed pair: vu[i] = {v_i, u_i}
                 f2v acc = {0.0f, 0.0f};
+                if constexpr (PCG_TGF_PKV && DT == 3) {
+                    // v_1 and v_2 as one packed chain (the same roundings in the same order as the
+                    // scalar chains: L_i0 m_0, + L_i1 m_1, + L_i2 m_2)
+                    const f2v l0 = {Lif[1][0], Lif[2][0]}, l1 = {Lif[1][1], Lif[2][1]};
+                    const f2v m0 = {mT[0], mT[0]}, m1 = {mT[1], mT[1]};
+                    const f2v p = __builtin_elementwise_fma(l1, m1, l0 * m0);
+                    vT[0] = Lif[0][0] * mT[0];
+                    vT[1] = p[0];
+                    vT[2] = fmaf(Lif[2][2], mT[2], p[1]);
+                } else if constexpr (PCG_TGF_PKV && DT == 2) {
+                    const f2v l0 = {Lif[0][0], Lif[1][0]}, m0 = {mT[0], mT[0]};
+                    const f2v p = l0 * m0;
+                    vT[0] = p[0];
+                    vT[1] = fmaf(Lif[1][1], mT[1], p[1]);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < DT; ++i) {
+                        float v = 0.0f;
+#pragma unroll
+                        for (int j = 0; j <= i; ++j) v = fmaf(Lif[i][j], mT[j], v);
+                        vT[i] = v;
+                    }
+                }
 #pragma unroll
                 for (int i = 0; i < DT; ++i) {
-                    float v = 0.0f;
-#pragma unroll
-                    for (int j = 0; j <= i; ++j) v = fmaf(Lif[i][j], mT[j], v);
-                    vT[i] = v;
-                    const f2v vu = {v, uTf[i]}, vb = {v, v};
+                    const f2v vu = {vT[i], uTf[i]}, vb = {vT[i], vT[i]};
                     acc = __builtin_elementwise_fma(vu, vb, acc);
                 }
                 const f2v b2 = pre.md - acc;   // {byy, bxy}
@@ -5007,7 +5067,9 @@ uint64_t tgroup_tasks(const pcg_handle *h, int D, int d) {
     return acc;
 }
 
-bool use_tgroup(int mode, int d) { return mode == MODE_DECIDE && d >= 2 && d <= 4; }
+// (full-p mode too: threshold decisions with the exact band, records by the exact path — the
+// p-values the caller can observe; k_level_lds_t routes recorded pairs there)
+bool use_tgroup(int mode, int d) { return (mode == MODE_DECIDE || mode == MODE_FULLP) && d >= 2 && d <= 4; }
 // depths whose narrow class runs k_level_wave (one wave per conditioning set); PCG_WAVE_LO
 // overrides the first such depth (A/B knob)
 // k_level_wave_pr (the factorisation shared between consecutive sets) instead of k_level_wave;
@@ -5419,6 +5481,7 @@ int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks, bool bound
         const char *sm = getenv("PCG_SCREEN_MASK");
         h->screen_eff = sm ? (int)strtol(sm, nullptr, 0) : (h->screen_mask < 0 ? PCG_TG_F32 : h->screen_mask);
         h->screen_eff &= 0x1c;   // the error bound (KE = 64) is derived for d = 2..4 only
+        if (h->flags & PCG_FLAG_RECORD) h->screen_eff = 0;   // records: the fp64 T-group kernels route them
         {   // Schur-prefix sweep for the narrow class (PCG_SP A/B knob, read per depth)
             const char *spe = getenv("PCG_SP");
             const int spm = spe ? (int)strtol(spe, nullptr, 0) : PCG_SP;
@@ -5955,7 +6018,10 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
         }
         const int m = d + 2;
         const int per = (m * m + 2 * m) * 8;      // one LDS slot per wave
-        hipLaunchKernelGGL(k_exact, dim3(256), dim3(256), (size_t)per * 4, h->stream, a);
+        // (records: every test of a recorded pair comes here — up to ~1e6 at config 5 depth 4 with
+        // a 1-in-4099 pair sample — so more waves than the threshold mode's few band tests need)
+        const unsigned xg = (h->flags & PCG_FLAG_RECORD) ? 2048u : 256u;
+        hipLaunchKernelGGL(k_exact, dim3(xg), dim3(256), (size_t)per * 4, h->stream, a);
         PCG_HIP(h, hipGetLastError());
         return PCG_OK;
     }
