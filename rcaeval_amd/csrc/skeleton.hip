@@ -2292,7 +2292,7 @@ __device__ int eval_test_global(const LevelArgs &a, int x, int y, const int *Sg)
     return decide<MODE_DECIDE>(a, cxy0 - uv, dx - uu, dy - vv, a.tau / gmin, nullptr);
 }
 
-template <int DM, bool WIDE>
+template <int DM, bool WIDE, bool REC = false>
 __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds_f(LevelArgs a) {
     using Mask = LMask<WIDE>;
     constexpr int DT = DM - 1;
@@ -2397,9 +2397,23 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
     }
     const int ng = (D - DM) / TG + 1;
     tgroup_pairs<DM, TG>(D, x, nxs, btab, ppre, pinfo, s_tx, s_np);
+    // records (PCG_FLAG_RECORD): the recorded pairs (x, y) of this node, bit t; every live test of
+    // such a y goes to the exact path (decided and recorded there, as in k_level_lds_t)
+    __shared__ Mask s_recm;
+    if (tid < 64) {
+        Mask rm_ = 0;
+        if (REC && a.record)
+            for (int k0 = 0; k0 < D; k0 += 64) {
+                const int t = k0 + tid;
+                const int yg = t < D ? nxs[t] : 0;
+                rm_ |= (Mask)__ballot(t < D && rec_on(a, min(x, yg), max(x, yg))) << k0;
+            }
+        if (tid == 0) s_recm = rm_;
+    }
     __syncthreads();
     const int tx = *s_tx;
     const int np = *s_np;
+    const Mask recm = REC ? s_recm : (Mask)0;   // (threshold-mode builds: no record code in the sweep)
     const double Cxx = (double)(float)a.diag[x];                  // A~_xx
     const uint64_t ntask = ppre[np];
     const uint64_t spl = a.spl_dev ? (uint64_t)*a.spl_dev : (uint64_t)a.spl;
@@ -2668,6 +2682,14 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
             for (int i = 0; i < DT; ++i) sg[i + 1] = nxs[T[i]];
             push_screen(a, x, nxs[t], sg, DM);
         };
+        // a recorded pair's live test: to the exact path
+        auto push_rec = [&](int jj, int t) {
+            int sg[DM];
+            sg[0] = nxs[cbase + jj];
+#pragma unroll
+            for (int i = 0; i < DT; ++i) sg[i + 1] = nxs[T[i]];
+            push_deferred(a, x, nxs[t], sg, DM);
+        };
         auto sweep = [&](auto nc_tag) {
             constexpr int NC = decltype(nc_tag)::value;
             constexpr int NQ = NC / 2;
@@ -2764,12 +2786,16 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
                     const unsigned skip = own ? (unsigned)(lm >> cbase) : 0u;
                     const unsigned live = inTset ? 0u : (vmask & ~tb & ~skip);
                     tcount += __popc(live);
-                    const unsigned rare = live & ~(dp & okm);
+                    const bool recy = REC && (bool)((recm >> t) & 1u);     // wave-uniform
+                    const unsigned rare = recy ? live : (live & ~(dp & okm));
                     if (__builtin_amdgcn_ballot_w64(rare != 0u)) {
                         if (rare) {
 #pragma unroll
                             for (int jj = 0; jj < TG; ++jj)
-                                if ((rare >> jj) & 1u) rare_cand(jj, t, Mt, vT, byy, bxy, lm);
+                                if ((rare >> jj) & 1u) {
+                                    if (recy) push_rec(jj, t);
+                                    else rare_cand(jj, t, Mt, vT, byy, bxy, lm);
+                                }
                         }
                     }
                     return;
@@ -2796,9 +2822,11 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
                     }
                 }
                 const unsigned long long inT = __builtin_amdgcn_ballot_w64((bool)((Tmask >> t) & 1u));
+                const bool recy = REC && (bool)((recm >> t) & 1u);     // wave-uniform
                 unsigned long long rarel = ((~dall & __builtin_amdgcn_read_exec()) | notok) & ~inT;
                 if (YM == 2) rarel |= __builtin_amdgcn_ballot_w64((unsigned)(t - cbase) < (unsigned)nval);
                 if (t < tx) rarel |= __builtin_amdgcn_ballot_w64((lm & Tmask) == Tmask) & ~inT;
+                if (recy) rarel = __builtin_amdgcn_read_exec() & ~inT;
                 if (!rarel) return;
                 if (!(rarel & lanebit)) return;
                 // rare path (this lane): live set and dedup skips as in k_level_lds_t
@@ -2810,7 +2838,10 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
                 tcount -= __popc(vmask & ~tb & skip);
 #pragma unroll
                 for (int jj = 0; jj < TG; ++jj)
-                    if ((live >> jj) & 1u) rare_cand(jj, t, Mt, vT, byy, bxy, lm);
+                    if ((live >> jj) & 1u) {
+                        if (recy) push_rec(jj, t);
+                        else rare_cand(jj, t, Mt, vT, byy, bxy, lm);
+                    }
                 }
             };
             using Y0 = std::integral_constant<int, 0>;
@@ -4112,6 +4143,97 @@ __device__ __forceinline__ int lu_from_lds(const double *A, double *i00, double 
 // One wave per deferred test: the lanes gather the (d+2)^2 correlation entries in parallel
 // into the wave's LDS slot (a single lane's rolled gather would wait out one HBM latency per
 // entry), then lane 0 factors and decides.
+// the exact path's verdict for one deferred test, after its factorisation (sing, i00, i01, i11 =
+// the inverse's top-left 2 x 2 entries): numpy's errors, the reference p expression, records,
+// near-alpha entries, and an independence's removal flags and per-side unions
+__device__ __forceinline__ void exact_finish(const LevelArgs &a, const DeferredEntry &e, int sing, double i00, double i01,
+                                             double i11, unsigned long long &nexact, unsigned long long &nindep) {
+    const int d = a.d;
+    const int x = e.x, y = e.y;
+    const int lo_ = x < y ? x : y, hi_ = x < y ? y : x;
+    double p = __builtin_nan("");
+    int err = 0;
+    if (sing) {
+        err = 1;
+    } else {
+        const double prod = i00 * i11;
+        if (prod < 0.0) err = 2;
+        else if (a.dof_negative) err = 2;
+        else {
+            const double r = -i01 / sqrt(prod);
+            p = pcg_pvalue_from_r(r, a.sqrt_dof, &err);
+        }
+    }
+    ++nexact;
+    if (err) { flag_error(a, err); return; }
+    if (rec_on(a, lo_, hi_)) push_record(a.records, a.rec_cap, &a.ctr->records, lo_, hi_, d, e.s, p);
+    if (fabs(p - a.alpha) < 1e-9) push_record(a.nearl, a.near_cap, &a.ctr->near_alpha, lo_, hi_, d, e.s, p);
+    if (p > a.alpha) {
+        ++nindep;
+        a.rm[(int64_t)x * a.n + y] = 1;
+        a.rm[(int64_t)y * a.n + x] = 1;
+        if (d > 0) {
+            bool in_y = true;
+            for (int q = 0; q < d; ++q)
+                in_y = in_y && ((a.adj[(int64_t)y * a.W + (e.s[q] >> 6)] >> (e.s[q] & 63)) & 1ull);
+            const int sx = a.off[x] + find_in_sorted(a.nbr + a.off[x], a.deg[x], y);
+            for (int q = 0; q < d; ++q)
+                atomicOr(reinterpret_cast<unsigned long long *>(&a.ug[(int64_t)sx * a.W + (e.s[q] >> 6)]),
+                         1ull << (e.s[q] & 63));
+            if (in_y && y > x) {
+                const int sy = a.off[y] + find_in_sorted(a.nbr + a.off[y], a.deg[y], x);
+                for (int q = 0; q < d; ++q)
+                    atomicOr(reinterpret_cast<unsigned long long *>(&a.ug[(int64_t)sy * a.W + (e.s[q] >> 6)]),
+                             1ull << (e.s[q] & 63));
+            }
+        }
+    }
+}
+
+// lane-per-test form for d <= 4 (m = d + 2 <= 6): each lane gathers its test's m^2 entries into
+// registers (all loads issued before the first use) and factors them (numpy.linalg.inv's order,
+// the same register routine the wave form's lane 0 runs: identical results). Used when the list
+// is long — the full-p mode's recorded pairs put ~1e6 tests here at config 5 depth 4, where one
+// wave per test left 63 of its 64 lanes idle through every factorisation
+template <int M>
+__device__ __forceinline__ void exact_lanes(const LevelArgs &a, int64_t count, int blk, int nblk,
+                                            unsigned long long &nexact, unsigned long long &nindep) {
+    constexpr int D = M - 2;
+    const int64_t lanes = (int64_t)nblk * blockDim.x;
+    for (int64_t i = (int64_t)blk * blockDim.x + threadIdx.x; i < count; i += lanes) {
+        const DeferredEntry e = a.deferred[i];
+        int var[M];
+        var[0] = e.x < e.y ? e.x : e.y;
+        var[1] = e.x < e.y ? e.y : e.x;
+#pragma unroll
+        for (int q = 0; q < D; ++q) var[2 + q] = e.s[q];
+        double R[M][M];
+#pragma unroll
+        for (int r = 0; r < M; ++r)
+#pragma unroll
+            for (int c = 0; c < M; ++c) R[r][c] = a.C[(int64_t)var[r] * a.ldc + var[c]];
+        double i00, i01, i11;
+        const int sing = pcg_lu_inv01_reg<M>(R, &i00, &i01, &i11);
+        exact_finish(a, e, sing, i00, i01, i11, nexact, nindep);
+    }
+}
+// the exact path with a lane per test (d <= 4; launched with records, whose recorded pairs put
+// every test of those pairs on the list): the overflow check of k_exact, wave-summed counters
+template <int M>
+__global__ __launch_bounds__(256) void k_exact_lanes(LevelArgs a) {
+    const unsigned long long pushed = *(volatile const unsigned long long *)&a.ctr->deferred;
+    const int64_t count = (int64_t)min((unsigned long long)a.def_cap, pushed);
+    if (blockIdx.x == 0 && threadIdx.x == 0 &&
+        ((int64_t)pushed > a.def_cap || (a.record && (int64_t)a.ctr->records > a.rec_cap)))
+        a.rm[(int64_t)a.n * a.n] = 1;      // overflow: every rank reruns (status byte 0)
+    unsigned long long nexact = 0, nindep = 0;
+    exact_lanes<M>(a, count, blockIdx.x, gridDim.x, nexact, nindep);
+    nexact = wave_sum(nexact);
+    nindep = wave_sum(nindep);
+    if ((threadIdx.x & 63) == 0 && nexact) atomicAdd(&a.ctr->exact, nexact);
+    if ((threadIdx.x & 63) == 0 && nindep) atomicAdd(&a.ctr->indep, nindep);
+}
+
 __device__ __forceinline__ void exact_waves(const LevelArgs &a, unsigned char *smem, int blk, int nblk) {
     const int d = a.d;
     const int m = d + 2;
@@ -4149,8 +4271,7 @@ __device__ __forceinline__ void exact_waves(const LevelArgs &a, unsigned char *s
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (lane != 0) continue;
-        double i00, i01, i11, p = __builtin_nan("");
-        int err = 0;
+        double i00, i01, i11;
         int sing;
         switch (m) {     // depths 0..4: the factorisation in registers; deeper: in the LDS slot
         case 2: sing = lu_from_lds<2>(A, &i00, &i01, &i11); break;
@@ -4160,41 +4281,7 @@ __device__ __forceinline__ void exact_waves(const LevelArgs &a, unsigned char *s
         case 6: sing = lu_from_lds<6>(A, &i00, &i01, &i11); break;
         default: sing = pcg_lu_inv01(A, m, piv, B0, B1, &i00, &i01, &i11);
         }
-        if (sing) {
-            err = 1;
-        } else {
-            const double prod = i00 * i11;
-            if (prod < 0.0) err = 2;
-            else if (a.dof_negative) err = 2;
-            else {
-                const double r = -i01 / sqrt(prod);
-                p = pcg_pvalue_from_r(r, a.sqrt_dof, &err);
-            }
-        }
-        ++nexact;
-        if (err) { flag_error(a, err); continue; }
-        if (rec_on(a, lo_, hi_)) push_record(a.records, a.rec_cap, &a.ctr->records, lo_, hi_, d, e.s, p);
-        if (fabs(p - a.alpha) < 1e-9) push_record(a.nearl, a.near_cap, &a.ctr->near_alpha, lo_, hi_, d, e.s, p);
-        if (p > a.alpha) {
-            ++nindep;
-            a.rm[(int64_t)x * a.n + y] = 1;
-            a.rm[(int64_t)y * a.n + x] = 1;
-            if (d > 0) {
-                bool in_y = true;
-                for (int q = 0; q < d; ++q)
-                    in_y = in_y && ((a.adj[(int64_t)y * a.W + (e.s[q] >> 6)] >> (e.s[q] & 63)) & 1ull);
-                const int sx = a.off[x] + find_in_sorted(a.nbr + a.off[x], a.deg[x], y);
-                for (int q = 0; q < d; ++q)
-                    atomicOr(reinterpret_cast<unsigned long long *>(&a.ug[(int64_t)sx * a.W + (e.s[q] >> 6)]),
-                             1ull << (e.s[q] & 63));
-                if (in_y && y > x) {
-                    const int sy = a.off[y] + find_in_sorted(a.nbr + a.off[y], a.deg[y], x);
-                    for (int q = 0; q < d; ++q)
-                        atomicOr(reinterpret_cast<unsigned long long *>(&a.ug[(int64_t)sy * a.W + (e.s[q] >> 6)]),
-                                 1ull << (e.s[q] & 63));
-                }
-            }
-        }
+        exact_finish(a, e, sing, i00, i01, i11, nexact, nindep);
     }
     if (nexact) atomicAdd(&a.ctr->exact, nexact);
     if (nindep) atomicAdd(&a.ctr->indep, nindep);
@@ -5481,7 +5568,6 @@ int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks, bool bound
         const char *sm = getenv("PCG_SCREEN_MASK");
         h->screen_eff = sm ? (int)strtol(sm, nullptr, 0) : (h->screen_mask < 0 ? PCG_TG_F32 : h->screen_mask);
         h->screen_eff &= 0x1c;   // the error bound (KE = 64) is derived for d = 2..4 only
-        if (h->flags & PCG_FLAG_RECORD) h->screen_eff = 0;   // records: the fp64 T-group kernels route them
         {   // Schur-prefix sweep for the narrow class (PCG_SP A/B knob, read per depth)
             const char *spe = getenv("PCG_SP");
             const int spm = spe ? (int)strtol(spe, nullptr, 0) : PCG_SP;
@@ -5844,6 +5930,7 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
         return pcg_fail(h, PCG_ERR_INVALID, "pcg_level_run: chunk range");
     const int d = h->depth;
     const int mode = mode_of(h, d);
+    const bool rec = (h->flags & PCG_FLAG_RECORD) != 0;   // T-group sweeps with record routing
     PCG_HT(h, "run:start");
     {
         LevelArgs a = make_args(h, d, mode == MODE_EXACT);
@@ -5924,9 +6011,9 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                         as.lds_btab_off = (int)lds_f32_core(dl, 8);
                         const size_t ldsf = lds_tgroup_f_bytes(dl, d, 8);
                         const dim3 grid((unsigned)(s_hi - s_lo)), block(256);
-                        if (d == 2) hipLaunchKernelGGL((k_level_lds_f<2, false>), grid, block, ldsf, h->stream, as);
-                        else if (d == 3) hipLaunchKernelGGL((k_level_lds_f<3, false>), grid, block, ldsf, h->stream, as);
-                        else hipLaunchKernelGGL((k_level_lds_f<4, false>), grid, block, ldsf, h->stream, as);
+                        if (d == 2) { if (rec) hipLaunchKernelGGL((k_level_lds_f<2, false, true>), grid, block, ldsf, h->stream, as); else hipLaunchKernelGGL((k_level_lds_f<2, false>), grid, block, ldsf, h->stream, as); }
+                        else if (d == 3) { if (rec) hipLaunchKernelGGL((k_level_lds_f<3, false, true>), grid, block, ldsf, h->stream, as); else hipLaunchKernelGGL((k_level_lds_f<3, false>), grid, block, ldsf, h->stream, as); }
+                        else { if (rec) hipLaunchKernelGGL((k_level_lds_f<4, false, true>), grid, block, ldsf, h->stream, as); else hipLaunchKernelGGL((k_level_lds_f<4, false>), grid, block, ldsf, h->stream, as); }
                     } else if (h->tgroup) {
                         const dim3 grid((unsigned)(s_hi - s_lo)), block(256);
                         if (d == 2) hipLaunchKernelGGL((k_level_lds_t<2, false>), grid, block, lds, h->stream, as);
@@ -5956,9 +6043,9 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                     if (use_screen32(h, d)) {
                         aw.lds_btab_off = (int)lds_f32_core(dl, 16);
                         const size_t lds = lds_tgroup_f_bytes(dl, d, 16);
-                        if (d == 2) hipLaunchKernelGGL((k_level_lds_f<2, true>), grid, block, lds, h->stream, aw);
-                        else if (d == 3) hipLaunchKernelGGL((k_level_lds_f<3, true>), grid, block, lds, h->stream, aw);
-                        else hipLaunchKernelGGL((k_level_lds_f<4, true>), grid, block, lds, h->stream, aw);
+                        if (d == 2) { if (rec) hipLaunchKernelGGL((k_level_lds_f<2, true, true>), grid, block, lds, h->stream, aw); else hipLaunchKernelGGL((k_level_lds_f<2, true>), grid, block, lds, h->stream, aw); }
+                        else if (d == 3) { if (rec) hipLaunchKernelGGL((k_level_lds_f<3, true, true>), grid, block, lds, h->stream, aw); else hipLaunchKernelGGL((k_level_lds_f<3, true>), grid, block, lds, h->stream, aw); }
+                        else { if (rec) hipLaunchKernelGGL((k_level_lds_f<4, true, true>), grid, block, lds, h->stream, aw); else hipLaunchKernelGGL((k_level_lds_f<4, true>), grid, block, lds, h->stream, aw); }
                     } else {
                         aw.lds_btab_off = (int)lds_small_core(dl, 16);
                         const size_t lds = lds_tgroup_bytes(dl, d, 16);
@@ -6018,10 +6105,19 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
         }
         const int m = d + 2;
         const int per = (m * m + 2 * m) * 8;      // one LDS slot per wave
-        // (records: every test of a recorded pair comes here — up to ~1e6 at config 5 depth 4 with
-        // a 1-in-4099 pair sample — so more waves than the threshold mode's few band tests need)
-        const unsigned xg = (h->flags & PCG_FLAG_RECORD) ? 2048u : 256u;
-        hipLaunchKernelGGL(k_exact, dim3(xg), dim3(256), (size_t)per * 4, h->stream, a);
+        // records: every test of a recorded pair comes here (up to ~1e6 at config 5 depth 4 with a
+        // 1-in-4099 pair sample), a lane each at d <= 4; otherwise the threshold mode's few band
+        // tests, a wave each
+        if ((h->flags & PCG_FLAG_RECORD) && m <= 6) {
+            const dim3 g(1024), b(256);
+            if (m == 2) hipLaunchKernelGGL(k_exact_lanes<2>, g, b, 0, h->stream, a);
+            else if (m == 3) hipLaunchKernelGGL(k_exact_lanes<3>, g, b, 0, h->stream, a);
+            else if (m == 4) hipLaunchKernelGGL(k_exact_lanes<4>, g, b, 0, h->stream, a);
+            else if (m == 5) hipLaunchKernelGGL(k_exact_lanes<5>, g, b, 0, h->stream, a);
+            else hipLaunchKernelGGL(k_exact_lanes<6>, g, b, 0, h->stream, a);
+        } else {
+            hipLaunchKernelGGL(k_exact, dim3(256), dim3(256), (size_t)per * 4, h->stream, a);
+        }
         PCG_HIP(h, hipGetLastError());
         return PCG_OK;
     }
@@ -6129,7 +6225,11 @@ int level_end_finish(pcg_handle *h, int d, unsigned long long seq, pcg_stats *st
         if (stats) *stats = h->st;
         return pcg_fail(h, PCG_ERR_PEER, "level %d: another rank failed at this depth", d);
     }
-    if (status[0]) {
+    // the record list can also overflow inside the exact path itself (full-p mode sends every test
+    // of a recorded pair there), after that kernel's own check: the summary's final count decides
+    // (one GPU; a sharded run keeps the device status byte, which every rank agrees on)
+    const bool rec_over = h->world == 1 && !h->rm_ext && (h->flags & PCG_FLAG_RECORD) && (int64_t)c.records > h->rec_cap;
+    if (status[0] || rec_over) {
         // some rank's exact-path (or record) list overflowed: the level is incomplete on every
         // rank. Enlarge and let the driver rerun the skeleton (pcg_skeleton does it itself).
         h->def_cap = std::max<int64_t>(h->def_cap * 4, (int64_t)c.deferred * 2);

@@ -106,7 +106,71 @@ def cost_of(op, costs):
     raise KeyError(op)
 
 
+def class_cycles(ops, pmc, costs, sub=None):
+    """cycles of one region: per class, the region's dynamic count (pmc minus `sub` when given)
+    times the mean cost of the class's opcodes in the region's static mix"""
+    by_class = collections.defaultdict(dict)
+    for op, n in ops.items():
+        if n > 0:
+            by_class[class_of(op) or "OTHER"][op] = n
+    dyn = dict(pmc)
+    if sub is not None:
+        dyn = {k: max(pmc.get(k, 0.0) - sub.get(k, 0.0), 0.0) for k in set(pmc) | set(sub)}
+    total = dyn.get("SQ_INSTS_VALU", 0.0)
+    counted, cyc, lo, hi, detail = 0.0, 0.0, 0.0, 0.0, {}
+    for cls, members in sorted(by_class.items()):
+        n_dyn = (total - sum(dyn.get(PMC_OF[c], 0.0) for c in PMC_OF)) if cls == "OTHER" else dyn.get(PMC_OF[cls], 0.0)
+        n_dyn = max(n_dyn, 0.0)
+        counted += n_dyn
+        static = sum(members.values())
+        cs = {op: cost_of(op, costs) for op in members}
+        mean = sum(members[op] * cs[op][0] for op in members) / static
+        cyc += n_dyn * mean
+        lo += n_dyn * min(c for c, _ in cs.values())
+        hi += n_dyn * max(c for c, _ in cs.values())
+        detail[cls] = {"dynamic": n_dyn, "mean_cost": mean, "isa_static": dict(members)}
+    return {"valu_instructions": total, "valu_issue_cycles": cyc, "bounds": [lo, hi], "classes": detail,
+            "salu_instructions": dyn.get("SQ_INSTS_SALU", 0.0)}
+
+
+def main_regions():
+    """Two-region form (round 4): the dominant kernel's dynamic class counts split into its y
+    sweep and everything else by an ablation build without the sweeps (-DPCG_TGF_ABL=1): sweep =
+    base PMC - ablation PMC, rest = ablation PMC, each class's opcodes weighted by that region's
+    own static mix (sweep = the opcodes the base ISA has beyond the ablation ISA; rest = the
+    ablation ISA). usage: roofline_model.py --regions BASE.s ABL.s KERNEL_SUBSTR PMC_BASE.json
+    PMC_ABL.json PMC_KERNEL_NAME COSTS.json WAVES OUT.json"""
+    a = sys.argv[sys.argv.index("--regions") + 1:]
+    isa_b, isa_a, pat, pmcb, pmca, pmck, costf, waves, out = a[:9]
+    waves = int(waves)
+    rows = json.load(open(costf))["rows"]
+    costs = {r["name"].split(" ")[0]: r["cyc_at_2p4"] for r in rows if r["waves_per_simd"] == waves
+             and not r["name"].startswith("mix") and "bank" not in r["name"]}
+    costs.pop("v_cndmask_b32_e32", None)
+    ob, oa = isa_opcodes(isa_b, pat), isa_opcodes(isa_a, pat)
+    sweep_ops = collections.Counter({op: ob[op] - oa.get(op, 0) for op in ob if ob[op] > oa.get(op, 0)})
+    pb = {k: v["per_dispatch_mean"] for k, v in json.load(open(pmcb))[pmck].items()}
+    pa = {k: v["per_dispatch_mean"] for k, v in json.load(open(pmca))[pmck].items()}
+    sweep = class_cycles(sweep_ops, pb, costs, sub=pa)
+    rest = class_cycles(oa, pa, costs)
+    total = pb["SQ_INSTS_VALU"]
+    cyc = sweep["valu_issue_cycles"] + rest["valu_issue_cycles"]
+    res = {"kernel": pmck, "waves_per_simd": waves, "model": "two-region dynamic (sweep / rest by ablation build)",
+           "valu_instructions": total, "valu_issue_cycles": cyc,
+           "valu_issue_cycles_bounds": [sweep["bounds"][0] + rest["bounds"][0], sweep["bounds"][1] + rest["bounds"][1]],
+           "mean_cycles_per_valu": cyc / total, "salu_instructions": pb.get("SQ_INSTS_SALU", 0.0),
+           "regions": {"sweep": sweep, "rest": rest}, "cost_source": costf,
+           "pmc_source": [pmcb, pmca], "isa_source": [isa_b, isa_a]}
+    json.dump(res, open(out, "w"), indent=1, sort_keys=True)
+    print(json.dumps({k: res[k] for k in ("kernel", "valu_instructions", "valu_issue_cycles", "valu_issue_cycles_bounds",
+                                          "mean_cycles_per_valu")}))
+    print("sweep", round(sweep["valu_instructions"]), round(sweep["valu_issue_cycles"]), "rest",
+          round(rest["valu_instructions"]), round(rest["valu_issue_cycles"]))
+
+
 def main():
+    if "--regions" in sys.argv:
+        return main_regions()
     isa, pat, pmcf, pmck, costf, waves, out = sys.argv[1:8]
     waves = int(waves)
     rows = json.load(open(costf))["rows"]
