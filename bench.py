@@ -176,12 +176,14 @@ def dominant_kernel(d: int, full_p: bool) -> str:
     its fp32-screened form k_level_lds_f at the depths of PCG_TG_F32 / PCG_SCREEN_MASK)."""
     if d == 0:
         return f"k_level0<{1 if full_p else 0}>"
-    if not full_p and 2 <= d <= 4:
+    if 2 <= d <= 4:   # (full-p mode runs the T-group sweeps too, since round 4)
         mask = int(os.environ.get("PCG_SCREEN_MASK", "0x18"), 0)
         sp = int(os.environ.get("PCG_SP", "0"), 0)
         if (mask >> d) & 1 and (sp >> d) & 1 and d in (3, 4):
             return f"k_level_sp<{d}>"
-        return f"k_level_lds_{'f' if (mask >> d) & 1 else 't'}<{d}, false>"
+        if (mask >> d) & 1:   # k_level_lds_f<d, WIDE, REC>: REC = the record-routing build
+            return f"k_level_lds_f<{d}, false, false>"
+        return f"k_level_lds_t<{d}, false>"
     return f"k_level_lds<{d}, {1 if full_p else 0}>"
 
 

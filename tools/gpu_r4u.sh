@@ -6,7 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/r4/u
-mkdir -p $O
+mkdir -p $O $O/pm_base $O/pm_abl1
 B="python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-full-p"
 rocprofv3 -L > $O/counters.txt 2>&1 || true
 cp rcaeval_amd/libpcgpu.so /tmp/libpcgpu_base.so
