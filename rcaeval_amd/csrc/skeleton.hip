@@ -134,6 +134,25 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
+// the wave's LDS slot of the one-wave-per-set kernels: the L rows of the current set (md x (md + 1)),
+// reused by the exact path (m x m matrix, two solution columns, m variable ids; m <= md + 2)
+constexpr int WAVE_SLOT_DOUBLES(int md) {
+    return (md + 2) * (md + 2) + 3 * (md + 2) > md * (md + 1) ? (md + 2) * (md + 2) + 3 * (md + 2) : md * (md + 1);
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v, int l) {
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)v, l);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(v >> 32), l);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -1186,6 +1205,75 @@ __global__ __launch_bounds__(256) void k_level1_pairs(LevelArgs a) {
     block_flush_counts(a.ctr, tests, indep);
 }
 
+// The exact path of one test (numpy.linalg.inv-order LU of the m x m matrix A in LDS, the
+// reference p expression): 0 ok, 1 singular, 2 math domain. Not inlined: its polynomial
+// constants would otherwise be hoisted into registers across the callers' hot loops.
+__device__ __attribute__((noinline)) int exact_lu_pvalue(double *A, int m, double *B0, double *B1, double sqrt_dof,
+                                                         double *pv) {
+    int piv[PCG_MAX_LEVEL_DEPTH + 2];
+    double i00, i01, i11;
+    if (pcg_lu_inv01(A, m, piv, B0, B1, &i00, &i01, &i11)) return 1;
+    const double prod = i00 * i11;
+    if (prod < 0.0) return 2;
+    int err = 0;
+    *pv = pcg_pvalue_from_r(-i01 / sqrt(prod), sqrt_dof, &err);
+    return err;
+}
+
+// k_level_lds beyond PCG_MAX_DEPTH (no deferred list): the band tests a wave's lanes collected in
+// their per-lane masks (bit t: the test (x, nbr t | S) of the lane's set S), decided one at a time
+// by the whole wave in its LDS slot — gather the (d + 2)^2 submatrix of C, LU and the reference p
+// on lane 0 (exact_lu_pvalue), as k_level_wave does. Every lane of the wave must call it.
+__device__ void deep_band_exact(const LevelArgs &a, double *slot, int D, int d, int x, const int32_t *nxs,
+                                const unsigned long long *lmask, unsigned long long *uself,
+                                unsigned long long *uprop, int tx, unsigned long long Smask,
+                                unsigned long long band, unsigned long long &indep) {
+    const int lane = threadIdx.x & 63;
+    unsigned long long need = __ballot(band != 0ull);
+    const int mm = d + 2;
+    double *A = slot, *B0 = slot + mm * mm, *B1 = B0 + mm;
+    int *var = reinterpret_cast<int *>(B1 + mm);
+    while (need) {
+        const int L = __builtin_ctzll(need);
+        need &= need - 1;
+        const unsigned long long sm = readlane_u64(Smask, L);
+        unsigned long long bm = readlane_u64(band, L);
+        while (bm) {
+            const int t = __builtin_ctzll(bm);
+            bm &= bm - 1;
+            const int yg = nxs[t];
+            wave_sync();
+            if (lane < D && ((sm >> lane) & 1ull)) var[2 + __popcll(sm & ((1ull << lane) - 1ull))] = nxs[lane];
+            if (lane == 0) {
+                var[0] = x < yg ? x : yg;
+                var[1] = x < yg ? yg : x;
+            }
+            wave_sync();
+            for (int k = lane; k < mm * mm; k += 64) {
+                const int r = k / mm, c = k - r * mm;
+                A[k] = a.C[(int64_t)var[r] * a.ldc + var[c]];
+            }
+            wave_sync();
+            if (lane == 0) {
+                double pv = __builtin_nan("");
+                const int err = exact_lu_pvalue(A, mm, B0, B1, a.sqrt_dof, &pv);
+                atomicAdd(&a.ctr->exact, 1ull);
+                if (err) {
+                    flag_error(a, err);
+                } else {
+                    if (fabs(pv - a.alpha) < 1e-9) atomicAdd(&a.ctr->near_alpha, 1ull);
+                    if (pv > a.alpha) {
+                        ++indep;
+                        atomicOr(&uself[t], sm);
+                        if (((lmask[t] & sm) == sm) && t >= tx) atomicOr(&uprop[t], sm);
+                    }
+                }
+            }
+        }
+    }
+    wave_sync();
+}
+
 // ---------------------------------------------------------------------------------------
 // depth d >= 1, nodes with D <= 64 neighbours: the node's whole local correlation block
 // M[t][k] = C[nbr t, nbr k] (D x D), C[x, nbr t], C[nbr t, nbr t] and the local adjacency
@@ -1195,6 +1283,13 @@ __global__ __launch_bounds__(256) void k_level1_pairs(LevelArgs a) {
 // walks `spl` S ranks (stride = block size) so the staging is amortised over
 // spl * 256 * (D - d) tests. Sepset unions and removal flags accumulate in LDS (local bits)
 // and are flushed once per block.
+#ifndef PCG_LDS_EXACT_DM
+#define PCG_LDS_EXACT_DM 1   // depths 5-12 (threshold / full-p): one k_level_lds instantiation per depth
+#endif
+#ifndef PCG_LDS_DEEP_TOP
+#define PCG_LDS_DEEP_TOP 16   // k_level_lds instantiations beyond PCG_MAX_DEPTH (threshold mode), <= 20
+#endif
+static_assert(PCG_LDS_DEEP_TOP >= 12 && PCG_LDS_DEEP_TOP <= 20, "PCG_LDS_DEEP_TOP");
 template <int DM, int MODE>
 __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1205,7 +1300,7 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
     int lo = chunk_node(a.cpre, a.n, chunk);
     const int x = lo;
     const int D = a.deg[x];
-    const int d = DM <= 4 ? DM : a.d;
+    const int d = (DM <= 4 || (MODE != MODE_EXACT && PCG_LDS_EXACT_DM)) ? DM : a.d;
     const int32_t *nxg = a.nbr + a.off[x];
 
     double *M = reinterpret_cast<double *>(smem);                 // D * D
@@ -1374,11 +1469,20 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
             }
         }
     } else {
-        for (uint64_t rank = r0 + tid; rank < r1; rank += bs) {
+        // DM > PCG_MAX_DEPTH (threshold mode, depths 13..PCG_LDS_DEEP_MAX): no deferred list; a lane
+        // marks its band tests in `band` and the wave decides them after the lane's sweep
+        // (deep_band_exact), so the rank loop runs a wave-uniform trip count there
+        constexpr bool DEEP = DM > PCG_MAX_DEPTH;
+        static_assert(!DEEP || MODE == MODE_DECIDE, "k_level_lds beyond PCG_MAX_DEPTH: threshold mode only");
+        double *dslot = DEEP ? reinterpret_cast<double *>(smem + a.lds_btab_off) + (size_t)(tid >> 6) * WAVE_SLOT_DOUBLES(DM)
+                             : nullptr;
+        for (uint64_t rank0 = r0 + (DEEP ? (uint64_t)(tid & ~63) : (uint64_t)tid); rank0 < r1; rank0 += bs) {
+            const uint64_t rank = DEEP ? rank0 + (uint64_t)(tid & 63) : rank0;
+            const bool act = !DEEP || rank < r1;
             int k[DM];
     #pragma unroll
             for (int i = 0; i < DM; ++i) k[i] = 0;
-            pcg_unrank_colex<DM>(rank, d, D, a.binom, k);
+            pcg_unrank_colex<DM>(act ? rank : rank0, d, D, a.binom, k);
             unsigned long long Smask = 0;
     #pragma unroll
             for (int i = 0; i < DM; ++i)
@@ -1426,8 +1530,9 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
             const double cxx = Cxx - uu;
             ok = ok && (cxx == cxx);
 
+            unsigned long long band = 0;
             for (int t = 0; t < D; ++t) {
-                if ((Smask >> t) & 1ull) continue;
+                if (!act || ((Smask >> t) & 1ull)) continue;
                 const unsigned long long lm = lmask[t];
                 const bool in_y = (lm & Smask) == Smask;
                 if (t < tx && in_y) continue;          // node nbr[t] < x owns this test (memo)
@@ -1451,7 +1556,12 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
                     }
                     dec = decide<MODE>(a, Mx[t] - uv, cxx, Md[t] - vv, a.tau / gmin, &p);
                 }
-                if (dec == 2 || (MODE == MODE_FULLP && (a.record || fabs(p - a.alpha) < 1e-9))) {
+                if constexpr (DEEP) {
+                    if (dec == 2) {
+                        band |= 1ull << t;
+                        continue;
+                    }
+                } else if (dec == 2 || (MODE == MODE_FULLP && (a.record || fabs(p - a.alpha) < 1e-9))) {
                     int sg[DM];
     #pragma unroll
                     for (int i = 0; i < DM; ++i) sg[i] = i < d ? nxs[k[i]] : 0;
@@ -1471,6 +1581,7 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
                     if (in_y && t >= tx) atomicOr(&uprop[t], Smask);
                 }
             }
+            if constexpr (DEEP) deep_band_exact(a, dslot, D, d, x, nxs, lmask, uself, uprop, tx, Smask, band, indep);
         }
     }
     __syncthreads();
@@ -3670,37 +3781,8 @@ __global__ __launch_bounds__(64) void k_level_deep(LevelArgs a, double *scratch,
 // in the wave's LDS slot beyond). Per S: |S|^2 readlanes + |S|^2 / 2 fp64 FMAs per lane, for
 // D - |S| tests — replaces the per-test global-scratch LU of k_level_deep (10 ms for 19 tests).
 // Consecutive sets of a wave follow colex order (Gosper's next-combination on the 64-bit mask).
-#ifndef PCG_WAVE_LO
-#define PCG_WAVE_LO 13
-#endif
+
 constexpr int WAVE_MAXD = 63;    // D + 1 lanes (the neighbours and x) per wave
-// the wave's LDS slot: the L rows of the current set (md x (md + 1)), reused by the exact path
-// (m x m matrix, two solution columns, m variable ids; m <= md + 2)
-constexpr int WAVE_SLOT_DOUBLES(int md) {
-    return (md + 2) * (md + 2) + 3 * (md + 2) > md * (md + 1) ? (md + 2) * (md + 2) + 3 * (md + 2) : md * (md + 1);
-}
-
-__device__ __forceinline__ double readlane_f64(double v, int l) {
-    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-    const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l);
-    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
-    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
-
-// The exact path of one test (numpy.linalg.inv-order LU of the m x m matrix A in LDS, the
-// reference p expression): 0 ok, 1 singular, 2 math domain. Not inlined: its polynomial
-// constants would otherwise be hoisted into registers across the callers' hot loops.
-__device__ __attribute__((noinline)) int exact_lu_pvalue(double *A, int m, double *B0, double *B1, double sqrt_dof,
-                                                         double *pv) {
-    int piv[PCG_MAX_LEVEL_DEPTH + 2];
-    double i00, i01, i11;
-    if (pcg_lu_inv01(A, m, piv, B0, B1, &i00, &i01, &i11)) return 1;
-    const double prod = i00 * i11;
-    if (prod < 0.0) return 2;
-    int err = 0;
-    *pv = pcg_pvalue_from_r(-i01 / sqrt(prod), sqrt_dof, &err);
-    return err;
-}
 
 // global ids of the members of a local set mask (ascending), -1 padded to PCG_MAX_DEPTH
 __device__ __forceinline__ void set_members(unsigned long long mask, const int32_t *nxs, int (&sg)[PCG_MAX_DEPTH]) {
@@ -5114,9 +5196,36 @@ void launch_lds_mode(pcg_handle *h, const LevelArgs &a, int64_t nchunks, size_t 
     else if (d == 2) hipLaunchKernelGGL((k_level_lds<2, MODE>), grid, block, lds, h->stream, a);
     else if (d == 3) hipLaunchKernelGGL((k_level_lds<3, MODE>), grid, block, lds, h->stream, a);
     else if (d == 4) hipLaunchKernelGGL((k_level_lds<4, MODE>), grid, block, lds, h->stream, a);
-    else if (d <= 6) hipLaunchKernelGGL((k_level_lds<6, MODE>), grid, block, lds, h->stream, a);
-    else if (d <= 8) hipLaunchKernelGGL((k_level_lds<8, MODE>), grid, block, lds, h->stream, a);
-    else hipLaunchKernelGGL((k_level_lds<12, MODE>), grid, block, lds, h->stream, a);
+    else if constexpr (MODE != MODE_EXACT && PCG_LDS_EXACT_DM) {
+        // one instantiation per depth: the per-lane Cholesky arrays sized by d, not by the bucket's
+        // largest depth (k_level_lds<12> took 256 VGPRs + 1 AGPR, one wave per SIMD, at d = 9)
+        if (d == 5) hipLaunchKernelGGL((k_level_lds<5, MODE>), grid, block, lds, h->stream, a);
+        else if (d == 6) hipLaunchKernelGGL((k_level_lds<6, MODE>), grid, block, lds, h->stream, a);
+        else if (d == 7) hipLaunchKernelGGL((k_level_lds<7, MODE>), grid, block, lds, h->stream, a);
+        else if (d == 8) hipLaunchKernelGGL((k_level_lds<8, MODE>), grid, block, lds, h->stream, a);
+        else if (d == 9) hipLaunchKernelGGL((k_level_lds<9, MODE>), grid, block, lds, h->stream, a);
+        else if (d == 10) hipLaunchKernelGGL((k_level_lds<10, MODE>), grid, block, lds, h->stream, a);
+        else if (d == 11) hipLaunchKernelGGL((k_level_lds<11, MODE>), grid, block, lds, h->stream, a);
+        else if constexpr (MODE == MODE_DECIDE) {
+            // beyond PCG_MAX_DEPTH (up to PCG_LDS_DEEP_TOP; use_wave sends deeper levels to the
+            // one-wave-per-set kernels)
+            if (d == 13) hipLaunchKernelGGL((k_level_lds<13, MODE>), grid, block, lds, h->stream, a);
+            else if (d == 14) hipLaunchKernelGGL((k_level_lds<14, MODE>), grid, block, lds, h->stream, a);
+            else if (d == 15) hipLaunchKernelGGL((k_level_lds<15, MODE>), grid, block, lds, h->stream, a);
+            else if (d == 16) hipLaunchKernelGGL((k_level_lds<16, MODE>), grid, block, lds, h->stream, a);
+#if PCG_LDS_DEEP_TOP > 16
+            else if (d == 17) hipLaunchKernelGGL((k_level_lds<17, MODE>), grid, block, lds, h->stream, a);
+            else if (d == 18) hipLaunchKernelGGL((k_level_lds<18, MODE>), grid, block, lds, h->stream, a);
+            else if (d == 19) hipLaunchKernelGGL((k_level_lds<19, MODE>), grid, block, lds, h->stream, a);
+            else if (d == 20) hipLaunchKernelGGL((k_level_lds<20, MODE>), grid, block, lds, h->stream, a);
+#endif
+            else hipLaunchKernelGGL((k_level_lds<12, MODE>), grid, block, lds, h->stream, a);
+        } else hipLaunchKernelGGL((k_level_lds<12, MODE>), grid, block, lds, h->stream, a);
+    } else {
+        if (d <= 6) hipLaunchKernelGGL((k_level_lds<6, MODE>), grid, block, lds, h->stream, a);
+        else if (d <= 8) hipLaunchKernelGGL((k_level_lds<8, MODE>), grid, block, lds, h->stream, a);
+        else hipLaunchKernelGGL((k_level_lds<12, MODE>), grid, block, lds, h->stream, a);
+    }
 }
 
 constexpr int SMALL_DEG = 64;        // LDS-resident kernels handle nodes with <= 64 neighbours
@@ -5166,10 +5275,20 @@ bool wave_pr() {
     return !e || atoi(e) != 0;
 }
 
+// threshold mode: the deepest depth on the per-lane k_level_lds (PCG_MAX_DEPTH .. PCG_LDS_DEEP_TOP;
+// the A/B knob PCG_LDS_DEEP, read per depth)
+int lds_deep_max() {
+    const char *e = getenv("PCG_LDS_DEEP");
+    const int v = e ? atoi(e) : PCG_LDS_DEEP_TOP;
+    return std::min(std::max(v, PCG_MAX_DEPTH), PCG_LDS_DEEP_TOP);
+}
 bool use_wave(int mode, int d) {
+    if (!(mode == MODE_DECIDE || mode == MODE_FULLP) || d > PCG_MAX_LEVEL_DEPTH) return false;
     const char *e = getenv("PCG_WAVE_LO");        // read per depth, like PCG_SCREEN_MASK
-    const int lo = e ? atoi(e) : PCG_WAVE_LO;
-    return (mode == MODE_DECIDE || mode == MODE_FULLP) && d >= std::max(lo, 5) && d <= PCG_MAX_LEVEL_DEPTH;
+    if (e) return d >= std::max(atoi(e), 5);      // explicit: the wave kernels from that depth up
+    // default: the wave kernels beyond the per-lane kernel's depths (PCG_MAX_DEPTH; threshold
+    // mode up to lds_deep_max())
+    return d > (mode == MODE_DECIDE ? lds_deep_max() : PCG_MAX_DEPTH);
 }
 // depth 1's large class runs k_level1_pairs (pcg_level_run); its chunks split a node's
 // D(D-1)/2 neighbour pairs evenly, ~L1_PAIRS_PER_CHUNK each, so a high-degree node is spread
@@ -5186,7 +5305,9 @@ int64_t l1_pair_chunks(int D) { return std::max<int64_t>(1, ((int64_t)D * (D - 1
 // node class of a degree-D node at depth d: 0 narrow, 1 wide (T-group depths only), 2 large
 int level_class(const pcg_handle *h, int D, int d, bool tg) {
     if (h->wavek) return D <= std::min(WAVE_MAXD, h->narrow_deg) ? 0 : 2;   // k_level_wave depths
-    if (D <= std::min(SMALL_DEG, h->narrow_deg) && d <= PCG_MAX_DEPTH) return 0;
+    if (D <= std::min(SMALL_DEG, h->narrow_deg) &&
+        (d <= PCG_MAX_DEPTH || (mode_of(h, d) == MODE_DECIDE && d <= lds_deep_max())))
+        return 0;
     if (tg && D <= WIDE_DEG && lds_tgroup_bytes((D + 3) & ~3, d, 16) <= LDS_MAX) return 1;
     return 2;
 }
@@ -5978,7 +6099,9 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                     as.bs = 256;
                     const int dl = h->tgroup ? (h->maxdeg_small + 3) & ~3 : h->maxdeg_small;
                     as.lds_btab_off = (int)lds_small_core(dl);
-                    const size_t lds = h->tgroup ? lds_tgroup_bytes(dl, d) : lds_small_bytes(dl);
+                    size_t lds = h->tgroup ? lds_tgroup_bytes(dl, d) : lds_small_bytes(dl);
+                    if (!h->tgroup && d > PCG_MAX_DEPTH)   // k_level_lds's per-wave exact-path slots
+                        lds = std::max(lds, lds_small_core(dl) + 4 * sizeof(double) * WAVE_SLOT_DOUBLES(PCG_LDS_DEEP_TOP));
                     if (h->wavek) {
                         const dim3 grid((unsigned)(s_hi - s_lo)), block(256);
                         const size_t core = lds_small_core(h->maxdeg_small);
