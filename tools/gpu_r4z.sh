@@ -23,6 +23,11 @@ for l in open(sys.argv[1]):
         print(sys.argv[2], 'n', d['n'], 'gpu_ms', round(d['gpu_ms'], 3), 'kernel', round(sum(d['kernel_ms']), 3), 'levels', d['levels'], 'tests', sum(d['tests']), hash(tuple(d['tests'])) % 100000, hash(tuple(d['max_degree'])) % 100000, 'kms', [round(v, 2) for v in d['kernel_ms'][13:]])
 PY
 }
+step tests 600 python -u -m pytest tests/test_gpu_skeleton.py tests/test_gpu_e2e.py -x -q --timeout 300 --timeout-method thread -k "full_depth or wave_kernel or max_depth or skeleton_matches_oracle or sepset or export or e2e"
+tail -2 $O/tests.log
+step d500_intree 120 python -u tools/profile_deep.py --n 500 --reps 5
+PCG_EXPORT_INLINE=0 step d500_intree_noinl 120 python -u tools/profile_deep.py --n 500 --reps 5
+step d1000_intree 200 python -u tools/profile_deep.py --n 1000 --reps 1
 cp rcaeval_amd/libpcgpu.so /tmp/libpcgpu_intree.so
 cp tools/variants_r4/libpcgpu_top20.so rcaeval_amd/libpcgpu.so
 for v in 16 17 18 20; do
@@ -31,3 +36,4 @@ for v in 16 17 18 20; do
 done
 cp /tmp/libpcgpu_intree.so rcaeval_amd/libpcgpu.so
 for v in 16 17 18 20; do summ $O/d1000_$v.log d1000_$v; summ $O/d500_$v.log d500_$v; done
+for f in d500_intree d500_intree_noinl d1000_intree; do summ $O/$f.log $f; done

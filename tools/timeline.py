@@ -1,12 +1,14 @@
 """Timeline of the last bench step from a rocprofv3 kernel trace: per dispatch the start offset,
 duration and the idle gap before it (per stream), from the last k_colsum_partial on.
-usage: python tools/timeline.py run_kernel_trace.csv"""
+usage: python tools/timeline.py run_kernel_trace.csv [ANCHOR]
+(ANCHOR: the kernel that starts a step, default k_colsum_partial; k_init for skeleton-only runs)"""
 import csv
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-starts = [i for i, r in enumerate(rows) if "k_colsum_partial" in r["Kernel_Name"]] + [len(rows)]
+anchor = sys.argv[2] if len(sys.argv) > 2 else "k_colsum_partial"
+starts = [i for i, r in enumerate(rows) if anchor in r["Kernel_Name"]] + [len(rows)]
 # the last threshold-mode step (k_level0<0>), not the full-p side run
 pick = [(a, b) for a, b in zip(starts, starts[1:]) if any("k_level0<0>" in r["Kernel_Name"] for r in rows[a:b])][-1]
 rows = rows[pick[0]:pick[1]]
