@@ -42,10 +42,16 @@ bool pcg_ensure_pinned(pcg_handle *h, PinBuf &b, size_t bytes) {
         hipStreamSynchronize(h->stream);
         hipHostFree(b.p);
         b.p = nullptr;
+        b.dp = nullptr;
         b.bytes = 0;
     }
     if (hipHostMalloc(&b.p, bytes, hipHostMallocMapped) != hipSuccess) {   // device-readable (k_copy_i64)
         b.p = nullptr;
+        return false;
+    }
+    if (hipHostGetDevicePointer(&b.dp, b.p, 0) != hipSuccess) {   // once per allocation, not per level
+        hipHostFree(b.p);
+        b.p = b.dp = nullptr;
         return false;
     }
     b.bytes = bytes;

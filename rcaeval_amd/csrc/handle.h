@@ -18,6 +18,7 @@ struct DevBuf {
 
 struct PinBuf {                    // page-locked host staging (async per-level transfers)
     void *p = nullptr;
+    void *dp = nullptr;            // its device address (hipHostMallocMapped), queried once
     size_t bytes = 0;
 };
 
@@ -89,6 +90,7 @@ struct pcg_handle {
     hipEvent_t ev_xready = nullptr, ev_xdone[2] = {nullptr, nullptr};
     bool xpending[2] = {false, false};    // an export reading set i is queued on xs
     bool xany = false;               // exports queued since the last export_sync
+    bool xinl = false;               // ... some of them on the handle's stream (small graphs)
     DevBuf exp_ctr;                  // rows exported so far (device, persists across depths)
     PinBuf ctr_pin, deg_pin, off_pin, cpre_pin, status_pin;
     DevBuf gbar;                     // the fused level barrier's grid-barrier words (k_level_end)
@@ -151,6 +153,7 @@ struct pcg_handle {
     int32_t maxdeg = 0;
     int64_t sumdeg = 0;
     LevelSummary *summary = nullptr;    // host-mapped, coherent (graph_launch / level_wait)
+    void *summary_dev = nullptr;        // its device address, queried once at allocation
     size_t summary_bytes = 0;
     unsigned long long summary_seq = 0;
     // PCG_HOST_TRACE=1: host timestamps of the level loop's steps, printed after each skeleton

@@ -1274,6 +1274,31 @@ __device__ void deep_band_exact(const LevelArgs &a, double *slot, int D, int d, 
     wave_sync();
 }
 
+// Element ii (0-based, from the top) of a colex unrank with remaining rank rr < C(hi, ii + 1): the
+// largest c in [ii, hi - 1] with C(c, ii + 1) <= rr. Closed forms for the two lowest positions
+// (every T-group task decodes them): C(c, 1) = c gives c = rr; C(c, 2) = c (c - 1) / 2 gives
+// c = floor((1 + sqrt(1 + 8 rr)) / 2), fixed up by one either way (rr < C(128, 2): the fp32 root is
+// within 1e-4 of the exact one). Deeper positions search the LDS table tab[c * stride + ii + 1].
+#ifndef PCG_COLEX_CF
+#define PCG_COLEX_CF 1   // A/B: 0 = the table search at every position
+#endif
+template <typename R, typename TAB>
+__device__ __forceinline__ int colex_elem(int ii, R rr, int hi, const TAB *tab, int stride) {
+    if (PCG_COLEX_CF && ii == 0) return (int)rr;
+    if (PCG_COLEX_CF && ii == 1) {
+        int c = (int)((1.0f + __builtin_sqrtf(1.0f + 8.0f * (float)rr)) * 0.5f);
+        if ((R)(c * (c - 1) / 2) > rr) --c;
+        else if ((R)((c + 1) * c / 2) <= rr) ++c;
+        return c;
+    }
+    int lo_ = ii, up = hi - 1;
+    while (lo_ < up) {
+        const int mid = (lo_ + up + 1) >> 1;
+        if (tab[mid * stride + ii + 1] <= rr) lo_ = mid; else up = mid - 1;
+    }
+    return lo_;
+}
+
 // ---------------------------------------------------------------------------------------
 // depth d >= 1, nodes with D <= 64 neighbours: the node's whole local correlation block
 // M[t][k] = C[nbr t, nbr k] (D x D), C[x, nbr t], C[nbr t, nbr t] and the local adjacency
@@ -1287,7 +1312,11 @@ __device__ void deep_band_exact(const LevelArgs &a, double *slot, int D, int d, 
 #define PCG_LDS_EXACT_DM 1   // depths 5-12 (threshold / full-p): one k_level_lds instantiation per depth
 #endif
 #ifndef PCG_LDS_DEEP_TOP
-#define PCG_LDS_DEEP_TOP 16   // k_level_lds instantiations beyond PCG_MAX_DEPTH (threshold mode), <= 20
+#define PCG_LDS_DEEP_TOP 20   // k_level_lds instantiations beyond PCG_MAX_DEPTH (threshold mode), <= 20
+#endif
+#ifndef PCG_LDS_SPILL_MIN
+#define PCG_LDS_SPILL_MIN 1e7 // depths 17..20 (instantiations that spill to scratch) take the per-lane kernel
+                              // only for levels of at least this many tests (else the wave kernels)
 #endif
 static_assert(PCG_LDS_DEEP_TOP >= 12 && PCG_LDS_DEEP_TOP <= 20, "PCG_LDS_DEEP_TOP");
 template <int DM, int MODE>
@@ -1363,11 +1392,7 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
                 int hi_ = D;
 #pragma unroll
                 for (int ii = DM - 1; ii >= 0; --ii) {
-                    int lo_ = ii, up = hi_ - 1;
-                    while (lo_ < up) {
-                        const int mid = (lo_ + up + 1) >> 1;
-                        if (btab[mid * (DM + 1) + ii + 1] <= rr) lo_ = mid; else up = mid - 1;
-                    }
+                    const int lo_ = colex_elem(ii, rr, hi_, btab, DM + 1);
                     k[ii] = lo_;
                     rr -= btab[lo_ * (DM + 1) + ii + 1];
                     hi_ = lo_;
@@ -1842,11 +1867,7 @@ __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_
             int hi_ = D - T[0] - 1;
 #pragma unroll
             for (int ii = DT - 2; ii >= 0; --ii) {
-                int lo_ = ii, up = hi_ - 1;
-                while (lo_ < up) {
-                    const int mid = (lo_ + up + 1) >> 1;
-                    if (btab[mid * (DM + 1) + ii + 1] <= rr) lo_ = mid; else up = mid - 1;
-                }
+                const int lo_ = colex_elem(ii, rr, hi_, btab, DM + 1);
                 T[ii + 1] = lo_;
                 rr -= btab[lo_ * (DM + 1) + ii + 1];
                 hi_ = lo_;
@@ -2563,11 +2584,7 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
             int hi_ = D - T[0] - 1;
 #pragma unroll
             for (int ii = DT - 2; ii >= 0; --ii) {
-                int lo_ = ii, up = hi_ - 1;
-                while (lo_ < up) {
-                    const int mid = (lo_ + up + 1) >> 1;
-                    if (btab[mid * (DM + 1) + ii + 1] <= rr) lo_ = mid; else up = mid - 1;
-                }
+                const int lo_ = colex_elem(ii, rr, hi_, btab, DM + 1);
                 T[ii + 1] = lo_;
                 rr -= btab[lo_ * (DM + 1) + ii + 1];
                 hi_ = lo_;
@@ -5282,13 +5299,18 @@ int lds_deep_max() {
     const int v = e ? atoi(e) : PCG_LDS_DEEP_TOP;
     return std::min(std::max(v, PCG_MAX_DEPTH), PCG_LDS_DEEP_TOP);
 }
-bool use_wave(int mode, int d) {
+// tests: the level's test count bound (sum over nodes of C(D, d) (D - d))
+bool use_wave(int mode, int d, double tests) {
     if (!(mode == MODE_DECIDE || mode == MODE_FULLP) || d > PCG_MAX_LEVEL_DEPTH) return false;
     const char *e = getenv("PCG_WAVE_LO");        // read per depth, like PCG_SCREEN_MASK
     if (e) return d >= std::max(atoi(e), 5);      // explicit: the wave kernels from that depth up
     // default: the wave kernels beyond the per-lane kernel's depths (PCG_MAX_DEPTH; threshold
-    // mode up to lds_deep_max())
-    return d > (mode == MODE_DECIDE ? lds_deep_max() : PCG_MAX_DEPTH);
+    // mode up to lds_deep_max(), from depth 17 on only for large levels: those instantiations
+    // spill to scratch at one wave per SIMD, which loses to the wave kernels on a few thousand
+    // tests — n = 500's depths 17-18: 0.05 vs 0.02 ms — and wins 2.3-2.7x on 1e9)
+    if (mode != MODE_DECIDE) return d > PCG_MAX_DEPTH;
+    if (d > lds_deep_max()) return true;
+    return d > 16 && tests < PCG_LDS_SPILL_MIN;
 }
 // depth 1's large class runs k_level1_pairs (pcg_level_run); its chunks split a node's
 // D(D-1)/2 neighbour pairs evenly, ~L1_PAIRS_PER_CHUNK each, so a high-degree node is spread
@@ -5333,11 +5355,13 @@ int graph_launch(pcg_handle *h, const LevelArgs *fa) {
     if (!h->summary || h->summary_bytes < 2 * slot) {
         if (h->summary) { (void)hipStreamSynchronize(h->stream); (void)hipHostFree(h->summary); }
         h->summary = nullptr;
+        h->summary_dev = nullptr;
         h->summary_bytes = 0;
         void *p = nullptr;
         if (hipHostMalloc(&p, 2 * slot, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
             return pcg_fail(h, PCG_ERR_OOM, "host-mapped level summary");
         h->summary = (LevelSummary *)p;
+        PCG_HIP(h, hipHostGetDevicePointer(&h->summary_dev, p, 0));
         h->summary_bytes = 2 * slot;
         h->summary_slot = slot;
         sum_slot(h, 0)->seq = 0;
@@ -5345,9 +5369,7 @@ int graph_launch(pcg_handle *h, const LevelArgs *fa) {
         h->summary_seq = 0;
     }
     const unsigned long long seq = ++h->summary_seq;
-    void *dsum = nullptr;
-    PCG_HIP(h, hipHostGetDevicePointer(&dsum, sum_slot(h, seq), 0));
-    LevelSummary *ds = (LevelSummary *)dsum;
+    LevelSummary *ds = reinterpret_cast<LevelSummary *>(reinterpret_cast<char *>(h->summary_dev) + (seq & 1) * h->summary_slot);
     uint8_t *status = h->depth >= 0 ? (h->rm_ext ? h->rm_ext : (uint8_t *)h->rm.p) + (int64_t)n * n : nullptr;
     // the next depth's CSR is built from the device degrees while the host waits for the
     // summary; nbr is sized by the current graph (degrees only fall), and the union rows are
@@ -5497,6 +5519,7 @@ extern "C" int pcg_skeleton_init(pcg_handle *h, const double *C, int64_t n, int6
     if (h->xs) PCG_HIP(h, hipStreamSynchronize(h->xs));   // a previous run's exports are done
     h->xpending[0] = h->xpending[1] = false;
     h->xany = false;
+    h->xinl = false;
     h->cb = 0;
     h->export_rows = 0;
     h->rec_h.clear(); h->near_h.clear();
@@ -5579,8 +5602,7 @@ int level_begin_bound_upload(pcg_handle *h, int depth, int64_t blk_cap) {
     if (h->nblk && (!pcg_ensure(h, h->cblk, sizeof(double) * std::max<int64_t>(blk_cap, 1)) ||
                     !pcg_ensure(h, h->lmk, sizeof(uint64_t) * std::max<int64_t>(h->sumdeg, 1))))
         return pcg_fail(h, PCG_ERR_OOM, "compact node blocks");
-    void *src = nullptr;
-    PCG_HIP(h, hipHostGetDevicePointer(&src, pb.p, 0));
+    const void *src = pb.dp;
     int64_t *dev = (int64_t *)h->cpre.p;
     hipLaunchKernelGGL(k_copy_i64, dim3((unsigned)((up + 255) / 256)), dim3(256), 0, h->stream, (const int64_t *)src, up,
                        dev + h->sp_tab_off);
@@ -5684,7 +5706,14 @@ int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks, bool bound
         // small class units: T-group lane tasks (threshold mode, depth 2..4) or S ranks
         const bool tg = use_tgroup(mode_of(h, depth), depth);
         h->tgroup = tg;
-        h->wavek = use_wave(mode_of(h, depth), depth);
+        double tests_bound = 0.0;            // sum over nodes of C(D, d) (D - d)
+        for (int D = depth + 1; D <= maxd; ++D) {
+            if (!hist[D]) continue;
+            double c = 1.0;
+            for (int i = 0; i < depth; ++i) c = c * (double)(D - i) / (double)(i + 1);
+            tests_bound += (double)hist[D] * c * (double)(D - depth);
+        }
+        h->wavek = use_wave(mode_of(h, depth), depth, tests_bound);
         // fp32-screened depths: pcg_set_screen_precision, or the PCG_SCREEN_MASK A/B knob
         const char *sm = getenv("PCG_SCREEN_MASK");
         h->screen_eff = sm ? (int)strtol(sm, nullptr, 0) : (h->screen_mask < 0 ? PCG_TG_F32 : h->screen_mask);
@@ -5893,8 +5922,7 @@ int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks, bool bound
     // rm, the counters and the status bytes were cleared by the previous depth's k_apply /
     // k_level_summary (or at init); the union rows by k_fill_nbr (or here, on first use)
     {
-        void *src = nullptr;
-        PCG_HIP(h, hipHostGetDevicePointer(&src, h->cpre_pin.p, 0));
+        const void *src = h->cpre_pin.dp;
         hipLaunchKernelGGL(k_copy_i64, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, h->stream,
                            (const int64_t *)src, cnt, (int64_t *)h->cpre.p);
         PCG_HIP(h, hipGetLastError());
@@ -6218,6 +6246,9 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
         // exact path over the deferred list; the kernel reads the list length on the device
         // (no host round trip) and raises the overflow status byte if the list overflowed
         if (h->fuse_end) return PCG_OK;   // the screen and exact path run in k_level_end
+        // beyond PCG_MAX_DEPTH every kernel decides its band tests itself (k_level_wave,
+        // k_level_lds's wave slots, k_level_deep): nothing is deferred, no launch
+        if (d > PCG_MAX_DEPTH) return PCG_OK;
         a = make_args(h, d, mode == MODE_EXACT);
         if (h->tgroup && use_screen32(h, d)) {   // the fp32 sweep's undecided tests, in fp64
             // the list length is only known on the device; a grid-stride loop over it (1024 blocks
@@ -6246,6 +6277,15 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
     }
 }
 
+// graphs whose CSR holds at most this many entries export on the handle's stream (PCG_EXPORT_INLINE)
+#ifndef PCG_EXPORT_INLINE
+#define PCG_EXPORT_INLINE 16384
+#endif
+int64_t export_inline_max() {
+    const char *e = getenv("PCG_EXPORT_INLINE");
+    return e ? atoll(e) : (int64_t)PCG_EXPORT_INLINE;
+}
+
 // the level barrier of the current depth, enqueued: removals applied, the next graph's summary and
 // CSR (k_summary_fill), the depth's sepset export on the export stream. Returns the summary's
 // sequence number in *seq (level_end_finish waits for it).
@@ -6270,7 +6310,19 @@ int level_end_enqueue(pcg_handle *h, unsigned long long *seq) {
     // degrees + counters + status -> host-mapped summary (fused: after the screen, exact path
     // and removals of the same launch)
     int rc = graph_launch(h, h->fuse_end ? &fa : nullptr);
-    if (!rc && d >= 1 && xsum > 0) {
+    if (!rc && d >= 1 && xsum > 0 && xsum <= export_inline_max()) {
+        // a small graph's export on the handle's stream, right behind the barrier: one launch
+        // instead of the export stream's four calls (it runs while the host decomposes the next
+        // depth, and is done before any later launch can reuse buffer set xcb)
+        hipLaunchKernelGGL(k_export, dim3((unsigned)((xsum + 255) / 256)), dim3(256), 0, h->stream,
+                           (const int32_t *)h->off2[xcb].p, (const int32_t *)h->nbr2[xcb].p,
+                           (const int8_t *)h->rl, d, (const uint64_t *)h->ug2[xcb].p, n, W, xsum,
+                           (int32_t *)h->export_xy.p, (uint64_t *)h->exportbuf.p, h->export_cap,
+                           (unsigned long long *)h->exp_ctr.p);
+        PCG_HIP(h, hipGetLastError());
+        h->xany = true;
+        h->xinl = true;
+    } else if (!rc && d >= 1 && xsum > 0) {
         // depth d's sepset export on the export stream, queued behind the barrier (removed_level
         // written); it reads buffer set xcb while the next depth runs on the other set
         if (!h->xs) PCG_HIP(h, hipStreamCreateWithFlags(&h->xs, hipStreamNonBlocking));
@@ -6518,6 +6570,7 @@ int skeleton_small(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64
     if (h->xs) PCG_HIP(h, hipStreamSynchronize(h->xs));
     h->xpending[0] = h->xpending[1] = false;
     h->xany = false;
+    h->xinl = false;
     h->export_rows = 0;
     h->rec_h.clear(); h->near_h.clear();
     h->rec_total = h->near_total = 0;
@@ -6661,10 +6714,19 @@ int export_sync(pcg_handle *h) {
     if (!h->xany) return PCG_OK;
     // the row counter comes back on the export stream itself: one stream sync, no device-wide copy
     if (!pcg_ensure_pinned(h, h->ctr_pin, sizeof(unsigned long long))) return pcg_fail(h, PCG_ERR_OOM, "pinned counter");
-    PCG_HIP(h, hipMemcpyAsync(h->ctr_pin.p, h->exp_ctr.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, h->xs));
-    PCG_HIP(h, hipStreamSynchronize(h->xs));
+    // exports on the handle's stream (xinl) and/or on the export stream: the counter is read
+    // behind all of them
+    hipStream_t s = h->xs ? h->xs : h->stream;
+    if (h->xs && h->xinl) {
+        if (!h->ev_xready) PCG_HIP(h, hipEventCreateWithFlags(&h->ev_xready, hipEventDisableTiming));
+        PCG_HIP(h, hipEventRecord(h->ev_xready, h->stream));
+        PCG_HIP(h, hipStreamWaitEvent(h->xs, h->ev_xready, 0));
+    }
+    PCG_HIP(h, hipMemcpyAsync(h->ctr_pin.p, h->exp_ctr.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    PCG_HIP(h, hipStreamSynchronize(s));
     const unsigned long long rows = *(const unsigned long long *)h->ctr_pin.p;
     h->xany = false;
+    h->xinl = false;
     h->xpending[0] = h->xpending[1] = false;
     if ((int64_t)rows > h->export_cap)
         return pcg_fail(h, PCG_ERR_OVERFLOW, "sepset export overflow (%llu rows > %lld)", rows,
