@@ -6605,7 +6605,8 @@ int skeleton_small(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64
     a.rec_cap = h->rec_cap;
     a.rec_mod = h->rec_mod;
     a.rec_res = h->rec_res;
-    a.fullp = (flags & PCG_FLAG_FULL_P) ? 1 : 0;
+    // RECORD alone records every unique test with its p: full-p mode, as the level loop (mode_of)
+    a.fullp = (flags & (PCG_FLAG_FULL_P | PCG_FLAG_RECORD)) ? 1 : 0;
     a.record = (flags & PCG_FLAG_RECORD) ? 1 : 0;
     a.exact_all = (flags & PCG_FLAG_EXACT_ALL) ? 1 : 0;
     a.sum = (SmallSummary *)h->small_sum.p;

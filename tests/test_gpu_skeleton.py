@@ -551,3 +551,42 @@ def test_wave_kernel_from_depth5_matches_oracle(eng, n, N, seed, wl, wh, ep, fla
         keys = sorted(d)
         assert fisherz.p_close([g[k] for k in keys], [d[k] for k in keys]).all()
 
+
+
+def _engine_state(out):
+    return (np.asarray(out.removed_level).copy(), list(out.stats["tests"]), list(out.stats["indep"]),
+            unions_from_engine(out))
+
+
+def test_deep_per_lane_kernel_equals_wave_kernels_n1000(eng, monkeypatch):
+    """Threshold-mode depths 13..20 on the per-lane k_level_lds (band tests decided by the wave in
+    its LDS slot; depths 17..20 for levels of >= 1e7 tests) against the one-wave-per-set kernels
+    (PCG_LDS_DEEP=12) on n = 1000 at unlimited depth (30 levels, 3.3e10 tests): removal depths,
+    per-level counts and sepset unions identical. (The C oracle takes hours here; n = 500's oracle
+    test covers depths 13..16 of the same path.)"""
+    X = synth.gaussian_sem(1000, 10000, seed=0)
+    C = np.corrcoef(X.T)
+    a = _engine_state(eng.skeleton(C, 10000))
+    monkeypatch.setenv("PCG_LDS_DEEP", "12")
+    b = _engine_state(eng.skeleton(C, 10000))
+    assert len(a[1]) == len(b[1]) == 30
+    np.testing.assert_array_equal(a[0], b[0])
+    assert a[1] == b[1] and a[2] == b[2]
+    assert a[3] == b[3]
+
+
+@pytest.mark.parametrize("n,N,seed,wl,wh,ep", CASES[:3])
+def test_inline_export_equals_export_stream(eng, n, N, seed, wl, wh, ep, monkeypatch):
+    """Small graphs export their sepset unions on the handle's stream (PCG_EXPORT_INLINE); the
+    export stream (PCG_EXPORT_INLINE=0) gives the same rows, and both match the oracle."""
+    monkeypatch.setenv("PCG_SMALL", "0")
+    X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
+    C = np.corrcoef(X.T)
+    ref = cpc.skeleton(C, N)
+    a = eng.skeleton(C, N)
+    assert_skeleton_matches(a, ref, n)
+    monkeypatch.setenv("PCG_EXPORT_INLINE", "0")
+    b = eng.skeleton(C, N)
+    sa, sb = _engine_state(a), _engine_state(b)
+    np.testing.assert_array_equal(sa[0], sb[0])
+    assert sa[3] == sb[3]

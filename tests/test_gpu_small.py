@@ -58,7 +58,8 @@ def test_small_equals_level_loop_and_oracle(eng, monkeypatch, n, N, seed, wl, wh
 
 
 @pytest.mark.parametrize("n,N,seed,wl,wh,ep", CASES[2:7])
-@pytest.mark.parametrize("flags", [_lib.PCG_FLAG_FULL_P | _lib.PCG_FLAG_RECORD, _lib.PCG_FLAG_EXACT_ALL | _lib.PCG_FLAG_RECORD])
+@pytest.mark.parametrize("flags", [_lib.PCG_FLAG_FULL_P | _lib.PCG_FLAG_RECORD, _lib.PCG_FLAG_RECORD,
+                                   _lib.PCG_FLAG_EXACT_ALL | _lib.PCG_FLAG_RECORD])
 def test_small_records_equal_level_loop(eng, monkeypatch, n, N, seed, wl, wh, ep, flags):
     X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
     C = np.corrcoef(X.T)
