@@ -1311,6 +1311,10 @@ __device__ __forceinline__ int colex_elem(int ii, R rr, int hi, const TAB *tab, 
 #ifndef PCG_LDS_EXACT_DM
 #define PCG_LDS_EXACT_DM 1   // depths 5-12 (threshold / full-p): one k_level_lds instantiation per depth
 #endif
+#ifndef PCG_LDS_COLSOLVE
+#define PCG_LDS_COLSOLVE 1   // k_level_lds beyond PCG_MAX_DEPTH: column-order forward solve (n = 1000 unlimited
+                             // depth: depths 13-16 5 % faster; at depth 9 it cost 30 %, so only there)
+#endif
 #ifndef PCG_LDS_DEEP_TOP
 #define PCG_LDS_DEEP_TOP 20   // k_level_lds instantiations beyond PCG_MAX_DEPTH (threshold mode), <= 20
 #endif
@@ -1566,17 +1570,40 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
                 double p = 0.0;
                 if (ok) {
                     const double *Mt = M + t * D;
-                    double vv = 0.0, uv = 0.0, v[DM];
+                    double vv = 0.0, uv = 0.0;
+                    if constexpr (PCG_LDS_COLSOLVE && DM > PCG_MAX_DEPTH) {
+                        // the forward solve column by column: step q finishes v_q and updates every
+                        // later row's partial sum, so the d - q - 1 updates of a step are
+                        // independent (the row-by-row form gave the scheduler one dependent fp64
+                        // chain at the one wave per SIMD of the deep instantiations). Each row's
+                        // sum subtracts the same products in the same order: identical results.
+                        double tt[DM];
     #pragma unroll
-                    for (int i = 0; i < DM; ++i) {
-                        if (i < d) {
-                            double tt = Mt[k[i]];
+                        for (int i = 0; i < DM; ++i) tt[i] = i < d ? Mt[k[i]] : 0.0;
     #pragma unroll
-                            for (int q = 0; q < DM; ++q)
-                                if (q < i) tt -= L[i][q] * v[q];
-                            v[i] = tt * rinv[i];
-                            vv += v[i] * v[i];
-                            uv += u[i] * v[i];
+                        for (int q = 0; q < DM; ++q) {
+                            if (q < d) {
+                                const double vq = tt[q] * rinv[q];
+                                vv += vq * vq;
+                                uv += u[q] * vq;
+    #pragma unroll
+                                for (int i = q + 1; i < DM; ++i)
+                                    if (i < d) tt[i] -= L[i][q] * vq;
+                            }
+                        }
+                    } else {
+                        double v[DM];
+    #pragma unroll
+                        for (int i = 0; i < DM; ++i) {
+                            if (i < d) {
+                                double tt = Mt[k[i]];
+    #pragma unroll
+                                for (int q = 0; q < DM; ++q)
+                                    if (q < i) tt -= L[i][q] * v[q];
+                                v[i] = tt * rinv[i];
+                                vv += v[i] * v[i];
+                                uv += u[i] * v[i];
+                            }
                         }
                     }
                     dec = decide<MODE>(a, Mx[t] - uv, cxx, Md[t] - vv, a.tau / gmin, &p);
