@@ -1315,6 +1315,10 @@ __device__ __forceinline__ int colex_elem(int ii, R rr, int hi, const TAB *tab, 
 #define PCG_LDS_COLSOLVE 1   // k_level_lds beyond PCG_MAX_DEPTH: column-order forward solve (n = 1000 unlimited
                              // depth: depths 13-16 5 % faster; at depth 9 it cost 30 %, so only there)
 #endif
+#ifndef PCG_LDS_COLCHOL
+#define PCG_LDS_COLCHOL 0    // ... and the right-looking Cholesky there (same products, same order per entry;
+                             // measured slower: n = 1000 900 vs 850 ms, its upfront block load spills at d >= 18)
+#endif
 #ifndef PCG_LDS_DEEP_TOP
 #define PCG_LDS_DEEP_TOP 20   // k_level_lds instantiations beyond PCG_MAX_DEPTH (threshold mode), <= 20
 #endif
@@ -1520,6 +1524,39 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
             double L[DM][DM], rinv[DM], u[DM];
             bool ok = true;
             double gmin = 1.0;
+            double uu = 0.0;
+            if constexpr (PCG_LDS_COLSOLVE && DM > PCG_MAX_DEPTH && PCG_LDS_COLCHOL) {
+                // right-looking (column) order, as the forward solve below: step j finishes column j
+                // and updates the trailing entries and u's partial sums — independent updates, and
+                // every entry subtracts the same products in the same (ascending) order as the
+                // left-looking form: identical results
+                double tu[DM];
+    #pragma unroll
+                for (int i = 0; i < DM; ++i) {
+                    tu[i] = Mx[k[i]];
+    #pragma unroll
+                    for (int m = 0; m <= i; ++m) L[i][m] = M[k[i] * D + k[m]];
+                }
+    #pragma unroll
+                for (int j = 0; j < DM; ++j) {
+                    const double sj = L[j][j];
+                    ok = ok && (sj > 0.0);
+                    gmin = fmin(gmin, sj);
+                    const double ljj = sqrt(sj);
+                    rinv[j] = 1.0 / ljj;
+                    L[j][j] = ljj;
+                    u[j] = tu[j] * rinv[j];
+                    uu += u[j] * u[j];
+    #pragma unroll
+                    for (int i = j + 1; i < DM; ++i) L[i][j] = L[i][j] * rinv[j];
+    #pragma unroll
+                    for (int i = j + 1; i < DM; ++i) {
+                        tu[i] -= L[i][j] * u[j];
+    #pragma unroll
+                        for (int m = j + 1; m <= i; ++m) L[i][m] -= L[i][j] * L[m][j];
+                    }
+                }
+            } else {
     #pragma unroll
             for (int j = 0; j < DM; ++j) {
                 if (j < d) {
@@ -1544,7 +1581,6 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
                     }
                 }
             }
-            double uu = 0.0;
     #pragma unroll
             for (int i = 0; i < DM; ++i) {
                 if (i < d) {
@@ -1555,6 +1591,7 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
                     u[i] = t * rinv[i];
                     uu += u[i] * u[i];
                 }
+            }
             }
             const double cxx = Cxx - uu;
             ok = ok && (cxx == cxx);
