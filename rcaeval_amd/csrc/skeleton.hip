@@ -1308,12 +1308,24 @@ __device__ __forceinline__ int colex_elem(int ii, R rr, int hi, const TAB *tab, 
 // walks `spl` S ranks (stride = block size) so the staging is amortised over
 // spl * 256 * (D - d) tests. Sepset unions and removal flags accumulate in LDS (local bits)
 // and are flushed once per block.
+// 1/sqrt(x) in fp64 from the fp32 hardware estimate plus one Newton step (relative
+// error ~1e-14 for normal fp32-range x; x <= 0 or out of fp32 range gives inf / NaN, which the
+// callers' checks reject)
+__device__ __forceinline__ double rsq_nr(double x) {
+    const double r0 = (double)__builtin_amdgcn_rsqf((float)x);
+    return r0 * fma(-0.5 * x * r0, r0, 1.5);
+}
+
 #ifndef PCG_LDS_EXACT_DM
 #define PCG_LDS_EXACT_DM 1   // depths 5-12 (threshold / full-p): one k_level_lds instantiation per depth
 #endif
 #ifndef PCG_LDS_COLSOLVE
 #define PCG_LDS_COLSOLVE 1   // k_level_lds beyond PCG_MAX_DEPTH: column-order forward solve (n = 1000 unlimited
                              // depth: depths 13-16 5 % faster; at depth 9 it cost 30 %, so only there)
+#endif
+#ifndef PCG_LDS_RSQ
+#define PCG_LDS_RSQ 0        // k_level_lds beyond PCG_MAX_DEPTH: pivot reciprocals by rsq_nr (fewer VALU, but
+                             // measured slower: n = 1000 900 vs 850 ms — the allocation of depths 19-20 spills more)
 #endif
 #ifndef PCG_LDS_COLCHOL
 #define PCG_LDS_COLCHOL 0    // ... and the right-looking Cholesky there (same products, same order per entry;
@@ -1566,9 +1578,17 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
                         if (q < j) s -= L[j][q] * L[j][q];
                     ok = ok && (s > 0.0);
                     gmin = fmin(gmin, s);
-                    const double ljj = sqrt(s);
-                    rinv[j] = 1.0 / ljj;
-                    L[j][j] = ljj;
+                    if constexpr (DM > PCG_MAX_DEPTH && PCG_LDS_RSQ) {
+                        // threshold mode only: 1 / sqrt by the fp32 estimate + one Newton step
+                        // (1e-14 relative, far inside the +-1e-6 band) instead of an IEEE sqrt and
+                        // divide; a pivot below 1e-30 is clamped, and its tiny gmin keeps every
+                        // test of the set off the decision (guard tau / gmin), so it goes exact
+                        rinv[j] = rsq_nr(fmax(s, 1e-30));
+                    } else {
+                        const double ljj = sqrt(s);
+                        rinv[j] = 1.0 / ljj;
+                        L[j][j] = ljj;
+                    }
     #pragma unroll
                     for (int i = 0; i < DM; ++i) {
                         if (i > j && i < d) {
@@ -2425,13 +2445,6 @@ constexpr double F32_U = 5.9604644775390625e-08;   // 2^-24
 #endif
 __host__ __device__ constexpr int tgf_minblocks(int DM) { return DM == 2 ? PCG_MBF2 : (DM == 3 ? PCG_MBF3 : PCG_MBF4); }
 
-// 1/sqrt(x) in fp64 from the fp32 hardware estimate plus one Newton step (relative
-// error ~1e-14 for normal fp32-range x; x <= 0 or out of fp32 range gives inf / NaN, which the
-// callers' checks reject)
-__device__ __forceinline__ double rsq_nr(double x) {
-    const double r0 = (double)__builtin_amdgcn_rsqf((float)x);
-    return r0 * fma(-0.5 * x * r0, r0, 1.5);
-}
 
 // (x, y | S) in fp64 from the C in HBM (Cholesky of C_SS, the fp64 kernels' guard and band):
 // 0 dependent, 1 independent, 2 exact path
