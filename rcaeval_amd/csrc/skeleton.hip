@@ -3883,8 +3883,9 @@ __global__ __launch_bounds__(64) void k_level_deep(LevelArgs a, double *scratch,
 }
 
 // ---------------------------------------------------------------------------------------
-// Deep levels (d >= PCG_WAVE_LO, default 13; the reference's unlimited-depth loop reaches them on
-// sparse graphs, SkeletonDiscovery.py:72), narrow nodes (D <= WAVE_MAXD), threshold / full-p
+// Deep levels (full-p mode from d = 13, threshold mode beyond the per-lane k_level_lds — see
+// use_wave; PCG_WAVE_LO forces it from a given depth; the reference's unlimited-depth loop reaches
+// them on sparse graphs, SkeletonDiscovery.py:72), narrow nodes (D <= WAVE_MAXD), threshold / full-p
 // modes: ONE WAVE PER CONDITIONING SET S, lanes = the columns of the node block — lane t < D
 // the neighbour t, lane D the node x itself. Every lane forward-solves its own column,
 //   v_c = L^-1 C[S, c],   L = chol(C_SS),
@@ -5385,7 +5386,7 @@ uint64_t tgroup_tasks(const pcg_handle *h, int D, int d) {
 // p-values the caller can observe; k_level_lds_t routes recorded pairs there)
 bool use_tgroup(int mode, int d) { return (mode == MODE_DECIDE || mode == MODE_FULLP) && d >= 2 && d <= 4; }
 // depths whose narrow class runs k_level_wave (one wave per conditioning set); PCG_WAVE_LO
-// overrides the first such depth (A/B knob)
+// sets the first such depth for every mode (A/B knob)
 // k_level_wave_pr (the factorisation shared between consecutive sets) instead of k_level_wave;
 // PCG_WAVE_PR=0: the per-set factorisation (A/B knob, read per launch)
 bool wave_pr() {
