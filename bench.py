@@ -59,24 +59,55 @@ def _issue_model(kernel: str):
     return (m if m.get("kernel") == kernel else None), os.path.basename(f)
 
 
+# The guide's VALU issue cost of one wave64 instruction on a SIMD-32 with other waves to interleave
+# (MI355X_MICROARCH.md:54,473: a non-packed FP32 / INT32 VALU occupies the SIMD 2 cycles; packed
+# FP32 and FP64 4; transcendentals 8)
+TRANSCENDENTAL = ("v_exp_", "v_log_", "v_rcp_", "v_rsq_", "v_sqrt_", "v_sin_", "v_cos_")
+
+
+def guide_cycles(op: str) -> float:
+    if op.startswith(TRANSCENDENTAL):
+        return 8.0
+    if op.startswith("v_pk_") or "f64" in op or op.startswith(("v_lshl_add_u64", "v_mad_u64", "v_mad_i64")):
+        return 4.0
+    return 2.0
+
+
+def guide_issue_cycles(model: dict) -> float:
+    """SIMD-cycles of the kernel's dynamic VALU instruction mix at the guide's issue costs: every
+    PMC class count of every region split over its opcodes in the proportions of the region's own
+    ISA (as tools/roofline_model.py splits them), each opcode at guide_cycles."""
+    tot = 0.0
+    for reg in model["regions"].values():
+        for cls in reg["classes"].values():
+            ops = cls.get("isa_static") or {}
+            n_static = sum(ops.values())
+            if not n_static:
+                tot += 2.0 * cls["dynamic"]
+                continue
+            tot += cls["dynamic"] * sum(c * guide_cycles(op) for op, c in ops.items()) / n_static
+    return tot
+
+
 def roofline_of(kernel: str, tests: int, d: int, k_ms: float) -> dict:
     """Roofline of the dominant CI-test kernel.
 
     Binding resource: VALU issue. The kernel stages each node's correlation block in LDS, so
     its HBM traffic (PMC) is far below SURVEY §8(d)'s per-test byte model and HBM is not what
-    binds. achieved = the SIMD-cycles its VALU instructions need to issue, per launch ÷ the
-    live kernel time; peak = 1024 SIMDs × 2.4 GHz; frac = achieved / peak.
+    binds. achieved = the SIMD-cycles its VALU instructions need to issue at the GUIDE's rates,
+    per launch ÷ the live kernel time; peak = 1024 SIMDs × 2.4 GHz; frac = achieved / peak.
 
-    The SIMD-cycles per launch come from the committed issue-cost model
-    (profiles/r*_roofline_model.json, tools/roofline_model.py): the PMC class counters of this
-    kernel on this bench command (SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_{F32,F64}, _INT32, _INT64,
-    _CVT, SQ_INSTS_VALU for the rest), each class split over its opcodes in the proportions of
-    the kernel's ISA, times the wall-clock cycles of those opcodes measured by
-    tools/micro/issue_cost.hip at the kernel's occupancy (profiles/r03_issue_cost.json). The
-    model's bounds (every class at its cheapest / dearest opcode) ride along as frac_bounds."""
+    The instruction mix is the committed model's (profiles/r*_roofline_model.json,
+    tools/roofline_model.py): the PMC class counters of this kernel on this bench command
+    (SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_{F32,F64}, _INT32, _INT64, _CVT, SQ_INSTS_VALU for the
+    rest), each class split over its opcodes in the proportions of the kernel's ISA. Costed at
+    the guide's issue cycles (guide_cycles: 2 non-packed, 4 packed / fp64, 8 transcendental) that
+    gives `frac`; costed at the cycles tools/micro/issue_cost.hip MEASURED for those opcodes at the
+    kernel's occupancy (VOP3 v_fma_f32 with its sources in one VGPR bank 4.56, packed 4.6 —
+    profiles/r03_issue_cost.json) it gives `frac_model`, with that model's bounds."""
     peak_gcyc = 1024 * 2.4   # G SIMD-cycles/s
-    line = {"bound": "valu", "unit": "G SIMD-cycles/s (VALU issue)", "peak": peak_gcyc, "achieved": None,
-            "frac": None, "traffic": None, "kernel": kernel, "kernel_ms": k_ms}
+    line = {"bound": "valu", "unit": "G SIMD-cycles/s (VALU issue at the guide's rates)", "peak": peak_gcyc,
+            "achieved": None, "frac": None, "traffic": None, "kernel": kernel, "kernel_ms": k_ms}
     alg = tests * bytes_per_test(d)
     sec = {"hbm_contract_bytes_per_test": bytes_per_test(d),
            "hbm_contract_gbs": alg / (k_ms / 1e3) / 1e9 if k_ms > 0 else None,
@@ -84,11 +115,14 @@ def roofline_of(kernel: str, tests: int, d: int, k_ms: float) -> dict:
     model, msrc = _issue_model(kernel)
     line["model_source"] = msrc
     if k_ms > 0 and model:
+        gcyc = guide_issue_cycles(model)
+        line["achieved"] = gcyc / (k_ms / 1e3) / 1e9
+        line["frac"] = line["achieved"] / peak_gcyc
+        line["guide_issue_cycles_per_launch"] = gcyc
         cyc = float(model["valu_issue_cycles"])
         lo, hi = (float(v) for v in model["valu_issue_cycles_bounds"])
-        line["achieved"] = cyc / (k_ms / 1e3) / 1e9
-        line["frac"] = line["achieved"] / peak_gcyc
-        line["frac_bounds"] = [lo / (k_ms / 1e3) / 1e9 / peak_gcyc, hi / (k_ms / 1e3) / 1e9 / peak_gcyc]
+        line["frac_model"] = cyc / (k_ms / 1e3) / 1e9 / peak_gcyc
+        line["frac_model_bounds"] = [lo / (k_ms / 1e3) / 1e9 / peak_gcyc, hi / (k_ms / 1e3) / 1e9 / peak_gcyc]
         line["valu_issue_cycles_per_launch"] = cyc
         line["valu_instructions_per_launch"] = model["valu_instructions"]
         line["mean_cycles_per_valu"] = model["mean_cycles_per_valu"]
@@ -117,13 +151,12 @@ CRT_MODULI = (256, 255, 253, 251, 247, 241, 239, 233, 229, 227, 223, 217, 211, 1
 CRT_TILE = 256
 
 
-def k1_crt_moduli(n: int, N: int):
+def k1_crt_moduli(n: int, N: int, tune: dict):
     """(k, b) of corr.hip's crt_plan, or None when K1 takes the digit / fp64 path: the fewest
-    moduli whose product M leaves b >= PCG_K1_CRT_BITS bits per value with M > 2 N 4^b."""
-    if (os.environ.get("PCG_K1_I8", "1") == "0" or os.environ.get("PCG_K1_CRT", "1") == "0"
-            or n < int(os.environ.get("PCG_K1_CRT_MINN", "256"))):
+    moduli whose product M leaves b >= PCG_TUNE_K1_CRT_BITS bits per value with M > 2 N 4^b."""
+    if not tune["K1_I8"] or not tune["K1_CRT"] or n < tune["K1_CRT_MINN"]:
         return None
-    bmin = int(os.environ.get("PCG_K1_CRT_BITS", "56"))
+    bmin = tune["K1_CRT_BITS"]
     lm = 0.0
     for k, m in enumerate(CRT_MODULI, 1):
         lm += math.log2(m)
@@ -133,15 +166,15 @@ def k1_crt_moduli(n: int, N: int):
     return None
 
 
-def k1_roofline(n: int, N: int, corr_ms: float) -> dict:
+def k1_roofline(n: int, N: int, corr_ms: float, tune: dict) -> dict:
     """K1 (np.corrcoef). Default path for n >= 256 (corr.hip, CRT): the centred X truncated to
     b-bit integers, k residue planes, the Gram as k exact int8 GEMMs of the upper-triangle
     256-square tiles on v_mfma_i32_32x32x32_i8, rebuilt by the Chinese remainder theorem;
     executed int8 ops = k x 2 x T(T+1)/2 x 256^2 x N_pad. Below n = 256: 9 digit planes and 45
     GEMMs of 64-square tiles. The fp64 path (PCG_K1_I8=0) runs v_mfma_f64_16x16x4_f64 on 64-square
     tiles. Either way the algorithmic work is 2 N n^2 (reported as achieved_algorithmic, TFLOP/s)."""
-    i8 = os.environ.get("PCG_K1_I8", "1") != "0"
-    crt = k1_crt_moduli(n, N)
+    i8 = bool(tune["K1_I8"])
+    crt = k1_crt_moduli(n, N, tune)
     npad = (N + 63) // 64 * 64
     line = {"bound": "mfma", "ms": corr_ms, "path": "int8 CRT" if crt else ("int8 digits" if i8 else "fp64"),
             "achieved_algorithmic_tflops": 2.0 * N * n * n / (corr_ms / 1e3) / 1e12,
@@ -169,18 +202,15 @@ def k1_roofline(n: int, N: int, corr_ms: float) -> dict:
     return line
 
 
-def dominant_kernel(d: int, full_p: bool) -> str:
+def dominant_kernel(d: int, full_p: bool, screen_mask: int = -1) -> str:
     """Name (as rocprofv3 prints it, template args kept) of the CI-test kernel that runs
     depth ``d`` for nodes of degree <= 64 — the host dispatch in skeleton.hip
     (``use_tgroup``: threshold mode at depths 2..4 uses the T-group kernel; ``use_screen32``:
-    its fp32-screened form k_level_lds_f at the depths of PCG_TG_F32 / PCG_SCREEN_MASK)."""
+    its fp32-screened form k_level_lds_f at the depths of PCG_TG_F32 / PCG_TUNE_SCREEN_MASK)."""
     if d == 0:
         return f"k_level0<{1 if full_p else 0}>"
     if 2 <= d <= 4:   # (full-p mode runs the T-group sweeps too, since round 4)
-        mask = int(os.environ.get("PCG_SCREEN_MASK", "0x18"), 0)
-        sp = int(os.environ.get("PCG_SP", "0"), 0)
-        if (mask >> d) & 1 and (sp >> d) & 1 and d in (3, 4):
-            return f"k_level_sp<{d}>"
+        mask = 0x18 if screen_mask < 0 else screen_mask
         if (mask >> d) & 1:   # k_level_lds_f<d, WIDE, REC>: REC = the record-routing build
             return f"k_level_lds_f<{d}, false, false>"
         return f"k_level_lds_t<{d}, false>"
@@ -480,7 +510,7 @@ def main():
     # dominant kernel: the CI-test kernel of the deepest, largest level
     dmax = int(np.argmax(st["tests"]))
     k_ms = st["kernel_ms"][dmax]
-    kname = dominant_kernel(dmax, args.full_p)
+    kname = dominant_kernel(dmax, args.full_p, eng.get_tuning("SCREEN_MASK"))
     roof = roofline_of(kname, int(st["tests"][dmax]), dmax, k_ms)
     if world == 1:      # K1 alone (for its roofline), outside the timed steps
         for _ in range(4):
@@ -492,12 +522,14 @@ def main():
         corr_med = float(np.median([1000 * t for n_, t in phases if n_ == "corr"][1:]))
     else:
         corr_med = float(np.median([1000 * t for n_, t in phases if n_ == "corr"][args.warmup:] or [0.0]))
-    roof["k1"] = k1_roofline(args.n, args.samples, corr_med) if corr_med > 0 else None
+    k1_tune = {k: eng.get_tuning(k) for k in ("K1_I8", "K1_CRT", "K1_CRT_MINN", "K1_CRT_BITS")}
+    roof["k1"] = k1_roofline(args.n, args.samples, corr_med, k1_tune) if corr_med > 0 else None
 
-    # the full-p mode (PCG_FLAG_FULL_P | PCG_FLAG_RECORD) after the timed steps: the same skeleton
-    # with the reference-arithmetic p of every test of a 1-in-4099 pair sample recorded (the
+    # the p-value mode (PCG_FLAG_FULL_P | PCG_FLAG_RECORD) after the timed steps: the same skeleton
+    # with the reference-arithmetic p of every test of a 1-in-4099 pair SAMPLE recorded (the
     # parity test's sample; the exact path computes those p with numpy.linalg.inv's LU), the
-    # threshold decisions elsewhere. Twice: the first call sizes the exact-path list
+    # threshold decisions elsewhere — NOT every test's p (pcgpu.h PCG_FLAG_FULL_P). Twice: the
+    # first call sizes the exact-path list
     full_p = None
     if not args.full_p and not args.no_full_p and world == 1:
         progress("full-p comparison run")
@@ -508,7 +540,9 @@ def main():
                              record_capacity=4_000_000, record_sample=(4099, 17))
         fp_ms = float(sum(o.stats["level_ms"]))
         same = bool(np.array_equal(o.removed_level, out.removed_level)) and o.stats["tests"] == st["tests"]
-        full_p = {"skeleton_device_ms": fp_ms, "tests_per_s": sum(o.stats["tests"]) / (fp_ms / 1e3),
+        full_p = {"what": "sampled records: the reference p of every test of a 1-in-4099 pair sample, "
+                          "threshold decisions elsewhere (not every test's p)",
+                  "skeleton_device_ms": fp_ms, "tests_per_s": sum(o.stats["tests"]) / (fp_ms / 1e3),
                   "flags": "FULL_P|RECORD, record_sample=(4099, 17)", "records": int(len(o.records)),
                   "kernel_ms_per_level": [round(v, 3) for v in o.stats["kernel_ms"]],
                   "level_ms": [round(v, 3) for v in o.stats["level_ms"]],
@@ -535,7 +569,7 @@ def main():
             "level_ms": [round(v, 3) for v in st["level_ms"]],
             "edges_after": st["edges_after"], "exact_path": st["exact"], "screened": st["screened"], "near_alpha": st["near_alpha"],
             "roofline": roof,
-            "full_p": full_p,
+            "sampled_records": full_p,
         }
         if not args.no_cpu_baseline and world == 1:
             progress("CPU baseline")

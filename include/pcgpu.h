@@ -45,11 +45,15 @@ extern "C" {
                                 every rank leaves the level loop at the same depth         */
 
 /* skeleton flags */
-#define PCG_FLAG_FULL_P 0x1   /* compute the Fisher-z p-value of every test (reference
-                                 arithmetic); default decides p > alpha through the
-                                 monotone |r| threshold and computes p only in the
-                                 +-1e-6 band around it (identical decisions)            */
-#define PCG_FLAG_RECORD 0x2   /* record (a, b, S, p) of every unique test (parity runs) */
+#define PCG_FLAG_FULL_P 0x1   /* the p-value mode of the reference arithmetic: every p a caller
+                                 can observe is the reference expression's (records, the
+                                 near-alpha list). Decisions stay on the monotone |r|
+                                 threshold; the +-1e-6 band around it and every test of a
+                                 recorded pair go to the exact path, which computes the
+                                 reference p (LU like numpy.linalg.inv). Without records,
+                                 only the band tests get a p (identical decisions either way) */
+#define PCG_FLAG_RECORD 0x2   /* record (a, b, S, p) of every unique test (parity runs), or of
+                                 the pcg_set_record_sample pairs; implies FULL_P            */
 #define PCG_FLAG_EXACT_ALL 0x4 /* route every test through the LU (numpy.linalg.inv-like)
                                  exact path                                            */
 
@@ -75,7 +79,15 @@ typedef struct {
     int32_t levels;                    /* depths run                                        */
     int32_t error;                     /* 0 or PCG_ERR_SINGULAR / PCG_ERR_DOMAIN            */
     int64_t screened[PCG_MAX_LEVELS];  /* tests the fp32 sweep left to its fp64 screen      */
+    int32_t driver;                    /* which driver produced the result: PCG_DRIVER_*     */
+    int32_t driver_pad;
 } pcg_stats;
+
+/* pcg_stats.driver */
+#define PCG_DRIVER_LEVELS 0        /* the multi-kernel level loop                            */
+#define PCG_DRIVER_SMALL 1         /* the single-workgroup small-graph kernel (n <= 64)      */
+#define PCG_DRIVER_SMALL_RERUN 2   /* the small kernel stopped (deeper than its 16 levels or a
+                                      full band queue) and the level loop reran the skeleton */
 
 typedef struct {                       /* one unique CI test (PCG_FLAG_RECORD / near-alpha) */
     int32_t a, b;                      /* a < b                                             */
@@ -86,8 +98,9 @@ typedef struct {                       /* one unique CI test (PCG_FLAG_RECORD / 
 
 /* ---- ABI identity ------------------------------------------------------------------
  * Bumped whenever a struct above changes layout or an entry point changes signature.
- * Round 3: pcg_stats gained `screened` (v2 had no such field).                         */
-#define PCG_ABI_VERSION 3
+ * v3: pcg_stats gained `screened`. v4: pcg_stats gained `driver`; pcg_corr_shard_bytes takes
+ * the handle; pcg_set_tuning / pcg_get_tuning / pcg_k1_plan_signature added.            */
+#define PCG_ABI_VERSION 4
 /* Sizes of the structs this library writes through caller pointers, and its ABI version;
  * a binding checks them against its own declarations before the first call (host only, no
  * GPU needed). Any out pointer may be NULL.                                             */
@@ -108,6 +121,38 @@ int pcg_set_capacity(pcg_handle *h, int64_t record_capacity, int64_t deferred_ca
  * canonical pair (a < b) has (a*n + b) % modulus == residue; modulus 0 or 1 = every test.  */
 int pcg_set_record_sample(pcg_handle *h, int64_t modulus, int64_t residue);
 
+/* Tuning and testing knobs of one handle. No knob changes a result (every setting is covered
+ * by the parity tests); they choose kernels, launch shapes and thresholds. Defaults are read
+ * ONCE, in pcg_create, from the environment variable of the knob's name (e.g. PCG_SMALL=0),
+ * else the built-in value below; pcg_set_tuning overrides them per handle.             */
+#define PCG_TUNE_SMALL 0          /* 1: n <= 64 on the single-workgroup kernel; 0: level loop (1)  */
+#define PCG_TUNE_SMALL_QCAP 1     /* band tests per depth the small kernel queues, 1..1024 (1024);
+                                     a full queue ends the small run (PCG_DRIVER_SMALL_RERUN)      */
+#define PCG_TUNE_LDS_DEEP 2       /* threshold mode: deepest depth on the per-lane k_level_lds,
+                                     12..20 (20); deeper levels run one wave per set              */
+#define PCG_TUNE_LDS_SPILL_MIN 3  /* depths 17..20 take the per-lane kernel only for levels of at
+                                     least this many tests (10000000); below, one wave per set    */
+#define PCG_TUNE_WAVE_LO 4        /* >= 5: one wave per conditioning set from this depth on
+                                     (0 = the default split)                                     */
+#define PCG_TUNE_SCREEN_MASK 5    /* depths (bit 1 << d, d = 2..4) of the fp32-screened sweep;
+                                     -1 = pcg_set_screen_precision's choice (0x18)               */
+#define PCG_TUNE_NODE_BLOCKS 6    /* depths (bit 1 << d) that stage compact node blocks (0x10)    */
+#define PCG_TUNE_EXPORT_INLINE 7  /* graphs of at most this many CSR entries export their sepset
+                                     rows on the handle's stream (16384)                          */
+#define PCG_TUNE_NB 8             /* narrow-class blocks per depth and rank (0 = per-depth default) */
+#define PCG_TUNE_NBW 9            /* wide-class blocks per depth and rank (512)                    */
+#define PCG_TUNE_HOST_TRACE 10    /* 1: print the level loop's host timeline to stderr (0)         */
+#define PCG_TUNE_K1_I8 11         /* 1: K1 on the int8 matrix cores (1); 0: fp64 MFMA              */
+#define PCG_TUNE_K1_CRT 12        /* 1: the CRT residue K1 for n >= PCG_TUNE_K1_CRT_MINN (1)       */
+#define PCG_TUNE_K1_CRT_MINN 13   /* (256)                                                         */
+#define PCG_TUNE_K1_CRT_BITS 14   /* fewest bits kept per centred value, 32..63 (56)               */
+#define PCG_TUNE_K1_CRT_KS 15     /* CRT split-K slabs (0 = cost model)                            */
+#define PCG_TUNE_K1_I8_KS 16      /* digit-path split-K slabs (0 = default)                        */
+#define PCG_TUNE_K1_SUPER_ORDER 17 /* 1: digit-path tiles in super-rows (1); 0: row-major         */
+#define PCG_TUNE_COUNT 18
+int pcg_set_tuning(pcg_handle *h, int key, int64_t value);
+int pcg_get_tuning(pcg_handle *h, int key, int64_t *value);
+
 /* ---- K1: correlation -------------------------------------------------------------
  * Replaces FisherZ.__init__'s `np.corrcoef(data.T)` [U]: column means,
  * centred X^T X, *= 1/(N-1), /= s_i, /= s_j, clip to [-1, 1] (numpy's order). The Gram runs on
@@ -126,7 +171,11 @@ int pcg_corr(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx,
  * the same handle (it reads the column exponents pcg_corr_shard left there), which rebuilds,
  * mirrors and normalises: C is bitwise the single-GPU pcg_corr result for every world size.
  * pcg_corr_shard_rows: the digit / fp64 path's rows_per_rank (packed = rows x n doubles).     */
-int pcg_corr_shard_bytes(int64_t n, int64_t N, int world, int64_t *bytes_per_rank);
+int pcg_corr_shard_bytes(pcg_handle *h, int64_t n, int64_t N, int world, int64_t *bytes_per_rank);
+/* A signature of K1's plan for (n, N) under this handle's knobs (path; the CRT path's moduli,
+ * bits, split-K and unit count): ranks compare it before exchanging shards. h may be NULL
+ * (built-in defaults), also for pcg_corr_shard_bytes.                                      */
+int pcg_k1_plan_signature(pcg_handle *h, int64_t n, int64_t N, int64_t *signature);
 int pcg_corr_shard_rows(int64_t n, int world, int64_t *rows_per_rank);
 int pcg_corr_shard(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx, int rank,
                    int world, double *packed);

@@ -10,7 +10,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpcgpu.so")
+# PCG_LIB_PATH: an A/B build variant (tools/variant_bench.sh) loaded instead of the in-tree library,
+# so no script ever overwrites rcaeval_amd/libpcgpu.so
+LIB_PATH = os.environ.get("PCG_LIB_PATH") or os.path.join(_HERE, "libpcgpu.so")
 
 PCG_OK = 0
 PCG_ERR_INVALID = -1
@@ -27,10 +29,23 @@ PCG_FLAG_RECORD = 0x2
 PCG_FLAG_EXACT_ALL = 0x4
 
 PCG_MAX_LEVELS = 32
-PCG_ABI_VERSION = 3         # include/pcgpu.h; checked against the library by load()
+PCG_ABI_VERSION = 4         # include/pcgpu.h; checked against the library by load()
 PCG_RM_STATUS = 64          # status bytes after the n*n removal flags (pcgpu.h)
 PCG_MAX_DEPTH = 12
 PCG_MAX_LEVEL_DEPTH = 30
+
+# pcg_stats.driver
+PCG_DRIVER_LEVELS = 0
+PCG_DRIVER_SMALL = 1
+PCG_DRIVER_SMALL_RERUN = 2
+DRIVER_NAMES = {PCG_DRIVER_LEVELS: "levels", PCG_DRIVER_SMALL: "small", PCG_DRIVER_SMALL_RERUN: "small_rerun"}
+
+# pcg_set_tuning keys (include/pcgpu.h PCG_TUNE_*), by their environment names without "PCG_"
+TUNE_KEYS = {
+    "SMALL": 0, "SMALL_QCAP": 1, "LDS_DEEP": 2, "LDS_SPILL_MIN": 3, "WAVE_LO": 4, "SCREEN_MASK": 5,
+    "NODE_BLOCKS": 6, "EXPORT_INLINE": 7, "NB": 8, "NBW": 9, "HOST_TRACE": 10, "K1_I8": 11, "K1_CRT": 12,
+    "K1_CRT_MINN": 13, "K1_CRT_BITS": 14, "K1_CRT_KS": 15, "K1_I8_KS": 16, "K1_SUPER_ORDER": 17,
+}
 
 I64 = ctypes.c_int64
 I32 = ctypes.c_int32
@@ -52,6 +67,8 @@ class PcgStats(ctypes.Structure):
         ("levels", I32),
         ("error", I32),
         ("screened", I64 * PCG_MAX_LEVELS),
+        ("driver", I32),
+        ("driver_pad", I32),
     ]
 
     def as_dict(self) -> dict:
@@ -69,6 +86,7 @@ class PcgStats(ctypes.Structure):
             "level_ms": list(self.level_ms[:L]),
             "kernel_ms": list(self.kernel_ms[:L]),
             "screened": list(self.screened[:L]),
+            "driver": DRIVER_NAMES.get(self.driver, str(self.driver)),
         }
 
 
@@ -85,9 +103,12 @@ SIGNATURES = [
     ("pcg_set_stream", I32, [P, P]),
     ("pcg_set_capacity", I32, [P, I64, I64]),
     ("pcg_set_record_sample", I32, [P, I64, I64]),
+    ("pcg_set_tuning", I32, [P, ctypes.c_int, I64]),
+    ("pcg_get_tuning", I32, [P, ctypes.c_int, ctypes.POINTER(I64)]),
+    ("pcg_k1_plan_signature", I32, [P, I64, I64, ctypes.POINTER(I64)]),
     ("pcg_corr", I32, [P, P, I64, I64, I64, P, I64]),
     ("pcg_corr_shard_rows", I32, [I64, ctypes.c_int, ctypes.POINTER(I64)]),
-    ("pcg_corr_shard_bytes", I32, [I64, I64, ctypes.c_int, ctypes.POINTER(I64)]),
+    ("pcg_corr_shard_bytes", I32, [P, I64, I64, ctypes.c_int, ctypes.POINTER(I64)]),
     ("pcg_corr_shard", I32, [P, P, I64, I64, I64, ctypes.c_int, ctypes.c_int, P]),
     ("pcg_corr_shard_finish", I32, [P, P, I64, I64, ctypes.c_int, P, I64]),
     ("pcg_skeleton", I32, [P, P, I64, I64, I64, D, ctypes.c_int, ctypes.c_int, P, ctypes.POINTER(PcgStats)]),

@@ -1,6 +1,8 @@
 // api.hip — handle lifetime, error reporting and scratch management of libpcgpu.so.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "handle.h"
@@ -65,6 +67,56 @@ extern "C" int pcg_abi_info(int64_t *stats_bytes, int64_t *record_bytes, int32_t
     return PCG_OK;
 }
 
+namespace {
+struct TuneSpec {
+    const char *env;
+    int64_t dflt, lo, hi;
+};
+// the knobs of pcgpu.h (PCG_TUNE_*): environment name, built-in value, accepted range
+const TuneSpec kTune[PCG_TUNE_COUNT] = {
+    {"PCG_SMALL", 1, 0, 1},
+    {"PCG_SMALL_QCAP", 1024, 1, 1024},
+    {"PCG_LDS_DEEP", 20, 12, 20},
+    {"PCG_LDS_SPILL_MIN", 10000000, 0, INT64_MAX},
+    {"PCG_WAVE_LO", 0, 0, PCG_MAX_LEVEL_DEPTH + 1},
+    {"PCG_SCREEN_MASK", -1, -1, 0x1c},
+    {"PCG_NODE_BLOCKS", 0x10, 0, 0x1c},
+    {"PCG_EXPORT_INLINE", 16384, 0, INT64_MAX},
+    {"PCG_NB", 0, 0, 1 << 24},
+    {"PCG_NBW", 512, 1, 1 << 24},
+    {"PCG_HOST_TRACE", 0, 0, 1},
+    {"PCG_K1_I8", 1, 0, 1},
+    {"PCG_K1_CRT", 1, 0, 1},
+    {"PCG_K1_CRT_MINN", 256, 1, 1 << 24},
+    {"PCG_K1_CRT_BITS", 56, 32, 63},
+    {"PCG_K1_CRT_KS", 0, 0, 16},
+    {"PCG_K1_I8_KS", 0, 0, 256},
+    {"PCG_K1_SUPER_ORDER", 1, 0, 1},
+};
+}  // namespace
+
+void pcg_tuning_defaults(int64_t *tune) {
+    for (int k = 0; k < PCG_TUNE_COUNT; ++k) {
+        int64_t v = kTune[k].dflt;
+        if (const char *e = getenv(kTune[k].env)) v = strtoll(e, nullptr, 0);   // read once, at pcg_create
+        tune[k] = std::min(std::max(v, kTune[k].lo), kTune[k].hi);
+    }
+}
+
+extern "C" int pcg_set_tuning(pcg_handle *h, int key, int64_t value) {
+    if (!h || key < 0 || key >= PCG_TUNE_COUNT || value < kTune[key].lo || value > kTune[key].hi)
+        return pcg_fail(h, PCG_ERR_INVALID, "pcg_set_tuning: key %d value %lld", key, (long long)value);
+    h->tune[key] = value;
+    return PCG_OK;
+}
+
+extern "C" int pcg_get_tuning(pcg_handle *h, int key, int64_t *value) {
+    if (!h || !value || key < 0 || key >= PCG_TUNE_COUNT)
+        return pcg_fail(h, PCG_ERR_INVALID, "pcg_get_tuning: key %d", key);
+    *value = h->tune[key];
+    return PCG_OK;
+}
+
 extern "C" int pcg_create(int device, pcg_handle **out) {
     if (!out) return PCG_ERR_INVALID;
     *out = nullptr;
@@ -74,6 +126,7 @@ extern "C" int pcg_create(int device, pcg_handle **out) {
     if (hipSetDevice(device) != hipSuccess) return PCG_ERR_HIP;
     pcg_handle *h = new pcg_handle();
     h->device = device;
+    pcg_tuning_defaults(h->tune);
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         delete h;
         return PCG_ERR_HIP;
@@ -98,11 +151,10 @@ extern "C" int pcg_destroy(pcg_handle *h) {
                       &h->ug2[1], &h->exp_ctr, &h->cpre, &h->binom, &h->ctr,
                       &h->deferred, &h->screenq, &h->records, &h->nearbuf, &h->exportbuf, &h->export_xy, &h->diag,
                       &h->colmean, &h->pr_scratch, &h->batch_scratch, &h->chisq_scratch, &h->cblk, &h->lmk,
-                      &h->k1_digits, &h->small_sum, &h->gbar, &h->spl_buf};
+                      &h->k1_digits, &h->small_sum};
     for (DevBuf *b : bufs)
         if (b->p) hipFree(b->p);
-    PinBuf *pins[] = {&h->ctr_pin, &h->deg_pin, &h->off_pin, &h->cpre_pin, &h->status_pin, &h->tab_pin[0],
-                      &h->tab_pin[1], &h->small_pin};
+    PinBuf *pins[] = {&h->ctr_pin, &h->deg_pin, &h->off_pin, &h->cpre_pin, &h->status_pin, &h->small_pin};
     for (PinBuf *b : pins)
         if (b->p) hipHostFree(b->p);
     if (h->summary) hipHostFree(h->summary);
@@ -113,8 +165,6 @@ extern "C" int pcg_destroy(pcg_handle *h) {
     for (auto &pr : h->rev)
         for (auto &e : pr)
             if (e) hipEventDestroy(e);
-    for (hipEvent_t &e : h->k1ev)
-        if (e) hipEventDestroy(e);
     if (h->ev_fork) hipEventDestroy(h->ev_fork);
     if (h->ev_join) hipEventDestroy(h->ev_join);
     if (h->aux) hipStreamDestroy(h->aux);

@@ -357,7 +357,7 @@ extern "C" int pcg_corr_sharded(pcg_handle *h, const double *X, int64_t N, int64
     int rc = need_comm(h);
     if (rc) return rc;
     int64_t bytes = 0;
-    rc = pcg_corr_shard_bytes(n, N, h->comm_world, &bytes);
+    rc = pcg_corr_shard_bytes(h, n, N, h->comm_world, &bytes);
     if (rc) return pcg_fail(h, rc, "pcg_corr_shard_bytes");   // a function of (n, N, world): every rank agrees
     const size_t per = (size_t)bytes / sizeof(double);
     // buffer growth is the same decision on every rank (same n, world, call history); when it
@@ -378,7 +378,7 @@ extern "C" int pcg_corr_sharded(pcg_handle *h, const double *X, int64_t N, int64
     // with different knobs would gather mismatched units, so its signature is agreed with the outcome
     const int local = pcg_corr_shard(h, X, N, n, ldx, h->comm_rank, h->comm_world, (double *)h->comm_packed.p);
     bool same = true;
-    const int g = agree_value(h, local != 0, k1_plan_signature(n, N), &same);
+    const int g = agree_value(h, local != 0, k1_plan_signature(h, n, N), &same);
     if (g) return agreed_failure(h, local, g, "sharded K1");
     if (!same) return pcg_fail(h, PCG_ERR_INVALID, "sharded K1: the ranks' K1 plans differ (PCG_K1_* environment)");
     PCG_NCCL(h, rccl().all_gather(h->comm_packed.p, h->comm_gathered.p, per, ncclFloat64, (ncclComm_t)h->comm,

@@ -527,7 +527,6 @@ static_assert(CRT_NS * CRT_KB * 16384 <= 160 * 1024 && CRT_NS >= 2 && CRT_NS <= 
 constexpr int CRT_STAGE = CRT_KB * 16384;  // bytes per stage: CRT_KB x (A, B) x 4 column blocks x 2 KB
 constexpr int CRT_MAXKB = 4095;            // k-blocks per slab: 4095 x 32 x 128^2 < 2^31
 constexpr int CRT_UNIT = CRT_T * CRT_T;    // residue bytes per (tile, modulus, slab)
-constexpr int CRT_MAXG = 4;                // modulus groups overlapping residues and GEMM (handle events)
 static const int kCrtModuli[CRT_KMAX] = {256, 255, 253, 251, 247, 241, 239, 233, 229, 227, 223, 217,
                                          211, 199, 197, 193, 191, 181, 179, 173, 167, 163, 157, 151};
 
@@ -853,154 +852,17 @@ __global__ __launch_bounds__(512, 1) void k_xtx_crt(const int8_t *R, int TB, int
         }
 }
 
-// The same unit with 4 waves as 2 x 2, each 128 x 128 (4 x 4 MFMA tiles, 256 int32 accumulators
-// in AGPRs, one wave per SIMD). Per k-block a wave reads 8 fragments (8 KB for the CU's four waves
-// x 4 = 32 KB) for 16 MFMAs, where the 2 x 4 form reads 48 KB for the same 64 MFMAs per CU: with
-// the 16 KB the DMA writes, 48 instead of 64 KB of LDS traffic per 512 MFMA cycles of each SIMD
-// (LDS peak 128 B per CU cycle: 73 % instead of 98 % of it). Measured slower, so off by default
-// (PCG_K1_CRT_W4=1): 0.49 vs 0.40 ms per launch at config 5, MFMA busy 37 vs 44 % — with one wave
-// per SIMD the stage barriers and DMA waits are no longer covered by the other wave
-// (SQ_WAIT_INST_ANY 48 % of wave cycles); the LDS traffic was not what bound the 8-wave form.
-// Bitwise equal results (test_corr_crt_split_invariant). Staging: one DMA instruction moves
-// 4 KB (256 threads x 16 B); q = 0 .. 4 CRT_KB - 1 of a stage is k-block q >> 2, side (q >> 1) & 1,
-// column blocks 2 (q & 1) + (tid >> 7), word tid & 127 -- the same LDS image as k_xtx_crt's.
-// Unit byte order: ((w * 4 + a) * 4 + b) * 1024 + lane * 16 + kk (crt_unit_offset<true>).
-__global__ __launch_bounds__(256, 1) void k_xtx_crt4(const int8_t *R, int TB, int64_t plane, int T, int ntiles, int ks,
-                                                   int kb, CrtTab tab, int64_t u0, int64_t nu, uint8_t *out) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    int64_t lin = blockIdx.x;
-    {   // XCD-contiguous runs: an XCD's resident blocks share the modulus and slab (all panels in its L2)
-        const int64_t per = gridDim.x / 8;
-        lin = (blockIdx.x % 8) * per + blockIdx.x / 8;
-        if (lin >= nu) return;
-    }
-    const int64_t u = u0 + lin;
-    const int t = (int)(u % ntiles);
-    const int64_t sm = u / ntiles;
-    const int mi = (int)(sm / ks), slab = (int)(sm % ks);
-    int bi, bj;
-    tile_of(t, T, bi, bj);
-    const int tb0 = slab * kb, tb1 = min(TB, tb0 + kb);
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int r = lane & 31, hh = lane >> 5;
-    const int wr = w >> 1, wc = w & 1;
-
-    v16i acc[4][4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-#pragma unroll
-            for (int q = 0; q < 16; ++q) acc[a][b][q] = 0;
-
-    const int8_t *Rm = R + (int64_t)mi * plane;
-    const int8_t *srcA = Rm + (int64_t)(bi * 4 + (tid >> 7)) * TB * 2048 + (tid & 127) * 16;
-    const int8_t *srcB = Rm + (int64_t)(bj * 4 + (tid >> 7)) * TB * 2048 + (tid & 127) * 16;
-    const int64_t cb2 = (int64_t)2 * TB * 2048;    // two column blocks on
-    const int nkb = tb1 - tb0;
-    const int ns = (nkb + CRT_KB - 1) / CRT_KB;
-    auto issue = [&](int sidx) {
-        if (sidx >= ns) return;
-        unsigned char *dst = smem + (sidx % CRT_NS) * CRT_STAGE + w * 1024;
-#pragma unroll
-        for (int q = 0; q < 4 * CRT_KB; ++q) {
-            // a partial last stage re-reads its last k-block (fixed DMA count per stage)
-            const int64_t tb = tb0 + min(sidx * CRT_KB + (q >> 2), nkb - 1);
-            const int8_t *src = (((q >> 1) & 1) ? srcB : srcA) + ((q & 1) ? cb2 : 0) + tb * 2048;
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                             (__attribute__((address_space(3))) void *)(dst + q * 4096), 16, 0, 0);
-        }
-    };
-#pragma unroll
-    for (int sidx = 0; sidx < CRT_NS - 1; ++sidx) issue(sidx);
-    const unsigned char *fa = smem + (2 * wr * 2048 + hh * 1024 + r * 16);
-    const unsigned char *fb = smem + (8192 + 2 * wc * 2048 + hh * 1024 + r * 16);
-    for (int sidx = 0; sidx < ns; ++sidx) {
-        const int ahead = min(CRT_NS - 2, ns - 1 - sidx);
-        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * 4 * CRT_KB) : "memory");
-        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * CRT_KB) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        issue(sidx + CRT_NS - 1);
-        const int off = (sidx % CRT_NS) * CRT_STAGE;
-        v4i af[2][4], bf[2][4];
-        auto frag = [&](int kk, int sl) {
-#pragma unroll
-            for (int a = 0; a < 4; ++a)
-                af[sl][a] = *reinterpret_cast<const v4i *>(fa + off + kk * 16384 + (a >> 1) * 2048 + (a & 1) * 512);
-#pragma unroll
-            for (int b = 0; b < 4; ++b)
-                bf[sl][b] = *reinterpret_cast<const v4i *>(fb + off + kk * 16384 + (b >> 1) * 2048 + (b & 1) * 512);
-        };
-        const int cnt = min(CRT_KB, nkb - sidx * CRT_KB);
-        frag(0, 0);
-#pragma unroll
-        for (int kk = 0; kk < CRT_KB; ++kk) {
-            if (kk < cnt) {
-                const bool nxt = kk + 1 < CRT_KB && kk + 1 < cnt;
-                if (nxt) frag(kk + 1, (kk + 1) & 1);
-#pragma unroll
-                for (int a = 0; a < 4; ++a)
-#pragma unroll
-                    for (int b = 0; b < 4; ++b)
-                        acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[kk & 1][a], bf[kk & 1][b], acc[a][b], 0,
-                                                                          0, 0);
-                if (PCG_CRT_SCHED && nxt) {
-                    // the 8 fragment reads of k-block kk + 1 between the first 8 of kk's 16 MFMAs
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
-                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // 1 DS read
-                    }
-                    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-                }
-            }
-        }
-    }
-    const int m = tab.m[mi];
-    const double dm = (double)m, dinv = tab.dinv[mi];
-    uint8_t *o = out + lin * CRT_UNIT + (int64_t)w * 16384 + lane * 16;
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            v4i pk = {0, 0, 0, 0};
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int v = acc[a][b][q];
-                uint32_t rr;
-                if (m == 256) {
-                    rr = (uint32_t)v & 255u;
-                } else {
-                    const double d = (double)v;
-                    int x = (int)fma(floor(d * dinv), -dm, d);
-                    x += x < 0 ? m : 0;
-                    x -= x >= m ? m : 0;
-                    rr = (uint32_t)x;
-                }
-                pk[q >> 2] |= (int)(rr << (8 * (q & 3)));
-            }
-            *reinterpret_cast<v4i *>(o + (a * 4 + b) * 1024) = pk;
-        }
-}
-
-// byte offset of entry (li, lj) of a unit (the lane order of k_xtx_crt's epilogue; W4:
-// k_xtx_crt4's)
-template <bool W4>
+// byte offset of entry (li, lj) of a unit (the lane order of k_xtx_crt's epilogue)
 __device__ __forceinline__ int crt_unit_offset(int li, int lj) {
     const int wr = li >> 7, a = (li >> 5) & 3, rr = li & 31;
     const int hh = (rr >> 2) & 1, q = (rr & 3) | ((rr >> 3) << 2);
-    if (W4) {
-        const int wc = lj >> 7, b = (lj >> 5) & 3, r = lj & 31;
-        return ((((wr * 2 + wc) * 4 + a) * 4 + b) * 64 + r + 32 * hh) * 16 + q;
-    }
     const int wc = lj >> 6, b = (lj >> 5) & 1, r = lj & 31;
     return ((((wr * 4 + wc) * 4 + a) * 2 + b) * 64 + r + 32 * hh) * 16 + q;
 }
 
 // sd_i = sqrt(G_ii / (N - 1)) from the diagonal entries' residues (one thread per i; every
 // residue load issued before the first use)
-template <int L, bool W4>
+template <int L>
 __global__ __launch_bounds__(256) void k_crt_diag(const uint8_t *Rs, int T, int ntiles, int ks, CrtTab tab,
                                                  const int *expo, int n, double scale, double *sd) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1014,7 +876,7 @@ __global__ __launch_bounds__(256) void k_crt_diag(const uint8_t *Rs, int T, int 
     }
     const int k = tab.k;
     const int64_t ustride = (int64_t)ntiles * CRT_UNIT;
-    const uint8_t *src = Rs + (int64_t)t * CRT_UNIT + crt_unit_offset<W4>(i % CRT_T, i % CRT_T);
+    const uint8_t *src = Rs + (int64_t)t * CRT_UNIT + crt_unit_offset(i % CRT_T, i % CRT_T);
     uint32_t sv[CRT_KMAX];
 #pragma unroll
     for (int mi = 0; mi < CRT_KMAX; ++mi) sv[mi] = 0;
@@ -1037,7 +899,7 @@ __global__ __launch_bounds__(256) void k_crt_diag(const uint8_t *Rs, int T, int 
 // 16-byte lane word of the units: the same column j, 4 consecutive rows i); residues summed over
 // the ks slabs in u16 lanes, moduli outermost (each modulus' constants read once, 4 independent
 // chains); writes C_ij and its mirror C_ji, each in numpy's division order
-template <int L, bool W4>
+template <int L>
 __global__ __launch_bounds__(256) void k_crt_finish(const uint8_t *Rs, int T, int ntiles, int ks, CrtTab tab,
                                                    const int *expo, int n, const double *sd, double scale, double *C,
                                                    int64_t ldc) {
@@ -1048,20 +910,9 @@ __global__ __launch_bounds__(256) void k_crt_finish(const uint8_t *Rs, int T, in
     tile_of(t, T, bi, bj);
     const int lane = rem & 63, wab = rem >> 6;
     const int r = lane & 31, hh = lane >> 5;
-    int a, b, wr, wc, j;
-    if (W4) {                               // ((w * 4 + a) * 4 + b), w = 2 wr + wc (k_xtx_crt4)
-        b = wab & 3;
-        a = (wab >> 2) & 3;
-        wr = wab >> 5;
-        wc = (wab >> 4) & 1;
-        j = bj * CRT_T + wc * 128 + b * 32 + r;
-    } else {                                // ((w * 4 + a) * 2 + b), w = 4 wr + wc (k_xtx_crt)
-        b = wab & 1;
-        a = (wab >> 1) & 3;
-        wr = wab >> 5;
-        wc = (wab >> 3) & 3;
-        j = bj * CRT_T + wc * 64 + b * 32 + r;
-    }
+    // ((w * 4 + a) * 2 + b), w = 4 wr + wc: k_xtx_crt's epilogue order
+    const int b = wab & 1, a = (wab >> 1) & 3, wr = wab >> 5, wc = (wab >> 3) & 3;
+    const int j = bj * CRT_T + wc * 64 + b * 32 + r;
     // this word: accumulators q = 4 g .. 4 g + 3, rows ibase + (q & 3) + 8 (q >> 2) = ibase + q4 + 8 g
     const int ibase = bi * CRT_T + wr * 128 + a * 32 + 4 * hh + 8 * g;
     if (j >= n || ibase > j) return;
@@ -1117,12 +968,12 @@ __global__ __launch_bounds__(256) void k_crt_finish(const uint8_t *Rs, int T, in
 
 // slab split of the digit GEMM: a function of (n, N) only (every world size sums the same slabs
 // in the same order), rows per slab a multiple of the 32-row digit block and <= K1_I8_MAXK
-int split_k_i8(int n, int64_t N, int *kb_out) {
+int split_k_i8(const int64_t *tune, int n, int64_t N, int *kb_out) {
     const int T = (n + 63) / 64;
     const int ntiles = T * (T + 1) / 2;
     const int TB = (int)((N + 63) / 64 * 2);
     int ks = (int)std::max<int64_t>(1, (PCG_K1_BLOCKS + ntiles / 2) / ntiles);
-    if (const char *e = getenv("PCG_K1_I8_KS")) ks = std::max(1, atoi(e));   // A/B knob
+    if (tune[PCG_TUNE_K1_I8_KS] > 0) ks = (int)tune[PCG_TUNE_K1_I8_KS];   // PCG_TUNE_K1_I8_KS
     ks = std::min(ks, std::max(1, TB / 2));          // >= 64 rows per slab
     ks = std::min(ks, 256);
     int kb = (TB + ks - 1) / ks;
@@ -1131,44 +982,22 @@ int split_k_i8(int n, int64_t N, int *kb_out) {
     return (TB + kb - 1) / kb;
 }
 
-int k1_super() {                               // A/B knob: PCG_K1_SUPER_ORDER=0 -> row-major tiles
-    const char *e = getenv("PCG_K1_SUPER_ORDER");
-    return !e || atoi(e) != 0;
-}
-
-bool k1_i8() {
-    const char *e = getenv("PCG_K1_I8");
-    return !e || atoi(e) != 0;
-}
+// the knobs of a handle, or the built-in / environment defaults for a null handle (the host-only
+// pcg_corr_shard_bytes / pcg_k1_plan_signature calls)
+struct K1Tune {
+    int64_t v[PCG_TUNE_COUNT];
+    explicit K1Tune(const pcg_handle *h) {
+        if (h) memcpy(v, h->tune, sizeof(v));
+        else pcg_tuning_defaults(v);
+    }
+};
 
 // the CRT path's plan: a function of (n, N) only, so every rank and world size agrees
 struct CrtPlan {
     CrtTab tab;
     int T = 0, ntiles = 0, ks = 0, kb = 0, TB = 0, CBp = 0;
     int64_t units = 0;
-    bool w4 = false;    // k_xtx_crt4 (4 waves of 128 x 128) and its unit byte order (PCG_K1_CRT_W4=1); else k_xtx_crt
 };
-
-static int env_int(const char *name, int dflt) {
-    const char *e = getenv(name);
-    return e ? atoi(e) : dflt;
-}
-
-// the plan's A/B knobs (read at each call; pcg_corr_sharded agrees the resulting plan's signature
-// across ranks before its all-gather, so ranks started with different knobs fail together)
-struct CrtKnobs {
-    bool on, w4;
-    int minn, bmin, ks;
-};
-static CrtKnobs crt_knobs() {
-    CrtKnobs v;
-    v.on = k1_i8() && env_int("PCG_K1_CRT", 1) != 0;
-    v.minn = env_int("PCG_K1_CRT_MINN", 256);
-    v.bmin = std::min(63, std::max(32, env_int("PCG_K1_CRT_BITS", 56)));   // k_residues needs b in [32, 63]
-    v.ks = env_int("PCG_K1_CRT_KS", 0);
-    v.w4 = env_int("PCG_K1_CRT_W4", 0) != 0;   // off: 0.49 vs 0.40 ms (one wave per SIMD waits out its latencies)
-    return v;
-}
 
 // little-endian 32-bit limb helpers for the host tables
 static void big_mul_small(uint32_t *x, int L, uint32_t m) {
@@ -1189,10 +1018,11 @@ static uint32_t big_div_small(const uint32_t *x, int L, uint32_t m, uint32_t *q)
     return (uint32_t)r;
 }
 
-bool crt_plan(int n, int64_t N, CrtPlan &p) {
-    const CrtKnobs kn = crt_knobs();
-    if (!kn.on || n < kn.minn) return false;
-    const int bmin = kn.bmin;
+// the plan's knobs are the handle's (pcg_corr_sharded agrees the resulting plan's signature
+// across ranks before its all-gather, so ranks with different knobs fail together)
+bool crt_plan(const int64_t *tune, int n, int64_t N, CrtPlan &p) {
+    if (!tune[PCG_TUNE_K1_I8] || !tune[PCG_TUNE_K1_CRT] || n < tune[PCG_TUNE_K1_CRT_MINN]) return false;
+    const int bmin = (int)std::min<int64_t>(63, std::max<int64_t>(32, tune[PCG_TUNE_K1_CRT_BITS]));   // k_residues: b in [32, 63]
     // k: the fewest moduli whose product leaves b >= bmin bits per value, M > 2 N 4^b (0.01 bit margin)
     double lm = 0.0;
     int k = 0, b = 0;
@@ -1203,7 +1033,6 @@ bool crt_plan(int n, int64_t N, CrtPlan &p) {
     }
     if (b < bmin) return false;
     b = std::min(b, 63);
-    p.w4 = kn.w4;
     CrtTab &t = p.tab;
     memset(&t, 0, sizeof(t));
     t.k = k;
@@ -1254,7 +1083,7 @@ bool crt_plan(int n, int64_t N, CrtPlan &p) {
     // each unit writes and k_crt_finish reads (128 KB, ~0.026 us of chip bandwidth)
     int best = 1;
     double best_cost = 1e300;
-    const int force = kn.ks;
+    const int force = (int)tune[PCG_TUNE_K1_CRT_KS];
     for (int ks = 1; ks <= 16; ++ks) {
         int kbk = (p.TB + ks - 1) / ks;
         kbk = (kbk + CRT_KB - 1) / CRT_KB * CRT_KB;
@@ -1294,12 +1123,8 @@ int crt_residues(pcg_handle *h, const CrtPlan &p, const double *X, int64_t N, in
 void crt_gemm(pcg_handle *h, const CrtPlan &p, const int8_t *R, int64_t u0, int64_t nu, uint8_t *out) {
     if (nu <= 0) return;
     const int64_t plane = (int64_t)p.CBp * p.TB * 2048;
-    if (p.w4)
-        hipLaunchKernelGGL(k_xtx_crt4, dim3((unsigned)((nu + 7) / 8 * 8)), dim3(256), CRT_NS * CRT_STAGE, h->stream, R,
-                           p.TB, plane, p.T, p.ntiles, p.ks, p.kb, p.tab, u0, nu, out);
-    else
-        hipLaunchKernelGGL(k_xtx_crt, dim3((unsigned)((nu + 7) / 8 * 8)), dim3(512), CRT_NS * CRT_STAGE, h->stream, R,
-                           p.TB, plane, p.T, p.ntiles, p.ks, p.kb, p.tab, u0, nu, out);
+    hipLaunchKernelGGL(k_xtx_crt, dim3((unsigned)((nu + 7) / 8 * 8)), dim3(512), CRT_NS * CRT_STAGE, h->stream, R,
+                       p.TB, plane, p.T, p.ntiles, p.ks, p.kb, p.tab, u0, nu, out);
 }
 
 // C from the units' residues: the diagonal (sd) first, then every upper entry and its mirror
@@ -1307,18 +1132,13 @@ void crt_finish(pcg_handle *h, const CrtPlan &p, const uint8_t *Rs, const int *e
                 double *C, int64_t ldc) {
     const double scale = 1.0 / (double)(N - 1);
     const int64_t threads = (int64_t)p.ntiles * 16384;
-#define CRT_LAUNCH_W(L_, W_)                                                                                    \
-    hipLaunchKernelGGL((k_crt_diag<L_, W_>), dim3((unsigned)((nn + 255) / 256)), dim3(256), 0, h->stream, Rs, p.T, \
-                       p.ntiles, p.ks, p.tab, expo, nn, scale, sd);                                              \
-    hipLaunchKernelGGL((k_crt_finish<L_, W_>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, h->stream, Rs, \
-                       p.T, p.ntiles, p.ks, p.tab, expo, nn, (const double *)sd, scale, C, ldc)
-#define CRT_LAUNCH(L_)                  \
-    do {                                \
-        if (p.w4) {                     \
-            CRT_LAUNCH_W(L_, true);     \
-        } else {                        \
-            CRT_LAUNCH_W(L_, false);    \
-        }                               \
+#define CRT_LAUNCH(L_)                                                                                       \
+    do {                                                                                                     \
+        hipLaunchKernelGGL((k_crt_diag<L_>), dim3((unsigned)((nn + 255) / 256)), dim3(256), 0, h->stream, Rs, \
+                           p.T, p.ntiles, p.ks, p.tab, expo, nn, scale, sd);                                  \
+        hipLaunchKernelGGL((k_crt_finish<L_>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,         \
+                           h->stream, Rs, p.T, p.ntiles, p.ks, p.tab, expo, nn, (const double *)sd, scale, C, \
+                           ldc);                                                                              \
     } while (0)
     if (p.tab.L <= 4) { CRT_LAUNCH(4); }
     else if (p.tab.L == 5) { CRT_LAUNCH(5); }
@@ -1516,12 +1336,22 @@ int column_means(pcg_handle *h, const double *X, int64_t N, int nn, int64_t ldx,
 
 // a signature of K1's plan for (n, N) (path, and the CRT path's k, b, split-K and unit count):
 // ranks whose environments select different plans would all-gather mismatched units
-int64_t k1_plan_signature(int64_t n, int64_t N) {
+int64_t k1_plan_signature(const pcg_handle *h, int64_t n, int64_t N) {
+    const K1Tune t(h);
     CrtPlan cp;
-    if (crt_plan((int)n, N, cp))
-        return ((int64_t)1 << 62) | ((int64_t)cp.w4 << 56) | ((int64_t)cp.tab.k << 48) | ((int64_t)cp.tab.b << 40) |
-               ((int64_t)cp.ks << 32) | (cp.units & 0xffffffffll);
-    return k1_i8() ? 1 : 2;
+    if (crt_plan(t.v, (int)n, N, cp))
+        return ((int64_t)1 << 62) | ((int64_t)cp.tab.k << 48) | ((int64_t)cp.tab.b << 40) | ((int64_t)cp.ks << 32) |
+               (cp.units & 0xffffffffll);
+    if (!t.v[PCG_TUNE_K1_I8]) return 2;
+    int kb = 0;                               // the digit path: its slab split and tile order
+    const int ks = split_k_i8(t.v, (int)n, N, &kb);
+    return ((int64_t)1 << 61) | ((int64_t)ks << 32) | ((int64_t)kb << 8) | (t.v[PCG_TUNE_K1_SUPER_ORDER] ? 1 : 0);
+}
+
+extern "C" int pcg_k1_plan_signature(pcg_handle *h, int64_t n, int64_t N, int64_t *signature) {
+    if (n < 1 || N < 2 || n > (1 << 24) || !signature) return pcg_fail(h, PCG_ERR_INVALID, "pcg_k1_plan_signature");
+    *signature = k1_plan_signature(h, n, N);
+    return PCG_OK;
 }
 
 extern "C" int pcg_corr_shard_rows(int64_t n, int world, int64_t *rows_per_rank) {
@@ -1533,10 +1363,11 @@ extern "C" int pcg_corr_shard_rows(int64_t n, int world, int64_t *rows_per_rank)
 
 // bytes of one rank's share (the pcg_corr_shard buffer; the all-gather moves world x this): the
 // CRT path's residue units, else the digit / fp64 path's packed Gram rows
-extern "C" int pcg_corr_shard_bytes(int64_t n, int64_t N, int world, int64_t *bytes_per_rank) {
+extern "C" int pcg_corr_shard_bytes(pcg_handle *h, int64_t n, int64_t N, int world, int64_t *bytes_per_rank) {
     if (n < 1 || N < 2 || world < 1 || n > (1 << 24) || !bytes_per_rank) return PCG_ERR_INVALID;
+    const K1Tune t(h);
     CrtPlan cp;
-    if (crt_plan((int)n, N, cp)) {
+    if (crt_plan(t.v, (int)n, N, cp)) {
         *bytes_per_rank = (cp.units + world - 1) / world * (int64_t)CRT_UNIT;
         return PCG_OK;
     }
@@ -1560,7 +1391,7 @@ extern "C" int pcg_corr_shard(pcg_handle *h, const double *X, int64_t N, int64_t
     PCG_HIP(h, hipSetDevice(h->device));
     const int nn = (int)n;
     CrtPlan cp;
-    if (crt_plan(nn, N, cp)) {     // this rank's contiguous run of (tile, modulus, slab) units
+    if (crt_plan(h->tune, nn, N, cp)) {     // this rank's contiguous run of (tile, modulus, slab) units
         double *mean;
         int *expo = nullptr;
         int rc = column_means(h, X, N, nn, ldx, &mean, &expo);
@@ -1568,7 +1399,7 @@ extern "C" int pcg_corr_shard(pcg_handle *h, const double *X, int64_t N, int64_t
         h->k1_stamp[0] = N;
         h->k1_stamp[1] = nn;
         h->k1_stamp[2] = cp.tab.k;
-        h->k1_stamp[3] = cp.tab.b;
+        h->k1_stamp[3] = ((int64_t)cp.tab.b << 32) | ((int64_t)cp.ks << 16) | cp.kb;
         h->k1_stamp_ok = true;
         const int8_t *R = nullptr;
         rc = crt_residues(h, cp, X, N, nn, ldx, mean, expo, 0, cp.tab.k, h->stream, &R);
@@ -1596,14 +1427,14 @@ extern "C" int pcg_corr_shard(pcg_handle *h, const double *X, int64_t N, int64_t
     }
     const int ntiles = (int)(tl.size() / 3);
     if (ntiles == 0) return PCG_OK;
-    const bool i8 = k1_i8();
+    const bool i8 = h->tune[PCG_TUNE_K1_I8] != 0;
     double *mean;
     int *expo = nullptr;
     int rc = column_means(h, X, N, nn, ldx, &mean, i8 ? &expo : nullptr);
     if (rc) return rc;
     int64_t kchunk = 0;
     int kb = 0;
-    const int ks = i8 ? split_k_i8(nn, N, &kb) : split_k(nn, N, &kchunk);
+    const int ks = i8 ? split_k_i8(h->tune, nn, N, &kb) : split_k(nn, N, &kchunk);
     const int64_t stride = rows * nn;
     if (!pcg_ensure(h, h->pr_scratch, sizeof(double) * ((size_t)stride * (ks > 1 ? ks : 0) + tl.size())))
         return pcg_fail(h, PCG_ERR_OOM, "pcg_corr_shard slabs");
@@ -1638,9 +1469,9 @@ extern "C" int pcg_corr_shard_finish(pcg_handle *h, const double *gathered, int6
     const int nn = (int)n;
     const double scale = 1.0 / (double)(N - 1);
     CrtPlan cp;
-    if (crt_plan(nn, N, cp)) {     // gathered = every unit in canonical order; exponents from pcg_corr_shard
+    if (crt_plan(h->tune, nn, N, cp)) {     // gathered = every unit in canonical order; exponents from pcg_corr_shard
         if (!h->k1_stamp_ok || h->k1_stamp[0] != N || h->k1_stamp[1] != nn || h->k1_stamp[2] != cp.tab.k ||
-            h->k1_stamp[3] != cp.tab.b)
+            h->k1_stamp[3] != (((int64_t)cp.tab.b << 32) | ((int64_t)cp.ks << 16) | cp.kb))
             return pcg_fail(h, PCG_ERR_INVALID,
                             "pcg_corr_shard_finish: no CRT-mode pcg_corr_shard of (N %lld, n %lld) on this handle since "
                             "the last K1 call", (long long)N, (long long)n);
@@ -1675,7 +1506,7 @@ int pcg_corr_launch(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_
     const int nn = (int)n;
     const double scale = 1.0 / (double)(N - 1);
     CrtPlan cp;
-    if (crt_plan(nn, N, cp)) {
+    if (crt_plan(h->tune, nn, N, cp)) {
         double *mean;
         int *expo = nullptr;
         int rc = column_means(h, X, N, nn, ldx, &mean, &expo);
@@ -1685,41 +1516,17 @@ int pcg_corr_launch(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_
             return pcg_fail(h, PCG_ERR_OOM, "pcg_corr CRT scratch");
         double *sd = (double *)h->pr_scratch.p;
         uint8_t *Rs = (uint8_t *)h->pr_scratch.p + sbytes;
-        // PCG_K1_CRT_GROUPS > 1: moduli in groups, the residue planes of group g + 1 computed on the
-        // aux stream while the GEMM of group g runs. Measured slower (pcg_corr 0.63 ms at 1 group,
-        // 0.76 / 0.80 / 0.95 ms at 2 / 3 / 4: the co-resident residue blocks delay the GEMM's
-        // one-block-per-CU waves more than they hide), so 1 is the default.
-        const int k = cp.tab.k;
-        const int groups = std::max(1, std::min(k, std::min(CRT_MAXG, env_int("PCG_K1_CRT_GROUPS", 1))));
+        // (round 4 measured the residue planes of modulus groups on the aux stream beside the GEMM:
+        // slower — the co-resident residue blocks delay the GEMM's waves — and removed it in round 5)
         const int8_t *R = nullptr;
-        if (groups == 1) {
-            rc = crt_residues(h, cp, X, N, nn, ldx, mean, expo, 0, k, h->stream, &R);
-            if (rc) return rc;
-            crt_gemm(h, cp, R, 0, cp.units, Rs);
-        } else {
-            if (!h->aux) PCG_HIP(h, hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking));
-            for (int g = 0; g <= groups; ++g)
-                if (!h->k1ev[g]) PCG_HIP(h, hipEventCreateWithFlags(&h->k1ev[g], hipEventDisableTiming));
-            PCG_HIP(h, hipEventRecord(h->k1ev[groups], h->stream));        // column statistics done
-            PCG_HIP(h, hipStreamWaitEvent(h->aux, h->k1ev[groups], 0));
-            const int64_t per_mod = (int64_t)cp.ks * cp.ntiles;
-            for (int g = 0; g < groups; ++g) {
-                const int m0 = k * g / groups, m1 = k * (g + 1) / groups;
-                rc = crt_residues(h, cp, X, N, nn, ldx, mean, expo, m0, m1, h->aux, &R);
-                if (rc) return rc;
-                PCG_HIP(h, hipEventRecord(h->k1ev[g], h->aux));
-            }
-            for (int g = 0; g < groups; ++g) {
-                const int m0 = k * g / groups, m1 = k * (g + 1) / groups;
-                PCG_HIP(h, hipStreamWaitEvent(h->stream, h->k1ev[g], 0));
-                crt_gemm(h, cp, R, m0 * per_mod, (m1 - m0) * per_mod, Rs + m0 * per_mod * CRT_UNIT);
-            }
-        }
+        rc = crt_residues(h, cp, X, N, nn, ldx, mean, expo, 0, cp.tab.k, h->stream, &R);
+        if (rc) return rc;
+        crt_gemm(h, cp, R, 0, cp.units, Rs);
         crt_finish(h, cp, Rs, expo, nn, N, sd, C, ldc);
         PCG_HIP(h, hipGetLastError());
         return PCG_OK;
     }
-    const bool i8 = k1_i8();
+    const bool i8 = h->tune[PCG_TUNE_K1_I8] != 0;
     double *mean;
     int *expo = nullptr;
     int rc = column_means(h, X, N, nn, ldx, &mean, i8 ? &expo : nullptr);
@@ -1728,7 +1535,7 @@ int pcg_corr_launch(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_
     const int ntiles = T * (T + 1) / 2;
     int64_t kchunk = 0;
     int kb = 0;
-    const int ks = i8 ? split_k_i8(nn, N, &kb) : split_k(nn, N, &kchunk);
+    const int ks = i8 ? split_k_i8(h->tune, nn, N, &kb) : split_k(nn, N, &kchunk);
     double *G = C;
     int64_t ldg = ldc, stride = 0;
     if (ks > 1) {
@@ -1745,7 +1552,7 @@ int pcg_corr_launch(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_
         if (rc) return rc;
         hipLaunchKernelGGL(k_xtx_i8, dim3(xtx_grid(ntiles * ks)), dim3(256), 0, h->stream, Dg, CB, TB, nn,
                            (const int *)expo, ntiles, ks, kb, G, ldg, stride, (const int32_t *)nullptr,
-                           k1_super());
+                           h->tune[PCG_TUNE_K1_SUPER_ORDER] != 0 ? 1 : 0);
     } else {
         hipLaunchKernelGGL(k_xtx, dim3(xtx_grid(ntiles * ks)), dim3(256), 0, h->stream, X, N, nn, ldx, mean, ntiles,
                            ks, kchunk, G, ldg, stride, (const int32_t *)nullptr);

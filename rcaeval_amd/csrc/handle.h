@@ -61,6 +61,7 @@ inline double pcg_now_us() {
 
 struct pcg_handle {
     int device = 0;
+    int64_t tune[PCG_TUNE_COUNT] = {};   // pcg_set_tuning knobs (defaults from the environment at pcg_create)
     hipStream_t stream = nullptr;
     bool own_stream = false;
     std::string err;
@@ -78,7 +79,6 @@ struct pcg_handle {
     // pcg_corr_shard_finish refuses to rebuild C from exponents of any other call
     int64_t k1_stamp[4] = {0, 0, 0, 0};
     bool k1_stamp_ok = false;
-    hipEvent_t k1ev[5] = {};        // K1 CRT: residue groups done on aux (+ column statistics done)
     // CSR (offsets, neighbour lists) and sepset union rows, double-buffered: depth d's sepset
     // export reads buffer set cb on the export stream while depth d + 1 runs on set 1 - cb
     DevBuf off2[2], nbr2[2], ug2[2];
@@ -93,8 +93,6 @@ struct pcg_handle {
     bool xinl = false;               // ... some of them on the handle's stream (small graphs)
     DevBuf exp_ctr;                  // rows exported so far (device, persists across depths)
     PinBuf ctr_pin, deg_pin, off_pin, cpre_pin, status_pin;
-    DevBuf gbar;                     // the fused level barrier's grid-barrier words (k_level_end)
-    bool fuse_end = false;           // this depth's screen / exact path / removals run fused in k_level_end
     DevBuf small_sum;                // single-workgroup small-graph skeleton: summary + counters
     PinBuf small_pin;                // its host copy
     std::vector<uint64_t> binom_h;   // host copy of the binomial table
@@ -126,24 +124,9 @@ struct pcg_handle {
     int narrow_deg = 64;             // pcg_set_narrow_degree (testing: route more nodes to the wide class)
     bool tgroup = false;             // small class runs k_level_lds_t this depth
     bool wavek = false;              // small class runs k_level_wave this depth (deep levels)
-    bool sp = false;                 // small class runs k_level_sp this depth (Schur-prefix sweep)
     bool nblk = false;               // small class stages per-node compact blocks (k_node_blocks) this depth
-    DevBuf cblk, lmk;                // k_level_sp: per-node compact correlation blocks, local masks
-    std::vector<int64_t> sp_ctab, sp_coff;   // k_level_sp chunk tables per degree (host copies)
-    int64_t sp_tab_off = 0;          // int64 offset of [coff, ctab, bo] in cpre / cpre_pin
-    // pipelined level loop (skeleton_once, single GPU, threshold mode): depth d >= 2 is decomposed
-    // on upper-bound degrees (those at the start of d - 1) and enqueued before depth d - 1's
-    // summary is read; k_decompose computes the exact prefixes on the device
-    bool bound = false;              // the current depth was prepared in bound mode
-    bool dspl = false;               // bound mode: k_decompose_dev picks spl / spl_w on the device (spl_buf)
-    int dspl_lanes = 256;            // lanes per narrow-class chunk unit (4: a wave per set)
-    double dspl_tgt[2] = {0, 0};     // narrow / wide block targets
-    int dspl_cap[2] = {64, 64};      // narrow / wide spl caps
-    DevBuf spl_buf;                  // int32[2]: the device's narrow / wide spl
-    int64_t dtab_off = 0;            // int64 offset of the per-degree class tables in cpre (bound mode)
-    int64_t bo_off = 0;              // int64 offset of the compact-block offsets in cpre
-    int dtab_maxd = 0;               // their largest degree
-    PinBuf tab_pin[2];               // bound-mode uploads, alternating by depth parity
+    DevBuf cblk, lmk;                // k_node_blocks: per-node compact correlation blocks, local masks
+    int64_t bo_off = 0;              // int64 offset of the compact-block offsets in cpre / cpre_pin
     hipEvent_t rev[PCG_MAX_LEVELS][2] = {};   // per-depth CI-test kernel brackets
     int64_t near_seen = 0;           // near-alpha entries copied so far (the device list accumulates)
     int64_t near_total_dev = 0;      // the device's cumulative near-alpha count at the last level end
@@ -156,7 +139,7 @@ struct pcg_handle {
     void *summary_dev = nullptr;        // its device address, queried once at allocation
     size_t summary_bytes = 0;
     unsigned long long summary_seq = 0;
-    // PCG_HOST_TRACE=1: host timestamps of the level loop's steps, printed after each skeleton
+    // PCG_TUNE_HOST_TRACE: host timestamps of the level loop's steps, printed after each skeleton
     bool htrace_on = false;
     std::vector<std::pair<const char *, double>> htrace;
     std::vector<int32_t> deg_h;      // degrees at the start of the current depth
@@ -184,7 +167,8 @@ void pcg_comm_release(pcg_handle *h);      // comm.hip: destroy the communicator
 // corr.hip: K1 queued on h->stream without the host sync of pcg_corr (pcg_pc_skeleton)
 int export_sync(pcg_handle *h);   // skeleton.hip: wait for the sepset exports, take their row count
 int pcg_corr_launch(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx, double *C, int64_t ldc);
-int64_t k1_plan_signature(int64_t n, int64_t N);   // corr.hip: K1's plan for (n, N), for cross-rank agreement
+int64_t k1_plan_signature(const pcg_handle *h, int64_t n, int64_t N);   // corr.hip: K1's plan, for cross-rank agreement
+void pcg_tuning_defaults(int64_t *tune);   // api.hip: the built-in values, overridden by the environment
 
 int pcg_fail(pcg_handle *h, int code, const char *fmt, ...);
 bool pcg_ensure(pcg_handle *h, DevBuf &b, size_t bytes);   // grow-only allocation

@@ -119,11 +119,8 @@ struct LevelArgs {
     int64_t rec_mod, rec_res;    // record sample: canonical pair (a, b) with (a*n + b) % rec_mod == rec_res
     int64_t chunk_lo;            // first chunk of this launch (within its class)
     int spl;                     // S ranks per lane (LDS-resident kernel)
-    const int32_t *spl_dev;      // pipelined loop: the spl k_decompose chose on the device (else null)
     int lds_btab_off;            // byte offset of the LDS binomial table (LDS-resident kernel)
-    // Schur-prefix sweep (k_level_sp): per-degree chunk tables and the per-node compact blocks
-    const int64_t *ctab;         // chunk (t0 << 40 | first task << 20 | tasks), per degree D from coff[D]
-    const int64_t *coff;         // SP_DMAX + 2 offsets into ctab
+    // depth 4's per-node compact blocks (k_node_blocks)
     const int64_t *bo;           // n + 1 offsets of the compact blocks (doubles)
     double *cblk;                // per node: C[adj(x) + x, adj(x) + x], stride D + 1, x last
     uint64_t *lmk;               // per node: local adjacency masks of adj(x), at off[x]
@@ -397,7 +394,7 @@ __global__ __launch_bounds__(256) void k_export(const int32_t *off, const int32_
     const int64_t slot = wave_base + lane;
     int x = -1, y = -1;
     bool removed = false;
-    if (slot < sumdeg && slot < off[n]) {   // (sumdeg may be an upper bound: pipelined level loop)
+    if (slot < sumdeg && slot < off[n]) {
         int lo = 0, hi = n;  // off[lo] <= slot < off[hi]
         while (hi - lo > 1) {
             const int mid = (lo + hi) >> 1;
@@ -478,7 +475,7 @@ __device__ __forceinline__ void summary_nodes(const int32_t *deg, int n, int W, 
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) ps += __shfl_xor(ps, o);
         int base = ps;
-        const int dx = *(const volatile int32_t *)&deg[x];   // (written by other blocks in the fused barrier)
+        const int dx = *(const volatile int32_t *)&deg[x];
         if (ug && (int64_t)base + dx <= ug_rows) {
             const int64_t lo = (int64_t)base * W, hi = (int64_t)(base + dx) * W;
             for (int64_t e = lo + lane; e < hi; e += 64) ug[e] = 0ull;
@@ -505,12 +502,11 @@ __device__ __forceinline__ void summary_nodes(const int32_t *deg, int n, int W, 
     }
 }
 
-// the summary part (one block): CSR offsets, degrees, counters, status bytes (plus `extra` ORed
-// into status byte 4: a fused barrier's failure) -> host-mapped memory, then the sequence number
+// the summary part (one block): CSR offsets, degrees, counters, status bytes -> host-mapped
+// memory, then the sequence number
 __device__ __forceinline__ void summary_block(const int32_t *deg, int n, int32_t *off, const uint64_t *ug,
                                               int64_t ug_rows, DevCounters *ctr, uint8_t *status, LevelSummary *out,
-                                              int32_t *out_deg, unsigned long long seq, int nfill, int32_t *part,
-                                              uint8_t extra) {
+                                              int32_t *out_deg, unsigned long long seq, int nfill, int32_t *part) {
     const int tid = threadIdx.x;
     const int per = (n + 255) / 256;
     const int lo = min(n, tid * per), hi = min(n, lo + per);
@@ -532,7 +528,6 @@ __device__ __forceinline__ void summary_block(const int32_t *deg, int n, int32_t
     for (int i = lo; i < hi; ++i) { off[i] = acc; acc += deg[i]; }
     if (tid == 255) off[n] = part[255];
     if (tid == 0) {
-        // (volatile reads: in the fused barrier other blocks of this launch wrote them)
         volatile unsigned long long *cw = reinterpret_cast<volatile unsigned long long *>(ctr);
         unsigned long long *ow = reinterpret_cast<unsigned long long *>(&out->ctr);
         constexpr int NW = (int)(sizeof(DevCounters) / sizeof(unsigned long long));
@@ -543,7 +538,6 @@ __device__ __forceinline__ void summary_block(const int32_t *deg, int n, int32_t
         }
         const volatile uint8_t *sv = status;
         for (int k = 0; k < 8; ++k) out->status[k] = status ? sv[k] : 0;
-        out->status[4] |= extra;
         out->ug_clean = ug != nullptr && nfill > 0 && (int64_t)part[255] <= ug_rows;
         if (status)
             for (int k = 0; k < PCG_RM_STATUS; ++k) status[k] = 0;
@@ -565,200 +559,7 @@ __global__ __launch_bounds__(256) void k_summary_fill(const int32_t *deg, int n,
         return;
     }
     __shared__ int32_t part[256];
-    summary_block(deg, n, off, ug, ug_rows, ctr, status, out, out_deg, seq, nfill, part, 0);
-}
-
-// The exact per-class chunk prefixes of the current graph from per-degree tables the host built
-// on upper-bound degrees (pipelined level loop, pcg_level_begin in bound mode): tab[c * (maxd + 1)
-// + D] = chunks of a degree-D node in class c (0 narrow, 1 wide, 2 large; 0 when D is not in c).
-// One block: each thread scans a contiguous node range; cpre gets 3 x (n + 1) prefixes, bo the
-// compact-block offsets of the narrow class (nblk). The reference loop condition (max degree - 1
-// > depth - 1) is evaluated here: when it fails every class total is 0 and the level's launches
-// exit at once.
-__global__ __launch_bounds__(256) void k_decompose(const int32_t *deg, int n, const int64_t *tab, int maxd, int depth,
-                                                   int nblk, int64_t *cpre, int64_t *bo) {
-    __shared__ int64_t part[4][256];
-    __shared__ int mx[256];
-    const int tid = threadIdx.x;
-    const int per = (n + 255) / 256;
-    const int lo = min(n, tid * per), hi = min(n, lo + per);
-    int64_t sum[4] = {0, 0, 0, 0};
-    int m = 0;
-    for (int i = lo; i < hi; ++i) {
-        const int D = min(deg[i], maxd);
-        m = max(m, deg[i]);
-#pragma unroll
-        for (int c = 0; c < 3; ++c) sum[c] += tab[c * (maxd + 1) + D];
-        if (nblk && tab[D] > 0) sum[3] += (int64_t)(D + 1) * (D + 1);
-    }
-#pragma unroll
-    for (int c = 0; c < 4; ++c) part[c][tid] = sum[c];
-    mx[tid] = m;
-    __syncthreads();
-    for (int o = 1; o < 256; o <<= 1) {        // inclusive scans of the four sums, max of the degrees
-        int64_t v[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) v[c] = tid >= o ? part[c][tid - o] : 0;
-        const int vm = tid >= o ? mx[tid - o] : 0;
-        __syncthreads();
-#pragma unroll
-        for (int c = 0; c < 4; ++c) part[c][tid] += v[c];
-        mx[tid] = max(mx[tid], vm);
-        __syncthreads();
-    }
-    const bool run = mx[255] - 1 > depth - 1;
-    int64_t acc[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) acc[c] = (run && tid) ? part[c][tid - 1] : 0;
-    for (int i = lo; i < hi; ++i) {
-        const int D = min(deg[i], maxd);
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            cpre[c * (int64_t)(n + 1) + i] = acc[c];
-            if (run) acc[c] += tab[c * (maxd + 1) + D];
-        }
-        if (nblk) {
-            bo[i] = acc[3];
-            if (run && tab[D] > 0) acc[3] += (int64_t)(D + 1) * (D + 1);
-        }
-    }
-    if (tid == 255) {
-#pragma unroll
-        for (int c = 0; c < 3; ++c) cpre[c * (int64_t)(n + 1) + n] = run ? part[c][255] : 0;
-        if (nblk) bo[n] = run ? part[3][255] : 0;
-    }
-}
-
-// The pipelined loop's decomposition with the chunk size chosen on the device. tab[0][D] /
-// tab[1][D] = units (T-group lane tasks or S ranks) of a degree-D node in the narrow / wide class
-// (0 if D is in another class), tab[2][D] = its large-class chunks. From the exact degrees: the
-// class sums, spl = clamp(floor(sum / (lanes * target)), 1, cap) per class (the host rule of
-// pcg_level_begin, now on the degrees the depth really starts from), chunks = ceil(units / (lanes
-// * spl)), the class prefixes, the compact-block offsets and spl_out[2] (which the level kernels
-// read through LevelArgs::spl_dev). One 1024-thread block; a thread's nodes are contiguous and
-// every load of a pass is issued before the first is used (the single-block form with one
-// dependent load chain per node took 21-42 us at n = 2000). The launch sizes of the depth are
-// host bounds on these counts (pcg_level_begin, bound mode); the reference loop condition is
-// evaluated here: when it fails every class total is 0.
-constexpr int DEC_THREADS = 1024, DEC_PER = 8;
-__global__ __launch_bounds__(DEC_THREADS) void k_decompose_dev(const int32_t *deg, int n, const int64_t *tab, int maxd,
-                                                               int depth, int nblk, int lanes0, double tgt0, int cap0,
-                                                               double tgt1, int cap1, int64_t *cpre, int64_t *bo,
-                                                               int32_t *spl_out) {
-    __shared__ int64_t part[4][DEC_THREADS / 64];
-    __shared__ int64_t wsum[4][DEC_THREADS / 64];
-    __shared__ int mxw[DEC_THREADS / 64];
-    __shared__ int s_spl[2];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int per = (n + DEC_THREADS - 1) / DEC_THREADS;
-    const int lo = min(n, tid * per), hi = min(n, lo + per);
-    // pass 1: the class unit sums and the largest degree
-    int64_t u0 = 0, u1 = 0;
-    int m = 0;
-    for (int b = lo; b < hi; b += DEC_PER) {
-        int Dk[DEC_PER];
-#pragma unroll
-        for (int k = 0; k < DEC_PER; ++k) Dk[k] = b + k < hi ? deg[b + k] : 0;
-        int64_t t0[DEC_PER], t1[DEC_PER];
-#pragma unroll
-        for (int k = 0; k < DEC_PER; ++k) {
-            const int D = min(Dk[k], maxd);
-            m = max(m, Dk[k]);
-            t0[k] = b + k < hi ? tab[D] : 0;
-            t1[k] = b + k < hi ? tab[(maxd + 1) + D] : 0;
-        }
-#pragma unroll
-        for (int k = 0; k < DEC_PER; ++k) { u0 += t0[k]; u1 += t1[k]; }
-    }
-    auto wred = [&](int64_t v) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-        return v;
-    };
-    u0 = wred(u0);
-    u1 = wred(u1);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o));
-    if (lane == 0) { wsum[0][wv] = u0; wsum[1][wv] = u1; mxw[wv] = m; }
-    __syncthreads();
-    if (tid == 0) {
-        int64_t s0 = 0, s1 = 0;
-        int mm = 0;
-        for (int w = 0; w < DEC_THREADS / 64; ++w) { s0 += wsum[0][w]; s1 += wsum[1][w]; mm = max(mm, mxw[w]); }
-        const bool run = mm - 1 > depth - 1;
-        const double f0 = floor((double)s0 / ((double)lanes0 * tgt0)), f1 = floor((double)s1 / (256.0 * tgt1));
-        s_spl[0] = run ? (int)fmin((double)cap0, fmax(1.0, f0)) : 0;   // 0: the depth does not run
-        s_spl[1] = (int)fmin((double)cap1, fmax(1.0, f1));
-        spl_out[0] = max(s_spl[0], 1);
-        spl_out[1] = s_spl[1];
-    }
-    __syncthreads();
-    const bool run = s_spl[0] > 0;
-    const int64_t csz0 = (int64_t)lanes0 * max(s_spl[0], 1), csz1 = (int64_t)256 * s_spl[1];
-    // pass 2: per-node chunks (re-read: the loads stay batched), the thread's sums, the scan
-    auto chunks = [&](int i, int c, int64_t *v) {
-        const int D = min(deg[i], maxd);
-        v[0] = tab[D];
-        v[1] = tab[(maxd + 1) + D];
-        v[2] = tab[2 * (maxd + 1) + D];
-        v[3] = D;
-        (void)c;
-    };
-    int64_t sum[4] = {0, 0, 0, 0};
-    for (int i = lo; i < hi; ++i) {
-        int64_t v[4];
-        chunks(i, 0, v);
-        if (!run) continue;
-        sum[0] += (v[0] + csz0 - 1) / csz0;
-        sum[1] += (v[1] + csz1 - 1) / csz1;
-        sum[2] += v[2];
-        if (nblk && v[0] > 0) sum[3] += (v[3] + 1) * (v[3] + 1);
-    }
-    // exclusive scan over threads: wave inclusive scans, then the wave totals
-    int64_t inc[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        int64_t v = sum[c];
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int64_t t = __shfl_up(v, o);
-            if (lane >= o) v += t;
-        }
-        inc[c] = v;
-        if (lane == 63) part[c][wv] = v;
-    }
-    __syncthreads();
-    if (tid < 4) {
-        int64_t acc = 0;
-        for (int w = 0; w < DEC_THREADS / 64; ++w) {
-            const int64_t v = part[tid][w];
-            part[tid][w] = acc;
-            acc += v;
-        }
-        wsum[tid][0] = acc;       // the class totals
-    }
-    __syncthreads();
-    int64_t acc[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) acc[c] = part[c][wv] + inc[c] - sum[c];
-    for (int i = lo; i < hi; ++i) {
-        int64_t v[4];
-        chunks(i, 0, v);
-        cpre[i] = acc[0];
-        cpre[(int64_t)(n + 1) + i] = acc[1];
-        cpre[2 * (int64_t)(n + 1) + i] = acc[2];
-        if (nblk) bo[i] = acc[3];
-        if (!run) continue;
-        acc[0] += (v[0] + csz0 - 1) / csz0;
-        acc[1] += (v[1] + csz1 - 1) / csz1;
-        acc[2] += v[2];
-        if (nblk && v[0] > 0) acc[3] += (v[3] + 1) * (v[3] + 1);
-    }
-    if (tid == 0) {
-#pragma unroll
-        for (int c = 0; c < 3; ++c) cpre[c * (int64_t)(n + 1) + n] = wsum[c][0];
-        if (nblk) bo[n] = wsum[3][0];
-    }
+    summary_block(deg, n, off, ug, ug_rows, ctr, status, out, out_deg, seq, nfill, part);
 }
 
 // The node owning a chunk: the last x < n with cpre[x] <= chunk (the caller checked chunk <
@@ -812,7 +613,7 @@ template <int MODE>
 __global__ __launch_bounds__(256) void k_level0(LevelArgs a) {
     __shared__ uint8_t flag[64][68];
     const int64_t chunk = a.chunk_lo + blockIdx.x;
-    if (chunk >= a.cpre[a.n]) return;   // a launch sized by an upper bound (pipelined level loop)
+    if (chunk >= a.cpre[a.n]) return;   // (defensive: launches are sized by the exact prefix)
     int lo = chunk_node(a.cpre, a.n, chunk);
     const int bi = lo >> 6;
     const int bj = bi + (int)(chunk - a.cpre[lo]);
@@ -865,7 +666,7 @@ __global__ __launch_bounds__(256) void k_level(LevelArgs a) {
     const int wave = tid >> 6;
     const int bs = blockDim.x;
     const int64_t chunk = a.chunk_lo + blockIdx.x;
-    if (chunk >= a.cpre[a.n]) return;   // a launch sized by an upper bound (pipelined level loop)
+    if (chunk >= a.cpre[a.n]) return;   // (defensive: launches are sized by the exact prefix)
 
     // node owning this chunk
     int lo = chunk_node(a.cpre, a.n, chunk);
@@ -1099,7 +900,7 @@ __global__ __launch_bounds__(256) void k_level1_pairs(LevelArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x;
     const int64_t chunk = a.chunk_lo + blockIdx.x;
-    if (chunk >= a.cpre[a.n]) return;   // a launch sized by an upper bound (pipelined level loop)
+    if (chunk >= a.cpre[a.n]) return;   // (defensive: launches are sized by the exact prefix)
     int lo = chunk_node(a.cpre, a.n, chunk);
     const int x = lo;
     const int D = a.deg[x];
@@ -1345,7 +1146,7 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
     const int tid = threadIdx.x;
     const int bs = blockDim.x;
     const int64_t chunk = a.chunk_lo + blockIdx.x;
-    if (chunk >= a.cpre[a.n]) return;   // a launch sized by an upper bound (pipelined level loop)
+    if (chunk >= a.cpre[a.n]) return;   // (defensive: launches are sized by the exact prefix)
     int lo = chunk_node(a.cpre, a.n, chunk);
     const int x = lo;
     const int D = a.deg[x];
@@ -1390,7 +1191,7 @@ __global__ __launch_bounds__(256) void k_level_lds(LevelArgs a) {
     const int tx = *s_tx;
     const double Cxx = a.diag[x];
     const uint64_t nS = pcg_binom(a.binom, D, d);
-    const uint64_t spl = a.spl_dev ? (uint64_t)*a.spl_dev : (uint64_t)a.spl;
+    const uint64_t spl = (uint64_t)a.spl;
     const uint64_t r0 = (uint64_t)(chunk - a.cpre[x]) * (uint64_t)bs * spl;
     const uint64_t r1 = min(nS, r0 + (uint64_t)bs * spl);
     unsigned long long tests = 0, indep = 0;
@@ -1846,7 +1647,7 @@ __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_
     const int tid = threadIdx.x;
     const int bs = blockDim.x;
     const int64_t chunk = a.chunk_lo + blockIdx.x;
-    if (chunk >= a.cpre[a.n]) return;   // a launch sized by an upper bound (pipelined level loop)
+    if (chunk >= a.cpre[a.n]) return;   // (defensive: launches are sized by the exact prefix)
     int lo = chunk_node(a.cpre, a.n, chunk);
     const int x = lo;
     const int D = a.deg[x];
@@ -1935,7 +1736,6 @@ __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_
         uself[t] = 0;
         uprop[t] = 0;
     }
-    const int ng = (D - DM) / TG + 1;     // groups with g*TG <= D - d
     tgroup_pairs<DM, TG>(D, x, nxs, btab, ppre, pinfo, s_tx, s_np);
     // full-p mode with records (PCG_FLAG_RECORD): the recorded pairs (x, y) of this node, bit t.
     // Every live test of such a y goes to the exact path, which decides it with the reference's
@@ -1957,7 +1757,7 @@ __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_
     const Mask recm = s_recm;
     const double Cxx = a.diag[x];
     const uint64_t ntask = ppre[np];
-    const uint64_t spl = a.spl_dev ? (uint64_t)*a.spl_dev : (uint64_t)a.spl;
+    const uint64_t spl = (uint64_t)a.spl;
     const uint64_t r0 = (uint64_t)(chunk - a.cpre[x]) * (uint64_t)bs * spl;
     const uint64_t r1 = min(ntask, r0 + (uint64_t)bs * spl);
     unsigned long long tests = 0, indep = 0;
@@ -2537,7 +2337,7 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
     const int tid = threadIdx.x;
     const int bs = blockDim.x;
     const int64_t chunk = a.chunk_lo + blockIdx.x;
-    if (chunk >= a.cpre[a.n]) return;   // a launch sized by an upper bound (pipelined level loop)
+    if (chunk >= a.cpre[a.n]) return;   // (defensive: launches are sized by the exact prefix)
     int lo = chunk_node(a.cpre, a.n, chunk);
     const int x = lo;
     const int D = a.deg[x];
@@ -2630,7 +2430,6 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
         uself[t] = 0;
         uprop[t] = 0;
     }
-    const int ng = (D - DM) / TG + 1;
     tgroup_pairs<DM, TG>(D, x, nxs, btab, ppre, pinfo, s_tx, s_np);
     // records (PCG_FLAG_RECORD): the recorded pairs (x, y) of this node, bit t; every live test of
     // such a y goes to the exact path (decided and recorded there, as in k_level_lds_t)
@@ -2651,7 +2450,7 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
     const Mask recm = REC ? s_recm : (Mask)0;   // (threshold-mode builds: no record code in the sweep)
     const double Cxx = (double)(float)a.diag[x];                  // A~_xx
     const uint64_t ntask = ppre[np];
-    const uint64_t spl = a.spl_dev ? (uint64_t)*a.spl_dev : (uint64_t)a.spl;
+    const uint64_t spl = (uint64_t)a.spl;
     const uint64_t r0 = (uint64_t)(chunk - a.cpre[x]) * (uint64_t)bs * spl;
     constexpr int ABL = (DM == PCG_TGF_ABL_D && !WIDE) ? PCG_TGF_ABL : 0;
     const uint64_t r1 = (ABL & 2) ? r0 : min(ntask, r0 + (uint64_t)bs * spl);   // (ablation: no tasks)
@@ -3164,7 +2963,6 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
 // flags and both sides' unions as k_exact does, the band goes on to the exact path.
 template <int DM>
 __device__ __forceinline__ void screen_lanes(const LevelArgs &a, int blk, int nblk) {
-    // (volatile: in the fused barrier these counters were written by other blocks of this launch)
     const unsigned long long pushed = *(volatile const unsigned long long *)&a.ctr->screened;
     const int64_t count = (int64_t)min((unsigned long long)a.scr_cap, pushed);
     if (blk == 0 && threadIdx.x == 0 && (int64_t)pushed > a.scr_cap)
@@ -3211,86 +3009,10 @@ __global__ __launch_bounds__(256) void k_screen(LevelArgs a) {
     screen_lanes<DM>(a, blockIdx.x, gridDim.x);
 }
 
-// ---------------------------------------------------------------------------------------
-// Schur-prefix sweep (threshold mode, fp32 screen, narrow class, depths 3-4; PCG_SP).
-//
-// S = {c} + T with c < T[0] as in k_level_lds_f, T = {t0, (t1,) t}. A block owns a run of lane
-// tasks of one node x whose prefixes t0 take at most sp_pb(D) values; for each it stages
-//     P1 = C - w0 w0^T,  w0 = C[., t0] / sqrt(C[t0, t0])   (the Schur complement given t0)
-// over adj(x) + x, computed in fp64 from the compact block and rounded once to fp32. A lane task
-// = (t0, [t1,] t, candidate group): per y the sweep needs only the one or two Schur steps the
-// prefix does not cover (w_y = P1[y, t1] r1, q_y = (P1[y, t] - w_t w_y) rt) instead of the full
-// L_T^-1 projection of k_level_lds_f, and the task setup (r1, w, rt, q, lambda_c, u_c, c_xx)
-// runs in fp64 from the exact C entries (compact block, L2). The decision, its error bound
-// (|c^ - c| <= 18 u32 (1 + nu)^2, the same form as k_level_lds_f's), the rare path,
-// dedup and unions are k_level_lds_f's.
-#ifndef PCG_SP
-#define PCG_SP 0          // depths (bit 1 << d) whose narrow class runs k_level_sp (A/B; off: at depth 4
-                          // it measured 2.23-2.27 ms vs k_level_lds_f<4>'s 2.09 once both lost their
-                          // spills, at depth 3 0.78-0.81 vs 0.69 ms)
-#endif
-#ifndef PCG_SP_TG
-#define PCG_SP_TG 6       // candidates per lane task
-#endif
-#ifndef PCG_SP_PBUF
-#define PCG_SP_PBUF 32768 // LDS bytes for one block's fp32 P1 buffers
-#endif
-#ifndef PCG_SP_PBMAX
-#define PCG_SP_PBMAX 8    // prefixes t0 per block
-#endif
-#ifndef PCG_SP_MB
-#define PCG_SP_MB 4       // blocks per CU (launch bounds: 128 VGPRs)
-#endif
 #ifndef PCG_NODE_BLOCKS
 #define PCG_NODE_BLOCKS 0x10  // depths (bit 1 << d) whose fp32-screened narrow sweep stages compact node blocks
                               // (depth 4: kernel 2.13-2.16 -> 2.08 ms, FETCH 1.8 -> 0.18 GB; depth 3 measured no gain)
 #endif
-#ifndef PCG_SP_FAKE_SETUP
-#define PCG_SP_FAKE_SETUP 0
-#endif
-#ifndef PCG_SP_XCD
-#define PCG_SP_XCD 1      // XCD-contiguous chunk order (each XCD's L2 sees few nodes at a time)
-#endif
-constexpr int SP_DMAX = 64;
-static_assert(PCG_SP_TG == 4 || PCG_SP_TG == 6 || PCG_SP_TG == 8, "k_level_sp candidate groups of 4, 6 or 8");
-__host__ __device__ constexpr int sp_stride(int D) { return (D + 3) & ~3; }
-__host__ __device__ constexpr int sp_pb(int D) {
-    return PCG_SP_PBUF / (D * sp_stride(D) * 4) < 1 ? 1
-         : (PCG_SP_PBUF / (D * sp_stride(D) * 4) > PCG_SP_PBMAX ? PCG_SP_PBMAX : PCG_SP_PBUF / (D * sp_stride(D) * 4));
-}
-// (t1, t) pairs (depth 4) or t choices (depth 3) after prefix t0, and lane tasks of prefix t0
-__host__ __device__ inline int64_t sp_npair(int D, int DM, int t0) {
-    const int64_t m = D - 1 - t0;
-    if (t0 < 1 || m < DM - 2) return 0;
-    return DM == 4 ? m * (m - 1) / 2 : m;
-}
-__host__ __device__ inline int64_t sp_tasks(int D, int DM, int t0) {
-    return (int64_t)((t0 + PCG_SP_TG - 1) / PCG_SP_TG) * sp_npair(D, DM, t0);
-}
-// LDS layout (bytes) of k_level_sp for a node of degree D (offsets of the doubles, float2 and
-// float arrays stay 8-byte aligned: DS is a multiple of 4)
-struct SpLds {
-    int DS, PB;
-    size_t w0, cdg, pdx, pf, nxs, cell, total;
-};
-// a block's lane tasks run candidate-group major over its prefixes (cells (g, prefix) in that
-// order), so the lanes of a wave share the candidate window: at most ceil(64 / TG) groups x
-// PBMAX prefixes
-constexpr int SP_CMAX = ((SP_DMAX + PCG_SP_TG - 1) / PCG_SP_TG) * PCG_SP_PBMAX;
-__host__ __device__ inline SpLds sp_lds(int D, int mask_bytes) {
-    SpLds s{};
-    s.DS = sp_stride(D);
-    s.PB = sp_pb(D);
-    s.w0 = (size_t)3 * s.DS * mask_bytes;                         // lmask, uself, uprop
-    s.cdg = s.w0 + (size_t)8 * s.PB * (s.DS + 4);                 // w0[PB][DS + 4] (index D = x)
-    s.pdx = s.cdg + (size_t)16 * (s.DS + 4);                      // cdg[DS + 4], cxr[DS + 4]
-    s.pf = s.pdx + (size_t)8 * s.PB * s.DS;                       // Pdx[PB][DS] {P1_yy, P1_xy}
-    s.nxs = s.pf + (size_t)4 * s.PB * D * s.DS;                   // Pf[PB][D][DS]
-    s.cell = s.nxs + (size_t)4 * s.DS;                            // nxs[DS]
-    s.total = s.cell + (size_t)4 * (2 * SP_CMAX + 2);             // cell prefix [CMAX + 1], info [CMAX], count
-    return s;
-}
-
 // the per-node compact blocks of the nodes with a chunk in [s_lo, s_hi): C[adj(x) + x, adj(x) + x]
 // (row-major, stride D + 1, x last; each C entry read once, in C's own orientation) and the
 // local adjacency masks (bit k of row t: nbr t and nbr k adjacent)
@@ -3299,7 +3021,7 @@ __global__ __launch_bounds__(256) void k_node_blocks(LevelArgs a, int64_t s_lo, 
     if (a.cpre[x + 1] <= s_lo || a.cpre[x] >= s_hi || a.cpre[x + 1] == a.cpre[x]) return;
     const int D = a.deg[x];
     const int L = D + 1;
-    __shared__ int ids[SP_DMAX + 1];
+    __shared__ int ids[65];   // narrow nodes: D <= 64
     const int32_t *nx = a.nbr + a.off[x];
     for (int i = threadIdx.x; i < D; i += blockDim.x) ids[i] = nx[i];
     if (threadIdx.x == 0) ids[D] = x;
@@ -3319,485 +3041,6 @@ __global__ __launch_bounds__(256) void k_node_blocks(LevelArgs a, int64_t s_lo, 
     }
 }
 
-template <int DM>
-__global__ __launch_bounds__(256, PCG_SP_MB) void k_level_sp(LevelArgs a) {
-    using Mask = unsigned long long;
-    constexpr int DT = DM - 1;                                    // |T|
-    constexpr int TG = PCG_SP_TG;
-    constexpr int NP = TG / 2;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int tid = threadIdx.x;
-    int64_t bid = blockIdx.x;
-    if (PCG_SP_XCD) {   // workgroups go to the 8 XCDs round-robin: give each XCD a contiguous chunk range
-        const int64_t nbk = gridDim.x, q = nbk >> 3, r = nbk & 7, xcd = bid & 7, i = bid >> 3;
-        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + i;
-    }
-    const int64_t chunk = a.chunk_lo + bid;
-    if (chunk >= a.cpre[a.n]) return;   // a launch sized by an upper bound (pipelined level loop)
-    int lo = chunk_node(a.cpre, a.n, chunk);
-    const int x = lo;
-    const int D = a.deg[x];
-    const int L = D + 1;
-    const SpLds ly = sp_lds(D, 8);
-    const int DS = ly.DS;
-    Mask *lmask = reinterpret_cast<Mask *>(smem);
-    Mask *uself = lmask + DS;
-    Mask *uprop = uself + DS;
-    double *w0s = reinterpret_cast<double *>(smem + ly.w0);      // [PB][DS + 4]
-    double *cdg = reinterpret_cast<double *>(smem + ly.cdg);     // C(r, r), r = D: C(x, x)
-    double *cxr = cdg + DS + 4;                                   // C(x, r)
-    f2v *Pdx = reinterpret_cast<f2v *>(smem + ly.pdx);           // [PB][DS]
-    float *Pf = reinterpret_cast<float *>(smem + ly.pf);         // [PB][D * DS]
-    int32_t *nxs = reinterpret_cast<int32_t *>(smem + ly.nxs);
-    int32_t *cpre_ = reinterpret_cast<int32_t *>(smem + ly.cell);  // [SP_CMAX + 1]
-    int32_t *cinfo = cpre_ + SP_CMAX + 1;                          // g | b << 8 | j0 << 12
-    int32_t *s_ncell = cinfo + SP_CMAX;
-
-    const int64_t e = a.ctab[a.coff[D] + (chunk - a.cpre[x])];
-    const int t0s = (int)(e >> 40);
-    const int ks = (int)((e >> 20) & 0xFFFFF);
-    const int nt = (int)(e & 0xFFFFF);
-    // buffers: prefixes t0s, t0s + 1, ... until the chunk's tasks are covered (<= sp_pb(D))
-    int nb = 0;
-    {
-        int acc = 0;
-        for (int b = 0; b < PCG_SP_PBMAX && acc < nt; ++b) {
-            acc += (int)sp_tasks(D, DM, t0s + b) - (b == 0 ? ks : 0);
-            nb = b + 1;
-        }
-    }
-    if (tid == 0) {   // cells (g, b): the tasks of prefix t0s + b in candidate group g, g-major
-        int nc = 0, acc = 0;
-        const int gmax = (t0s + nb - 1 + TG - 1) / TG;
-        auto upto = [&](int b) {           // the chunk's tasks in prefixes t0s .. t0s + b - 1
-            int s = 0;
-            for (int q = 0; q < b; ++q) s += (int)sp_tasks(D, DM, t0s + q) - (q == 0 ? ks : 0);
-            return min(s, nt);
-        };
-        for (int g = 0; g < gmax; ++g)
-            for (int b = 0; b < nb; ++b) {
-                const int np_ = (int)sp_npair(D, DM, t0s + b);
-                const int klo = b == 0 ? ks : 0, khi = klo + (upto(b + 1) - upto(b));
-                const int lo_ = max(klo, g * np_), hi_ = min(khi, (g + 1) * np_);
-                if (hi_ <= lo_) continue;
-                cpre_[nc] = acc;
-                cinfo[nc] = g | (b << 8) | ((lo_ - g * np_) << 12);
-                acc += hi_ - lo_;
-                ++nc;
-            }
-        cpre_[nc] = acc;
-        *s_ncell = nc;
-    }
-    const double *cb = a.cblk + a.bo[x];
-    for (int i = tid; i < D; i += 256) {
-        nxs[i] = a.nbr[a.off[x] + i];
-        lmask[i] = a.lmk[a.off[x] + i];
-        uself[i] = 0;
-        uprop[i] = 0;
-    }
-    for (int r = tid; r < L; r += 256) {
-        cdg[r] = cb[r * L + r];
-        cxr[r] = cb[D * L + r];
-    }
-    for (int i = tid; i < nb * L; i += 256) {
-        const int b = i / L, r = i - b * L, t0 = t0s + b;
-        w0s[b * (DS + 4) + r] = cb[r * L + t0] / sqrt(cb[t0 * L + t0]);
-    }
-    if (tid < nb) {   // per prefix, in w0's padding: 1 / C(t0, t0) (= ||L_t0^-1||_F^2) and C(t0, t0)
-        const double g0 = cb[(t0s + tid) * L + t0s + tid];
-        w0s[tid * (DS + 4) + DS + 1] = 1.0 / g0;
-        w0s[tid * (DS + 4) + DS + 2] = g0;
-    }
-    __syncthreads();
-    {   // P1 in fp32: a wave per row t, lane = column k (D <= 64)
-        const int lane = tid & 63, wv = tid >> 6;
-        for (int t = wv; t < D; t += 4) {
-            const double v = lane < D ? cb[t * L + lane] : 0.0;
-            for (int b = 0; b < nb; ++b) {
-                const double *w = w0s + b * (DS + 4);
-                if (lane < DS) Pf[(b * D + t) * DS + lane] = lane < D ? (float)(v - w[t] * w[lane]) : 0.0f;
-                if (lane == 0) {
-                    const f2v dxv = {(float)(cdg[t] - w[t] * w[t]), (float)(cxr[t] - w[D] * w[t])};
-                    Pdx[b * DS + t] = dxv;
-                }
-            }
-        }
-    }
-    __syncthreads();
-    int tx = 0;
-    {
-        int lo2 = 0, hi2 = D;                 // first local index with global id > x
-        while (lo2 < hi2) {
-            const int mid = (lo2 + hi2) >> 1;
-            if (nxs[mid] < x) lo2 = mid + 1; else hi2 = mid;
-        }
-        tx = lo2;
-    }
-
-    unsigned long long tests = 0, indep = 0;
-    unsigned tcount = 0;
-    const unsigned long long lanebit = 1ull << (tid & 63);
-    const float inv_sf = (float)a.inv_s;
-    const float lo2f = (float)(a.lo2 * (1.0 - 4.0 * F32_U));
-    const float hi2f = (float)(a.hi2 * (1.0 + 4.0 * F32_U));
-    const f2v s2 = {(float)(a.s_amgm * (1.0 + 4.0 * F32_U)), (float)(a.s_amgm * (1.0 + 4.0 * F32_U))};
-    constexpr double RUd = 1.0 + 16.0 * F32_U;
-    const f2v ke2 = {(float)(2.0 * PCG_F32_KE * F32_U * RUd), (float)(2.0 * PCG_F32_KE * F32_U * RUd)};
-    const f2v ke2u = {(float)((2.0 * PCG_F32_KE + 1.0) * F32_U * RUd), (float)((2.0 * PCG_F32_KE + 1.0) * F32_U * RUd)};
-    const f2v inv_su = {(float)(a.inv_s * RUd), (float)(a.inv_s * RUd)};
-    const f2v tauu = {(float)(a.tau * RUd * RUd), (float)(a.tau * RUd * RUd)};
-    const f2v two_u = {(float)(2.0 * (1.0 + 8.0 * F32_U) * RUd), (float)(2.0 * (1.0 + 8.0 * F32_U) * RUd)};
-    const f2v one_u = {(float)((1.0 + 8.0 * F32_U) * RUd), (float)((1.0 + 8.0 * F32_U) * RUd)};
-    const f2v s2u = s2 + (float)F32_U;
-
-    const int ncell = *s_ncell;
-    for (int task = tid; task < nt; task += 256) {
-        int clo = 0, chi = ncell;
-        while (chi - clo > 1) {
-            const int mid = (clo + chi) >> 1;
-            if (cpre_[mid] <= task) clo = mid; else chi = mid;
-        }
-        const int info = cinfo[clo];
-        const int g = info & 255, b = (info >> 8) & 15;
-        const int j = (info >> 12) + (task - cpre_[clo]);
-        const int t0 = t0s + b;
-        int t1 = 0, t;
-        if constexpr (DM == 4) {   // colex pair (a_ < b_) of [0, D - 1 - t0): j = b_(b_-1)/2 + a_
-            int b_ = (int)((1.0f + __builtin_sqrtf(1.0f + 8.0f * (float)j)) * 0.5f);
-            while (b_ * (b_ - 1) / 2 > j) --b_;
-            while ((b_ + 1) * b_ / 2 <= j) ++b_;
-            t1 = t0 + 1 + (j - b_ * (b_ - 1) / 2);
-            t = t0 + 1 + b_;
-        } else {
-            t = t0 + 1 + j;
-        }
-        const int cbase = g * TG;
-        const int nval = min(t0 - cbase, TG);
-        int nmax_ = 1;
-#pragma unroll
-        for (int q = 2; q <= TG; ++q) nmax_ += (__ballot(nval >= q) != 0);
-        const int nmax = __builtin_amdgcn_readfirstlane(nmax_);
-        Mask Tmask = ((Mask)1 << t0) | ((Mask)1 << t);
-        if constexpr (DM == 4) Tmask |= (Mask)1 << t1;
-        const double *w0 = w0s + b * (DS + 4);
-        const float *Pb = Pf + (size_t)b * D * DS;
-        const f2v *Pdxb = Pdx + b * DS;
-
-        // task setup in fp64 from the exact C entries (P1(r, s) = C(r, s) - w0_r w0_s)
-#if PCG_SP_FAKE_SETUP   // timing experiment only (wrong precision): C entries from the fp32 P1 buffer
-#define SPC(r_, s_) ((double)Pb[(r_) * DS + (s_)] + w0[r_] * w0[s_])
-#else
-#define SPC(r_, s_) cb[(r_) * L + (s_)]
-#endif
-        const double g0 = w0[DS + 2];
-        const double liF0 = w0[DS + 1];
-        double r1 = 0.0, wt = 0.0, wx = 0.0, liF1 = liF0, g1 = 1.0;
-        if constexpr (DM == 4) {
-            const double p11 = cdg[t1] - w0[t1] * w0[t1];
-            r1 = rsq_nr(p11);
-            wt = (SPC(t, t1) - w0[t] * w0[t1]) * r1;
-            wx = (cxr[t1] - w0[D] * w0[t1]) * r1;
-            liF1 = liF0 + (liF0 * w0[t1] * w0[t1] + 1.0) * r1 * r1;
-            g1 = p11;
-        }
-        const double lt2 = cdg[t] - w0[t] * w0[t] - wt * wt;
-        const double rt = rsq_nr(lt2);
-        const double qx = (cxr[t] - w0[D] * w0[t] - wx * wt) * rt;
-        const double pxx = cdg[D] - w0[D] * w0[D] - wx * wx - qx * qx;
-        const double liF = liF1 + (liF1 * (w0[t] * w0[t] + wt * wt) + 1.0) * rt * rt;
-        const bool okT = g0 > 0.0 && g1 > 0.0 && lt2 > 0.0;
-        const double gT = fmin(fmin(g0, g1), lt2);
-        const float r1f = (float)r1, wtf = (float)wt, rtf = (float)rt, wxf = (float)wx, qxf = (float)qx;
-        f2v wcp[NP], qcp[NP], rlp[NP], ucp[NP], mp[NP], hhp[NP], k1p[NP], k2p[NP];
-        bool okc[TG];
-        f2v cxp[NP], l2p[NP], r2p[NP], llp[NP];
-        bool vldc[TG];
-#pragma unroll
-        for (int q = 0; q < NP; ++q) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int jj = 2 * q + h;
-                wcp[q][h] = qcp[q][h] = rlp[q][h] = ucp[q][h] = 0.0f;
-                cxp[q][h] = l2p[q][h] = r2p[q][h] = llp[q][h] = 0.0f;
-                vldc[jj] = false;
-                if (jj < nmax) {                      // wave-uniform
-                    const int c = cbase + jj;
-                    const bool valid = c < t0;
-                    const int cc = valid ? c : 0;
-                    double wc = 0.0;
-                    if constexpr (DM == 4) wc = (SPC(cc, t1) - w0[cc] * w0[t1]) * r1;
-                    const double qc = (SPC(cc, t) - w0[cc] * w0[t] - wc * wt) * rt;
-                    const double lam2 = cdg[cc] - w0[cc] * w0[cc] - wc * wc - qc * qc;
-                    const double r = rsq_nr(lam2);
-                    const double u = (cxr[cc] - w0[D] * w0[cc] - wx * wc - qx * qc) * r;
-                    wcp[q][h] = (float)wc;
-                    qcp[q][h] = (float)qc;
-                    rlp[q][h] = (float)r;
-                    ucp[q][h] = (float)u;
-                    cxp[q][h] = (float)(pxx - u * u);
-                    l2p[q][h] = (float)lam2;
-                    r2p[q][h] = (float)(r * r);
-                    llp[q][h] = (float)(cdg[cc] - lam2);  // |l_c|^2: explained by T
-                    vldc[jj] = valid && okT && (lam2 > 0.0);
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        const float liFf = (float)(liF * RUd);
-        const float gTf = (float)gT * (1.0f - (float)(4.0 * F32_U));
-#pragma unroll
-        for (int q = 0; q < NP; ++q) {   // decision bounds: k_level_lds_f's, term for term
-            const f2v cxf = cxp[q], l2f = l2p[q], r2f = r2p[q], llf = llp[q];
-            constexpr float U = (float)F32_U;
-            constexpr float RD = 1.0f - 16.0f * U, U8 = 8.0f * U;
-            const f2v one = {1.0f, 1.0f};
-            const f2v liF2 = {liFf, liFf};
-            const f2v nu2 = __builtin_elementwise_fma(__builtin_elementwise_fma(liF2, llf, one), r2f, liF2);
-            const f2v E = __builtin_elementwise_fma(nu2, ke2, ke2u);
-            const f2v te = E * inv_su;
-            const f2v gT2 = {gTf, gTf};
-            const f2v gg = (__builtin_elementwise_min(gT2, l2f) - (E + 2.0f * U)) * RD;
-            const f2v cmE = (cxf - E) * RD;
-            const f2v rg = {__builtin_amdgcn_rcpf(gg[0]), __builtin_amdgcn_rcpf(gg[1])};
-            const f2v kg = tauu * rg;
-            const f2v hx = hi2f * (cxf + E);
-            const f2v f1 = __builtin_elementwise_fma(te, two_u, one_u);
-            const f2v al = hx * f1;
-            const f2v be = E * (hx + s2) * f1;
-            const f2v ga = (cmE - cmE * te) * ((1.0f - U8) * RD);
-            const f2v ka = __builtin_elementwise_fma(E, cxf + s2u, kg) * ((1.0f + U8) * (1.0f + 16.0f * U));
-            const f2v mm = 0.5f * (al + ga);
-            const f2v hw = __builtin_elementwise_fma(-2.0f * U8 * one, ga, 0.5f * (ga - al));
-            const f2v kk1 = 0.5f * (be - ka);
-            const f2v kk2 = (be + ka) * (0.5f * (1.0f + U8));
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const bool ok = vldc[2 * q + h] && (te[h] <= 0.5f) && (cmE[h] > 0.0f) && (gg[h] > 0.0f) && (ga[h] > al[h]);
-                okc[2 * q + h] = ok;
-                // an unusable candidate always passes the sweep's compare (|c_xy^2| < 3e38): its
-                // lanes take the rare path through `notok`, whose per-candidate check reads okc
-                mp[q][h] = ok ? mm[h] : 0.0f;
-                hhp[q][h] = ok ? hw[h] : 0.0f;
-                k1p[q][h] = ok ? kk1[h] : 0.0f;
-                k2p[q][h] = ok ? kk2[h] : -3.0e38f;
-            }
-            // opaque: the rare path must read these registers, not keep (spill) the unselected values
-            asm volatile("" : "+v"(mp[q]), "+v"(hhp[q]), "+v"(k1p[q]), "+v"(k2p[q]));
-        }
-        const int cend = min(t0, cbase + TG);
-        unsigned okm = 0;
-#pragma unroll
-        for (int jj = 0; jj < TG; ++jj) okm |= (unsigned)okc[jj] << jj;
-        const unsigned vmask = (1u << (cend - cbase)) - 1u;
-        constexpr bool SG = (PCG_TGF_SGPR >> DM) & 1;
-        unsigned long long okv[TG];
-        if (SG) tcount += (unsigned)(nval * (D - DT - 1));
-#pragma unroll
-        for (int jj = 0; jj < TG; ++jj) okv[jj] = __builtin_amdgcn_ballot_w64(okc[jj]);
-        const unsigned long long notok = __builtin_amdgcn_ballot_w64((vmask & ~okm) != 0u);
-        const int cb0 = __builtin_amdgcn_readfirstlane(cbase);
-        const bool uni = __builtin_amdgcn_ballot_w64(cbase != cb0) == 0ull;
-
-        // a live test of candidate jj at y = ty that the sweep's check did not make certain
-        auto rare_cand = [&](int jj, int ty, const float *Pr, float wy, float qy, float byy, float bxy, Mask lm) {
-            const int q = jj >> 1, h = jj & 1;
-            int c = cbase + jj;
-            asm volatile("" : "+v"(c));      // no per-candidate masks / ids hoisted into the hot loop
-            if (okc[jj]) {
-                float s_ = Pr[c];
-                if constexpr (DM == 4) s_ = fmaf(-wcp[q][h], wy, s_);
-                s_ = fmaf(-qcp[q][h], qy, s_);
-                const float vc = s_ * rlp[q][h];
-                const float cyy = fmaf(-vc, vc, byy);
-                const float cxy = fmaf(-ucp[q][h], vc, bxy);
-                const float w = fmaf(-mp[q][h], cyy, fmaf(cxy, cxy, -k1p[q][h]));
-                if (__builtin_fabsf(w) < fmaf(hhp[q][h], cyy, -k2p[q][h])) return;
-                constexpr float U8 = (float)(8.0 * F32_U);
-                float m_ = mp[q][h], hh_ = hhp[q][h], k1_ = k1p[q][h], k2_ = k2p[q][h];
-                asm volatile("" : "+v"(m_), "+v"(hh_), "+v"(k1_), "+v"(k2_));
-                const float Alb = (m_ + hh_) * (1.0f - U8);
-                const float Eub = (k1_ + k2_) * inv_sf * (1.0f + U8);
-                const float kgub = (k2_ - k1_) * (1.0f + U8);
-                const float ay = (cyy - Eub) * (1.0f - U8);
-                const float ax = (__builtin_fabsf(cxy) + Eub) * (1.0f + U8);
-                if (ay > 0.0f && ax * ax * (1.0f + U8) < lo2f * Alb * ay &&
-                    fmaf(ax, ax, kgub) * (1.0f + U8) < Alb * ay) {
-                    const Mask Smask = Tmask | ((Mask)1 << c);
-                    ++indep;
-                    lmask_atomic_or<false>(&uself[ty], Smask);
-                    if (((lm & Smask) == Smask) && ty >= tx) lmask_atomic_or<false>(&uprop[ty], Smask);
-                    return;
-                }
-            }
-            int sg[DM];
-            sg[0] = nxs[c];
-            sg[1] = nxs[t0];
-            if constexpr (DM == 4) sg[2] = nxs[t1];
-            sg[DM - 1] = nxs[t];
-            push_screen(a, x, nxs[ty], sg, DM);
-        };
-        auto sweep = [&](auto nc_tag) {
-            constexpr int NC = decltype(nc_tag)::value;
-            constexpr int NQ = NC / 2;
-            auto ystep = [&](int ty, auto ym_tag) {
-                constexpr int YM = decltype(ym_tag)::value;
-                const float *Pr = Pb + ty * DS;
-                f2v sc[NQ];
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) sc[q] = *reinterpret_cast<const f2v *>(Pr + cbase + 2 * q);
-                float wy = 0.0f, qy;
-                f2v b2 = Pdxb[ty];                     // {P1_yy, P1_xy}
-                if constexpr (DM == 4) {
-                    wy = Pr[t1] * r1f;
-                    qy = fmaf(-wtf, wy, Pr[t]) * rtf;
-                    const f2v wv = {wy, wxf}, wb = {wy, wy};
-                    b2 = __builtin_elementwise_fma(-wv, wb, b2);
-                } else {
-                    qy = Pr[t] * rtf;
-                }
-                {
-                    const f2v qv = {qy, qxf}, qb = {qy, qy};
-                    b2 = __builtin_elementwise_fma(-qv, qb, b2);
-                }
-                const float byy = b2[0];
-                const float bxy = b2[1];
-                const f2v qb = {qy, qy};
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    if constexpr (DM == 4) {
-                        const f2v wb = {wy, wy};
-                        sc[q] = __builtin_elementwise_fma(-wcp[q], wb, sc[q]);
-                    }
-                    sc[q] = __builtin_elementwise_fma(-qcp[q], qb, sc[q]);
-                }
-                const f2v byy2 = {byy, byy}, bxy2 = {bxy, bxy};
-                const Mask lm = lmask[ty];
-                if constexpr (YM == 3) {
-                    unsigned dp = 0;
-#pragma unroll
-                    for (int q = 0; q < NQ; ++q) {
-                        const f2v vc = sc[q] * rlp[q];
-                        const f2v cyy = __builtin_elementwise_fma(-vc, vc, byy2);
-                        const f2v cxy = __builtin_elementwise_fma(-ucp[q], vc, bxy2);
-                        const f2v nm = __builtin_elementwise_fma(cxy, cxy, -k1p[q]);
-                        const f2v w = __builtin_elementwise_fma(-mp[q], cyy, nm);
-                        const f2v hh = __builtin_elementwise_fma(hhp[q], cyy, -k2p[q]);
-                        dp |= ((unsigned)(__builtin_fabsf(w[0]) < hh[0]) << (2 * q)) |
-                              ((unsigned)(__builtin_fabsf(w[1]) < hh[1]) << (2 * q + 1));
-                    }
-                    const bool inTset = (bool)((Tmask >> ty) & 1u);
-                    const bool own = (ty < tx) && ((lm & Tmask) == Tmask);
-                    const unsigned tb = ((unsigned)(ty - cbase) < (unsigned)TG) ? (1u << (ty - cbase)) : 0u;
-                    const unsigned skip = own ? (unsigned)(lm >> cbase) : 0u;
-                    const unsigned live = inTset ? 0u : (vmask & ~tb & ~skip);
-                    tcount += __popc(live);
-                    const unsigned rare = live & ~(dp & okm);
-                    if (__builtin_amdgcn_ballot_w64(rare != 0u)) {
-                        if (rare) {
-#pragma unroll
-                            for (int jj = 0; jj < TG; ++jj)
-                                if ((rare >> jj) & 1u) rare_cand(jj, ty, Pr, wy, qy, byy, bxy, lm);
-                        }
-                    }
-                    return;
-                } else {
-                    // YM 0: no candidate of the window is y; YM 1: candidate ty - cb0 (the same in
-                    // every lane) is y and is skipped; YM 2: windows differ, lanes whose window
-                    // holds y take the rare path. dall = lanes where every candidate is certainly
-                    // dependent (unusable ones always pass, see the setup)
-                    const int jdead = YM == 1 ? ty - cb0 : -1;
-                    unsigned long long dall = ~0ull;
-#pragma unroll
-                    for (int q = 0; q < NQ; ++q) {
-                        const f2v vc = sc[q] * rlp[q];
-                        const f2v cyy = __builtin_elementwise_fma(-vc, vc, byy2);
-                        const f2v cxy = __builtin_elementwise_fma(-ucp[q], vc, bxy2);
-                        const f2v nm = __builtin_elementwise_fma(cxy, cxy, -k1p[q]);
-                        const f2v w = __builtin_elementwise_fma(-mp[q], cyy, nm);
-                        const f2v hh = __builtin_elementwise_fma(hhp[q], cyy, -k2p[q]);
-                        const unsigned long long d0 = __builtin_amdgcn_ballot_w64(__builtin_fabsf(w[0]) < hh[0]);
-                        const unsigned long long d1 = __builtin_amdgcn_ballot_w64(__builtin_fabsf(w[1]) < hh[1]);
-                        if (YM == 1) {
-                            dall &= 2 * q == jdead ? ~0ull : d0;
-                            dall &= 2 * q + 1 == jdead ? ~0ull : d1;
-                        } else {
-                            dall &= d0 & d1;
-                        }
-                    }
-                    // lanes that need the per-lane path; y in T is masked only when some lane does
-                    unsigned long long rarel = (~dall & __builtin_amdgcn_read_exec()) | notok;
-                    if (YM == 2) rarel |= __builtin_amdgcn_ballot_w64((unsigned)(ty - cbase) < (unsigned)nval);
-                    if (ty < tx) rarel |= __builtin_amdgcn_ballot_w64((lmask[ty] & Tmask) == Tmask);
-                    if (!rarel) return;
-                    rarel &= ~__builtin_amdgcn_ballot_w64((bool)((Tmask >> ty) & 1u));
-                    if (!(rarel & lanebit)) return;
-                    const bool own = (ty < tx) && ((lm & Tmask) == Tmask);
-                    const unsigned tb = ((unsigned)(ty - cbase) < (unsigned)TG) ? (1u << (ty - cbase)) : 0u;
-                    const unsigned skip = own ? (unsigned)(lm >> cbase) : 0u;
-                    if ((Tmask >> ty) & 1u) return;
-                    const unsigned live = vmask & ~tb & ~skip;
-                    tcount -= __popc(vmask & ~tb & skip);
-#pragma unroll
-                    for (int jj = 0; jj < TG; ++jj)
-                        if ((live >> jj) & 1u) rare_cand(jj, ty, Pr, wy, qy, byy, bxy, lm);
-                }
-            };
-            using Y0 = std::integral_constant<int, 0>;
-            using Y1 = std::integral_constant<int, 1>;
-            using Y2 = std::integral_constant<int, 2>;
-            using Y3 = std::integral_constant<int, 3>;
-            if (!SG) {
-                for (int ty = 0; ty < D; ++ty) ystep(ty, Y3{});
-            } else if (uni) {   // y outside the shared window [cb0, cb0 + NC) needs no dead candidate
-                const int w0_ = min(cb0, D), w1_ = min(cb0 + NC, D);
-                for (int ty = 0; ty < w0_; ++ty) ystep(ty, Y0{});
-                for (int ty = w0_; ty < w1_; ++ty) ystep(ty, Y1{});
-                for (int ty = w1_; ty < D; ++ty) ystep(ty, Y0{});
-            } else {
-                for (int ty = 0; ty < D; ++ty) ystep(ty, Y2{});
-            }
-        };
-        if constexpr (TG == 4) {
-            if (nmax > 2) sweep(std::integral_constant<int, 4>{});
-            else sweep(std::integral_constant<int, 2>{});
-        } else if constexpr (TG == 6) {
-            if (nmax > 4) sweep(std::integral_constant<int, 6>{});
-            else if (nmax > 2) sweep(std::integral_constant<int, 4>{});
-            else sweep(std::integral_constant<int, 2>{});
-        } else {
-            if (nmax > 6) sweep(std::integral_constant<int, 8>{});
-            else if (nmax > 4) sweep(std::integral_constant<int, 6>{});
-            else if (nmax > 2) sweep(std::integral_constant<int, 4>{});
-            else sweep(std::integral_constant<int, 2>{});
-        }
-        tests += tcount;
-        tcount = 0;
-    }
-    __syncthreads();
-    for (int ty = tid; ty < D; ty += 256) {
-        const Mask us = uself[ty], up = uprop[ty];
-        if (!(us | up)) continue;
-        const int yg = nxs[ty];
-        a.rm[(int64_t)x * a.n + yg] = 1;
-        a.rm[(int64_t)yg * a.n + x] = 1;
-        for (int side = 0; side < 2; ++side) {
-            const Mask bits = side ? up : us;
-            if (!bits) continue;
-            const int64_t slot = side ? (int64_t)a.off[yg] + find_in_sorted(a.nbr + a.off[yg], a.deg[yg], x)
-                                      : (int64_t)a.off[x] + ty;
-            unsigned long long *row = reinterpret_cast<unsigned long long *>(a.ug + slot * a.W);
-            unsigned long long m = bits;
-            while (m) {
-                const int bb = __ffsll((long long)m) - 1;
-                const int gid = nxs[bb];
-                atomicOr(&row[gid >> 6], 1ull << (gid & 63));
-                m &= m - 1;
-            }
-        }
-    }
-    block_flush_counts(a.ctr, tests, indep);
-}
-
 // ---------------------------------------------------------------------------------------
 // depths > PCG_MAX_DEPTH (degenerate graphs, e.g. constant columns whose NaN correlations
 // never separate): one thread per (x, S rank), exact LU path per test with per-thread
@@ -3815,7 +3058,7 @@ __global__ __launch_bounds__(64) void k_level_deep(LevelArgs a, double *scratch,
     unsigned long long tests = 0, nindep = 0;
     for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
         const int64_t chunk = a.chunk_lo + c;
-        if (chunk >= a.cpre[a.n]) break;    // (a bound-sized chunk range, pipelined level loop)
+        if (chunk >= a.cpre[a.n]) break;    // (defensive)
         int lo = chunk_node(a.cpre, a.n, chunk);
         const int x = lo;
         const int D = a.deg[x];
@@ -3912,216 +3155,15 @@ __device__ __forceinline__ void set_members(unsigned long long mask, const int32
     }
 }
 
+// The factorisation is shared between consecutive sets. A wave walks its run of colex ranks; the
+// colex successor (Gosper) changes only the LOWEST elements of S, so the steps run in DESCENDING
+// element order: steps 0..k-1 (the elements above the highest changed bit) and every lane's solve
+// values, pivot, |v|^2 and u.v prefixes up to them stay valid, and only the steps of the changed
+// low elements are redone — ~1-2 steps per set instead of |S| (round 3: the per-set
+// factorisation, removed in round 5, measured slower on every deep level). The guard uses the
+// smallest pivot^2 of this factorisation order.
 template <int MD, int MODE>
 __global__ __launch_bounds__(256) void k_level_wave(LevelArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, wv = tid >> 6;
-    const int64_t chunk = a.chunk_lo + blockIdx.x;
-    if (chunk >= a.cpre[a.n]) return;   // a launch sized by an upper bound (pipelined level loop)
-    int lo = chunk_node(a.cpre, a.n, chunk);
-    const int x = lo;
-    const int D = a.deg[x];
-    const int d = a.d;
-    const int32_t *nxg = a.nbr + a.off[x];
-
-    double *M = reinterpret_cast<double *>(smem);                 // D * D
-    double *Mx = M + D * D;                                       // D
-    double *Md = Mx + D;                                          // D
-    unsigned long long *lmask = reinterpret_cast<unsigned long long *>(Md + D);   // D
-    unsigned long long *uself = lmask + D;                        // D
-    unsigned long long *uprop = uself + D;                        // D
-    int32_t *nxs = reinterpret_cast<int32_t *>(uprop + D);       // D
-    int *s_tx = nxs + D;                                          // 1
-    // the wave's LDS slot (L rows; the exact path's matrix beyond PCG_MAX_DEPTH)
-    double *slot = reinterpret_cast<double *>(smem + a.lds_btab_off) + (size_t)wv * WAVE_SLOT_DOUBLES(MD);
-
-    for (int i = tid; i < D; i += blockDim.x) nxs[i] = nxg[i];
-    __syncthreads();
-    for (int e = tid; e < D * D; e += blockDim.x) {
-        const int t = e / D, k = e - t * D;
-        M[e] = a.C[(int64_t)nxs[t] * a.ldc + nxs[k]];
-    }
-    stage_lmask(a, nxs, D, lmask);
-    for (int t = tid; t < D; t += blockDim.x) {
-        const int yg = nxs[t];
-        Mx[t] = a.C[(int64_t)x * a.ldc + yg];
-        Md[t] = a.diag[yg];
-        uself[t] = 0;
-        uprop[t] = 0;
-    }
-    if (tid < 64) {                   // #neighbours below x (nxs ascends; D <= 64 here)
-        const int c = __popcll(__ballot(tid < D && nxs[tid] < x));
-        if (tid == 0) *s_tx = c;
-    }
-    __syncthreads();
-    const int tx = *s_tx;
-    const double Cxx = a.diag[x];
-    const uint64_t nS = pcg_binom(a.binom, D, d);
-    const uint64_t spl = a.spl_dev ? (uint64_t)*a.spl_dev : (uint64_t)a.spl;
-    const uint64_t r0 = (uint64_t)(chunk - a.cpre[x]) * 4u * spl + (uint64_t)wv * spl;
-    const uint64_t r1 = min(nS, r0 + spl);
-    unsigned long long tests = 0, indep = 0;
-    if (r0 < r1) {
-        unsigned long long mask = 0;      // colex unrank of r0 (wave-uniform)
-        {
-            uint64_t rr = r0;
-            int hi_ = D;
-            for (int ii = d - 1; ii >= 0; --ii) {
-                int lo_ = ii, up = hi_ - 1;
-                while (lo_ < up) {
-                    const int mid = (lo_ + up + 1) >> 1;
-                    if (pcg_binom(a.binom, mid, ii + 1) <= rr) lo_ = mid; else up = mid - 1;
-                }
-                mask |= 1ull << lo_;
-                rr -= pcg_binom(a.binom, lo_, ii + 1);
-                hi_ = lo_;
-            }
-        }
-        const int cl = lane < D ? lane : 0;            // lane D (x) and idle lanes: a safe column
-        double *Lm = slot;                             // L rows of the current set: Lm[i * LS + q]
-        constexpr int LS = MD + 1;
-        for (uint64_t rank = r0; rank < r1; ++rank) {
-            double v[MD];
-            double vv = 0.0, uv = 0.0, gmin = 1.0;
-            bool ok = true;
-            unsigned long long m = mask;
-            // S position of this lane's column when it is a member (row of L it produces)
-            const bool member = lane < D && ((mask >> lane) & 1ull);
-            const int mypos = member ? __popcll(mask & ((1ull << lane) - 1ull)) : -1;
-#pragma unroll
-            for (int i = 0; i < MD; ++i) {
-                if (i < d) {                           // wave-uniform (no break: the loop stays unrolled)
-                    const int si = __builtin_ctzll(m); // S_i, wave-uniform
-                    m &= m - 1;
-                    double t = lane < D ? M[si * D + cl] : Mx[si];
-                    const double *Li = Lm + i * LS;    // row i of L (written by lane S_i, steps q < i)
-#pragma unroll
-                    for (int q = 0; q < i; ++q) t -= Li[q] * v[q];
-                    const double piv = readlane_f64(t, si);
-                    ok = ok && (piv > 0.0);
-                    gmin = fmin(gmin, piv);
-                    v[i] = t * (1.0 / sqrt(piv));
-                    vv += v[i] * v[i];
-                    uv += readlane_f64(v[i], D) * v[i];
-                    if (mypos > i) Lm[mypos * LS + i] = v[i];   // L[mypos][i] for the later steps
-                    wave_sync();
-                }
-            }
-            const double cxx = Cxx - readlane_f64(vv, D);
-            const double kg = a.tau / gmin;
-            bool live = lane < D && !((mask >> lane) & 1ull);
-            const unsigned long long lm = live ? lmask[cl] : 0ull;
-            const bool in_y = (lm & mask) == mask;
-            live = live && !(lane < tx && in_y);
-            tests += live;
-            int dec = 2;
-            double p = 0.0;
-            if (live && ok) dec = decide<MODE>(a, Mx[cl] - uv, cxx, Md[cl] - vv, kg, &p);
-            if (live && dec == 1) {
-                ++indep;
-                atomicOr(&uself[cl], mask);
-                if (in_y && lane >= tx) atomicOr(&uprop[cl], mask);
-            }
-            if (MODE == MODE_FULLP && live && dec != 2) {
-                const int yg = nxs[cl];
-                const int lo_ = x < yg ? x : yg, hi_ = x < yg ? yg : x;
-                const bool near = fabs(p - a.alpha) < 1e-9;
-                if (d <= PCG_MAX_DEPTH && (near || rec_on(a, lo_, hi_))) {
-                    int sg[PCG_MAX_DEPTH];
-                    set_members(mask, nxs, sg);
-                    if (rec_on(a, lo_, hi_)) push_record(a.records, a.rec_cap, &a.ctr->records, lo_, hi_, d, sg, p);
-                    if (near) push_record(a.nearl, a.near_cap, &a.ctr->near_alpha, lo_, hi_, d, sg, p);
-                } else if (near) {
-                    atomicAdd(&a.ctr->near_alpha, 1ull);   // counts only beyond PCG_MAX_DEPTH
-                }
-            }
-            if (d <= PCG_MAX_DEPTH) {
-                if (live && dec == 2) {
-                    int sg[PCG_MAX_DEPTH];
-                    set_members(mask, nxs, sg);
-                    push_deferred(a, x, nxs[cl], sg, d);
-                }
-            } else {
-                // the exact LU of each remaining test, one at a time in the wave's LDS slot
-                unsigned long long need = __ballot(live && dec == 2);
-                const int mm = d + 2;
-                double *A = slot, *B0 = slot + mm * mm, *B1 = B0 + mm;
-                int *var = reinterpret_cast<int *>(B1 + mm);   // mm ints after the two columns
-                while (need) {
-                    const int L = __builtin_ctzll(need);
-                    need &= need - 1;
-                    const int yg = nxs[L];
-                    wave_sync();
-                    if (lane < D && ((mask >> lane) & 1ull))      // S members in ascending order
-                        var[2 + __popcll(mask & ((1ull << lane) - 1ull))] = nxs[lane];
-                    if (lane == 0) {
-                        var[0] = x < yg ? x : yg;
-                        var[1] = x < yg ? yg : x;
-                    }
-                    wave_sync();
-                    for (int k = lane; k < mm * mm; k += 64) {
-                        const int r = k / mm, c = k - r * mm;
-                        A[k] = a.C[(int64_t)var[r] * a.ldc + var[c]];
-                    }
-                    wave_sync();
-                    if (lane == 0) {
-                        double pv = __builtin_nan("");
-                        const int err = exact_lu_pvalue(A, mm, B0, B1, a.sqrt_dof, &pv);
-                        atomicAdd(&a.ctr->exact, 1ull);
-                        if (err) {
-                            flag_error(a, err);
-                        } else {
-                            if (fabs(pv - a.alpha) < 1e-9) atomicAdd(&a.ctr->near_alpha, 1ull);
-                            if (pv > a.alpha) {
-                                ++indep;
-                                atomicOr(&uself[L], mask);
-                                if (((lmask[L] & mask) == mask) && L >= tx) atomicOr(&uprop[L], mask);
-                            }
-                        }
-                    }
-                }
-            }
-            // next set in colex order (Gosper: the next larger 64-bit word with |S| bits)
-            const unsigned long long c0 = mask & (0ull - mask);
-            const unsigned long long rr = mask + c0;
-            mask = (((rr ^ mask) >> 2) >> __builtin_ctzll(mask)) | rr;
-        }
-    }
-    __syncthreads();
-    // flush unions (local bits -> global node bits) and removal flags
-    for (int t = tid; t < D; t += blockDim.x) {
-        const unsigned long long us = uself[t], up = uprop[t];
-        if (!(us | up)) continue;
-        const int yg = nxs[t];
-        a.rm[(int64_t)x * a.n + yg] = 1;
-        a.rm[(int64_t)yg * a.n + x] = 1;
-        for (int side = 0; side < 2; ++side) {
-            unsigned long long mb = side ? up : us;
-            if (!mb) continue;
-            const int64_t s = side ? (int64_t)a.off[yg] + find_in_sorted(a.nbr + a.off[yg], a.deg[yg], x)
-                                   : (int64_t)a.off[x] + t;
-            unsigned long long *row = reinterpret_cast<unsigned long long *>(a.ug + s * a.W);
-            while (mb) {
-                const int b = __ffsll((long long)mb) - 1;
-                const int g = nxs[b];
-                atomicOr(&row[g >> 6], 1ull << (g & 63));
-                mb &= mb - 1;
-            }
-        }
-    }
-    block_flush_counts(a.ctr, tests, indep);
-}
-
-// k_level_wave with the factorisation shared between consecutive sets. A wave walks its run of
-// colex ranks; the colex successor (Gosper) changes only the LOWEST elements of S, so the steps
-// run in DESCENDING element order: steps 0..k-1 (the elements above the highest changed bit) and
-// every lane's solve values, pivot, |v|^2 and u.v prefixes up to them stay valid, and only the
-// steps of the changed low elements are redone — ~1-2 steps per set instead of |S|. Same tests,
-// same memo and union bookkeeping, same decision (threshold band, guard on the smallest pivot^2
-// of this factorisation order) and exact path as k_level_wave.
-template <int MD, int MODE>
-__global__ __launch_bounds__(256) void k_level_wave_pr(LevelArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6;
@@ -4167,7 +3209,7 @@ __global__ __launch_bounds__(256) void k_level_wave_pr(LevelArgs a) {
     const int tx = *s_tx;
     const double Cxx = a.diag[x];
     const uint64_t nS = pcg_binom(a.binom, D, d);
-    const uint64_t spl = a.spl_dev ? (uint64_t)*a.spl_dev : (uint64_t)a.spl;
+    const uint64_t spl = (uint64_t)a.spl;
     const uint64_t r0 = (uint64_t)(chunk - a.cpre[x]) * 4u * spl + (uint64_t)wv * spl;
     const uint64_t r1 = min(nS, r0 + spl);
     unsigned long long tests = 0, indep = 0;
@@ -4494,101 +3536,6 @@ __global__ __launch_bounds__(256) void k_exact(LevelArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
-// The fused level barrier (single GPU): the fp32 sweep's fp64 screen, the exact path, the
-// removals (SkeletonDiscovery.py:141-144) and the next graph's summary + CSR in ONE launch of
-// FUSE_BLOCKS persistent blocks, its phases separated by grid barriers instead of four dependent
-// kernel launches (each a dispatch gap plus a ramp on an almost empty grid).
-//
-// Grid barrier: a self-resetting arrival count and a generation word in device memory. Block
-// leader: read gen, fence, add 1 to count; the last arrival zeroes count and bumps gen, the
-// others spin on gen. Every block of the grid is co-resident (FUSE_BLOCKS = one per CU, 256
-// threads, <= 64 KB LDS), so the spin always ends; it is bounded anyway: a leader that waits
-// ~1 s raises `abort`, every waiter leaves, the summary carries status byte 4 and the host
-// fails the level with PCG_ERR_HIP and clears the barrier words.
-constexpr int FUSE_BLOCKS = 256;
-struct GridBar {
-    unsigned count, gen, abort, pad;
-};
-
-__device__ bool grid_sync(GridBar *g, unsigned nblk) {
-    // every wave's stores have reached its XCD's L2 (gfx9 counts stores in vmcnt) before the
-    // leader's single agent-scope release writes the L2 back; the leader then polls with relaxed
-    // loads (an acquire per poll would invalidate the XCD's L2 on every iteration) and acquires
-    // once. (Measured first form: every thread fenced and every poll acquired, ~25-50 us per
-    // barrier.)
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    __shared__ int ok_s;
-    if (threadIdx.x == 0) {
-        int ok = 1;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        const unsigned gen = __hip_atomic_load(&g->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned arrived = __hip_atomic_fetch_add(&g->count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (arrived == nblk - 1) {
-            (void)__hip_atomic_exchange(&g->count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(&g->gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            unsigned spins = 0;
-            while (__hip_atomic_load(&g->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
-                __builtin_amdgcn_s_sleep(2);
-                if (__hip_atomic_load(&g->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { ok = 0; break; }
-                if (++spins > (1u << 22)) {
-                    __hip_atomic_store(&g->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok = 0;
-                    break;
-                }
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        ok_s = ok;
-    }
-    __syncthreads();
-    return ok_s != 0;
-}
-
-struct LevelEndArgs {
-    GridBar *bar;
-    uint8_t *rm;
-    uint64_t *adj;
-    int32_t *deg;
-    int8_t *rl;
-    int n, W, d, nfill;
-    int32_t *off_new, *nbr_new;      // the next graph's CSR (the other buffer set)
-    uint64_t *ug_new;
-    int64_t ug_rows;
-    DevCounters *ctr;
-    uint8_t *status;
-    LevelSummary *out;
-    int32_t *out_deg;
-    unsigned long long seq;
-};
-
-template <int SDM>
-__global__ __launch_bounds__(256) void k_level_end(LevelArgs a, LevelEndArgs f) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    __shared__ int cleared[4];
-    __shared__ int32_t part[256];
-    const int blk = blockIdx.x, nblk = gridDim.x;
-    bool ok = true;
-    if constexpr (SDM > 0) {
-        screen_lanes<SDM>(a, blk, nblk);
-        ok = grid_sync(f.bar, nblk);
-    }
-    if (ok) {
-        exact_waves(a, smem, blk, nblk);
-        ok = grid_sync(f.bar, nblk);
-    }
-    if (ok) {
-        close_rows(f.rm, f.adj, f.deg, f.rl, f.n, f.W, f.d, blk, nblk, cleared);
-        ok = grid_sync(f.bar, nblk);
-    }
-    if (blk == nblk - 1)   // the summary first: the host waits on it
-        summary_block(f.deg, f.n, f.off_new, f.ug_new, f.ug_rows, f.ctr, f.status, f.out, f.out_deg, f.seq, f.nfill,
-                      part, ok ? 0 : 1);
-    if (ok) summary_nodes(f.deg, f.n, f.W, f.adj, f.nbr_new, f.ug_new, f.ug_rows, f.nfill, blk, nblk);
-}
-
-// ---------------------------------------------------------------------------------------
 // Small graphs (n <= 64: the RQ2 cases, 30-49 metrics): the WHOLE stable skeleton in one
 // workgroup launch. The multi-kernel level loop costs ~90 us of launches and host round trips
 // per depth whatever the work; an RQ2 case has 6-8 depths of 10^2..10^4 tests. Here C, the
@@ -4604,7 +3551,7 @@ constexpr int SMALL_LANE_D = 6;       // depths 1..6: one lane per test (chunks 
 constexpr int SMALL_K = 32;
 constexpr int SMALL_WAVES = 8;        // 512 threads: two waves per SIMD (256 VGPRs: the fused solves fit unspilled)
 constexpr int SMALL_SLOT = (SMALL_MAXD + 2) * (SMALL_MAXD + 2) + 3 * (SMALL_MAXD + 2);   // doubles per wave
-constexpr int SMALL_QCAP = 1024;      // band tests per depth waiting for the exact path (overflow: the level loop reruns)
+constexpr int SMALL_QCAP = 1024;      // band-queue slots per depth (PCG_TUNE_SMALL_QCAP <= this; full: the level loop reruns)
 static_assert(SMALL_SLOT >= SMALL_MAXD * (SMALL_MAXD + 1), "the wave slot holds the L rows too");
 
 struct SmallArgs {
@@ -4622,6 +3569,7 @@ struct SmallArgs {
     int64_t near_cap, rec_cap, rec_mod, rec_res;
     unsigned long long *ctr;          // [0] near-alpha, [1] records (cumulative over the run)
     int fullp, record, exact_all;
+    int qcap;                         // band tests per depth the queue takes (<= SMALL_QCAP)
     // per depth d (device memory, 4 doubles each): the threshold band on r^2 (lo2, hi2),
     // sqrt(N - d - 3), and 1.0 when N - d - 3 < 0 (a dynamically indexed kernel-argument array
     // would be copied to scratch)
@@ -4635,7 +3583,7 @@ struct SmallDepth {
 };
 
 struct SmallSummary {
-    int32_t levels, status;           // status: 1 singular, 2 math domain, 4 deeper than SMALL_MAXD / queue full
+    int32_t levels, status;           // status: 1 singular, 2 math domain, 4 deeper than SMALL_MAXD, 8 band queue full
     int64_t xrows;                    // exported sepset rows
     int64_t tests[PCG_MAX_LEVELS], calls[PCG_MAX_LEVELS], indep[PCG_MAX_LEVELS], exact[PCG_MAX_LEVELS];
     int64_t near_alpha[PCG_MAX_LEVELS], edges_after[PCG_MAX_LEVELS];
@@ -4912,7 +3860,18 @@ __global__ __launch_bounds__(SMALL_WAVES * 64, 1) void k_pc_small(SmallArgs a) {
         for (int k = 0; k < 8; ++k) cnt[k] = 0;
         sum->xrows = 0;
     }
+    // NaN nodes (a constant or non-finite column: numpy's corrcoef row is NaN throughout, its
+    // diagonal included): a test with one among x, y, S is NaN in the reference — the inverse of a
+    // NaN sub-matrix is NaN (no LinAlgError), so r and p are NaN and p > alpha is False: dependent.
+    // The lane-per-test depths decide those directly instead of queueing every one of them for the
+    // exact path (whose LU gives the same NaN), so a NaN column no longer fills the band queue.
+    __shared__ unsigned long long s_nanm;
+    if (tid < 64) {
+        const unsigned long long m = __ballot(tid < n && Cf[tid * n + tid] != Cf[tid * n + tid]);
+        if (tid == 0) s_nanm = m;
+    }
     __syncthreads();
+    const unsigned long long nanm = s_nanm;
     auto B = [&](int c, int k) -> uint64_t { return (c < k || c < 0) ? 0ull : bin[c * (SMALL_MAXD + 1) + k]; };
     // an independent (x, y | S): removal flags both ways, x's side union, and y's when x's visit
     // also served y's (S within adj(y), y > x)
@@ -5026,17 +3985,20 @@ __global__ __launch_bounds__(SMALL_WAVES * 64, 1) void k_pc_small(SmallArgs a) {
                         ++tests;
                         double p = 0.0;
                         int dec;
-                        if (d <= 2) dec = small_lane_eval<2>(a, kd, Cf, n, d, x, y, reinterpret_cast<const int(&)[2]>(sg), &p);
+                        if ((Sg | (1ull << x) | (1ull << y)) & nanm) {
+                            dec = 0;
+                            p = __builtin_nan("");
+                        } else if (d <= 2) dec = small_lane_eval<2>(a, kd, Cf, n, d, x, y, reinterpret_cast<const int(&)[2]>(sg), &p);
                         else if (d <= 4) dec = small_lane_eval<4>(a, kd, Cf, n, d, x, y, reinterpret_cast<const int(&)[4]>(sg), &p);
                         else dec = small_lane_eval<SMALL_LANE_D>(a, kd, Cf, n, d, x, y, sg, &p);
                         const int lo_ = x < y ? x : y, hi_ = x < y ? y : x;
                         if (dec == 2) {
                             const unsigned long long slot = atomicAdd(&cnt[6], 1ull);
-                            if (slot < SMALL_QCAP) {
+                            if (slot < (unsigned long long)a.qcap) {
                                 qxy[slot] = (uint16_t)(x | (y << 8));
                                 qS[slot] = Sg;
                             } else {
-                                atomicOr(&status, 4);    // more band tests than the queue holds
+                                atomicOr(&status, 8);    // more band tests than the queue holds
                             }
                         } else {
                             if (a.fullp) {
@@ -5065,7 +4027,7 @@ __global__ __launch_bounds__(SMALL_WAVES * 64, 1) void k_pc_small(SmallArgs a) {
             }
             __syncthreads();
             // the exact path of the queued band tests: one wave per test
-            const int qn = (int)min(cnt[6], (unsigned long long)SMALL_QCAP);
+            const int qn = (int)min(cnt[6], (unsigned long long)a.qcap);
             for (int i = wv; i < qn; i += SMALL_WAVES) {
                 const int x = qxy[i] & 255, y = qxy[i] >> 8;
                 const unsigned long long Sg = qS[i];
@@ -5181,9 +4143,13 @@ __global__ __launch_bounds__(SMALL_WAVES * 64, 1) void k_pc_small(SmallArgs a) {
             for (int k = 1; k < 5; ++k) cnt[k] = 0;
         }
         __syncthreads();
-        // a singular / domain error ends the run after its depth; a full band queue (status 4:
-        // this depth's decisions are incomplete) ends it at once, the host reruns on the level loop
-        if (status & 7) break;
+        // a singular / domain error ends the run after its depth; a full band queue (status 8:
+        // this depth's decisions are incomplete) ends it at once, the host reruns on the level loop.
+        // (Round 4 first broke on status & 3 only: after an overflow the block went on deciding
+        // depths from incomplete removals, and on dense near-threshold graphs it kept overflowing
+        // every depth up to SMALL_MAXD inside one 512-thread workgroup — a 60 s hang in a parity
+        // test, fixed by breaking on the overflow itself.)
+        if (status & 15) break;
     }
     for (int e = tid; e < n * n; e += blockDim.x) a.rl[e] = rlv[(e / n) * SMALL_N + e % n];
     if (tid == 0) {
@@ -5281,11 +4247,7 @@ LevelArgs make_args(pcg_handle *h, int d, int mode_exact_all) {
     a.rec_mod = h->rec_mod;
     a.rec_res = h->rec_res;
     a.spl = h->spl;
-    a.spl_dev = (h->bound && h->dspl) ? (const int32_t *)h->spl_buf.p : nullptr;
     if (h->nblk) {
-        const int64_t *t = (const int64_t *)h->cpre.p + h->sp_tab_off;
-        a.coff = t;
-        a.ctab = t + SP_DMAX + 2;
         a.bo = (const int64_t *)h->cpre.p + h->bo_off;
         a.cblk = (double *)h->cblk.p;
         a.lmk = (uint64_t *)h->lmk.p;
@@ -5385,34 +4347,26 @@ uint64_t tgroup_tasks(const pcg_handle *h, int D, int d) {
 // (full-p mode too: threshold decisions with the exact band, records by the exact path — the
 // p-values the caller can observe; k_level_lds_t routes recorded pairs there)
 bool use_tgroup(int mode, int d) { return (mode == MODE_DECIDE || mode == MODE_FULLP) && d >= 2 && d <= 4; }
-// depths whose narrow class runs k_level_wave (one wave per conditioning set); PCG_WAVE_LO
-// sets the first such depth for every mode (A/B knob)
-// k_level_wave_pr (the factorisation shared between consecutive sets) instead of k_level_wave;
-// PCG_WAVE_PR=0: the per-set factorisation (A/B knob, read per launch)
-bool wave_pr() {
-    const char *e = getenv("PCG_WAVE_PR");
-    return !e || atoi(e) != 0;
-}
-
 // threshold mode: the deepest depth on the per-lane k_level_lds (PCG_MAX_DEPTH .. PCG_LDS_DEEP_TOP;
-// the A/B knob PCG_LDS_DEEP, read per depth)
-int lds_deep_max() {
-    const char *e = getenv("PCG_LDS_DEEP");
-    const int v = e ? atoi(e) : PCG_LDS_DEEP_TOP;
-    return std::min(std::max(v, PCG_MAX_DEPTH), PCG_LDS_DEEP_TOP);
+// PCG_TUNE_LDS_DEEP)
+int lds_deep_max(const pcg_handle *h) {
+    return std::min(std::max((int)h->tune[PCG_TUNE_LDS_DEEP], PCG_MAX_DEPTH), PCG_LDS_DEEP_TOP);
 }
-// tests: the level's test count bound (sum over nodes of C(D, d) (D - d))
-bool use_wave(int mode, int d, double tests) {
+// depths whose narrow class runs k_level_wave (one wave per conditioning set); PCG_TUNE_WAVE_LO
+// sets the first such depth for every mode. tests: the level's test count bound (sum over nodes
+// of C(D, d) (D - d))
+bool use_wave(const pcg_handle *h, int mode, int d, double tests) {
     if (!(mode == MODE_DECIDE || mode == MODE_FULLP) || d > PCG_MAX_LEVEL_DEPTH) return false;
-    const char *e = getenv("PCG_WAVE_LO");        // read per depth, like PCG_SCREEN_MASK
-    if (e) return d >= std::max(atoi(e), 5);      // explicit: the wave kernels from that depth up
+    const int lo = (int)h->tune[PCG_TUNE_WAVE_LO];
+    if (lo > 0) return d >= std::max(lo, 5);      // explicit: the wave kernels from that depth up
     // default: the wave kernels beyond the per-lane kernel's depths (PCG_MAX_DEPTH; threshold
     // mode up to lds_deep_max(), from depth 17 on only for large levels: those instantiations
     // spill to scratch at one wave per SIMD, which loses to the wave kernels on a few thousand
-    // tests — n = 500's depths 17-18: 0.05 vs 0.02 ms — and wins 2.3-2.7x on 1e9)
+    // tests — n = 500's depths 17-18: 0.05 vs 0.02 ms — and wins 2.3-2.7x on 1e9;
+    // PCG_TUNE_LDS_SPILL_MIN)
     if (mode != MODE_DECIDE) return d > PCG_MAX_DEPTH;
-    if (d > lds_deep_max()) return true;
-    return d > 16 && tests < PCG_LDS_SPILL_MIN;
+    if (d > lds_deep_max(h)) return true;
+    return d > 16 && tests < (double)h->tune[PCG_TUNE_LDS_SPILL_MIN];
 }
 // depth 1's large class runs k_level1_pairs (pcg_level_run); its chunks split a node's
 // D(D-1)/2 neighbour pairs evenly, ~L1_PAIRS_PER_CHUNK each, so a high-degree node is spread
@@ -5430,7 +4384,7 @@ int64_t l1_pair_chunks(int D) { return std::max<int64_t>(1, ((int64_t)D * (D - 1
 int level_class(const pcg_handle *h, int D, int d, bool tg) {
     if (h->wavek) return D <= std::min(WAVE_MAXD, h->narrow_deg) ? 0 : 2;   // k_level_wave depths
     if (D <= std::min(SMALL_DEG, h->narrow_deg) &&
-        (d <= PCG_MAX_DEPTH || (mode_of(h, d) == MODE_DECIDE && d <= lds_deep_max())))
+        (d <= PCG_MAX_DEPTH || (mode_of(h, d) == MODE_DECIDE && d <= lds_deep_max(h))))
         return 0;
     if (tg && D <= WIDE_DEG && lds_tgroup_bytes((D + 3) & ~3, d, 16) <= LDS_MAX) return 1;
     return 2;
@@ -5442,16 +4396,14 @@ int mode_of(const pcg_handle *h, int d) {
     return MODE_DECIDE;
 }
 
-// the summary slot of sequence number seq (a ring of two: the pipelined loop reads depth d - 1's
-// summary while depth d's may already be written)
+// the summary slot of sequence number seq (a ring of two)
 LevelSummary *sum_slot(const pcg_handle *h, unsigned long long seq) {
     return reinterpret_cast<LevelSummary *>(reinterpret_cast<char *>(h->summary) + (seq & 1) * h->summary_slot);
 }
 
 // the level summary (degrees, counters, status) of the current adjacency -> host-mapped memory;
-// level_wait() spins until the device has written it. With `fa` (the fused barrier, single GPU)
-// the depth's screen, exact path and removals run in the same launch (k_level_end) first.
-int graph_launch(pcg_handle *h, const LevelArgs *fa) {
+// level_wait() spins until the device has written it.
+int graph_launch(pcg_handle *h) {
     const int n = (int)h->n, W = h->W;
     const size_t slot = (sizeof(LevelSummary) + sizeof(int32_t) * (size_t)n + 255) & ~(size_t)255;
     if (!h->summary || h->summary_bytes < 2 * slot) {
@@ -5502,44 +4454,10 @@ int graph_launch(pcg_handle *h, const LevelArgs *fa) {
     h->ug_clean2[t] = ug != nullptr && nfill > 0 && ug_rows >= h->sumdeg;
     h->ug_pend_seq = (ug && !h->ug_clean2[t]) ? seq : 0;
     h->ug_pend_set = t;
-    if (fa) {
-        if (!h->gbar.p) {
-            if (!pcg_ensure(h, h->gbar, sizeof(GridBar))) return pcg_fail(h, PCG_ERR_OOM, "grid barrier");
-            PCG_HIP(h, hipMemsetAsync(h->gbar.p, 0, sizeof(GridBar), h->stream));
-        }
-        LevelEndArgs f{};
-        f.bar = (GridBar *)h->gbar.p;
-        f.rm = h->rm_ext ? h->rm_ext : (uint8_t *)h->rm.p;
-        f.adj = (uint64_t *)h->adj.p;
-        f.deg = (int32_t *)h->deg.p;
-        f.rl = h->rl;
-        f.n = n;
-        f.W = W;
-        f.d = h->depth;
-        f.nfill = nfill;
-        f.off_new = (int32_t *)h->off2[t].p;
-        f.nbr_new = (int32_t *)h->nbr2[t].p;
-        f.ug_new = ug;
-        f.ug_rows = ug_rows;
-        f.ctr = (DevCounters *)h->ctr.p;
-        f.status = status;
-        f.out = ds;
-        f.out_deg = reinterpret_cast<int32_t *>(ds + 1);
-        f.seq = seq;
-        const int m = h->depth + 2;
-        const size_t lds = sizeof(double) * (size_t)(m * m + 2 * m) * 4;   // k_exact's slot per wave
-        const int sdm = fa->d >= 2 && fa->d <= 4 && h->tgroup && use_screen32(h, fa->d) ? fa->d : 0;
-        const dim3 grid(FUSE_BLOCKS), block(256);
-        if (sdm == 2) hipLaunchKernelGGL(k_level_end<2>, grid, block, lds, h->stream, *fa, f);
-        else if (sdm == 3) hipLaunchKernelGGL(k_level_end<3>, grid, block, lds, h->stream, *fa, f);
-        else if (sdm == 4) hipLaunchKernelGGL(k_level_end<4>, grid, block, lds, h->stream, *fa, f);
-        else hipLaunchKernelGGL(k_level_end<0>, grid, block, lds, h->stream, *fa, f);
-    } else {
-        hipLaunchKernelGGL(k_summary_fill, dim3((unsigned)(nfill + 1)), dim3(256), 0, h->stream,
-                           (const int32_t *)h->deg.p, n, W, (const uint64_t *)h->adj.p, (int32_t *)h->off2[t].p,
-                           (int32_t *)h->nbr2[t].p, ug, ug_rows, (DevCounters *)h->ctr.p, status, ds,
-                           reinterpret_cast<int32_t *>(ds + 1), seq, nfill);
-    }
+    hipLaunchKernelGGL(k_summary_fill, dim3((unsigned)(nfill + 1)), dim3(256), 0, h->stream,
+                       (const int32_t *)h->deg.p, n, W, (const uint64_t *)h->adj.p, (int32_t *)h->off2[t].p,
+                       (int32_t *)h->nbr2[t].p, ug, ug_rows, (DevCounters *)h->ctr.p, status, ds,
+                       reinterpret_cast<int32_t *>(ds + 1), seq, nfill);
     h->cb = t;
     PCG_HIP(h, hipGetLastError());
     if (h->lev_on && h->lev_n < 2 * PCG_MAX_LEVELS) {   // depth boundary (skeleton_once), off the host's critical path
@@ -5651,7 +4569,7 @@ extern "C" int pcg_skeleton_init(pcg_handle *h, const double *C, int64_t n, int6
     PCG_HIP(h, hipGetLastError());
     // the level counters start at zero (k_summary_fill keeps the run's near-alpha count)
     PCG_HIP(h, hipMemsetAsync(h->ctr.p, 0, sizeof(DevCounters), h->stream));
-    int rc = graph_launch(h, nullptr);   // also clears the counters
+    int rc = graph_launch(h);   // also clears the counters
     if (rc) return rc;
     // the complete graph's degrees are known (k_init writes n - 1 everywhere): depth 0 is
     // decided and enqueued without waiting for this summary (the next level_wait covers it)
@@ -5682,73 +4600,7 @@ void level_start_stats(pcg_handle *h, int depth) {
 
 int level_begin_buffers(pcg_handle *h, int depth);
 
-// bound mode: the per-degree tables (and k_level_sp's chunk tables) go up through the depth
-// parity's pinned buffer; k_decompose then writes the exact class prefixes and compact-block
-// offsets of the device degrees into h->cpre: [3 x (n + 1) prefixes][coff][ctab][tab][bo]
-int level_begin_bound_upload(pcg_handle *h, int depth, int64_t blk_cap) {
-    const int n = (int)h->n, maxd = h->dtab_maxd;
-    const int64_t ntab = 3 * (int64_t)(maxd + 1);
-    const int64_t up = (int64_t)(SP_DMAX + 2) + (int64_t)h->sp_ctab.size() + ntab;
-    h->dtab_off = h->sp_tab_off + (int64_t)(SP_DMAX + 2) + (int64_t)h->sp_ctab.size();
-    h->bo_off = h->dtab_off + ntab;
-    const int64_t cnt = h->bo_off + (n + 1);
-    PinBuf &pb = h->tab_pin[depth & 1];
-    if (!pcg_ensure_pinned(h, pb, sizeof(int64_t) * up)) return pcg_fail(h, PCG_ERR_OOM, "pinned level tables");
-    int64_t *p = (int64_t *)pb.p;
-    memcpy(p, h->sp_coff.data(), sizeof(int64_t) * (SP_DMAX + 2));
-    p += SP_DMAX + 2;
-    if (!h->sp_ctab.empty()) memcpy(p, h->sp_ctab.data(), sizeof(int64_t) * h->sp_ctab.size());
-    p += h->sp_ctab.size();
-    memcpy(p, h->cpre_h.data(), sizeof(int64_t) * ntab);
-    if (!pcg_ensure(h, h->cpre, sizeof(int64_t) * cnt)) return PCG_ERR_OOM;
-    if (h->nblk && (!pcg_ensure(h, h->cblk, sizeof(double) * std::max<int64_t>(blk_cap, 1)) ||
-                    !pcg_ensure(h, h->lmk, sizeof(uint64_t) * std::max<int64_t>(h->sumdeg, 1))))
-        return pcg_fail(h, PCG_ERR_OOM, "compact node blocks");
-    const void *src = pb.dp;
-    int64_t *dev = (int64_t *)h->cpre.p;
-    hipLaunchKernelGGL(k_copy_i64, dim3((unsigned)((up + 255) / 256)), dim3(256), 0, h->stream, (const int64_t *)src, up,
-                       dev + h->sp_tab_off);
-    if (h->dspl) {
-        if (!pcg_ensure(h, h->spl_buf, 2 * sizeof(int32_t))) return pcg_fail(h, PCG_ERR_OOM, "device spl");
-        hipLaunchKernelGGL(k_decompose_dev, dim3(1), dim3(DEC_THREADS), 0, h->stream, (const int32_t *)h->deg.p, n,
-                           (const int64_t *)(dev + h->dtab_off), maxd, depth, h->nblk ? 1 : 0, h->dspl_lanes,
-                           h->dspl_tgt[0], h->dspl_cap[0], h->dspl_tgt[1], h->dspl_cap[1], dev, dev + h->bo_off,
-                           (int32_t *)h->spl_buf.p);
-    } else {
-        hipLaunchKernelGGL(k_decompose, dim3(1), dim3(256), 0, h->stream, (const int32_t *)h->deg.p, n,
-                           (const int64_t *)(dev + h->dtab_off), maxd, depth, h->nblk ? 1 : 0, dev, dev + h->bo_off);
-    }
-    PCG_HIP(h, hipGetLastError());
-    PCG_HT(h, "begin:decompose-launched");
-    return level_begin_buffers(h, depth);
-}
-
-// bound: h->deg_h holds upper bounds of the degrees (those at the start of depth - 1; the
-// pipelined loop in skeleton_once). The class tables then cover every degree up to the bound, the
-// launch sizes are upper bounds, and k_decompose writes the exact prefixes on the device.
-// the pipelined loop's chunk size chosen on the device (k_decompose_dev); PCG_DEV_SPL=0: the
-// host's, from the bound degrees (A/B knob)
-static bool dev_spl_ok() {
-    const char *e = getenv("PCG_DEV_SPL");
-    return !e || atoi(e) != 0;
-}
-
-// the fused level barrier (k_level_end, PCG_FUSE_END=1) on one GPU with the handle's own removal
-// flags (a sharded run merges the ranks' flags between the exact path and the removals). Off by
-// default: measured slower than the separate k_screen / k_exact / k_level_close / k_summary_fill
-// launches (config 5: 4.77 vs 4.43 ms per step, n = 500 unlimited depth: 3.14 vs 2.50 ms; the
-// launch ran 87-143 us per depth against ~35 us for the four kernels and their gaps): its 256
-// persistent blocks process rows and nodes one after another where the separate launches put
-// one block per row / four nodes in flight at once, and a software grid barrier costs ~20 us
-// on this part against ~2.5 us for a dependent kernel boundary (tools/micro/grid_barrier.hip,
-// profiles/r04_grid_barrier.txt; timeline: profiles/r04_timeline_fused_barrier.txt)
-static bool fuse_end_ok(const pcg_handle *h) {
-    if (h->world != 1 || h->rm_ext) return false;
-    const char *e = getenv("PCG_FUSE_END");
-    return e && atoi(e) != 0;
-}
-
-int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks, bool bound) {
+int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks) {
     if (!h || depth != h->depth + 1) return pcg_fail(h, PCG_ERR_INVALID, "pcg_level_begin: depth order");
     // reference loop condition: while max_degree() - 1 > depth_prev
     if (!(h->maxdeg - 1 > depth - 1)) {
@@ -5758,31 +4610,21 @@ int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks, bool bound
     if (depth >= PCG_MAX_LEVELS || depth > PCG_MAX_LEVEL_DEPTH)
         return pcg_fail(h, PCG_ERR_INVALID, "conditioning depth %d exceeds PCG_MAX_LEVEL_DEPTH=%d", depth,
                         PCG_MAX_LEVEL_DEPTH);
-    if (bound && depth < 1) return pcg_fail(h, PCG_ERR_INVALID, "bound-mode decomposition at depth 0");
     h->depth = depth;
-    h->bound = bound;
-    h->fuse_end = fuse_end_ok(h);
     const int n = (int)h->n;
-    if (!bound) level_start_stats(h, depth);
+    level_start_stats(h, depth);
     // per-degree tables: the decomposition below is O(n) lookups (it sits between two
     // device phases of the level loop, so it is on the critical path)
     const int maxd = h->maxdeg;
     std::vector<int64_t> hist(maxd + 1, 0);
     for (int x = 0; x < n; ++x) ++hist[h->deg_h[x]];
-    // bound mode: every degree up to the bound may occur
-    std::vector<int64_t> hist_t(hist);
-    if (bound)
-        for (int D = 0; D <= maxd; ++D) hist_t[D] = std::max<int64_t>(hist_t[D], 1);
     // work decomposition: depth 0 = one chunk per row; depth >= 1 = three node classes:
     // narrow (D <= 64: LDS-resident kernels), wide (64 < D <= 128 at the T-group depths: the
     // T-group kernel with 128-bit masks), large (the rest: staged generic kernels)
     h->cpre_h.assign(3 * (size_t)(n + 1), 0);
     int64_t *cs = h->cpre_h.data(), *cw = cs + (n + 1), *cl = cw + (n + 1);
-    std::vector<int64_t> bo;           // k_level_sp compact-block offsets (doubles)
-    h->sp = false;
+    std::vector<int64_t> bo;           // compact-block offsets (doubles, k_node_blocks)
     h->nblk = false;
-    h->sp_ctab.clear();
-    h->sp_coff.assign(SP_DMAX + 2, 0);
     h->work_h.assign(n, 0);
     h->maxdeg_small = 0;
     h->maxdeg_wide = 0;
@@ -5793,6 +4635,7 @@ int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks, bool bound
         h->chunk = 256;
         h->spl = 1;
         h->tgroup = false;
+        h->wavek = false;
         const int T = (n + 63) / 64;
         int64_t acc = 0;
         for (int x = 0; x <= n; ++x) {
@@ -5815,20 +4658,13 @@ int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks, bool bound
             for (int i = 0; i < depth; ++i) c = c * (double)(D - i) / (double)(i + 1);
             tests_bound += (double)hist[D] * c * (double)(D - depth);
         }
-        h->wavek = use_wave(mode_of(h, depth), depth, tests_bound);
-        // fp32-screened depths: pcg_set_screen_precision, or the PCG_SCREEN_MASK A/B knob
-        const char *sm = getenv("PCG_SCREEN_MASK");
-        h->screen_eff = sm ? (int)strtol(sm, nullptr, 0) : (h->screen_mask < 0 ? PCG_TG_F32 : h->screen_mask);
+        h->wavek = use_wave(h, mode_of(h, depth), depth, tests_bound);
+        // fp32-screened depths: PCG_TUNE_SCREEN_MASK, else pcg_set_screen_precision's choice
+        const int64_t tm = h->tune[PCG_TUNE_SCREEN_MASK];
+        h->screen_eff = tm >= 0 ? (int)tm : (h->screen_mask < 0 ? PCG_TG_F32 : h->screen_mask);
         h->screen_eff &= 0x1c;   // the error bound (KE = 64) is derived for d = 2..4 only
-        {   // Schur-prefix sweep for the narrow class (PCG_SP A/B knob, read per depth)
-            const char *spe = getenv("PCG_SP");
-            const int spm = spe ? (int)strtol(spe, nullptr, 0) : PCG_SP;
-            h->sp = tg && use_screen32(h, depth) && (depth == 3 || depth == 4) && ((spm >> depth) & 1);
-            // compact node blocks (k_node_blocks) for the narrow class of the fp32-screened sweeps
-            const char *nbe = getenv("PCG_NODE_BLOCKS");
-            const int nbm = nbe ? (int)strtol(nbe, nullptr, 0) : PCG_NODE_BLOCKS;
-            h->nblk = h->sp || (tg && use_screen32(h, depth) && ((nbm >> depth) & 1));
-        }
+        // compact node blocks (k_node_blocks) for the narrow class of the fp32-screened sweeps
+        h->nblk = tg && use_screen32(h, depth) && ((h->tune[PCG_TUNE_NODE_BLOCKS] >> depth) & 1);
         std::vector<uint64_t> ns_of(maxd + 1, 0), units_of(maxd + 1, 0);
         std::vector<int> cls_of(maxd + 1, 2);
         double sum_small = 0.0, sum_wide = 0.0, sum_large = 0.0;
@@ -5840,40 +4676,29 @@ int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks, bool bound
             ns_of[D] = ns;
             cls_of[D] = level_class(h, D, depth, tg);
             units_of[D] = cls_of[D] < 2 ? (tg ? tgroup_tasks(h, D, depth) : ns) : ns;
-            if (h->sp && cls_of[D] == 0) {
-                uint64_t u = 0;
-                for (int t0 = 1; t0 <= D - depth + 1; ++t0) u += (uint64_t)sp_tasks(D, depth, t0);
-                units_of[D] = u;
-            }
-            if (hist_t[D] && cls_of[D] == 0) h->maxdeg_small = D;   // (bound mode: any degree up to the bound)
-            if (hist_t[D] && cls_of[D] == 1) h->maxdeg_wide = D;
             if (!hist[D]) continue;
             if (cls_of[D] == 0) {
+                h->maxdeg_small = D;
                 sum_small += (double)units_of[D] * hist[D];
             } else if (cls_of[D] == 1) {
+                h->maxdeg_wide = D;
                 sum_wide += (double)units_of[D] * hist[D];
             } else {
                 sum_large += (double)ns * hist[D];
                 cnt_large += (int)hist[D];
             }
         }
-        // ~4096 LDS-resident blocks per depth and rank; each lane walks spl units. The wide class
-        // (a few nodes) aims at ~512 blocks so its nodes are spread over the chip
-        // narrow-class block target: ~4096 blocks per depth and rank, 16384 at depth 4, whose long
-        // per-node task lists otherwise leave a tail (measured 2.53 -> 2.40 ms; depth 3 is best at
-        // 4096); PCG_NB / PCG_NB<d> override (A/B knobs)
-        double nb_target = getenv("PCG_NB") ? atof(getenv("PCG_NB")) : (depth == 4 ? 16384.0 : 4096.0);
-        {
-            char nm[16];
-            snprintf(nm, sizeof nm, "PCG_NB%d", depth);
-            if (getenv(nm)) nb_target = atof(getenv(nm));
-        }
-        // lanes per block: 256 S ranks / T-group tasks, or 4 conditioning sets (k_level_wave: a wave each)
+        // narrow-class block target: ~4096 LDS-resident blocks per depth and rank, 16384 at depth
+        // 4, whose long per-node task lists otherwise leave a tail (measured 2.53 -> 2.40 ms; depth
+        // 3 is best at 4096); each lane walks spl units. The wide class (a few nodes) aims at ~512
+        // blocks so its nodes are spread over the chip. PCG_TUNE_NB / PCG_TUNE_NBW override.
+        const double nb_target = h->tune[PCG_TUNE_NB] > 0 ? (double)h->tune[PCG_TUNE_NB] : (depth == 4 ? 16384.0 : 4096.0);
+        // lanes per block: 256 S ranks / T-group tasks, or 4 conditioning sets (k_level_wave: a
+        // wave each, sharing the factorisation along a wave's run of sets: longer runs there)
         const double per_block = h->wavek ? 4.0 : 256.0;
-        // (k_level_wave_pr shares the factorisation along a wave's run of sets: longer runs there)
-        const double spl_cap = (h->wavek && wave_pr()) ? 512.0 : 64.0;
+        const double spl_cap = h->wavek ? 512.0 : 64.0;
         h->spl = (int)std::min(spl_cap, std::max(1.0, std::floor(sum_small / (per_block * nb_target * h->world))));
-        const double nbw_target = getenv("PCG_NBW") ? atof(getenv("PCG_NBW")) : 512.0;   // A/B knob
+        const double nbw_target = (double)h->tune[PCG_TUNE_NBW];
         h->spl_w = (int)std::min(64.0, std::max(1.0, std::floor(sum_wide / (256.0 * nbw_target * h->world))));
         const double mean_large = cnt_large ? sum_large / cnt_large : 0.0;
         h->chunk = (depth > PCG_MAX_DEPTH || mean_large <= 64) ? 64 : (mean_large <= 128 ? 128 : 256);
@@ -5885,92 +4710,7 @@ int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks, bool bound
             nch_of[D] = c == 0 ? (int64_t)((units_of[D] + csz - 1) / csz)
                                : c == 1 ? (int64_t)((units_of[D] + cszw - 1) / cszw)
                                         : l1p ? l1_pair_chunks(D) : (int64_t)((ns_of[D] + h->chunk - 1) / h->chunk);
-            if (h->sp && c == 0 && hist_t[D]) {
-                // k_level_sp chunks of a degree-D node: runs of <= csz consecutive lane tasks
-                // (prefix t0 major) spanning at most sp_pb(D) prefixes
-                h->sp_coff[D] = (int64_t)h->sp_ctab.size();
-                const int pb = sp_pb(D);
-                int64_t cur_t0 = -1, cur_k = 0, cur_n = 0;
-                int cur_b = 0;
-                auto emit = [&]() {
-                    if (cur_n > 0) h->sp_ctab.push_back((cur_t0 << 40) | (cur_k << 20) | cur_n);
-                    cur_n = 0;
-                    cur_b = 0;
-                };
-                for (int t0 = 1; t0 <= D - depth + 1; ++t0) {
-                    const int64_t T = sp_tasks(D, depth, t0);
-                    int64_t pos = 0;
-                    while (pos < T) {
-                        if (cur_n == 0) { cur_t0 = t0; cur_k = pos; }
-                        const int64_t take = std::min<int64_t>(T - pos, (int64_t)csz - cur_n);
-                        cur_n += take;
-                        pos += take;
-                        ++cur_b;
-                        if (cur_n >= (int64_t)csz || cur_b >= pb) emit();
-                    }
-                }
-                emit();
-                nch_of[D] = (int64_t)h->sp_ctab.size() - h->sp_coff[D];
-            }
         }
-        if (bound) {
-            // launch sizes: a node whose degree is at most its bound D_b may fall into any class,
-            // with at most the largest chunk count of that class over degrees <= D_b
-            std::vector<int64_t> pm(3 * (size_t)(maxd + 1), 0), pu(2 * (size_t)(maxd + 1), 0);
-            for (int D = 0; D <= maxd; ++D) {
-                for (int c = 0; c < 3; ++c)
-                    pm[c * (maxd + 1) + D] = std::max(D ? pm[c * (maxd + 1) + D - 1] : 0,
-                                                      (D >= depth + 1 && cls_of[D] == c) ? nch_of[D] : (int64_t)0);
-                for (int c = 0; c < 2; ++c)
-                    pu[c * (maxd + 1) + D] = std::max(D ? pu[c * (maxd + 1) + D - 1] : 0,
-                                                      (D >= depth + 1 && cls_of[D] == c) ? (int64_t)units_of[D] : (int64_t)0);
-            }
-            int64_t tot[3] = {0, 0, 0}, sb = 0, ub[2] = {0, 0}, nb_[2] = {0, 0};
-            for (int x = 0; x < n; ++x) {
-                const int Db = h->deg_h[x];
-                for (int c = 0; c < 3; ++c) tot[c] += pm[c * (maxd + 1) + Db];
-                for (int c = 0; c < 2; ++c) {
-                    ub[c] += pu[c * (maxd + 1) + Db];
-                    nb_[c] += pu[c * (maxd + 1) + Db] > 0;
-                }
-                int Dn = std::min(Db, std::min(SMALL_DEG, h->narrow_deg));   // largest narrow block
-                sb += (int64_t)(Dn + 1) * (Dn + 1);
-            }
-            // the chunk size chosen on the device (k_decompose_dev) from the exact degrees, unless
-            // the Schur-prefix sweep's per-degree chunk tables need the host's
-            h->dspl = !h->sp && dev_spl_ok();
-            h->dspl_lanes = h->wavek ? 4 : 256;
-            h->dspl_tgt[0] = nb_target * h->world;
-            h->dspl_tgt[1] = nbw_target * h->world;
-            h->dspl_cap[0] = (int)spl_cap;
-            h->dspl_cap[1] = 64;
-            if (h->dspl) {
-                // chunks <= nodes + sum / (lanes * spl): with spl = floor(sum / (lanes * target))
-                // >= 1 the second term is < 2 * target, with spl = 1 it is < target, and with spl at
-                // its cap it is at most the bound sum / (lanes * cap); never more than spl = 1 gives
-                const double L[2] = {(double)h->dspl_lanes, 256.0};
-                for (int c = 0; c < 2; ++c) {
-                    const double caps = std::ceil((double)ub[c] / (L[c] * h->dspl_cap[c]));
-                    const int64_t lim = nb_[c] + (int64_t)std::max(2.0 * h->dspl_tgt[c], caps) + 1;
-                    int64_t one = 0;          // the count at spl = 1
-                    for (int x = 0; x < n; ++x) {
-                        const int64_t u = pu[c * (maxd + 1) + h->deg_h[x]];
-                        one += (u + (int64_t)L[c] - 1) / (int64_t)L[c];
-                    }
-                    tot[c] = std::min(lim, one);
-                }
-            }
-            h->total_small = tot[0];
-            h->total_wide = tot[1];
-            h->total_large = tot[2];
-            // the per-degree class tables k_decompose reads: tab[c][D] = chunks of a degree-D node in
-            // class c (k_decompose_dev: units for the narrow and wide classes, chunks for the large)
-            h->dtab_maxd = maxd;
-            h->cpre_h.assign(3 * (size_t)(maxd + 1), 0);
-            for (int D = depth + 1; D <= maxd; ++D)
-                h->cpre_h[cls_of[D] * (maxd + 1) + D] = (h->dspl && cls_of[D] < 2) ? (int64_t)units_of[D] : nch_of[D];
-            bo.assign(1, sb);                 // compact-block capacity (an upper bound)
-        } else {
         int64_t ss = 0, sw = 0, sl = 0, sb = 0;
         if (h->nblk) bo.assign(n + 1, 0);
         for (int x = 0; x < n; ++x) {
@@ -5992,37 +4732,28 @@ int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks, bool bound
         h->total_small = ss;
         h->total_wide = sw;
         h->total_large = sl;
-        }
     }
     h->total_chunks = h->total_small + h->total_wide + h->total_large;
     if (total_chunks) *total_chunks = h->total_chunks;
     PCG_HT(h, "begin:decomposed");
-    h->sp_tab_off = 3 * (int64_t)(n + 1);
-    if (bound) return level_begin_bound_upload(h, depth, bo.empty() ? 0 : bo[0]);
-    // host-mapped upload: the three class prefixes, then (k_level_sp) the per-degree chunk table
-    // offsets, the chunk table and the compact-block offsets
-    const int64_t cnt = h->sp_tab_off + (h->nblk ? (int64_t)(SP_DMAX + 2) + (int64_t)h->sp_ctab.size() + (n + 1) : 0);
-    h->bo_off = h->sp_tab_off + (int64_t)(SP_DMAX + 2) + (int64_t)h->sp_ctab.size();
+    // host-mapped upload: the three class prefixes, then (k_node_blocks) the compact-block offsets
+    h->bo_off = 3 * (int64_t)(n + 1);
+    const int64_t cnt = h->bo_off + (h->nblk ? (int64_t)(n + 1) : 0);
     if (!pcg_ensure_pinned(h, h->cpre_pin, sizeof(int64_t) * cnt))
         return pcg_fail(h, PCG_ERR_OOM, "pinned chunk prefix");
     {
         int64_t *pin = (int64_t *)h->cpre_pin.p;
         memcpy(pin, h->cpre_h.data(), sizeof(int64_t) * 3 * (n + 1));
         if (h->nblk) {
-            int64_t *p = pin + h->sp_tab_off;
-            memcpy(p, h->sp_coff.data(), sizeof(int64_t) * (SP_DMAX + 2));
-            p += SP_DMAX + 2;
-            if (!h->sp_ctab.empty()) memcpy(p, h->sp_ctab.data(), sizeof(int64_t) * h->sp_ctab.size());
-            p += h->sp_ctab.size();
-            memcpy(p, bo.data(), sizeof(int64_t) * (n + 1));
+            memcpy(pin + h->bo_off, bo.data(), sizeof(int64_t) * (n + 1));
             if (!pcg_ensure(h, h->cblk, sizeof(double) * std::max<int64_t>(bo[n], 1)) ||
                 !pcg_ensure(h, h->lmk, sizeof(uint64_t) * std::max<int64_t>(h->sumdeg, 1)))
-                return pcg_fail(h, PCG_ERR_OOM, "Schur-prefix node blocks");
+                return pcg_fail(h, PCG_ERR_OOM, "compact node blocks");
         }
     }
     if (!pcg_ensure(h, h->cpre, sizeof(int64_t) * cnt)) return PCG_ERR_OOM;
-    // rm, the counters and the status bytes were cleared by the previous depth's k_apply /
-    // k_level_summary (or at init); the union rows by k_fill_nbr (or here, on first use)
+    // rm, the counters and the status bytes were cleared by the previous depth's k_level_close /
+    // k_summary_fill (or at init); the union rows by k_summary_fill (or here, on first use)
     {
         const void *src = h->cpre_pin.dp;
         hipLaunchKernelGGL(k_copy_i64, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, h->stream,
@@ -6061,7 +4792,7 @@ extern "C" int pcg_level_begin(pcg_handle *h, int depth, int64_t *total_chunks, 
                                uint8_t **rm_dev) {
     if (h && max_degree) *max_degree = h->maxdeg;
     if (h && rm_dev) *rm_dev = h->rm_ext ? h->rm_ext : (uint8_t *)h->rm.p;
-    return level_begin_impl(h, depth, total_chunks, false);
+    return level_begin_impl(h, depth, total_chunks);
 }
 
 extern "C" int pcg_set_forbidden_pairs(pcg_handle *h, const uint8_t *banned_dev) {
@@ -6121,14 +4852,6 @@ extern "C" int pcg_level_chunk_work(pcg_handle *h, int64_t *prefix_host, int64_t
                 continue;
             }
             const int D = h->deg_h[x];
-            if (cls == 0 && h->sp) {   // k_level_sp: the chunk's lane tasks x candidates x y
-                const int64_t *tab = h->sp_ctab.data() + h->sp_coff[D];
-                for (int64_t c = c0; c < c1; ++c) {
-                    acc += (tab[c - c0] & 0xFFFFF) * PCG_SP_TG * (D - h->depth) + 1;
-                    prefix_host[base + c + 1] = acc;
-                }
-                continue;
-            }
             if (cls == 2 && use_l1_pairs(h, h->depth)) {   // k_level1_pairs: an even share of the pairs, two tests each
                 const int64_t np = (int64_t)D * (D - 1) / 2, nch = c1 - c0;
                 for (int64_t c = c0; c < c1; ++c) {
@@ -6236,28 +4959,15 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                         const dim3 grid((unsigned)(s_hi - s_lo)), block(256);
                         const size_t core = lds_small_core(h->maxdeg_small);
                         as.lds_btab_off = (int)core;
-                        const bool pr = wave_pr();
                         if (d <= 16) {
                             const size_t ldsw = core + 4 * sizeof(double) * (WAVE_SLOT_DOUBLES(16) + 16);
-                            if (pr && mode == MODE_DECIDE) hipLaunchKernelGGL((k_level_wave_pr<16, MODE_DECIDE>), grid, block, ldsw, h->stream, as);
-                            else if (pr) hipLaunchKernelGGL((k_level_wave_pr<16, MODE_FULLP>), grid, block, ldsw, h->stream, as);
-                            else if (mode == MODE_DECIDE) hipLaunchKernelGGL((k_level_wave<16, MODE_DECIDE>), grid, block, ldsw, h->stream, as);
+                            if (mode == MODE_DECIDE) hipLaunchKernelGGL((k_level_wave<16, MODE_DECIDE>), grid, block, ldsw, h->stream, as);
                             else hipLaunchKernelGGL((k_level_wave<16, MODE_FULLP>), grid, block, ldsw, h->stream, as);
                         } else {
                             const size_t ldsw = core + 4 * sizeof(double) * (WAVE_SLOT_DOUBLES(32) + 32);
-                            if (pr && mode == MODE_DECIDE) hipLaunchKernelGGL((k_level_wave_pr<32, MODE_DECIDE>), grid, block, ldsw, h->stream, as);
-                            else if (pr) hipLaunchKernelGGL((k_level_wave_pr<32, MODE_FULLP>), grid, block, ldsw, h->stream, as);
-                            else if (mode == MODE_DECIDE) hipLaunchKernelGGL((k_level_wave<32, MODE_DECIDE>), grid, block, ldsw, h->stream, as);
+                            if (mode == MODE_DECIDE) hipLaunchKernelGGL((k_level_wave<32, MODE_DECIDE>), grid, block, ldsw, h->stream, as);
                             else hipLaunchKernelGGL((k_level_wave<32, MODE_FULLP>), grid, block, ldsw, h->stream, as);
                         }
-                    } else if (h->sp) {
-                        // per-node compact blocks of this range's nodes, then the Schur-prefix sweep
-                        hipLaunchKernelGGL(k_node_blocks, dim3((unsigned)h->n), dim3(256), 0, h->stream, as, s_lo, s_hi);
-                        size_t ldsp = 0;
-                        for (int D = d + 1; D <= h->maxdeg_small; ++D) ldsp = std::max(ldsp, sp_lds(D, 8).total);
-                        const dim3 grid((unsigned)(s_hi - s_lo)), block(256);
-                        if (d == 3) hipLaunchKernelGGL((k_level_sp<3>), grid, block, ldsp, h->stream, as);
-                        else hipLaunchKernelGGL((k_level_sp<4>), grid, block, ldsp, h->stream, as);
                     } else if (h->tgroup && use_screen32(h, d)) {
                         if (h->nblk)   // compact node blocks: the sweep stages them instead of gathering C
                             hipLaunchKernelGGL(k_node_blocks, dim3((unsigned)h->n), dim3(256), 0, h->stream, as, s_lo, s_hi);
@@ -6290,7 +5000,6 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                     aw.chunk_lo = w_lo;
                     aw.bs = 256;
                     aw.spl = h->spl_w;
-                    aw.spl_dev = a.spl_dev ? a.spl_dev + 1 : nullptr;
                     const int dl = (h->maxdeg_wide + 3) & ~3;
                     const dim3 grid((unsigned)(w_hi - w_lo)), block(256);
                     if (use_screen32(h, d)) {
@@ -6347,7 +5056,6 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
         PCG_HT(h, "run:launched");
         // exact path over the deferred list; the kernel reads the list length on the device
         // (no host round trip) and raises the overflow status byte if the list overflowed
-        if (h->fuse_end) return PCG_OK;   // the screen and exact path run in k_level_end
         // beyond PCG_MAX_DEPTH every kernel decides its band tests itself (k_level_wave,
         // k_level_lds's wave slots, k_level_deep): nothing is deferred, no launch
         if (d > PCG_MAX_DEPTH) return PCG_OK;
@@ -6379,15 +5087,6 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
     }
 }
 
-// graphs whose CSR holds at most this many entries export on the handle's stream (PCG_EXPORT_INLINE)
-#ifndef PCG_EXPORT_INLINE
-#define PCG_EXPORT_INLINE 16384
-#endif
-int64_t export_inline_max() {
-    const char *e = getenv("PCG_EXPORT_INLINE");
-    return e ? atoll(e) : (int64_t)PCG_EXPORT_INLINE;
-}
-
 // the level barrier of the current depth, enqueued: removals applied, the next graph's summary and
 // CSR (k_summary_fill), the depth's sepset export on the export stream. Returns the summary's
 // sequence number in *seq (level_end_finish waits for it).
@@ -6398,21 +5097,16 @@ int level_end_enqueue(pcg_handle *h, unsigned long long *seq) {
     // everything below is stream-ordered; the level costs ONE host sync: export the unions of
     // removed pairs (device-side append), apply the removals (SkeletonDiscovery.py:141-144),
     // recount degrees, and fetch counters + status + degrees in one batch
-    LevelArgs fa{};
-    if (h->fuse_end) {
-        fa = make_args(h, d, mode_of(h, d) == MODE_EXACT);
-    } else {
-        hipLaunchKernelGGL(k_level_close, dim3((unsigned)n), dim3(256), 0, h->stream, rmb, (uint64_t *)h->adj.p,
-                           (int32_t *)h->deg.p, h->rl, n, W, d);
-        PCG_HIP(h, hipGetLastError());
-    }
+    hipLaunchKernelGGL(k_level_close, dim3((unsigned)n), dim3(256), 0, h->stream, rmb, (uint64_t *)h->adj.p,
+                       (int32_t *)h->deg.p, h->rl, n, W, d);
+    PCG_HIP(h, hipGetLastError());
     PCG_HT(h, "end:tail-launched");
     const int xcb = h->cb;               // depth d's CSR / union buffer set (graph_launch flips cb)
     const int64_t xsum = h->sumdeg;
-    // degrees + counters + status -> host-mapped summary (fused: after the screen, exact path
-    // and removals of the same launch)
-    int rc = graph_launch(h, h->fuse_end ? &fa : nullptr);
-    if (!rc && d >= 1 && xsum > 0 && xsum <= export_inline_max()) {
+    // degrees + counters + status -> host-mapped summary
+    int rc = graph_launch(h);
+    // graphs whose CSR holds at most PCG_TUNE_EXPORT_INLINE entries export on the handle's stream
+    if (!rc && d >= 1 && xsum > 0 && xsum <= h->tune[PCG_TUNE_EXPORT_INLINE]) {
         // a small graph's export on the handle's stream, right behind the barrier: one launch
         // instead of the export stream's four calls (it runs while the host decomposes the next
         // depth, and is done before any later launch can reuse buffer set xcb)
@@ -6493,11 +5187,6 @@ int level_end_finish(pcg_handle *h, int d, unsigned long long seq, pcg_stats *st
     h->st.screened[d] = (int64_t)c.screened;
     h->st.near_alpha[d] = near_d;
     h->st.kernel_ms[d] = h->run_ms;
-    if (status[4]) {   // the fused barrier's grid barrier timed out: clear its words, fail the level
-        if (h->gbar.p) PCG_HIP(h, hipMemsetAsync(h->gbar.p, 0, sizeof(GridBar), h->stream));
-        if (stats) *stats = h->st;
-        return pcg_fail(h, PCG_ERR_HIP, "level %d: fused level barrier timed out", d);
-    }
     if (status[3]) {   // checked first: the failed rank will not rerun, so nobody may
         if (stats) *stats = h->st;
         return pcg_fail(h, PCG_ERR_PEER, "level %d: another rank failed at this depth", d);
@@ -6538,32 +5227,12 @@ extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
     return level_end_finish(h, h->depth, seq, stats);
 }
 
-// the pipelined level loop (PCG_PIPELINE=1; single GPU, the handle's own removal flags, threshold
-// mode) from depth PCG_PIPELINE_LO on. Off by default: it removes the host round trip per depth,
-// but that was not what the device waited for. Round 3, config 5 with depths 2-4 pipelined:
-// 5.21-5.25 vs 5.09 ms per step (bound-sized decomposition: too few, too large chunks where the
-// degrees still fall fast; k_decompose 21-42 us); n = 500 full depth (19 levels) from depth 2, 3
-// or 5: 2.49-2.51 vs 2.45-2.49 ms. Round 4, with the chunk size chosen on the device from the exact
-// degrees (k_decompose_dev, batched loads): config 5 4.53 vs 4.43 ms, n = 500 2.68 vs 2.50 ms
-// (host-chosen chunk size: 4.62 / 2.57) — the per-depth table upload and decomposition launches
-// and the bound-sized grids cost what the host round trip saved.
-#ifndef PCG_PIPELINE_LO
-#define PCG_PIPELINE_LO 5
-#endif
-static bool pipeline_ok(const pcg_handle *h) {
-    if (h->world != 1 || h->rm_ext) return false;
-    if (h->flags & (PCG_FLAG_FULL_P | PCG_FLAG_RECORD | PCG_FLAG_EXACT_ALL)) return false;
-    const char *e = getenv("PCG_PIPELINE");
-    return e && atoi(e) != 0;
-}
-static int pipeline_lo() {
-    const char *e = getenv("PCG_PIPELINE_LO");
-    return std::max(2, e ? atoi(e) : PCG_PIPELINE_LO);
-}
-
+// The single-GPU level loop. (Round 3/4 built a pipelined form that enqueued depth d before depth
+// d - 1's summary was read, and a fused one-launch level barrier; both measured slower — DESIGN §9
+// — and were removed in round 5.)
 static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N, double alpha,
                          int max_depth, int flags, int8_t *removed_level) {
-    h->htrace_on = getenv("PCG_HOST_TRACE") != nullptr;
+    h->htrace_on = h->tune[PCG_TUNE_HOST_TRACE] != 0;
     h->htrace.clear();
     PCG_HT(h, "init:start");
     // level d's wall time = between the depth-boundary events graph_launch records after init's
@@ -6574,59 +5243,20 @@ static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc,
     if (rc) { h->lev_on = false; return rc; }
     PCG_HT(h, "init:done");
     int done = 0;
-    // Depth d >= 2 is decomposed on the degrees at the start of depth d - 1 (upper bounds) and
-    // enqueued before depth d - 1's summary is read, so the device runs from one depth into the
-    // next without waiting for the host; k_decompose computes the exact prefixes, the launches are
-    // sized by the bounds and their surplus blocks exit at once. `pending` is the depth whose
-    // summary has not been read yet.
-    int pending = -1;
-    unsigned long long pending_seq = 0;
-    auto finish_pending = [&]() -> int {
-        if (pending < 0) return PCG_OK;
-        const int r = level_end_finish(h, pending, pending_seq, nullptr);
-        pending = -1;
-        return r;
-    };
     for (int depth = 0;; ++depth) {
         if (max_depth >= 0 && depth > max_depth) break;
         if (depth >= PCG_MAX_LEVELS) break;   // pcg_level_begin refuses deeper levels itself
         int64_t total = 0;
         PCG_HT(h, "loop:begin");
-        const bool pipe = depth >= pipeline_lo() && pending == depth - 1 && pipeline_ok(h) &&
-                          mode_of(h, depth) == MODE_DECIDE;
-        if (!pipe) {
-            rc = finish_pending();
-            if (!rc) rc = level_begin_impl(h, depth, &total, false);
-            if (rc == 1) break;
-            if (!rc) rc = pcg_level_run(h, 0, total);
-            unsigned long long seq = 0;
-            if (!rc) rc = level_end_enqueue(h, &seq);
-            if (rc) { h->lev_on = false; return rc; }
-            done = depth + 1;
-            if (depth + 1 >= pipeline_lo() && pipeline_ok(h)) {   // the next depth is enqueued before this summary is read
-                pending = depth;
-                pending_seq = seq;
-            } else {
-                rc = level_end_finish(h, depth, seq, nullptr);
-                if (rc) { h->lev_on = false; return rc; }
-            }
-            continue;
-        }
-        rc = level_begin_impl(h, depth, &total, true);
-        if (rc == 1) break;                   // not even the bound degrees allow another depth
+        rc = level_begin_impl(h, depth, &total);
+        if (rc == 1) break;
         if (!rc) rc = pcg_level_run(h, 0, total);
         unsigned long long seq = 0;
         if (!rc) rc = level_end_enqueue(h, &seq);
-        if (!rc) rc = finish_pending();       // depth - 1's counters; h->deg_h: the start of depth
+        if (!rc) rc = level_end_finish(h, depth, seq, nullptr);
         if (rc) { h->lev_on = false; return rc; }
-        if (!(h->maxdeg - 1 > depth - 1)) break;   // the enqueued depth found no work on the device
-        level_start_stats(h, depth);
         done = depth + 1;
-        pending = depth;
-        pending_seq = seq;
     }
-    rc = finish_pending();
-    if (rc) { h->lev_on = false; return rc; }
     h->lev_on = false;
     rc = export_sync(h);                 // the last depth's export (the skeleton's sepset rows)
     if (rc) return rc;
@@ -6651,14 +5281,14 @@ static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc,
 
 namespace {
 // the small-graph path is taken for n <= SMALL_N on one rank with the handle's own removal flags
-// (PCG_SMALL=0: the level loop for every size, an A/B knob)
+// (PCG_TUNE_SMALL = 0: the level loop for every size)
 bool small_ok(const pcg_handle *h, int64_t n) {
     if (n < 2 || n > SMALL_N || h->world != 1 || h->rm_ext) return false;
-    const char *e = getenv("PCG_SMALL");
-    return !e || atoi(e) != 0;
+    return h->tune[PCG_TUNE_SMALL] != 0;
 }
 
-// returns PCG_OK, an error, or 1: deeper than SMALL_MAXD (the caller reruns on the level loop)
+// returns PCG_OK, an error, or 1: deeper than SMALL_MAXD or a full band queue (the caller reruns
+// on the level loop)
 int skeleton_small(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N, double alpha, int max_depth,
                    int flags, int8_t *removed_level) {
     if (!h || !C || !removed_level || n < 2 || ldc < n || !(alpha > 0 && alpha < 1))
@@ -6711,6 +5341,7 @@ int skeleton_small(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64
     a.fullp = (flags & (PCG_FLAG_FULL_P | PCG_FLAG_RECORD)) ? 1 : 0;
     a.record = (flags & PCG_FLAG_RECORD) ? 1 : 0;
     a.exact_all = (flags & PCG_FLAG_EXACT_ALL) ? 1 : 0;
+    a.qcap = (int)std::min<int64_t>(std::max<int64_t>(h->tune[PCG_TUNE_SMALL_QCAP], 1), SMALL_QCAP);
     a.sum = (SmallSummary *)h->small_sum.p;
     a.ctr = reinterpret_cast<unsigned long long *>((char *)h->small_sum.p + sizeof(SmallSummary) + 8 -
                                                    (sizeof(SmallSummary) % 8));
@@ -6731,21 +5362,33 @@ int skeleton_small(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64
     double *cst_dev = reinterpret_cast<double *>((char *)a.ctr + 64);
     a.depth_cst = cst_dev;
     PCG_HIP(h, hipMemcpyAsync(cst_dev, cst, sizeof(cst), hipMemcpyHostToDevice, h->stream));
-    PCG_HIP(h, hipMemsetAsync(a.ctr, 0, 2 * sizeof(unsigned long long), h->stream));
     hipEvent_t *ev = h->lev;
     for (int k = 0; k < 2; ++k)
         if (!ev[k]) PCG_HIP(h, hipEventCreate(&ev[k]));
-    PCG_HIP(h, hipEventRecord(ev[0], h->stream));
-    hipLaunchKernelGGL(k_pc_small, dim3(1), dim3(SMALL_WAVES * 64), small_lds_bytes((int)n), h->stream, a);
-    PCG_HIP(h, hipGetLastError());
-    PCG_HIP(h, hipEventRecord(ev[1], h->stream));
-    const size_t sb = sizeof(SmallSummary) + 64;
-    PCG_HIP(h, hipMemcpyAsync(h->small_pin.p, h->small_sum.p, sb, hipMemcpyDeviceToHost, h->stream));
-    PCG_HIP(h, hipStreamSynchronize(h->stream));
     const SmallSummary *sm = (const SmallSummary *)h->small_pin.p;
     const unsigned long long *c2 = reinterpret_cast<const unsigned long long *>(
         (const char *)h->small_pin.p + ((const char *)a.ctr - (const char *)h->small_sum.p));
-    if (sm->status & 4) return 1;
+    for (int attempt = 0;; ++attempt) {
+        PCG_HIP(h, hipMemsetAsync(a.ctr, 0, 2 * sizeof(unsigned long long), h->stream));
+        PCG_HIP(h, hipEventRecord(ev[0], h->stream));
+        hipLaunchKernelGGL(k_pc_small, dim3(1), dim3(SMALL_WAVES * 64), small_lds_bytes((int)n), h->stream, a);
+        PCG_HIP(h, hipGetLastError());
+        PCG_HIP(h, hipEventRecord(ev[1], h->stream));
+        const size_t sb = sizeof(SmallSummary) + 64;
+        PCG_HIP(h, hipMemcpyAsync(h->small_pin.p, h->small_sum.p, sb, hipMemcpyDeviceToHost, h->stream));
+        PCG_HIP(h, hipStreamSynchronize(h->stream));
+        if (sm->status & 12) return 1;
+        // the record list overflowed (the records are of the whole run: a too small
+        // record_capacity, or none set): enlarge it as the level loop does and run again
+        if (!(flags & PCG_FLAG_RECORD) || (int64_t)c2[1] <= h->rec_cap) break;
+        if (attempt >= 2)
+            return pcg_fail(h, PCG_ERR_OVERFLOW, "record buffer overflow (%llu > %lld)", c2[1], (long long)h->rec_cap);
+        h->rec_cap = std::max<int64_t>(h->rec_cap * 4, (int64_t)c2[1] * 2);
+        if (!pcg_ensure(h, h->records, sizeof(pcg_record) * h->rec_cap))
+            return pcg_fail(h, PCG_ERR_OOM, "record buffer (%lld)", (long long)h->rec_cap);
+        a.records = (pcg_record *)h->records.p;
+        a.rec_cap = h->rec_cap;
+    }
     int wall_khz = 100000;            // wall_clock64's rate (kHz)
     (void)hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, h->device);
     if (wall_khz <= 0) wall_khz = 100000;
@@ -6769,8 +5412,6 @@ int skeleton_small(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64
         PCG_HIP(h, hipMemcpy(h->near_h.data(), h->nearbuf.p, sizeof(pcg_record) * nn, hipMemcpyDeviceToHost));
     }
     if (flags & PCG_FLAG_RECORD) {
-        if ((int64_t)c2[1] > h->rec_cap)
-            return pcg_fail(h, PCG_ERR_OVERFLOW, "record buffer overflow (%llu > %lld)", c2[1], (long long)h->rec_cap);
         h->rec_h.resize((size_t)c2[1]);
         if (c2[1])
             PCG_HIP(h, hipMemcpy(h->rec_h.data(), h->records.p, sizeof(pcg_record) * c2[1], hipMemcpyDeviceToHost));
@@ -6789,17 +5430,21 @@ int skeleton_small(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64
 extern "C" int pcg_skeleton(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N, double alpha,
                             int max_depth, int flags, int8_t *removed_level, pcg_stats *stats) {
     int rc = PCG_OK;
+    int driver = PCG_DRIVER_LEVELS;
     if (h && small_ok(h, n)) {
         rc = skeleton_small(h, C, n, ldc, N, alpha, max_depth, flags, removed_level);
         if (rc != 1) {
+            h->st.driver = PCG_DRIVER_SMALL;
             if (stats) *stats = h->st;
             return rc;
         }
+        driver = PCG_DRIVER_SMALL_RERUN;
     }
     for (int attempt = 0; attempt < 6; ++attempt) {
         rc = skeleton_once(h, C, n, ldc, N, alpha, max_depth, flags, removed_level);
         if (rc != PCG_ERR_OVERFLOW) break;
     }
+    if (h) h->st.driver = driver;
     if (stats && h) *stats = h->st;
     return rc;
 }

@@ -281,20 +281,22 @@ def sharded_corr(eng, X, group=None):
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     cdev = eng.device if dist.get_backend(group) == "nccl" else "cpu"
     N, n = X.shape
-    # a local failure (e.g. OOM on the residue planes) and the share's size (a function of the
-    # K1 plan, which each process's PCG_K1_* knobs select) are agreed before the all-gather, so no
-    # rank waits in it for a peer that raised or gathers shares of another size
-    packed, err = None, None
+    # a local failure (e.g. OOM on the residue planes) and the K1 plan (path, moduli, bits,
+    # split-K: pcg_k1_plan_signature under each handle's PCG_TUNE_K1_* knobs) with the share's size
+    # are agreed before the all-gather, so no rank waits in it for a peer that raised, or gathers
+    # shares it would read in another unit order
+    packed, err, sig = None, None, 0
     try:
+        sig = int(eng.k1_plan_signature(n, N))
         packed = eng.corr_shard(eng.to_device(X), rank, world)
     except Exception as e:   # noqa: BLE001 - must reach the agreement below
         err = e
-    failed, same = agree_value(err is not None, packed.numel() if packed is not None else 0, device=cdev,
-                               group=group)
+    plan = ((sig * 1000003) ^ (packed.numel() if packed is not None else 0)) & ((1 << 62) - 1)
+    failed, same = agree_value(err is not None, plan, device=cdev, group=group)
     if failed:
         raise_agreed(err, "sharded K1")
     if not same:
-        raise _lib.PcgError(_lib.PCG_ERR_INVALID, "sharded K1: the ranks' K1 plans differ (PCG_K1_* environment)")
+        raise _lib.PcgError(_lib.PCG_ERR_INVALID, "sharded K1: the ranks' K1 plans differ (PCG_TUNE_K1_* knobs)")
     if dist.get_backend(group) == "nccl":
         gathered = torch.empty(world * packed.numel(), dtype=torch.float64, device=eng.device)
         dist.all_gather_into_tensor(gathered, packed, group=group)

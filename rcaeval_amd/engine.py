@@ -6,6 +6,7 @@ arithmetic runs in the HIP kernels of ``libpcgpu.so``.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import time
 
@@ -107,6 +108,33 @@ class Engine:
         except Exception:
             pass
 
+    # ------------------------------------------------------------------ tuning knobs
+    def get_tuning(self, key: str) -> int:
+        v = ctypes.c_int64()
+        check(self.h, self.lib.pcg_get_tuning(self.h, _lib.TUNE_KEYS[key], ctypes.byref(v)), "pcg_get_tuning")
+        return v.value
+
+    def set_tuning(self, key: str, value: int) -> None:
+        check(self.h, self.lib.pcg_set_tuning(self.h, _lib.TUNE_KEYS[key], int(value)), f"pcg_set_tuning({key})")
+
+    @contextlib.contextmanager
+    def tuned(self, **knobs):
+        """Set pcg_set_tuning knobs (``eng.tuned(SMALL=0, LDS_DEEP=12)``) for the ``with`` body,
+        restoring the previous values after it."""
+        old = {k: self.get_tuning(k) for k in knobs}
+        try:
+            for k, v in knobs.items():
+                self.set_tuning(k, v)
+            yield self
+        finally:
+            for k, v in old.items():
+                self.set_tuning(k, v)
+
+    def k1_plan_signature(self, n: int, N: int) -> int:
+        v = ctypes.c_int64()
+        check(self.h, self.lib.pcg_k1_plan_signature(self.h, int(n), int(N), ctypes.byref(v)), "pcg_k1_plan_signature")
+        return v.value
+
     # ------------------------------------------------------------------ helpers
     def to_device(self, a) -> "object":
         torch = _torch()
@@ -135,7 +163,8 @@ class Engine:
         Xd = self.to_device(X)
         N, n = Xd.shape
         nbytes = ctypes.c_int64()
-        check(self.h, self.lib.pcg_corr_shard_bytes(n, N, int(world), ctypes.byref(nbytes)), "pcg_corr_shard_bytes")
+        check(self.h, self.lib.pcg_corr_shard_bytes(self.h, n, N, int(world), ctypes.byref(nbytes)),
+              "pcg_corr_shard_bytes")
         packed = torch.empty(nbytes.value // 8, dtype=torch.float64, device=self.device)
         check(self.h, self.lib.pcg_corr_shard(self.h, ctypes.c_void_p(Xd.data_ptr()), N, n, n, int(rank),
                                               int(world), ctypes.c_void_p(packed.data_ptr())), "pcg_corr_shard")

@@ -283,10 +283,14 @@ def stop_loaders() -> None:
 
 
 def run(dataset_dir: str, method: str, dataset: str, output: str = "output", length=None, tdelta: int = 0,
-        test: bool = False, rank: int = 0, world: int = 1, prefetch: int = 2, loader: str = "process") -> dict:
+        test: bool = False, rank: int = 0, world: int = 1, prefetch: int = 2, loader: str = "thread") -> dict:
     """Every case of ``dataset_dir`` through ``method``; rank ``r`` of ``world`` takes cases
     ``r, r + world, ...`` of the sorted list. Returns this rank's timings and, on rank 0,
-    the evaluation (after a barrier when ``world > 1``)."""
+    the evaluation (after a barrier when ``world > 1``). ``prefetch`` loaders read the next
+    cases ahead of the GPU thread: threads by default (safe from any caller); ``loader="process"``
+    uses spawned processes (faster — pandas' parser holds the GIL — but the caller's script needs
+    an ``if __name__ == "__main__"`` guard; ``main`` and ``bench.py`` opt in, and ``main`` stops them
+    at its end)."""
     is_synthetic = "circa" in dataset or "rcd" in dataset
     result_path = join(output, "results")
     os.makedirs(result_path, exist_ok=True)
@@ -361,8 +365,11 @@ def main(argv=None):
     dataset_dir = join(args.data_root, DATASET_MAP[args.dataset])
     if not exists(dataset_dir):
         raise SystemExit(f"{dataset_dir} not found (datasets are not downloaded here)")
-    res = run(dataset_dir, args.method, args.dataset, args.output, args.length, args.tdelta, args.test,
-              rank, world)
+    try:
+        res = run(dataset_dir, args.method, args.dataset, args.output, args.length, args.tdelta, args.test,
+                  rank, world, loader="process")
+    finally:
+        stop_loaders()
     if rank == 0:
         print("--- Evaluation results ---")
         for k, v in res["summary"].items():

@@ -345,7 +345,8 @@ def test_allgather_rows_packs_ragged_ranks():
 
 class _FakeK1Engine:
     """Engine stand-in for dist.sharded_corr (test only): shares of 8 doubles per rank; rank 1
-    fails ('fail') or sizes its share from another plan ('plan')."""
+    fails ('fail'), sizes its share from another plan ('plan'), or has a plan of the same share
+    size but another unit order ('sig', e.g. another split-K)."""
     device = "cpu"
 
     def __init__(self, rank, mode):
@@ -354,6 +355,9 @@ class _FakeK1Engine:
     def to_device(self, X):
         import torch
         return torch.as_tensor(X)
+
+    def k1_plan_signature(self, n, N):
+        return (1 << 62) | (7 if (self.mode == "sig" and self.rank == 1) else 3) << 32
 
     def corr_shard(self, Xd, rank, world):
         import torch
@@ -383,11 +387,12 @@ def _k1_worker(rank, world, port, mode, q):
     q.put((rank, res))
 
 
-@pytest.mark.parametrize("mode", ["ok", "fail", "plan"])
+@pytest.mark.parametrize("mode", ["ok", "fail", "plan", "sig"])
 def test_sharded_corr_agrees_failures_and_plans(mode):
     """dist.sharded_corr: shares gathered in rank order; a rank whose corr_shard raises re-raises
     its own error and every peer raises PCG_ERR_PEER before the all-gather; ranks whose K1 plans
-    give shares of different sizes all raise PCG_ERR_INVALID (nobody waits in the gather)."""
+    differ (shares of different sizes, or the same size in another unit order) all raise
+    PCG_ERR_INVALID (nobody waits in the gather)."""
     import multiprocessing as mp
     world = 3
     ctx = mp.get_context("spawn")

@@ -14,6 +14,7 @@ import numpy as np
 import pytest
 
 from rcaeval_amd import synth
+from tests_support import assert_skeleton_matches
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -328,6 +329,96 @@ def test_sharded_skeleton_two_ranks_one_gpu():
         np.testing.assert_array_equal(rl, ref.removed_level)
         assert unions(xy, bits) == unions(ref.sep_xy, ref.sep_bits)
         assert tests == ref.stats["tests"]
+
+
+def _config5_sharded_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    from rcaeval_amd.dist import sharded_corr, sharded_skeleton
+    from rcaeval_amd.engine import get_engine
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = get_engine(0)
+    X = synth.gaussian_sem(2000, 10000, seed=0)
+    C = sharded_corr(eng, eng.to_device(X))          # K1 sharded: each rank its residue units
+    out = sharded_skeleton(eng, C, 10000, max_depth=4)
+    near = [(int(r["a"]), int(r["b"])) for r in out.near_alpha]
+    q.put((rank, out.removed_level.copy(), out.sep_xy.copy(), out.sep_bits.copy(), out.stats["tests"], near,
+           float(np.abs(C.cpu().numpy() - np.corrcoef(X.T)).max())))
+    dist.barrier()
+    dist.destroy_process_group()
+    torch.cuda.synchronize()
+
+
+@pytest.mark.timeout(900)
+def test_config5_sharded_two_ranks_one_gpu_matches_oracle(config5):
+    """North-star config 5 (2000 vars x 10 000 samples, depth 4) through the multi-GPU protocol at
+    full size: 2 gloo ranks sharing cuda:0, K1 sharded by residue units (rcaeval_amd.dist
+    .sharded_corr) and every depth's work list edge-sharded (pcg_level_split) with the packed
+    removal-bit all-gather + OR merge at each level barrier. Every rank's removal depths,
+    per-level unique-test counts (summed over ranks) and sepset unions equal the C oracle's on
+    np.corrcoef(X.T) (near-alpha pairs exempt as in the single-GPU test). The protocol is verified
+    at full size; its multi-GPU timing stays unmeasured on hardware (one GPU here)."""
+    import multiprocessing as mp
+    from types import SimpleNamespace
+    _, _, ref = config5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_config5_sharded_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=800) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for rank, rl, xy, bits, tests, near, cerr in res:
+        assert cerr <= 2e-14
+        out = SimpleNamespace(removed_level=rl, sep_xy=xy, sep_bits=bits, stats={"tests": tests},
+                              near_alpha=[{"a": a, "b": b} for a, b in near])
+        assert_skeleton_matches(out, ref, 2000)
+        assert sum(tests) > 4.5e9
+
+
+def _rq2_worker(rank, world, port, root, out_dir, q):
+    import torch.distributed as dist
+    from rcaeval_amd import rq2
+    from rcaeval_amd.engine import get_engine
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    get_engine(0)
+    res = rq2.run(root, "pc_pagerank", "online-boutique", out_dir, rank=rank, world=world)
+    q.put((rank, res["my_cases"], res.get("summary")))
+    dist.destroy_process_group()
+
+
+def test_rq2_two_ranks_deal_cases_one_gpu(tmp_path):
+    """BASELINE config 2's dealing: rq2.run with rank r of 2 taking cases r, r + 2, ... of the
+    sorted tree (two processes sharing cuda:0, gloo barrier); every case's rank list, whichever
+    rank ran it, equals the CPU oracle pipeline, and rank 0 evaluates all of them."""
+    import multiprocessing as mp
+    from rcaeval_amd import rq2
+    root = os.path.join(str(tmp_path), "data", "online-boutique")
+    paths = synth.write_rq2_dataset(root, services=["cartservice", "adservice", "emailservice"],
+                                    faults=("cpu", "delay"), cases=1, rows=1200)
+    out_dir = os.path.join(str(tmp_path), "out")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rq2_worker, args=(r, 2, port, root, out_dir, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (mine, summ)) for r, mine, summ in (q.get(timeout=300) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert res[0][0] + res[1][0] == len(paths) == 6 and res[0][0] == res[1][0] == 3
+    assert set(res[0][1]) >= {"Avg@5-CPU", "Avg@5-DELAY"}
+    for p in paths:
+        c = rq2.load_case(p)
+        ranks, _ = _oracle_pipeline(c["data"], "online-boutique", "pagerank")
+        got = rq2.load_json(os.path.join(out_dir, "results", c["result_name"]))["0"]
+        assert got == ranks
 
 
 @pytest.mark.parametrize("world", [2, 3, 8])

@@ -106,26 +106,21 @@ def test_corr_crt_extreme_magnitudes(eng, N):
 
 
 @pytest.mark.parametrize("n,N", [(300, 1200), (2000, 10000)])
-def test_corr_crt_split_invariant(eng, n, N, monkeypatch):
-    """The CRT result is the correctly rounded exact Gram, so every split-K choice, the grouped
-    residue / GEMM overlap and both GEMM wave layouts (k_xtx_crt4 / k_xtx_crt) give the same bits;
-    the digit path (PCG_K1_CRT=0) agrees to within its own truncation."""
+def test_corr_crt_split_invariant(eng, n, N):
+    """The CRT result is the correctly rounded exact Gram, so every split-K choice gives the same
+    bits (and a different plan signature); the digit path (PCG_TUNE_K1_CRT = 0) agrees to within
+    its own truncation."""
     X = synth.gaussian_sem(n, N, seed=5, w_low=0.1, w_high=0.5)
     Xd = eng.to_device(X)
     C0 = eng.corr(Xd).cpu().numpy()
-    for ks in ("1", "3", "7"):
-        monkeypatch.setenv("PCG_K1_CRT_KS", ks)
-        np.testing.assert_array_equal(eng.corr(Xd).cpu().numpy(), C0)
-    monkeypatch.delenv("PCG_K1_CRT_KS")
-    for groups in ("2", "4"):            # residue groups on the aux stream beside the GEMM
-        monkeypatch.setenv("PCG_K1_CRT_GROUPS", groups)
-        np.testing.assert_array_equal(eng.corr(Xd).cpu().numpy(), C0)
-    monkeypatch.delenv("PCG_K1_CRT_GROUPS")
-    monkeypatch.setenv("PCG_K1_CRT_W4", "1")   # the 4-wave 128 x 128 GEMM and its unit byte order
-    np.testing.assert_array_equal(eng.corr(Xd).cpu().numpy(), C0)
-    monkeypatch.delenv("PCG_K1_CRT_W4")
-    monkeypatch.setenv("PCG_K1_CRT", "0")
-    Cd = eng.corr(Xd).cpu().numpy()
+    sigs = {eng.k1_plan_signature(n, N)}
+    for ks in (1, 3, 7):
+        with eng.tuned(K1_CRT_KS=ks):
+            np.testing.assert_array_equal(eng.corr(Xd).cpu().numpy(), C0)
+            sigs.add(eng.k1_plan_signature(n, N))
+    assert len(sigs) >= 3
+    with eng.tuned(K1_CRT=0):
+        Cd = eng.corr(Xd).cpu().numpy()
     np.testing.assert_allclose(Cd, C0, rtol=0, atol=1e-15)
 
 
@@ -140,15 +135,17 @@ def test_corr_small_n_many_slabs(eng, n, N):
 
 @pytest.mark.parametrize("n,N,seed,wl,wh,ep", CASES)
 @pytest.mark.parametrize("flags", [0, _lib.PCG_FLAG_FULL_P | _lib.PCG_FLAG_RECORD])
-@pytest.mark.parametrize("small", ["1", "0"])
-def test_skeleton_matches_oracle(eng, n, N, seed, wl, wh, ep, flags, small, monkeypatch):
+@pytest.mark.parametrize("small", [1, 0])
+def test_skeleton_matches_oracle(eng, n, N, seed, wl, wh, ep, flags, small):
     """Both drivers: n <= 64 runs the single-workgroup small-graph kernel (k_pc_small) unless
-    PCG_SMALL=0 sends it through the level loop; larger n always take the level loop."""
-    monkeypatch.setenv("PCG_SMALL", small)
+    PCG_TUNE_SMALL = 0 sends it through the level loop; larger n always take the level loop
+    (pcg_stats.driver says which one produced the result)."""
     X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
     C = np.corrcoef(X.T)
     ref = cpc.skeleton(C, N, record_cap=2_000_000)
-    out = eng.skeleton(C, N, flags=flags, record_capacity=2_000_000)
+    with eng.tuned(SMALL=small):
+        out = eng.skeleton(C, N, flags=flags, record_capacity=2_000_000)
+    assert out.stats["driver"] == ("small" if small and n <= 64 else "levels")
     assert_skeleton_matches(out, ref, n)
     if flags & _lib.PCG_FLAG_RECORD:
         d = {_key(r): r["p"] for r in ref.records}
@@ -161,104 +158,42 @@ def test_skeleton_matches_oracle(eng, n, N, seed, wl, wh, ep, flags, small, monk
 
 @pytest.mark.parametrize("narrow", [4, 16])
 @pytest.mark.parametrize("n,N,seed,wl,wh,ep", CASES)
-def test_wide_and_large_classes_match_oracle(eng, n, N, seed, wl, wh, ep, narrow, monkeypatch):
+def test_wide_and_large_classes_match_oracle(eng, n, N, seed, wl, wh, ep, narrow):
     """Nodes above `narrow` neighbours leave the LDS-resident class: at the T-group depths they
     run the WIDE (128-bit mask) T-group kernel, elsewhere the staged kernels — the skeleton,
     the unions and the per-level test counts stay the oracle's."""
-    monkeypatch.setenv("PCG_SMALL", "0")   # the level-loop kernels under test, also at n <= 64
     X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
     C = np.corrcoef(X.T)
     ref = cpc.skeleton(C, N)
     _lib.check(eng.h, eng.lib.pcg_set_narrow_degree(eng.h, narrow), "pcg_set_narrow_degree")
     try:
-        out = eng.skeleton(C, N)
+        with eng.tuned(SMALL=0):   # the level-loop kernels under test, also at n <= 64
+            out = eng.skeleton(C, N)
     finally:
         eng.lib.pcg_set_narrow_degree(eng.h, 64)
+    assert out.stats["driver"] == "levels"
     assert_skeleton_matches(out, ref, n)
 
 
-@pytest.mark.parametrize("mask", ["0", "0x1c"])
+@pytest.mark.parametrize("mask", [0, 0x1c])
 @pytest.mark.parametrize("narrow", [64, 16])
 @pytest.mark.parametrize("n,N,seed,wl,wh,ep", CASES[2:])
-def test_screen_precision_masks_match_oracle(eng, n, N, seed, wl, wh, ep, narrow, mask, monkeypatch):
+def test_screen_precision_masks_match_oracle(eng, n, N, seed, wl, wh, ep, narrow, mask):
     """The fp32-screened T-group sweep (k_level_lds_f) against the all-fp64 one (mask 0) and
     with depth 2 screened too (0x1c), narrow and wide classes: identical skeletons, unions and
-    per-level counts (PCG_SCREEN_MASK is read per skeleton call)."""
-    monkeypatch.setenv("PCG_SMALL", "0")   # the level-loop kernels under test, also at n <= 64
+    per-level counts (PCG_TUNE_SCREEN_MASK)."""
     X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
     C = np.corrcoef(X.T)
     ref = cpc.skeleton(C, N)
-    monkeypatch.setenv("PCG_SCREEN_MASK", mask)
     _lib.check(eng.h, eng.lib.pcg_set_narrow_degree(eng.h, narrow), "pcg_set_narrow_degree")
     try:
-        out = eng.skeleton(C, N)
+        with eng.tuned(SMALL=0, SCREEN_MASK=mask):   # the level-loop kernels, also at n <= 64
+            out = eng.skeleton(C, N)
     finally:
         eng.lib.pcg_set_narrow_degree(eng.h, 64)
     assert_skeleton_matches(out, ref, n)
-    if mask == "0":
+    if mask == 0:
         assert sum(out.stats["screened"]) == 0
-
-
-@pytest.mark.parametrize("sp", ["0", "0x8", "0x10", "0x18"])
-@pytest.mark.parametrize("n,N,seed,wl,wh,ep", CASES[2:] + [(300, 1500, 7, 0.1, 0.6, 0.06)])
-def test_schur_prefix_sweep_matches_oracle(eng, n, N, seed, wl, wh, ep, sp, monkeypatch):
-    """The Schur-prefix sweep (k_level_sp: P1 = C - w0 w0^T staged per prefix t0, chunks of
-    several prefixes per block) on depth 3, depth 4, both, or neither (k_level_lds_f):
-    identical skeletons, unions and per-level counts (PCG_SP is read per depth)."""
-    monkeypatch.setenv("PCG_SMALL", "0")   # the level-loop kernels under test, also at n <= 64
-    X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
-    C = np.corrcoef(X.T)
-    ref = cpc.skeleton(C, N)
-    monkeypatch.setenv("PCG_SP", sp)
-    out = eng.skeleton(C, N)
-    assert_skeleton_matches(out, ref, n)
-
-
-@pytest.mark.parametrize("lo,dspl", [("2", "1"), ("3", "1"), ("5", "1"), ("2", "0")])
-@pytest.mark.parametrize("n,N,seed,wl,wh,ep", [CASES[6], (300, 1500, 7, 0.1, 0.6, 0.06)])
-def test_pipelined_level_loop_matches_oracle(eng, n, N, seed, wl, wh, ep, lo, dspl, monkeypatch):
-    """The pipelined level loop (PCG_PIPELINE=1: depth d >= PCG_PIPELINE_LO decomposed on the
-    degrees at the start of d - 1 and enqueued before depth d - 1's summary is read, the exact
-    prefixes written on the device — with the chunk size chosen there from the exact degrees
-    (k_decompose_dev) or the host's from the bounds (PCG_DEV_SPL=0, k_decompose) — bound-sized
-    launches): the oracle's skeleton, unions, per-level counts and level count, unlimited depth."""
-    monkeypatch.setenv("PCG_SMALL", "0")   # the level-loop kernels under test, also at n <= 64
-    X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
-    C = np.corrcoef(X.T)
-    ref = cpc.skeleton(C, N)
-    monkeypatch.setenv("PCG_PIPELINE", "1")
-    monkeypatch.setenv("PCG_PIPELINE_LO", lo)
-    monkeypatch.setenv("PCG_DEV_SPL", dspl)
-    out = eng.skeleton(C, N)
-    assert_skeleton_matches(out, ref, n)
-    assert out.levels == ref.levels
-
-
-@pytest.mark.parametrize("flags", [0, _lib.PCG_FLAG_FULL_P | _lib.PCG_FLAG_RECORD, _lib.PCG_FLAG_EXACT_ALL])
-@pytest.mark.parametrize("n,N,seed,wl,wh,ep", [CASES[6], (300, 1500, 7, 0.1, 0.6, 0.06)])
-def test_fused_level_barrier_equals_separate_launches(eng, n, N, seed, wl, wh, ep, flags, monkeypatch):
-    """The fused level barrier (k_level_end: screen, exact path, removals, summary + CSR in one
-    launch with grid barriers) against the separate launches (PCG_FUSE_END=0): identical removal
-    depths, per-level counters, degree snapshots and sepset rows; both equal the oracle."""
-    monkeypatch.setenv("PCG_SMALL", "0")   # the level-loop kernels under test, also at n <= 64
-    X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
-    C = np.corrcoef(X.T)
-    outs = []
-    for fuse in ("1", "0"):
-        monkeypatch.setenv("PCG_FUSE_END", fuse)
-        outs.append(eng.skeleton(C, N, flags=flags, record_capacity=2_000_000))
-    a, b = outs
-    np.testing.assert_array_equal(a.removed_level, b.removed_level)
-    for k in ("levels", "tests", "calls", "indep", "exact", "screened", "edges_after", "max_degree", "error"):
-        assert a.stats[k] == b.stats[k], k
-    np.testing.assert_array_equal(a.deg_levels, b.deg_levels)
-    rows = [sorted((int(x), int(y), tuple(int(v) for v in r)) for (x, y), r in
-                   zip(np.asarray(o.sep_xy.cpu() if hasattr(o.sep_xy, "cpu") else o.sep_xy),
-                       np.asarray(o.sep_bits.cpu() if hasattr(o.sep_bits, "cpu") else o.sep_bits))) for o in outs]
-    assert rows[0] == rows[1]
-    if flags & _lib.PCG_FLAG_RECORD:
-        assert len(a.records) == len(b.records)
-    assert_skeleton_matches(a, cpc.skeleton(C, N), n)
 
 
 def test_screen_list_overflow_reruns(eng):
@@ -318,7 +253,7 @@ def test_decide_and_fullp_agree_2000_depth2(eng):
 
 
 @pytest.mark.timeout(900)
-def test_config5_full_depth4_matches_oracle(eng):
+def test_config5_full_depth4_matches_oracle(eng, config5):
     """BASELINE config 5 at full size and full depth: 2000 vars x 10 000 samples, seed 0,
     max_depth 4 — the benchmarked workload, whose depth 4 (83 % of the 4.9e9 unique tests) runs
     on the dominant k_level_lds_t<4> kernel. Threshold-mode removal depth of every pair from
@@ -327,21 +262,15 @@ def test_config5_full_depth4_matches_oracle(eng):
     full-p kernels on the same graph, with recorded p of a fixed pair sample (1 in 4099 pairs,
     every depth) within 1e-9 relative (+2^-51) of the oracle's FisherZ."""
     import sys
-    import time
-    X = synth.gaussian_sem(2000, 10000, seed=0)
+    X, Ch, ref = config5
     # K1 + skeleton through the one C call (pcg_pc_skeleton); the oracle runs on numpy's
     # corrcoef, so the correlation kernel is inside the end-to-end comparison
     a, C = eng.corr_skeleton(X, max_depth=4, flags=0)
-    Ch = np.corrcoef(X.T)
     assert np.abs(C.cpu().numpy() - Ch).max() <= 2e-14
     assert a.levels == 5 and sum(a.stats["tests"]) > 4.5e9
     b = eng.skeleton(C, 10000, max_depth=4, flags=_lib.PCG_FLAG_FULL_P | _lib.PCG_FLAG_RECORD,
                      record_capacity=4_000_000, record_sample=(4099, 17))
-    t0 = time.perf_counter()
-    print("oracle: config 5 to depth 4 ...", file=sys.stderr, flush=True)
-    ref = cpc.skeleton(Ch, 10000, max_depth=4, want_union=True)
-    print(f"oracle done in {time.perf_counter() - t0:.1f} s: tests {ref.tests}, "
-          f"near-alpha {len(ref.near_alpha)} / engine {len(a.near_alpha)}", file=sys.stderr, flush=True)
+    print(f"near-alpha: oracle {len(ref.near_alpha)} / engine {len(a.near_alpha)}", file=sys.stderr, flush=True)
     flips = assert_skeleton_matches(a, ref, 2000)
     flips_b = assert_skeleton_matches(b, ref, 2000)
     # the fp32-screened sweep (default at depths 3-4) left only a small share to its fp64
@@ -519,30 +448,44 @@ def test_packed_barrier_or_merges_ranks(eng, n):
         lib.pcg_set_removal_buffer(h, None, 0)
 
 
-def test_full_depth_n500_matches_oracle(eng):
-    """The reference's default: no depth cap (SkeletonDiscovery.py:72). n = 500 of the config-5
-    SEM family runs 19 levels; depths >= 13 take the one-wave-per-set kernel (k_level_wave) —
-    removal depths, per-level test counts and sepset unions equal the C oracle's."""
+@pytest.fixture(scope="module")
+def n500():
+    """n = 500 of the config-5 SEM family at unlimited depth, and the C oracle's run on it."""
     X = synth.gaussian_sem(500, 10000, seed=0)
     C = np.corrcoef(X.T)
-    ref = cpc.skeleton(C, 10000, max_depth=-1)
-    out = eng.skeleton(C, 10000)
+    return C, cpc.skeleton(C, 10000, max_depth=-1)
+
+
+@pytest.mark.parametrize("kernels", ["default", "per_lane_all", "wave_from_13"])
+def test_full_depth_n500_matches_oracle(eng, n500, kernels):
+    """The reference's default: no depth cap (SkeletonDiscovery.py:72). n = 500 of the config-5
+    SEM family runs 19 levels — removal depths, per-level test counts and sepset unions equal the C
+    oracle's for every deep-level kernel choice:
+    * default: depths 13-16 on the per-lane k_level_lds<13..16>, 17-18 (levels of < 1e7 tests) on
+      the one-wave-per-set k_level_wave;
+    * per_lane_all: PCG_TUNE_LDS_SPILL_MIN = 0 puts depths 17 and 18 on the spilling per-lane
+      instantiations k_level_lds<17>, <18> too (band tests decided by the wave in its LDS slot);
+    * wave_from_13: PCG_TUNE_LDS_DEEP = 12, every depth beyond 12 on k_level_wave."""
+    C, ref = n500
+    knobs = {"default": {}, "per_lane_all": {"LDS_SPILL_MIN": 0}, "wave_from_13": {"LDS_DEEP": 12}}[kernels]
+    with eng.tuned(**knobs):
+        out = eng.skeleton(C, 10000)
     assert out.levels == ref.levels == 19
+    assert out.stats["tests"][17] > 0 and out.stats["tests"][18] > 0
     assert_skeleton_matches(out, ref, 500)
 
 
 @pytest.mark.parametrize("n,N,seed,wl,wh,ep", CASES[:5])
 @pytest.mark.parametrize("flags", [0, _lib.PCG_FLAG_FULL_P | _lib.PCG_FLAG_RECORD])
-def test_wave_kernel_from_depth5_matches_oracle(eng, n, N, seed, wl, wh, ep, flags, monkeypatch):
-    """k_level_wave at every depth >= 5 (PCG_WAVE_LO=5): the deferred-list exact path and the
-    FULL_P records of |S| <= 12 go through it too; skeleton, unions, counts and records as the
+def test_wave_kernel_from_depth5_matches_oracle(eng, n, N, seed, wl, wh, ep, flags):
+    """k_level_wave at every depth >= 5 (PCG_TUNE_WAVE_LO = 5): the deferred-list exact path and
+    the FULL_P records of |S| <= 12 go through it too; skeleton, unions, counts and records as the
     oracle's."""
-    monkeypatch.setenv("PCG_SMALL", "0")   # the level-loop kernels under test, also at n <= 64
-    monkeypatch.setenv("PCG_WAVE_LO", "5")
     X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
     C = np.corrcoef(X.T)
     ref = cpc.skeleton(C, N, record_cap=2_000_000)
-    out = eng.skeleton(C, N, flags=flags, record_capacity=2_000_000)
+    with eng.tuned(SMALL=0, WAVE_LO=5):   # the level-loop kernels under test, also at n <= 64
+        out = eng.skeleton(C, N, flags=flags, record_capacity=2_000_000)
     assert_skeleton_matches(out, ref, n)
     if flags & _lib.PCG_FLAG_RECORD:
         d = {_key(r): r["p"] for r in ref.records}
@@ -558,17 +501,18 @@ def _engine_state(out):
             unions_from_engine(out))
 
 
-def test_deep_per_lane_kernel_equals_wave_kernels_n1000(eng, monkeypatch):
+def test_deep_per_lane_kernel_equals_wave_kernels_n1000(eng):
     """Threshold-mode depths 13..20 on the per-lane k_level_lds (band tests decided by the wave in
     its LDS slot; depths 17..20 for levels of >= 1e7 tests) against the one-wave-per-set kernels
-    (PCG_LDS_DEEP=12) on n = 1000 at unlimited depth (30 levels, 3.3e10 tests): removal depths,
-    per-level counts and sepset unions identical. (The C oracle takes hours here; n = 500's oracle
-    test covers depths 13..16 of the same path.)"""
+    (PCG_TUNE_LDS_DEEP = 12) on n = 1000 at unlimited depth (30 levels, 3.3e10 tests): removal
+    depths, per-level counts and sepset unions identical. (The C oracle takes hours here; both
+    kernel families at every depth they run here are pinned to the oracle by n = 500's test,
+    test_full_depth_n500_matches_oracle, and by the n = 1000 golden below.)"""
     X = synth.gaussian_sem(1000, 10000, seed=0)
     C = np.corrcoef(X.T)
     a = _engine_state(eng.skeleton(C, 10000))
-    monkeypatch.setenv("PCG_LDS_DEEP", "12")
-    b = _engine_state(eng.skeleton(C, 10000))
+    with eng.tuned(LDS_DEEP=12):
+        b = _engine_state(eng.skeleton(C, 10000))
     assert len(a[1]) == len(b[1]) == 30
     np.testing.assert_array_equal(a[0], b[0])
     assert a[1] == b[1] and a[2] == b[2]
@@ -576,17 +520,17 @@ def test_deep_per_lane_kernel_equals_wave_kernels_n1000(eng, monkeypatch):
 
 
 @pytest.mark.parametrize("n,N,seed,wl,wh,ep", CASES[:3])
-def test_inline_export_equals_export_stream(eng, n, N, seed, wl, wh, ep, monkeypatch):
-    """Small graphs export their sepset unions on the handle's stream (PCG_EXPORT_INLINE); the
-    export stream (PCG_EXPORT_INLINE=0) gives the same rows, and both match the oracle."""
-    monkeypatch.setenv("PCG_SMALL", "0")
+def test_inline_export_equals_export_stream(eng, n, N, seed, wl, wh, ep):
+    """Small graphs export their sepset unions on the handle's stream (PCG_TUNE_EXPORT_INLINE);
+    the export stream (0) gives the same rows, and both match the oracle."""
     X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
     C = np.corrcoef(X.T)
     ref = cpc.skeleton(C, N)
-    a = eng.skeleton(C, N)
+    with eng.tuned(SMALL=0):
+        a = eng.skeleton(C, N)
     assert_skeleton_matches(a, ref, n)
-    monkeypatch.setenv("PCG_EXPORT_INLINE", "0")
-    b = eng.skeleton(C, N)
+    with eng.tuned(SMALL=0, EXPORT_INLINE=0):
+        b = eng.skeleton(C, N)
     sa, sb = _engine_state(a), _engine_state(b)
     np.testing.assert_array_equal(sa[0], sb[0])
     assert sa[3] == sb[3]

@@ -1,8 +1,11 @@
 """GPU: the single-workgroup small-graph skeleton (k_pc_small, n <= 64: the RQ2 cases) against
-the level loop (PCG_SMALL=0) and the C oracle: removal depths, per-level unique tests / calls /
-independences / edges / max degree / degree snapshots, sepset union rows, near-alpha lists,
-FULL_P | RECORD records, EXACT_ALL, background-knowledge bans, depth caps, constant (NaN)
-columns, the singular and math-domain errors, and the n = 64 / 65 switch."""
+the level loop (PCG_TUNE_SMALL = 0) and the C oracle: removal depths, per-level unique tests /
+calls / independences / edges / max degree / degree snapshots, sepset union rows, near-alpha
+lists, FULL_P | RECORD records, EXACT_ALL, background-knowledge bans, depth caps, constant (NaN)
+columns, the singular and math-domain errors, and the n = 64 / 65 switch. Every run states which
+driver produced it (pcg_stats.driver): a comparison of "small" with the level loop is only made
+when the small kernel really ran; its fallback (a full band queue, or deeper than 16 levels) is
+forced and checked on its own."""
 import numpy as np
 import pytest
 
@@ -20,9 +23,14 @@ def eng():
     return get_engine(0)
 
 
-def _run(eng, monkeypatch, small, C, N, **kw):
-    monkeypatch.setenv("PCG_SMALL", small)
-    return eng.skeleton(C, N, **kw)
+def _run(eng, monkeypatch, small, C, N, expect=None, **kw):
+    """One skeleton with PCG_TUNE_SMALL = small; the driver that produced it must be `expect`
+    (default: "small" when small = "1", else "levels")."""
+    with eng.tuned(SMALL=int(small)):
+        out = eng.skeleton(C, N, **kw)
+    want = expect or ("small" if small == "1" else "levels")
+    assert out.stats["driver"] == want, (out.stats["driver"], want)
+    return out
 
 
 def _rows(out):
@@ -63,8 +71,12 @@ def test_small_equals_level_loop_and_oracle(eng, monkeypatch, n, N, seed, wl, wh
 def test_small_records_equal_level_loop(eng, monkeypatch, n, N, seed, wl, wh, ep, flags):
     X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
     C = np.corrcoef(X.T)
-    s = _run(eng, monkeypatch, "1", C, N, flags=flags, record_capacity=1_000_000)
+    # EXACT_ALL queues every test for the wave-per-test exact path: a depth of more than the band
+    # queue's 1024 tests ends the small run and the level loop reruns (asserted below)
+    exact_all = bool(flags & _lib.PCG_FLAG_EXACT_ALL)
     lvl = _run(eng, monkeypatch, "0", C, N, flags=flags, record_capacity=1_000_000)
+    expect = "small_rerun" if exact_all and max(lvl.stats["tests"]) > 1024 else "small"
+    s = _run(eng, monkeypatch, "1", C, N, expect=expect, flags=flags, record_capacity=1_000_000)
     _same(s, lvl)
 
     def recs(o):
@@ -93,10 +105,10 @@ def test_small_constant_column_runs_deep(eng, monkeypatch):
     X[:, 4] = 1.0
     with np.errstate(invalid="ignore", divide="ignore"):
         C = np.corrcoef(X.T)
-    s = _run(eng, monkeypatch, "1", C, 400)
+    ref = cpc.skeleton(C, 400)
+    s = _run(eng, monkeypatch, "1", C, 400, expect="small" if ref.levels <= 17 else "small_rerun")
     lvl = _run(eng, monkeypatch, "0", C, 400)
     _same(s, lvl)
-    ref = cpc.skeleton(C, 400)
     assert s.levels == ref.levels > 13
     np.testing.assert_array_equal(s.removed_level, ref.removed_level)
 
@@ -107,14 +119,16 @@ def test_small_singular_and_domain_errors_like_level_loop(eng, monkeypatch):
     C = np.corrcoef(X.T)
     for small in ("1", "0"):     # the engine raises causal-learn's ValueError [U] for both
         with pytest.raises(ValueError, match="singular"):
-            _run(eng, monkeypatch, small, C, 500)
+            with eng.tuned(SMALL=int(small)):
+                eng.skeleton(C, 500)
     # N - d - 3 < 0: the reference's sqrt of a negative count (math domain error)
     X = synth.gaussian_sem(8, 5, seed=3, w_low=.5, w_high=1.0, edge_prob=.9)
     C = np.corrcoef(X.T)
     outcomes = []
     for small in ("1", "0"):
         try:
-            out = _run(eng, monkeypatch, small, C, 5)
+            with eng.tuned(SMALL=int(small)):
+                out = eng.skeleton(C, 5)
             outcomes.append(("ok", out.removed_level.tolist()))
         except Exception as e:     # noqa: BLE001 - the two drivers must fail alike
             outcomes.append((type(e).__name__, str(e)))
@@ -126,5 +140,53 @@ def test_small_switch_at_64(eng, monkeypatch):
     for n in (64, 65):
         X = synth.gaussian_sem(n, 900, seed=n, w_low=.2, w_high=.8, edge_prob=.08)
         C = np.corrcoef(X.T)
-        out = _run(eng, monkeypatch, "1", C, 900)
+        out = _run(eng, monkeypatch, "1", C, 900, expect="small" if n == 64 else "levels")
         assert_skeleton_matches(out, cpc.skeleton(C, 900), n)
+
+
+def _near_collinear(n=40, N=800, noise=1e-4):
+    """Near-duplicate columns: their tests fail the conditioning guard and queue for the exact
+    path (the band queue) in threshold mode."""
+    rng = np.random.default_rng(11)
+    X = synth.gaussian_sem(n, N, seed=12, w_low=0.2, w_high=0.8, edge_prob=0.1)
+    for j, i in ((5, 3), (17, 9), (30, 31), (22, 5)):
+        X[:, j] = X[:, i] + noise * rng.standard_normal(N)
+    return np.corrcoef(X.T), N
+
+
+@pytest.mark.parametrize("qcap", [1, 4])
+def test_small_band_queue_overflow_falls_back_to_level_loop(eng, monkeypatch, qcap):
+    """A band queue smaller than a depth's exact-path tests (PCG_TUNE_SMALL_QCAP) ends the small
+    run at that depth (status 8) and the level loop reruns the skeleton from scratch
+    (PCG_DRIVER_SMALL_RERUN): the result equals the oracle and the level loop. With the default
+    queue the same graph runs on the small kernel. (Round 4 kept deciding depths after such an
+    overflow, from incomplete removals, and hung a parity test for 60 s)"""
+    C, N = _near_collinear()
+    ref = cpc.skeleton(C, N)
+    if ref.error:
+        pytest.skip("this draw is singular")
+    full = _run(eng, monkeypatch, "1", C, N)
+    assert max(full.stats["exact"]) > qcap            # some depth sent more tests to the exact path
+    with eng.tuned(SMALL_QCAP=qcap):
+        s = _run(eng, monkeypatch, "1", C, N, expect="small_rerun")
+    lvl = _run(eng, monkeypatch, "0", C, N)
+    _same(s, lvl)
+    _same(full, lvl)
+    assert_skeleton_matches(s, ref, C.shape[0])
+
+
+def test_small_records_without_capacity_grow_the_buffer(monkeypatch):
+    """PCG_FLAG_RECORD on a fresh handle (record capacity 0): the small kernel's record list
+    overflows, the buffer grows and the small kernel runs again — every record is returned,
+    equal to the oracle's (this used to fail with PCG_ERR_OVERFLOW)."""
+    from rcaeval_amd.engine import Engine
+    e = Engine(0)
+    try:
+        X = synth.gaussian_sem(24, 600, seed=3, w_low=0.3, w_high=0.9)
+        C = np.corrcoef(X.T)
+        out = _run(e, monkeypatch, "1", C, 600, flags=_lib.PCG_FLAG_RECORD)
+        ref = cpc.skeleton(C, 600, record_cap=1 << 16)
+        assert len(out.records) == len(ref.records) == sum(out.stats["tests"])
+        assert_skeleton_matches(out, ref, 24)
+    finally:
+        e.close()

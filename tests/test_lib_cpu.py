@@ -316,7 +316,7 @@ def test_page_rank_preprocess_table_equals_visit_loop():
 def _crt_units_host(n, N):
     """corr.hip crt_plan restated: (moduli k, split-K slabs ks) of the CRT K1, or None."""
     import bench
-    km = bench.k1_crt_moduli(n, N)
+    km = bench.k1_crt_moduli(n, N, {"K1_I8": 1, "K1_CRT": 1, "K1_CRT_MINN": 256, "K1_CRT_BITS": 56})
     if km is None:
         return None
     k = km[0]
@@ -344,7 +344,7 @@ def test_corr_shard_bytes_follow_the_k1_plan(n, N, world):
     from rcaeval_amd import _lib
     lib = _lib.load()
     got = ctypes.c_int64()
-    assert lib.pcg_corr_shard_bytes(n, N, world, ctypes.byref(got)) == 0
+    assert lib.pcg_corr_shard_bytes(None, n, N, world, ctypes.byref(got)) == 0
     plan = _crt_units_host(n, N)
     if plan is None:
         rows = ctypes.c_int64()
@@ -359,11 +359,18 @@ def test_corr_shard_bytes_follow_the_k1_plan(n, N, world):
 
 
 def test_corr_crt_path_switch(monkeypatch):
-    """PCG_K1_CRT=0 routes n >= 256 back to the digit path's row share."""
+    """PCG_K1_CRT=0 (the environment default of PCG_TUNE_K1_CRT; a NULL handle reads the defaults)
+    routes n >= 256 back to the digit path's row share, with another plan signature."""
     from rcaeval_amd import _lib
     lib = _lib.load()
     got, rows = ctypes.c_int64(), ctypes.c_int64()
     monkeypatch.setenv("PCG_K1_CRT", "0")
-    assert lib.pcg_corr_shard_bytes(2000, 10000, 4, ctypes.byref(got)) == 0
+    assert lib.pcg_corr_shard_bytes(None, 2000, 10000, 4, ctypes.byref(got)) == 0
     assert lib.pcg_corr_shard_rows(2000, 4, ctypes.byref(rows)) == 0
     assert got.value == rows.value * 2000 * 8
+    sig_digit = ctypes.c_int64()
+    assert lib.pcg_k1_plan_signature(None, 2000, 10000, ctypes.byref(sig_digit)) == 0
+    monkeypatch.delenv("PCG_K1_CRT")
+    sig_crt = ctypes.c_int64()
+    assert lib.pcg_k1_plan_signature(None, 2000, 10000, ctypes.byref(sig_crt)) == 0
+    assert sig_crt.value != sig_digit.value and sig_crt.value >> 62 == 1

@@ -1,11 +1,11 @@
 #!/bin/bash
 # Build an A/B variant of libpcgpu.so with extra -D flags on skeleton.hip only (the other objects
 # are the in-tree build's): tools/build_variant.sh NAME "-DPCG_X=1 -DPCG_Y=2"
-# -> tools/micro/variants/libpcgpu_NAME.so (+ its kernel resource report)
+# -> tools/ab/libpcgpu_NAME.so (+ its kernel resource report)
 set -eu
 cd "$(dirname "$0")/../rcaeval_amd/csrc"
 name=$1; flags=$2
-out=../../tools/variants_r4
+out=../../tools/ab
 mkdir -p $out build
 make -s -j8 >/dev/null
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I../../include -I. -Wall -Wno-unused-result \

@@ -17,7 +17,7 @@ run() {
 for step in "$@"; do
   case $step in
     smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    test)  run pytest_gpu 1200 python -u -m pytest tests -m gpu -q -x --timeout 600 --timeout-method thread ;;
+    test)  run pytest_gpu 1200 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     testall) run pytest_gpu 1200 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread ;;
     bench) run bench 900 python bench.py --steps 3 --warmup 1 ;;
     benchfast) run bench 600 python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
