@@ -241,6 +241,8 @@ def parse():
     ap.add_argument("--rq2-loader", choices=["process", "thread"], default="process")
     ap.add_argument("--rq2-dataset", choices=["online-boutique", "sock-shop"], default="online-boutique",
                     help="shape of the synthetic RQ2 tree (config 2 names both)")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="pcg_set_tuning knob for the engine (e.g. NBW=2048; include/pcgpu.h PCG_TUNE_*), A/B runs")
     return ap.parse_args()
 
 
@@ -421,6 +423,9 @@ def main():
         else:
             dist.init_process_group(backend)
     eng = get_engine(device)
+    for kv in args.tune:
+        k, v = kv.split("=", 1)
+        eng.set_tuning(k, int(v, 0))
     flags = _lib.PCG_FLAG_FULL_P if args.full_p else 0
 
     X = synth.gaussian_sem(args.n, args.samples, seed=args.seed)
@@ -559,7 +564,8 @@ def main():
                                    f"ER DAG p=2/(n-1), weights +-U(0.1,0.5)",
                        "parallelism": (f"edge-sharded x{world}" + (" (native RCCL driver)" if native else ""))
                                       if world > 1 else "single GPU",
-                       "decision": "full p-value" if args.full_p else "threshold + exact band"},
+                       "decision": "full p-value" if args.full_p else "threshold + exact band",
+                       **({"tuning": args.tune} if args.tune else {})},
             "skeleton_ms": ms,
             "step_ms_all": [round(1000 * t, 3) for t in times],
             "corr_ms": [round(1000 * t, 3) for n_, t in phases if n_ == "corr"],

@@ -149,6 +149,8 @@ struct pcg_handle {
     std::vector<pcg_record> rec_h, near_h;
     int64_t rec_total = 0, near_total = 0;
     pcg_stats st{};
+    double thr_alpha = -1.0, thr_N = -1.0;   // threshold_r2 cache (make_args)
+    double thr_r2[PCG_MAX_LEVELS + 1] = {};
     float run_ms = 0.f;              // CI-test kernel time of the current level
     bool run_timed = false;          // ev[2]/ev[3] bracket this level's CI-test kernels
 

@@ -2253,6 +2253,13 @@ constexpr double F32_U = 5.9604644775390625e-08;   // 2^-24
 #ifndef PCG_TGF_ABL_D
 #define PCG_TGF_ABL_D 4   // the depth the ablation applies to (the narrow class only)
 #endif
+#ifndef PCG_TGF_PROF
+#define PCG_TGF_PROF 0    // diagnostic builds only: per-phase shader-clock cycles of k_level_lds_f at depth
+                          // PCG_TGF_PROF (narrow class) summed into g_tgf_prof, printed per level to stderr
+#endif
+#if PCG_TGF_PROF
+__device__ unsigned long long g_tgf_prof[8];   // block, staging, setup, sweep cycles (per wave); tasks; y iters; waves
+#endif
 #ifndef PCG_TGF_PKV
 #define PCG_TGF_PKV 1     // k_level_lds_f: v_T = L_T^-1 m_T with two of its rows as one packed chain (A/B: 0)
 #endif
@@ -2262,6 +2269,9 @@ constexpr double F32_U = 5.9604644775390625e-08;   // 2^-24
 #endif
 #ifndef PCG_MBF2
 #define PCG_MBF2 4
+#endif
+#ifndef PCG_WIDE_MB
+#define PCG_WIDE_MB 2     // k_level_lds_f, wide class: blocks per CU of the launch bounds
 #endif
 #ifndef PCG_MBF3
 #define PCG_MBF3 4
@@ -2328,7 +2338,7 @@ __device__ int eval_test_global(const LevelArgs &a, int x, int y, const int *Sg)
 }
 
 template <int DM, bool WIDE, bool REC = false>
-__global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds_f(LevelArgs a) {
+__global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k_level_lds_f(LevelArgs a) {
     using Mask = LMask<WIDE>;
     constexpr int DT = DM - 1;
     constexpr int TG = tg_of_depth(DM);
@@ -2343,6 +2353,11 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
     const int D = a.deg[x];
     const int32_t *nxg = a.nbr + a.off[x];
 
+#if PCG_TGF_PROF
+    constexpr bool PROF = !WIDE && !REC && DM == PCG_TGF_PROF;
+    const unsigned long long prof_t0 = PROF ? clock64() : 0ull;
+    unsigned long long prof_setup = 0, prof_sweep = 0, prof_tasks = 0, prof_y = 0, prof_stage = 0;
+#endif
     const int DS = (D + 3) & ~3;                                  // padded length / row stride
     Mask *lmask = reinterpret_cast<Mask *>(smem);                 // DS
     Mask *uself = lmask + DS;                                     // DS
@@ -2448,6 +2463,9 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
     const int tx = *s_tx;
     const int np = *s_np;
     const Mask recm = REC ? s_recm : (Mask)0;   // (threshold-mode builds: no record code in the sweep)
+#if PCG_TGF_PROF
+    if (PROF) prof_stage = clock64() - prof_t0;
+#endif
     const double Cxx = (double)(float)a.diag[x];                  // A~_xx
     const uint64_t ntask = ppre[np];
     const uint64_t spl = (uint64_t)a.spl;
@@ -2473,6 +2491,10 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
 
     int lq_prev = 0;
     for (uint64_t task = r0 + tid; task < r1; task += bs) {
+#if PCG_TGF_PROF
+        const unsigned long long prof_a = PROF ? clock64() : 0ull;
+        if (PROF) { ++prof_tasks; prof_y += D; }
+#endif
         int lq = tg_pair_search<(PCG_TG_GALLOP & 2) != 0>(ppre, np, (unsigned)task, lq_prev);
         lq_prev = lq;
         const int info = pinfo[lq];
@@ -2664,6 +2686,10 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
         const unsigned long long notok = __builtin_amdgcn_ballot_w64((vmask & ~okm) != 0u);
         const int cb0 = __builtin_amdgcn_readfirstlane(cbase);
         const bool uni = __builtin_amdgcn_ballot_w64(cbase != cb0) == 0ull;
+#if PCG_TGF_PROF
+        const unsigned long long prof_b = PROF ? clock64() : 0ull;
+        if (PROF) prof_setup += prof_b - prof_a;
+#endif
 
         // a live test of candidate jj at y = t that the sweep's check did not make certain:
         // certain independence in fp32 (recomputed) or the fp64 screen list
@@ -2930,8 +2956,24 @@ __global__ __launch_bounds__(256, WIDE ? 2 : tgf_minblocks(DM)) void k_level_lds
         }
         tests += tcount;
         tcount = 0;
+#if PCG_TGF_PROF
+        if (PROF) prof_sweep += clock64() - prof_b;
+#endif
     }
+#if PCG_TGF_PROF
+    if (PROF && (tid & 63) == 0) {
+        atomicAdd(&g_tgf_prof[1], prof_stage);
+        atomicAdd(&g_tgf_prof[2], prof_setup);
+        atomicAdd(&g_tgf_prof[3], prof_sweep);
+        atomicAdd(&g_tgf_prof[4], prof_tasks);
+        atomicAdd(&g_tgf_prof[5], prof_y);
+        atomicAdd(&g_tgf_prof[6], 1ull);
+    }
+#endif
     __syncthreads();
+#if PCG_TGF_PROF
+    if (PROF && tid == 0) atomicAdd(&g_tgf_prof[0], clock64() - prof_t0);
+#endif
     for (int t = tid; t < D; t += bs) {
         const Mask us = uself[t], up = uprop[t];
         if (!(us | up)) continue;
@@ -4233,7 +4275,14 @@ LevelArgs make_args(pcg_handle *h, int d, int mode_exact_all) {
     a.dof_negative = dof < 0;
     a.sqrt_dof = dof >= 0 ? std::sqrt(dof) : 0.0;
     if (dof > 0) {
-        const double r2 = threshold_r2(h->alpha, (double)h->N, d);
+        // cached per (alpha, N, d): the Newton solve is on the host's per-depth critical path
+        if (h->thr_alpha != h->alpha || h->thr_N != h->N) {
+            h->thr_alpha = h->alpha;
+            h->thr_N = h->N;
+            for (int k = 0; k <= PCG_MAX_LEVELS; ++k) h->thr_r2[k] = -1.0;
+        }
+        if (h->thr_r2[d] < 0.0) h->thr_r2[d] = threshold_r2(h->alpha, (double)h->N, d);
+        const double r2 = h->thr_r2[d];
         a.lo2 = r2 * (1.0 - 1e-6);
         a.hi2 = r2 * (1.0 + 1e-6);
         a.s_amgm = 0.5 * std::sqrt(r2);
@@ -4374,6 +4423,9 @@ bool use_wave(const pcg_handle *h, int mode, int d, double tests) {
 // 4096 0.192)
 #ifndef PCG_L1_PAIRS
 #define PCG_L1_PAIRS 4096
+#endif
+#ifndef PCG_CLASS_ORDER
+#define PCG_CLASS_ORDER 0
 #endif
 constexpr int64_t L1_PAIRS_PER_CHUNK = PCG_L1_PAIRS;
 int mode_of(const pcg_handle *h, int d);
@@ -4938,7 +4990,10 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                 // narrow and (wide or large) present: the wide / large classes run on the aux
                 // stream beside the narrow class, forked after everything already on the main
                 // stream and joined before the exact path
-                const bool fork = s_hi > s_lo && (w_hi > w_lo || l_hi > l_lo);
+                // PCG_CLASS_ORDER (A/B): 0 narrow launched first, the wide / large classes forked
+                // beside it; 1 the same with the wide / large launches first; 2 / 3 no fork (one
+                // stream: narrow then the rest / the rest then narrow)
+                const bool fork = PCG_CLASS_ORDER <= 1 && s_hi > s_lo && (w_hi > w_lo || l_hi > l_lo);
                 hipStream_t main_stream = h->stream;
                 if (fork) {
                     if (!h->aux) PCG_HIP(h, hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking));
@@ -4946,108 +5001,114 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                     if (!h->ev_join) PCG_HIP(h, hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
                     PCG_HIP(h, hipEventRecord(h->ev_fork, main_stream));
                 }
-                if (s_hi > s_lo) {
-                    LevelArgs as = a;
-                    as.chunk_lo = s_lo;
-                    as.bs = 256;
-                    const int dl = h->tgroup ? (h->maxdeg_small + 3) & ~3 : h->maxdeg_small;
-                    as.lds_btab_off = (int)lds_small_core(dl);
-                    size_t lds = h->tgroup ? lds_tgroup_bytes(dl, d) : lds_small_bytes(dl);
-                    if (!h->tgroup && d > PCG_MAX_DEPTH)   // k_level_lds's per-wave exact-path slots
-                        lds = std::max(lds, lds_small_core(dl) + 4 * sizeof(double) * WAVE_SLOT_DOUBLES(PCG_LDS_DEEP_TOP));
-                    if (h->wavek) {
-                        const dim3 grid((unsigned)(s_hi - s_lo)), block(256);
-                        const size_t core = lds_small_core(h->maxdeg_small);
-                        as.lds_btab_off = (int)core;
-                        if (d <= 16) {
-                            const size_t ldsw = core + 4 * sizeof(double) * (WAVE_SLOT_DOUBLES(16) + 16);
-                            if (mode == MODE_DECIDE) hipLaunchKernelGGL((k_level_wave<16, MODE_DECIDE>), grid, block, ldsw, h->stream, as);
-                            else hipLaunchKernelGGL((k_level_wave<16, MODE_FULLP>), grid, block, ldsw, h->stream, as);
-                        } else {
-                            const size_t ldsw = core + 4 * sizeof(double) * (WAVE_SLOT_DOUBLES(32) + 32);
-                            if (mode == MODE_DECIDE) hipLaunchKernelGGL((k_level_wave<32, MODE_DECIDE>), grid, block, ldsw, h->stream, as);
-                            else hipLaunchKernelGGL((k_level_wave<32, MODE_FULLP>), grid, block, ldsw, h->stream, as);
-                        }
-                    } else if (h->tgroup && use_screen32(h, d)) {
-                        if (h->nblk)   // compact node blocks: the sweep stages them instead of gathering C
-                            hipLaunchKernelGGL(k_node_blocks, dim3((unsigned)h->n), dim3(256), 0, h->stream, as, s_lo, s_hi);
-                        as.lds_btab_off = (int)lds_f32_core(dl, 8);
-                        const size_t ldsf = lds_tgroup_f_bytes(dl, d, 8);
-                        const dim3 grid((unsigned)(s_hi - s_lo)), block(256);
-                        if (d == 2) { if (rec) hipLaunchKernelGGL((k_level_lds_f<2, false, true>), grid, block, ldsf, h->stream, as); else hipLaunchKernelGGL((k_level_lds_f<2, false>), grid, block, ldsf, h->stream, as); }
-                        else if (d == 3) { if (rec) hipLaunchKernelGGL((k_level_lds_f<3, false, true>), grid, block, ldsf, h->stream, as); else hipLaunchKernelGGL((k_level_lds_f<3, false>), grid, block, ldsf, h->stream, as); }
-                        else { if (rec) hipLaunchKernelGGL((k_level_lds_f<4, false, true>), grid, block, ldsf, h->stream, as); else hipLaunchKernelGGL((k_level_lds_f<4, false>), grid, block, ldsf, h->stream, as); }
-                    } else if (h->tgroup) {
-                        const dim3 grid((unsigned)(s_hi - s_lo)), block(256);
-                        if (d == 2) hipLaunchKernelGGL((k_level_lds_t<2, false>), grid, block, lds, h->stream, as);
-                        else if (d == 3) hipLaunchKernelGGL((k_level_lds_t<3, false>), grid, block, lds, h->stream, as);
-                        else hipLaunchKernelGGL((k_level_lds_t<4, false>), grid, block, lds, h->stream, as);
-                    } else if (mode == MODE_DECIDE) launch_lds_mode<MODE_DECIDE>(h, as, s_hi - s_lo, lds);
-                    else if (mode == MODE_FULLP) launch_lds_mode<MODE_FULLP>(h, as, s_hi - s_lo, lds);
-                    else launch_lds_mode<MODE_EXACT>(h, as, s_hi - s_lo, lds);
-                }
-                struct StreamSwap {   // the wide / large classes launch on h->aux; restored on every exit
-                    pcg_handle *h; hipStream_t main; bool on;
-                    ~StreamSwap() { if (on) h->stream = main; }
-                } swap{h, main_stream, fork};
-                if (fork) {
-                    PCG_HIP(h, hipStreamWaitEvent(h->aux, h->ev_fork, 0));
-                    h->stream = h->aux;
-                }
-                if (w_hi > w_lo) {
-                    LevelArgs aw = a;
-                    aw.cpre = (const int64_t *)h->cpre.p + (h->n + 1);
-                    aw.chunk_lo = w_lo;
-                    aw.bs = 256;
-                    aw.spl = h->spl_w;
-                    const int dl = (h->maxdeg_wide + 3) & ~3;
-                    const dim3 grid((unsigned)(w_hi - w_lo)), block(256);
-                    if (use_screen32(h, d)) {
-                        aw.lds_btab_off = (int)lds_f32_core(dl, 16);
-                        const size_t lds = lds_tgroup_f_bytes(dl, d, 16);
-                        if (d == 2) { if (rec) hipLaunchKernelGGL((k_level_lds_f<2, true, true>), grid, block, lds, h->stream, aw); else hipLaunchKernelGGL((k_level_lds_f<2, true>), grid, block, lds, h->stream, aw); }
-                        else if (d == 3) { if (rec) hipLaunchKernelGGL((k_level_lds_f<3, true, true>), grid, block, lds, h->stream, aw); else hipLaunchKernelGGL((k_level_lds_f<3, true>), grid, block, lds, h->stream, aw); }
-                        else { if (rec) hipLaunchKernelGGL((k_level_lds_f<4, true, true>), grid, block, lds, h->stream, aw); else hipLaunchKernelGGL((k_level_lds_f<4, true>), grid, block, lds, h->stream, aw); }
-                    } else {
-                        aw.lds_btab_off = (int)lds_small_core(dl, 16);
-                        const size_t lds = lds_tgroup_bytes(dl, d, 16);
-                        if (d == 2) hipLaunchKernelGGL((k_level_lds_t<2, true>), grid, block, lds, h->stream, aw);
-                        else if (d == 3) hipLaunchKernelGGL((k_level_lds_t<3, true>), grid, block, lds, h->stream, aw);
-                        else hipLaunchKernelGGL((k_level_lds_t<4, true>), grid, block, lds, h->stream, aw);
+                auto run_narrow = [&]() -> int {
+                    if (s_hi > s_lo) {
+                        LevelArgs as = a;
+                        as.chunk_lo = s_lo;
+                        as.bs = 256;
+                        const int dl = h->tgroup ? (h->maxdeg_small + 3) & ~3 : h->maxdeg_small;
+                        as.lds_btab_off = (int)lds_small_core(dl);
+                        size_t lds = h->tgroup ? lds_tgroup_bytes(dl, d) : lds_small_bytes(dl);
+                        if (!h->tgroup && d > PCG_MAX_DEPTH)   // k_level_lds's per-wave exact-path slots
+                            lds = std::max(lds, lds_small_core(dl) + 4 * sizeof(double) * WAVE_SLOT_DOUBLES(PCG_LDS_DEEP_TOP));
+                        if (h->wavek) {
+                            const dim3 grid((unsigned)(s_hi - s_lo)), block(256);
+                            const size_t core = lds_small_core(h->maxdeg_small);
+                            as.lds_btab_off = (int)core;
+                            if (d <= 16) {
+                                const size_t ldsw = core + 4 * sizeof(double) * (WAVE_SLOT_DOUBLES(16) + 16);
+                                if (mode == MODE_DECIDE) hipLaunchKernelGGL((k_level_wave<16, MODE_DECIDE>), grid, block, ldsw, h->stream, as);
+                                else hipLaunchKernelGGL((k_level_wave<16, MODE_FULLP>), grid, block, ldsw, h->stream, as);
+                            } else {
+                                const size_t ldsw = core + 4 * sizeof(double) * (WAVE_SLOT_DOUBLES(32) + 32);
+                                if (mode == MODE_DECIDE) hipLaunchKernelGGL((k_level_wave<32, MODE_DECIDE>), grid, block, ldsw, h->stream, as);
+                                else hipLaunchKernelGGL((k_level_wave<32, MODE_FULLP>), grid, block, ldsw, h->stream, as);
+                            }
+                        } else if (h->tgroup && use_screen32(h, d)) {
+                            if (h->nblk)   // compact node blocks: the sweep stages them instead of gathering C
+                                hipLaunchKernelGGL(k_node_blocks, dim3((unsigned)h->n), dim3(256), 0, h->stream, as, s_lo, s_hi);
+                            as.lds_btab_off = (int)lds_f32_core(dl, 8);
+                            const size_t ldsf = lds_tgroup_f_bytes(dl, d, 8);
+                            const dim3 grid((unsigned)(s_hi - s_lo)), block(256);
+                            if (d == 2) { if (rec) hipLaunchKernelGGL((k_level_lds_f<2, false, true>), grid, block, ldsf, h->stream, as); else hipLaunchKernelGGL((k_level_lds_f<2, false>), grid, block, ldsf, h->stream, as); }
+                            else if (d == 3) { if (rec) hipLaunchKernelGGL((k_level_lds_f<3, false, true>), grid, block, ldsf, h->stream, as); else hipLaunchKernelGGL((k_level_lds_f<3, false>), grid, block, ldsf, h->stream, as); }
+                            else { if (rec) hipLaunchKernelGGL((k_level_lds_f<4, false, true>), grid, block, ldsf, h->stream, as); else hipLaunchKernelGGL((k_level_lds_f<4, false>), grid, block, ldsf, h->stream, as); }
+                        } else if (h->tgroup) {
+                            const dim3 grid((unsigned)(s_hi - s_lo)), block(256);
+                            if (d == 2) hipLaunchKernelGGL((k_level_lds_t<2, false>), grid, block, lds, h->stream, as);
+                            else if (d == 3) hipLaunchKernelGGL((k_level_lds_t<3, false>), grid, block, lds, h->stream, as);
+                            else hipLaunchKernelGGL((k_level_lds_t<4, false>), grid, block, lds, h->stream, as);
+                        } else if (mode == MODE_DECIDE) launch_lds_mode<MODE_DECIDE>(h, as, s_hi - s_lo, lds);
+                        else if (mode == MODE_FULLP) launch_lds_mode<MODE_FULLP>(h, as, s_hi - s_lo, lds);
+                        else launch_lds_mode<MODE_EXACT>(h, as, s_hi - s_lo, lds);
                     }
-                }
-                if (l_hi > l_lo && d > PCG_MAX_DEPTH) {
-                    LevelArgs al = a;
-                    al.cpre = (const int64_t *)h->cpre.p + 2 * (h->n + 1);
-                    const int64_t nch_deep = l_hi - l_lo;
-                    const int grid = (int)std::min<int64_t>(nch_deep, 512);
-                    const int m = d + 2;
-                    const size_t per = (size_t)(m * m + 2 * m + (d + 2));
-                    if (!pcg_ensure(h, h->pr_scratch, sizeof(double) * per * 64 * grid))
-                        return pcg_fail(h, PCG_ERR_OOM, "deep-level scratch");
-                    al.chunk_lo = l_lo;
-                    hipLaunchKernelGGL(k_level_deep, dim3(grid), dim3(64), 0, h->stream, al, (double *)h->pr_scratch.p,
-                                       nch_deep);
-                } else if (l_hi > l_lo) {
-                    LevelArgs al = a;
-                    al.cpre = (const int64_t *)h->cpre.p + 2 * (h->n + 1);
-                    al.chunk_lo = l_lo;
-                    const size_t lds = level_lds(h, al.bs);
-                    if (lds > LDS_MAX)
-                        return pcg_fail(h, PCG_ERR_INVALID, "max degree %d too large for LDS staging", h->maxdeg);
-                    if (mode == MODE_DECIDE && d == 1 && h->maxdeg <= L1_MAXD)
-                        hipLaunchKernelGGL(k_level1_pairs, dim3((unsigned)(l_hi - l_lo)), dim3(256),
-                                           l1_lds_bytes(h->maxdeg), h->stream, al);
-                    else if (mode == MODE_DECIDE) launch_level_mode<MODE_DECIDE>(h, al, l_hi - l_lo, lds);
-                    else if (mode == MODE_FULLP) launch_level_mode<MODE_FULLP>(h, al, l_hi - l_lo, lds);
-                    else launch_level_mode<MODE_EXACT>(h, al, l_hi - l_lo, lds);
-                }
-                if (fork) {
-                    PCG_HIP(h, hipEventRecord(h->ev_join, h->aux));
-                    h->stream = main_stream;
-                    swap.on = false;
-                    PCG_HIP(h, hipStreamWaitEvent(main_stream, h->ev_join, 0));
-                }
+                    return PCG_OK;
+                };
+                auto run_rest = [&]() -> int {
+                    struct StreamSwap {   // the wide / large classes launch on h->aux; restored on every exit
+                        pcg_handle *h; hipStream_t main; bool on;
+                        ~StreamSwap() { if (on) h->stream = main; }
+                    } swap{h, main_stream, fork};
+                    if (fork) {
+                        PCG_HIP(h, hipStreamWaitEvent(h->aux, h->ev_fork, 0));
+                        h->stream = h->aux;
+                    }
+                    if (w_hi > w_lo) {
+                        LevelArgs aw = a;
+                        aw.cpre = (const int64_t *)h->cpre.p + (h->n + 1);
+                        aw.chunk_lo = w_lo;
+                        aw.bs = 256;
+                        aw.spl = h->spl_w;
+                        const int dl = (h->maxdeg_wide + 3) & ~3;
+                        const dim3 grid((unsigned)(w_hi - w_lo)), block(256);
+                        if (use_screen32(h, d)) {
+                            aw.lds_btab_off = (int)lds_f32_core(dl, 16);
+                            const size_t lds = lds_tgroup_f_bytes(dl, d, 16);
+                            if (d == 2) { if (rec) hipLaunchKernelGGL((k_level_lds_f<2, true, true>), grid, block, lds, h->stream, aw); else hipLaunchKernelGGL((k_level_lds_f<2, true>), grid, block, lds, h->stream, aw); }
+                            else if (d == 3) { if (rec) hipLaunchKernelGGL((k_level_lds_f<3, true, true>), grid, block, lds, h->stream, aw); else hipLaunchKernelGGL((k_level_lds_f<3, true>), grid, block, lds, h->stream, aw); }
+                            else { if (rec) hipLaunchKernelGGL((k_level_lds_f<4, true, true>), grid, block, lds, h->stream, aw); else hipLaunchKernelGGL((k_level_lds_f<4, true>), grid, block, lds, h->stream, aw); }
+                        } else {
+                            aw.lds_btab_off = (int)lds_small_core(dl, 16);
+                            const size_t lds = lds_tgroup_bytes(dl, d, 16);
+                            if (d == 2) hipLaunchKernelGGL((k_level_lds_t<2, true>), grid, block, lds, h->stream, aw);
+                            else if (d == 3) hipLaunchKernelGGL((k_level_lds_t<3, true>), grid, block, lds, h->stream, aw);
+                            else hipLaunchKernelGGL((k_level_lds_t<4, true>), grid, block, lds, h->stream, aw);
+                        }
+                    }
+                    if (l_hi > l_lo && d > PCG_MAX_DEPTH) {
+                        LevelArgs al = a;
+                        al.cpre = (const int64_t *)h->cpre.p + 2 * (h->n + 1);
+                        const int64_t nch_deep = l_hi - l_lo;
+                        const int grid = (int)std::min<int64_t>(nch_deep, 512);
+                        const int m = d + 2;
+                        const size_t per = (size_t)(m * m + 2 * m + (d + 2));
+                        if (!pcg_ensure(h, h->pr_scratch, sizeof(double) * per * 64 * grid))
+                            return pcg_fail(h, PCG_ERR_OOM, "deep-level scratch");
+                        al.chunk_lo = l_lo;
+                        hipLaunchKernelGGL(k_level_deep, dim3(grid), dim3(64), 0, h->stream, al, (double *)h->pr_scratch.p,
+                                           nch_deep);
+                    } else if (l_hi > l_lo) {
+                        LevelArgs al = a;
+                        al.cpre = (const int64_t *)h->cpre.p + 2 * (h->n + 1);
+                        al.chunk_lo = l_lo;
+                        const size_t lds = level_lds(h, al.bs);
+                        if (lds > LDS_MAX)
+                            return pcg_fail(h, PCG_ERR_INVALID, "max degree %d too large for LDS staging", h->maxdeg);
+                        if (mode == MODE_DECIDE && d == 1 && h->maxdeg <= L1_MAXD)
+                            hipLaunchKernelGGL(k_level1_pairs, dim3((unsigned)(l_hi - l_lo)), dim3(256),
+                                               l1_lds_bytes(h->maxdeg), h->stream, al);
+                        else if (mode == MODE_DECIDE) launch_level_mode<MODE_DECIDE>(h, al, l_hi - l_lo, lds);
+                        else if (mode == MODE_FULLP) launch_level_mode<MODE_FULLP>(h, al, l_hi - l_lo, lds);
+                        else launch_level_mode<MODE_EXACT>(h, al, l_hi - l_lo, lds);
+                    }
+                    if (fork) PCG_HIP(h, hipEventRecord(h->ev_join, h->aux));
+                    return PCG_OK;
+                };
+                const bool rest_first = PCG_CLASS_ORDER == 1 || PCG_CLASS_ORDER == 3;
+                int rc2 = rest_first ? run_rest() : run_narrow();
+                if (!rc2) rc2 = rest_first ? run_narrow() : run_rest();
+                if (rc2) return rc2;
+                if (fork) PCG_HIP(h, hipStreamWaitEvent(main_stream, h->ev_join, 0));
             }
         }
         PCG_HIP(h, hipGetLastError());
@@ -5150,7 +5211,7 @@ int level_end_finish(pcg_handle *h, int d, unsigned long long seq, pcg_stats *st
     const DevCounters c = sm->ctr;
     uint8_t status[8];
     for (int k = 0; k < 8; ++k) status[k] = sm->status[k];
-    if (h->rev[d][1]) {
+    if (h->rev[d][1] && !h->lev_on) {   // (skeleton_once reads every depth's brackets after its last depth)
         float ms = 0.f;
         hipError_t e = hipEventElapsedTime(&ms, h->rev[d][0], h->rev[d][1]);
         if (e == hipErrorNotReady) {        // the summary can land before the runtime marks the event
@@ -5186,7 +5247,19 @@ int level_end_finish(pcg_handle *h, int d, unsigned long long seq, pcg_stats *st
     h->st.exact[d] = (int64_t)c.exact;
     h->st.screened[d] = (int64_t)c.screened;
     h->st.near_alpha[d] = near_d;
-    h->st.kernel_ms[d] = h->run_ms;
+    if (!h->lev_on) h->st.kernel_ms[d] = h->run_ms;
+#if PCG_TGF_PROF
+    if (d == PCG_TGF_PROF) {
+        unsigned long long pr[8] = {};
+        (void)hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_tgf_prof), sizeof(pr), 0, hipMemcpyDeviceToHost);
+        fprintf(stderr, "[tgf prof d%d] waves %llu  per wave: stage %.0f setup %.0f sweep %.0f cyc; tasks/lane %.2f "
+                "y/task %.1f; per wave-task setup %.0f, per wave-y sweep %.1f cyc; block %.0f cyc\n", d, pr[6],
+                (double)pr[1] / pr[6], (double)pr[2] / pr[6], (double)pr[3] / pr[6], (double)pr[4] / pr[6],
+                (double)pr[5] / pr[4], (double)pr[2] / pr[4], (double)pr[3] / pr[5], (double)pr[0] * 4.0 / pr[6]);
+        memset(pr, 0, sizeof(pr));
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tgf_prof), pr, sizeof(pr), 0, hipMemcpyHostToDevice);
+    }
+#endif
     if (status[3]) {   // checked first: the failed rank will not rerun, so nobody may
         if (stats) *stats = h->st;
         return pcg_fail(h, PCG_ERR_PEER, "level %d: another rank failed at this depth", d);
@@ -5266,6 +5339,10 @@ static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc,
             float ms = 0.f;
             PCG_HIP(h, hipEventElapsedTime(&ms, h->lev[depth], h->lev[depth + 1]));
             h->st.level_ms[depth] = ms;
+            if (h->rev[depth][1]) {     // the CI-test kernel brackets, read here, off the per-depth path
+                PCG_HIP(h, hipEventElapsedTime(&ms, h->rev[depth][0], h->rev[depth][1]));
+                h->st.kernel_ms[depth] = ms;
+            }
         }
     }
     if (h->htrace_on && !h->htrace.empty()) {

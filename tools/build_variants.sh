@@ -4,7 +4,6 @@
 set -eu
 cd "$(dirname "$0")/../rcaeval_amd/csrc"
 mkdir -p ../../tools/ab
-rm -f ../../tools/ab/libpcgpu_*.so
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   make -s -j8 BUILD=/tmp/pcg_build_$name OUT=../../tools/ab/libpcgpu_$name.so EXTRA="$flags"
