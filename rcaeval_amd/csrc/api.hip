@@ -165,7 +165,6 @@ extern "C" int pcg_destroy(pcg_handle *h) {
     for (auto &pr : h->rev)
         for (auto &e : pr)
             if (e) hipEventDestroy(e);
-    if (h->ev_fork) hipEventDestroy(h->ev_fork);
     if (h->ev_join) hipEventDestroy(h->ev_join);
     if (h->aux) hipStreamDestroy(h->aux);
     if (h->xs) hipStreamDestroy(h->xs);

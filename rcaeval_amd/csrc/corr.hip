@@ -1020,7 +1020,29 @@ static uint32_t big_div_small(const uint32_t *x, int L, uint32_t m, uint32_t *q)
 
 // the plan's knobs are the handle's (pcg_corr_sharded agrees the resulting plan's signature
 // across ranks before its all-gather, so ranks with different knobs fail together)
+static bool crt_plan_build(const int64_t *tune, int n, int64_t N, CrtPlan &p);
+
+// the plan is a pure function of (n, N) and five knobs; building it (modular inverses, the limb
+// tables) costs ~25 us of host time, which sat before K1's first launch on every call: one cached
+// plan per host thread
 bool crt_plan(const int64_t *tune, int n, int64_t N, CrtPlan &p) {
+    struct Entry {
+        int64_t key[7];
+        bool ok;
+        CrtPlan plan;
+    };
+    thread_local Entry e{{-1, -1, -1, -1, -1, -1, -1}, false, CrtPlan{}};
+    const int64_t key[7] = {n, N, tune[PCG_TUNE_K1_I8], tune[PCG_TUNE_K1_CRT], tune[PCG_TUNE_K1_CRT_MINN],
+                            tune[PCG_TUNE_K1_CRT_BITS], tune[PCG_TUNE_K1_CRT_KS]};
+    if (memcmp(key, e.key, sizeof(key)) != 0) {
+        e.ok = crt_plan_build(tune, n, N, e.plan);
+        memcpy(e.key, key, sizeof(key));
+    }
+    if (e.ok) p = e.plan;
+    return e.ok;
+}
+
+static bool crt_plan_build(const int64_t *tune, int n, int64_t N, CrtPlan &p) {
     if (!tune[PCG_TUNE_K1_I8] || !tune[PCG_TUNE_K1_CRT] || n < tune[PCG_TUNE_K1_CRT_MINN]) return false;
     const int bmin = (int)std::min<int64_t>(63, std::max<int64_t>(32, tune[PCG_TUNE_K1_CRT_BITS]));   // k_residues: b in [32, 63]
     // k: the fewest moduli whose product leaves b >= bmin bits per value, M > 2 N 4^b (0.01 bit margin)

@@ -156,7 +156,7 @@ struct pcg_handle {
 
     // second stream: a depth's large-degree class runs beside its LDS-resident class
     hipStream_t aux = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipEvent_t ev_join = nullptr;
 
     // RCCL communicator of pcg_comm_init (comm.hip): one per (process, device)
     void *comm = nullptr;

@@ -2242,8 +2242,11 @@ constexpr double F32_U = 5.9604644775390625e-08;   // 2^-24
 #ifndef PCG_TGF_SGPR
 #define PCG_TGF_SGPR 0x10 // k_level_lds_f depths (bit 1 << d) whose per-y bookkeeping is in wave lane masks
 #endif
+#ifndef PCG_TGF_Y3FAST
+#define PCG_TGF_Y3FAST 1     // per-lane y loop (YM 3): skip the dependence-bit packing when no lane needs it
+#endif
 #ifndef PCG_TGF_PREFETCH
-#define PCG_TGF_PREFETCH 0   // k_level_lds_f depths (bit 1 << d) whose per-lane y loop prefetches row t + 1
+#define PCG_TGF_PREFETCH 0  // k_level_lds_f depths (bit 1 << d) whose per-lane y loop prefetches row t + 1
                              // (depth 3: 0.703 vs 0.698 ms without it; measured no gain, off)
 #endif
 #ifndef PCG_TGF_ABL
@@ -2822,17 +2825,22 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
                 const f2v byy2 = {byy, byy}, bxy2 = {bxy, bxy};
                 const Mask lm = pre.lm;
                 if constexpr (YM == 3) {
-                    unsigned dp = 0;
+                    // dall: lanes whose every candidate is certainly dependent (lane masks, combined
+                    // on the scalar unit); the per-lane dependence bits are only built when some
+                    // lane has a candidate that is not, or an unusable one (notok)
+                    f2v wq[NQ], hq[NQ];
+                    unsigned long long dall = ~0ull;
 #pragma unroll
                     for (int q = 0; q < NQ; ++q) {
                         const f2v vc = sc[q] * rlp[q];
                         const f2v cyy = __builtin_elementwise_fma(-vc, vc, byy2);
                         const f2v cxy = __builtin_elementwise_fma(-ucp[q], vc, bxy2);
                         const f2v nm = __builtin_elementwise_fma(cxy, cxy, -k1p[q]);
-                        const f2v w = __builtin_elementwise_fma(-mp[q], cyy, nm);
-                        const f2v hh = __builtin_elementwise_fma(hhp[q], cyy, -k2p[q]);
-                        dp |= ((unsigned)(__builtin_fabsf(w[0]) < hh[0]) << (2 * q)) |
-                              ((unsigned)(__builtin_fabsf(w[1]) < hh[1]) << (2 * q + 1));
+                        wq[q] = __builtin_elementwise_fma(-mp[q], cyy, nm);
+                        hq[q] = __builtin_elementwise_fma(hhp[q], cyy, -k2p[q]);
+                        if (PCG_TGF_Y3FAST)
+                            dall &= __builtin_amdgcn_ballot_w64(__builtin_fabsf(wq[q][0]) < hq[q][0]) &
+                                    __builtin_amdgcn_ballot_w64(__builtin_fabsf(wq[q][1]) < hq[q][1]);
                     }
                     const bool inTset = (bool)((Tmask >> t) & 1u);
                     const bool own = (t < tx) && ((lm & Tmask) == Tmask);
@@ -2841,6 +2849,14 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
                     const unsigned live = inTset ? 0u : (vmask & ~tb & ~skip);
                     tcount += __popc(live);
                     const bool recy = REC && (bool)((recm >> t) & 1u);     // wave-uniform
+                    // a lane in dall with every valid candidate usable has rare = 0 (dp & okm covers
+                    // every live bit): the wave skips the bit packing when no lane is outside that
+                    if (PCG_TGF_Y3FAST && !recy && !((~dall | notok) & __builtin_amdgcn_read_exec())) return;
+                    unsigned dp = 0;
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q)
+                        dp |= ((unsigned)(__builtin_fabsf(wq[q][0]) < hq[q][0]) << (2 * q)) |
+                              ((unsigned)(__builtin_fabsf(wq[q][1]) < hq[q][1]) << (2 * q + 1));
                     const unsigned rare = recy ? live : (live & ~(dp & okm));
                     if (__builtin_amdgcn_ballot_w64(rare != 0u)) {
                         if (rare) {
@@ -4995,11 +5011,11 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                 // stream: narrow then the rest / the rest then narrow)
                 const bool fork = PCG_CLASS_ORDER <= 1 && s_hi > s_lo && (w_hi > w_lo || l_hi > l_lo);
                 hipStream_t main_stream = h->stream;
+                // the fork point is the kernel bracket's start event rv[0], recorded on the main stream
+                // just above: one event record less between the prefix copy and the first class launch
                 if (fork) {
                     if (!h->aux) PCG_HIP(h, hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking));
-                    if (!h->ev_fork) PCG_HIP(h, hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
                     if (!h->ev_join) PCG_HIP(h, hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
-                    PCG_HIP(h, hipEventRecord(h->ev_fork, main_stream));
                 }
                 auto run_narrow = [&]() -> int {
                     if (s_hi > s_lo) {
@@ -5050,7 +5066,7 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                         ~StreamSwap() { if (on) h->stream = main; }
                     } swap{h, main_stream, fork};
                     if (fork) {
-                        PCG_HIP(h, hipStreamWaitEvent(h->aux, h->ev_fork, 0));
+                        PCG_HIP(h, hipStreamWaitEvent(h->aux, rv[0], 0));
                         h->stream = h->aux;
                     }
                     if (w_hi > w_lo) {

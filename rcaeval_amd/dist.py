@@ -164,7 +164,7 @@ class GpuLevelBackend:
 
     def finish(self):
         self.lib.pcg_set_world_size(self.h, 1)
-        return self.eng._collect(self.n, self.rl, self.stats, 0.0)
+        return self.eng._collect(self.n, self.rl, self.stats, None)
 
 
 def run_sharded_levels(backend, rank: int, world: int, max_depth: int = -1, group=None, trace=None):

@@ -213,7 +213,7 @@ class Engine:
                                            ctypes.byref(st))
         check(self.h, rc, "pcg_skeleton_sharded")
         self.sync()
-        return self._collect(n, rl, st, 0.0)
+        return self._collect(n, rl, st, None)
 
     # ------------------------------------------------------------------ K2/K3
     def _banned(self, banned, n: int):
@@ -227,6 +227,14 @@ class Engine:
         check(self.h, self.lib.pcg_set_forbidden_pairs(self.h, ctypes.c_void_p(bd.data_ptr())),
               "pcg_set_forbidden_pairs")
         return bd
+
+    def _events(self):
+        """The call's (start, end) timing events, created once per engine (a fresh pair per call
+        costs two event creations on the host path between steps)."""
+        if getattr(self, "_ev_pair", None) is None:
+            torch = _torch()
+            self._ev_pair = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        return self._ev_pair
 
     def _unban(self, bd) -> None:
         if bd is not None:
@@ -247,7 +255,7 @@ class Engine:
         check(self.h, self.lib.pcg_set_record_sample(self.h, int(record_sample[0]), int(record_sample[1])),
               "pcg_set_record_sample")
         st = PcgStats()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0, ev1 = self._events()
         bd = self._banned(banned, n)
         try:
             ev0.record()
@@ -258,9 +266,8 @@ class Engine:
         finally:
             self._unban(bd)
         check(self.h, rc, "pcg_skeleton")
-        ev1.synchronize()       # the call returned after its last device phase; the timing event follows it
         t0 = time.perf_counter()
-        out = self._collect(n, rl, st, ev0.elapsed_time(ev1))
+        out = self._collect(n, rl, st, (ev0, ev1))
         out.extra["collect_ms"] = 1000.0 * (time.perf_counter() - t0)
         out.extra["device_ms"] = out.device_ms
         return out
@@ -277,7 +284,7 @@ class Engine:
             check(self.h, self.lib.pcg_set_capacity(self.h, int(record_capacity), 0), "pcg_set_capacity")
         check(self.h, self.lib.pcg_set_record_sample(self.h, 0, 0), "pcg_set_record_sample")
         st = PcgStats()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0, ev1 = self._events()
         bd = self._banned(banned, n)
         try:
             ev0.record()
@@ -288,19 +295,15 @@ class Engine:
         finally:
             self._unban(bd)
         check(self.h, rc, "pcg_pc_skeleton")
-        ev1.synchronize()
         t0 = time.perf_counter()
-        out = self._collect(n, rl, st, ev0.elapsed_time(ev1))
+        out = self._collect(n, rl, st, (ev0, ev1))
         out.extra["collect_ms"] = 1000.0 * (time.perf_counter() - t0)
         out.extra["device_ms"] = out.device_ms
         return out, C
 
-    def _collect(self, n: int, rl, st: PcgStats, device_ms: float) -> SkeletonOut:
-        L = st.levels
-        deg = np.zeros((max(L, 1), n), np.int32)
-        if L:
-            check(self.h, self.lib.pcg_degrees(self.h, deg.ctypes.data_as(ctypes.c_void_p), deg.size),
-                  "pcg_degrees")
+    def _collect(self, n: int, rl, st: PcgStats, events=None) -> SkeletonOut:
+        # the sepset rows' device copies are enqueued first (they are the step's last device work);
+        # the host-side results are gathered while they run
         torch = _torch()
         cnt, W = ctypes.c_int64(), ctypes.c_int32()
         check(self.h, self.lib.pcg_sepset_count(self.h, ctypes.byref(cnt), ctypes.byref(W)), "pcg_sepset_count")
@@ -310,6 +313,11 @@ class Engine:
             check(self.h, self.lib.pcg_sepset_export_device(self.h, ctypes.c_void_p(xy.data_ptr()),
                                                             ctypes.c_void_p(bits.data_ptr()), cnt.value),
                   "pcg_sepset_export_device")
+        L = st.levels
+        deg = np.zeros((max(L, 1), n), np.int32)
+        if L:
+            check(self.h, self.lib.pcg_degrees(self.h, deg.ctypes.data_as(ctypes.c_void_p), deg.size),
+                  "pcg_degrees")
         rc_, nc_ = ctypes.c_int64(), ctypes.c_int64()
         check(self.h, self.lib.pcg_record_count(self.h, ctypes.byref(rc_), ctypes.byref(nc_)), "pcg_record_count")
         rec = np.zeros(rc_.value, RECORD_DTYPE)
@@ -322,6 +330,10 @@ class Engine:
         # after them; any other current stream waits for them
         if torch.cuda.current_stream(self.device) != self.stream:
             torch.cuda.current_stream(self.device).wait_stream(self.stream)
+        device_ms = 0.0
+        if events is not None:      # (start, end) events around the call
+            events[1].synchronize()     # the call returned after its last device phase; the end event follows it
+            device_ms = events[0].elapsed_time(events[1])
         return SkeletonOut(n, rl, xy, bits, deg[:L].copy(), st.as_dict(), rec, near, device_ms)
 
     # ------------------------------------------------------------------ batched CI tests
