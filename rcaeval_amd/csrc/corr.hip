@@ -501,7 +501,7 @@ __global__ __launch_bounds__(256, 2) void k_xtx_i8(const int8_t *Dg, int CB, int
 // (b >= 56; b = 59 with k = 17 at N = 10^4); the digit path's 45 GEMMs become k.
 // Kernels: k_residues (the k residue planes, the digit path's blocked layout), k_xtx_crt
 // (one 256 x 256 upper tile x one modulus x one split-K slab per 512-thread block, operands
-// staged by LDS-DMA through a 4-stage ring; the residue
+// staged by LDS-DMA through an 8-slot ring of k-blocks, 6 in flight; the residue
 // sums of the slab written mod m as bytes in the MFMA's own lane order), k_crt_finish (slab sums,
 // the CRT rebuild, the upper triangle of G), then k_normalize_tiles as for the other paths.
 // A result is the correctly rounded fp64 of the exact truncated Gram, so every tile split,
@@ -509,22 +509,13 @@ __global__ __launch_bounds__(256, 2) void k_xtx_i8(const int8_t *Dg, int CB, int
 constexpr int CRT_KMAX = 24;               // moduli (M < 2^192)
 constexpr int CRT_L = 6;                   // 32-bit limbs of M
 constexpr int CRT_T = 256;                 // output tile
-#ifndef PCG_CRT_KB
-#define PCG_CRT_KB 4
+constexpr int CRT_KB = 4;                  // a slab's k-blocks are a multiple of this (the plan's split-K rounding)
+#ifndef PCG_CRT_PR
+#define PCG_CRT_PR 8
 #endif
-#ifndef PCG_CRT_NS
-#define PCG_CRT_NS 2
-#endif
-#ifndef PCG_CRT_SCHED
-#define PCG_CRT_SCHED 1         // interleave fragment reads with MFMAs (sched_group_barrier)
-#endif
-#ifndef PCG_CRT_PRIO
-#define PCG_CRT_PRIO 0          // s_setprio 1 around the MFMAs of a stage
-#endif
-constexpr int CRT_KB = PCG_CRT_KB;         // 32-row k-blocks per LDS stage
-constexpr int CRT_NS = PCG_CRT_NS;         // LDS ring stages (CRT_NS x CRT_KB x 16 KB <= 160 KB)
-static_assert(CRT_NS * CRT_KB * 16384 <= 160 * 1024 && CRT_NS >= 2 && CRT_NS <= 5, "CRT LDS ring");
-constexpr int CRT_STAGE = CRT_KB * 16384;  // bytes per stage: CRT_KB x (A, B) x 4 column blocks x 2 KB
+constexpr int CRT_PR = PCG_CRT_PR;         // LDS ring slots of one k-block (16 KB: A and B, 4 column blocks x 2 KB each)
+constexpr int CRT_PL = CRT_PR - 2;         // k-blocks in flight (a slot is restaged >= 2 phases after its last read)
+static_assert(CRT_PR * 16384 <= 160 * 1024 && CRT_PL >= 1, "CRT LDS ring");
 constexpr int CRT_MAXKB = 4095;            // k-blocks per slab: 4095 x 32 x 128^2 < 2^31
 constexpr int CRT_UNIT = CRT_T * CRT_T;    // residue bytes per (tile, modulus, slab)
 static const int kCrtModuli[CRT_KMAX] = {256, 255, 253, 251, 247, 241, 239, 233, 229, 227, 223, 217,
@@ -717,9 +708,9 @@ __global__ __launch_bounds__(256) void k_residues(const double *X, int64_t N, in
 }
 
 // the residue GEMM of one 256 x 256 upper tile, one modulus and one split-K slab. 8 waves as 2 x 4,
-// each 128 x 64 (4 x 2 v_mfma_i32_32x32x32_i8 tiles, 128 accumulators); CRT_KB k-blocks per LDS
-// stage, two stages. Units u = (mi * ks + slab) * ntiles + tile (modulus-major: a modulus group is
-// one contiguous run, launched as soon as its residue planes exist), this launch runs u0 .. u0 + nu - 1
+// each 128 x 64 (4 x 2 v_mfma_i32_32x32x32_i8 tiles, 128 accumulators); one k-block per phase
+// from an 8-slot LDS ring (6 k-blocks in flight). Units u = (mi * ks + slab) * ntiles + tile (modulus-major: a modulus group is
+// one contiguous run), this launch runs u0 .. u0 + nu - 1
 // (a rank's share) and writes unit u0 + l at out + l * CRT_UNIT, in lane order:
 // byte ((w * 4 + a) * 2 + b) * 1024 + lane * 16 + kk = accumulator kk of MFMA tile (a, b) of wave w.
 __global__ __launch_bounds__(512, 1) void k_xtx_crt(const int8_t *R, int TB, int64_t plane, int T, int ntiles, int ks,
@@ -750,69 +741,61 @@ __global__ __launch_bounds__(512, 1) void k_xtx_crt(const int8_t *R, int TB, int
 #pragma unroll
             for (int q = 0; q < 16; ++q) acc[a][b][q] = 0;
 
-    // staging by LDS-DMA (global_load_lds_dwordx4, no VGPR round trip): a stage is CRT_KB k-blocks,
-    // word o = q * 512 + tid of a stage is k-block q >> 1, side q & 1 (A = tile row bi, B = tile
-    // column bj), column block tid >> 7 of the side, 16-byte word tid & 127 of its 2 KB block --
-    // lane-linear per wave, as the DMA writes; the block keeps the planes' k-half-major order. CRT_NS stages in a ring, CRT_NS - 1 in flight across the raw barriers
-    // (counted vmcnt, never a __syncthreads() that would drain them).
+    // staging by LDS-DMA (global_load_lds_dwordx4, no VGPR round trip): a ring slot is one k-block,
+    // A then B, each 4 column blocks x 2 KB; a thread's DMA word is column block tid >> 7, 16-byte
+    // word tid & 127 of its 2 KB block — lane-linear per wave, as the DMA writes, in the planes'
+    // k-half-major order
     const int8_t *Rm = R + (int64_t)mi * plane;
     const int8_t *srcA = Rm + (int64_t)(bi * 4 + (tid >> 7)) * TB * 2048 + (tid & 127) * 16;
     const int8_t *srcB = Rm + (int64_t)(bj * 4 + (tid >> 7)) * TB * 2048 + (tid & 127) * 16;
     const int nkb = tb1 - tb0;
-    const int ns = (nkb + CRT_KB - 1) / CRT_KB;
-    auto issue = [&](int sidx) {
-        if (sidx >= ns) return;
-        unsigned char *dst = smem + (sidx % CRT_NS) * CRT_STAGE + w * 1024;
+    // one phase per k-block p: stage k-block p + PL (2 DMAs per thread: its A and B words) into
+    // ring slot (p + PL) % PR; wait (counted, never 0) until this thread's DMAs of k-block p + 1
+    // landed; barrier (every wave's DMAs of p + 1 visible, every wave past its reads of the slot
+    // being restaged: those were for k-block p + PL - PR <= p - 2, consumed before phase p - 1's
+    // barrier); then p's 8 MFMAs on the fragments read during phase p - 1, interleaved with the
+    // 6 fragment reads of k-block p + 1. The tail re-stages the last k-block (uniform counts).
+    auto stage = [&](int g) {
+        const int64_t tb = tb0 + min(g, nkb - 1);
+        unsigned char *dst = smem + (g % CRT_PR) * 16384 + w * 1024;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(srcA + tb * 2048),
+                                         (__attribute__((address_space(3))) void *)dst, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(srcB + tb * 2048),
+                                         (__attribute__((address_space(3))) void *)(dst + 8192), 16, 0, 0);
+    };
+    const unsigned char *fa0 = smem + (2 * wr * 2048 + hh * 1024 + r * 16);
+    const unsigned char *fb0 = smem + (8192 + wc * 2048 + hh * 1024 + r * 16);
+    v4i af[2][4], bf[2][2];
+    auto frag = [&](int g, int sl) {
+        const int off = (g % CRT_PR) * 16384;
 #pragma unroll
-        for (int q = 0; q < 2 * CRT_KB; ++q) {
-            // a partial last stage re-reads its last k-block (the DMA count per stage stays fixed
-            // for the counted waits; those k-blocks are not multiplied)
-            const int64_t tb = tb0 + min(sidx * CRT_KB + (q >> 1), nkb - 1);
-            __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void *)(((q & 1) ? srcB : srcA) + tb * 2048),
-                (__attribute__((address_space(3))) void *)(dst + q * 8192), 16, 0, 0);
-        }
+        for (int a = 0; a < 4; ++a)
+            af[sl][a] = *reinterpret_cast<const v4i *>(fa0 + off + (a >> 1) * 2048 + (a & 1) * 512);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) bf[sl][b] = *reinterpret_cast<const v4i *>(fb0 + off + b * 512);
     };
 #pragma unroll
-    for (int sidx = 0; sidx < CRT_NS - 1; ++sidx) issue(sidx);
-    const unsigned char *fa = smem + (2 * wr * 2048 + hh * 1024 + r * 16);
-    const unsigned char *fb = smem + (8192 + wc * 2048 + hh * 1024 + r * 16);
-    for (int sidx = 0; sidx < ns; ++sidx) {
-        // stage sidx landed (this thread's DMAs; the later stages stay in flight), then the
-        // barrier: every wave's DMAs of sidx are in LDS and every wave is done reading sidx - 1
-        const int ahead = min(CRT_NS - 2, ns - 1 - sidx);
-        if (ahead >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * 2 * CRT_KB) : "memory");
-        else if (ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * 2 * CRT_KB) : "memory");
-        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * CRT_KB) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        issue(sidx + CRT_NS - 1);               // into the ring slot read in iteration sidx - 1
-        const int off = (sidx % CRT_NS) * CRT_STAGE;
-        v4i af[2][4], bf[2][2];
-        auto frag = [&](int kk, int sl) {
+    for (int g = 0; g < CRT_PL; ++g) stage(g);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (CRT_PL - 1)) : "memory");   // k-block 0 (own DMAs)
+    __builtin_amdgcn_s_barrier();
+    frag(0, 0);
+    for (int p = 0; p < nkb; p += 2) {
+        // two phases per iteration, so the fragment buffers stay compile-time (p even: buffer 0)
 #pragma unroll
-            for (int a = 0; a < 4; ++a)
-                af[sl][a] = *reinterpret_cast<const v4i *>(fa + off + kk * 16384 + (a >> 1) * 2048 + (a & 1) * 512);
-#pragma unroll
-            for (int b = 0; b < 2; ++b)
-                bf[sl][b] = *reinterpret_cast<const v4i *>(fb + off + kk * 16384 + b * 512);
-        };
-        const int cnt = min(CRT_KB, nkb - sidx * CRT_KB);
-        frag(0, 0);
-        if (PCG_CRT_PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int kk = 0; kk < CRT_KB; ++kk) {
-            if (kk < cnt) {
-                const bool nxt = kk + 1 < CRT_KB && kk + 1 < cnt;
-                if (nxt) frag(kk + 1, (kk + 1) & 1);
+        for (int h2 = 0; h2 < 2; ++h2) {
+            const int q = p + h2;
+            if (q < nkb) {
+                stage(q + CRT_PL);
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (CRT_PL - 1)) : "memory");   // k-block q + 1
+                __builtin_amdgcn_s_barrier();
+                const bool nxt = q + 1 < nkb;
+                if (nxt) frag(q + 1, h2 ^ 1);
 #pragma unroll
                 for (int a = 0; a < 4; ++a)
 #pragma unroll
                     for (int b = 0; b < 2; ++b)
-                        acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[kk & 1][a], bf[kk & 1][b], acc[a][b], 0,
-                                                                          0, 0);
-                if (PCG_CRT_SCHED && nxt) {
-                    // interleave the 6 fragment reads of k-block kk + 1 with the 8 MFMAs of kk
+                        acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[h2][a], bf[h2][b], acc[a][b], 0, 0, 0);
+                if (nxt) {
 #pragma unroll
                     for (int u = 0; u < 6; ++u) {
                         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
@@ -822,11 +805,12 @@ __global__ __launch_bounds__(512, 1) void k_xtx_crt(const int8_t *R, int TB, int
                 }
             }
         }
-        if (PCG_CRT_PRIO) __builtin_amdgcn_s_setprio(0);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may land in LDS after the block ends
     // epilogue: the slab's sums mod m as bytes, 16 per lane per MFMA tile (one 16-byte store)
     const int m = tab.m[mi];
-    const double dm = (double)m, dinv = tab.dinv[mi];
+    const float fm = (float)m, finv = tab.finv[mi];
+    const int c16 = (int)((tab.wlo[mi] >> 16) & 0xffu);      // 2^16 mod m
     uint8_t *o = out + lin * CRT_UNIT + (int64_t)w * 8192 + lane * 16;
 #pragma unroll
     for (int a = 0; a < 4; ++a)
@@ -840,8 +824,12 @@ __global__ __launch_bounds__(512, 1) void k_xtx_crt(const int8_t *R, int TB, int
                 if (m == 256) {
                     rr = (uint32_t)v & 255u;
                 } else {
-                    const double d = (double)v;
-                    int x = (int)fma(floor(d * dinv), -dm, d);
+                    // |v| < 2^31: t = (v >> 16)(2^16 mod m) + (v & 0xffff) = v (mod m) with |t| < 2^24
+                    // (24-bit multiply), so t and t - q m are exact in fp32; q = rint(t fl(1/m)) is off
+                    // the exact quotient by < 2^-7, so t - q m lies in (-m/2 - 1, m/2 + 1)
+                    const int t = __mul24(v >> 16, c16) + (v & 0xffff);
+                    const float tf = (float)t;
+                    int x = (int)fmaf(-rintf(tf * finv), fm, tf);
                     x += x < 0 ? m : 0;
                     x -= x >= m ? m : 0;
                     rr = (uint32_t)x;
@@ -1145,7 +1133,7 @@ int crt_residues(pcg_handle *h, const CrtPlan &p, const double *X, int64_t N, in
 void crt_gemm(pcg_handle *h, const CrtPlan &p, const int8_t *R, int64_t u0, int64_t nu, uint8_t *out) {
     if (nu <= 0) return;
     const int64_t plane = (int64_t)p.CBp * p.TB * 2048;
-    hipLaunchKernelGGL(k_xtx_crt, dim3((unsigned)((nu + 7) / 8 * 8)), dim3(512), CRT_NS * CRT_STAGE, h->stream, R,
+    hipLaunchKernelGGL(k_xtx_crt, dim3((unsigned)((nu + 7) / 8 * 8)), dim3(512), CRT_PR * 16384, h->stream, R,
                        p.TB, plane, p.T, p.ntiles, p.ks, p.kb, p.tab, u0, nu, out);
 }
 
