@@ -2242,6 +2242,9 @@ constexpr double F32_U = 5.9604644775390625e-08;   // 2^-24
 #ifndef PCG_TGF_SGPR
 #define PCG_TGF_SGPR 0x10 // k_level_lds_f depths (bit 1 << d) whose per-y bookkeeping is in wave lane masks
 #endif
+#ifndef PCG_NBLK_T
+#define PCG_NBLK_T 1         // compact node blocks built transposed (k_node_blocks_t) when C's row fits in LDS
+#endif
 #ifndef PCG_TGF_Y3FAST
 #define PCG_TGF_Y3FAST 1     // per-lane y loop (YM 3): skip the dependence-bit packing when no lane needs it
 #endif
@@ -3096,6 +3099,66 @@ __global__ __launch_bounds__(256) void k_node_blocks(LevelArgs a, int64_t s_lo, 
             const unsigned long long m = __ballot(bit);
             if (lane == 0) a.lmk[a.off[x] + r] = m;
         }
+    }
+}
+
+// the same compact blocks, built transposed: one block per SOURCE row y stages C[y, :] and y's
+// adjacency row in LDS (coalesced reads, C read once per depth), then writes row iy of the block
+// of every node x whose block holds y (x in adj(y), and x = y itself for the block's last row):
+// cb_x[iy][k] = C[y][ids_x[k]] from LDS, and (iy < D_x) x's local mask of y. A wave per target
+// node; its rows are contiguous writes. k_node_blocks gathers the same entries from C's
+// scattered columns — FETCH ~13x the block bytes at config 5's depth 4.
+__global__ __launch_bounds__(256) void k_node_blocks_t(LevelArgs a, int64_t s_lo, int64_t s_hi, int maxdeg) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    double *row = reinterpret_cast<double *>(smem);
+    uint64_t *arow = reinterpret_cast<uint64_t *>(row + a.n);
+    int64_t *tbo = reinterpret_cast<int64_t *>(arow + a.W);   // per target: block offset,
+    int *tx = reinterpret_cast<int *>(tbo + maxdeg + 1);       // node (-1: no block), degree, CSR offset
+    int *tD = tx + maxdeg + 1, *toff = tD + maxdeg + 1;
+    const int y = blockIdx.x;
+    const int Dy = a.deg[y];
+    const int32_t *ny = a.nbr + a.off[y];
+    // the targets' descriptors in one round of loads (t = Dy: y's own block)
+    bool any = false;
+    for (int t = threadIdx.x; t <= Dy; t += blockDim.x) {
+        const int x = t < Dy ? ny[t] : y;
+        const bool hb = !(a.cpre[x + 1] <= s_lo || a.cpre[x] >= s_hi || a.cpre[x + 1] == a.cpre[x]);
+        tx[t] = hb ? x : -1;
+        tD[t] = a.deg[x];
+        toff[t] = a.off[x];
+        tbo[t] = hb ? a.bo[x] : 0;
+        any = any || hb;
+    }
+    if (!__syncthreads_or(any)) return;
+    const double *cy = a.C + (int64_t)y * a.ldc;
+    for (int k = threadIdx.x; k < a.n; k += blockDim.x) row[k] = cy[k];
+    const uint64_t *ay = a.adj + (int64_t)y * a.W;
+    for (int k = threadIdx.x; k < a.W; k += blockDim.x) arow[k] = ay[k];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    // a target's list is one coalesced load (D <= 64: a lane per entry), issued one target ahead;
+    // y's position in it is the count of smaller entries (a ballot, no dependent search)
+    auto load = [&](int t) {
+        const int x = tx[t], D = tD[t];
+        return (x >= 0 && lane < D) ? a.nbr[toff[t] + lane] : x;
+    };
+    int g = wv <= Dy ? load(wv) : 0;
+    for (int t = wv; t <= Dy; t += nwv) {
+        const int gn = t + nwv <= Dy ? load(t + nwv) : 0;
+        const int x = tx[t];
+        if (x >= 0) {
+            const int D = tD[t], L = D + 1;
+            const int iy = x == y ? D : __popcll(__ballot(lane < D && g < y));
+            double *cb = a.cblk + tbo[t] + (int64_t)iy * L;
+            if (lane < L) cb[lane] = row[g];                 // lane D: column x (g = x there)
+            if (L > 64 && lane == 0) cb[64] = row[x];        // D = 64: the block's last column
+            if (iy < D) {
+                const bool bit = lane < D && ((arow[g >> 6] >> (g & 63)) & 1ull);
+                const unsigned long long m = __ballot(bit);
+                if (lane == 0) a.lmk[toff[t] + iy] = m;
+            }
+        }
+        g = gn;
     }
 }
 
@@ -5041,8 +5104,16 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                                 else hipLaunchKernelGGL((k_level_wave<32, MODE_FULLP>), grid, block, ldsw, h->stream, as);
                             }
                         } else if (h->tgroup && use_screen32(h, d)) {
-                            if (h->nblk)   // compact node blocks: the sweep stages them instead of gathering C
-                                hipLaunchKernelGGL(k_node_blocks, dim3((unsigned)h->n), dim3(256), 0, h->stream, as, s_lo, s_hi);
+                            if (h->nblk) {   // compact node blocks: the sweep stages them instead of gathering C
+                                // built transposed (C's rows staged in LDS) when a row fits
+                                const size_t tl = sizeof(double) * (size_t)h->n + sizeof(uint64_t) * (size_t)h->W +
+                                                  (size_t)(h->maxdeg + 1) * (sizeof(int64_t) + 3 * sizeof(int));
+                                if (PCG_NBLK_T && tl <= 64 * 1024)
+                                    hipLaunchKernelGGL(k_node_blocks_t, dim3((unsigned)h->n), dim3(256), tl, h->stream, as, s_lo, s_hi,
+                                                       (int)h->maxdeg);
+                                else
+                                    hipLaunchKernelGGL(k_node_blocks, dim3((unsigned)h->n), dim3(256), 0, h->stream, as, s_lo, s_hi);
+                            }
                             as.lds_btab_off = (int)lds_f32_core(dl, 8);
                             const size_t ldsf = lds_tgroup_f_bytes(dl, d, 8);
                             const dim3 grid((unsigned)(s_hi - s_lo)), block(256);
