@@ -573,7 +573,7 @@ def main():
             "tests_per_level": st["tests"], "calls_per_level": st["calls"],
             "kernel_ms_per_level": [round(v, 3) for v in st["kernel_ms"]],
             "level_ms": [round(v, 3) for v in st["level_ms"]],
-            "edges_after": st["edges_after"], "exact_path": st["exact"], "screened": st["screened"], "near_alpha": st["near_alpha"],
+            "edges_after": st["edges_after"], "exact_path": st["exact"], "screened": st["screened"], "near_alpha": st["near_alpha"], "indep_per_level": st["indep"],
             "roofline": roof,
             "sampled_records": full_p,
         }

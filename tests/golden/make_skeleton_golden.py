@@ -1,5 +1,11 @@
 """Golden vectors for the PC skeleton loop and for FCI, produced by EXECUTING the reference's own
-vendored causal-learn code (run in the build container, where /root/reference exists):
+vendored causal-learn code.
+
+MANUAL, SANDBOXED STEP. This script loads and runs Python files from /root/reference (untrusted
+public content) as modules, so it is kept out of every automated path: no test, build, smoke or
+bench imports or runs it (the tests import the case definitions from ``skeleton_cases.py``), and
+the committed ``skeleton_ref.json`` is the only artefact they read. A maintainer regenerates the
+goldens by hand, in a throwaway container with no credentials and no network:
 
   python tests/golden/make_skeleton_golden.py
 
@@ -52,61 +58,7 @@ PY39 = "/opt/conda/bin/python3.9"
 OUT = os.path.join(HERE, "skeleton_ref.json")
 sys.path.insert(0, ROOT)
 
-# name: (n, N, seed, w_low, w_high, edge_prob, options)
-#   stable      SkeletonDiscovery(stable=...)
-#   const       column index set to a constant (NaN correlations, never separated)
-#   dup         (a, b): column b := column a (exactly singular sub-matrices -> ValueError)
-#   forbid      [(i, j), ...] background knowledge: i -> j forbidden (pairs listed both ways are
-#               banned edges, SkeletonDiscovery.py:88-106)
-PC_CASES = {
-    "p12": (12, 500, 1, .3, .9, .3, {}),
-    "p20": (20, 800, 2, .2, .8, .2, {}),
-    "p30": (30, 600, 3, .3, .9, .15, {}),
-    "p25": (25, 300, 9, .1, .5, .3, {}),
-    "p18": (18, 250, 11, .4, .9, .35, {}),
-    "p15deep": (15, 3000, 4, .5, 1.0, .45, {}),
-    "p32multi": (32, 400, 3, .1, .3, .3, {}),
-    "u20": (20, 800, 2, .2, .8, .2, {"stable": False}),
-    "u30": (30, 600, 3, .3, .9, .15, {"stable": False}),
-    "u18": (18, 250, 11, .4, .9, .35, {"stable": False}),
-    "const11": (11, 400, 31, .3, .9, .3, {"const": 4}),
-    "bk20": (20, 800, 2, .2, .8, .2, {"forbid": [(0, 1), (1, 0), (3, 7), (7, 3), (5, 6), (2, 9), (9, 2)]}),
-    "dup12": (12, 500, 1, .3, .9, .3, {"dup": (2, 7)}),
-}
-# name: (n, N, seed, w_low, w_high, edge_prob, depth)
-FCI_CASES = {
-    "f12": (12, 500, 1, .3, .9, .3, -1),
-    "f20": (20, 800, 2, .2, .8, .2, -1),
-    "f30": (30, 600, 3, .3, .9, .15, -1),
-    "f25": (25, 300, 9, .1, .5, .3, -1),
-    "f18": (18, 250, 11, .4, .9, .35, -1),
-    "f20d1": (20, 800, 2, .2, .8, .2, 1),
-    "f20d2": (20, 800, 2, .2, .8, .2, 2),
-}
-
-
-def pc_input(name):
-    """The seeded N x n input of one PC case (tests rebuild it the same way)."""
-    from rcaeval_amd import synth
-    n, N, seed, wl, wh, ep, opt = PC_CASES[name]
-    X = synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
-    if "const" in opt:
-        X[:, opt["const"]] = 1.0
-    if "dup" in opt:
-        a, b = opt["dup"]
-        X[:, b] = X[:, a]
-    return np.ascontiguousarray(X)
-
-
-def fci_input(name):
-    from rcaeval_amd import synth
-    n, N, seed, wl, wh, ep, _ = FCI_CASES[name]
-    return synth.gaussian_sem(n, N, seed=seed, w_low=wl, w_high=wh, edge_prob=ep)
-
-
-def digest(a) -> str:
-    a = np.ascontiguousarray(np.asarray(a, dtype=np.float64))
-    return hashlib.sha256(a.tobytes() + str(a.shape).encode()).hexdigest()
+from tests.golden.skeleton_cases import FCI_CASES, PC_CASES, digest, fci_input, pc_input  # noqa: E402,F401
 
 
 def stage_a(tmp):

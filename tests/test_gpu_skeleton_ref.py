@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 
 from oracle import fisherz
-from tests.golden import make_skeleton_golden as mk
+from tests.golden import skeleton_cases as mk
 
 pytestmark = pytest.mark.gpu
 

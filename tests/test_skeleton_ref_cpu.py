@@ -21,7 +21,7 @@ from oracle import fci as ofci
 from oracle import fisherz
 from oracle import orient as oor
 from oracle import skeleton as osk
-from tests.golden import make_skeleton_golden as mk
+from tests.golden import skeleton_cases as mk
 
 GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "skeleton_ref.json")))
 PC = GOLD["pc"]
