@@ -894,8 +894,11 @@ __global__ __launch_bounds__(256) void k_level(LevelArgs a) {
 // for (x, y | z): v = C_yz / sqrt(C_zz), c_xy = C_xy - u_z v, c_yy = C_yy - v^2.
 // A chunk is (x, a contiguous share of the D(D-1)/2 pairs, row-major over y < z).
 constexpr int L1_MAXD = 1024;
-constexpr int L1_PB = 4;              // pairs in flight per lane (independent gathers)
+constexpr int L1_PB = 4;              // pairs in flight per lane (independent gathers; 8 and 16 measured slower)
 size_t l1_lds_bytes(int D) { return (size_t)D * (4 + 5 * 8) + 16; }
+// I32: every index of C, adj and rm fits 31 bits (n * ldc < 2^31): 32-bit offsets instead of
+// 64-bit multiplies in the hot loop (the pair arithmetic is 32-bit always: D <= L1_MAXD)
+template <bool I32>
 __global__ __launch_bounds__(256) void k_level1_pairs(LevelArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x;
@@ -927,22 +930,23 @@ __global__ __launch_bounds__(256) void k_level1_pairs(LevelArgs a) {
         s_cxx[k] = ((s > 0.0) && (cxx == cxx)) ? cxx : __builtin_nan("");   // NaN marks !chol_ok
     }
     __syncthreads();
-    const int64_t npairs = (int64_t)D * (D - 1) / 2;
-    const int64_t nch = a.cpre[x + 1] - a.cpre[x];
-    const int64_t c = chunk - a.cpre[x];
-    const int64_t p0 = npairs * c / nch, p1 = npairs * (c + 1) / nch;
-    unsigned long long tests = 0, indep = 0;
+    const int npairs = D * (D - 1) / 2;                    // < 2^19 (D <= L1_MAXD)
+    const int nch = (int)(a.cpre[x + 1] - a.cpre[x]);
+    const int c = (int)(chunk - a.cpre[x]);
+    const int p0 = (int)((int64_t)npairs * c / nch), p1 = (int)((int64_t)npairs * (c + 1) / nch);
+    unsigned tests = 0, indep = 0;
     const float twoD1 = 2.0f * D - 1.0f;
-    auto rowstart = [&](int r) -> int64_t { return (int64_t)r * (2 * D - 1 - r) / 2; };
+    auto rowstart = [&](int r) -> int { return r * (2 * D - 1 - r) / 2; };
+    const int ldc = (int)a.ldc;
 
-    for (int64_t pb = p0 + tid; pb < p1; pb += (int64_t)L1_PB * blockDim.x) {
+    for (int pb = p0 + tid; pb < p1; pb += L1_PB * (int)blockDim.x) {
         // L1_PB pairs per lane: indices first, then every gather, then the tests
         int ys[L1_PB], zs[L1_PB];
         double cyz[L1_PB];
         uint64_t aw[L1_PB];
 #pragma unroll
         for (int q = 0; q < L1_PB; ++q) {
-            const int64_t p = pb + (int64_t)q * blockDim.x;
+            const int p = pb + q * (int)blockDim.x;
             int y = 0, z = 1;
             if (p < p1) {
                 // pair p -> (y, z), y < z: row y starts at y(2D - 1 - y)/2 (fp32 root, then exact fix-up)
@@ -950,7 +954,7 @@ __global__ __launch_bounds__(256) void k_level1_pairs(LevelArgs a) {
                 if (y < 0) y = 0;
                 while (y > 0 && rowstart(y) > p) --y;
                 while (rowstart(y + 1) <= p) ++y;
-                z = y + 1 + (int)(p - rowstart(y));
+                z = y + 1 + (p - rowstart(y));
             }
             ys[q] = y;
             zs[q] = z;
@@ -958,12 +962,17 @@ __global__ __launch_bounds__(256) void k_level1_pairs(LevelArgs a) {
 #pragma unroll
         for (int q = 0; q < L1_PB; ++q) {
             const int yg = s_nx[ys[q]], zg = s_nx[zs[q]];
-            cyz[q] = a.C[(int64_t)yg * a.ldc + zg];
-            aw[q] = a.adj[(int64_t)yg * W + (zg >> 6)];
+            if constexpr (I32) {
+                cyz[q] = a.C[(uint32_t)(yg * ldc + zg)];
+                aw[q] = a.adj[(uint32_t)(yg * W + (zg >> 6))];
+            } else {
+                cyz[q] = a.C[(int64_t)yg * a.ldc + zg];
+                aw[q] = a.adj[(int64_t)yg * W + (zg >> 6)];
+            }
         }
 #pragma unroll
         for (int q = 0; q < L1_PB; ++q) {
-            if (pb + (int64_t)q * blockDim.x >= p1) continue;
+            if (pb + q * (int)blockDim.x >= p1) continue;
             const int y = ys[q], z = zs[q];
             const int yg = s_nx[y], zg = s_nx[z];
             const bool adj_yz = (aw[q] >> (zg & 63)) & 1ull;
@@ -5182,8 +5191,15 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                         if (lds > LDS_MAX)
                             return pcg_fail(h, PCG_ERR_INVALID, "max degree %d too large for LDS staging", h->maxdeg);
                         if (mode == MODE_DECIDE && d == 1 && h->maxdeg <= L1_MAXD)
-                            hipLaunchKernelGGL(k_level1_pairs, dim3((unsigned)(l_hi - l_lo)), dim3(256),
-                                               l1_lds_bytes(h->maxdeg), h->stream, al);
+                        {
+                            const bool i32 = (int64_t)h->n * std::max<int64_t>(h->ldc, h->n) < ((int64_t)1 << 31);
+                            if (i32)
+                                hipLaunchKernelGGL(k_level1_pairs<true>, dim3((unsigned)(l_hi - l_lo)), dim3(256),
+                                                   l1_lds_bytes(h->maxdeg), h->stream, al);
+                            else
+                                hipLaunchKernelGGL(k_level1_pairs<false>, dim3((unsigned)(l_hi - l_lo)), dim3(256),
+                                                   l1_lds_bytes(h->maxdeg), h->stream, al);
+                        }
                         else if (mode == MODE_DECIDE) launch_level_mode<MODE_DECIDE>(h, al, l_hi - l_lo, lds);
                         else if (mode == MODE_FULLP) launch_level_mode<MODE_FULLP>(h, al, l_hi - l_lo, lds);
                         else launch_level_mode<MODE_EXACT>(h, al, l_hi - l_lo, lds);
