@@ -2393,30 +2393,25 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
     }
     __syncthreads();
     if (!WIDE && a.cblk) {   // this depth's compact node block (k_node_blocks): coalesced rows
-        // a wave loads SR rows (and their masks) before storing any: SR loads in flight per lane,
-        // not one dependent round trip per row
-        constexpr int SR = 8;
+        // a wave loads SR rows before storing any (SR loads in flight per lane, not one dependent
+        // round trip per row; SR = 8 spilled 4 more VGPRs in the sweep); the masks a lane each
+        constexpr int SR = 4;
         const double *cb = a.cblk + a.bo[x];
         const uint64_t *lk = a.lmk + a.off[x];
         const int L = D + 1;
         const int lane = tid & 63, wv = tid >> 6, nwv = bs >> 6;
         for (int t0 = wv * SR; t0 < D; t0 += nwv * SR) {
             double v[SR];
-            uint64_t mk[SR];
 #pragma unroll
-            for (int r = 0; r < SR; ++r) {
-                const int t = min(t0 + r, D - 1);
-                v[r] = lane < D ? cb[t * L + lane] : 0.0;
-                mk[r] = lk[t];
-            }
+            for (int r = 0; r < SR; ++r) v[r] = lane < D ? cb[min(t0 + r, D - 1) * L + lane] : 0.0;
 #pragma unroll
             for (int r = 0; r < SR; ++r) {
                 const int t = t0 + r;
                 if (t >= D) break;                   // wave-uniform
-                if (lane < DS) M[t * DS + lane] = lane < D ? (float)v[r] : 0.0f;
-                if (lane == 0) lmask[t] = (Mask)mk[r];
+                if (lane < DS) M[t * DS + lane] = (float)v[r];
             }
         }
+        for (int t = tid; t < D; t += bs) lmask[t] = (Mask)lk[t];
     } else if constexpr (WIDE) {   // (the row-batched form below measured slower for the 128-wide blocks)
         for (int e = tid; e < D * DS; e += bs) {
             const int t = e / DS, k = e - t * DS;
