@@ -154,7 +154,7 @@ extern "C" int pcg_destroy(pcg_handle *h) {
                       &h->k1_digits, &h->small_sum};
     for (DevBuf *b : bufs)
         if (b->p) hipFree(b->p);
-    PinBuf *pins[] = {&h->ctr_pin, &h->deg_pin, &h->off_pin, &h->cpre_pin, &h->status_pin, &h->small_pin};
+    PinBuf *pins[] = {&h->ctr_pin, &h->deg_pin, &h->off_pin, &h->cpre_pin, &h->status_pin, &h->small_pin, &h->near_pin};
     for (PinBuf *b : pins)
         if (b->p) hipHostFree(b->p);
     if (h->summary) hipHostFree(h->summary);

@@ -130,6 +130,9 @@ struct pcg_handle {
     hipEvent_t rev[PCG_MAX_LEVELS][2] = {};   // per-depth CI-test kernel brackets
     int64_t near_seen = 0;           // near-alpha entries copied so far (the device list accumulates)
     int64_t near_total_dev = 0;      // the device's cumulative near-alpha count at the last level end
+    int64_t near_pending = 0;        // the device list's length (capped) at the last level end
+    bool defer_near = false;         // skeleton_once: near-alpha records copied once after the last depth
+    PinBuf near_pin;                 // their host staging
     size_t summary_slot = 0;         // bytes per slot of the two-slot host-mapped summary ring
     int screen_eff = 0;              // the current depth's effective mask (set by pcg_level_begin)
     int screen_mask = -1;            // depths (bit 1 << d) with the fp32-screened T-group sweep (k_level_lds_f); -1 = default

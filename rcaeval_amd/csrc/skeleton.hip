@@ -623,14 +623,25 @@ __global__ __launch_bounds__(256) void k_level0(LevelArgs a) {
     unsigned long long tests = 0, indep = 0;
     const int y = y0 + tx;
     const double cyy = y < a.n ? a.diag[y] : 0.0;
-#pragma unroll 4
-    for (int r = ty; r < 64; r += 4) {
+    // the thread's 16 entries (and their rows' diagonals) are all loaded before the first test:
+    // one memory latency per thread, not four
+    double cv[16], dv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int x = x0 + ty + 4 * i;
+        const bool in = x < a.n && y < a.n && y > x;
+        cv[i] = in ? a.C[(int64_t)x * a.ldc + y] : 0.0;
+        dv[i] = in ? a.diag[x] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int r = ty + 4 * i;
         const int x = x0 + r;
         uint8_t f = 0;
         if (x < a.n && y < a.n && y > x) {
-            const double cxy = a.C[(int64_t)x * a.ldc + y];
+            const double cxy = cv[i];
             double p = 0.0;
-            const int dec = decide<MODE>(a, cxy, a.diag[x], cyy, a.tau, &p);
+            const int dec = decide<MODE>(a, cxy, dv[i], cyy, a.tau, &p);
             ++tests;
             if (dec == 2) {
                 push_deferred(a, x, y, S0, 0);
@@ -5348,7 +5359,8 @@ int level_end_finish(pcg_handle *h, int d, unsigned long long seq, pcg_stats *st
     // the device's near-alpha list accumulates over the run: this depth's entries follow the
     // ones already copied
     const int64_t near_cum = std::min<int64_t>((int64_t)c.near_alpha, h->near_cap);
-    if (near_cum > h->near_seen) {
+    h->near_pending = near_cum;
+    if (!h->defer_near && near_cum > h->near_seen) {
         const size_t old = h->near_h.size();
         h->near_h.resize(old + (near_cum - h->near_seen));
         PCG_HIP(h, hipMemcpy(h->near_h.data() + old, (pcg_record *)h->nearbuf.p + h->near_seen,
@@ -5356,7 +5368,7 @@ int level_end_finish(pcg_handle *h, int d, unsigned long long seq, pcg_stats *st
     }
     const int64_t near_d = (int64_t)c.near_alpha - h->near_total_dev;
     h->near_total_dev = (int64_t)c.near_alpha;
-    h->near_seen = std::max(h->near_seen, near_cum);
+    if (!h->defer_near) h->near_seen = std::max(h->near_seen, near_cum);
     h->st.tests[d] = (int64_t)c.tests;
     h->st.indep[d] = (int64_t)c.indep;
     h->st.exact[d] = (int64_t)c.exact;
@@ -5427,8 +5439,12 @@ static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc,
     // and after each depth's barrier launches (lev[d], lev[d + 1]), read after the last depth
     h->lev_on = true;
     h->lev_n = 0;
+    // the near-alpha records are copied once, after the last depth, on the handle's stream
+    // (a synchronous copy per depth that has some sat on the level loop's critical path)
+    h->defer_near = true;
+    h->near_pending = 0;
     int rc = pcg_skeleton_init(h, C, n, ldc, N, alpha, flags, removed_level);
-    if (rc) { h->lev_on = false; return rc; }
+    if (rc) { h->lev_on = false; h->defer_near = false; return rc; }
     PCG_HT(h, "init:done");
     int done = 0;
     for (int depth = 0;; ++depth) {
@@ -5442,12 +5458,26 @@ static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc,
         unsigned long long seq = 0;
         if (!rc) rc = level_end_enqueue(h, &seq);
         if (!rc) rc = level_end_finish(h, depth, seq, nullptr);
-        if (rc) { h->lev_on = false; return rc; }
+        if (rc) { h->lev_on = false; h->defer_near = false; return rc; }
         done = depth + 1;
     }
     h->lev_on = false;
+    h->defer_near = false;
+    const int64_t nnew = h->near_pending - h->near_seen;
+    if (nnew > 0) {
+        if (!pcg_ensure_pinned(h, h->near_pin, sizeof(pcg_record) * (size_t)nnew))
+            return pcg_fail(h, PCG_ERR_OOM, "pinned near-alpha records");
+        PCG_HIP(h, hipMemcpyAsync(h->near_pin.p, (pcg_record *)h->nearbuf.p + h->near_seen,
+                                  sizeof(pcg_record) * (size_t)nnew, hipMemcpyDeviceToHost, h->stream));
+    }
     rc = export_sync(h);                 // the last depth's export (the skeleton's sepset rows)
     if (rc) return rc;
+    if (nnew > 0) {
+        PCG_HIP(h, hipStreamSynchronize(h->stream));
+        const pcg_record *src = (const pcg_record *)h->near_pin.p;
+        h->near_h.insert(h->near_h.end(), src, src + nnew);
+        h->near_seen = h->near_pending;
+    }
     if (done && h->lev_n > done) {
         PCG_HIP(h, hipEventSynchronize(h->lev[done]));
         for (int depth = 0; depth < done; ++depth) {
