@@ -74,8 +74,9 @@ typedef struct {
     int64_t near_alpha[PCG_MAX_LEVELS];/* tests with |p - alpha| < 1e-9 (enumerated)        */
     int64_t edges_after[PCG_MAX_LEVELS];/* undirected edges left after each depth           */
     int32_t max_degree[PCG_MAX_LEVELS];/* max degree at the start of each depth            */
-    double level_ms[PCG_MAX_LEVELS];   /* device wall time per depth (HIP events)           */
-    double kernel_ms[PCG_MAX_LEVELS];  /* time of the CI-test kernel alone per depth        */
+    double level_ms[PCG_MAX_LEVELS];   /* device wall time per depth (pcg_skeleton: device  */
+                                       /* clock stamps; level-step API: HIP events)         */
+    double kernel_ms[PCG_MAX_LEVELS];  /* time of the CI-test kernels alone per depth       */
     int32_t levels;                    /* depths run                                        */
     int32_t error;                     /* 0 or PCG_ERR_SINGULAR / PCG_ERR_DOMAIN            */
     int64_t screened[PCG_MAX_LEVELS];  /* tests the fp32 sweep left to its fp64 screen      */

@@ -166,6 +166,7 @@ extern "C" int pcg_destroy(pcg_handle *h) {
         for (auto &e : pr)
             if (e) hipEventDestroy(e);
     if (h->ev_join) hipEventDestroy(h->ev_join);
+    if (h->ev_fork) hipEventDestroy(h->ev_fork);
     if (h->aux) hipStreamDestroy(h->aux);
     if (h->xs) hipStreamDestroy(h->xs);
     if (h->ev_xready) hipEventDestroy(h->ev_xready);

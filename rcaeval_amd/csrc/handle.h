@@ -33,6 +33,9 @@ struct DevCounters {
     unsigned long long exported;   // sepset rows exported this level
     unsigned long long error;      // PCG_ERR_* bits (1 singular, 2 domain)
     unsigned long long screened;   // tests the fp32 sweep handed to the fp64 screen list (may exceed capacity)
+    // skeleton_once's kernel bracket in device wall-clock ticks: after the chunk-prefix copy, at the
+    // start of the first kernel behind the CI-test classes (0: not stamped)
+    unsigned long long t_run0, t_run1;
 };
 
 // host-mapped per-level summary (k_level_summary); n int32 degrees follow the struct
@@ -40,6 +43,7 @@ struct LevelSummary {
     DevCounters ctr;
     uint8_t status[8];
     int32_t ug_clean;              // k_summary_fill cleared every union row of the new graph
+    unsigned long long stamp;      // device wall-clock ticks when the summary was written
     unsigned long long seq;        // written last, after a system-scope fence
 };
 
@@ -133,6 +137,12 @@ struct pcg_handle {
     int64_t near_pending = 0;        // the device list's length (capped) at the last level end
     bool defer_near = false;         // skeleton_once: near-alpha records copied once after the last depth
     PinBuf near_pin;                 // their host staging
+    int run_max_depth = -1;
+    // skeleton_once's depth boundaries (the summaries' wall-clock stamps; PCG_KBRACKET = 0)
+    std::vector<unsigned long long> lev_stamp;
+    bool stamps = false;
+    int wall_khz = 0;
+    hipEvent_t ev_fork = nullptr;    // the class fork point when the kernel brackets are stamped          // skeleton_once's max_depth (-1: unbounded, or the level-step API)
     size_t summary_slot = 0;         // bytes per slot of the two-slot host-mapped summary ring
     int screen_eff = 0;              // the current depth's effective mask (set by pcg_level_begin)
     int screen_mask = -1;            // depths (bit 1 << d) with the fp32-screened T-group sweep (k_level_lds_f); -1 = default

@@ -124,7 +124,13 @@ struct LevelArgs {
     const int64_t *bo;           // n + 1 offsets of the compact blocks (doubles)
     double *cblk;                // per node: C[adj(x) + x, adj(x) + x], stride D + 1, x last
     uint64_t *lmk;               // per node: local adjacency masks of adj(x), at off[x]
+    int stamp_end;               // block 0 stamps ctr->t_run1 at entry (the kernel bracket's end)
 };
+
+// the kernel bracket's end (skeleton_once with PCG_KBRACKET = 0): one store by one thread
+__device__ __forceinline__ void stamp_run_end(const LevelArgs &a) {
+    if (a.stamp_end && blockIdx.x == 0 && threadIdx.x == 0) a.ctr->t_run1 = wall_clock64();
+}
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -541,6 +547,7 @@ __device__ __forceinline__ void summary_block(const int32_t *deg, int n, int32_t
         out->ug_clean = ug != nullptr && nfill > 0 && (int64_t)part[255] <= ug_rows;
         if (status)
             for (int k = 0; k < PCG_RM_STATUS; ++k) status[k] = 0;
+        out->stamp = wall_clock64();
     }
     __threadfence_system();
     __syncthreads();
@@ -2262,6 +2269,13 @@ constexpr double F32_U = 5.9604644775390625e-08;   // 2^-24
 #ifndef PCG_TGF_SGPR
 #define PCG_TGF_SGPR 0x10 // k_level_lds_f depths (bit 1 << d) whose per-y bookkeeping is in wave lane masks
 #endif
+#ifndef PCG_KBRACKET
+#define PCG_KBRACKET 0       // skeleton_once's depth / kernel brackets: 1 timing events (each one a ~6 us marker
+                             // on the device's critical path), 0 device wall-clock stamps in kernels already queued
+#endif
+#ifndef PCG_LAST_XINL
+#define PCG_LAST_XINL 1      // the last depth of a max_depth-bounded run exports on the handle's stream
+#endif
 #ifndef PCG_NBLK_T
 #define PCG_NBLK_T 1         // compact node blocks built transposed (k_node_blocks_t) when C's row fits in LDS
 #endif
@@ -3099,6 +3113,7 @@ __device__ __forceinline__ void screen_lanes(const LevelArgs &a, int blk, int nb
 
 template <int DM>
 __global__ __launch_bounds__(256) void k_screen(LevelArgs a) {
+    stamp_run_end(a);
     screen_lanes<DM>(a, blockIdx.x, gridDim.x);
 }
 
@@ -3617,6 +3632,7 @@ __device__ __forceinline__ void exact_lanes(const LevelArgs &a, int64_t count, i
 // every test of those pairs on the list): the overflow check of k_exact, wave-summed counters
 template <int M>
 __global__ __launch_bounds__(256) void k_exact_lanes(LevelArgs a) {
+    stamp_run_end(a);
     const unsigned long long pushed = *(volatile const unsigned long long *)&a.ctr->deferred;
     const int64_t count = (int64_t)min((unsigned long long)a.def_cap, pushed);
     if (blockIdx.x == 0 && threadIdx.x == 0 &&
@@ -3685,6 +3701,7 @@ __device__ __forceinline__ void exact_waves(const LevelArgs &a, unsigned char *s
 
 __global__ __launch_bounds__(256) void k_exact(LevelArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    stamp_run_end(a);
     exact_waves(a, smem, blockIdx.x, gridDim.x);
 }
 
@@ -4623,7 +4640,7 @@ int graph_launch(pcg_handle *h) {
                        reinterpret_cast<int32_t *>(ds + 1), seq, nfill);
     h->cb = t;
     PCG_HIP(h, hipGetLastError());
-    if (h->lev_on && h->lev_n < 2 * PCG_MAX_LEVELS) {   // depth boundary (skeleton_once), off the host's critical path
+    if (h->lev_on && !h->stamps && h->lev_n < 2 * PCG_MAX_LEVELS) {   // depth boundary (skeleton_once), off the host's critical path
         hipEvent_t &e = h->lev[h->lev_n++];
         if (!e) PCG_HIP(h, hipEventCreate(&e));
         PCG_HIP(h, hipEventRecord(e, h->stream));
@@ -4633,9 +4650,10 @@ int graph_launch(pcg_handle *h) {
 
 // chunk prefix (host-mapped, written by the decomposition) -> device, by a kernel on the
 // handle's stream (no DMA-engine round trip in the level's launch burst)
-__global__ void k_copy_i64(const int64_t *src, int64_t count, int64_t *dst) {
+__global__ void k_copy_i64(const int64_t *src, int64_t count, int64_t *dst, DevCounters *stamp) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < count) dst[i] = src[i];
+    if (stamp && i == 0) stamp->t_run0 = wall_clock64();   // the kernel bracket's start (h->stamps)
 }
 
 // spin until the summary with sequence number `want` is visible (a stream error or a stream that
@@ -4920,7 +4938,8 @@ int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks) {
     {
         const void *src = h->cpre_pin.dp;
         hipLaunchKernelGGL(k_copy_i64, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, h->stream,
-                           (const int64_t *)src, cnt, (int64_t *)h->cpre.p);
+                           (const int64_t *)src, cnt, (int64_t *)h->cpre.p,
+                           h->stamps ? (DevCounters *)h->ctr.p : nullptr);
         PCG_HIP(h, hipGetLastError());
     }
     PCG_HT(h, "begin:prefix-copy-launched");
@@ -5074,9 +5093,12 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
         a.chunk_lo = chunk_lo;
         const int64_t nch = chunk_hi - chunk_lo;
         hipEvent_t *rv = h->rev[d];
+        // kernel bracket: timing events, or (skeleton_once) the prefix copy's and the first
+        // post-class kernel's wall-clock stamps
+        const bool kb = !h->stamps || d > PCG_MAX_DEPTH;
         for (int k = 0; k < 2; ++k)
             if (!rv[k]) PCG_HIP(h, hipEventCreate(&rv[k]));
-        PCG_HIP(h, hipEventRecord(rv[0], h->stream));
+        if (kb) PCG_HIP(h, hipEventRecord(rv[0], h->stream));
         if (nch > 0) {
             if (d == 0) {
                 const dim3 grid((unsigned)nch), block(256);
@@ -5111,6 +5133,10 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                 if (fork) {
                     if (!h->aux) PCG_HIP(h, hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking));
                     if (!h->ev_join) PCG_HIP(h, hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+                    if (!kb) {   // the fork point (no timing)
+                        if (!h->ev_fork) PCG_HIP(h, hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+                        PCG_HIP(h, hipEventRecord(h->ev_fork, h->stream));
+                    }
                 }
                 auto run_narrow = [&]() -> int {
                     if (s_hi > s_lo) {
@@ -5169,7 +5195,7 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                         ~StreamSwap() { if (on) h->stream = main; }
                     } swap{h, main_stream, fork};
                     if (fork) {
-                        PCG_HIP(h, hipStreamWaitEvent(h->aux, rv[0], 0));
+                        PCG_HIP(h, hipStreamWaitEvent(h->aux, kb ? rv[0] : h->ev_fork, 0));
                         h->stream = h->aux;
                     }
                     if (w_hi > w_lo) {
@@ -5238,8 +5264,8 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
             }
         }
         PCG_HIP(h, hipGetLastError());
-        PCG_HIP(h, hipEventRecord(rv[1], h->stream));
-        h->run_timed = true;
+        if (kb) PCG_HIP(h, hipEventRecord(rv[1], h->stream));
+        h->run_timed = kb;
         PCG_HT(h, "run:launched");
         // exact path over the deferred list; the kernel reads the list length on the device
         // (no host round trip) and raises the overflow status byte if the list overflowed
@@ -5247,12 +5273,14 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
         // k_level_lds's wave slots, k_level_deep): nothing is deferred, no launch
         if (d > PCG_MAX_DEPTH) return PCG_OK;
         a = make_args(h, d, mode == MODE_EXACT);
+        a.stamp_end = kb ? 0 : 1;     // the first kernel behind the classes closes the bracket
         if (h->tgroup && use_screen32(h, d)) {   // the fp32 sweep's undecided tests, in fp64
             // the list length is only known on the device; a grid-stride loop over it (1024 blocks
             // measured no faster than 256: 40 vs 36 us for 1.3e5 tests)
             if (d == 2) hipLaunchKernelGGL(k_screen<2>, dim3(256), dim3(256), 0, h->stream, a);
             else if (d == 3) hipLaunchKernelGGL(k_screen<3>, dim3(256), dim3(256), 0, h->stream, a);
             else hipLaunchKernelGGL(k_screen<4>, dim3(256), dim3(256), 0, h->stream, a);
+            a.stamp_end = 0;
         }
         const int m = d + 2;
         const int per = (m * m + 2 * m) * 8;      // one LDS slot per wave
@@ -5293,7 +5321,10 @@ int level_end_enqueue(pcg_handle *h, unsigned long long *seq) {
     // degrees + counters + status -> host-mapped summary
     int rc = graph_launch(h);
     // graphs whose CSR holds at most PCG_TUNE_EXPORT_INLINE entries export on the handle's stream
-    if (!rc && d >= 1 && xsum > 0 && xsum <= h->tune[PCG_TUNE_EXPORT_INLINE]) {
+    // the last depth of a max_depth-bounded run has no next depth to overlap its export with: it
+    // runs right behind the barrier on the handle's stream (no cross-stream hop before the sync)
+    const bool last = PCG_LAST_XINL && h->run_max_depth >= 0 && d >= h->run_max_depth;
+    if (!rc && d >= 1 && xsum > 0 && (last || xsum <= h->tune[PCG_TUNE_EXPORT_INLINE])) {
         // a small graph's export on the handle's stream, right behind the barrier: one launch
         // instead of the export stream's four calls (it runs while the host decomposes the next
         // depth, and is done before any later launch can reuse buffer set xcb)
@@ -5335,9 +5366,20 @@ int level_end_finish(pcg_handle *h, int d, unsigned long long seq, pcg_stats *st
     PCG_HT(h, "end:summary-seen");
     const LevelSummary *sm = sum_slot(h, seq);
     const DevCounters c = sm->ctr;
+    if (h->stamps) {
+        // depth d's boundaries: the summary before it (init's at depth 0, still in the other slot of
+        // the ring, which holds seq - 1 until the next launch) and this one
+        if (h->lev_stamp.empty()) {
+            const LevelSummary *pv = sum_slot(h, seq - 1);
+            h->lev_stamp.push_back(pv->seq == seq - 1 ? pv->stamp : 0ull);
+        }
+        h->lev_stamp.push_back(sm->stamp);
+        if (d < PCG_MAX_LEVELS && c.t_run0 && c.t_run1 > c.t_run0 && h->wall_khz > 0)
+            h->st.kernel_ms[d] = (double)(c.t_run1 - c.t_run0) / h->wall_khz;
+    }
     uint8_t status[8];
     for (int k = 0; k < 8; ++k) status[k] = sm->status[k];
-    if (h->rev[d][1] && !h->lev_on) {   // (skeleton_once reads every depth's brackets after its last depth)
+    if (h->rev[d][1] && !h->lev_on && h->run_timed) {   // (skeleton_once reads every depth's brackets after its last depth)
         float ms = 0.f;
         hipError_t e = hipEventElapsedTime(&ms, h->rev[d][0], h->rev[d][1]);
         if (e == hipErrorNotReady) {        // the summary can land before the runtime marks the event
@@ -5443,8 +5485,16 @@ static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc,
     // (a synchronous copy per depth that has some sat on the level loop's critical path)
     h->defer_near = true;
     h->near_pending = 0;
+    h->run_max_depth = max_depth;
+    h->stamps = !PCG_KBRACKET;
+    h->lev_stamp.clear();
+    if (h->stamps && h->wall_khz <= 0) {
+        int khz = 0;
+        (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device);
+        h->wall_khz = khz > 0 ? khz : 100000;
+    }
     int rc = pcg_skeleton_init(h, C, n, ldc, N, alpha, flags, removed_level);
-    if (rc) { h->lev_on = false; h->defer_near = false; return rc; }
+    if (rc) { h->lev_on = false; h->defer_near = false; h->run_max_depth = -1; h->stamps = false; return rc; }
     PCG_HT(h, "init:done");
     int done = 0;
     for (int depth = 0;; ++depth) {
@@ -5458,11 +5508,14 @@ static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc,
         unsigned long long seq = 0;
         if (!rc) rc = level_end_enqueue(h, &seq);
         if (!rc) rc = level_end_finish(h, depth, seq, nullptr);
-        if (rc) { h->lev_on = false; h->defer_near = false; return rc; }
+        if (rc) { h->lev_on = false; h->defer_near = false; h->run_max_depth = -1; h->stamps = false; return rc; }
         done = depth + 1;
     }
     h->lev_on = false;
     h->defer_near = false;
+    h->run_max_depth = -1;
+    const bool stamped = h->stamps;
+    h->stamps = false;
     const int64_t nnew = h->near_pending - h->near_seen;
     if (nnew > 0) {
         if (!pcg_ensure_pinned(h, h->near_pin, sizeof(pcg_record) * (size_t)nnew))
@@ -5478,7 +5531,19 @@ static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc,
         h->near_h.insert(h->near_h.end(), src, src + nnew);
         h->near_seen = h->near_pending;
     }
-    if (done && h->lev_n > done) {
+    if (stamped) {
+        for (int depth = 0; depth < done && depth + 1 < (int)h->lev_stamp.size(); ++depth) {
+            const unsigned long long t0 = h->lev_stamp[depth], t1 = h->lev_stamp[depth + 1];
+            if (t0 && t1 > t0) h->st.level_ms[depth] = (double)(t1 - t0) / h->wall_khz;
+        }
+        for (int depth = PCG_MAX_DEPTH + 1; depth < done; ++depth)   // (unstamped depths: event brackets)
+            if (h->rev[depth][1]) {
+                float ms = 0.f;
+                PCG_HIP(h, hipEventSynchronize(h->rev[depth][1]));
+                PCG_HIP(h, hipEventElapsedTime(&ms, h->rev[depth][0], h->rev[depth][1]));
+                h->st.kernel_ms[depth] = ms;
+            }
+    } else if (done && h->lev_n > done) {
         PCG_HIP(h, hipEventSynchronize(h->lev[done]));
         for (int depth = 0; depth < done; ++depth) {
             float ms = 0.f;
@@ -5687,7 +5752,12 @@ int export_sync(pcg_handle *h) {
     // exports on the handle's stream (xinl) and/or on the export stream: the counter is read
     // behind all of them
     hipStream_t s = h->xs ? h->xs : h->stream;
-    if (h->xs && h->xinl) {
+    if (PCG_LAST_XINL && h->xs && h->xinl) {
+        // the counter is read on the handle's stream, behind the export stream's pending exports
+        for (int i = 0; i < 2; ++i)
+            if (h->xpending[i]) PCG_HIP(h, hipStreamWaitEvent(h->stream, h->ev_xdone[i], 0));
+        s = h->stream;
+    } else if (h->xs && h->xinl) {
         if (!h->ev_xready) PCG_HIP(h, hipEventCreateWithFlags(&h->ev_xready, hipEventDisableTiming));
         PCG_HIP(h, hipEventRecord(h->ev_xready, h->stream));
         PCG_HIP(h, hipStreamWaitEvent(h->xs, h->ev_xready, 0));
