@@ -4552,6 +4552,9 @@ bool use_wave(const pcg_handle *h, int mode, int d, double tests) {
 #ifndef PCG_L1_PAIRS
 #define PCG_L1_PAIRS 4096
 #endif
+#ifndef PCG_REST_MAIN
+#define PCG_REST_MAIN 0x6    // depths (bit 1 << d) whose wide / large class runs on the main stream, the narrow one on aux
+#endif
 #ifndef PCG_CLASS_ORDER
 #define PCG_CLASS_ORDER 0
 #endif
@@ -5128,8 +5131,12 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                 // stream: narrow then the rest / the rest then narrow)
                 const bool fork = PCG_CLASS_ORDER <= 1 && s_hi > s_lo && (w_hi > w_lo || l_hi > l_lo);
                 hipStream_t main_stream = h->stream;
-                // the fork point is the kernel bracket's start event rv[0], recorded on the main stream
-                // just above: one event record less between the prefix copy and the first class launch
+                // the fork point is the kernel bracket's start event rv[0] (or ev_fork), recorded on the
+                // main stream after the prefix copy. The class expected to finish first runs on the aux
+                // stream (PCG_REST_MAIN: depths whose wide / large class is the longer one run it on
+                // the main stream and the narrow class on aux), so the join waits on an event that has
+                // usually fired already instead of one that fires a cross-stream hop late
+                const bool rest_main = fork && ((PCG_REST_MAIN >> d) & 1);
                 if (fork) {
                     if (!h->aux) PCG_HIP(h, hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking));
                     if (!h->ev_join) PCG_HIP(h, hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
@@ -5190,14 +5197,6 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                     return PCG_OK;
                 };
                 auto run_rest = [&]() -> int {
-                    struct StreamSwap {   // the wide / large classes launch on h->aux; restored on every exit
-                        pcg_handle *h; hipStream_t main; bool on;
-                        ~StreamSwap() { if (on) h->stream = main; }
-                    } swap{h, main_stream, fork};
-                    if (fork) {
-                        PCG_HIP(h, hipStreamWaitEvent(h->aux, kb ? rv[0] : h->ev_fork, 0));
-                        h->stream = h->aux;
-                    }
                     if (w_hi > w_lo) {
                         LevelArgs aw = a;
                         aw.cpre = (const int64_t *)h->cpre.p + (h->n + 1);
@@ -5253,14 +5252,27 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                         else if (mode == MODE_FULLP) launch_level_mode<MODE_FULLP>(h, al, l_hi - l_lo, lds);
                         else launch_level_mode<MODE_EXACT>(h, al, l_hi - l_lo, lds);
                     }
-                    if (fork) PCG_HIP(h, hipEventRecord(h->ev_join, h->aux));
                     return PCG_OK;
                 };
+                if (fork) PCG_HIP(h, hipStreamWaitEvent(h->aux, kb ? rv[0] : h->ev_fork, 0));
+                // a class launched on the aux stream (h->stream swapped; restored on every exit)
+                auto launch = [&](bool on_aux, auto &&fn) -> int {
+                    struct StreamSwap {
+                        pcg_handle *h; hipStream_t main; bool on;
+                        ~StreamSwap() { if (on) h->stream = main; }
+                    } swap{h, main_stream, on_aux};
+                    if (on_aux) h->stream = h->aux;
+                    return fn();
+                };
                 const bool rest_first = PCG_CLASS_ORDER == 1 || PCG_CLASS_ORDER == 3;
-                int rc2 = rest_first ? run_rest() : run_narrow();
-                if (!rc2) rc2 = rest_first ? run_narrow() : run_rest();
+                const bool narrow_aux = fork && rest_main, rest_aux = fork && !rest_main;
+                int rc2 = rest_first ? launch(rest_aux, run_rest) : launch(narrow_aux, run_narrow);
+                if (!rc2) rc2 = rest_first ? launch(narrow_aux, run_narrow) : launch(rest_aux, run_rest);
                 if (rc2) return rc2;
-                if (fork) PCG_HIP(h, hipStreamWaitEvent(main_stream, h->ev_join, 0));
+                if (fork) {
+                    PCG_HIP(h, hipEventRecord(h->ev_join, h->aux));
+                    PCG_HIP(h, hipStreamWaitEvent(main_stream, h->ev_join, 0));
+                }
             }
         }
         PCG_HIP(h, hipGetLastError());
