@@ -167,6 +167,7 @@ extern "C" int pcg_destroy(pcg_handle *h) {
             if (e) hipEventDestroy(e);
     if (h->ev_join) hipEventDestroy(h->ev_join);
     if (h->ev_fork) hipEventDestroy(h->ev_fork);
+    if (h->tail) hipHostFree(h->tail);
     if (h->aux) hipStreamDestroy(h->aux);
     if (h->xs) hipStreamDestroy(h->xs);
     if (h->ev_xready) hipEventDestroy(h->ev_xready);

@@ -137,12 +137,16 @@ struct pcg_handle {
     int64_t near_pending = 0;        // the device list's length (capped) at the last level end
     bool defer_near = false;         // skeleton_once: near-alpha records copied once after the last depth
     PinBuf near_pin;                 // their host staging
-    int run_max_depth = -1;
+    int run_max_depth = -1;          // skeleton_once's max_depth (-1: unbounded, or the level-step API)
     // skeleton_once's depth boundaries (the summaries' wall-clock stamps; PCG_KBRACKET = 0)
     std::vector<unsigned long long> lev_stamp;
     bool stamps = false;
     int wall_khz = 0;
-    hipEvent_t ev_fork = nullptr;    // the class fork point when the kernel brackets are stamped          // skeleton_once's max_depth (-1: unbounded, or the level-step API)
+    hipEvent_t ev_fork = nullptr;    // the class fork point when the kernel brackets are stamped
+    // skeleton_once's last device -> host transfer (k_tail_copy): host-coherent, mapped
+    void *tail = nullptr, *tail_dev = nullptr;
+    size_t tail_bytes = 0;
+    unsigned long long tail_seq = 0;
     size_t summary_slot = 0;         // bytes per slot of the two-slot host-mapped summary ring
     int screen_eff = 0;              // the current depth's effective mask (set by pcg_level_begin)
     int screen_mask = -1;            // depths (bit 1 << d) with the fp32-screened T-group sweep (k_level_lds_f); -1 = default

@@ -4552,6 +4552,9 @@ bool use_wave(const pcg_handle *h, int mode, int d, double tests) {
 #ifndef PCG_L1_PAIRS
 #define PCG_L1_PAIRS 4096
 #endif
+#ifndef PCG_TAIL_SPIN
+#define PCG_TAIL_SPIN 1      // skeleton_once's last transfer: one kernel into host-coherent memory, host spin (0: blits + sync)
+#endif
 #ifndef PCG_REST_MAIN
 #define PCG_REST_MAIN 0x6    // depths (bit 1 << d) whose wide / large class runs on the main stream, the narrow one on aux
 #endif
@@ -4649,6 +4652,24 @@ int graph_launch(pcg_handle *h) {
         PCG_HIP(h, hipEventRecord(e, h->stream));
     }
     return PCG_OK;
+}
+
+// skeleton_once's last device -> host transfer, one launch: the near-alpha records not yet copied
+// and the sepset row counter into host-coherent memory (out[1], records from out + 8), then the
+// sequence number out[0] the host spins on (no blit launches, no stream-synchronize wake-up)
+__global__ void k_tail_copy(const unsigned long long *exp_ctr, const pcg_record *near_src, int64_t nnew,
+                            unsigned long long *out, unsigned long long seq) {
+    constexpr int WORDS = (int)(sizeof(pcg_record) / sizeof(uint32_t));
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(near_src);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(out + 8);
+    for (int64_t i = threadIdx.x; i < nnew * WORDS; i += blockDim.x) dst[i] = src[i];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        out[1] = exp_ctr ? *reinterpret_cast<const volatile unsigned long long *>(exp_ctr) : 0ull;
+        __threadfence_system();
+        __atomic_store_n(&out[0], seq, __ATOMIC_RELEASE);
+    }
 }
 
 // chunk prefix (host-mapped, written by the decomposition) -> device, by a kernel on the
@@ -5481,6 +5502,62 @@ extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
     return level_end_finish(h, h->depth, seq, stats);
 }
 
+// the level loop's tail (PCG_TAIL_SPIN): the exports still on the export stream joined into the
+// handle's stream, then k_tail_copy; the host spins on its sequence number as on a level summary
+static int tail_copy(pcg_handle *h, int64_t nnew) {
+    const size_t need = 64 + sizeof(pcg_record) * (size_t)std::max<int64_t>(nnew, 0);
+    if (h->tail_bytes < need) {
+        if (h->tail) { PCG_HIP(h, hipStreamSynchronize(h->stream)); (void)hipHostFree(h->tail); }
+        h->tail = h->tail_dev = nullptr;
+        h->tail_bytes = 0;
+        void *p = nullptr;
+        if (hipHostMalloc(&p, need, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+            return pcg_fail(h, PCG_ERR_OOM, "host-mapped tail buffer");
+        h->tail = p;
+        PCG_HIP(h, hipHostGetDevicePointer(&h->tail_dev, p, 0));
+        h->tail_bytes = need;
+        reinterpret_cast<volatile unsigned long long *>(p)[0] = 0;
+        h->tail_seq = 0;
+    }
+    for (int i = 0; i < 2; ++i)
+        if (h->xpending[i]) PCG_HIP(h, hipStreamWaitEvent(h->stream, h->ev_xdone[i], 0));
+    const unsigned long long seq = ++h->tail_seq;
+    hipLaunchKernelGGL(k_tail_copy, dim3(1), dim3(256), 0, h->stream,
+                       h->xany ? (const unsigned long long *)h->exp_ctr.p : nullptr,
+                       (const pcg_record *)h->nearbuf.p + h->near_seen, std::max<int64_t>(nnew, 0),
+                       (unsigned long long *)h->tail_dev, seq);
+    PCG_HIP(h, hipGetLastError());
+    const unsigned long long *tw = reinterpret_cast<const unsigned long long *>(h->tail);
+    unsigned spins = 0;
+    while (__atomic_load_n(&tw[0], __ATOMIC_ACQUIRE) != seq) {
+        if ((++spins & 1023) == 0) {
+            const hipError_t e = hipStreamQuery(h->stream);
+            if (e == hipSuccess) {
+                if (__atomic_load_n(&tw[0], __ATOMIC_ACQUIRE) == seq) break;
+                return pcg_fail(h, PCG_ERR_HIP, "tail copy not written (seq %llu)", seq);
+            }
+            if (e != hipErrorNotReady) return pcg_fail(h, PCG_ERR_HIP, "stream error: %s", hipGetErrorString(e));
+        }
+        __builtin_ia32_pause();
+    }
+    if (nnew > 0) {
+        const pcg_record *src = reinterpret_cast<const pcg_record *>(tw + 8);
+        h->near_h.insert(h->near_h.end(), src, src + nnew);
+        h->near_seen = h->near_pending;
+    }
+    if (h->xany) {
+        const unsigned long long rows = tw[1];
+        h->xany = false;
+        h->xinl = false;
+        h->xpending[0] = h->xpending[1] = false;
+        if ((int64_t)rows > h->export_cap)
+            return pcg_fail(h, PCG_ERR_OVERFLOW, "sepset export overflow (%llu rows > %lld)", rows,
+                            (long long)h->export_cap);
+        h->export_rows = (int64_t)rows;
+    }
+    return PCG_OK;
+}
+
 // The single-GPU level loop. (Round 3/4 built a pipelined form that enqueued depth d before depth
 // d - 1's summary was read, and a fused one-launch level barrier; both measured slower — DESIGN §9
 // — and were removed in round 5.)
@@ -5529,15 +5606,18 @@ static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc,
     const bool stamped = h->stamps;
     h->stamps = false;
     const int64_t nnew = h->near_pending - h->near_seen;
-    if (nnew > 0) {
+    if (PCG_TAIL_SPIN) {
+        rc = tail_copy(h, nnew);
+        if (rc) return rc;
+    } else if (nnew > 0) {
         if (!pcg_ensure_pinned(h, h->near_pin, sizeof(pcg_record) * (size_t)nnew))
             return pcg_fail(h, PCG_ERR_OOM, "pinned near-alpha records");
         PCG_HIP(h, hipMemcpyAsync(h->near_pin.p, (pcg_record *)h->nearbuf.p + h->near_seen,
                                   sizeof(pcg_record) * (size_t)nnew, hipMemcpyDeviceToHost, h->stream));
     }
-    rc = export_sync(h);                 // the last depth's export (the skeleton's sepset rows)
+    if (!PCG_TAIL_SPIN) rc = export_sync(h);   // the last depth's export (the skeleton's sepset rows)
     if (rc) return rc;
-    if (nnew > 0) {
+    if (!PCG_TAIL_SPIN && nnew > 0) {
         PCG_HIP(h, hipStreamSynchronize(h->stream));
         const pcg_record *src = (const pcg_record *)h->near_pin.p;
         h->near_h.insert(h->near_h.end(), src, src + nnew);
