@@ -4555,6 +4555,12 @@ bool use_wave(const pcg_handle *h, int mode, int d, double tests) {
 #ifndef PCG_TAIL_SPIN
 #define PCG_TAIL_SPIN 1      // skeleton_once's last transfer: one kernel into host-coherent memory, host spin (0: blits + sync)
 #endif
+#ifndef PCG_TAIL_EARLY
+#define PCG_TAIL_EARLY 1     // the tail kernel queued behind the depth bound's last barrier (0: after the host read it)
+#endif
+#ifndef PCG_MAIN_FIRST
+#define PCG_MAIN_FIRST 1     // with PCG_REST_MAIN: the main-stream (longer) class launched before the forked one
+#endif
 #ifndef PCG_REST_MAIN
 #define PCG_REST_MAIN 0x6    // depths (bit 1 << d) whose wide / large class runs on the main stream, the narrow one on aux
 #endif
@@ -4657,16 +4663,21 @@ int graph_launch(pcg_handle *h) {
 // skeleton_once's last device -> host transfer, one launch: the near-alpha records not yet copied
 // and the sepset row counter into host-coherent memory (out[1], records from out + 8), then the
 // sequence number out[0] the host spins on (no blit launches, no stream-synchronize wake-up)
-__global__ void k_tail_copy(const unsigned long long *exp_ctr, const pcg_record *near_src, int64_t nnew,
-                            unsigned long long *out, unsigned long long seq) {
+// (the count of new records, out[2], from the device's cumulative near-alpha counter: the kernel
+// can be queued before the host has read the last summary)
+__global__ void k_tail_copy(const unsigned long long *exp_ctr, const DevCounters *ctr, const pcg_record *nearl,
+                            int64_t near_seen, int64_t near_cap, unsigned long long *out, unsigned long long seq) {
     constexpr int WORDS = (int)(sizeof(pcg_record) / sizeof(uint32_t));
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(near_src);
+    const int64_t cum = min((int64_t)*reinterpret_cast<const volatile unsigned long long *>(&ctr->near_alpha), near_cap);
+    const int64_t nnew = max(cum - near_seen, (int64_t)0);
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(nearl + near_seen);
     uint32_t *dst = reinterpret_cast<uint32_t *>(out + 8);
     for (int64_t i = threadIdx.x; i < nnew * WORDS; i += blockDim.x) dst[i] = src[i];
     __threadfence_system();
     __syncthreads();
     if (threadIdx.x == 0) {
         out[1] = exp_ctr ? *reinterpret_cast<const volatile unsigned long long *>(exp_ctr) : 0ull;
+        out[2] = (unsigned long long)nnew;
         __threadfence_system();
         __atomic_store_n(&out[0], seq, __ATOMIC_RELEASE);
     }
@@ -5285,7 +5296,8 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                     if (on_aux) h->stream = h->aux;
                     return fn();
                 };
-                const bool rest_first = PCG_CLASS_ORDER == 1 || PCG_CLASS_ORDER == 3;
+                // (the class on the main stream is launched first: it is the longer one)
+                const bool rest_first = PCG_CLASS_ORDER == 1 || PCG_CLASS_ORDER == 3 || (PCG_MAIN_FIRST && rest_main);
                 const bool narrow_aux = fork && rest_main, rest_aux = fork && !rest_main;
                 int rc2 = rest_first ? launch(rest_aux, run_rest) : launch(narrow_aux, run_narrow);
                 if (!rc2) rc2 = rest_first ? launch(narrow_aux, run_narrow) : launch(rest_aux, run_rest);
@@ -5503,9 +5515,10 @@ extern "C" int pcg_level_end(pcg_handle *h, pcg_stats *stats) {
 }
 
 // the level loop's tail (PCG_TAIL_SPIN): the exports still on the export stream joined into the
-// handle's stream, then k_tail_copy; the host spins on its sequence number as on a level summary
-static int tail_copy(pcg_handle *h, int64_t nnew) {
-    const size_t need = 64 + sizeof(pcg_record) * (size_t)std::max<int64_t>(nnew, 0);
+// handle's stream, then k_tail_copy (queued right behind the last depth's barrier when the depth
+// bound says it is the last); the host spins on its sequence number as on a level summary
+static int tail_launch(pcg_handle *h) {
+    const size_t need = 64 + sizeof(pcg_record) * (size_t)std::max<int64_t>(h->near_cap, 1);
     if (h->tail_bytes < need) {
         if (h->tail) { PCG_HIP(h, hipStreamSynchronize(h->stream)); (void)hipHostFree(h->tail); }
         h->tail = h->tail_dev = nullptr;
@@ -5521,12 +5534,16 @@ static int tail_copy(pcg_handle *h, int64_t nnew) {
     }
     for (int i = 0; i < 2; ++i)
         if (h->xpending[i]) PCG_HIP(h, hipStreamWaitEvent(h->stream, h->ev_xdone[i], 0));
-    const unsigned long long seq = ++h->tail_seq;
     hipLaunchKernelGGL(k_tail_copy, dim3(1), dim3(256), 0, h->stream,
-                       h->xany ? (const unsigned long long *)h->exp_ctr.p : nullptr,
-                       (const pcg_record *)h->nearbuf.p + h->near_seen, std::max<int64_t>(nnew, 0),
-                       (unsigned long long *)h->tail_dev, seq);
+                       h->xany ? (const unsigned long long *)h->exp_ctr.p : nullptr, (const DevCounters *)h->ctr.p,
+                       (const pcg_record *)h->nearbuf.p, h->near_seen, h->near_cap,
+                       (unsigned long long *)h->tail_dev, ++h->tail_seq);
     PCG_HIP(h, hipGetLastError());
+    return PCG_OK;
+}
+
+static int tail_wait(pcg_handle *h) {
+    const unsigned long long seq = h->tail_seq;
     const unsigned long long *tw = reinterpret_cast<const unsigned long long *>(h->tail);
     unsigned spins = 0;
     while (__atomic_load_n(&tw[0], __ATOMIC_ACQUIRE) != seq) {
@@ -5540,11 +5557,12 @@ static int tail_copy(pcg_handle *h, int64_t nnew) {
         }
         __builtin_ia32_pause();
     }
+    const int64_t nnew = (int64_t)tw[2];
     if (nnew > 0) {
         const pcg_record *src = reinterpret_cast<const pcg_record *>(tw + 8);
         h->near_h.insert(h->near_h.end(), src, src + nnew);
-        h->near_seen = h->near_pending;
     }
+    h->near_seen += nnew;
     if (h->xany) {
         const unsigned long long rows = tw[1];
         h->xany = false;
@@ -5586,6 +5604,7 @@ static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc,
     if (rc) { h->lev_on = false; h->defer_near = false; h->run_max_depth = -1; h->stamps = false; return rc; }
     PCG_HT(h, "init:done");
     int done = 0;
+    bool tail_queued = false;
     for (int depth = 0;; ++depth) {
         if (max_depth >= 0 && depth > max_depth) break;
         if (depth >= PCG_MAX_LEVELS) break;   // pcg_level_begin refuses deeper levels itself
@@ -5596,6 +5615,11 @@ static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc,
         if (!rc) rc = pcg_level_run(h, 0, total);
         unsigned long long seq = 0;
         if (!rc) rc = level_end_enqueue(h, &seq);
+        // the depth bound's last depth: the tail transfer queued behind its barrier right away
+        if (!rc && PCG_TAIL_SPIN && PCG_TAIL_EARLY && max_depth >= 0 && depth >= max_depth) {
+            rc = tail_launch(h);
+            tail_queued = true;
+        }
         if (!rc) rc = level_end_finish(h, depth, seq, nullptr);
         if (rc) { h->lev_on = false; h->defer_near = false; h->run_max_depth = -1; h->stamps = false; return rc; }
         done = depth + 1;
@@ -5607,7 +5631,8 @@ static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc,
     h->stamps = false;
     const int64_t nnew = h->near_pending - h->near_seen;
     if (PCG_TAIL_SPIN) {
-        rc = tail_copy(h, nnew);
+        if (!tail_queued) rc = tail_launch(h);
+        if (!rc) rc = tail_wait(h);
         if (rc) return rc;
     } else if (nnew > 0) {
         if (!pcg_ensure_pinned(h, h->near_pin, sizeof(pcg_record) * (size_t)nnew))
