@@ -17,7 +17,10 @@
  *    caller-owned; "host" pointers are ordinary host memory. Scratch (adjacency bitmask,
  *    work lists, sepset unions, records) is owned by the handle and grows on demand.
  *  - One handle per (process, device). Calls are ordered on the handle's HIP stream and are
- *    synchronous w.r.t. the host on return unless stated otherwise. Not re-entrant per handle;
+ *    synchronous w.r.t. the host on return unless stated otherwise (pcg_skeleton /
+ *    pcg_pc_skeleton return once every result write has completed: their last kernel signals the
+ *    host through host-coherent memory and may still be retiring on the handle's stream, which
+ *    orders any later work behind it). Not re-entrant per handle;
  *    separate handles may be used from separate threads. No global mutable state.
  *  - Matrices are row-major with an explicit leading dimension (in elements).
  */
