@@ -307,6 +307,22 @@ int pcg_set_removal_buffer(pcg_handle *h, uint8_t *rm_dev, int64_t bytes);
 int pcg_comm_unique_id(void *id_out, int64_t bytes);
 int pcg_comm_init(pcg_handle *h, const void *unique_id, int rank, int world);
 int pcg_comm_destroy(pcg_handle *h);
+/* In-process transport for the same driver: a group of `world` handles used from separate
+ * threads of ONE process (on one or several devices), with host-staged collectives that
+ * complete before they return. RCCL refuses two ranks on one device, so this is the transport
+ * that runs the driver's rank-dependent steps (level split, packed all-gather + OR merge, stats
+ * all-reduce, sepset gathers) at world 2..8 on a single GPU; results are those of the RCCL
+ * transport. Every collective is checked to be the same (kind, type, size) on every rank — a
+ * mismatch, a rank failing inside a collective, or a barrier waiting longer than `timeout_s`
+ * (<= 0: 300 s) breaks the group and every rank returns PCG_ERR_RCCL instead of hanging.
+ * pcg_comm_init_group attaches handle `h` as `rank` (pcg_comm_destroy detaches it);
+ * pcg_comm_group_destroy refuses a group that still has an attached handle.
+ * pcg_comm_group_stats: collectives completed, bytes contributed by all ranks, broken flag. */
+typedef struct pcg_comm_group pcg_comm_group;
+int pcg_comm_group_create(int world, double timeout_s, pcg_comm_group **out);
+int pcg_comm_group_destroy(pcg_comm_group *g);
+int pcg_comm_group_stats(pcg_comm_group *g, int64_t *collectives, int64_t *bytes, int32_t *broken);
+int pcg_comm_init_group(pcg_handle *h, pcg_comm_group *g, int rank);
 /* K1 on the communicator: pcg_corr_shard + RCCL all-gather + pcg_corr_shard_finish; C is
  * bitwise the single-GPU pcg_corr result on every rank.                                   */
 int pcg_corr_sharded(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx,

@@ -137,6 +137,10 @@ SIGNATURES = [
     ("pcg_comm_unique_id", I32, [P, I64]),
     ("pcg_comm_init", I32, [P, P, ctypes.c_int, ctypes.c_int]),
     ("pcg_comm_destroy", I32, [P]),
+    ("pcg_comm_group_create", I32, [ctypes.c_int, D, ctypes.POINTER(P)]),
+    ("pcg_comm_group_destroy", I32, [P]),
+    ("pcg_comm_group_stats", I32, [P, ctypes.POINTER(I64), ctypes.POINTER(I64), ctypes.POINTER(I32)]),
+    ("pcg_comm_init_group", I32, [P, P, ctypes.c_int]),
     ("pcg_corr_sharded", I32, [P, P, I64, I64, I64, P, I64]),
     ("pcg_skeleton_sharded", I32, [P, P, I64, I64, I64, D, ctypes.c_int, ctypes.c_int, P, ctypes.POINTER(PcgStats)]),
     ("pcg_pagerank_dense", I32, [P, P, I64, I64, D, ctypes.c_int, D, P]),

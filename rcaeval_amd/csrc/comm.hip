@@ -7,16 +7,39 @@
 // so every rank ORs the gathered copies itself) before pcg_level_end applies them identically
 // everywhere. The loop runs in C: no host-language round trip between the per-depth steps.
 //
-// RCCL is resolved at run time: first the copy the process has already loaded (PyTorch ships
-// one), else librccl.so.1 — so a process that also uses torch.distributed holds one RCCL.
+// The driver's collectives go through a per-handle transport table (CommOps):
+//  * RCCL (pcg_comm_init, the default): resolved at run time — first the copy the process has
+//    already loaded (PyTorch ships one), else librccl.so.1 — so a process that also uses
+//    torch.distributed holds one RCCL;
+//  * an in-process group of handles (pcg_comm_group_create / pcg_comm_init_group): host-staged
+//    collectives between handles driven from separate threads of one process. RCCL refuses two
+//    ranks on one device (rccl.h ncclCommInitRank: "each rank must use a different device"), so
+//    this is how the rank-dependent code of the driver (the level split, the packed all-gather
+//    + merge, the stats all-reduce, the sepset gathers) runs at world 2..8 on one GPU. The group
+//    also checks that every rank issues the same collective (kind, size) in the same order — the
+//    mismatch RCCL would hang on — and fails all ranks with PCG_ERR_RCCL when they do not.
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
 #include <mutex>
 
 #include "handle.h"
+
+enum CommType { COMM_I32, COMM_I64 };
+enum CommOp { COMM_MAX, COMM_SUM };
+
+// the collectives of the native driver, on the handle's stream (RCCL) or completed on return
+// (group). all_gather: `bytes` per rank, rank-major into recv; all_reduce: in place.
+struct CommOps {
+    const char *name;
+    int (*all_gather)(pcg_handle *h, const void *send, void *recv, size_t bytes);
+    int (*all_reduce)(pcg_handle *h, void *buf, size_t count, CommType t, CommOp op);
+    void (*release)(pcg_handle *h);
+};
 
 namespace {
 
@@ -66,9 +89,183 @@ const Rccl &rccl() {
             return pcg_fail((h), PCG_ERR_RCCL, "%s failed: %s", #expr, rccl().error_string(_r)); \
     } while (0)
 
+// ---- RCCL transport -------------------------------------------------------------------
+int rccl_all_gather(pcg_handle *h, const void *send, void *recv, size_t bytes) {
+    PCG_NCCL(h, rccl().all_gather(send, recv, bytes, ncclUint8, (ncclComm_t)h->comm, h->stream));
+    return PCG_OK;
+}
+
+int rccl_all_reduce(pcg_handle *h, void *buf, size_t count, CommType t, CommOp op) {
+    PCG_NCCL(h, rccl().all_reduce(buf, buf, count, t == COMM_I32 ? ncclInt32 : ncclInt64,
+                                  op == COMM_MAX ? ncclMax : ncclSum, (ncclComm_t)h->comm, h->stream));
+    return PCG_OK;
+}
+
+void rccl_release(pcg_handle *h) {
+    if (h->comm && rccl().ok) rccl().comm_destroy((ncclComm_t)h->comm);
+}
+
+const CommOps kRcclOps = {"rccl", rccl_all_gather, rccl_all_reduce, rccl_release};
+
+}  // namespace
+
+// ---- in-process group transport ---------------------------------------------------------
+// One slot of host memory per rank. A collective: each rank copies its device operand into its
+// slot (stream-synchronised), all ranks meet at a barrier, each rank reads every slot (gather:
+// concatenates, reduce: combines in rank order) and copies the result to its device buffer, and
+// all ranks meet again before any slot is reused. A barrier that waits longer than the group's
+// timeout, or a rank that fails inside a collective, breaks the group: every waiting and later
+// collective returns PCG_ERR_RCCL instead of hanging.
+struct pcg_comm_group {
+    int world = 1;
+    double timeout_s = 300.0;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t gen = 0;
+    bool broken = false;
+    std::string why;
+    std::vector<std::vector<unsigned char>> slot;
+    std::vector<uint64_t> tag;          // per rank: the collective it is in (kind, type, op, bytes)
+    std::vector<pcg_handle *> member;
+    int64_t collectives = 0;            // completed collectives (counted once per group)
+    int64_t bytes = 0;                  // bytes contributed by all ranks over them
+};
+
+namespace {
+
+void group_break(pcg_comm_group *g, const std::string &why) {
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (!g->broken) {
+        g->broken = true;
+        g->why = why;
+    }
+    g->cv.notify_all();
+}
+
+// 0, or -1 when the group is (or becomes) broken
+int group_barrier(pcg_comm_group *g) {
+    std::unique_lock<std::mutex> lk(g->mu);
+    if (g->broken) return -1;
+    const uint64_t my = g->gen;
+    if (++g->arrived == g->world) {
+        g->arrived = 0;
+        ++g->gen;
+        g->cv.notify_all();
+        return 0;
+    }
+    const bool done = g->cv.wait_for(lk, std::chrono::duration<double>(g->timeout_s),
+                                     [&] { return g->gen != my || g->broken; });
+    if (g->gen != my) return 0;
+    if (!done && !g->broken) {
+        g->broken = true;
+        g->why = "a rank did not reach the collective within the group's timeout";
+        g->cv.notify_all();
+    }
+    return -1;
+}
+
+int group_fail(pcg_handle *h, pcg_comm_group *g) {
+    std::lock_guard<std::mutex> lk(g->mu);
+    return pcg_fail(h, PCG_ERR_RCCL, "in-process group collective failed: %s",
+                    g->why.empty() ? "group broken" : g->why.c_str());
+}
+
+uint64_t group_tag(int kind, int t, int op, size_t bytes) {
+    return ((uint64_t)kind << 60) | ((uint64_t)t << 56) | ((uint64_t)op << 52) | (uint64_t)(bytes & ((1ull << 52) - 1));
+}
+
+// deposit this rank's operand and meet the others; then check every rank is in the same collective
+int group_enter(pcg_handle *h, const void *dev, size_t bytes, uint64_t tag) {
+    pcg_comm_group *g = (pcg_comm_group *)h->comm;
+    const int r = h->comm_rank;
+    std::vector<unsigned char> &s = g->slot[r];
+    s.resize(bytes);
+    hipError_t e = bytes ? hipMemcpyAsync(s.data(), dev, bytes, hipMemcpyDeviceToHost, h->stream) : hipSuccess;
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) {
+        group_break(g, std::string("rank ") + std::to_string(r) + ": " + hipGetErrorString(e));
+        return group_fail(h, g);
+    }
+    g->tag[r] = tag;
+    if (group_barrier(g)) return group_fail(h, g);
+    for (int q = 0; q < g->world; ++q)
+        if (g->tag[q] != g->tag[0]) {   // every rank sees the same tags: all of them leave here
+            group_break(g, "ranks issued different collectives (kind / type / size) at the same step");
+            return group_fail(h, g);
+        }
+    return PCG_OK;
+}
+
+int group_leave(pcg_handle *h, void *dev, const std::vector<unsigned char> &res) {
+    pcg_comm_group *g = (pcg_comm_group *)h->comm;
+    if (group_barrier(g)) return group_fail(h, g);       // every rank has read every slot
+    if (h->comm_rank == 0) {
+        std::lock_guard<std::mutex> lk(g->mu);
+        ++g->collectives;
+    }
+    hipError_t e = res.empty() ? hipSuccess
+                               : hipMemcpyAsync(dev, res.data(), res.size(), hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return pcg_fail(h, PCG_ERR_HIP, "group collective result copy: %s", hipGetErrorString(e));
+    return PCG_OK;
+}
+
+int group_all_gather(pcg_handle *h, const void *send, void *recv, size_t bytes) {
+    pcg_comm_group *g = (pcg_comm_group *)h->comm;
+    int rc = group_enter(h, send, bytes, group_tag(1, 0, 0, bytes));
+    if (rc) return rc;
+    std::vector<unsigned char> all(bytes * (size_t)g->world);
+    for (int q = 0; q < g->world; ++q)
+        if (bytes) std::memcpy(all.data() + (size_t)q * bytes, g->slot[q].data(), bytes);
+    if (h->comm_rank == 0) {
+        std::lock_guard<std::mutex> lk(g->mu);
+        g->bytes += (int64_t)(bytes * (size_t)g->world);
+    }
+    return group_leave(h, recv, all);
+}
+
+template <typename T>
+void reduce_into(std::vector<unsigned char> &out, const std::vector<std::vector<unsigned char>> &slot, size_t count,
+                 CommOp op) {
+    T *o = (T *)out.data();
+    for (size_t i = 0; i < count; ++i) {
+        T v = ((const T *)slot[0].data())[i];
+        for (size_t q = 1; q < slot.size(); ++q) {
+            const T w = ((const T *)slot[q].data())[i];
+            v = op == COMM_MAX ? std::max(v, w) : (T)(v + w);
+        }
+        o[i] = v;
+    }
+}
+
+int group_all_reduce(pcg_handle *h, void *buf, size_t count, CommType t, CommOp op) {
+    pcg_comm_group *g = (pcg_comm_group *)h->comm;
+    const size_t bytes = count * (t == COMM_I32 ? 4 : 8);
+    int rc = group_enter(h, buf, bytes, group_tag(2, (int)t, (int)op, bytes));
+    if (rc) return rc;
+    std::vector<unsigned char> res(bytes);
+    if (t == COMM_I32) reduce_into<int32_t>(res, g->slot, count, op);
+    else reduce_into<int64_t>(res, g->slot, count, op);
+    if (h->comm_rank == 0) {
+        std::lock_guard<std::mutex> lk(g->mu);
+        g->bytes += (int64_t)(bytes * (size_t)g->world);
+    }
+    return group_leave(h, buf, res);
+}
+
+void group_release(pcg_handle *h) {
+    pcg_comm_group *g = (pcg_comm_group *)h->comm;
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (h->comm_rank >= 0 && h->comm_rank < g->world && g->member[h->comm_rank] == h) g->member[h->comm_rank] = nullptr;
+}
+
+const CommOps kGroupOps = {"group", group_all_gather, group_all_reduce, group_release};
+
 int need_comm(pcg_handle *h) {
     if (!h) return PCG_ERR_INVALID;
-    if (!h->comm) return pcg_fail(h, PCG_ERR_INVALID, "no communicator: call pcg_comm_init first");
+    if (!h->comm || !h->comm_ops)
+        return pcg_fail(h, PCG_ERR_INVALID, "no communicator: call pcg_comm_init (or pcg_comm_init_group) first");
     return PCG_OK;
 }
 
@@ -82,7 +279,7 @@ int agree(pcg_handle *h, int failed) {
     int32_t v = failed ? 1 : 0;
     int32_t *d = (int32_t *)h->comm_status.p;
     PCG_HIP(h, hipMemcpyAsync(d, &v, sizeof(v), hipMemcpyHostToDevice, h->stream));
-    PCG_NCCL(h, rccl().all_reduce(d, d, 1, ncclInt32, ncclMax, (ncclComm_t)h->comm, h->stream));
+    if (int rc = h->comm_ops->all_reduce(h, d, 1, COMM_I32, COMM_MAX)) return rc;
     PCG_HIP(h, hipMemcpyAsync(&v, d, sizeof(v), hipMemcpyDeviceToHost, h->stream));
     PCG_HIP(h, hipStreamSynchronize(h->stream));
     return v;
@@ -94,7 +291,7 @@ int agree_value(pcg_handle *h, int failed, int64_t v, bool *same) {
     int64_t a[3] = {failed ? 1 : 0, v, -v};
     int64_t *d = (int64_t *)h->comm_small.p;     // >= 5 * PCG_MAX_LEVELS int64 since pcg_comm_init
     PCG_HIP(h, hipMemcpyAsync(d, a, sizeof(a), hipMemcpyHostToDevice, h->stream));
-    PCG_NCCL(h, rccl().all_reduce(d, d, 3, ncclInt64, ncclMax, (ncclComm_t)h->comm, h->stream));
+    if (int rc = h->comm_ops->all_reduce(h, d, 3, COMM_I64, COMM_MAX)) return rc;
     PCG_HIP(h, hipMemcpyAsync(a, d, sizeof(a), hipMemcpyDeviceToHost, h->stream));
     PCG_HIP(h, hipStreamSynchronize(h->stream));
     *same = a[1] == -a[2];
@@ -165,7 +362,6 @@ int sharded_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t
         return agreed_failure(h, local, g, "skeleton set-up");
     }
     int rc = PCG_OK;
-    ncclComm_t comm = (ncclComm_t)h->comm;
     uint64_t *packed = (uint64_t *)h->comm_packed.p, *gathered = (uint64_t *)h->comm_gathered.p;
     for (int depth = 0; !rc; ++depth) {
         if (max_depth >= 0 && depth > max_depth) break;
@@ -187,10 +383,10 @@ int sharded_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t
             (void)hipMemcpyAsync(packed + (P - 1), &failed_word, sizeof(failed_word), hipMemcpyHostToDevice,
                                  h->stream);
         }
-        const ncclResult_t r = rccl().all_gather(packed, gathered, (size_t)P, ncclUint64, comm, h->stream);
+        const int r = h->comm_ops->all_gather(h, packed, gathered, sizeof(uint64_t) * (size_t)P);
         if (rc) break;
-        if (r != ncclSuccess) {
-            rc = pcg_fail(h, PCG_ERR_RCCL, "ncclAllGather(packed removal flags) failed: %s", rccl().error_string(r));
+        if (r) {
+            rc = r;
             break;
         }
         rc = pcg_level_merge(h, gathered, world);
@@ -223,8 +419,7 @@ int reduce_stats(pcg_handle *h) {
     // comm_small holds 5 * PCG_MAX_LEVELS int64 since pcg_comm_init: no allocation between collectives
     PCG_HIP(h, hipMemcpyAsync(h->comm_small.p, v.data(), sizeof(int64_t) * v.size(), hipMemcpyHostToDevice,
                               h->stream));
-    PCG_NCCL(h, rccl().all_reduce(h->comm_small.p, h->comm_small.p, v.size(), ncclInt64, ncclSum,
-                                  (ncclComm_t)h->comm, h->stream));
+    if (int rc = h->comm_ops->all_reduce(h, h->comm_small.p, v.size(), COMM_I64, COMM_SUM)) return rc;
     PCG_HIP(h, hipMemcpyAsync(v.data(), h->comm_small.p, sizeof(int64_t) * v.size(), hipMemcpyDeviceToHost,
                               h->stream));
     PCG_HIP(h, hipStreamSynchronize(h->stream));
@@ -243,13 +438,12 @@ int reduce_stats(pcg_handle *h) {
 // move, so a rank that fails here takes its peers out of the gather with it.
 int gather_sepsets(pcg_handle *h) {
     const int world = h->comm_world, W = h->W;
-    ncclComm_t comm = (ncclComm_t)h->comm;
     int local = export_sync(h);
     const std::string sync_err = local ? h->err : std::string();
     int64_t *cnt_d = (int64_t *)h->comm_small.p;
     const int64_t mine = local ? -1 : h->export_rows;
     PCG_HIP(h, hipMemcpyAsync(cnt_d + world, &mine, sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
-    PCG_NCCL(h, rccl().all_gather(cnt_d + world, cnt_d, 1, ncclInt64, comm, h->stream));
+    if (int rc = h->comm_ops->all_gather(h, cnt_d + world, cnt_d, sizeof(int64_t))) return rc;
     std::vector<int64_t> cnt(world);
     PCG_HIP(h, hipMemcpyAsync(cnt.data(), cnt_d, sizeof(int64_t) * world, hipMemcpyDeviceToHost, h->stream));
     PCG_HIP(h, hipStreamSynchronize(h->stream));
@@ -274,7 +468,8 @@ int gather_sepsets(pcg_handle *h) {
     hipLaunchKernelGGL(k_pack_rows, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, h->stream,
                        (const int32_t *)h->export_xy.p, (const uint64_t *)h->exportbuf.p, mine, W, mx,
                        (int64_t *)h->comm_packed.p);
-    PCG_NCCL(h, rccl().all_gather(h->comm_packed.p, h->comm_gathered.p, (size_t)per, ncclInt64, comm, h->stream));
+    if (int rc = h->comm_ops->all_gather(h, h->comm_packed.p, h->comm_gathered.p, sizeof(int64_t) * (size_t)per))
+        return rc;
     // the last collective of the call: the export buffers grow (their rows are packed already)
     const int64_t cap = std::max<int64_t>(total, 1);
     if (!pcg_ensure(h, h->exportbuf, sizeof(uint64_t) * (size_t)cap * W) ||
@@ -300,8 +495,9 @@ int gather_sepsets(pcg_handle *h) {
 
 void pcg_comm_release(pcg_handle *h) {
     if (!h) return;
-    if (h->comm && rccl().ok) rccl().comm_destroy((ncclComm_t)h->comm);
+    if (h->comm && h->comm_ops) h->comm_ops->release(h);
     h->comm = nullptr;
+    h->comm_ops = nullptr;
     for (DevBuf *b : {&h->comm_rm, &h->comm_packed, &h->comm_gathered, &h->comm_small, &h->comm_status})
         if (b->p) {
             (void)hipFree(b->p);
@@ -339,8 +535,61 @@ extern "C" int pcg_comm_init(pcg_handle *h, const void *unique_id, int rank, int
         return pcg_fail(h, PCG_ERR_OOM, "pcg_comm_init: status buffers");
     }
     h->comm = comm;
+    h->comm_ops = &kRcclOps;
     h->comm_rank = rank;
     h->comm_world = world;
+    return PCG_OK;
+}
+
+extern "C" int pcg_comm_group_create(int world, double timeout_s, pcg_comm_group **out) {
+    if (!out || world < 1 || world > 4096) return PCG_ERR_INVALID;
+    pcg_comm_group *g = new pcg_comm_group();
+    g->world = world;
+    if (timeout_s > 0) g->timeout_s = timeout_s;
+    g->slot.resize((size_t)world);
+    g->tag.assign((size_t)world, 0);
+    g->member.assign((size_t)world, nullptr);
+    *out = g;
+    return PCG_OK;
+}
+
+extern "C" int pcg_comm_group_destroy(pcg_comm_group *g) {
+    if (!g) return PCG_OK;
+    {
+        std::lock_guard<std::mutex> lk(g->mu);
+        for (pcg_handle *m : g->member)
+            if (m) return PCG_ERR_INVALID;     // a handle still uses it: pcg_comm_destroy that first
+    }
+    delete g;
+    return PCG_OK;
+}
+
+extern "C" int pcg_comm_group_stats(pcg_comm_group *g, int64_t *collectives, int64_t *bytes, int32_t *broken) {
+    if (!g) return PCG_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (collectives) *collectives = g->collectives;
+    if (bytes) *bytes = g->bytes;
+    if (broken) *broken = g->broken ? 1 : 0;
+    return PCG_OK;
+}
+
+extern "C" int pcg_comm_init_group(pcg_handle *h, pcg_comm_group *g, int rank) {
+    if (!h || !g || rank < 0 || rank >= g->world)
+        return pcg_fail(h, PCG_ERR_INVALID, "pcg_comm_init_group: rank %d", rank);
+    pcg_comm_release(h);
+    PCG_HIP(h, hipSetDevice(h->device));
+    if (!pcg_ensure(h, h->comm_status, 64) ||
+        !pcg_ensure(h, h->comm_small, sizeof(int64_t) * (size_t)std::max(5 * PCG_MAX_LEVELS, g->world + 1)))
+        return pcg_fail(h, PCG_ERR_OOM, "pcg_comm_init_group: status buffers");
+    {
+        std::lock_guard<std::mutex> lk(g->mu);
+        if (g->member[rank]) return pcg_fail(h, PCG_ERR_INVALID, "pcg_comm_init_group: rank %d already joined", rank);
+        g->member[rank] = h;
+    }
+    h->comm = g;
+    h->comm_ops = &kGroupOps;
+    h->comm_rank = rank;
+    h->comm_world = g->world;
     return PCG_OK;
 }
 
@@ -381,8 +630,7 @@ extern "C" int pcg_corr_sharded(pcg_handle *h, const double *X, int64_t N, int64
     const int g = agree_value(h, local != 0, k1_plan_signature(h, n, N), &same);
     if (g) return agreed_failure(h, local, g, "sharded K1");
     if (!same) return pcg_fail(h, PCG_ERR_INVALID, "sharded K1: the ranks' K1 plans differ (PCG_K1_* environment)");
-    PCG_NCCL(h, rccl().all_gather(h->comm_packed.p, h->comm_gathered.p, per, ncclFloat64, (ncclComm_t)h->comm,
-                                  h->stream));
+    if (int rc2 = h->comm_ops->all_gather(h, h->comm_packed.p, h->comm_gathered.p, sizeof(double) * per)) return rc2;
     return pcg_corr_shard_finish(h, (const double *)h->comm_gathered.p, N, n, h->comm_world, C, ldc);
 }
 

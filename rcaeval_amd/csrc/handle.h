@@ -175,8 +175,10 @@ struct pcg_handle {
     hipStream_t aux = nullptr;
     hipEvent_t ev_join = nullptr;
 
-    // RCCL communicator of pcg_comm_init (comm.hip): one per (process, device)
+    // the native sharded driver's transport (comm.hip): an RCCL communicator (pcg_comm_init), or
+    // a pcg_comm_group of handles in this process (pcg_comm_init_group); comm_ops its collectives
     void *comm = nullptr;
+    const struct CommOps *comm_ops = nullptr;
     int comm_rank = 0, comm_world = 1;
     DevBuf comm_rm, comm_packed, comm_gathered, comm_small;
     DevBuf comm_status;   // agree(): one int32 all-reduced with MAX, allocated before the communicator

@@ -359,6 +359,76 @@ def native_comm(eng, group=None) -> None:
     eng.comm_init(bytes(buf.cpu().numpy().tobytes()), rank, world)
 
 
+class LocalGroup:
+    """An in-process group of ``world`` engine handles for the native driver
+    (``pcg_comm_group_create``): each rank is a handle driven from its own thread, and the
+    driver's collectives are host-staged between them. RCCL refuses two ranks on one device, so
+    this runs ``pcg_corr_sharded`` / ``pcg_skeleton_sharded`` — the C level loop bench.py uses at
+    N > 1 — with world 2..8 on one GPU. Every collective is checked to be the same on every rank;
+    a mismatch, a failing rank or a wait beyond ``timeout_s`` fails every rank with PCG_ERR_RCCL."""
+
+    def __init__(self, world: int, timeout_s: float = 300.0):
+        self.lib = _lib.load()
+        g = ctypes.c_void_p()
+        rc = self.lib.pcg_comm_group_create(int(world), float(timeout_s), ctypes.byref(g))
+        if rc != 0:
+            raise _lib.PcgError(rc, f"pcg_comm_group_create(world={world}) failed")
+        self.g, self.world = g, int(world)
+
+    def stats(self) -> dict:
+        c, b, br = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int32()
+        self.lib.pcg_comm_group_stats(self.g, ctypes.byref(c), ctypes.byref(b), ctypes.byref(br))
+        return {"collectives": c.value, "bytes": b.value, "broken": bool(br.value)}
+
+    def close(self):
+        if self.g:
+            rc = self.lib.pcg_comm_group_destroy(self.g)
+            if rc != 0:
+                raise _lib.PcgError(rc, "pcg_comm_group_destroy: a handle is still attached")
+            self.g = None
+
+
+def run_local_ranks(world: int, fn, device: int = 0, timeout_s: float = 300.0):
+    """Run ``fn(eng, rank, world)`` on ``world`` threads, each with its own engine handle on
+    ``device`` and its own torch stream, attached to one ``LocalGroup``. Returns the per-rank
+    results in rank order (the first exception is re-raised after every thread ended)."""
+    import threading
+
+    import torch
+
+    from .engine import Engine
+    group = LocalGroup(world, timeout_s)
+    out, errs = [None] * world, [None] * world
+
+    def body(r):
+        eng = None
+        try:
+            s = torch.cuda.Stream(device=device)
+            with torch.cuda.stream(s):
+                eng = Engine(device, stream=s)
+                eng.comm_init_group(group, r)
+                out[r] = fn(eng, r, world)
+                s.synchronize()
+        except BaseException as e:   # noqa: BLE001 - re-raised by the caller's thread
+            errs[r] = e
+        finally:
+            if eng is not None:
+                eng.comm_destroy()
+                eng.close()
+
+    threads = [threading.Thread(target=body, args=(r,), name=f"pcg-rank{r}") for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    stats = group.stats()
+    group.close()
+    for e in errs:
+        if e is not None:
+            raise e
+    return out, stats
+
+
 def native_sharded_corr(eng, X):
     """K1 sharded with the all-gather issued from C (needs ``native_comm`` first)."""
     return eng.corr_sharded(X)
@@ -372,5 +442,5 @@ def native_sharded_skeleton(eng, C, N: int, alpha: float = 0.05, max_depth: int 
 
 
 __all__ = ["agree", "agreed_backend", "split_by_work", "run_sharded_levels", "sharded_skeleton", "sharded_corr", "GpuLevelBackend",
-           "native_comm", "native_sharded_corr", "native_sharded_skeleton"]
+           "native_comm", "native_sharded_corr", "native_sharded_skeleton", "LocalGroup", "run_local_ranks"]
 _ = _lib

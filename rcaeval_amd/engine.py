@@ -80,7 +80,9 @@ class SkeletonOut:
 class Engine:
     """One handle on one HIP device."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, stream=None):
+        """``stream``: the torch stream the handle runs on (default: the current stream of
+        ``device`` in the calling thread)."""
         torch = _torch()
         if not torch.cuda.is_available():
             raise _lib.EngineUnavailable("no HIP device is visible (torch.cuda.is_available() is False)")
@@ -92,8 +94,9 @@ class Engine:
         if rc != 0:
             raise _lib.PcgError(rc, f"pcg_create(device={device}) failed")
         self.h = h
-        with torch.cuda.device(self.device):
-            stream = torch.cuda.current_stream(self.device)
+        if stream is None:
+            with torch.cuda.device(self.device):
+                stream = torch.cuda.current_stream(self.device)
         self.stream = stream
         check(self.h, self.lib.pcg_set_stream(self.h, ctypes.c_void_p(stream.cuda_stream)), "pcg_set_stream")
 
@@ -190,6 +193,15 @@ class Engine:
     def comm_init(self, unique_id: bytes, rank: int, world: int) -> None:
         buf = ctypes.create_string_buffer(bytes(unique_id), 128)
         check(self.h, self.lib.pcg_comm_init(self.h, buf, int(rank), int(world)), "pcg_comm_init")
+
+    def comm_init_group(self, group, rank: int) -> None:
+        """Attach this handle as ``rank`` of an in-process ``rcaeval_amd.dist.LocalGroup``
+        (pcg_comm_init_group): the native driver's collectives then run host-staged between the
+        group's handles, which other threads of this process drive."""
+        check(self.h, self.lib.pcg_comm_init_group(self.h, group.g, int(rank)), "pcg_comm_init_group")
+
+    def comm_destroy(self) -> None:
+        check(self.h, self.lib.pcg_comm_destroy(self.h), "pcg_comm_destroy")
 
     def corr_sharded(self, X):
         """K1 on the handle's communicator (pcg_corr_sharded): bitwise ``corr``."""

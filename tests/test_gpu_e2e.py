@@ -286,36 +286,45 @@ def _free_port():
     return p
 
 
-def _sharded_worker(rank, world, port, X, q):
+def _sharded_worker(rank, world, port, X, q, max_depth=3):
     import torch
     import torch.distributed as dist
-    from rcaeval_amd.dist import sharded_skeleton
+    from rcaeval_amd.dist import sharded_corr, sharded_skeleton
     from rcaeval_amd.engine import get_engine
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     eng = get_engine(0)
-    C = eng.corr(X)
-    out = sharded_skeleton(eng, C, X.shape[0], max_depth=3)
-    q.put((rank, out.removed_level.copy(), out.sep_xy.copy(), out.sep_bits.copy(), out.stats["tests"]))
+    C = sharded_corr(eng, eng.to_device(X)) if world > 2 else eng.corr(X)
+    out = sharded_skeleton(eng, C, X.shape[0], max_depth=max_depth)
+    q.put((rank, out.removed_level.copy(), out.sep_xy.copy(), out.sep_bits.copy(), out.stats["tests"],
+           [(int(r["a"]), int(r["b"])) for r in out.near_alpha]))
     dist.barrier()
     dist.destroy_process_group()
     torch.cuda.synchronize()
 
 
-def test_sharded_skeleton_two_ranks_one_gpu():
-    """The multi-GPU protocol with 2 ranks sharing cuda:0 (gloo all-reduce on device tensors)."""
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world,n,N,max_depth", [(2, 300, 3000, 3), (4, 700, 5000, 4), (8, 700, 5000, 5), (8, 300, 3000, -1)])
+def test_sharded_skeleton_ranks_one_gpu(world, n, N, max_depth):
+    """The torch.distributed driver (rcaeval_amd.dist, gloo on device tensors) with 2 / 4 / 8
+    ranks sharing cuda:0 (K1 sharded too at 4 and 8): every rank's removal depths, per-level
+    tests and sepset unions equal the single-GPU engine's and the C oracle's."""
     import multiprocessing as mp
+    from types import SimpleNamespace
+
+    from oracle import cpc
     from rcaeval_amd.engine import get_engine
-    X = synth.gaussian_sem(300, 3000, seed=12)
+    X = synth.gaussian_sem(n, N, seed=12)
     eng = get_engine(0)
-    ref = eng.skeleton(eng.corr(X), 3000, max_depth=3)
+    ref = eng.skeleton(eng.corr(X), N, max_depth=max_depth)
+    oref = cpc.skeleton(np.corrcoef(X.T), N, max_depth=max_depth, want_union=True)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_sharded_worker, args=(r, 2, port, X, q)) for r in range(2)]
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, X, q, max_depth)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=600) for _ in range(2)]
+    res = [q.get(timeout=500) for _ in range(world)]
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -325,10 +334,13 @@ def test_sharded_skeleton_two_ranks_one_gpu():
         for (x, y), b in zip(xy, bits):
             d[(int(x), int(y))] = d.get((int(x), int(y)), 0) | int.from_bytes(b.tobytes(), "little")
         return d
-    for rank, rl, xy, bits, tests in res:
+    for rank, rl, xy, bits, tests, near in res:
         np.testing.assert_array_equal(rl, ref.removed_level)
         assert unions(xy, bits) == unions(ref.sep_xy, ref.sep_bits)
         assert tests == ref.stats["tests"]
+        out = SimpleNamespace(removed_level=rl, sep_xy=xy, sep_bits=bits, stats={"tests": tests},
+                              near_alpha=[{"a": a, "b": b} for a, b in near])
+        assert_skeleton_matches(out, oref, n)
 
 
 def _config5_sharded_worker(rank, world, port, q):

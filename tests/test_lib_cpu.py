@@ -57,6 +57,21 @@ def test_integration_stub_matches_library_abi():
     assert [f[0] for f in ns["Stats"]._fields_] == [f[0] for f in _lib.PcgStats._fields_]
 
 
+def test_comm_group_lifecycle_host_only():
+    """The in-process transport's group object (pcg_comm_group_*) is host-only: create, stats,
+    destroy; bad arguments are refused; a NULL handle cannot join."""
+    from rcaeval_amd import _lib
+    from rcaeval_amd.dist import LocalGroup
+    lib = _lib.load()
+    g = ctypes.c_void_p()
+    assert lib.pcg_comm_group_create(0, 10.0, ctypes.byref(g)) == _lib.PCG_ERR_INVALID
+    grp = LocalGroup(4, timeout_s=5.0)
+    assert grp.stats() == {"collectives": 0, "bytes": 0, "broken": False}
+    assert lib.pcg_comm_init_group(None, grp.g, 0) == _lib.PCG_ERR_INVALID
+    grp.close()
+    assert grp.g is None
+
+
 def test_create_fails_loudly_without_gpu():
     import torch
     if torch.cuda.is_available():
