@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cerrno>
 #include <cstdlib>
 #include <cstring>
 
@@ -95,11 +96,23 @@ const TuneSpec kTune[PCG_TUNE_COUNT] = {
 };
 }  // namespace
 
+// read once, at pcg_create. A value pcg_set_tuning would refuse (not a whole base-0 integer, or
+// outside the knob's range) keeps the built-in default and is reported on stderr, so a typo in an
+// A/B knob never silently changes a plan or a launch shape
 void pcg_tuning_defaults(int64_t *tune) {
     for (int k = 0; k < PCG_TUNE_COUNT; ++k) {
         int64_t v = kTune[k].dflt;
-        if (const char *e = getenv(kTune[k].env)) v = strtoll(e, nullptr, 0);   // read once, at pcg_create
-        tune[k] = std::min(std::max(v, kTune[k].lo), kTune[k].hi);
+        if (const char *e = getenv(kTune[k].env)) {
+            char *end = nullptr;
+            errno = 0;
+            const long long p = strtoll(e, &end, 0);
+            if (end == e || *end != '\0' || errno == ERANGE || p < kTune[k].lo || p > kTune[k].hi)
+                fprintf(stderr, "pcgpu: ignoring %s=%s (not an integer in [%lld, %lld]); using %lld\n", kTune[k].env, e,
+                        (long long)kTune[k].lo, (long long)kTune[k].hi, (long long)kTune[k].dflt);
+            else
+                v = p;
+        }
+        tune[k] = v;
     }
 }
 

@@ -1091,6 +1091,8 @@ static bool crt_plan_build(const int64_t *tune, int n, int64_t N, CrtPlan &p) {
     p.TB = (int)((N + 63) / 64 * 2);
     // split-K: rounds of 256 resident blocks x k-blocks per slab (~0.3 us each) + the residue bytes
     // each unit writes and k_crt_finish reads (128 KB, ~0.026 us of chip bandwidth)
+    // a forced count (PCG_TUNE_K1_CRT_KS) that the k-block rounding cannot reach takes the nearest
+    // achievable count (it used to fall back to one slab silently)
     int best = 1;
     double best_cost = 1e300;
     const int force = (int)tune[PCG_TUNE_K1_CRT_KS];
@@ -1100,8 +1102,9 @@ static bool crt_plan_build(const int64_t *tune, int n, int64_t N, CrtPlan &p) {
         const int kse = (p.TB + kbk - 1) / kbk;
         if (kse != ks || kbk > CRT_MAXKB) continue;
         const int64_t U = (int64_t)p.ntiles * k * ks;
-        const double cost = (double)((U + 255) / 256) * kbk * 0.3 + (double)U * 0.026;
-        if (force > 0 ? ks == force : cost < best_cost) {
+        const double cost = force > 0 ? (double)std::abs(ks - force)
+                                      : (double)((U + 255) / 256) * kbk * 0.3 + (double)U * 0.026;
+        if (cost < best_cost) {
             best_cost = cost;
             best = ks;
         }

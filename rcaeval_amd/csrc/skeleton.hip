@@ -5621,6 +5621,16 @@ static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc,
             tail_queued = true;
         }
         if (!rc) rc = level_end_finish(h, depth, seq, nullptr);
+        if (rc && tail_queued) {
+            // the last depth failed after its tail kernel was queued (singular / domain / overflow):
+            // let that kernel finish writing the tail buffer before returning, and leave no export
+            // marked pending, so no later call reads a half-written tail or stale export state
+            const std::string err = h->err;
+            (void)tail_wait(h);
+            h->err = err;
+            h->xany = h->xinl = false;
+            h->xpending[0] = h->xpending[1] = false;
+        }
         if (rc) { h->lev_on = false; h->defer_near = false; h->run_max_depth = -1; h->stamps = false; return rc; }
         done = depth + 1;
     }

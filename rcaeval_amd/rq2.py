@@ -299,7 +299,7 @@ def run(dataset_dir: str, method: str, dataset: str, output: str = "output", len
     t0 = time.perf_counter()
     per_case = []
     if prefetch > 0 and len(mine) > 1:
-        # loaders (processes by default, or threads) read and window the next cases while this
+        # loaders (threads by default, or spawned processes) read and window the next cases while this
         # thread runs the current case on the GPU; cases are still processed, and their errors
         # raised, in the sorted order of the sequential loop
         from collections import deque

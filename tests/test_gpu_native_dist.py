@@ -1,5 +1,5 @@
 """GPU: the native multi-GPU driver (pcg_corr_sharded / pcg_skeleton_sharded — the C level loop
-bench.py runs at N > 1) at world 2, 3 and 8 on ONE device, through the in-process transport
+bench.py runs at N > 1) at world 2, 3, 4 and 8 on ONE device, through the in-process transport
 (pcg_comm_group_*: one handle per rank, each driven from its own thread and stream, host-staged
 collectives). RCCL refuses two ranks on one device (rccl.h ncclCommInitRank), so this is how the
 driver's rank-dependent steps run here: the per-depth pcg_level_split cut, the packed all-gather +
@@ -85,8 +85,8 @@ def test_native_driver_full_p_records_world3():
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_native_driver_config5_matches_oracle(config5, world):
     """North-star config 5 (2000 vars x 10 000 samples, depth 4) through the native C driver at
-    world 2 on one GPU: K1 sharded by CRT residue units (C bitwise numpy's to 2e-14 and identical
-    on both ranks), every depth's chunk list cut by pcg_level_split, the packed-bit barrier, the
+    world 2, 4 and 8 on one GPU: K1 sharded by CRT residue units (C bitwise numpy's to 2e-14 and
+    identical on every rank), every depth's chunk list cut by pcg_level_split, the packed-bit barrier, the
     counters summed and the sepset rows gathered in C. Each rank's skeleton equals the oracle's."""
     from rcaeval_amd.dist import run_local_ranks
     X, Ch, ref = config5

@@ -36,13 +36,15 @@ def main():
         return 1000.0 * (time.perf_counter() - t0) / reps
 
     res = {"n": n, "N": N, "corr_ms": t(lambda: eng.corr(Xd))}
-    for small in ("1", "0"):
-        os.environ["PCG_SMALL"] = small
-        res[f"skeleton_ms_small{small}"] = t(lambda: eng.skeleton(C, N))
-        res[f"corr_skeleton_ms_small{small}"] = t(lambda: eng.corr_skeleton(Xd))
-        res[f"pc_ms_small{small}"] = t(lambda: pc(X))
-        out = eng.skeleton(C, N)
+    for small in (1, 0):
+        # the knob is read once per handle (pcg_create): set it on the live handle
+        with eng.tuned(SMALL=small):
+            res[f"skeleton_ms_small{small}"] = t(lambda: eng.skeleton(C, N))
+            res[f"corr_skeleton_ms_small{small}"] = t(lambda: eng.corr_skeleton(Xd))
+            res[f"pc_ms_small{small}"] = t(lambda: pc(X))
+            out = eng.skeleton(C, N)
         res[f"levels_small{small}"] = out.stats["levels"]
+        res[f"driver_small{small}"] = out.stats["driver"]
         res[f"kernel_ms_small{small}"] = [round(v, 4) for v in out.stats["kernel_ms"]]
     print(res, flush=True)
 

@@ -22,14 +22,14 @@ C = np.corrcoef(X.T)
 ref = cpc.skeleton(C, 600, record_cap=1 << 16)
 d = keys(ref.records)
 print("ref levels", ref.levels, "tests", list(ref.tests), "records", len(d))
-for small in ["1", "0"]:
-    os.environ["PCG_SMALL"] = small
+for small in [1, 0]:
     for flags in (2, 3):
-        out = eng.skeleton(C, 600, flags=flags, record_capacity=1 << 16)
+        with eng.tuned(SMALL=small):      # the knob is read once per handle: set it on the handle
+            out = eng.skeleton(C, 600, flags=flags, record_capacity=1 << 16)
         g = keys(out.records)
         byd = collections.Counter(len(k[2]) for k in g)
         byr = collections.Counter(len(k[2]) for k in d)
-        print("PCG_SMALL", small, "flags", flags, "levels", out.levels, "tests", out.stats["tests"], "records", len(g),
+        print("SMALL", small, "driver", out.stats["driver"], "flags", flags, "levels", out.levels, "tests", out.stats["tests"], "records", len(g),
               "skeleton equal", bool(np.array_equal(out.removed_level, ref.removed_level)))
         print("   per depth gpu", sorted(byd.items()), "ref", sorted(byr.items()))
         print("   only ref", sorted(set(d) - set(g))[:8])
