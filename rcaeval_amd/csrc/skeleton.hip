@@ -2259,6 +2259,10 @@ __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_
 // decides it like the fp64 kernels (band -> exact path). Decisions are therefore the fp64
 // kernels' decisions; only where the fp32 sweep is certain does it decide.
 typedef float f2v __attribute__((ext_vector_type(2)));
+struct alignas(16) YRecN {       // k_level_lds_f (narrow): a y's {A~_yy, A~_xy} and local adjacency mask
+    f2v md;
+    unsigned long long lm;
+};
 constexpr double F32_U = 5.9604644775390625e-08;   // 2^-24
 #ifndef PCG_F32_KE
 #define PCG_F32_KE 64.0
@@ -2403,8 +2407,11 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
     Mask *uself = lmask + DS;                                     // DS
     Mask *uprop = uself + DS;                                     // DS
     float *M = reinterpret_cast<float *>(uprop + DS);             // D * DS (columns >= D zero)
-    float *Mdx = M + D * DS;                                      // 2 DS: {A~_yy, A~_xy} per y
-    int32_t *nxs = reinterpret_cast<int32_t *>(Mdx + 2 * DS);    // DS
+    // one 16-byte (wide: 32-byte) record per y: {A~_yy, A~_xy, [pad,] local adjacency mask}, so the
+    // sweep reads a y's wave-uniform operands with one LDS instruction
+    constexpr int YS = WIDE ? 8 : 4;                              // floats per record
+    float *Yr = M + D * DS;                                       // DS records, 16-B aligned
+    int32_t *nxs = reinterpret_cast<int32_t *>(Yr + YS * DS);    // DS
     int *s_tx = nxs + DS;                                         // 1
     int *s_np = s_tx + 1;                                         // 1
     unsigned *btab = reinterpret_cast<unsigned *>(smem + a.lds_btab_off);   // C(c, i), c <= D, i <= DM
@@ -2436,7 +2443,10 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
                 if (lane < DS) M[t * DS + lane] = (float)v[r];
             }
         }
-        for (int t = tid; t < D; t += bs) lmask[t] = (Mask)lk[t];
+        for (int t = tid; t < D; t += bs) {
+            lmask[t] = (Mask)lk[t];
+            *reinterpret_cast<Mask *>(Yr + YS * t + (WIDE ? 4 : 2)) = (Mask)lk[t];
+        }
     } else if constexpr (WIDE) {   // (the row-batched form below measured slower for the 128-wide blocks)
         for (int e = tid; e < D * DS; e += bs) {
             const int t = e / DS, k = e - t * DS;
@@ -2450,7 +2460,10 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
                 const bool bit = k < D && ((ar[nxs[k] >> 6] >> (nxs[k] & 63)) & 1ull);
                 m |= (Mask)__ballot(bit) << k0;
             }
-            if ((tid & 63) == 0) lmask[t] = m;
+            if ((tid & 63) == 0) {
+                lmask[t] = m;
+                *reinterpret_cast<Mask *>(Yr + YS * t + (WIDE ? 4 : 2)) = m;
+            }
         }
     } else {   // rows of A~ and of the local adjacency masks: a wave takes SR rows at a time, lane k
         // column k (its global id hoisted), so SR x (C entry, adjacency word) loads are in flight
@@ -2486,14 +2499,17 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
                     const bool bit = kg[hh] >= 0 && ((w[r][hh] >> (kg[hh] & 63)) & 1ull);
                     m |= (Mask)__ballot(bit) << (64 * hh);
                 }
-                if (lane == 0) lmask[t] = m;
+                if (lane == 0) {
+                    lmask[t] = m;
+                    *reinterpret_cast<Mask *>(Yr + YS * t + (WIDE ? 4 : 2)) = m;
+                }
             }
         }
     }
     for (int t = tid; t < D; t += bs) {
         const int yg = nxs[t];
-        Mdx[2 * t] = (float)a.diag[yg];
-        Mdx[2 * t + 1] = (float)a.C[(int64_t)x * a.ldc + yg];
+        Yr[YS * t] = (float)a.diag[yg];
+        Yr[YS * t + 1] = (float)a.C[(int64_t)x * a.ldc + yg];
         uself[t] = 0;
         uprop[t] = 0;
     }
@@ -2611,7 +2627,7 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
             double t = 0.0;
 #pragma unroll
             for (int j = 0; j <= i; ++j) {
-                t += Li[i][j] * (double)Mdx[2 * T[j] + 1];
+                t += Li[i][j] * (double)Yr[YS * T[j] + 1];
                 liF += Li[i][j] * Li[i][j];
             }
             uT[i] = t;
@@ -2666,7 +2682,7 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
                     }
                     const double lam2 = (double)M[cc * DS + cc] - ll;
                     const double r = rsq_nr(lam2);
-                    const double u = ((double)Mdx[2 * cc + 1] - lu) * r;
+                    const double u = ((double)Yr[YS * cc + 1] - lu) * r;
                     const double cxx = cx0 - u * u;
 #pragma unroll
                     for (int i = 0; i < DT; ++i) lcp[q][i][h] = (float)lc[i];
@@ -2736,6 +2752,11 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
 #pragma unroll
         for (int jj = 0; jj < TG; ++jj) okv[jj] = __builtin_amdgcn_ballot_w64(okc[jj]);
         const unsigned long long notok = __builtin_amdgcn_ballot_w64((vmask & ~okm) != 0u);
+        // LDS byte offsets of the lane's candidate window and T columns within a row of A~
+        const unsigned cofs = (unsigned)cbase * 4u;
+        unsigned tofs[DT];
+#pragma unroll
+        for (int j = 0; j < DT; ++j) tofs[j] = (unsigned)T[j] * 4u;
         const int cb0 = __builtin_amdgcn_readfirstlane(cbase);
         const bool uni = __builtin_amdgcn_ballot_w64(cbase != cb0) == 0ull;
 #if PCG_TGF_PROF
@@ -2814,13 +2835,21 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
             };
             auto yload = [&](int t) {
                 YPre p;
-                const float *Mt = M + t * DS;
+                // byte addresses: the row's (wave-uniform) base plus each lane's hoisted column
+                // offsets (one v_add per operand instead of a shift-and-add of the column index)
+                const char *Mb = reinterpret_cast<const char *>(M) + (unsigned)(t * DS) * 4u;
 #pragma unroll
-                for (int q = 0; q < NQ; ++q) p.sc[q] = *reinterpret_cast<const f2v *>(Mt + cbase + 2 * q);
+                for (int q = 0; q < NQ; ++q) p.sc[q] = *reinterpret_cast<const f2v *>(Mb + cofs + 8u * q);
 #pragma unroll
-                for (int j = 0; j < DT; ++j) p.mT[j] = Mt[T[j]];
-                p.md = *reinterpret_cast<const f2v *>(Mdx + 2 * t);
-                p.lm = lmask[t];
+                for (int j = 0; j < DT; ++j) p.mT[j] = *reinterpret_cast<const float *>(Mb + tofs[j]);
+                if constexpr (!WIDE) {   // the y record in one 16-byte read
+                    const YRecN r = *reinterpret_cast<const YRecN *>(Yr + 4 * t);
+                    p.md = r.md;
+                    p.lm = r.lm;
+                } else {
+                    p.md = *reinterpret_cast<const f2v *>(Yr + YS * t);
+                    p.lm = *reinterpret_cast<const Mask *>(Yr + YS * t + 4);
+                }
                 return p;
             };
             auto ystep = [&](int t, auto ym_tag, const YPre &pre) {
@@ -2832,8 +2861,11 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
                 float vT[DT], mT[DT];
 #pragma unroll
                 for (int j = 0; j < DT; ++j) mT[j] = pre.mT[j];
-                // (|v_T|^2, u_T.v_T) accumulated as one packed pair: vu[i] = {v_i, u_i}
-                f2v acc = {0.0f, 0.0f};
+                // (|v_T|^2, u_T.v_T) accumulated as one packed pair (vu[i] = {v_i, u_i}) onto
+                // -{A~_yy, A~_xy}: acc = -{b_yy, b_xy} with no separate subtraction (three roundings
+                // of partial sums <= 2 in magnitude instead of k <= 1 plus one: the b_yy / b_xy error
+                // terms grow by 2u, inside DESIGN §4.1's 14 u (1 + nu)^2 and 9 u (1 + nu)^2)
+                f2v acc = -pre.md;
                 if constexpr (PCG_TGF_PKV && DT == 3) {
                     // v_1 and v_2 as one packed chain (the same roundings in the same order as the
                     // scalar chains: L_i0 m_0, + L_i1 m_1, + L_i2 m_2)
@@ -2862,9 +2894,8 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
                     const f2v vu = {vT[i], uTf[i]}, vb = {vT[i], vT[i]};
                     acc = __builtin_elementwise_fma(vu, vb, acc);
                 }
-                const f2v b2 = pre.md - acc;   // {byy, bxy}
-                const float byy = b2[0];
-                const float bxy = b2[1];
+                const float byy = -acc[0];
+                const float bxy = -acc[1];
 #pragma unroll
                 for (int i = 0; i < DT; ++i) {
                     const f2v vb = {vT[i], vT[i]};
@@ -4498,10 +4529,11 @@ size_t lds_tgroup_bytes(int D, int DM, int mask_bytes = 8) {
     const size_t np = (size_t)tg_pairs(D, DM);
     return lds_small_core(D, mask_bytes) + (size_t)(D + 1) * (DM + 1) * 4 + (np + 1) * 4 + np * 2 + 16;
 }
-// k_level_lds_f (D padded to 4): three mask arrays, fp32 M, Mx, Md, nxs, two ints; then the
+// k_level_lds_f (D padded to 4): three mask arrays, fp32 M, the y records, nxs, two ints; then the
 // same binomial table and task prefix as k_level_lds_t
 size_t lds_f32_core(int D, int mask_bytes) {
-    return ((size_t)D * 3 * mask_bytes + (size_t)D * D * 4 + (size_t)D * 3 * 4 + 8 + 15) & ~(size_t)15;
+    // (y records: 16 B per y with 8-byte masks, 32 B with 16-byte ones; nxs 4 B)
+    return ((size_t)D * 3 * mask_bytes + (size_t)D * D * 4 + (size_t)D * (2 * mask_bytes + 4) + 8 + 15) & ~(size_t)15;
 }
 size_t lds_tgroup_f_bytes(int D, int DM, int mask_bytes) {
     const size_t np = (size_t)tg_pairs(D, DM);

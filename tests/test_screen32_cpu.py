@@ -111,8 +111,13 @@ def _sweep(Cb, N):
     Lif, uTf, lcf, rlf, ucf = Li.astype(f), uT.astype(f), lc.astype(f), r.astype(f), u.astype(f)
     mT = A[:, Ti, Y].astype(f)
     vT = np.einsum("bij,bj->bi", Lif, mT).astype(f)
-    byy = (A[:, Y, Y].astype(f) - (vT * vT).sum(1, dtype=f)).astype(f)
-    bxy = (A[:, X, Y].astype(f) - (uTf * vT).sum(1, dtype=f)).astype(f)
+    # the kernel accumulates onto -{A~_yy, A~_xy} (acc = -b after the k products, no separate
+    # subtraction): the same order here, one rounding per step
+    ay_, ax_ = -A[:, Y, Y].astype(f), -A[:, X, Y].astype(f)
+    for i in range(vT.shape[1]):
+        ay_ = (ay_ + vT[:, i] * vT[:, i]).astype(f)
+        ax_ = (ax_ + uTf[:, i] * vT[:, i]).astype(f)
+    byy, bxy = -ay_, -ax_
     sc = (A[:, Cc, Y].astype(f) - (lcf * vT).sum(1, dtype=f)).astype(f)
     vc = (sc * rlf).astype(f)
     cyy = (byy - vc * vc).astype(f)

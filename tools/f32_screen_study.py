@@ -92,10 +92,12 @@ def main():
         Lif, uTf, lcf, rlf, ucf = (a.astype(f) for a in (Li, uT, lc, rl, uc))
         mT = Cm[gT, gy[:, None]].astype(f)
         vT = np.einsum("bij,bj->bi", Lif, mT).astype(f)
-        vv = (vT * vT).sum(1, dtype=f)
-        uv = (uTf * vT).sum(1, dtype=f)
-        byy = (Cm[gy, gy].astype(f) - vv).astype(f)
-        bxy = (Cm[gx, gy].astype(f) - uv).astype(f)
+        # the kernel's order: the k products accumulated onto -{A~_yy, A~_xy}
+        ay_, ax_ = -Cm[gy, gy].astype(f), -Cm[gx, gy].astype(f)
+        for i in range(vT.shape[1]):
+            ay_ = (ay_ + vT[:, i] * vT[:, i]).astype(f)
+            ax_ = (ax_ + uTf[:, i] * vT[:, i]).astype(f)
+        byy, bxy = -ay_, -ax_
         sc = (Cm[gc, gy].astype(f) - (lcf * vT).sum(1, dtype=f)).astype(f)
         vc = (sc * rlf).astype(f)
         cyy = (byy - vc * vc).astype(f)

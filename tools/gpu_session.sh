@@ -24,6 +24,12 @@ for step in "$@"; do
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     dist2) PCG_DIST_TRACE=1 PCG_BENCH_DEVICE=0 PCG_DIST_BACKEND=gloo run dist2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 2 --warmup 1 ;;
     sim) run sim 600 python tools/shard_sim.py ;;
+    quick) run quick 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-full-p ;;
+    # the sharded drivers at world 1 (their fixed overhead over the single-GPU call): native C / RCCL, torch.distributed
+    dist1n) PCG_BENCH_FORCE_DIST=1 run dist1n 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29512 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-full-p ;;
+    dist1t) PCG_BENCH_FORCE_DIST=1 PCG_DIST_NATIVE=0 run dist1t 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29513 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-full-p ;;
+    k:*) run "pytest_${step#k:}" 900 python -u -m pytest tests -m gpu -v -x --timeout 600 --timeout-method thread -p no:cacheprovider -k "${step#k:}" ;;
+    htrace) PCG_HOST_TRACE=1 run htrace 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-full-p ;;
     *) echo "unknown step $step" ;;
   esac
 done
