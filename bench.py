@@ -452,10 +452,19 @@ def main():
         torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MIN)
         native = bool(flag.item())
 
+    k1_events = []
+
     def one_step():
         t0 = time.perf_counter()
         if native:
+            # stream-ordered, no host sync between K1 and the skeleton; K1's time from events on
+            # the handle's stream, read after the step
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record(eng.stream)
             C = eng.corr_sharded(Xd)
+            ev[1].record(eng.stream)
+            k1_events.append(ev)
+            return eng.skeleton_sharded(C, args.samples, alpha=args.alpha, max_depth=args.max_depth, flags=flags)
         elif dist_path:
             from rcaeval_amd.dist import sharded_corr
             C = sharded_corr(eng, Xd)
@@ -463,8 +472,6 @@ def main():
             return eng.corr_skeleton(Xd, alpha=args.alpha, max_depth=args.max_depth, flags=flags)[0]
         torch.cuda.synchronize()
         phases.append(("corr", time.perf_counter() - t0))
-        if native:
-            return eng.skeleton_sharded(C, args.samples, alpha=args.alpha, max_depth=args.max_depth, flags=flags)
         if dist_path:
             from rcaeval_amd.dist import sharded_skeleton
             trace = [] if os.environ.get("PCG_DIST_TRACE") else None
@@ -525,6 +532,11 @@ def main():
             torch.cuda.synchronize()
             phases.append(("corr", time.perf_counter() - t0))
         corr_med = float(np.median([1000 * t for n_, t in phases if n_ == "corr"][1:]))
+    elif native:
+        torch.cuda.synchronize()
+        for e0, e1 in k1_events:
+            phases.append(("corr", e0.elapsed_time(e1) / 1000.0))
+        corr_med = float(np.median([1000 * t for n_, t in phases if n_ == "corr"][args.warmup:] or [0.0]))
     else:
         corr_med = float(np.median([1000 * t for n_, t in phases if n_ == "corr"][args.warmup:] or [0.0]))
     k1_tune = {k: eng.get_tuning(k) for k in ("K1_I8", "K1_CRT", "K1_CRT_MINN", "K1_CRT_BITS")}

@@ -216,6 +216,17 @@ int pcg_sepset_export(pcg_handle *h, int32_t *xy_host /* 2*count */,
                       uint64_t *bits_host /* count*W */, int64_t count);
 /* Same, into caller-owned device buffers (stream-ordered copy, no host round trip).     */
 int pcg_sepset_export_device(pcg_handle *h, int32_t *xy_dev, uint64_t *bits_dev, int64_t count);
+/* Export the sepset rows of the following one-GPU pcg_skeleton / pcg_pc_skeleton / level-step
+ * runs straight into caller-owned device buffers (xy: 2 x capacity int32, bits: capacity x W
+ * uint64, W = ceil(n / 64)) whenever they hold the run's row bound — the ordered pairs entering
+ * depth 1 — so no copy follows the call. NULL / 0 restores the handle's own buffers. The buffers
+ * must stay valid until the run's result has been read.
+ * pcg_sepset_target after a run: *in_caller = 1 when the rows are in the caller's buffers (rows
+ * 0 .. count - 1 of pcg_sepset_count), 0 when they are in the handle's own (copy them with
+ * pcg_sepset_export_device, which skips a copy onto itself); *capacity_needed = the run's row
+ * bound, the capacity that would have held them.                                          */
+int pcg_set_sepset_buffers(pcg_handle *h, int32_t *xy_dev, uint64_t *bits_dev, int64_t capacity);
+int pcg_sepset_target(pcg_handle *h, int32_t *in_caller, int64_t *capacity_needed);
 
 /* Records of the last pcg_skeleton (PCG_FLAG_RECORD) and the near-alpha list.         */
 int pcg_record_count(pcg_handle *h, int64_t *count, int64_t *near_alpha_count);
@@ -323,16 +334,23 @@ int pcg_comm_group_create(int world, double timeout_s, pcg_comm_group **out);
 int pcg_comm_group_destroy(pcg_comm_group *g);
 int pcg_comm_group_stats(pcg_comm_group *g, int64_t *collectives, int64_t *bytes, int32_t *broken);
 int pcg_comm_init_group(pcg_handle *h, pcg_comm_group *g, int rank);
-/* K1 on the communicator: pcg_corr_shard + RCCL all-gather + pcg_corr_shard_finish; C is
- * bitwise the single-GPU pcg_corr result on every rank.                                   */
+/* K1 on the communicator: this rank's share (pcg_corr_shard's units; on the CRT path only the
+ * residue planes of the moduli its units use) + all-gather + rebuild; C is bitwise the
+ * single-GPU pcg_corr result on every rank. On the CRT path (n >= 256) the call returns once
+ * its work is queued on the handle's stream (stream-ordered, no host sync); the set-up (buffers,
+ * the ranks' K1 plan signatures) is agreed across ranks on the first call of an (n, N, world,
+ * plan) and whenever a buffer grows, so K1 knobs must change on every rank or on none.       */
 int pcg_corr_sharded(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx,
                      double *C, int64_t ldc);
-/* The edge-sharded stable skeleton on the communicator: per depth begin / split / run on
+/* The edge-sharded stable skeleton on the communicator (the level loop of pcg_skeleton, with its
+ * device-clock depth stamps and tail kernel): per depth begin / split / run on
  * this rank's work-balanced chunk range / pack / RCCL all-gather of the packed removal bits
  * and status word / merge / end (a rank that fails locally still joins the all-gather, and
  * its peers return PCG_ERR_PEER at the same depth); then the per-level counters are summed over ranks and every rank's
  * sepset rows are all-gathered, so pcg_sepset_* and removed_level describe the whole
- * skeleton on every rank (a pair's row may appear once per rank that saw it: OR them).
+ * skeleton on every rank (a pair's row may appear once per rank that saw it: OR them) — the
+ * counters and row counts in one all-gather, the rows in a second. The set-up is agreed across
+ * ranks on the first call of an (n, world) and whenever a buffer grows.
  * Same arguments and results as pcg_skeleton.                                              */
 int pcg_skeleton_sharded(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N,
                          double alpha, int max_depth, int flags, int8_t *removed_level,

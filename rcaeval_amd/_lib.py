@@ -118,6 +118,8 @@ SIGNATURES = [
     ("pcg_sepset_count", I32, [P, ctypes.POINTER(I64), ctypes.POINTER(I32)]),
     ("pcg_sepset_export", I32, [P, P, P, I64]),
     ("pcg_sepset_export_device", I32, [P, P, P, I64]),
+    ("pcg_set_sepset_buffers", I32, [P, P, P, I64]),
+    ("pcg_sepset_target", I32, [P, ctypes.POINTER(I32), ctypes.POINTER(I64)]),
     ("pcg_record_count", I32, [P, ctypes.POINTER(I64), ctypes.POINTER(I64)]),
     ("pcg_record_export", I32, [P, P, I64, P, I64]),
     ("pcg_skeleton_init", I32, [P, P, I64, I64, I64, D, ctypes.c_int, P]),

@@ -30,6 +30,7 @@ bool pcg_ensure(pcg_handle *h, DevBuf &b, size_t bytes) {
         b.bytes = 0;
     }
     const size_t want = bytes + bytes / 8;  // headroom for the next level / call
+    ++h->alloc_events;
     if (hipMalloc(&b.p, want) != hipSuccess) {
         b.p = nullptr;
         return false;
@@ -48,6 +49,7 @@ bool pcg_ensure_pinned(pcg_handle *h, PinBuf &b, size_t bytes) {
         b.dp = nullptr;
         b.bytes = 0;
     }
+    ++h->alloc_events;
     if (hipHostMalloc(&b.p, bytes, hipHostMallocMapped) != hipSuccess) {   // device-readable (k_copy_i64)
         b.p = nullptr;
         return false;

@@ -262,6 +262,9 @@ void group_release(pcg_handle *h) {
 
 const CommOps kGroupOps = {"group", group_all_gather, group_all_reduce, group_release};
 
+// agree()'s int64 scratch and finish_sharded's gather: (world + 1) x (5 PCG_MAX_LEVELS + 1) int64
+size_t comm_small_bytes(int world) { return sizeof(int64_t) * (size_t)(world + 1) * (5 * PCG_MAX_LEVELS + 1); }
+
 int need_comm(pcg_handle *h) {
     if (!h) return PCG_ERR_INVALID;
     if (!h->comm || !h->comm_ops)
@@ -321,18 +324,16 @@ __global__ void k_pack_rows(const int32_t *xy, const uint64_t *bits, int64_t row
     out[e] = v;
 }
 
-__global__ void k_unpack_rows(const int64_t *in, int64_t rows, int W, int32_t *xy, uint64_t *bits) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= rows * (W + 1)) return;
-    const int64_t r = e / (W + 1);
-    const int c = (int)(e - r * (W + 1));
-    const int64_t v = in[e];
-    if (c == 0) {
-        xy[2 * r] = (int32_t)(uint32_t)(v & 0xffffffffll);
-        xy[2 * r + 1] = (int32_t)(uint32_t)((uint64_t)v >> 32);
-    } else {
-        bits[r * W + (c - 1)] = (uint64_t)v;
-    }
+// buffers a failed agreement leaves behind are released on EVERY rank, so the ranks' grow-only
+// buffers stay equal and the next call's "did anything allocate" decision agrees again
+void release_agreed(pcg_handle *h, std::initializer_list<DevBuf *> bufs) {
+    (void)hipStreamSynchronize(h->stream);
+    for (DevBuf *b : bufs)
+        if (b->p) {
+            (void)hipFree(b->p);
+            b->p = nullptr;
+            b->bytes = 0;
+        }
 }
 
 int sharded_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N, double alpha,
@@ -340,7 +341,12 @@ int sharded_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t
     int64_t P = 0;
     if (pcg_level_packed_words(n, &P)) return pcg_fail(h, PCG_ERR_INVALID, "n = %lld", (long long)n);
     const int world = h->comm_world;
-    // set-up (buffers, skeleton init) agreed by every rank before the first level collective
+    // set-up (buffers, skeleton init). It is agreed by every rank before the first level collective
+    // when it allocated anything or is the first of its (n, world) on this communicator; otherwise
+    // nothing in it can fail on one rank only (grow-only buffers already sized, arguments equal on
+    // every rank), and the host round trip of the agreement is skipped
+    const uint64_t a0 = h->alloc_events;
+    level_run_begin(h, max_depth);
     int local = PCG_OK;
     if (!pcg_ensure(h, h->comm_packed, sizeof(uint64_t) * (size_t)P) ||
         !pcg_ensure(h, h->comm_gathered, sizeof(uint64_t) * (size_t)P * world))
@@ -356,16 +362,26 @@ int sharded_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t
         if (!pcg_ensure(h, h->off2[t], sizeof(int32_t) * (size_t)(n + 1)) ||
             !pcg_ensure(h, h->nbr2[t], sizeof(int32_t) * (size_t)std::max<int64_t>(n * (n - 1), 1)))
             local = pcg_fail(h, PCG_ERR_OOM, "neighbour lists");
-    int g = agree(h, local != 0);
-    if (g) {
-        pcg_set_world_size(h, 1);
-        return agreed_failure(h, local, g, "skeleton set-up");
+    if (local || h->alloc_events != a0 || h->sk_agreed[0] != n || h->sk_agreed[1] != world) {
+        const int g = agree(h, local != 0);
+        if (g) {
+            level_run_abort(h, false);
+            pcg_set_world_size(h, 1);
+            h->sk_agreed[0] = h->sk_agreed[1] = -1;
+            release_agreed(h, {&h->comm_packed, &h->comm_gathered});
+            return agreed_failure(h, local, g, "skeleton set-up");
+        }
+        h->sk_agreed[0] = n;
+        h->sk_agreed[1] = world;
     }
-    int rc = PCG_OK;
+    PCG_HT(h, "init:done");
+    int rc = PCG_OK, done = 0;
+    bool tail_queued = false;
     uint64_t *packed = (uint64_t *)h->comm_packed.p, *gathered = (uint64_t *)h->comm_gathered.p;
     for (int depth = 0; !rc; ++depth) {
         if (max_depth >= 0 && depth > max_depth) break;
         int64_t total = 0, lo = 0, hi = 0;
+        PCG_HT(h, "loop:begin");
         // begin is deterministic over the replicated adjacency ("done" agrees on every rank);
         // a local failure of begin / split / run still joins the all-gather below, flagged in
         // the status word, so no peer waits in the collective for this rank
@@ -396,96 +412,126 @@ int sharded_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t
             rc = local;
             break;
         }
-        rc = pcg_level_end(h, nullptr);
+        unsigned long long seq = 0;
+        rc = level_end_enqueue(h, &seq);
+        if (!rc && level_run_tail_early(h, depth)) {
+            rc = level_run_tail_launch(h);
+            tail_queued = true;
+        }
+        if (!rc) rc = level_end_finish(h, depth, seq, nullptr);
+        if (!rc) done = depth + 1;
     }
+    if (rc) level_run_abort(h, tail_queued);
+    else rc = level_run_finish(h, done, tail_queued);
     pcg_set_world_size(h, 1);
     return rc;
 }
 
-// per-depth counters summed over ranks (replicated quantities — calls, degrees, edges — are
-// identical on every rank already). Its only early returns are HIP copy / sync errors, i.e. a
-// faulted device, after which no collective on this communicator can complete anyway.
-int reduce_stats(pcg_handle *h) {
-    const int L = h->st.levels;
-    if (L <= 0) return PCG_OK;
-    std::vector<int64_t> v((size_t)5 * L);
-    for (int d = 0; d < L; ++d) {
-        v[d] = h->st.tests[d];
-        v[L + d] = h->st.indep[d];
-        v[2 * L + d] = h->st.exact[d];
-        v[3 * L + d] = h->st.near_alpha[d];
-        v[4 * L + d] = h->st.screened[d];
+// The end of a sharded run, in one collective + one host sync: every rank contributes its
+// per-depth counters (tests, indep, exact, near-alpha, screened: summed over ranks; replicated
+// quantities — calls, degrees, edges — are identical everywhere already) and its exported row
+// count (-1 marks a rank that failed to take it) in one all-gather; then the rows themselves,
+// packed [x | y << 32, W union words] and zero-padded to the longest rank, in a second all-gather
+// and one unpack launch. The row buffers grow-only; their growth (the same decision on every rank:
+// all see the same counts) is agreed only when it happens. The rows land stream-ordered in the
+// handle's export buffers.
+__global__ void k_unpack_all(const int64_t *in, const int64_t *cnt_pre, int world, int64_t per_rows, int W,
+                             int32_t *xy, uint64_t *bits) {
+    const int64_t total = cnt_pre[world];
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= total * (W + 1)) return;
+    const int64_t row = e / (W + 1);
+    const int c = (int)(e - row * (W + 1));
+    int r = 0;
+    while (r + 1 < world && cnt_pre[r + 1] <= row) ++r;       // the rank whose rows hold `row`
+    const int64_t v = in[((int64_t)r * per_rows + (row - cnt_pre[r])) * (W + 1) + c];
+    if (c == 0) {
+        xy[2 * row] = (int32_t)(uint32_t)(v & 0xffffffffll);
+        xy[2 * row + 1] = (int32_t)(uint32_t)((uint64_t)v >> 32);
+    } else {
+        bits[row * W + (c - 1)] = (uint64_t)v;
     }
-    // comm_small holds 5 * PCG_MAX_LEVELS int64 since pcg_comm_init: no allocation between collectives
-    PCG_HIP(h, hipMemcpyAsync(h->comm_small.p, v.data(), sizeof(int64_t) * v.size(), hipMemcpyHostToDevice,
-                              h->stream));
-    if (int rc = h->comm_ops->all_reduce(h, h->comm_small.p, v.size(), COMM_I64, COMM_SUM)) return rc;
-    PCG_HIP(h, hipMemcpyAsync(v.data(), h->comm_small.p, sizeof(int64_t) * v.size(), hipMemcpyDeviceToHost,
-                              h->stream));
-    PCG_HIP(h, hipStreamSynchronize(h->stream));
-    for (int d = 0; d < L; ++d) {
-        h->st.tests[d] = v[d];
-        h->st.indep[d] = v[L + d];
-        h->st.exact[d] = v[2 * L + d];
-        h->st.near_alpha[d] = v[3 * L + d];
-        h->st.screened[d] = v[4 * L + d];
-    }
-    return PCG_OK;
 }
 
-// every rank's exported sepset rows -> the handle's export buffers on every rank. The row
-// counts travel with a failure marker (-1), and the row-buffer sizes are agreed before the rows
-// move, so a rank that fails here takes its peers out of the gather with it.
-int gather_sepsets(pcg_handle *h) {
+int finish_sharded(pcg_handle *h) {
     const int world = h->comm_world, W = h->W;
+    const int L = h->st.levels;
     int local = export_sync(h);
     const std::string sync_err = local ? h->err : std::string();
-    int64_t *cnt_d = (int64_t *)h->comm_small.p;
-    const int64_t mine = local ? -1 : h->export_rows;
-    PCG_HIP(h, hipMemcpyAsync(cnt_d + world, &mine, sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
-    if (int rc = h->comm_ops->all_gather(h, cnt_d + world, cnt_d, sizeof(int64_t))) return rc;
-    std::vector<int64_t> cnt(world);
-    PCG_HIP(h, hipMemcpyAsync(cnt.data(), cnt_d, sizeof(int64_t) * world, hipMemcpyDeviceToHost, h->stream));
+    // [5 L counters, row count] per rank
+    const int per = 5 * PCG_MAX_LEVELS + 1;
+    std::vector<int64_t> mine((size_t)per, 0), all((size_t)per * world);
+    for (int d = 0; d < L && d < PCG_MAX_LEVELS; ++d) {
+        mine[d] = h->st.tests[d];
+        mine[PCG_MAX_LEVELS + d] = h->st.indep[d];
+        mine[2 * PCG_MAX_LEVELS + d] = h->st.exact[d];
+        mine[3 * PCG_MAX_LEVELS + d] = h->st.near_alpha[d];
+        mine[4 * PCG_MAX_LEVELS + d] = h->st.screened[d];
+    }
+    mine[per - 1] = local ? -1 : h->export_rows;
+    // comm_small holds (world + 1) * per int64 since pcg_comm_init: no allocation between collectives
+    int64_t *sd = (int64_t *)h->comm_small.p;
+    PCG_HIP(h, hipMemcpyAsync(sd + (size_t)per * world, mine.data(), sizeof(int64_t) * per, hipMemcpyHostToDevice,
+                              h->stream));
+    if (int rc = h->comm_ops->all_gather(h, sd + (size_t)per * world, sd, sizeof(int64_t) * per)) return rc;
+    PCG_HIP(h, hipMemcpyAsync(all.data(), sd, sizeof(int64_t) * all.size(), hipMemcpyDeviceToHost, h->stream));
     PCG_HIP(h, hipStreamSynchronize(h->stream));
-    int64_t mx = 1, total = 0;
+    std::vector<int64_t> cnt(world), pre(world + 1, 0);
     bool peer_failed = false;
-    for (int64_t c : cnt) {
-        peer_failed = peer_failed || c < 0;
-        mx = std::max(mx, c);
-        total += std::max<int64_t>(c, 0);
+    int64_t mx = 1;
+    for (int r = 0; r < world; ++r) {
+        cnt[r] = all[(size_t)r * per + per - 1];
+        peer_failed = peer_failed || cnt[r] < 0;
+        mx = std::max(mx, cnt[r]);
+        pre[r + 1] = pre[r] + std::max<int64_t>(cnt[r], 0);
     }
     if (local) {
         h->err = sync_err;
         return local;
     }
     if (peer_failed) return pcg_fail(h, PCG_ERR_PEER, "sepset gather: another rank failed");
-    const int64_t per = mx * (W + 1);
-    if (!pcg_ensure(h, h->comm_packed, sizeof(int64_t) * (size_t)per) ||
-        !pcg_ensure(h, h->comm_gathered, sizeof(int64_t) * (size_t)per * world))
+    for (int d = 0; d < L && d < PCG_MAX_LEVELS; ++d) {
+        int64_t v[5] = {0, 0, 0, 0, 0};
+        for (int r = 0; r < world; ++r)
+            for (int k = 0; k < 5; ++k) v[k] += all[(size_t)r * per + k * PCG_MAX_LEVELS + d];
+        h->st.tests[d] = v[0];
+        h->st.indep[d] = v[1];
+        h->st.exact[d] = v[2];
+        h->st.near_alpha[d] = v[3];
+        h->st.screened[d] = v[4];
+    }
+    const int64_t total = pre[world];
+    const int64_t per_rows = mx, words = per_rows * (W + 1);
+    const uint64_t a0 = h->alloc_events;
+    if (!pcg_ensure(h, h->comm_packed, sizeof(int64_t) * (size_t)words + sizeof(int64_t) * (world + 1)) ||
+        !pcg_ensure(h, h->comm_gathered, sizeof(int64_t) * (size_t)words * world))
         local = pcg_fail(h, PCG_ERR_OOM, "sepset row gather (%lld rows x %d words)", (long long)mx, W + 1);
-    const int g = agree(h, local != 0);
-    if (g) return agreed_failure(h, local, g, "sepset gather");
-    hipLaunchKernelGGL(k_pack_rows, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, h->stream,
-                       (const int32_t *)h->export_xy.p, (const uint64_t *)h->exportbuf.p, mine, W, mx,
-                       (int64_t *)h->comm_packed.p);
-    if (int rc = h->comm_ops->all_gather(h, h->comm_packed.p, h->comm_gathered.p, sizeof(int64_t) * (size_t)per))
-        return rc;
+    if (h->alloc_events != a0) {    // grown (or failed to) on this rank, hence on every rank: agree
+        const int g = agree(h, local != 0);
+        if (g) {
+            release_agreed(h, {&h->comm_packed, &h->comm_gathered});
+            h->sk_agreed[0] = h->sk_agreed[1] = -1;
+            return agreed_failure(h, local, g, "sepset gather");
+        }
+    }
+    int64_t *pk = (int64_t *)h->comm_packed.p;
+    hipLaunchKernelGGL(k_pack_rows, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, h->stream,
+                       (const int32_t *)h->dst_xy, (const uint64_t *)h->dst_bits, cnt[h->comm_rank], W, mx, pk);
+    if (int rc = h->comm_ops->all_gather(h, pk, h->comm_gathered.p, sizeof(int64_t) * (size_t)words)) return rc;
     // the last collective of the call: the export buffers grow (their rows are packed already)
     const int64_t cap = std::max<int64_t>(total, 1);
     if (!pcg_ensure(h, h->exportbuf, sizeof(uint64_t) * (size_t)cap * W) ||
         !pcg_ensure(h, h->export_xy, sizeof(int32_t) * 2 * (size_t)cap))
         return pcg_fail(h, PCG_ERR_OOM, "sepset export buffer");
-    int64_t at = 0;
-    for (int r = 0; r < world; ++r) {
-        if (!cnt[r]) continue;
-        const int64_t e = cnt[r] * (W + 1);
-        hipLaunchKernelGGL(k_unpack_rows, dim3((unsigned)((e + 255) / 256)), dim3(256), 0, h->stream,
-                           (const int64_t *)h->comm_gathered.p + (int64_t)r * per, cnt[r], W,
-                           (int32_t *)h->export_xy.p + 2 * at, (uint64_t *)h->exportbuf.p + at * W);
-        at += cnt[r];
-    }
+    export_to_own(h, cap);             // every rank's rows land in the handle's own buffers
+    int64_t *pre_d = pk + words;          // the rank prefix, behind this rank's (already gathered) rows
+    PCG_HIP(h, hipMemcpyAsync(pre_d, pre.data(), sizeof(int64_t) * (world + 1), hipMemcpyHostToDevice, h->stream));
+    const int64_t e = total * (W + 1);
+    if (e > 0)
+        hipLaunchKernelGGL(k_unpack_all, dim3((unsigned)((e + 255) / 256)), dim3(256), 0, h->stream,
+                           (const int64_t *)h->comm_gathered.p, (const int64_t *)pre_d, world, per_rows, W,
+                           (int32_t *)h->export_xy.p, (uint64_t *)h->exportbuf.p);
     PCG_HIP(h, hipGetLastError());
-    PCG_HIP(h, hipStreamSynchronize(h->stream));
     h->export_rows = total;
     h->export_cap = std::max(h->export_cap, cap);
     return PCG_OK;
@@ -495,6 +541,7 @@ int gather_sepsets(pcg_handle *h) {
 
 void pcg_comm_release(pcg_handle *h) {
     if (!h) return;
+    h->k1_agreed[0] = h->sk_agreed[0] = -1;   // a new communicator agrees again
     if (h->comm && h->comm_ops) h->comm_ops->release(h);
     h->comm = nullptr;
     h->comm_ops = nullptr;
@@ -526,8 +573,7 @@ extern "C" int pcg_comm_init(pcg_handle *h, const void *unique_id, int rank, int
     // the status int of agree() and the small stats / row-count buffer exist before the first
     // collective, so no allocation can fail between two collectives later. A failure here still
     // joins the communicator's creation (its peers are blocked in it) and then leaves it.
-    const bool bufs = pcg_ensure(h, h->comm_status, 64) &&
-                      pcg_ensure(h, h->comm_small, sizeof(int64_t) * (size_t)std::max(5 * PCG_MAX_LEVELS, world + 1));
+    const bool bufs = pcg_ensure(h, h->comm_status, 64) && pcg_ensure(h, h->comm_small, comm_small_bytes(world));
     ncclComm_t comm = nullptr;
     PCG_NCCL(h, rccl().comm_init_rank(&comm, world, id, rank));
     if (!bufs) {
@@ -578,8 +624,7 @@ extern "C" int pcg_comm_init_group(pcg_handle *h, pcg_comm_group *g, int rank) {
         return pcg_fail(h, PCG_ERR_INVALID, "pcg_comm_init_group: rank %d", rank);
     pcg_comm_release(h);
     PCG_HIP(h, hipSetDevice(h->device));
-    if (!pcg_ensure(h, h->comm_status, 64) ||
-        !pcg_ensure(h, h->comm_small, sizeof(int64_t) * (size_t)std::max(5 * PCG_MAX_LEVELS, g->world + 1)))
+    if (!pcg_ensure(h, h->comm_status, 64) || !pcg_ensure(h, h->comm_small, comm_small_bytes(g->world)))
         return pcg_fail(h, PCG_ERR_OOM, "pcg_comm_init_group: status buffers");
     {
         std::lock_guard<std::mutex> lk(g->mu);
@@ -605,33 +650,52 @@ extern "C" int pcg_corr_sharded(pcg_handle *h, const double *X, int64_t N, int64
                                 int64_t ldc) {
     int rc = need_comm(h);
     if (rc) return rc;
+    if (!X || !C || N < 2 || n < 1 || ldx < n || ldc < n || n > (1 << 24))
+        return pcg_fail(h, PCG_ERR_INVALID, "pcg_corr_sharded: invalid arguments");   // equal on every rank
+    PCG_HIP(h, hipSetDevice(h->device));
+    const int world = h->comm_world;
+    // Set-up: every buffer the launches below use is sized first (the plan — path, moduli, bits,
+    // split-K — comes from (n, N) and the K1 knobs). The outcome and the plan signature are agreed
+    // by every rank when anything was allocated or this (n, N, world, plan) has not been agreed on
+    // this communicator yet; otherwise nothing can fail on one rank only and the agreement's host
+    // round trip is skipped (every rank makes the same calls: K1 knobs change on all ranks or none).
+    // Ranks started with different knobs thus fail together instead of gathering mismatched units.
+    const int64_t sig = k1_plan_signature(h, n, N);
+    const uint64_t a0 = h->alloc_events;
+    bool crt = false;
     int64_t bytes = 0;
-    rc = pcg_corr_shard_bytes(h, n, N, h->comm_world, &bytes);
-    if (rc) return pcg_fail(h, rc, "pcg_corr_shard_bytes");   // a function of (n, N, world): every rank agrees
-    const size_t per = (size_t)bytes / sizeof(double);
-    // buffer growth is the same decision on every rank (same n, world, call history); when it
-    // happens, its outcome is agreed before the all-gather
-    const size_t b1 = sizeof(double) * std::max<size_t>(per, 1);
-    const size_t b2 = sizeof(double) * std::max<size_t>(per * h->comm_world, 1);
-    if (h->comm_packed.bytes < b1 || h->comm_gathered.bytes < b2) {
-        int local = PCG_OK;
-        if (!pcg_ensure(h, h->comm_packed, b1) || !pcg_ensure(h, h->comm_gathered, b2))
-            local = pcg_fail(h, PCG_ERR_OOM, "sharded K1 buffers");
-        const int g = agree(h, local != 0);
-        if (g) return agreed_failure(h, local, g, "sharded K1");
+    int local = corr_shard_crt_prepare(h, N, n, world, &crt, &bytes);
+    if (!local && !crt) local = pcg_corr_shard_bytes(h, n, N, world, &bytes);
+    const size_t b1 = std::max<size_t>((size_t)bytes, 8), b2 = std::max<size_t>((size_t)bytes * world, 8);
+    if (!local && (!pcg_ensure(h, h->comm_packed, b1) || !pcg_ensure(h, h->comm_gathered, b2)))
+        local = pcg_fail(h, PCG_ERR_OOM, "sharded K1 buffers");
+    const bool agreed = h->k1_agreed[0] == n && h->k1_agreed[1] == N && h->k1_agreed[2] == world && h->k1_agreed[3] == sig;
+    if (local || h->alloc_events != a0 || !agreed || !crt) {
+        // (the digit / fp64 path keeps the synchronous protocol: pcg_corr_shard may allocate inside)
+        if (!crt && !local) local = pcg_corr_shard(h, X, N, n, ldx, h->comm_rank, world, (double *)h->comm_packed.p);
+        bool same = true;
+        const int g = agree_value(h, local != 0, sig, &same);
+        if (g || !same) {
+            h->k1_agreed[0] = -1;
+            release_agreed(h, {&h->comm_packed, &h->comm_gathered, &h->k1_digits});
+            if (g) return agreed_failure(h, local, g, "sharded K1");
+            return pcg_fail(h, PCG_ERR_INVALID, "sharded K1: the ranks' K1 plans differ (PCG_K1_* knobs)");
+        }
+        h->k1_agreed[0] = n;
+        h->k1_agreed[1] = N;
+        h->k1_agreed[2] = world;
+        h->k1_agreed[3] = sig;
     }
-    // pcg_corr_shard can fail on one rank only (its column-statistics and residue-plane scratch
-    // grow on demand: ~350 MB at n = 2000, N = 1e4): the outcome is agreed before the all-gather,
-    // so no peer rebuilds C from a failed rank's unwritten units and every rank leaves together
-    // the plan (path, k, b, split-K) comes from (n, N) and the process's K1 knobs: ranks started
-    // with different knobs would gather mismatched units, so its signature is agreed with the outcome
-    const int local = pcg_corr_shard(h, X, N, n, ldx, h->comm_rank, h->comm_world, (double *)h->comm_packed.p);
-    bool same = true;
-    const int g = agree_value(h, local != 0, k1_plan_signature(h, n, N), &same);
-    if (g) return agreed_failure(h, local, g, "sharded K1");
-    if (!same) return pcg_fail(h, PCG_ERR_INVALID, "sharded K1: the ranks' K1 plans differ (PCG_K1_* environment)");
-    if (int rc2 = h->comm_ops->all_gather(h, h->comm_packed.p, h->comm_gathered.p, sizeof(double) * per)) return rc2;
-    return pcg_corr_shard_finish(h, (const double *)h->comm_gathered.p, N, n, h->comm_world, C, ldc);
+    if (!crt) {
+        if (int r = h->comm_ops->all_gather(h, h->comm_packed.p, h->comm_gathered.p, (size_t)bytes)) return r;
+        return pcg_corr_shard_finish(h, (const double *)h->comm_gathered.p, N, n, world, C, ldc);
+    }
+    // the CRT path: this rank's units (and only its moduli's residue planes), the all-gather and the
+    // rebuild, all stream-ordered on the handle's stream with no host sync (a failure from here on
+    // is a launch / device fault)
+    if ((rc = corr_shard_crt_enqueue(h, X, N, n, ldx, h->comm_rank, world, (double *)h->comm_packed.p))) return rc;
+    if ((rc = h->comm_ops->all_gather(h, h->comm_packed.p, h->comm_gathered.p, (size_t)bytes))) return rc;
+    return corr_shard_crt_finish_enqueue(h, (const double *)h->comm_gathered.p, N, n, C, ldc);
 }
 
 extern "C" int pcg_skeleton_sharded(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N,
@@ -645,8 +709,7 @@ extern "C" int pcg_skeleton_sharded(pcg_handle *h, const double *C, int64_t n, i
     }
     // level errors (singular, domain, a peer's local failure) end every rank at the same depth
     // through the merged status word, so the collectives below are skipped consistently
-    if (!rc) rc = reduce_stats(h);
-    if (!rc) rc = gather_sepsets(h);
+    if (!rc) rc = finish_sharded(h);
     if (stats) *stats = h->st;
     return rc;
 }

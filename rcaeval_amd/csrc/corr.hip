@@ -1511,6 +1511,67 @@ extern "C" int pcg_corr_shard_finish(pcg_handle *h, const double *gathered, int6
     return PCG_OK;
 }
 
+// The native sharded K1 (comm.hip pcg_corr_sharded) on the CRT path, in three steps with no host
+// sync: corr_shard_crt_prepare sizes every buffer the launches use (so the only local failure, an
+// allocation, happens before any collective), corr_shard_crt_enqueue launches this rank's share —
+// the column statistics, the residue planes of ONLY the moduli its unit run touches (units are
+// modulus-major: at 8 ranks a rank forms ~1/8 of the 17 planes), its units of the GEMM — and
+// corr_shard_crt_finish_enqueue rebuilds C from the all-gathered units. *crt = false: K1 takes the
+// digit / fp64 path here and the caller uses pcg_corr_shard / pcg_corr_shard_finish instead.
+int corr_shard_crt_prepare(pcg_handle *h, int64_t N, int64_t n, int world, bool *crt, int64_t *unit_bytes) {
+    CrtPlan cp;
+    *crt = crt_plan(h->tune, (int)n, N, cp);
+    if (!*crt) return PCG_OK;
+    const int nn = (int)n;
+    const int nchunks = (int)((N + MEAN_ROWS - 1) / MEAN_ROWS);
+    const size_t parts = (size_t)nn * nchunks * 3;
+    if (!pcg_ensure(h, h->colmean, sizeof(double) * (parts + nn) + sizeof(int) * nn) ||
+        !pcg_ensure(h, h->k1_digits, (size_t)cp.tab.k * cp.CBp * cp.TB * 2048) ||
+        !pcg_ensure(h, h->pr_scratch, sizeof(double) * (size_t)(nn + 32)))
+        return pcg_fail(h, PCG_ERR_OOM, "sharded K1 scratch (n %lld, N %lld)", (long long)n, (long long)N);
+    *unit_bytes = (cp.units + world - 1) / world * (int64_t)CRT_UNIT;
+    return PCG_OK;
+}
+
+int corr_shard_crt_enqueue(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx, int rank, int world,
+                           double *packed) {
+    const int nn = (int)n;
+    CrtPlan cp;
+    if (!crt_plan(h->tune, nn, N, cp)) return pcg_fail(h, PCG_ERR_INVALID, "sharded K1: not the CRT path");
+    double *mean;
+    int *expo = nullptr;
+    int rc = column_means(h, X, N, nn, ldx, &mean, &expo);
+    if (rc) return rc;
+    h->k1_stamp[0] = N;
+    h->k1_stamp[1] = nn;
+    h->k1_stamp[2] = cp.tab.k;
+    h->k1_stamp[3] = ((int64_t)cp.tab.b << 32) | ((int64_t)cp.ks << 16) | cp.kb;
+    h->k1_stamp_ok = true;
+    const int64_t per = (cp.units + world - 1) / world, u0 = per * rank;
+    const int64_t nu = std::max<int64_t>(std::min<int64_t>(per, cp.units - u0), 0);
+    if (nu > 0) {
+        const int64_t um = (int64_t)cp.ntiles * cp.ks;       // units per modulus
+        const int m0 = (int)(u0 / um), m1 = (int)((u0 + nu - 1) / um) + 1;
+        const int8_t *R = nullptr;
+        rc = crt_residues(h, cp, X, N, nn, ldx, mean, expo, m0, m1, h->stream, &R);
+        if (rc) return rc;
+        crt_gemm(h, cp, R, u0, nu, (uint8_t *)packed);
+    }
+    PCG_HIP(h, hipGetLastError());
+    return PCG_OK;
+}
+
+int corr_shard_crt_finish_enqueue(pcg_handle *h, const double *gathered, int64_t N, int64_t n, double *C,
+                                  int64_t ldc) {
+    const int nn = (int)n;
+    CrtPlan cp;
+    if (!crt_plan(h->tune, nn, N, cp) || !h->k1_stamp_ok)
+        return pcg_fail(h, PCG_ERR_INVALID, "sharded K1 finish: no CRT-mode shard on this handle");
+    crt_finish(h, cp, (const uint8_t *)gathered, colmean_expo(h, N, nn), nn, N, (double *)h->pr_scratch.p, C, ldc);
+    PCG_HIP(h, hipGetLastError());
+    return PCG_OK;
+}
+
 // K1 launched on the handle's stream without a host sync (the fused pcg_pc_skeleton path)
 int pcg_corr_launch(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx, double *C, int64_t ldc) {
     if (!h || !X || !C || N < 2 || n < 1 || ldx < n || ldc < n || n > (1 << 24))

@@ -107,6 +107,16 @@ struct pcg_handle {
     int64_t rec_mod = 0, rec_res = 0;  // pcg_set_record_sample (0/1 = record every test)
     int64_t export_cap = 0;          // rows
     int64_t export_rows = 0;         // rows exported so far (host mirror)
+    // where this run's sepset rows go (pcg_set_sepset_buffers): the caller's device buffers when
+    // they hold the run's row bound (one GPU), else the handle's own exportbuf / export_xy
+    int32_t *usr_xy = nullptr;
+    uint64_t *usr_bits = nullptr;
+    int64_t usr_cap = 0;
+    int32_t *dst_xy = nullptr;
+    uint64_t *dst_bits = nullptr;
+    int64_t dst_cap = 0;
+    bool dst_user = false;
+    int64_t need_cap = 0;            // this run's row bound (the ordered pairs entering depth 1)
     int binom_n = -1;                // binom table built for 0..binom_n
 
     // skeleton state (single-GPU and level-step API)
@@ -182,6 +192,13 @@ struct pcg_handle {
     int comm_rank = 0, comm_world = 1;
     DevBuf comm_rm, comm_packed, comm_gathered, comm_small;
     DevBuf comm_status;   // agree(): one int32 all-reduced with MAX, allocated before the communicator
+    // the native driver's set-up agreements (comm.hip): the (n, N, world, plan signature) of the last
+    // agreed sharded K1 and the (n, world) of the last agreed skeleton set-up. A call that matches
+    // and allocates nothing skips the agreement's host round trip (every rank makes the same calls,
+    // so every rank skips it together); any allocation or a new tuple agrees again
+    int64_t k1_agreed[4] = {-1, -1, -1, 0};
+    int64_t sk_agreed[2] = {-1, -1};
+    uint64_t alloc_events = 0;       // device / pinned allocations made by pcg_ensure*, ever
 };
 
 void pcg_comm_release(pcg_handle *h);      // comm.hip: destroy the communicator, free its buffers
@@ -189,7 +206,31 @@ void pcg_comm_release(pcg_handle *h);      // comm.hip: destroy the communicator
 int export_sync(pcg_handle *h);   // skeleton.hip: wait for the sepset exports, take their row count
 int pcg_corr_launch(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx, double *C, int64_t ldc);
 int64_t k1_plan_signature(const pcg_handle *h, int64_t n, int64_t N);   // corr.hip: K1's plan, for cross-rank agreement
+// corr.hip: the native sharded K1's CRT path without host syncs (see corr.hip)
+int corr_shard_crt_prepare(pcg_handle *h, int64_t N, int64_t n, int world, bool *crt, int64_t *unit_bytes);
+int corr_shard_crt_enqueue(pcg_handle *h, const double *X, int64_t N, int64_t n, int64_t ldx, int rank, int world,
+                           double *packed);
+int corr_shard_crt_finish_enqueue(pcg_handle *h, const double *gathered, int64_t N, int64_t n, double *C, int64_t ldc);
+// skeleton.hip: one level-loop run's host-path state (device-clock depth stamps, near-alpha records
+// once after the last depth, the depth bound's last export on the handle's stream, the tail
+// kernel), shared by pcg_skeleton's loop and the native sharded driver
+void level_run_begin(pcg_handle *h, int max_depth);
+bool level_run_tail_early(const pcg_handle *h, int depth);   // queue the tail behind this depth's barrier?
+int level_run_tail_launch(pcg_handle *h);
+void level_run_abort(pcg_handle *h, bool tail_queued);
+int level_run_finish(pcg_handle *h, int done, bool tail_queued);
+int level_end_enqueue(pcg_handle *h, unsigned long long *seq);
+int level_end_finish(pcg_handle *h, int d, unsigned long long seq, pcg_stats *stats);
 void pcg_tuning_defaults(int64_t *tune);   // api.hip: the built-in values, overridden by the environment
+
+// the run's sepset rows go to the handle's own export buffers (capacity cap rows); called again
+// whenever those buffers are (re)allocated
+inline void export_to_own(pcg_handle *h, int64_t cap) {
+    h->dst_xy = (int32_t *)h->export_xy.p;
+    h->dst_bits = (uint64_t *)h->exportbuf.p;
+    h->dst_cap = cap;
+    h->dst_user = false;
+}
 
 int pcg_fail(pcg_handle *h, int code, const char *fmt, ...);
 bool pcg_ensure(pcg_handle *h, DevBuf &b, size_t bytes);   // grow-only allocation

@@ -4790,6 +4790,8 @@ extern "C" int pcg_skeleton_init(pcg_handle *h, const double *C, int64_t n, int6
     h->xinl = false;
     h->cb = 0;
     h->export_rows = 0;
+    export_to_own(h, 0);
+    h->need_cap = 0;
     h->rec_h.clear(); h->near_h.clear();
     h->rec_total = h->near_total = 0;
     h->near_seen = h->near_total_dev = 0;
@@ -5028,10 +5030,21 @@ int level_begin_buffers(pcg_handle *h, int depth) {
             // every ordered pair adjacent at depth 1 is exported at most once over all depths
             // (depth-0 removals carry empty sepsets), so one allocation covers the run
             const int64_t cap = std::max<int64_t>(h->sumdeg, 1);
-            if (!pcg_ensure(h, h->exportbuf, sizeof(uint64_t) * cap * h->W) ||
-                !pcg_ensure(h, h->export_xy, sizeof(int32_t) * 2 * cap))
-                return pcg_fail(h, PCG_ERR_OOM, "sepset export buffer");
-            h->export_cap = cap;
+            h->need_cap = cap;
+            if (h->usr_xy && h->usr_bits && h->usr_cap >= cap && h->world == 1 && !h->rm_ext) {
+                // the caller's buffers hold every row this run can export: no copy after the call
+                h->dst_xy = h->usr_xy;
+                h->dst_bits = h->usr_bits;
+                h->dst_cap = h->usr_cap;
+                h->dst_user = true;
+                h->export_cap = cap;
+            } else {
+                if (!pcg_ensure(h, h->exportbuf, sizeof(uint64_t) * cap * h->W) ||
+                    !pcg_ensure(h, h->export_xy, sizeof(int32_t) * 2 * cap))
+                    return pcg_fail(h, PCG_ERR_OOM, "sepset export buffer");
+                h->export_cap = cap;
+                export_to_own(h, cap);
+            }
         }
     }
     return PCG_OK;
@@ -5408,8 +5421,7 @@ int level_end_enqueue(pcg_handle *h, unsigned long long *seq) {
         hipLaunchKernelGGL(k_export, dim3((unsigned)((xsum + 255) / 256)), dim3(256), 0, h->stream,
                            (const int32_t *)h->off2[xcb].p, (const int32_t *)h->nbr2[xcb].p,
                            (const int8_t *)h->rl, d, (const uint64_t *)h->ug2[xcb].p, n, W, xsum,
-                           (int32_t *)h->export_xy.p, (uint64_t *)h->exportbuf.p, h->export_cap,
-                           (unsigned long long *)h->exp_ctr.p);
+                           h->dst_xy, h->dst_bits, h->dst_cap, (unsigned long long *)h->exp_ctr.p);
         PCG_HIP(h, hipGetLastError());
         h->xany = true;
         h->xinl = true;
@@ -5424,8 +5436,7 @@ int level_end_enqueue(pcg_handle *h, unsigned long long *seq) {
         hipLaunchKernelGGL(k_export, dim3((unsigned)((xsum + 255) / 256)), dim3(256), 0, h->xs,
                            (const int32_t *)h->off2[xcb].p, (const int32_t *)h->nbr2[xcb].p,
                            (const int8_t *)h->rl, d, (const uint64_t *)h->ug2[xcb].p, n, W, xsum,
-                           (int32_t *)h->export_xy.p, (uint64_t *)h->exportbuf.p, h->export_cap,
-                           (unsigned long long *)h->exp_ctr.p);
+                           h->dst_xy, h->dst_bits, h->dst_cap, (unsigned long long *)h->exp_ctr.p);
         PCG_HIP(h, hipEventRecord(h->ev_xdone[xcb], h->xs));
         h->xpending[xcb] = true;
         h->xany = true;
@@ -5600,28 +5611,25 @@ static int tail_wait(pcg_handle *h) {
         h->xany = false;
         h->xinl = false;
         h->xpending[0] = h->xpending[1] = false;
-        if ((int64_t)rows > h->export_cap)
+        if ((int64_t)rows > h->dst_cap)
             return pcg_fail(h, PCG_ERR_OVERFLOW, "sepset export overflow (%llu rows > %lld)", rows,
-                            (long long)h->export_cap);
+                            (long long)h->dst_cap);
         h->export_rows = (int64_t)rows;
     }
     return PCG_OK;
 }
 
-// The single-GPU level loop. (Round 3/4 built a pipelined form that enqueued depth d before depth
-// d - 1's summary was read, and a fused one-launch level barrier; both measured slower — DESIGN §9
-// — and were removed in round 5.)
-static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N, double alpha,
-                         int max_depth, int flags, int8_t *removed_level) {
+// One level-loop run's host-path state, shared by the single-GPU loop (skeleton_once) and the
+// native sharded driver (comm.hip sharded_once): level d's wall time from the summaries' device
+// wall-clock stamps (no timing events in the loop), the near-alpha records copied once after the
+// last depth (a synchronous copy per depth that had some sat on the loop's critical path), the
+// depth bound's last export on the handle's stream, and the tail kernel
+void level_run_begin(pcg_handle *h, int max_depth) {
     h->htrace_on = h->tune[PCG_TUNE_HOST_TRACE] != 0;
     h->htrace.clear();
     PCG_HT(h, "init:start");
-    // level d's wall time = between the depth-boundary events graph_launch records after init's
-    // and after each depth's barrier launches (lev[d], lev[d + 1]), read after the last depth
     h->lev_on = true;
     h->lev_n = 0;
-    // the near-alpha records are copied once, after the last depth, on the handle's stream
-    // (a synchronous copy per depth that has some sat on the level loop's critical path)
     h->defer_near = true;
     h->near_pending = 0;
     h->run_max_depth = max_depth;
@@ -5632,40 +5640,36 @@ static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc,
         (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device);
         h->wall_khz = khz > 0 ? khz : 100000;
     }
-    int rc = pcg_skeleton_init(h, C, n, ldc, N, alpha, flags, removed_level);
-    if (rc) { h->lev_on = false; h->defer_near = false; h->run_max_depth = -1; h->stamps = false; return rc; }
-    PCG_HT(h, "init:done");
-    int done = 0;
-    bool tail_queued = false;
-    for (int depth = 0;; ++depth) {
-        if (max_depth >= 0 && depth > max_depth) break;
-        if (depth >= PCG_MAX_LEVELS) break;   // pcg_level_begin refuses deeper levels itself
-        int64_t total = 0;
-        PCG_HT(h, "loop:begin");
-        rc = level_begin_impl(h, depth, &total);
-        if (rc == 1) break;
-        if (!rc) rc = pcg_level_run(h, 0, total);
-        unsigned long long seq = 0;
-        if (!rc) rc = level_end_enqueue(h, &seq);
-        // the depth bound's last depth: the tail transfer queued behind its barrier right away
-        if (!rc && PCG_TAIL_SPIN && PCG_TAIL_EARLY && max_depth >= 0 && depth >= max_depth) {
-            rc = tail_launch(h);
-            tail_queued = true;
-        }
-        if (!rc) rc = level_end_finish(h, depth, seq, nullptr);
-        if (rc && tail_queued) {
-            // the last depth failed after its tail kernel was queued (singular / domain / overflow):
-            // let that kernel finish writing the tail buffer before returning, and leave no export
-            // marked pending, so no later call reads a half-written tail or stale export state
-            const std::string err = h->err;
-            (void)tail_wait(h);
-            h->err = err;
-            h->xany = h->xinl = false;
-            h->xpending[0] = h->xpending[1] = false;
-        }
-        if (rc) { h->lev_on = false; h->defer_near = false; h->run_max_depth = -1; h->stamps = false; return rc; }
-        done = depth + 1;
+}
+
+// the depth bound's last depth: the tail transfer is queued behind its barrier right away
+bool level_run_tail_early(const pcg_handle *h, int depth) {
+    return PCG_TAIL_SPIN && PCG_TAIL_EARLY && h->run_max_depth >= 0 && depth >= h->run_max_depth;
+}
+
+int level_run_tail_launch(pcg_handle *h) { return tail_launch(h); }
+
+void level_run_abort(pcg_handle *h, bool tail_queued) {
+    if (tail_queued) {
+        // the last depth failed after its tail kernel was queued (singular / domain / overflow /
+        // a peer's failure): let that kernel finish writing the tail buffer before returning, and
+        // leave no export marked pending, so no later call reads a half-written tail or stale state
+        const std::string err = h->err;
+        (void)tail_wait(h);
+        h->err = err;
+        h->xany = h->xinl = false;
+        h->xpending[0] = h->xpending[1] = false;
     }
+    h->lev_on = false;
+    h->defer_near = false;
+    h->run_max_depth = -1;
+    h->stamps = false;
+}
+
+// after the last depth (done depths ran): the tail (export row count, near-alpha records) and
+// the per-depth wall times
+int level_run_finish(pcg_handle *h, int done, bool tail_queued) {
+    int rc = PCG_OK;
     h->lev_on = false;
     h->defer_near = false;
     h->run_max_depth = -1;
@@ -5725,6 +5729,38 @@ static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc,
     return PCG_OK;
 }
 
+// The single-GPU level loop. (Round 3/4 built a pipelined form that enqueued depth d before depth
+// d - 1's summary was read, and a fused one-launch level barrier; both measured slower — DESIGN §9
+// — and were removed in round 5.)
+static int skeleton_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t N, double alpha,
+                         int max_depth, int flags, int8_t *removed_level) {
+    level_run_begin(h, max_depth);
+    int rc = pcg_skeleton_init(h, C, n, ldc, N, alpha, flags, removed_level);
+    if (rc) { level_run_abort(h, false); return rc; }
+    PCG_HT(h, "init:done");
+    int done = 0;
+    bool tail_queued = false;
+    for (int depth = 0;; ++depth) {
+        if (max_depth >= 0 && depth > max_depth) break;
+        if (depth >= PCG_MAX_LEVELS) break;   // pcg_level_begin refuses deeper levels itself
+        int64_t total = 0;
+        PCG_HT(h, "loop:begin");
+        rc = level_begin_impl(h, depth, &total);
+        if (rc == 1) break;
+        if (!rc) rc = pcg_level_run(h, 0, total);
+        unsigned long long seq = 0;
+        if (!rc) rc = level_end_enqueue(h, &seq);
+        if (!rc && level_run_tail_early(h, depth)) {
+            rc = tail_launch(h);
+            tail_queued = true;
+        }
+        if (!rc) rc = level_end_finish(h, depth, seq, nullptr);
+        if (rc) { level_run_abort(h, tail_queued); return rc; }
+        done = depth + 1;
+    }
+    return level_run_finish(h, done, tail_queued);
+}
+
 namespace {
 // the small-graph path is taken for n <= SMALL_N on one rank with the handle's own removal flags
 // (PCG_TUNE_SMALL = 0: the level loop for every size)
@@ -5763,6 +5799,7 @@ int skeleton_small(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64
         !pcg_ensure_pinned(h, h->small_pin, sizeof(SmallSummary) + 64))
         return pcg_fail(h, PCG_ERR_OOM, "small-graph skeleton buffers (n=%lld)", (long long)n);
     h->export_cap = std::max(h->export_cap, rows);
+    export_to_own(h, h->export_cap);
     if (h->binom_n != (int)n) {
         build_binom(h, (int)n);
         if (!pcg_ensure(h, h->binom, sizeof(uint64_t) * h->binom_h.size())) return PCG_ERR_OOM;
@@ -5927,10 +5964,26 @@ int export_sync(pcg_handle *h) {
     h->xany = false;
     h->xinl = false;
     h->xpending[0] = h->xpending[1] = false;
-    if ((int64_t)rows > h->export_cap)
+    if ((int64_t)rows > h->dst_cap)
         return pcg_fail(h, PCG_ERR_OVERFLOW, "sepset export overflow (%llu rows > %lld)", rows,
-                        (long long)h->export_cap);
+                        (long long)h->dst_cap);
     h->export_rows = (int64_t)rows;
+    return PCG_OK;
+}
+
+extern "C" int pcg_set_sepset_buffers(pcg_handle *h, int32_t *xy_dev, uint64_t *bits_dev, int64_t capacity) {
+    if (!h || capacity < 0 || ((xy_dev == nullptr) != (bits_dev == nullptr)))
+        return pcg_fail(h, PCG_ERR_INVALID, "pcg_set_sepset_buffers: invalid arguments");
+    h->usr_xy = capacity > 0 ? xy_dev : nullptr;
+    h->usr_bits = capacity > 0 ? bits_dev : nullptr;
+    h->usr_cap = h->usr_xy ? capacity : 0;
+    return PCG_OK;
+}
+
+extern "C" int pcg_sepset_target(pcg_handle *h, int32_t *in_caller, int64_t *capacity_needed) {
+    if (!h) return PCG_ERR_INVALID;
+    if (in_caller) *in_caller = h->dst_user ? 1 : 0;
+    if (capacity_needed) *capacity_needed = h->need_cap;
     return PCG_OK;
 }
 
@@ -5957,8 +6010,8 @@ extern "C" int pcg_sepset_export(pcg_handle *h, int32_t *xy_host, uint64_t *bits
     if (rc) return rc;
     if (count > h->export_rows) return pcg_fail(h, PCG_ERR_INVALID, "pcg_sepset_export: count");
     if (count == 0) return PCG_OK;
-    PCG_HIP(h, hipMemcpy(xy_host, h->export_xy.p, sizeof(int32_t) * 2 * count, hipMemcpyDeviceToHost));
-    PCG_HIP(h, hipMemcpy(bits_host, h->exportbuf.p, sizeof(uint64_t) * count * h->W, hipMemcpyDeviceToHost));
+    PCG_HIP(h, hipMemcpy(xy_host, h->dst_xy, sizeof(int32_t) * 2 * count, hipMemcpyDeviceToHost));
+    PCG_HIP(h, hipMemcpy(bits_host, h->dst_bits, sizeof(uint64_t) * count * h->W, hipMemcpyDeviceToHost));
     return PCG_OK;
 }
 
@@ -5968,10 +6021,11 @@ extern "C" int pcg_sepset_export_device(pcg_handle *h, int32_t *xy_dev, uint64_t
     if (rc) return rc;
     if (count > h->export_rows) return pcg_fail(h, PCG_ERR_INVALID, "pcg_sepset_export_device: count");
     if (count == 0) return PCG_OK;
-    PCG_HIP(h, hipMemcpyAsync(xy_dev, h->export_xy.p, sizeof(int32_t) * 2 * count, hipMemcpyDeviceToDevice,
-                              h->stream));
-    PCG_HIP(h, hipMemcpyAsync(bits_dev, h->exportbuf.p, sizeof(uint64_t) * count * h->W,
-                              hipMemcpyDeviceToDevice, h->stream));
+    if (xy_dev != h->dst_xy)
+        PCG_HIP(h, hipMemcpyAsync(xy_dev, h->dst_xy, sizeof(int32_t) * 2 * count, hipMemcpyDeviceToDevice, h->stream));
+    if (bits_dev != h->dst_bits)
+        PCG_HIP(h, hipMemcpyAsync(bits_dev, h->dst_bits, sizeof(uint64_t) * count * h->W, hipMemcpyDeviceToDevice,
+                                  h->stream));
     return PCG_OK;
 }
 

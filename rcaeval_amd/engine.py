@@ -99,6 +99,11 @@ class Engine:
                 stream = torch.cuda.current_stream(self.device)
         self.stream = stream
         check(self.h, self.lib.pcg_set_stream(self.h, ctypes.c_void_p(stream.cuda_stream)), "pcg_set_stream")
+        # sepset rows exported straight into engine-owned buffers (pcg_set_sepset_buffers): the
+        # buffer (W, capacity, xy, bits) armed for the current call, and the row bound per n
+        self._sep_buf = None
+        self._sep_armed = None
+        self._sep_need: dict = {}
 
     def close(self):
         if getattr(self, "h", None):
@@ -224,10 +229,39 @@ class Engine:
                                            int(max_depth), int(flags), ctypes.c_void_p(rl.data_ptr()),
                                            ctypes.byref(st))
         check(self.h, rc, "pcg_skeleton_sharded")
-        self.sync()
+        # (results are stream-ordered on the handle's stream: no host sync here)
         return self._collect(n, rl, st, None)
 
     # ------------------------------------------------------------------ K2/K3
+    def _sep_arm(self, n: int) -> None:
+        """Let the next one-GPU run export its sepset rows straight into an engine-owned buffer
+        (pcg_set_sepset_buffers), sized from the last run's row bound for this n: the result then
+        holds views of it and no copy follows the call. A buffer that any live tensor still views
+        (an earlier result, or a slice a caller kept) is never written again: a fresh one is
+        allocated and the old one stays with its viewers."""
+        import sys
+        need = self._sep_need.get(n, 0)
+        self._sep_armed = None
+        if need <= 0:          # first run of this n: the handle's own buffers, then a copy
+            return
+        torch = _torch()
+        W = (n + 63) // 64
+        buf = self._sep_buf
+        # (2 references: self._sep_buf's tuple and getrefcount's argument; a live view adds one)
+        if buf is None or buf[0] != W or buf[1] < need or sys.getrefcount(buf[2]) > 2 or sys.getrefcount(buf[3]) > 2:
+            cap = need + need // 4 + 64
+            buf = (W, cap, torch.empty((cap, 2), dtype=torch.int32, device=self.device),
+                   torch.empty((cap, W), dtype=torch.int64, device=self.device))
+            self._sep_buf = buf
+        check(self.h, self.lib.pcg_set_sepset_buffers(self.h, ctypes.c_void_p(buf[2].data_ptr()),
+                                                      ctypes.c_void_p(buf[3].data_ptr()), buf[1]),
+              "pcg_set_sepset_buffers")
+        self._sep_armed = buf
+
+    def _sep_disarm(self) -> None:
+        if self._sep_armed is not None:
+            self.lib.pcg_set_sepset_buffers(self.h, None, None, 0)
+
     def _banned(self, banned, n: int):
         """Device copy of the n x n uint8 banned-pair mask, registered with the handle (or None)."""
         if banned is None:
@@ -269,6 +303,7 @@ class Engine:
         st = PcgStats()
         ev0, ev1 = self._events()
         bd = self._banned(banned, n)
+        self._sep_arm(n)
         try:
             ev0.record()
             rc = self.lib.pcg_skeleton(self.h, ctypes.c_void_p(Cd.data_ptr()), n, n, int(N), float(alpha),
@@ -277,6 +312,7 @@ class Engine:
             ev1.record()
         finally:
             self._unban(bd)
+            self._sep_disarm()
         check(self.h, rc, "pcg_skeleton")
         t0 = time.perf_counter()
         out = self._collect(n, rl, st, (ev0, ev1))
@@ -298,6 +334,7 @@ class Engine:
         st = PcgStats()
         ev0, ev1 = self._events()
         bd = self._banned(banned, n)
+        self._sep_arm(n)
         try:
             ev0.record()
             rc = self.lib.pcg_pc_skeleton(self.h, ctypes.c_void_p(Xd.data_ptr()), N, n, n,
@@ -306,6 +343,7 @@ class Engine:
             ev1.record()
         finally:
             self._unban(bd)
+            self._sep_disarm()
         check(self.h, rc, "pcg_pc_skeleton")
         t0 = time.perf_counter()
         out = self._collect(n, rl, st, (ev0, ev1))
@@ -319,12 +357,20 @@ class Engine:
         torch = _torch()
         cnt, W = ctypes.c_int64(), ctypes.c_int32()
         check(self.h, self.lib.pcg_sepset_count(self.h, ctypes.byref(cnt), ctypes.byref(W)), "pcg_sepset_count")
-        xy = torch.empty((cnt.value, 2), dtype=torch.int32, device=self.device)
-        bits = torch.empty((cnt.value, W.value), dtype=torch.int64, device=self.device)
-        if cnt.value:
-            check(self.h, self.lib.pcg_sepset_export_device(self.h, ctypes.c_void_p(xy.data_ptr()),
-                                                            ctypes.c_void_p(bits.data_ptr()), cnt.value),
-                  "pcg_sepset_export_device")
+        tgt, need = ctypes.c_int32(), ctypes.c_int64()
+        check(self.h, self.lib.pcg_sepset_target(self.h, ctypes.byref(tgt), ctypes.byref(need)), "pcg_sepset_target")
+        if need.value > 0:
+            self._sep_need[n] = int(need.value)
+        buf, self._sep_armed = self._sep_armed, None
+        if tgt.value and buf is not None and buf[0] == W.value:
+            xy, bits = buf[2][:cnt.value], buf[3][:cnt.value]      # rows already in place: views
+        else:
+            xy = torch.empty((cnt.value, 2), dtype=torch.int32, device=self.device)
+            bits = torch.empty((cnt.value, W.value), dtype=torch.int64, device=self.device)
+            if cnt.value:
+                check(self.h, self.lib.pcg_sepset_export_device(self.h, ctypes.c_void_p(xy.data_ptr()),
+                                                                ctypes.c_void_p(bits.data_ptr()), cnt.value),
+                      "pcg_sepset_export_device")
         L = st.levels
         deg = np.zeros((max(L, 1), n), np.int32)
         if L:

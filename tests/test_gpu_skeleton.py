@@ -549,3 +549,39 @@ def test_inline_export_equals_export_stream(eng, n, N, seed, wl, wh, ep):
     sa, sb = _engine_state(a), _engine_state(b)
     np.testing.assert_array_equal(sa[0], sb[0])
     assert sa[3] == sb[3]
+
+
+def test_sepset_rows_in_engine_buffers_never_overwrite_live_results(eng):
+    """pcg_set_sepset_buffers: from the second run of an n on, the sepset rows are exported straight
+    into an engine-owned buffer and the result holds views of it (no copy after the call). A
+    buffer that a live result, or any slice of it a caller kept, still views is never written
+    again; the rows equal the copy path's and the oracle's."""
+    from oracle import cpc
+    from tests_support import unions_from_oracle
+    n = 317                                      # an n no other test uses: its first run copies
+    X1 = synth.gaussian_sem(n, 2000, seed=9)
+    X2 = synth.gaussian_sem(n, 2000, seed=10)
+    C1, C2 = eng.corr(X1), eng.corr(X2)
+    a = eng.skeleton(C1, 2000)                  # the copy path (learns the row bound)
+    b = eng.skeleton(C1, 2000)                  # rows in the engine's buffer
+    assert b.sep_xy_dev._base is not None and a.sep_xy_dev._base is None
+    np.testing.assert_array_equal(b.sep_xy, a.sep_xy)
+    np.testing.assert_array_equal(b.sep_bits, a.sep_bits)
+    bxy = b.sep_xy_dev.cpu().numpy().copy()
+    bbits = b.sep_bits_dev.cpu().numpy().copy()
+    c = eng.skeleton(C2, 2000)                  # b is alive: another buffer
+    assert c.sep_xy_dev.data_ptr() != b.sep_xy_dev.data_ptr()
+    np.testing.assert_array_equal(b.sep_xy_dev.cpu().numpy(), bxy)
+    np.testing.assert_array_equal(b.sep_bits_dev.cpu().numpy(), bbits)
+    kept = c.sep_bits_dev[:5]                   # a caller keeps a slice, drops the result
+    kept_h = kept.cpu().numpy().copy()
+    del c
+    d = eng.skeleton(C1, 2000)
+    np.testing.assert_array_equal(kept.cpu().numpy(), kept_h)
+    np.testing.assert_array_equal(d.sep_bits, a.sep_bits)
+    ref = cpc.skeleton(np.corrcoef(X1.T), 2000, want_union=True)
+    assert unions_from_engine(d) == unions_from_oracle(ref, n)
+    del kept, b
+    e = eng.skeleton(C1, 2000)                  # nothing views the last buffer any more: reused
+    assert e.sep_bits_dev._base is not None
+    np.testing.assert_array_equal(e.sep_bits, a.sep_bits)
