@@ -435,16 +435,23 @@ int sharded_once(pcg_handle *h, const double *C, int64_t n, int64_t ldc, int64_t
 // and one unpack launch. The row buffers grow-only; their growth (the same decision on every rank:
 // all see the same counts) is agreed only when it happens. The rows land stream-ordered in the
 // handle's export buffers.
-__global__ void k_unpack_all(const int64_t *in, const int64_t *cnt_pre, int world, int64_t per_rows, int W,
+// every rank's gathered rows -> the export buffers, in rank order. The rank prefix is formed on
+// the device from the gathered row counts (sd_all: per int64 per rank, the count last), so no
+// host buffer has to outlive an asynchronous copy
+__global__ void k_unpack_all(const int64_t *in, const int64_t *sd_all, int per, int world, int64_t per_rows, int W,
                              int32_t *xy, uint64_t *bits) {
-    const int64_t total = cnt_pre[world];
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= total * (W + 1)) return;
     const int64_t row = e / (W + 1);
     const int c = (int)(e - row * (W + 1));
+    int64_t base = 0;
     int r = 0;
-    while (r + 1 < world && cnt_pre[r + 1] <= row) ++r;       // the rank whose rows hold `row`
-    const int64_t v = in[((int64_t)r * per_rows + (row - cnt_pre[r])) * (W + 1) + c];
+    for (; r < world; ++r) {              // the rank whose rows hold `row`
+        const int64_t cnt = sd_all[(int64_t)r * per + per - 1];
+        if (row < base + cnt) break;
+        base += cnt;
+    }
+    if (r >= world) return;               // beyond the last rank's rows
+    const int64_t v = in[((int64_t)r * per_rows + (row - base)) * (W + 1) + c];
     if (c == 0) {
         xy[2 * row] = (int32_t)(uint32_t)(v & 0xffffffffll);
         xy[2 * row + 1] = (int32_t)(uint32_t)((uint64_t)v >> 32);
@@ -503,7 +510,7 @@ int finish_sharded(pcg_handle *h) {
     const int64_t total = pre[world];
     const int64_t per_rows = mx, words = per_rows * (W + 1);
     const uint64_t a0 = h->alloc_events;
-    if (!pcg_ensure(h, h->comm_packed, sizeof(int64_t) * (size_t)words + sizeof(int64_t) * (world + 1)) ||
+    if (!pcg_ensure(h, h->comm_packed, sizeof(int64_t) * (size_t)words) ||
         !pcg_ensure(h, h->comm_gathered, sizeof(int64_t) * (size_t)words * world))
         local = pcg_fail(h, PCG_ERR_OOM, "sepset row gather (%lld rows x %d words)", (long long)mx, W + 1);
     if (h->alloc_events != a0) {    // grown (or failed to) on this rank, hence on every rank: agree
@@ -524,12 +531,10 @@ int finish_sharded(pcg_handle *h) {
         !pcg_ensure(h, h->export_xy, sizeof(int32_t) * 2 * (size_t)cap))
         return pcg_fail(h, PCG_ERR_OOM, "sepset export buffer");
     export_to_own(h, cap);             // every rank's rows land in the handle's own buffers
-    int64_t *pre_d = pk + words;          // the rank prefix, behind this rank's (already gathered) rows
-    PCG_HIP(h, hipMemcpyAsync(pre_d, pre.data(), sizeof(int64_t) * (world + 1), hipMemcpyHostToDevice, h->stream));
     const int64_t e = total * (W + 1);
     if (e > 0)
         hipLaunchKernelGGL(k_unpack_all, dim3((unsigned)((e + 255) / 256)), dim3(256), 0, h->stream,
-                           (const int64_t *)h->comm_gathered.p, (const int64_t *)pre_d, world, per_rows, W,
+                           (const int64_t *)h->comm_gathered.p, (const int64_t *)sd, per, world, per_rows, W,
                            (int32_t *)h->export_xy.p, (uint64_t *)h->exportbuf.p);
     PCG_HIP(h, hipGetLastError());
     h->export_rows = total;

@@ -565,8 +565,8 @@ def test_sepset_rows_in_engine_buffers_never_overwrite_live_results(eng):
     a = eng.skeleton(C1, 2000)                  # the copy path (learns the row bound)
     b = eng.skeleton(C1, 2000)                  # rows in the engine's buffer
     assert b.sep_xy_dev._base is not None and a.sep_xy_dev._base is None
-    np.testing.assert_array_equal(b.sep_xy, a.sep_xy)
-    np.testing.assert_array_equal(b.sep_bits, a.sep_bits)
+    # (rows are appended by atomics: their order differs run to run, the row sets do not)
+    assert unions_from_engine(b) == unions_from_engine(a) and len(b.sep_xy) == len(a.sep_xy)
     bxy = b.sep_xy_dev.cpu().numpy().copy()
     bbits = b.sep_bits_dev.cpu().numpy().copy()
     c = eng.skeleton(C2, 2000)                  # b is alive: another buffer
@@ -578,10 +578,10 @@ def test_sepset_rows_in_engine_buffers_never_overwrite_live_results(eng):
     del c
     d = eng.skeleton(C1, 2000)
     np.testing.assert_array_equal(kept.cpu().numpy(), kept_h)
-    np.testing.assert_array_equal(d.sep_bits, a.sep_bits)
+    assert unions_from_engine(d) == unions_from_engine(a)
     ref = cpc.skeleton(np.corrcoef(X1.T), 2000, want_union=True)
     assert unions_from_engine(d) == unions_from_oracle(ref, n)
     del kept, b
     e = eng.skeleton(C1, 2000)                  # nothing views the last buffer any more: reused
     assert e.sep_bits_dev._base is not None
-    np.testing.assert_array_equal(e.sep_bits, a.sep_bits)
+    assert unions_from_engine(e) == unions_from_engine(a)
