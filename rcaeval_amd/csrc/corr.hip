@@ -514,8 +514,12 @@ constexpr int CRT_KB = 4;                  // a slab's k-blocks are a multiple o
 #define PCG_CRT_PR 8
 #endif
 constexpr int CRT_PR = PCG_CRT_PR;         // LDS ring slots of one k-block (16 KB: A and B, 4 column blocks x 2 KB each)
-constexpr int CRT_PL = CRT_PR - 2;         // k-blocks in flight (a slot is restaged >= 2 phases after its last read)
-static_assert(CRT_PR * 16384 <= 160 * 1024 && CRT_PL >= 1, "CRT LDS ring");
+#ifndef PCG_CRT_KP
+#define PCG_CRT_KP 1
+#endif
+constexpr int CRT_KP = PCG_CRT_KP;         // k-blocks per phase (one block barrier each)
+constexpr int CRT_PL = CRT_PR - 2 * CRT_KP;   // k-blocks in flight (a slot is restaged >= 2 phases after its last read)
+static_assert(CRT_PR * 16384 <= 160 * 1024 && CRT_PL >= CRT_KP && CRT_PL % CRT_KP == 0, "CRT LDS ring");
 constexpr int CRT_MAXKB = 4095;            // k-blocks per slab: 4095 x 32 x 128^2 < 2^31
 constexpr int CRT_UNIT = CRT_T * CRT_T;    // residue bytes per (tile, modulus, slab)
 static const int kCrtModuli[CRT_KMAX] = {256, 255, 253, 251, 247, 241, 239, 233, 229, 227, 223, 217,
@@ -765,43 +769,56 @@ __global__ __launch_bounds__(512, 1) void k_xtx_crt(const int8_t *R, int TB, int
     };
     const unsigned char *fa0 = smem + (2 * wr * 2048 + hh * 1024 + r * 16);
     const unsigned char *fb0 = smem + (8192 + wc * 2048 + hh * 1024 + r * 16);
-    v4i af[2][4], bf[2][2];
+    v4i af[2][CRT_KP][4], bf[2][CRT_KP][2];
+    // the fragments of k-blocks g .. g + KP - 1 into buffer sl
     auto frag = [&](int g, int sl) {
-        const int off = (g % CRT_PR) * 16384;
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
-            af[sl][a] = *reinterpret_cast<const v4i *>(fa0 + off + (a >> 1) * 2048 + (a & 1) * 512);
+        for (int kk = 0; kk < CRT_KP; ++kk) {
+            const int off = ((g + kk) % CRT_PR) * 16384;
 #pragma unroll
-        for (int b = 0; b < 2; ++b) bf[sl][b] = *reinterpret_cast<const v4i *>(fb0 + off + b * 512);
+            for (int a = 0; a < 4; ++a)
+                af[sl][kk][a] = *reinterpret_cast<const v4i *>(fa0 + off + (a >> 1) * 2048 + (a & 1) * 512);
+#pragma unroll
+            for (int b = 0; b < 2; ++b) bf[sl][kk][b] = *reinterpret_cast<const v4i *>(fb0 + off + b * 512);
+        }
     };
+    // (KP > 1: a phase covers KP k-blocks — one barrier per KP k-blocks; a slot is restaged two
+    // phases after the phase whose fragment reads were its last; the tail's k-blocks past nkb are
+    // re-staged copies of the last one and their MFMAs are skipped)
 #pragma unroll
     for (int g = 0; g < CRT_PL; ++g) stage(g);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (CRT_PL - 1)) : "memory");   // k-block 0 (own DMAs)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (CRT_PL - CRT_KP)) : "memory");   // the first phase's k-blocks
     __builtin_amdgcn_s_barrier();
     frag(0, 0);
-    for (int p = 0; p < nkb; p += 2) {
-        // two phases per iteration, so the fragment buffers stay compile-time (p even: buffer 0)
+    for (int p = 0; p < nkb; p += 2 * CRT_KP) {
+        // two phases per iteration, so the fragment buffers stay compile-time (first phase: buffer 0)
 #pragma unroll
         for (int h2 = 0; h2 < 2; ++h2) {
-            const int q = p + h2;
+            const int q = p + h2 * CRT_KP;
             if (q < nkb) {
-                stage(q + CRT_PL);
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (CRT_PL - 1)) : "memory");   // k-block q + 1
+#pragma unroll
+                for (int kk = 0; kk < CRT_KP; ++kk) stage(q + CRT_PL + kk);
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (CRT_PL - CRT_KP)) : "memory");   // the next phase's
                 __builtin_amdgcn_s_barrier();
-                const bool nxt = q + 1 < nkb;
-                if (nxt) frag(q + 1, h2 ^ 1);
+                const bool nxt = q + CRT_KP < nkb;
+                if (nxt) frag(q + CRT_KP, h2 ^ 1);
 #pragma unroll
-                for (int a = 0; a < 4; ++a)
+                for (int kk = 0; kk < CRT_KP; ++kk) {
+                    if (kk > 0 && q + kk >= nkb) break;      // (wave-uniform)
 #pragma unroll
-                    for (int b = 0; b < 2; ++b)
-                        acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[h2][a], bf[h2][b], acc[a][b], 0, 0, 0);
+                    for (int a = 0; a < 4; ++a)
+#pragma unroll
+                        for (int b = 0; b < 2; ++b)
+                            acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[h2][kk][a], bf[h2][kk][b], acc[a][b],
+                                                                              0, 0, 0);
+                }
                 if (nxt) {
 #pragma unroll
-                    for (int u = 0; u < 6; ++u) {
+                    for (int u = 0; u < 6 * CRT_KP; ++u) {
                         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
                         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // 1 DS read
                     }
-                    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 2 * CRT_KP, 0);
                 }
             }
         }

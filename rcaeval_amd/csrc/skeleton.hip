@@ -2311,6 +2311,9 @@ __device__ unsigned long long g_tgf_prof[8];   // block, staging, setup, sweep c
 #define PCG_TGF_SPLIT 1   // k_level_lds_f, one candidate window per wave: y outside the window without the
                           // dead-candidate selects (depth 4: 2.24 -> 2.09 ms once the rare-path values were opaque)
 #endif
+#ifndef PCG_TGF_SR
+#define PCG_TGF_SR 4      // k_level_lds_f, narrow class gathering A~ from C: rows per wave with loads in flight
+#endif
 #ifndef PCG_MBF2
 #define PCG_MBF2 4
 #endif
@@ -2468,7 +2471,7 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
     } else {   // rows of A~ and of the local adjacency masks: a wave takes SR rows at a time, lane k
         // column k (its global id hoisted), so SR x (C entry, adjacency word) loads are in flight
         // per lane before the first is used; no index division
-        constexpr int H = 1, SR = 4;
+        constexpr int H = 1, SR = PCG_TGF_SR;
         const int lane = tid & 63, wv = tid >> 6, nwv = bs >> 6;
         int kg[H];
 #pragma unroll
@@ -4046,8 +4049,13 @@ __global__ __launch_bounds__(SMALL_WAVES * 64, 1) void k_pc_small(SmallArgs a) {
         uni[e] = 0;
         rlv[e] = -1;
     }
-    for (int e = tid; e < SMALL_N * (SMALL_MAXD + 1); e += blockDim.x)
-        bin[e] = pcg_binom(a.binom, e / (SMALL_MAXD + 1), e % (SMALL_MAXD + 1));
+    // the handle's table holds rows 0..n only (build_binom(n)): rows past n are never indexed here
+    // (degrees stay < n) and are zeroed, not read — reading them ran past a fresh handle's small
+    // allocation (an intermittent illegal address, r06)
+    for (int e = tid; e < SMALL_N * (SMALL_MAXD + 1); e += blockDim.x) {
+        const int c = e / (SMALL_MAXD + 1);
+        bin[e] = c <= n ? pcg_binom(a.binom, c, e % (SMALL_MAXD + 1)) : 0ull;
+    }
     const unsigned long long all = n == 64 ? ~0ull : ((1ull << n) - 1ull);
     for (int x = tid; x < SMALL_N; x += blockDim.x) {
         adjm[x] = x < n ? all & ~(1ull << x) : 0ull;
