@@ -124,6 +124,7 @@ struct LevelArgs {
     const int64_t *bo;           // n + 1 offsets of the compact blocks (doubles)
     double *cblk;                // per node: C[adj(x) + x, adj(x) + x], stride D + 1, x last
     uint64_t *lmk;               // per node: local adjacency masks of adj(x), at off[x]
+    int img;                     // cblk holds fp32 LDS images of k_level_lds_f (tgf_image_bytes each) instead
     int stamp_end;               // block 0 stamps ctr->t_run1 at entry (the kernel bracket's end)
 };
 
@@ -2259,6 +2260,16 @@ __global__ __launch_bounds__(256, WIDE ? 1 : tg_minblocks(DM)) void k_level_lds_
 // decides it like the fp64 kernels (band -> exact path). Decisions are therefore the fp64
 // kernels' decisions; only where the fp32 sweep is certain does it decide.
 typedef float f2v __attribute__((ext_vector_type(2)));
+#ifndef PCG_NODE_IMG
+#define PCG_NODE_IMG 1    // compact node blocks as fp32 LDS images of k_level_lds_f (DMA-staged), else fp64 rows
+#endif
+// k_level_lds_f's staged region of a node of degree D: M (D rows of DS floats, columns >= D zero),
+// the DS y records (2 mb bytes each) and nxs (DS ints). Narrow (mb = 8): rounded to 1 KB, the unit a
+// wave's LDS-DMA instruction writes (64 lanes x 16 B), so a node image is copied whole
+__host__ __device__ constexpr int tgf_image_bytes(int D, int mb) {
+    return mb == 8 ? (4 * D * ((D + 3) & ~3) + (2 * mb + 4) * ((D + 3) & ~3) + 1023) & ~1023
+                   : (4 * D * ((D + 3) & ~3) + (2 * mb + 4) * ((D + 3) & ~3) + 15) & ~15;
+}
 struct alignas(16) YRecN {       // k_level_lds_f (narrow): a y's {A~_yy, A~_xy} and local adjacency mask
     f2v md;
     unsigned long long lm;
@@ -2313,6 +2324,19 @@ __device__ unsigned long long g_tgf_prof[8];   // block, staging, setup, sweep c
 #endif
 #ifndef PCG_TGF_SR
 #define PCG_TGF_SR 4      // k_level_lds_f, narrow class gathering A~ from C: rows per wave with loads in flight
+#endif
+#ifndef PCG_NB3_TARGET
+#define PCG_NB3_TARGET 4096   // narrow-class block target at depth 3 (level_begin_impl)
+#endif
+#ifndef PCG_NB4_TARGET
+#define PCG_NB4_TARGET 16384  // ... at depth 4
+#endif
+#ifndef PCG_TGF_NSKIP
+#define PCG_TGF_NSKIP 1   // lane-mask sweep: the node's memo skips counted once in closed form, so a lane that
+                          // owns y no longer takes the rare path just to subtract its skips
+#endif
+#ifndef PCG_TGF_PRIO
+#define PCG_TGF_PRIO 0    // k_level_lds_f depths (bit 1 << d) whose staging runs at raised wave priority (s_setprio)
 #endif
 #ifndef PCG_MBF2
 #define PCG_MBF2 4
@@ -2406,28 +2430,46 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
     unsigned long long prof_setup = 0, prof_sweep = 0, prof_tasks = 0, prof_y = 0, prof_stage = 0;
 #endif
     const int DS = (D + 3) & ~3;                                  // padded length / row stride
-    Mask *lmask = reinterpret_cast<Mask *>(smem);                 // DS
-    Mask *uself = lmask + DS;                                     // DS
-    Mask *uprop = uself + DS;                                     // DS
-    float *M = reinterpret_cast<float *>(uprop + DS);             // D * DS (columns >= D zero)
+    // the staged region first (a node image, tgf_image_bytes: one DMA copy when k_node_blocks_t
+    // built it), then the union masks and two ints
+    float *M = reinterpret_cast<float *>(smem);                   // D * DS (columns >= D zero)
     // one 16-byte (wide: 32-byte) record per y: {A~_yy, A~_xy, [pad,] local adjacency mask}, so the
     // sweep reads a y's wave-uniform operands with one LDS instruction
     constexpr int YS = WIDE ? 8 : 4;                              // floats per record
     float *Yr = M + D * DS;                                       // DS records, 16-B aligned
     int32_t *nxs = reinterpret_cast<int32_t *>(Yr + YS * DS);    // DS
-    int *s_tx = nxs + DS;                                         // 1
+    const int img_b = tgf_image_bytes(D, (int)sizeof(Mask));
+    Mask *uself = reinterpret_cast<Mask *>(smem + img_b);         // DS
+    Mask *uprop = uself + DS;                                     // DS
+    int *s_tx = reinterpret_cast<int *>(uprop + DS);              // 1
     int *s_np = s_tx + 1;                                         // 1
     unsigned *btab = reinterpret_cast<unsigned *>(smem + a.lds_btab_off);   // C(c, i), c <= D, i <= DM
     unsigned *ppre = btab + (D + 1) * (DM + 1);                   // task prefix per (g, t0) pair
     unsigned short *pinfo = reinterpret_cast<unsigned short *>(ppre + tg_pairs(D, DM) + 1);  // g << 8 | t0
 
-    for (int i = tid; i < D; i += bs) nxs[i] = nxg[i];
+    constexpr bool PRIO = (PCG_TGF_PRIO >> DM) & 1;
+    if (PRIO) __builtin_amdgcn_s_setprio(3);
+    const bool img = !WIDE && a.img;
+    if (img) {
+        // the node's image (M, the y records, nxs) by LDS-DMA, 1 KB per wave instruction, every
+        // piece in flight at once (no VGPR round trip, one memory latency); the binomial table's
+        // loads below overlap it
+        const unsigned char *src = reinterpret_cast<const unsigned char *>(a.cblk + a.bo[x]);
+        const int lane = tid & 63, wv = tid >> 6, nwv = bs >> 6;
+        for (int off = wv * 1024; off < img_b; off += nwv * 1024)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + off + lane * 16),
+                                             (__attribute__((address_space(3))) void *)(smem + off), 16, 0, 0);
+    } else {
+        for (int i = tid; i < D; i += bs) nxs[i] = nxg[i];
+    }
     for (int e = tid; e < (D + 1) * (DM + 1); e += bs) {
         const int c = e / (DM + 1), i = e - c * (DM + 1);
         btab[e] = (unsigned)pcg_binom(a.binom, c, i);
     }
+    if (img) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's image pieces landed
     __syncthreads();
-    if (!WIDE && a.cblk) {   // this depth's compact node block (k_node_blocks): coalesced rows
+    if (img) {
+    } else if (!WIDE && a.cblk) {   // this depth's compact node block (k_node_blocks): coalesced rows
         // a wave loads SR rows before storing any (SR loads in flight per lane, not one dependent
         // round trip per row; SR = 8 spilled 4 more VGPRs in the sweep); the masks a lane each
         constexpr int SR = 4;
@@ -2446,10 +2488,7 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
                 if (lane < DS) M[t * DS + lane] = (float)v[r];
             }
         }
-        for (int t = tid; t < D; t += bs) {
-            lmask[t] = (Mask)lk[t];
-            *reinterpret_cast<Mask *>(Yr + YS * t + (WIDE ? 4 : 2)) = (Mask)lk[t];
-        }
+        for (int t = tid; t < D; t += bs) *reinterpret_cast<Mask *>(Yr + YS * t + (WIDE ? 4 : 2)) = (Mask)lk[t];
     } else if constexpr (WIDE) {   // (the row-batched form below measured slower for the 128-wide blocks)
         for (int e = tid; e < D * DS; e += bs) {
             const int t = e / DS, k = e - t * DS;
@@ -2463,10 +2502,7 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
                 const bool bit = k < D && ((ar[nxs[k] >> 6] >> (nxs[k] & 63)) & 1ull);
                 m |= (Mask)__ballot(bit) << k0;
             }
-            if ((tid & 63) == 0) {
-                lmask[t] = m;
-                *reinterpret_cast<Mask *>(Yr + YS * t + (WIDE ? 4 : 2)) = m;
-            }
+            if ((tid & 63) == 0) *reinterpret_cast<Mask *>(Yr + YS * t + (WIDE ? 4 : 2)) = m;
         }
     } else {   // rows of A~ and of the local adjacency masks: a wave takes SR rows at a time, lane k
         // column k (its global id hoisted), so SR x (C entry, adjacency word) loads are in flight
@@ -2502,17 +2538,16 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
                     const bool bit = kg[hh] >= 0 && ((w[r][hh] >> (kg[hh] & 63)) & 1ull);
                     m |= (Mask)__ballot(bit) << (64 * hh);
                 }
-                if (lane == 0) {
-                    lmask[t] = m;
-                    *reinterpret_cast<Mask *>(Yr + YS * t + (WIDE ? 4 : 2)) = m;
-                }
+                if (lane == 0) *reinterpret_cast<Mask *>(Yr + YS * t + (WIDE ? 4 : 2)) = m;
             }
         }
     }
     for (int t = tid; t < D; t += bs) {
-        const int yg = nxs[t];
-        Yr[YS * t] = (float)a.diag[yg];
-        Yr[YS * t + 1] = (float)a.C[(int64_t)x * a.ldc + yg];
+        if (!img) {
+            const int yg = nxs[t];
+            Yr[YS * t] = (float)a.diag[yg];
+            Yr[YS * t + 1] = (float)a.C[(int64_t)x * a.ldc + yg];
+        }
         uself[t] = 0;
         uprop[t] = 0;
     }
@@ -2534,6 +2569,7 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
     const int tx = *s_tx;
     const int np = *s_np;
     const Mask recm = REC ? s_recm : (Mask)0;   // (threshold-mode builds: no record code in the sweep)
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
 #if PCG_TGF_PROF
     if (PROF) prof_stage = clock64() - prof_t0;
 #endif
@@ -2544,6 +2580,19 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
     constexpr int ABL = (DM == PCG_TGF_ABL_D && !WIDE) ? PCG_TGF_ABL : 0;
     const uint64_t r1 = (ABL & 2) ? r0 : min(ntask, r0 + (uint64_t)bs * spl);   // (ablation: no tasks)
     unsigned long long tests = 0, indep = 0;
+    constexpr bool SGK = (PCG_TGF_SGPR >> DM) & 1;
+    if (SGK && PCG_TGF_NSKIP && chunk == a.cpre[x]) {
+        // the lane-mask sweep counts every (y, S) of its tasks; the node's first chunk takes back
+        // the memo skips in closed form: (x, y, S) with y < x (t < tx) and S within adj(y) is y's
+        // test (SkeletonDiscovery.py's cache hit), C(|adj(x) & adj(y)|, d) of them per such y
+        for (int t = tid; t < tx; t += bs) {
+            const Mask lm = *reinterpret_cast<const Mask *>(Yr + YS * t + (WIDE ? 4 : 2));
+            int c;
+            if constexpr (WIDE) c = __popcll((unsigned long long)lm) + __popcll((unsigned long long)(lm >> 64));
+            else c = __popcll(lm);
+            tests -= btab[c * (DM + 1) + DM];
+        }
+    }
     unsigned tcount = 0;
     const unsigned long long lanebit = 1ull << (tid & 63);
     const float inv_sf = (float)a.inv_s;                          // rounding covered by the check's margins
@@ -2978,7 +3027,7 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
                 const bool recy = REC && (bool)((recm >> t) & 1u);     // wave-uniform
                 unsigned long long rarel = ((~dall & __builtin_amdgcn_read_exec()) | notok) & ~inT;
                 if (YM == 2) rarel |= __builtin_amdgcn_ballot_w64((unsigned)(t - cbase) < (unsigned)nval);
-                if (t < tx) rarel |= __builtin_amdgcn_ballot_w64((lm & Tmask) == Tmask) & ~inT;
+                if (!PCG_TGF_NSKIP && t < tx) rarel |= __builtin_amdgcn_ballot_w64((lm & Tmask) == Tmask) & ~inT;
                 if (recy) rarel = __builtin_amdgcn_read_exec() & ~inT;
                 if (!rarel) return;
                 if (!(rarel & lanebit)) return;
@@ -2988,7 +3037,7 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
                 const unsigned skip = own ? (unsigned)(lm >> cbase) : 0u;
                 if ((Tmask >> t) & 1u) return;
                 const unsigned live = vmask & ~tb & ~skip;
-                tcount -= __popc(vmask & ~tb & skip);
+                if (!PCG_TGF_NSKIP) tcount -= __popc(vmask & ~tb & skip);
 #pragma unroll
                 for (int jj = 0; jj < TG; ++jj)
                     if ((live >> jj) & 1u) {
@@ -3189,6 +3238,11 @@ __global__ __launch_bounds__(256) void k_node_blocks(LevelArgs a, int64_t s_lo, 
 // cb_x[iy][k] = C[y][ids_x[k]] from LDS, and (iy < D_x) x's local mask of y. A wave per target
 // node; its rows are contiguous writes. k_node_blocks gathers the same entries from C's
 // scattered columns — FETCH ~13x the block bytes at config 5's depth 4.
+// IMG: the blocks are k_level_lds_f's fp32 LDS images instead (tgf_image_bytes, at bo[x] doubles):
+// row iy of M = fp32(C[y][ids_x[k]]) (zero-padded to DS), y's record {fp32(C[y][y]), ., local mask},
+// and from x's own row (y = x) every record's fp32(C[x][ids_x[k]]) and the id list — the values the
+// kernel's own staging computes, so the sweep's results are unchanged
+template <bool IMG>
 __global__ __launch_bounds__(256) void k_node_blocks_t(LevelArgs a, int64_t s_lo, int64_t s_hi, int maxdeg) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     double *row = reinterpret_cast<double *>(smem);
@@ -3227,7 +3281,26 @@ __global__ __launch_bounds__(256) void k_node_blocks_t(LevelArgs a, int64_t s_lo
     for (int t = wv; t <= Dy; t += nwv) {
         const int gn = t + nwv <= Dy ? load(t + nwv) : 0;
         const int x = tx[t];
-        if (x >= 0) {
+        if (IMG && x >= 0) {
+            const int D = tD[t], DS = (D + 3) & ~3;
+            float *img = reinterpret_cast<float *>(a.cblk + tbo[t]);
+            float *Yr = img + D * DS;
+            if (x == y) {
+                if (lane < D) {
+                    Yr[4 * lane + 1] = (float)row[g];
+                    reinterpret_cast<int32_t *>(Yr + 4 * DS)[lane] = g;
+                }
+            } else {
+                const int iy = __popcll(__ballot(lane < D && g < y));
+                if (lane < DS) img[iy * DS + lane] = lane < D ? (float)row[g] : 0.0f;
+                const bool bit = lane < D && ((arow[g >> 6] >> (g & 63)) & 1ull);
+                const unsigned long long m = __ballot(bit);
+                if (lane == 0) {
+                    Yr[4 * iy] = (float)row[y];
+                    *reinterpret_cast<unsigned long long *>(Yr + 4 * iy + 2) = m;
+                }
+            }
+        } else if (x >= 0) {
             const int D = tD[t], L = D + 1;
             const int iy = x == y ? D : __popcll(__ballot(lane < D && g < y));
             double *cb = a.cblk + tbo[t] + (int64_t)iy * L;
@@ -4467,6 +4540,7 @@ LevelArgs make_args(pcg_handle *h, int d, int mode_exact_all) {
         a.bo = (const int64_t *)h->cpre.p + h->bo_off;
         a.cblk = (double *)h->cblk.p;
         a.lmk = (uint64_t *)h->lmk.p;
+        a.img = h->nimg ? 1 : 0;
     }
     (void)mode_exact_all;
     return a;
@@ -4540,8 +4614,9 @@ size_t lds_tgroup_bytes(int D, int DM, int mask_bytes = 8) {
 // k_level_lds_f (D padded to 4): three mask arrays, fp32 M, the y records, nxs, two ints; then the
 // same binomial table and task prefix as k_level_lds_t
 size_t lds_f32_core(int D, int mask_bytes) {
-    // (y records: 16 B per y with 8-byte masks, 32 B with 16-byte ones; nxs 4 B)
-    return ((size_t)D * 3 * mask_bytes + (size_t)D * D * 4 + (size_t)D * (2 * mask_bytes + 4) + 8 + 15) & ~(size_t)15;
+    // (the staged region, tgf_image_bytes: M, y records of 16 B per y with 8-byte masks, 32 B with
+    // 16-byte ones, nxs 4 B; then two union mask arrays and two ints)
+    return ((size_t)tgf_image_bytes(D, mask_bytes) + (size_t)D * 2 * mask_bytes + 8 + 15) & ~(size_t)15;
 }
 size_t lds_tgroup_f_bytes(int D, int DM, int mask_bytes) {
     const size_t np = (size_t)tg_pairs(D, DM);
@@ -4883,6 +4958,7 @@ int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks) {
     int64_t *cs = h->cpre_h.data(), *cw = cs + (n + 1), *cl = cw + (n + 1);
     std::vector<int64_t> bo;           // compact-block offsets (doubles, k_node_blocks)
     h->nblk = false;
+    h->nimg = false;
     h->work_h.assign(n, 0);
     h->maxdeg_small = 0;
     h->maxdeg_wide = 0;
@@ -4923,6 +4999,9 @@ int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks) {
         h->screen_eff &= 0x1c;   // the error bound (KE = 64) is derived for d = 2..4 only
         // compact node blocks (k_node_blocks) for the narrow class of the fp32-screened sweeps
         h->nblk = tg && use_screen32(h, depth) && ((h->tune[PCG_TUNE_NODE_BLOCKS] >> depth) & 1);
+        // ... as fp32 LDS images when the transposed builder's row of C fits its LDS
+        h->nimg = h->nblk && PCG_NODE_IMG && PCG_NBLK_T &&
+                  8 * (size_t)n + 8 * (size_t)h->W + (size_t)(maxd + 1) * (sizeof(int64_t) + 3 * sizeof(int)) <= 64 * 1024;
         std::vector<uint64_t> ns_of(maxd + 1, 0), units_of(maxd + 1, 0);
         std::vector<int> cls_of(maxd + 1, 2);
         double sum_small = 0.0, sum_wide = 0.0, sum_large = 0.0;
@@ -4950,7 +5029,8 @@ int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks) {
         // 4, whose long per-node task lists otherwise leave a tail (measured 2.53 -> 2.40 ms; depth
         // 3 is best at 4096); each lane walks spl units. The wide class (a few nodes) aims at ~512
         // blocks so its nodes are spread over the chip. PCG_TUNE_NB / PCG_TUNE_NBW override.
-        const double nb_target = h->tune[PCG_TUNE_NB] > 0 ? (double)h->tune[PCG_TUNE_NB] : (depth == 4 ? 16384.0 : 4096.0);
+        const double nb_target = h->tune[PCG_TUNE_NB] > 0 ? (double)h->tune[PCG_TUNE_NB]
+                                 : (depth == 4 ? (double)PCG_NB4_TARGET : depth == 3 ? (double)PCG_NB3_TARGET : 4096.0);
         // lanes per block: 256 S ranks / T-group tasks, or 4 conditioning sets (k_level_wave: a
         // wave each, sharing the factorisation along a wave's run of sets: longer runs there)
         const double per_block = h->wavek ? 4.0 : 256.0;
@@ -4981,7 +5061,7 @@ int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks) {
             h->work_h[x] = (int64_t)ns_of[D] * (D - depth);
             const int c = cls_of[D];
             (c == 0 ? ss : c == 1 ? sw : sl) += nch_of[D];
-            if (h->nblk && c == 0) sb += (int64_t)(D + 1) * (D + 1);
+            if (h->nblk && c == 0) sb += h->nimg ? tgf_image_bytes(D, 8) / 8 : (int64_t)(D + 1) * (D + 1);
         }
         if (h->nblk) bo[n] = sb;
         cs[n] = ss;
@@ -5258,9 +5338,12 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                                 // built transposed (C's rows staged in LDS) when a row fits
                                 const size_t tl = sizeof(double) * (size_t)h->n + sizeof(uint64_t) * (size_t)h->W +
                                                   (size_t)(h->maxdeg + 1) * (sizeof(int64_t) + 3 * sizeof(int));
-                                if (PCG_NBLK_T && tl <= 64 * 1024)
-                                    hipLaunchKernelGGL(k_node_blocks_t, dim3((unsigned)h->n), dim3(256), tl, h->stream, as, s_lo, s_hi,
-                                                       (int)h->maxdeg);
+                                if (h->nimg)
+                                    hipLaunchKernelGGL(k_node_blocks_t<true>, dim3((unsigned)h->n), dim3(256), tl, h->stream, as, s_lo,
+                                                       s_hi, (int)h->maxdeg);
+                                else if (PCG_NBLK_T && tl <= 64 * 1024)
+                                    hipLaunchKernelGGL(k_node_blocks_t<false>, dim3((unsigned)h->n), dim3(256), tl, h->stream, as, s_lo,
+                                                       s_hi, (int)h->maxdeg);
                                 else
                                     hipLaunchKernelGGL(k_node_blocks, dim3((unsigned)h->n), dim3(256), 0, h->stream, as, s_lo, s_hi);
                             }
