@@ -142,6 +142,8 @@ struct pcg_handle {
     bool nimg = false;               // ... as fp32 LDS images of k_level_lds_f (k_node_blocks_t<true>)
     DevBuf cblk, lmk;                // k_node_blocks: per-node compact correlation blocks, local masks
     int64_t bo_off = 0;              // int64 offset of the compact-block offsets in cpre / cpre_pin
+    int64_t lpt_off = 0;             // ... of k_level_lds_f's dispatch order (int32 nps, then nord)
+    int nlpt = 0;                    // nodes in that order (0: canonical order)
     hipEvent_t rev[PCG_MAX_LEVELS][2] = {};   // per-depth CI-test kernel brackets
     int64_t near_seen = 0;           // near-alpha entries copied so far (the device list accumulates)
     int64_t near_total_dev = 0;      // the device's cumulative near-alpha count at the last level end

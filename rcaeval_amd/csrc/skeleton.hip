@@ -125,6 +125,11 @@ struct LevelArgs {
     double *cblk;                // per node: C[adj(x) + x, adj(x) + x], stride D + 1, x last
     uint64_t *lmk;               // per node: local adjacency masks of adj(x), at off[x]
     int img;                     // cblk holds fp32 LDS images of k_level_lds_f (tgf_image_bytes each) instead
+    // k_level_lds_f's dispatch order (a launch over the whole narrow class): block b runs the b-th
+    // chunk of the nodes taken by degree, largest first (nord: nodes, nps: their chunk prefix), so
+    // the level's last blocks are its shortest ones
+    const int32_t *nord, *nps;
+    int nm;
     int stamp_end;               // block 0 stamps ctr->t_run1 at entry (the kernel bracket's end)
 };
 
@@ -582,6 +587,22 @@ __device__ __forceinline__ int chunk_node(const int64_t *cpre, int n, int64_t ch
         const int idx = lo + lane * step;
         const bool le = idx < hi && cpre[idx] <= chunk;   // a prefix of the lanes (cpre ascends)
         const unsigned long long b = __ballot(le);        // lane 0 always set
+        const int j = 63 - __builtin_clzll(b);
+        lo += j * step;
+        hi = min(hi, lo + step);
+    }
+    return lo;
+}
+
+// chunk_node over an int32 prefix (LevelArgs::nps)
+__device__ __forceinline__ int chunk_node32(const int32_t *pre, int n, int v) {
+    const int lane = threadIdx.x & 63;
+    int lo = 0, hi = n;                                   // pre[lo] <= v < pre[hi]
+    while (hi - lo > 1) {
+        const int step = (hi - lo + 63) >> 6;
+        const int idx = lo + lane * step;
+        const bool le = idx < hi && pre[idx] <= v;
+        const unsigned long long b = __ballot(le);
         const int j = 63 - __builtin_clzll(b);
         lo += j * step;
         hi = min(hi, lo + step);
@@ -2312,6 +2333,15 @@ constexpr double F32_U = 5.9604644775390625e-08;   // 2^-24
 #define PCG_TGF_PROF 0    // diagnostic builds only: per-phase shader-clock cycles of k_level_lds_f at depth
                           // PCG_TGF_PROF (narrow class) summed into g_tgf_prof, printed per level to stderr
 #endif
+#ifndef PCG_TGF_BLKT
+#define PCG_TGF_BLKT 0    // diagnostic builds only: per-block wall-clock (start, end, D, tasks) of k_level_lds_f at
+                          // depth PCG_TGF_BLKT (narrow class: g_blkt, wide: g_blkw), summarised per level on stderr
+#endif
+#if PCG_TGF_BLKT
+constexpr int BLKT_MAX = 32768;
+__device__ unsigned long long g_blkt[BLKT_MAX][4];
+__device__ unsigned long long g_blkw[4096][4];
+#endif
 #if PCG_TGF_PROF
 __device__ unsigned long long g_tgf_prof[8];   // block, staging, setup, sweep cycles (per wave); tasks; y iters; waves
 #endif
@@ -2330,6 +2360,11 @@ __device__ unsigned long long g_tgf_prof[8];   // block, staging, setup, sweep c
 #endif
 #ifndef PCG_NB4_TARGET
 #define PCG_NB4_TARGET 16384  // ... at depth 4
+#endif
+#ifndef PCG_TGF_LPT
+#define PCG_TGF_LPT 0x10  // depths (bit 1 << d) whose k_level_lds_f narrow class is dispatched largest degree first
+                          // (LevelArgs::nord; config 5 depth 4: kernel 1.715-1.74 -> 1.69-1.70 ms A/B; depth 3
+                          // measured 0.68-0.69 -> 0.69-0.72: its largest-degree blocks staged together first)
 #endif
 #ifndef PCG_TGF_NSKIP
 #define PCG_TGF_NSKIP 1   // lane-mask sweep: the node's memo skips counted once in closed form, so a lane that
@@ -2417,13 +2452,25 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x;
     const int bs = blockDim.x;
-    const int64_t chunk = a.chunk_lo + blockIdx.x;
-    if (chunk >= a.cpre[a.n]) return;   // (defensive: launches are sized by the exact prefix)
-    int lo = chunk_node(a.cpre, a.n, chunk);
-    const int x = lo;
+    int64_t chunk;
+    int x;
+    if (!WIDE && a.nord) {   // largest degree first: block b -> (node position i, its chunk b - nps[i])
+        const int b = (int)blockIdx.x;
+        if (b >= a.nps[a.nm]) return;
+        const int i = chunk_node32(a.nps, a.nm, b);
+        x = a.nord[i];
+        chunk = a.cpre[x] + (b - a.nps[i]);
+    } else {
+        chunk = a.chunk_lo + blockIdx.x;
+        if (chunk >= a.cpre[a.n]) return;   // (defensive: launches are sized by the exact prefix)
+        x = chunk_node(a.cpre, a.n, chunk);
+    }
     const int D = a.deg[x];
     const int32_t *nxg = a.nbr + a.off[x];
 
+#if PCG_TGF_BLKT
+    const unsigned long long blkt0 = wall_clock64();
+#endif
 #if PCG_TGF_PROF
     constexpr bool PROF = !WIDE && !REC && DM == PCG_TGF_PROF;
     const unsigned long long prof_t0 = PROF ? clock64() : 0ull;
@@ -3146,6 +3193,13 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
         }
     }
     block_flush_counts(a.ctr, tests, indep);
+#if PCG_TGF_BLKT
+    if (DM == PCG_TGF_BLKT && !REC && tid == 0) {
+        unsigned long long *e = WIDE ? (blockIdx.x < 4096 ? g_blkw[blockIdx.x] : nullptr)
+                                     : (blockIdx.x < BLKT_MAX ? g_blkt[blockIdx.x] : nullptr);
+        if (e) { e[0] = blkt0; e[1] = wall_clock64(); e[2] = (unsigned long long)D; e[3] = r1 - r0; }
+    }
+#endif
 }
 
 // The fp64 screen of the tests the fp32 sweep handed over (one lane per test, after the level
@@ -5073,10 +5127,36 @@ int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks) {
     }
     h->total_chunks = h->total_small + h->total_wide + h->total_large;
     if (total_chunks) *total_chunks = h->total_chunks;
+    // k_level_lds_f's dispatch order (narrow class): the nodes with narrow chunks by degree, largest
+    // first (a counting sort), and their chunk prefix in that order — a block's time grows with D,
+    // so the level's tail is made of its shortest blocks (int32, packed after the other arrays)
+    h->nlpt = 0;
+    std::vector<int32_t> lpt;
+    if (((PCG_TGF_LPT >> depth) & 1) && depth >= 1 && h->tgroup && !h->wavek && use_screen32(h, depth) && h->total_small > 0) {
+        const int64_t *cs = h->cpre_h.data();
+        const int maxd = h->maxdeg;
+        std::vector<int32_t> st(maxd + 2, 0);
+        int m = 0;
+        for (int x = 0; x < n; ++x)
+            if (cs[x + 1] > cs[x]) { ++st[h->deg_h[x]]; ++m; }
+        for (int D = maxd, pos = 0; D >= 0; --D) {
+            const int c = st[D];
+            st[D] = pos;
+            pos += c;
+        }
+        lpt.assign(2 * (size_t)m + 1, 0);
+        int32_t *nps = lpt.data(), *nord = nps + m + 1;
+        for (int x = 0; x < n; ++x)
+            if (cs[x + 1] > cs[x]) nord[st[h->deg_h[x]]++] = x;
+        for (int i = 0; i < m; ++i) nps[i + 1] = nps[i] + (int32_t)(cs[nord[i] + 1] - cs[nord[i]]);
+        h->nlpt = m;
+    }
     PCG_HT(h, "begin:decomposed");
-    // host-mapped upload: the three class prefixes, then (k_node_blocks) the compact-block offsets
+    // host-mapped upload: the three class prefixes, then (k_node_blocks) the compact-block offsets,
+    // then the dispatch order
     h->bo_off = 3 * (int64_t)(n + 1);
-    const int64_t cnt = h->bo_off + (h->nblk ? (int64_t)(n + 1) : 0);
+    h->lpt_off = h->bo_off + (h->nblk ? (int64_t)(n + 1) : 0);
+    const int64_t cnt = h->lpt_off + ((int64_t)lpt.size() + 1) / 2;
     if (!pcg_ensure_pinned(h, h->cpre_pin, sizeof(int64_t) * cnt))
         return pcg_fail(h, PCG_ERR_OOM, "pinned chunk prefix");
     {
@@ -5088,6 +5168,7 @@ int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks) {
                 !pcg_ensure(h, h->lmk, sizeof(uint64_t) * std::max<int64_t>(h->sumdeg, 1)))
                 return pcg_fail(h, PCG_ERR_OOM, "compact node blocks");
         }
+        if (!lpt.empty()) memcpy(pin + h->lpt_off, lpt.data(), sizeof(int32_t) * lpt.size());
     }
     if (!pcg_ensure(h, h->cpre, sizeof(int64_t) * cnt)) return PCG_ERR_OOM;
     // rm, the counters and the status bytes were cleared by the previous depth's k_level_close /
@@ -5350,6 +5431,11 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                             as.lds_btab_off = (int)lds_f32_core(dl, 8);
                             const size_t ldsf = lds_tgroup_f_bytes(dl, d, 8);
                             const dim3 grid((unsigned)(s_hi - s_lo)), block(256);
+                            if (h->nlpt && s_lo == 0 && s_hi == S) {   // the whole class: largest degree first
+                                as.nps = reinterpret_cast<const int32_t *>((const int64_t *)h->cpre.p + h->lpt_off);
+                                as.nord = as.nps + h->nlpt + 1;
+                                as.nm = h->nlpt;
+                            }
                             if (d == 2) { if (rec) hipLaunchKernelGGL((k_level_lds_f<2, false, true>), grid, block, ldsf, h->stream, as); else hipLaunchKernelGGL((k_level_lds_f<2, false>), grid, block, ldsf, h->stream, as); }
                             else if (d == 3) { if (rec) hipLaunchKernelGGL((k_level_lds_f<3, false, true>), grid, block, ldsf, h->stream, as); else hipLaunchKernelGGL((k_level_lds_f<3, false>), grid, block, ldsf, h->stream, as); }
                             else { if (rec) hipLaunchKernelGGL((k_level_lds_f<4, false, true>), grid, block, ldsf, h->stream, as); else hipLaunchKernelGGL((k_level_lds_f<4, false>), grid, block, ldsf, h->stream, as); }
@@ -5596,6 +5682,46 @@ int level_end_finish(pcg_handle *h, int d, unsigned long long seq, pcg_stats *st
     h->st.screened[d] = (int64_t)c.screened;
     h->st.near_alpha[d] = near_d;
     if (!h->lev_on) h->st.kernel_ms[d] = h->run_ms;
+#if PCG_TGF_BLKT
+    if (d == PCG_TGF_BLKT) {
+        static std::vector<unsigned long long> bt(BLKT_MAX * 4), bw(4096 * 4);
+        (void)hipMemcpyFromSymbol(bt.data(), HIP_SYMBOL(g_blkt), bt.size() * 8, 0, hipMemcpyDeviceToHost);
+        (void)hipMemcpyFromSymbol(bw.data(), HIP_SYMBOL(g_blkw), bw.size() * 8, 0, hipMemcpyDeviceToHost);
+        for (int cls = 0; cls < 2; ++cls) {
+            const std::vector<unsigned long long> &v = cls ? bw : bt;
+            const int nb = (int)std::min<int64_t>(cls ? h->total_wide : h->total_small, cls ? 4096 : BLKT_MAX);
+            if (nb <= 0) continue;
+            unsigned long long t0 = ~0ull, t1 = 0;
+            double dur = 0.0;
+            std::vector<unsigned long long> ends;
+            double dD[8] = {}, nD[8] = {};
+            for (int b = 0; b < nb; ++b) {
+                const unsigned long long *e = &v[4 * b];
+                if (!e[1]) continue;
+                t0 = std::min(t0, e[0]);
+                t1 = std::max(t1, e[1]);
+                dur += (double)(e[1] - e[0]);
+                ends.push_back(e[1]);
+                const int k = std::min(7, (int)(e[2] / 16));
+                dD[k] += (double)(e[1] - e[0]);
+                nD[k] += 1.0;
+            }
+            std::sort(ends.begin(), ends.end());
+            auto q = [&](double f) { return (double)(ends[(size_t)(f * (ends.size() - 1))] - t0) / 100.0; };
+            fprintf(stderr, "[blkt d%d %s] blocks %d span %.1f us  ends at 50/90/99/100%%: %.1f %.1f %.1f %.1f us  "
+                    "mean block %.1f us  slot-occupancy(1024) %.2f  mean us by D/16:", d, cls ? "wide" : "narrow", nb,
+                    (double)(t1 - t0) / 100.0, q(0.5), q(0.9), q(0.99), q(1.0), dur / nb / 100.0,
+                    dur / 100.0 / (1024.0 * (double)(t1 - t0) / 100.0));
+            for (int k = 0; k < 8; ++k)
+                if (nD[k] > 0) fprintf(stderr, " %d:%.1f(%d)", k, dD[k] / nD[k] / 100.0, (int)nD[k]);
+            fprintf(stderr, "\n");
+        }
+        std::fill(bt.begin(), bt.end(), 0ull);
+        std::fill(bw.begin(), bw.end(), 0ull);
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_blkt), bt.data(), bt.size() * 8, 0, hipMemcpyHostToDevice);
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_blkw), bw.data(), bw.size() * 8, 0, hipMemcpyHostToDevice);
+    }
+#endif
 #if PCG_TGF_PROF
     if (d == PCG_TGF_PROF) {
         unsigned long long pr[8] = {};
