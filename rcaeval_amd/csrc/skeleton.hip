@@ -2361,6 +2361,9 @@ __device__ unsigned long long g_tgf_prof[8];   // block, staging, setup, sweep c
 #ifndef PCG_NB4_TARGET
 #define PCG_NB4_TARGET 16384  // ... at depth 4
 #endif
+#ifndef PCG_SCREEN_EXACT
+#define PCG_SCREEN_EXACT 1   // the fp32 sweep's level end: screen + exact path in one launch (k_screen_exact)
+#endif
 #ifndef PCG_TGF_LPT
 #define PCG_TGF_LPT 0x10  // depths (bit 1 << d) whose k_level_lds_f narrow class is dispatched largest degree first
                           // (LevelArgs::nord; config 5 depth 4: kernel 1.715-1.74 -> 1.69-1.70 ms A/B; depth 3
@@ -3205,8 +3208,8 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
 // The fp64 screen of the tests the fp32 sweep handed over (one lane per test, after the level
 // kernels, before k_exact): decided like the fp64 kernels; independence writes the removal
 // flags and both sides' unions as k_exact does, the band goes on to the exact path.
-template <int DM>
-__device__ __forceinline__ void screen_lanes(const LevelArgs &a, int blk, int nblk) {
+template <int DM, typename Band>
+__device__ __forceinline__ void screen_lanes(const LevelArgs &a, int blk, int nblk, Band band) {
     const unsigned long long pushed = *(volatile const unsigned long long *)&a.ctr->screened;
     const int64_t count = (int64_t)min((unsigned long long)a.scr_cap, pushed);
     if (blk == 0 && threadIdx.x == 0 && (int64_t)pushed > a.scr_cap)
@@ -3221,7 +3224,7 @@ __device__ __forceinline__ void screen_lanes(const LevelArgs &a, int blk, int nb
         for (int q = 0; q < DM; ++q) sg[q] = e.s[q];
         const int dec = eval_test_global<DM>(a, x, y, sg);
         if (dec == 2) {
-            push_deferred(a, x, y, sg, DM);
+            band(x, y, sg);
         } else if (dec == 1) {
             ++nindep;
             a.rm[(int64_t)x * a.n + y] = 1;
@@ -3251,7 +3254,7 @@ __device__ __forceinline__ void screen_lanes(const LevelArgs &a, int blk, int nb
 template <int DM>
 __global__ __launch_bounds__(256) void k_screen(LevelArgs a) {
     stamp_run_end(a);
-    screen_lanes<DM>(a, blockIdx.x, gridDim.x);
+    screen_lanes<DM>(a, blockIdx.x, gridDim.x, [&](int x, int y, const int *sg) { push_deferred(a, x, y, sg, DM); });
 }
 
 #ifndef PCG_NODE_BLOCKS
@@ -3768,12 +3771,10 @@ __device__ __forceinline__ void exact_finish(const LevelArgs &a, const DeferredE
 // is long — the full-p mode's recorded pairs put ~1e6 tests here at config 5 depth 4, where one
 // wave per test left 63 of its 64 lanes idle through every factorisation
 template <int M>
-__device__ __forceinline__ void exact_lanes(const LevelArgs &a, int64_t count, int blk, int nblk,
-                                            unsigned long long &nexact, unsigned long long &nindep) {
+__device__ __forceinline__ void exact_one(const LevelArgs &a, const DeferredEntry &e, unsigned long long &nexact,
+                                          unsigned long long &nindep) {
     constexpr int D = M - 2;
-    const int64_t lanes = (int64_t)nblk * blockDim.x;
-    for (int64_t i = (int64_t)blk * blockDim.x + threadIdx.x; i < count; i += lanes) {
-        const DeferredEntry e = a.deferred[i];
+    {
         int var[M];
         var[0] = e.x < e.y ? e.x : e.y;
         var[1] = e.x < e.y ? e.y : e.x;
@@ -3787,6 +3788,15 @@ __device__ __forceinline__ void exact_lanes(const LevelArgs &a, int64_t count, i
         double i00, i01, i11;
         const int sing = pcg_lu_inv01_reg<M>(R, &i00, &i01, &i11);
         exact_finish(a, e, sing, i00, i01, i11, nexact, nindep);
+    }
+}
+template <int M>
+__device__ __forceinline__ void exact_lanes(const LevelArgs &a, int64_t count, int blk, int nblk,
+                                            unsigned long long &nexact, unsigned long long &nindep) {
+    const int64_t lanes = (int64_t)nblk * blockDim.x;
+    for (int64_t i = (int64_t)blk * blockDim.x + threadIdx.x; i < count; i += lanes) {
+        const DeferredEntry e = a.deferred[i];
+        exact_one<M>(a, e, nexact, nindep);
     }
 }
 // the exact path with a lane per test (d <= 4; launched with records, whose recorded pairs put
@@ -3864,6 +3874,35 @@ __global__ __launch_bounds__(256) void k_exact(LevelArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     stamp_run_end(a);
     exact_waves(a, smem, blockIdx.x, gridDim.x);
+}
+
+// the fp32 sweep's level end in one launch (no records, d <= 4): the level kernels' band tests
+// (the deferred list, final by stream order; a handful per level at config 5) and the fp64 screen,
+// whose band tests take the exact path on the spot in their lane instead of a second list. The
+// exact path is the lane form's (the same register LU and verdict as k_exact); every write is an
+// OR or a counter, so the order of the two parts does not matter. Replaces k_screen + k_exact
+// (config 5: 8-17 us of k_exact at depths 3 and 4 for 12-14 tests)
+template <int DM>
+__global__ __launch_bounds__(256) void k_screen_exact(LevelArgs a) {
+    stamp_run_end(a);
+    const unsigned long long pushed = *(volatile const unsigned long long *)&a.ctr->deferred;
+    const int64_t count = (int64_t)min((unsigned long long)a.def_cap, pushed);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (int64_t)pushed > a.def_cap)
+        a.rm[(int64_t)a.n * a.n] = 1;      // overflow: every rank reruns (status byte 0)
+    unsigned long long nexact = 0, nindep = 0;
+    exact_lanes<DM + 2>(a, count, blockIdx.x, gridDim.x, nexact, nindep);
+    screen_lanes<DM>(a, blockIdx.x, gridDim.x, [&](int x, int y, const int *sg) {
+        DeferredEntry e;
+        e.x = x;
+        e.y = y;
+#pragma unroll
+        for (int i = 0; i < PCG_MAX_DEPTH; ++i) e.s[i] = i < DM ? sg[i] : -1;
+        exact_one<DM + 2>(a, e, nexact, nindep);
+    });
+    nexact = wave_sum(nexact);
+    nindep = wave_sum(nindep);
+    if ((threadIdx.x & 63) == 0 && nexact) atomicAdd(&a.ctr->exact, nexact);
+    if ((threadIdx.x & 63) == 0 && nindep) atomicAdd(&a.ctr->indep, nindep);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -5541,6 +5580,14 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
         if (d > PCG_MAX_DEPTH) return PCG_OK;
         a = make_args(h, d, mode == MODE_EXACT);
         a.stamp_end = kb ? 0 : 1;     // the first kernel behind the classes closes the bracket
+        if (PCG_SCREEN_EXACT && h->tgroup && use_screen32(h, d) && !(h->flags & PCG_FLAG_RECORD)) {
+            // the screen and the exact path in one launch (k_screen_exact)
+            if (d == 2) hipLaunchKernelGGL(k_screen_exact<2>, dim3(256), dim3(256), 0, h->stream, a);
+            else if (d == 3) hipLaunchKernelGGL(k_screen_exact<3>, dim3(256), dim3(256), 0, h->stream, a);
+            else hipLaunchKernelGGL(k_screen_exact<4>, dim3(256), dim3(256), 0, h->stream, a);
+            PCG_HIP(h, hipGetLastError());
+            return PCG_OK;
+        }
         if (h->tgroup && use_screen32(h, d)) {   // the fp32 sweep's undecided tests, in fp64
             // the list length is only known on the device; a grid-stride loop over it (1024 blocks
             // measured no faster than 256: 40 vs 36 us for 1.3e5 tests)
