@@ -227,13 +227,47 @@ __device__ __forceinline__ void push_deferred(const LevelArgs &a, int x, int y, 
     }
 }
 
+#ifndef PCG_SCREEN_ABL
+#define PCG_SCREEN_ABL 0   // timing ablation only (wrong results): the fp32 sweep's screen pushes dropped
+#endif
 __device__ __forceinline__ void push_screen(const LevelArgs &a, int x, int y, const int *S, int d) {
+    if (PCG_SCREEN_ABL) return;
     const unsigned long long slot = atomicAdd(&a.ctr->screened, 1ull);
     if ((int64_t)slot < a.scr_cap) {
         ScreenEntry &e = a.screen[slot];
         e.x = x; e.y = y;
         for (int i = 0; i < 4; ++i) e.s[i] = i < d ? S[i] : -1;
     }
+}
+
+// k_level_lds_f's screen list entries are staged in a per-block LDS buffer and appended to the
+// global list with ONE counter atomic per block at its end: one returning atomic per entry on the
+// single list counter serialised at its L2 channel (config 5 depth 3: 8.9e4 pushes, kernel 0.68 ms;
+// 0.44 ms with the pushes dropped). A full buffer falls back to the per-entry push
+#ifndef PCG_SCREEN_BUF
+#define PCG_SCREEN_BUF 96
+#endif
+__device__ __forceinline__ void push_screen_blk(const LevelArgs &a, ScreenEntry *buf, unsigned *cnt, int x, int y,
+                                                const int *S, int d) {
+    const unsigned k = atomicAdd(cnt, 1u);
+    if (k < (unsigned)PCG_SCREEN_BUF) {
+        ScreenEntry &e = buf[k];
+        e.x = x; e.y = y;
+        for (int i = 0; i < 4; ++i) e.s[i] = i < d ? S[i] : -1;
+    } else {
+        push_screen(a, x, y, S, d);
+    }
+}
+// the block's buffered entries to the global list (every thread calls it after a block barrier)
+__device__ __forceinline__ void flush_screen_blk(const LevelArgs &a, const ScreenEntry *buf, const unsigned *cnt,
+                                                 unsigned long long *base) {
+    const unsigned nbuf = min(*cnt, (unsigned)PCG_SCREEN_BUF);
+    if (!nbuf) return;                                  // (block-uniform)
+    if (threadIdx.x == 0) *base = atomicAdd(&a.ctr->screened, (unsigned long long)nbuf);
+    __syncthreads();
+    const unsigned long long b0 = *base;
+    for (unsigned i = threadIdx.x; i < nbuf; i += blockDim.x)
+        if ((int64_t)(b0 + i) < a.scr_cap) a.screen[b0 + i] = buf[i];
 }
 
 // error bits (1 singular, 2 domain) into the level counters and into the status bytes that
@@ -2605,6 +2639,10 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
     // records (PCG_FLAG_RECORD): the recorded pairs (x, y) of this node, bit t; every live test of
     // such a y goes to the exact path (decided and recorded there, as in k_level_lds_t)
     __shared__ Mask s_recm;
+    __shared__ ScreenEntry s_scr[PCG_SCREEN_BUF];   // this block's screen list entries (flush_screen_blk)
+    __shared__ unsigned s_scr_n;
+    __shared__ unsigned long long s_scr_base;
+    if (tid == 0) s_scr_n = 0;
     if (tid < 64) {
         Mask rm_ = 0;
         if (REC && a.record)
@@ -2909,7 +2947,7 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
             sg[0] = nxs[c];
 #pragma unroll
             for (int i = 0; i < DT; ++i) sg[i + 1] = nxs[T[i]];
-            push_screen(a, x, nxs[t], sg, DM);
+            push_screen_blk(a, s_scr, &s_scr_n, x, nxs[t], sg, DM);
         };
         // a recorded pair's live test: to the exact path
         auto push_rec = [&](int jj, int t) {
@@ -3169,6 +3207,7 @@ __global__ __launch_bounds__(256, WIDE ? PCG_WIDE_MB : tgf_minblocks(DM)) void k
     }
 #endif
     __syncthreads();
+    flush_screen_blk(a, s_scr, &s_scr_n, &s_scr_base);
 #if PCG_TGF_PROF
     if (PROF && tid == 0) atomicAdd(&g_tgf_prof[0], clock64() - prof_t0);
 #endif
@@ -5754,6 +5793,14 @@ int level_end_finish(pcg_handle *h, int d, unsigned long long seq, pcg_stats *st
                 nD[k] += 1.0;
             }
             std::sort(ends.begin(), ends.end());
+            // concurrency: a sweep over the start / end events
+            std::vector<std::pair<unsigned long long, int>> ev;
+            for (int b = 0; b < nb; ++b)
+                if (v[4 * b + 1]) { ev.push_back({v[4 * b], 1}); ev.push_back({v[4 * b + 1], -1}); }
+            std::sort(ev.begin(), ev.end());
+            int cur = 0, cmax = 0;
+            for (auto &e2 : ev) { cur += e2.second; cmax = std::max(cmax, cur); }
+            fprintf(stderr, "[blkt d%d %s] max concurrent blocks %d\n", d, cls ? "wide" : "narrow", cmax);
             auto q = [&](double f) { return (double)(ends[(size_t)(f * (ends.size() - 1))] - t0) / 100.0; };
             fprintf(stderr, "[blkt d%d %s] blocks %d span %.1f us  ends at 50/90/99/100%%: %.1f %.1f %.1f %.1f us  "
                     "mean block %.1f us  slot-occupancy(1024) %.2f  mean us by D/16:", d, cls ? "wide" : "narrow", nb,
