@@ -202,9 +202,17 @@ __device__ __forceinline__ int find_in_sorted(const int32_t *a, int len, int v) 
     return lo;
 }
 
+// wave-aggregated like push_deferred: one counter atomic per call site and wave (the records of
+// every test of a sampled pair arrive together from one wave's lanes)
 __device__ __forceinline__ void push_record(pcg_record *buf, int64_t cap, unsigned long long *ctr,
                                             int a, int b, int d, const int *S, double p) {
-    const unsigned long long slot = atomicAdd(ctr, 1ull);
+    const unsigned long long act = __ballot(1);
+    const int leader = __ffsll((long long)act) - 1;
+    const unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(act >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)act, 0u));
+    unsigned long long base = 0;
+    if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(ctr, (unsigned long long)__popcll(act));
+    base = __shfl(base, leader);
+    const unsigned long long slot = base + rank;
     if ((int64_t)slot < cap) {
         pcg_record &r = buf[slot];
         r.a = a; r.b = b; r.d = d;
@@ -218,8 +226,17 @@ __device__ __forceinline__ bool rec_on(const LevelArgs &a, int lo, int hi) {
     return a.record && (a.rec_mod <= 1 || ((int64_t)lo * a.n + hi) % a.rec_mod == a.rec_res);
 }
 
+// wave-aggregated: the lanes active at the call take consecutive slots from ONE counter atomic (the
+// record routing puts every test of a sampled pair here — ~1e6 per config-5 run — and a returning
+// atomic per entry on the one list counter serialises at its L2 channel)
 __device__ __forceinline__ void push_deferred(const LevelArgs &a, int x, int y, const int *S, int d) {
-    const unsigned long long slot = atomicAdd(&a.ctr->deferred, 1ull);
+    const unsigned long long act = __ballot(1);
+    const int leader = __ffsll((long long)act) - 1;
+    const unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(act >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)act, 0u));
+    unsigned long long base = 0;
+    if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(&a.ctr->deferred, (unsigned long long)__popcll(act));
+    base = __shfl(base, leader);
+    const unsigned long long slot = base + rank;
     if ((int64_t)slot < a.def_cap) {
         DeferredEntry &e = a.deferred[slot];
         e.x = x; e.y = y;
@@ -2337,7 +2354,8 @@ constexpr double F32_U = 5.9604644775390625e-08;   // 2^-24
 #define PCG_TG_F32 0x18   // depths (bit 1 << d) whose T-group sweep is fp32-screened by default
 #endif
 #ifndef PCG_TGF_SGPR
-#define PCG_TGF_SGPR 0x10 // k_level_lds_f depths (bit 1 << d) whose per-y bookkeeping is in wave lane masks
+#define PCG_TGF_SGPR 0x18 // k_level_lds_f depths (bit 1 << d) whose per-y bookkeeping is in wave lane masks
+                          // (depth 3 joined in round 6 once the memo skips were counted per node: 0.52 -> 0.49 ms)
 #endif
 #ifndef PCG_KBRACKET
 #define PCG_KBRACKET 0       // skeleton_once's depth / kernel brackets: 1 timing events (each one a ~6 us marker
