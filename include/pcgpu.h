@@ -149,7 +149,7 @@ int pcg_set_record_sample(pcg_handle *h, int64_t modulus, int64_t residue);
 #define PCG_TUNE_K1_I8 11         /* 1: K1 on the int8 matrix cores (1); 0: fp64 MFMA              */
 #define PCG_TUNE_K1_CRT 12        /* 1: the CRT residue K1 for n >= PCG_TUNE_K1_CRT_MINN (1)       */
 #define PCG_TUNE_K1_CRT_MINN 13   /* (256)                                                         */
-#define PCG_TUNE_K1_CRT_BITS 14   /* fewest bits kept per centred value, 32..63 (56)               */
+#define PCG_TUNE_K1_CRT_BITS 14   /* fewest bits kept per centred value, 32..63 (53)               */
 #define PCG_TUNE_K1_CRT_KS 15     /* CRT split-K slabs (0 = cost model)                            */
 #define PCG_TUNE_K1_I8_KS 16      /* digit-path split-K slabs (0 = default)                        */
 #define PCG_TUNE_K1_SUPER_ORDER 17 /* 1: digit-path tiles in super-rows (1); 0: row-major         */

@@ -91,7 +91,7 @@ const TuneSpec kTune[PCG_TUNE_COUNT] = {
     {"PCG_K1_I8", 1, 0, 1},
     {"PCG_K1_CRT", 1, 0, 1},
     {"PCG_K1_CRT_MINN", 256, 1, 1 << 24},
-    {"PCG_K1_CRT_BITS", 56, 32, 63},
+    {"PCG_K1_CRT_BITS", 53, 32, 63},
     {"PCG_K1_CRT_KS", 0, 0, 16},
     {"PCG_K1_I8_KS", 0, 0, 256},
     {"PCG_K1_SUPER_ORDER", 1, 0, 1},

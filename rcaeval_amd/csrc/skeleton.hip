@@ -985,6 +985,9 @@ __global__ __launch_bounds__(256) void k_level(LevelArgs a) {
 // for (x, y | z): v = C_yz / sqrt(C_zz), c_xy = C_xy - u_z v, c_yy = C_yy - v^2.
 // A chunk is (x, a contiguous share of the D(D-1)/2 pairs, row-major over y < z).
 constexpr int L1_MAXD = 1024;
+#ifndef PCG_L1_ABL
+#define PCG_L1_ABL 0      // timing ablation only (wrong results): k_level1_pairs without its independence writes
+#endif
 constexpr int L1_PB = 4;              // pairs in flight per lane (independent gathers; 8 and 16 measured slower)
 size_t l1_lds_bytes(int D) { return (size_t)D * (4 + 5 * 8) + 16; }
 // I32: every index of C, adj and rm fits 31 bits (n * ldc < 2^31): 32-bit offsets instead of
@@ -1089,6 +1092,7 @@ __global__ __launch_bounds__(256) void k_level1_pairs(LevelArgs a) {
                     push_deferred(a, x, tg, sg, 1);
                 } else if (dec == 1) {
                     ++indep;
+                    if (PCG_L1_ABL) continue;      // timing ablation only (wrong results)
                     a.rm[(int64_t)x * a.n + tg] = 1;
                     a.rm[(int64_t)tg * a.n + x] = 1;
                     unsigned long long *row = reinterpret_cast<unsigned long long *>(
