@@ -331,7 +331,7 @@ def test_page_rank_preprocess_table_equals_visit_loop():
 def _crt_units_host(n, N):
     """corr.hip crt_plan restated: (moduli k, split-K slabs ks) of the CRT K1, or None."""
     import bench
-    km = bench.k1_crt_moduli(n, N, {"K1_I8": 1, "K1_CRT": 1, "K1_CRT_MINN": 256, "K1_CRT_BITS": 56})
+    km = bench.k1_crt_moduli(n, N, {"K1_I8": 1, "K1_CRT": 1, "K1_CRT_MINN": 256, "K1_CRT_BITS": 53})
     if km is None:
         return None
     k = km[0]
@@ -370,7 +370,7 @@ def test_corr_shard_bytes_follow_the_k1_plan(n, N, world):
         units = ntiles * k * ks
         assert got.value == -(-units // world) * 65536
     if (n, N) == (2000, 10000):
-        assert plan[:2] == (17, 2)          # the headline: 17 moduli (b = 59), 2 slabs
+        assert plan[:2] == (16, 2)          # the headline: 16 moduli (b = 55), 2 slabs
 
 
 def test_corr_crt_path_switch(monkeypatch):
