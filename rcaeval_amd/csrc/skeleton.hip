@@ -2352,7 +2352,7 @@ struct alignas(16) YRecN {       // k_level_lds_f (narrow): a y's {A~_yy, A~_xy}
 };
 constexpr double F32_U = 5.9604644775390625e-08;   // 2^-24
 #ifndef PCG_F32_KE
-#define PCG_F32_KE 64.0
+#define PCG_F32_KE 32.0   // E = 2 KE u32 (1 + nu^2) >= KE u32 (1 + nu)^2, 1.75x DESIGN §4.1's 18 u32 (1 + nu)^2
 #endif
 #ifndef PCG_TG_F32
 #define PCG_TG_F32 0x18   // depths (bit 1 << d) whose T-group sweep is fp32-screened by default

@@ -17,7 +17,7 @@ import numpy as np
 import pytest
 
 U32 = 2.0 ** -24
-KE = 64.0
+KE = 32.0      # = PCG_F32_KE (skeleton.hip)
 TAU = 1e-4
 
 
@@ -229,7 +229,7 @@ def test_screen32_near_threshold():
 
 def _err_ratio(Cb, N=10000):
     """max over (c_xx, c_yy, c_xy) of |fp32 sweep value - fp64 value on C| / (K u (1 + nu)^2),
-    K = KE = 64 (the derived bound, DESIGN.md "fp32 screen: error bound"; the kernel's E is
+    K = KE = 32 (the derived bound, DESIGN.md "fp32 screen: error bound"; the kernel's E is
     2 KE u (1 + nu^2) >= this), per block; NaN where the candidate is unusable (ok false: the
     test never reaches the fp32 decision)."""
     with np.errstate(all="ignore"):
@@ -253,7 +253,7 @@ def test_screen32_adversarial_error_ratio():
     relies on: blocks with near-collinear conditioning sets (nu up to the screen's cut-off,
     te = E / s <= 1/2), x and y nearly determined by S (small c_xx, c_yy), entries placed a
     half fp32 ulp from a rounding boundary; then a random hill-climb on the worst blocks. The
-    derived bound needs K ~ 18; KE = 64. The worst ratio found must stay < 1/2."""
+    derived bound needs K ~ 18; KE = 32. The worst ratio found must stay < 1/2."""
     rng = np.random.default_rng(2024)
     B, r = 512, 6
     worst = 0.0
