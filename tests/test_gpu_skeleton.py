@@ -210,6 +210,22 @@ def test_screen_precision_masks_match_oracle(eng, n, N, seed, wl, wh, ep, narrow
         assert sum(out.stats["screened"]) == 0
 
 
+@pytest.mark.parametrize("blocks", [0, 0x10, 0x18])
+@pytest.mark.parametrize("n,N,seed", [(300, 2000, 7), (700, 5000, 9)])
+def test_node_images_match_oracle(eng, n, N, seed, blocks):
+    """The fp32 sweep's staging choices (PCG_TUNE_NODE_BLOCKS): gathered from C (0), the fp32 LDS
+    images built by k_node_blocks_t<true> and copied by LDS-DMA at depth 4 (0x10, the default) and
+    at depths 3 and 4 (0x18); with depth 4 dispatched largest degree first. Removal depths,
+    per-level counts and sepset unions equal the C oracle's at unlimited depth."""
+    X = synth.gaussian_sem(n, N, seed=seed, w_low=0.1, w_high=0.5, edge_prob=8.0 / n)
+    C = np.corrcoef(X.T)
+    ref = cpc.skeleton(C, N)
+    with eng.tuned(SMALL=0, NODE_BLOCKS=blocks):
+        out = eng.skeleton(C, N)
+    assert_skeleton_matches(out, ref, n)
+    assert out.levels >= 5, out.levels
+
+
 def test_screen_list_overflow_reruns(eng):
     """A screen list too small for the fp32 sweep's undecided tests (config 5, depth <= 3:
     ~9e4 of them at depth 3) overflows, the level reports it with the capacity raised, and
@@ -270,7 +286,7 @@ def test_decide_and_fullp_agree_2000_depth2(eng):
 def test_config5_full_depth4_matches_oracle(eng, config5):
     """BASELINE config 5 at full size and full depth: 2000 vars x 10 000 samples, seed 0,
     max_depth 4 — the benchmarked workload, whose depth 4 (83 % of the 4.9e9 unique tests) runs
-    on the dominant k_level_lds_t<4> kernel. Threshold-mode removal depth of every pair from
+    on the dominant k_level_lds_f<4> kernel (the fp32-screened sweep). Threshold-mode removal depth of every pair from
     pcg_pc_skeleton (K1 + skeleton in one call), per-level unique-test counts and sepset unions
     against the C oracle on np.corrcoef(X.T) (only pairs touched by an enumerated |p - alpha| < 1e-9 test are exempt); then the
     full-p kernels on the same graph, with recorded p of a fixed pair sample (1 in 4099 pairs,
