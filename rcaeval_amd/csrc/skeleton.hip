@@ -1110,6 +1110,205 @@ __global__ __launch_bounds__(256) void k_level1_pairs(LevelArgs a) {
     block_flush_counts(a.ctr, tests, indep);
 }
 
+// ---------------------------------------------------------------------------------------
+// depth 1 by conditioning node (threshold mode, one rank over the whole level; PCG_L1Z). The
+// tests (x, t | z) with z in adj(x) are grouped by z: block z stages row z of C and of adj (both
+// contiguous) and walks x in adj(z), t in adj(x) \ {z}, so C_xt comes from the graph's per-edge
+// copy cxe[off[x] + j] = C[x][nbr[x][j]] (k_edge_c, read in CSR order) and C_tz, adj(t, z) from
+// LDS: the scattered C[y][z] gathers of k_level1_pairs become streams. Same tests (the memo
+// rule: (x, t | z) belongs to t's side when t < x and z in adj(t)), same arithmetic and decision
+// as k_level1_pairs; C_tz is read as C[z][t] (C need not be bitwise symmetric: a 1-ulp change
+// of an operand moves r^2 by ~1e-16, far inside the decision band, and band tests take the exact
+// path either way). The block's (x, j) items are flattened over a prefix of the x's degrees in
+// LDS (per-x terms staged once), so every lane has work and its loads of U items are in flight
+// together; the mirror union row of an independent pair is found from adj(t)'s bit rank (one
+// round of independent loads) instead of a binary search of nbr(t) (dependent loads).
+#ifndef PCG_L1Z
+#define PCG_L1Z 1
+#endif
+#ifndef PCG_L1Z_ABL
+#define PCG_L1Z_ABL 0     // timing ablation only (wrong results): 1 no mirror rows, 2 no independence writes
+#endif
+#ifndef PCG_L1Z_DTE
+#define PCG_L1Z_DTE 1     // C_tt per edge in CSR order (k_edge_c) instead of a gather of diag[t] per item
+#endif
+#ifndef L1Z_U
+#define L1Z_U 4           // items in flight per lane
+#endif
+#ifndef L1Z_BS
+#define L1Z_BS 512        // threads per block (one block per z; 8 waves fill a CU's wave slots at 4 blocks)
+#endif
+size_t l1z_lds_bytes(int64_t n, int W, int maxd) {
+    return sizeof(double) * ((size_t)n + 2 * (size_t)maxd) + sizeof(uint64_t) * (size_t)W +
+           sizeof(int32_t) * (3 * (size_t)maxd + 1) + 16;
+}
+
+__global__ __launch_bounds__(256) void k_edge_c(const double *C, int64_t ldc, const int32_t *deg, const int32_t *off,
+                                                const int32_t *nbr, int n, const double *diag, double *cxe, double *dte) {
+    const int x = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    if (x >= n) return;
+    const int lane = threadIdx.x & 63, D = deg[x], o = off[x];
+    const double *Cx = C + (int64_t)x * ldc;
+    for (int j = lane; j < D; j += 64) {
+        const int t = nbr[o + j];
+        cxe[o + j] = Cx[t];
+        if (PCG_L1Z_DTE) dte[o + j] = diag[t];
+    }
+}
+
+#ifndef L1Z_MCAP
+#define L1Z_MCAP 512      // mirror entries a block defers to its end (LDS); past them it searches inline
+#endif
+__global__ __launch_bounds__(L1Z_BS) void k_level1_z(LevelArgs a, const double *cxe, const double *dte) {
+    __shared__ int2 s_ml[L1Z_MCAP];
+    __shared__ unsigned s_mn;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int z = blockIdx.x, n = a.n, W = a.W, tid = threadIdx.x, lane = tid & 63;
+    const int Dz = a.deg[z];
+    unsigned tests = 0, indep = 0;
+    if (tid == 0) s_mn = 0;
+    if (Dz > 0) {
+        double *cz = reinterpret_cast<double *>(smem);        // row z of C
+        double *su = cz + n, *scxx = su + Dz;                  // per x in adj(z): u, c_xx|z (NaN: no Cholesky)
+        uint64_t *az = reinterpret_cast<uint64_t *>(scxx + Dz);   // row z of adj
+        int32_t *sx = reinterpret_cast<int32_t *>(az + W), *sox = sx + Dz, *spre = sox + Dz;   // x, off[x], item prefix
+        const double *Cz = a.C + (int64_t)z * a.ldc;
+        for (int e = tid; e < n; e += blockDim.x) cz[e] = Cz[e];
+        for (int e = tid; e < W; e += blockDim.x) az[e] = a.adj[(int64_t)z * W + e];
+        const double s = a.diag[z];
+        const double ri = 1.0 / sqrt(s);
+        const int32_t *nz = a.nbr + a.off[z];
+        for (int xi = tid; xi < Dz; xi += blockDim.x) {
+            const int x = nz[xi];
+            const double u = a.C[(int64_t)x * a.ldc + z] * ri;
+            const double cxx = a.diag[x] - u * u;
+            sx[xi] = x;
+            sox[xi] = a.off[x];
+            spre[xi] = a.deg[x];
+            su[xi] = u;
+            scxx[xi] = ((s > 0.0) && (cxx == cxx)) ? cxx : __builtin_nan("");
+        }
+        __syncthreads();
+        if (tid < 64) {   // exclusive prefix of the degrees (wave 0)
+            int carry = 0;
+            for (int b = 0; b < Dz; b += 64) {
+                const int i = b + lane;
+                const int v = i < Dz ? spre[i] : 0;
+                int incl = v;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int t = __shfl_up(incl, o);
+                    if (lane >= o) incl += t;
+                }
+                if (i < Dz) spre[i] = carry + incl - v;
+                carry += __shfl(incl, 63);
+            }
+            if (lane == 0) spre[Dz] = carry;
+        }
+        __syncthreads();
+        const int P = spre[Dz];
+        const double kg = a.tau * ri * ri;
+        const int sg[1] = {z};
+        // each wave walks a contiguous share of the items, 64 * L1Z_U at a time (lane l, slot q:
+        // item b + 64 q + l); a lane's items ascend, so its x cursor only moves forward (one LDS
+        // compare per item while D_x >= 64) after one binary search at the wave's start
+        const int nw = (int)(blockDim.x >> 6), wv = tid >> 6;
+        const int per = (P + nw - 1) / nw;
+        const int pw0 = min(P, wv * per), pw1 = min(P, pw0 + per);
+        int xi = 0;
+        {
+            const int p = min(pw0 + lane, max(P - 1, 0));
+            int lo = 0, hi = Dz;                       // spre[lo] <= p < spre[hi]
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (spre[mid] <= p) lo = mid; else hi = mid;
+            }
+            xi = lo;
+        }
+        for (int b = pw0; b < pw1; b += 64 * L1Z_U) {
+            int xs[L1Z_U], ts[L1Z_U], es[L1Z_U];
+            double ce[L1Z_U], dt[L1Z_U];
+#pragma unroll
+            for (int q = 0; q < L1Z_U; ++q) {
+                const int p = b + 64 * q + lane;
+                int e = 0, t = z;
+                if (p < pw1) {
+                    while (spre[xi + 1] <= p) ++xi;
+                    e = sox[xi] + (p - spre[xi]);
+                    t = a.nbr[e];
+                }
+                xs[q] = xi;
+                es[q] = e;
+                ts[q] = t;
+                ce[q] = p < pw1 ? cxe[e] : 0.0;
+                if (PCG_L1Z_DTE) dt[q] = p < pw1 ? dte[e] : 0.0;
+            }
+            if (!PCG_L1Z_DTE) {
+#pragma unroll
+                for (int q = 0; q < L1Z_U; ++q) dt[q] = ts[q] != z ? a.diag[ts[q]] : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < L1Z_U; ++q) {
+                const int t = ts[q];
+                if (t == z) continue;                  // (also the items past P)
+                const int xi = xs[q], x = sx[xi];
+                const bool adj_tz = (az[t >> 6] >> (t & 63)) & 1ull;
+                if (t < x && adj_tz) continue;         // memo: node t's side holds (t, x | z)
+                ++tests;
+                const double cxx = scxx[xi];
+                int dec = 2;
+                if (cxx == cxx) {
+                    double pv = 0.0;
+                    const double u = su[xi];
+                    const double v = cz[t] * ri;
+                    const double cxt = ce[q] - u * v;
+                    const double ctt = dt[q] - v * v;
+                    dec = decide<MODE_DECIDE>(a, cxt, cxx, ctt, kg, &pv);
+                }
+                if (dec == 2) {
+                    push_deferred(a, x, t, sg, 1);
+                } else if (dec == 1) {
+                    ++indep;
+                    if (PCG_L1Z_ABL == 2) continue;
+                    a.rm[(int64_t)x * n + t] = 1;
+                    a.rm[(int64_t)t * n + x] = 1;
+                    unsigned long long *row = reinterpret_cast<unsigned long long *>(a.ug + (int64_t)es[q] * W);
+                    atomicOr(&row[z >> 6], 1ull << (z & 63));
+                    if (PCG_L1Z_ABL != 1 && adj_tz && t > x) {   // S in adj(t): also t's side of the pair
+                        // its row (x's position in nbr(t)) is searched at the block's end, one lane per
+                        // entry, so the search's dependent loads do not stall the sweep (inline past
+                        // L1Z_MCAP entries)
+                        const unsigned long long act = __ballot(1);
+                        const int leader = __ffsll((long long)act) - 1;
+                        const unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(act >> 32),
+                                                                        __builtin_amdgcn_mbcnt_lo((unsigned)act, 0u));
+                        unsigned base = 0;
+                        if (lane == leader) base = atomicAdd(&s_mn, (unsigned)__popcll(act));
+                        base = __shfl(base, leader);
+                        const unsigned slot = base + rank;
+                        if (slot < (unsigned)L1Z_MCAP) {
+                            s_ml[slot] = make_int2(t, x);
+                        } else {
+                            const int r = find_in_sorted(a.nbr + a.off[t], a.deg[t], x);
+                            unsigned long long *rowt = reinterpret_cast<unsigned long long *>(a.ug + ((int64_t)a.off[t] + r) * W);
+                            atomicOr(&rowt[z >> 6], 1ull << (z & 63));
+                        }
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const int nm = (int)min(s_mn, (unsigned)L1Z_MCAP);
+    for (int i = tid; i < nm; i += blockDim.x) {
+        const int t = s_ml[i].x, x = s_ml[i].y;
+        const int r = find_in_sorted(a.nbr + a.off[t], a.deg[t], x);
+        unsigned long long *rowt = reinterpret_cast<unsigned long long *>(a.ug + ((int64_t)a.off[t] + r) * W);
+        atomicOr(&rowt[z >> 6], 1ull << (z & 63));
+    }
+    block_flush_counts(a.ctr, tests, indep);
+}
+
 // The exact path of one test (numpy.linalg.inv-order LU of the m x m matrix A in LDS, the
 // reference p expression): 0 ok, 1 singular, 2 math domain. Not inlined: its polynomial
 // constants would otherwise be hoisted into registers across the callers' hot loops.
@@ -2353,6 +2552,9 @@ struct alignas(16) YRecN {       // k_level_lds_f (narrow): a y's {A~_yy, A~_xy}
 constexpr double F32_U = 5.9604644775390625e-08;   // 2^-24
 #ifndef PCG_F32_KE
 #define PCG_F32_KE 32.0   // E = 2 KE u32 (1 + nu^2) >= KE u32 (1 + nu)^2, 1.75x DESIGN §4.1's 18 u32 (1 + nu)^2
+#endif
+#ifndef PCG_FORK_LATE
+#define PCG_FORK_LATE 1   // the aux stream's fork wait after the main stream's first class launch (0: before it)
 #endif
 #ifndef PCG_TG_F32
 #define PCG_TG_F32 0x18   // depths (bit 1 << d) whose T-group sweep is fp32-screened by default
@@ -5463,6 +5665,18 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                     hipLaunchKernelGGL(k_or_flags, dim3((unsigned)std::min<int64_t>((nn + 255) / 256, 4096)), dim3(256), 0,
                                        h->stream, h->banned, (int64_t)h->n, a.rm);
                 }
+            } else if (d == 1 && PCG_L1Z && mode == MODE_DECIDE && !rec && h->world == 1 && chunk_lo == 0 &&
+                       chunk_hi == h->total_chunks && l1z_lds_bytes(h->n, h->W, h->maxdeg) + 8 * L1Z_MCAP + 512 <= LDS_MAX) {
+                // the whole depth by conditioning node (k_level1_z); the per-edge C values go to the
+                // compact-block buffer, which depth 1 does not use otherwise
+                const int64_t S1 = std::max<int64_t>(h->sumdeg, 1);
+                if (!pcg_ensure(h, h->cblk, 2 * sizeof(double) * (size_t)S1))
+                    return pcg_fail(h, PCG_ERR_OOM, "depth-1 edge correlations");
+                double *cxe = (double *)h->cblk.p, *dte = cxe + S1;
+                hipLaunchKernelGGL(k_edge_c, dim3((unsigned)((h->n + 3) / 4)), dim3(256), 0, h->stream, a.C, a.ldc, a.deg,
+                                   a.off, a.nbr, (int)h->n, a.diag, cxe, dte);
+                hipLaunchKernelGGL(k_level1_z, dim3((unsigned)h->n), dim3(L1Z_BS), l1z_lds_bytes(h->n, h->W, h->maxdeg), h->stream,
+                                   a, (const double *)cxe, (const double *)dte);
             } else {
                 const int64_t S = h->total_small, Wd = h->total_wide;
                 const int64_t s_lo = chunk_lo, s_hi = std::min(chunk_hi, S);
@@ -5608,7 +5822,6 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                     }
                     return PCG_OK;
                 };
-                if (fork) PCG_HIP(h, hipStreamWaitEvent(h->aux, kb ? rv[0] : h->ev_fork, 0));
                 // a class launched on the aux stream (h->stream swapped; restored on every exit)
                 auto launch = [&](bool on_aux, auto &&fn) -> int {
                     struct StreamSwap {
@@ -5621,9 +5834,18 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                 // (the class on the main stream is launched first: it is the longer one)
                 const bool rest_first = PCG_CLASS_ORDER == 1 || PCG_CLASS_ORDER == 3 || (PCG_MAIN_FIRST && rest_main);
                 const bool narrow_aux = fork && rest_main, rest_aux = fork && !rest_main;
+                // the aux stream's wait on the fork point is enqueued after the main stream's first
+                // launch when that class runs on the main stream (PCG_FORK_LATE): the wait's host
+                // cost then lands behind a kernel that is already running
+                const bool late = PCG_FORK_LATE && fork && !(rest_first ? rest_aux : narrow_aux);
+                if (fork && !late) PCG_HIP(h, hipStreamWaitEvent(h->aux, kb ? rv[0] : h->ev_fork, 0));
+                PCG_HT(h, "run:forked");
                 int rc2 = rest_first ? launch(rest_aux, run_rest) : launch(narrow_aux, run_narrow);
+                PCG_HT(h, "run:first-class");
+                if (late && !rc2) PCG_HIP(h, hipStreamWaitEvent(h->aux, kb ? rv[0] : h->ev_fork, 0));
                 if (!rc2) rc2 = rest_first ? launch(narrow_aux, run_narrow) : launch(rest_aux, run_rest);
                 if (rc2) return rc2;
+                PCG_HT(h, "run:second-class");
                 if (fork) {
                     PCG_HIP(h, hipEventRecord(h->ev_join, h->aux));
                     PCG_HIP(h, hipStreamWaitEvent(main_stream, h->ev_join, 0));
