@@ -139,6 +139,7 @@ struct pcg_handle {
     bool tgroup = false;             // small class runs k_level_lds_t this depth
     bool wavek = false;              // small class runs k_level_wave this depth (deep levels)
     bool nblk = false;               // small class stages per-node compact blocks (k_node_blocks) this depth
+    bool l1z_pre = false;            // depth 1's per-edge C values (k_edge_c) enqueued by pcg_level_begin
     bool nimg = false;               // ... as fp32 LDS images of k_level_lds_f (k_node_blocks_t<true>)
     DevBuf cblk, lmk;                // k_node_blocks: per-node compact correlation blocks, local masks
     int64_t bo_off = 0;              // int64 offset of the compact-block offsets in cpre / cpre_pin

@@ -5289,6 +5289,25 @@ void level_start_stats(pcg_handle *h, int depth) {
 
 int level_begin_buffers(pcg_handle *h, int depth);
 
+// depth 1 by conditioning node (k_level1_z) over the whole level on one rank
+bool l1z_use(const pcg_handle *h, int d) {
+    return d == 1 && PCG_L1Z && mode_of(h, d) == MODE_DECIDE && !(h->flags & PCG_FLAG_RECORD) && h->world == 1 &&
+           l1z_lds_bytes(h->n, h->W, h->maxdeg) + 8 * L1Z_MCAP + 512 <= LDS_MAX;
+}
+
+// k_level1_z's per-edge C_xt / C_tt (into the compact-block buffer, which depth 1 does not use otherwise)
+int l1z_edges(pcg_handle *h) {
+    const int64_t S1 = std::max<int64_t>(h->sumdeg, 1);
+    if (!pcg_ensure(h, h->cblk, 2 * sizeof(double) * (size_t)S1))
+        return pcg_fail(h, PCG_ERR_OOM, "depth-1 edge correlations");
+    const LevelArgs a = make_args(h, 1, false);
+    double *cxe = (double *)h->cblk.p;
+    hipLaunchKernelGGL(k_edge_c, dim3((unsigned)((h->n + 3) / 4)), dim3(256), 0, h->stream, a.C, a.ldc, a.deg, a.off,
+                       a.nbr, (int)h->n, a.diag, cxe, cxe + S1);
+    PCG_HIP(h, hipGetLastError());
+    return PCG_OK;
+}
+
 int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks) {
     if (!h || depth != h->depth + 1) return pcg_fail(h, PCG_ERR_INVALID, "pcg_level_begin: depth order");
     // reference loop condition: while max_degree() - 1 > depth_prev
@@ -5301,6 +5320,12 @@ int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks) {
                         PCG_MAX_LEVEL_DEPTH);
     h->depth = depth;
     const int n = (int)h->n;
+    // depth 1's per-edge C values first: they run while the host decomposes the level
+    h->l1z_pre = false;
+    if (l1z_use(h, depth)) {
+        if (int rc = l1z_edges(h)) return rc;
+        h->l1z_pre = true;
+    }
     level_start_stats(h, depth);
     // per-degree tables: the decomposition below is O(n) lookups (it sits between two
     // device phases of the level loop, so it is on the critical path)
@@ -5665,18 +5690,14 @@ extern "C" int pcg_level_run(pcg_handle *h, int64_t chunk_lo, int64_t chunk_hi) 
                     hipLaunchKernelGGL(k_or_flags, dim3((unsigned)std::min<int64_t>((nn + 255) / 256, 4096)), dim3(256), 0,
                                        h->stream, h->banned, (int64_t)h->n, a.rm);
                 }
-            } else if (d == 1 && PCG_L1Z && mode == MODE_DECIDE && !rec && h->world == 1 && chunk_lo == 0 &&
-                       chunk_hi == h->total_chunks && l1z_lds_bytes(h->n, h->W, h->maxdeg) + 8 * L1Z_MCAP + 512 <= LDS_MAX) {
-                // the whole depth by conditioning node (k_level1_z); the per-edge C values go to the
-                // compact-block buffer, which depth 1 does not use otherwise
+            } else if (l1z_use(h, d) && chunk_lo == 0 && chunk_hi == h->total_chunks) {
+                // the whole depth by conditioning node (k_level1_z)
+                if (!h->l1z_pre)
+                    if (int rc = l1z_edges(h)) return rc;
                 const int64_t S1 = std::max<int64_t>(h->sumdeg, 1);
-                if (!pcg_ensure(h, h->cblk, 2 * sizeof(double) * (size_t)S1))
-                    return pcg_fail(h, PCG_ERR_OOM, "depth-1 edge correlations");
-                double *cxe = (double *)h->cblk.p, *dte = cxe + S1;
-                hipLaunchKernelGGL(k_edge_c, dim3((unsigned)((h->n + 3) / 4)), dim3(256), 0, h->stream, a.C, a.ldc, a.deg,
-                                   a.off, a.nbr, (int)h->n, a.diag, cxe, dte);
+                const double *cxe = (const double *)h->cblk.p, *dte = cxe + S1;
                 hipLaunchKernelGGL(k_level1_z, dim3((unsigned)h->n), dim3(L1Z_BS), l1z_lds_bytes(h->n, h->W, h->maxdeg), h->stream,
-                                   a, (const double *)cxe, (const double *)dte);
+                                   a, cxe, dte);
             } else {
                 const int64_t S = h->total_small, Wd = h->total_wide;
                 const int64_t s_lo = chunk_lo, s_hi = std::min(chunk_hi, S);
