@@ -33,6 +33,7 @@ if [ "$PART" = 1 ]; then
   step prof 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-full-p
   python tools/timeline.py "$(find $OUT/prof -name run_kernel_trace.csv | head -1)" > $OUT/${TAG}_timeline.txt 2>&1
   cp "$(find $OUT/prof -name run_kernel_stats.csv | head -1)" $OUT/${TAG}_kernel_stats.csv
+  if [ -n "${SKIP_PMC:-}" ]; then cat $OUT/round_status.log; exit 0; fi   # (the sweep kernels' PMC unchanged)
   step pmc 900 bash tools/pmc_passes.sh
   cp $OUT/pmc_summary.json $OUT/${TAG}_pmc_summary.json
   if [ -f tools/ab/libpcgpu_abl1.so ]; then
