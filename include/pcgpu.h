@@ -153,7 +153,9 @@ int pcg_set_record_sample(pcg_handle *h, int64_t modulus, int64_t residue);
 #define PCG_TUNE_K1_CRT_KS 15     /* CRT split-K slabs (0 = cost model)                            */
 #define PCG_TUNE_K1_I8_KS 16      /* digit-path split-K slabs (0 = default)                        */
 #define PCG_TUNE_K1_SUPER_ORDER 17 /* 1: digit-path tiles in super-rows (1); 0: row-major         */
-#define PCG_TUNE_COUNT 18
+#define PCG_TUNE_L1Z 18           /* 1: threshold-mode depth 1 grouped by conditioning node on one
+                                     rank (k_level1_z, 1); 0: the neighbour-pair kernel           */
+#define PCG_TUNE_COUNT 19
 int pcg_set_tuning(pcg_handle *h, int key, int64_t value);
 int pcg_get_tuning(pcg_handle *h, int key, int64_t *value);
 

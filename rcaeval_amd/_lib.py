@@ -45,6 +45,7 @@ TUNE_KEYS = {
     "SMALL": 0, "SMALL_QCAP": 1, "LDS_DEEP": 2, "LDS_SPILL_MIN": 3, "WAVE_LO": 4, "SCREEN_MASK": 5,
     "NODE_BLOCKS": 6, "EXPORT_INLINE": 7, "NB": 8, "NBW": 9, "HOST_TRACE": 10, "K1_I8": 11, "K1_CRT": 12,
     "K1_CRT_MINN": 13, "K1_CRT_BITS": 14, "K1_CRT_KS": 15, "K1_I8_KS": 16, "K1_SUPER_ORDER": 17,
+    "L1Z": 18,
 }
 
 I64 = ctypes.c_int64

@@ -95,6 +95,7 @@ const TuneSpec kTune[PCG_TUNE_COUNT] = {
     {"PCG_K1_CRT_KS", 0, 0, 16},
     {"PCG_K1_I8_KS", 0, 0, 256},
     {"PCG_K1_SUPER_ORDER", 1, 0, 1},
+    {"PCG_L1Z", 1, 0, 1},
 };
 }  // namespace
 

@@ -5291,7 +5291,7 @@ int level_begin_buffers(pcg_handle *h, int depth);
 
 // depth 1 by conditioning node (k_level1_z) over the whole level on one rank
 bool l1z_use(const pcg_handle *h, int d) {
-    return d == 1 && PCG_L1Z && mode_of(h, d) == MODE_DECIDE && !(h->flags & PCG_FLAG_RECORD) && h->world == 1 &&
+    return d == 1 && PCG_L1Z && h->tune[PCG_TUNE_L1Z] && mode_of(h, d) == MODE_DECIDE && !(h->flags & PCG_FLAG_RECORD) && h->world == 1 &&
            l1z_lds_bytes(h->n, h->W, h->maxdeg) + 8 * L1Z_MCAP + 512 <= LDS_MAX;
 }
 

@@ -226,6 +226,38 @@ def test_node_images_match_oracle(eng, n, N, seed, blocks):
     assert out.levels >= 5, out.levels
 
 
+def _star(m, N, seed):
+    """A common cause z (column 0) of m children: complete after depth 0, every child pair
+    separated by {z} at depth 1 (~m^2/2 independent tests in the block of z)."""
+    rng = np.random.default_rng(seed)
+    z = rng.standard_normal(N)
+    a = rng.uniform(0.5, 0.9, m)
+    return np.column_stack([z, z[:, None] * a + rng.standard_normal((N, m))])
+
+
+@pytest.mark.parametrize("l1z", [1, 0])
+@pytest.mark.parametrize("case", ["star", "sem"])
+def test_depth1_grouping_matches_oracle(eng, case, l1z):
+    """Depth 1 grouped by conditioning node (k_level1_z, PCG_TUNE_L1Z = 1, the default) and the
+    neighbour-pair kernel (0): equal skeletons, unions and per-level counts. The star's block
+    of z holds ~1.3e4 mirror union bits (an independent (x, t | z) with z in adj(t) also marks
+    the pair's other ordered side), past the kernel's 512-entry LDS list, so the inline search
+    runs too."""
+    if case == "star":   # (depth <= 2: the hub keeps its 160 edges, so deeper levels explode)
+        X, N, md = _star(160, 3000, 11), 3000, 2
+    else:
+        N, md = 3000, -1
+        X = synth.gaussian_sem(300, N, seed=12, w_low=0.2, w_high=0.6, edge_prob=0.05)
+    C = np.corrcoef(X.T)
+    ref = cpc.skeleton(C, N, max_depth=md)
+    with eng.tuned(L1Z=l1z):
+        out = eng.skeleton(C, N, max_depth=md)
+    assert out.stats["driver"] == "levels"
+    assert_skeleton_matches(out, ref, X.shape[1])
+    if case == "star":
+        assert out.stats["indep"][1] > 10000, out.stats["indep"]
+
+
 def test_screen_list_overflow_reruns(eng):
     """A screen list too small for the fp32 sweep's undecided tests (config 5, depth <= 3:
     ~9e4 of them at depth 3) overflows, the level reports it with the capacity raised, and
