@@ -5289,6 +5289,9 @@ void level_start_stats(pcg_handle *h, int depth) {
 
 int level_begin_buffers(pcg_handle *h, int depth);
 
+#ifndef PCG_L1Z_EARLY
+#define PCG_L1Z_EARLY 1   // k_edge_c enqueued before the level's host decomposition (1) or behind the prefix copy
+#endif                    // (0: depth-1 level 0.165-0.174 vs 0.157-0.163 ms, two A/B passes on one box)
 // depth 1 by conditioning node (k_level1_z) over the whole level on one rank
 bool l1z_use(const pcg_handle *h, int d) {
     return d == 1 && PCG_L1Z && h->tune[PCG_TUNE_L1Z] && mode_of(h, d) == MODE_DECIDE && !(h->flags & PCG_FLAG_RECORD) && h->world == 1 &&
@@ -5320,9 +5323,8 @@ int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks) {
                         PCG_MAX_LEVEL_DEPTH);
     h->depth = depth;
     const int n = (int)h->n;
-    // depth 1's per-edge C values first: they run while the host decomposes the level
     h->l1z_pre = false;
-    if (l1z_use(h, depth)) {
+    if (PCG_L1Z_EARLY && l1z_use(h, depth)) {   // depth 1's per-edge C values run while the host decomposes
         if (int rc = l1z_edges(h)) return rc;
         h->l1z_pre = true;
     }
@@ -5508,6 +5510,11 @@ int level_begin_impl(pcg_handle *h, int depth, int64_t *total_chunks) {
         PCG_HIP(h, hipGetLastError());
     }
     PCG_HT(h, "begin:prefix-copy-launched");
+    // (PCG_L1Z_EARLY 0) depth 1's per-edge C values right behind the prefix copy
+    if (!h->l1z_pre && l1z_use(h, depth)) {
+        if (int rc = l1z_edges(h)) return rc;
+        h->l1z_pre = true;
+    }
     return level_begin_buffers(h, depth);
 }
 
