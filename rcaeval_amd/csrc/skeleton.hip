@@ -1129,6 +1129,9 @@ __global__ __launch_bounds__(256) void k_level1_pairs(LevelArgs a) {
 #ifndef PCG_L1Z_ABL
 #define PCG_L1Z_ABL 0     // timing ablation only (wrong results): 1 no mirror rows, 2 no independence writes
 #endif
+#ifndef PCG_L1Z_FLAT
+#define PCG_L1Z_FLAT 0    // 1: the sweep's common path without branches (A/B); 0: k_level1_pairs' branch structure
+#endif
 #ifndef PCG_L1Z_DTE
 #define PCG_L1Z_DTE 1     // C_tt per edge in CSR order (k_edge_c) instead of a gather of diag[t] per item
 #endif
@@ -1250,20 +1253,36 @@ __global__ __launch_bounds__(L1Z_BS) void k_level1_z(LevelArgs a, const double *
 #pragma unroll
             for (int q = 0; q < L1Z_U; ++q) {
                 const int t = ts[q];
-                if (t == z) continue;                  // (also the items past P)
                 const int xi = xs[q], x = sx[xi];
                 const bool adj_tz = (az[t >> 6] >> (t & 63)) & 1ull;
-                if (t < x && adj_tz) continue;         // memo: node t's side holds (t, x | z)
-                ++tests;
-                const double cxx = scxx[xi];
                 int dec = 2;
-                if (cxx == cxx) {
-                    double pv = 0.0;
-                    const double u = su[xi];
+                if (PCG_L1Z_FLAT) {
+                    // branch-free common path: every item is evaluated (t = z and the items past P
+                    // too, on defined values) and only a live test that is not certainly dependent
+                    // leaves it; decide<MODE_DECIDE>'s steps as selects (a NaN c_xx|z fails den > 0)
+                    const bool live = t != z && !(t < x && adj_tz);   // memo: (t, x | z) on t's side
+                    tests += live;
+                    const double cxx = scxx[xi];
                     const double v = cz[t] * ri;
-                    const double cxt = ce[q] - u * v;
+                    const double cxt = ce[q] - su[xi] * v;
                     const double ctt = dt[q] - v * v;
-                    dec = decide<MODE_DECIDE>(a, cxt, cxx, ctt, kg, &pv);
+                    const double den = cxx * ctt, num = cxt * cxt;
+                    const bool ok = den > 0.0 && den - num > kg;
+                    dec = !ok ? 2 : num < a.lo2 * den ? 1 : num > a.hi2 * den ? 0 : 2;
+                    if (!live || dec == 0) continue;
+                } else {
+                    if (t == z) continue;              // (also the items past P)
+                    if (t < x && adj_tz) continue;     // memo: node t's side holds (t, x | z)
+                    ++tests;
+                    const double cxx = scxx[xi];
+                    if (cxx == cxx) {
+                        double pv = 0.0;
+                        const double u = su[xi];
+                        const double v = cz[t] * ri;
+                        const double cxt = ce[q] - u * v;
+                        const double ctt = dt[q] - v * v;
+                        dec = decide<MODE_DECIDE>(a, cxt, cxx, ctt, kg, &pv);
+                    }
                 }
                 if (dec == 2) {
                     push_deferred(a, x, t, sg, 1);
