@@ -1130,7 +1130,7 @@ __global__ __launch_bounds__(256) void k_level1_pairs(LevelArgs a) {
 #define PCG_L1Z_ABL 0     // timing ablation only (wrong results): 1 no mirror rows, 2 no independence writes
 #endif
 #ifndef PCG_L1Z_FLAT
-#define PCG_L1Z_FLAT 0    // 1: the sweep's common path without branches (A/B); 0: k_level1_pairs' branch structure
+#define PCG_L1Z_FLAT 1    // 1: the sweep's common path without branches (depth-1 kernel 0.095 -> 0.090 ms); 0: k_level1_pairs' branch structure
 #endif
 #ifndef PCG_L1Z_DTE
 #define PCG_L1Z_DTE 1     // C_tt per edge in CSR order (k_edge_c) instead of a gather of diag[t] per item
